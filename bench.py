@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: LeakDetector training steps on batched L-TOWN-A windows (BASELINE.json
+metric "windowed graphs/sec fwd+bwd on L-TOWN-A at 1/2/4/8 GPU; %HBM roofline").
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+  torchrun --nproc-per-node N ... bench.py --gpus N        (one rank per GPU, RCCL)
+
+A step = one full detector training step over one batch of B windows per rank:
+forward (GRU encoder, node init, 2x fused GCN layer, pipe gather, EdgeHead,
+pool, NoLeakHead) + cross-entropy + backward + gradient all-reduce (N>1) +
+clip_grad_norm_(1.0) + AdamW step — train mode, dropout 0.1, fp32.  Inputs are
+synthetic residual windows of the reference shape (B, 36, 29) with time features,
+resident in HBM before timing (the frozen-predictor residual build is a separate
+model and is not part of the detector step).  Weak scaling: B windows per rank.
+
+Roofline: the dominant HIP kernel is the fused GCN layer (lg_gcn_fwd, the
+scatter-aggregate).  Its algorithmic bytes per launch follow SURVEY §8(d):
+8*B*N*D + 4*(N+1) + 8*E'  (read x once, write y once, single-graph CSR), timed with
+HIP events on the launch stream over the timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "leak-det-gnn_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+LTA_INP = REPO / "leak-det-gnn_amd" / "data" / "L-TOWN-A.inp"
+SENSORS = ['n54', 'n105', 'n114', 'n163', 'n188', 'n229', 'n288', 'n296', 'n332', 'n342', 'n410', 'n415', 'n429',
+           'n458', 'n469', 'n495', 'n506', 'n516', 'n519', 'n549', 'n613', 'n636', 'n644', 'n679', 'n722', 'n726',
+           'n740', 'n752', 'n769']  # reference configs/sim_LTA.yaml:21
+
+
+def all_pipe_ids(inp: Path):
+    from models.utils import parse_epanet_inp
+    sec = parse_epanet_inp(inp)
+    return sorted({ln.split()[0] for ln in sec["PIPES"]})  # dataset order: sorted pipe ids (datasets.py:353)
+
+
+def time_features(B: int, L: int, gen: torch.Generator) -> torch.Tensor:
+    """(B, L, 9): hour sin/cos + day-of-week one-hot at 5-min steps (datasets.py:49-59)."""
+    start = torch.randint(0, 7 * 288, (B, 1), generator=gen)
+    t = start + torch.arange(L).view(1, L)
+    minutes = (t % 288) * 5
+    ang = 2 * np.pi * (minutes.float() / 60.0) / 24.0
+    dow = (t // 288) % 7
+    return torch.cat([ang.sin().unsqueeze(-1), ang.cos().unsqueeze(-1),
+                      torch.nn.functional.one_hot(dow, 7).float()], dim=-1)
+
+
+def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
+    """Time the oracle's CPU restatement of the same step on the host cores (reported only)."""
+    from oracle.detector_ref import LeakDetectorRef
+    torch.set_num_threads(threads)
+    pipes = all_pipe_ids(LTA_INP)
+    torch.manual_seed(0)
+    m = LeakDetectorRef(LTA_INP, SENSORS, pipes).train()
+    gen = torch.Generator().manual_seed(1234)
+    r = torch.randn(batch, 36, 29, generator=gen)
+    tf = time_features(batch, 36, gen)
+    lab = torch.randint(0, len(pipes) + 1, (batch,), generator=gen)
+
+    def step():
+        m.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(m(r, tf), lab).backward()
+
+    step()  # warm-up
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 20):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": batch / med, "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"{len(times)} train-mode fwd+CE+bwd steps of B={batch} L-TOWN-A windows, median "
+                      f"{med * 1e3:.1f} ms/step (oracle/detector_ref.py on torch CPU, {threads} threads)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="windows per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline sampling")
+    args = ap.parse_args()
+
+    from models import ops
+    from models.ddp import GradAllReduce, init_distributed
+    from models.detector import LeakDetector
+
+    rank, local_rank, world = init_distributed()
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    pipes = all_pipe_ids(LTA_INP)
+    P, B = len(pipes), args.batch
+
+    torch.manual_seed(0)
+    model = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
+                         use_time=True).to(dev).train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    allreduce = GradAllReduce(model.parameters())
+    N = len(model.node_names)
+    E1 = int(model.edge_index_single.shape[1]) + N  # E' = E + N self loops
+
+    gen = torch.Generator().manual_seed(1234 + rank)
+    residual = torch.randn(B, 36, len(SENSORS), generator=gen).to(dev)
+    tfeat = time_features(B, 36, gen).to(dev)
+    label = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
+    loss_fn = torch.nn.CrossEntropyLoss()
+
+    def step():
+        logits = model(residual, tfeat)
+        loss = loss_fn(logits, label)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        allreduce()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "pipe_gather", "pipe_scatter", "mean_pool"])
+    ops.set_kernel_timer(timer)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # pass 1: wall clock of exactly K steps (no event instrumentation inside)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # pass 2: per-kernel HIP-event durations over the same number of steps
+    timer.enabled = True
+    for _ in range(args.steps):
+        step()
+    barrier()
+    timer.enabled = False
+    kms = {k: timer.mean_ms(k) for k in timer.names}
+    final_loss = float(loss.item())
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    windows = B * world * args.steps
+    value = windows / elapsed
+    D = 64
+    fwd_bytes = 8 * B * N * D + 4 * (N + 1) + 8 * E1
+    fwd_ms = kms["gcn_fwd"]
+    achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    out = {
+        "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic residual windows (B,36,29) + time features, random-init weights",
+        "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",
+                   "nodes": N, "edge_columns": E1 - N, "pipes": P, "windows_per_rank": B,
+                   "global_batch": B * world, "feat": D, "gnn_layers": 2, "parallelism": f"dp{world}",
+                   "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode"},
+        "roofline": {"kernel": "lg_gcn_fwd (fused gather-aggregate + MFMA transform)", "bound": "hbm",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
+        "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
+        "final_loss": round(final_loss, 4),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(B, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

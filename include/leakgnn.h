@@ -1,0 +1,176 @@
+/*
+ * leakgnn.h — C ABI of the MI355X-native GNN message-passing library (libleakgnn.so).
+ *
+ * This is the drop-in boundary for the hot path of Mateng0228/Leak-det-gnn:
+ * the GCN message passing inside models/detector.py::LeakDetector (forward and
+ * backward).  The reference has no FFI of its own: its hot path calls PyG
+ * (`torch_geometric.nn.GCNConv`, `global_mean_pool`; detector.py:23,162-164,199,215)
+ * and plain torch indexing.  Each entry point below names the reference call it
+ * replaces (file:line relative to the reference repository root).  The Python
+ * binding a maintainer would add on the reference side is shown in INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *  - Pointers are DEVICE pointers (caller-owned, e.g. PyTorch caching allocator)
+ *    unless the parameter name ends in `_host`.  The library never allocates:
+ *    callers pass workspace sized by the matching *_workspace_bytes() query.
+ *  - Work is enqueued on `stream` (a hipStream_t; NULL = legacy default stream).
+ *    No entry point synchronises the device or the host, so every call is
+ *    capturable into a hipGraph.
+ *  - Return value: LG_OK (0) or a negative LG_E* code; lg_strerror() names it.
+ *    A launch failure returns LG_EHIP.  The library keeps no mutable global state
+ *    and is reentrant.
+ *  - Node features are fp32, row-major [B][N][D] (window-major, then node, then
+ *    feature; one 4·D-byte row per node).  B identical graphs form the disjoint
+ *    union of reference detector.py:105-114; the library keeps ONE single-graph
+ *    CSR and offsets rows by b·N itself, so the (2, B·E) batchified edge_index is
+ *    never materialised on the hot path.
+ *  - Supported feature widths D: 32, 64 (LG_EUNSUPPORTED otherwise).
+ */
+#ifndef LEAKGNN_H
+#define LEAKGNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* lg_stream_t; /* hipStream_t */
+
+enum {
+    LG_OK = 0,
+    LG_EINVAL = -1,        /* bad argument (null pointer, negative size, index out of range) */
+    LG_EUNSUPPORTED = -2,  /* unsupported feature width / flag combination */
+    LG_EHIP = -3           /* HIP launch or runtime error */
+};
+
+/* flags for lg_gcn_fwd / lg_gcn_bwd */
+#define LG_F_BIAS      0x01  /* fwd: add bias                                                  */
+#define LG_F_RELU      0x02  /* fwd: ReLU after bias (F.relu, detector.py:200)                 */
+#define LG_F_DROPOUT   0x04  /* fwd: inverted dropout after ReLU (nn.Dropout, detector.py:201) */
+#define LG_F_MASK_IN   0x08  /* bwd: dz = dy * scale_in * [y > 0]  (ReLU/dropout backward of THIS layer's output) */
+#define LG_F_MASK_OUT  0x10  /* bwd: dx_out = dx * scale_out * [x > 0] (ReLU/dropout backward of the PREVIOUS op) */
+
+int lg_abi_version(void);
+const char* lg_strerror(int code);
+
+/* ---------------------------------------------------------------------------
+ * K4  gcn_norm + CSR build, once per graph.
+ * Replaces: PyG GCNConv.forward -> gcn_norm (add_remaining_self_loops, degree,
+ * deg^-1/2, w = dis[src]*dis[dst]) recomputed on every call because the
+ * reference constructs GCNConv with cached=False (detector.py:163, 199).
+ * Semantics (PyG published algorithm):
+ *   add_self_loops: drop existing (i,i) edges, then append (i,i) for every node
+ *                   with weight fill_value (1.0; 2.0 for improved=True)
+ *   normalize:      deg[d] = sum of weights of edges into d;  dis = deg^-1/2 (inf -> 0);
+ *                   w_e = dis[src] * weight_e * dis[dst].     normalize=0 -> w_e = weight_e.
+ * Output CSR is keyed by destination (rowptr/col/w) and its transpose keyed by
+ * source (rowptr_t/col_t/w_t, used by the backward pass).  Inside each row the
+ * entries keep ascending edge order, appended self loop last — the order PyG's
+ * scatter_add visits them — so rowptr/col are bit-exact and deterministic.
+ *   edge_index : int64 [2][E] device (row 0 = source, row 1 = target)
+ *   rowptr, rowptr_t : int32 [N+1];  col, col_t : int32 [E+N];  w, w_t : fp32 [E+N]
+ *   rowptr[N] receives the entry count (E minus dropped loops, plus N loops).
+ * ------------------------------------------------------------------------- */
+int64_t lg_graph_workspace_bytes(int64_t E, int64_t N);
+int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
+                   int add_self_loops, int normalize, float fill_value,
+                   int32_t* rowptr, int32_t* col, float* w,
+                   int32_t* rowptr_t, int32_t* col_t, float* w_t,
+                   void* workspace, lg_stream_t stream);
+
+/* Pipe-endpoint incidence CSR, once per model (backward of detector.py:206-210).
+ *   ends : int64 [P][2] device (pipe_ends, utils.py:352-358)
+ *   inc_rowptr : int32 [N+1];  inc_item : int32 [2P], item = 2*p + role (role 0 = u, 1 = v),
+ *   ascending item order inside each node's row. */
+int64_t lg_incidence_workspace_bytes(int64_t P, int64_t N);
+int lg_incidence_build(const int64_t* ends, int64_t P, int64_t N,
+                       int32_t* inc_rowptr, int32_t* inc_item,
+                       void* workspace, lg_stream_t stream);
+
+/* K3  disjoint-union edge index (bit-exact).
+ * Replaces: detector.py:105-114 `_batchify_edge_index`:  out[:, b*E + e] = ei[:, e] + b*N.
+ *   edge_index : int64 [2][E];  out : int64 [2][B*E] */
+int lg_batchify_edge_index(const int64_t* edge_index, int64_t E, int64_t N, int64_t B,
+                           int64_t* out, lg_stream_t stream);
+
+/* K1+K2  node initialisation (detector.py:178-190) given the sensor projection.
+ *   x0[b][n] = dropout(relu(sensor_slot[n] >= 0 ? proj[b][sensor_slot[n]] : bias))
+ * where proj[b][s] = h_s[b][s] @ Ws[:, :D]^T + Ws[:, D] + bs is computed by the caller
+ * (a 7,424 x 64 x 64 GEMM at B=256) and bias = bs (rows with h0 = 0, mask = 0).
+ *   sensor_slot : int32 [N]  (-1 for non-sensor nodes)
+ *   proj : fp32 [B][S][D];  bias : fp32 [D];  x0 : fp32 [B][N][D]
+ *   flags: LG_F_DROPOUT (p, seed as lg_gcn_fwd; salt distinguishes the call site) */
+int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float* bias, float* x0,
+                     int64_t B, int64_t N, int64_t S, int64_t D,
+                     int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+
+/* K5+K6+K7  fused GCN layer forward (one launch).
+ * Replaces: GCNConv.forward (lin -> propagate -> +bias, detector.py:199) and the
+ * following F.relu + dropout (detector.py:200-201):
+ *   y = dropout(relu( Ahat (x W^T) + b ))  computed as  (Ahat x) W^T + b
+ * Each 64-lane wavefront owns a 16-row tile: CSR gather + segmented reduce of the
+ * neighbour rows (fp32), the tile staged in LDS, then the 16 x D x D product on
+ * MFMA (v_mfma_f32_16x16x4_f32, exact fp32), bias/ReLU/dropout epilogue, and a
+ * coalesced row store.
+ *   rowptr/col/w : CSR from lg_graph_build;  x, y : fp32 [B][N][D];  W : fp32 [D][D]
+ *   (nn.Linear layout [out][in]);  bias : fp32 [D] or NULL.
+ *   Dropout: keep element (row, c) iff hash(seed, salt, row*D + c) >= p, scale 1/(1-p).
+ *   x and y must not alias. */
+int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
+               const float* x, const float* W, const float* bias, float* y,
+               int64_t B, int64_t N, int64_t D,
+               int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+
+/* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
+ * weights; no transform).  Used for the HBM-roofline stress case (config C5). */
+int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,
+            const float* x, float* y, int64_t B, int64_t N, int64_t D, lg_stream_t stream);
+
+/* Fused GCN layer backward (one main launch + one deterministic slab reduction).
+ * Given dy = dL/dy of this layer's output:
+ *   dz     = LG_F_MASK_IN ? dy * scale_in * [y > 0] : dy
+ *   t      = Ahat^T dz                     (gather over the transposed CSR)
+ *   dx     = t W                           (MFMA)
+ *   dW     = t^T x                         (MFMA, per-block fp32 slabs, fixed-order reduce)
+ *   db     = sum_rows dz
+ *   dx_out = LG_F_MASK_OUT ? dx * scale_out * [x > 0] : dx
+ * Replaces: the autograd backward of GCNConv (lin, propagate, bias) and of the
+ * relu/dropout pairs around it (detector.py:189-190, 198-201).
+ *   y may be NULL unless LG_F_MASK_IN;  db may be NULL.
+ *   workspace : lg_gcn_bwd_workspace_bytes(D) bytes. */
+int64_t lg_gcn_bwd_workspace_bytes(int64_t D);
+int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t,
+               const float* dy, const float* y, const float* x, const float* W,
+               float* dx_out, float* dW, float* db,
+               int64_t B, int64_t N, int64_t D,
+               int flags, float scale_in, float scale_out,
+               void* workspace, lg_stream_t stream);
+
+/* K8 forward: per-pipe endpoint gather + EdgeHead feature build.
+ * Replaces: detector.py:206-210 and :87  feat = cat[h_u, h_v, |h_u - h_v|].
+ *   ends : int64 [P][2];  h : fp32 [B][N][D];  feat : fp32 [B][P][3D] */
+int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* feat,
+                       int64_t B, int64_t N, int64_t P, int64_t D, lg_stream_t stream);
+
+/* K8 backward + K10 backward, fused: deterministic segmented reduce over the
+ * incidence CSR (no atomics):
+ *   dh[b][n] = dpool[b]/N + sum over incidences (p, role) of n, in item order, of
+ *              role==u ? dfeat_u + dfeat_abs*sgn : dfeat_v - dfeat_abs*sgn,
+ *   sgn = sign(h[b][u] - h[b][v]).  dpool may be NULL.
+ * Replaces: autograd of h_nodes[:, u], h_nodes[:, v], cat, abs (detector.py:87,
+ * 209-210) and of global_mean_pool (detector.py:215). */
+int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const int64_t* ends,
+                        const float* h, const float* dfeat, const float* dpool, float* dh,
+                        int64_t B, int64_t N, int64_t P, int64_t D, lg_stream_t stream);
+
+/* K10 forward: per-window mean over the N node rows.
+ * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)
+ * (detector.py:214-215).   x : fp32 [B][N][D];  out : fp32 [B][D] */
+int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N, int64_t D, lg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LEAKGNN_H */

@@ -1,0 +1,213 @@
+// K1+K2 node init, K8 pipe-endpoint gather / incidence scatter, K10 mean pool.
+// All HBM-bound row kernels: D/4 lanes per row, one float4 per lane, rows read
+// and written as whole 4*D-byte lines.
+#include <algorithm>
+#include "common.h"
+
+namespace {
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// One row group of LPR lanes per (b, n) row.
+template <int D>
+__global__ void __launch_bounds__(256)
+k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, const float* __restrict__ bias,
+            float* __restrict__ x0, int64_t N, int64_t S, int64_t R, int dropout, float p, float scale,
+            uint64_t seed, uint32_t salt) {
+    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
+        const int64_t b = r / N, n = r - b * N;
+        const int32_t s = slot[n];
+        f32x4 v = s >= 0 ? ld4(proj + (b * S + s) * D + 4 * fg) : ld4(bias + 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = fmaxf(v[i], 0.f);
+            if (dropout) t = lg_dropout(t, p, scale, seed, salt, r * D + 4 * fg + i);
+            v[i] = t;
+        }
+        st4(x0 + r * D + 4 * fg, v);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+k_pipe_gather(const int64_t* __restrict__ ends, const float* __restrict__ h, float* __restrict__ feat, int64_t N,
+              int64_t P, int64_t BP) {
+    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * RPB + rl; i < BP; i += static_cast<int64_t>(gridDim.x) * RPB) {
+        const int64_t b = i / P, p = i - b * P;
+        const int64_t u = ends[2 * p], v = ends[2 * p + 1];
+        const f32x4 hu = ld4(h + (b * N + u) * D + 4 * fg);
+        const f32x4 hv = ld4(h + (b * N + v) * D + 4 * fg);
+        f32x4 ad;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ad[k] = fabsf(hu[k] - hv[k]);
+        float* f = feat + i * (3 * D) + 4 * fg;
+        st4(f, hu);
+        st4(f + D, hv);
+        st4(f + 2 * D, ad);
+    }
+}
+
+__device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
+
+template <int D>
+__global__ void __launch_bounds__(256)
+k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict__ inc_item,
+               const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ dfeat,
+               const float* __restrict__ dpool, float* __restrict__ dh, int64_t N, int64_t P, int64_t R) {
+    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    const float invN = static_cast<float>(N);
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
+        const int64_t b = r / N, n = r - b * N;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (dpool) {
+            const f32x4 g = ld4(dpool + b * D + 4 * fg);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = g[k] / invN;
+        }
+        const int32_t e0 = inc_rowptr[n], e1 = inc_rowptr[n + 1];
+        for (int32_t e = e0; e < e1; ++e) {
+            const int32_t it = inc_item[e];
+            const int64_t p = it >> 1;
+            const int role = it & 1;
+            const int64_t u = ends[2 * p], v = ends[2 * p + 1];
+            const float* df = dfeat + (b * P + p) * (3 * D) + 4 * fg;
+            const f32x4 hu = ld4(h + (b * N + u) * D + 4 * fg);
+            const f32x4 hv = ld4(h + (b * N + v) * D + 4 * fg);
+            const f32x4 dself = ld4(df + role * D);
+            const f32x4 dabs = ld4(df + 2 * D);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float sg = sgnf(hu[k] - hv[k]);
+                acc[k] += role == 0 ? dself[k] + dabs[k] * sg : dself[k] - dabs[k] * sg;
+            }
+        }
+        st4(dh + r * D + 4 * fg, acc);
+    }
+}
+
+// One block per window: 256 threads = RPB row groups x LPR lanes; LDS fold of the groups.
+template <int D>
+__global__ void __launch_bounds__(256)
+k_mean_pool(const float* __restrict__ x, float* __restrict__ out, int64_t N) {
+    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    __shared__ f32x4 part[256];
+    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    const int64_t b = blockIdx.x;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t n = rl; n < N; n += RPB) acc += ld4(x + (b * N + n) * D + 4 * fg);
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (rl == 0) {
+        f32x4 s = part[fg];
+        for (int g = 1; g < RPB; ++g) s += part[g * LPR + fg];
+        const float cnt = static_cast<float>(N);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = s[k] / cnt;
+        st4(out + b * D + 4 * fg, s);
+    }
+}
+
+inline unsigned row_grid(int64_t rows, int D) {
+    const int64_t rpb = 256 / (D / 4);
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, rpb), 16LL * lg_num_cus())));
+}
+
+}  // namespace
+
+extern "C" int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float* bias, float* x0,
+                                int64_t B, int64_t N, int64_t S, int64_t D, int flags, float dropout_p,
+                                uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || S < 0) return LG_EINVAL;
+    if (!sensor_slot || !bias || !x0 || (S > 0 && B > 0 && !proj)) return LG_EINVAL;
+    const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
+    if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    const int64_t R = B * N;
+    if (R == 0) return LG_OK;
+    const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    hipStream_t s = lg_stream(stream);
+    switch (D) {
+        case 64:
+            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, S, R, dropout, dropout_p,
+                                                            scale, seed, salt);
+            break;
+        case 32:
+            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, S, R, dropout, dropout_p,
+                                                            scale, seed, salt);
+            break;
+        default:
+            return LG_EUNSUPPORTED;
+    }
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* feat, int64_t B, int64_t N,
+                                  int64_t P, int64_t D, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
+    const int64_t BP = B * P;
+    if (BP == 0) return LG_OK;
+    if (!ends || !h || !feat) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    switch (D) {
+        case 64: k_pipe_gather<64><<<row_grid(BP, 64), 256, 0, s>>>(ends, h, feat, N, P, BP); break;
+        case 32: k_pipe_gather<32><<<row_grid(BP, 32), 256, 0, s>>>(ends, h, feat, N, P, BP); break;
+        default: return LG_EUNSUPPORTED;
+    }
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const int64_t* ends,
+                                   const float* h, const float* dfeat, const float* dpool, float* dh, int64_t B,
+                                   int64_t N, int64_t P, int64_t D, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
+    const int64_t R = B * N;
+    if (R == 0) return LG_OK;
+    if (!inc_rowptr || !h || !dh || (P > 0 && (!inc_item || !ends || !dfeat))) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    switch (D) {
+        case 64:
+            k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, ends, h, dfeat, dpool, dh, N, P,
+                                                               R);
+            break;
+        case 32:
+            k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, ends, h, dfeat, dpool, dh, N, P,
+                                                               R);
+            break;
+        default:
+            return LG_EUNSUPPORTED;
+    }
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N, int64_t D, lg_stream_t stream) {
+    if (B < 0 || N <= 0) return LG_EINVAL;
+    if (B == 0) return LG_OK;
+    if (!x || !out || B > INT32_MAX) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    switch (D) {
+        case 64: k_mean_pool<64><<<static_cast<unsigned>(B), 256, 0, s>>>(x, out, N); break;
+        case 32: k_mean_pool<32><<<static_cast<unsigned>(B), 256, 0, s>>>(x, out, N); break;
+        default: return LG_EUNSUPPORTED;
+    }
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_abi_version(void) { return 1; }
+
+extern "C" const char* lg_strerror(int code) {
+    switch (code) {
+        case LG_OK: return "ok";
+        case LG_EINVAL: return "invalid argument";
+        case LG_EUNSUPPORTED: return "unsupported feature width or flags";
+        case LG_EHIP: return "HIP launch/runtime error";
+        default: return "unknown error";
+    }
+}

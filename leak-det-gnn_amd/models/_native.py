@@ -1,0 +1,93 @@
+"""ctypes binding of libleakgnn.so (the C ABI declared in include/leakgnn.h).
+
+The product path has no CPU fallback: if the library is missing, or a tensor is
+not on a ROCm device, the ops raise.  The library is built in-tree by
+``make -C leak-det-gnn_amd`` (``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_PKG_ROOT = Path(__file__).resolve().parent.parent
+LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
+
+LG_F_BIAS = 0x01
+LG_F_RELU = 0x02
+LG_F_DROPOUT = 0x04
+LG_F_MASK_IN = 0x08
+LG_F_MASK_OUT = 0x10
+
+_i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
+                                    ctypes.c_float, ctypes.c_void_p)
+
+# name -> (restype, argtypes); mirrors include/leakgnn.h exactly.
+SIGNATURES = {
+    "lg_abi_version": (_i32, []),
+    "lg_strerror": (ctypes.c_char_p, [_i32]),
+    "lg_graph_workspace_bytes": (_i64, [_i64, _i64]),
+    "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "lg_incidence_workspace_bytes": (_i64, [_i64, _i64]),
+    "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
+    "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),
+    "lg_node_init_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "lg_gcn_bwd_workspace_bytes": (_i64, [_i64]),
+    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p, _p]),
+    "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
+}
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libleakgnn.so once; raise ImportError (never fall back) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.is_file():
+            raise ImportError(
+                f"libleakgnn.so not found at {LIB_PATH}; build it with `make -C {_PKG_ROOT}` "
+                "(or __graft_entry__.build()). The GNN hot path has no CPU fallback.")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+class LeakGNNError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().lg_strerror(rc).decode()
+        raise LeakGNNError(f"{what} failed: {msg} (code {rc})")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    """hipStream_t of torch's current stream on t's device (kernels are enqueued there)."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_device(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(
+                "leakgnn ops run only on a ROCm GPU (tensor on %s); there is no CPU path" % t.device)
+        if not t.is_contiguous():
+            raise RuntimeError("leakgnn ops need contiguous tensors")

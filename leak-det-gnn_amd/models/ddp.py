@@ -1,0 +1,83 @@
+"""Batch data parallelism for the detector: one process per GPU, windows sharded
+across ranks, one gradient all-reduce per step (RCCL over xGMI with backend
+"nccl"; gloo on CPU for tests).
+
+The reference is single-device; this is the one collective the
+multi-GPU path adds.  The gradient of the 60,418-parameter detector is 241.7 KB:
+a single flat bucket, all-reduced once after backward — at xGMI link rates this
+is a few tens of microseconds, so no bucketing/overlap machinery is warranted.
+Mean-reduction semantics: each rank's loss is the mean over its local windows,
+the all-reduce averages over ranks, so with equal shards the gradient equals the
+single-process gradient of the global batch.
+"""
+from __future__ import annotations
+
+import os
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def dist_env() -> tuple:
+    """(rank, local_rank, world_size) from torchrun's environment (1-process defaults)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init_distributed(backend: Optional[str] = None) -> tuple:
+    rank, local_rank, world = dist_env()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group(backend, rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    return rank, local_rank, world
+
+
+class GradAllReduce:
+    """Average gradients of `params` across the default process group in ONE flat bucket."""
+
+    def __init__(self, params: Iterable[torch.nn.Parameter], group=None):
+        self.params: List[torch.nn.Parameter] = [p for p in params if p.requires_grad]
+        self.group = group
+        numel = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.empty(numel, device=dev, dtype=torch.float32)
+
+    def __call__(self) -> None:
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
+            return
+        world = dist.get_world_size(self.group)
+        off = 0
+        views = []
+        for p in self.params:
+            n = p.numel()
+            v = self.flat[off:off + n].view_as(p)
+            if p.grad is None:
+                v.zero_()
+            else:
+                v.copy_(p.grad)
+            views.append(v)
+            off += n
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.flat.div_(world)
+        for p, v in zip(self.params, views):
+            if p.grad is None:
+                p.grad = v.clone()
+            else:
+                p.grad.copy_(v)
+
+
+def shard_range(global_batch: int, rank: int, world: int) -> range:
+    """Contiguous per-rank slice of the global sample index range (datasets are seeded by
+    seed + idx, datasets.py:236,490, so the global batch is the same at any world size)."""
+    if global_batch % world:
+        raise ValueError(f"global batch {global_batch} not divisible by world size {world}")
+    per = global_batch // world
+    return range(rank * per, (rank + 1) * per)

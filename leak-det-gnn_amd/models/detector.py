@@ -1,0 +1,155 @@
+"""LeakDetector on MI355X: drop-in for reference models/detector.py.
+
+Same module tree, constructor / forward signatures and state-dict keys as the
+reference (detector.py:28-218), so models/train_detector.py, eval/event_evaluator.py
+and models/window_evaluator.py use it unchanged:
+
+  sensor_encoder.gru.*              SharedSensorGRUEncoder   (detector.py:28-73)
+  sensor_to_node.{weight,bias}      node init Linear(65, 64)  (detector.py:160, 184-190)
+  convs.{i}.lin.weight, convs.{i}.bias   GCNConv               (detector.py:162-164)
+  edge_head.mlp.{0,3}.*             EdgeHead                  (detector.py:76-88)
+  noleak_head.mlp.{0,3}.*           NoLeakHead                (detector.py:91-102)
+
+What runs where (forward + backward):
+  * GRU sensor encoder, the 29-row sensor projection, the EdgeHead / NoLeakHead
+    MLPs and the loss: stock PyTorch-ROCm (MIOpen / hipBLASLt).
+  * Node init, every GCNConv + ReLU + dropout, the pipe-endpoint gather and the
+    per-window mean pool: libleakgnn HIP kernels (ops.GNNTrunkFn, ops.PipeHeadsFn)
+    over ONE device-resident single-graph CSR; the (2, B*E) batchified
+    edge_index of the reference (detector.py:195-196) is never built.
+There is no CPU path: forward raises on CPU tensors.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Dict, Optional, Sequence
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .gcn import GCNConv, global_mean_pool  # noqa: F401  (re-exported PyG-compatible API)
+from .utils import WDNGraph, build_wdn_graph_from_inp
+
+
+class SharedSensorGRUEncoder(nn.Module):
+    """One GRU shared by all sensors: (B, L, S) residuals (+ (B, L, 9) time features) -> (B, S, d)."""
+
+    def __init__(self, time_dim: int = 9, hidden_size: int = 64, num_layers: int = 1, dropout: float = 0.0,
+                 use_time: bool = True) -> None:
+        super().__init__()
+        self.use_time = bool(use_time)
+        self.hidden_size = int(hidden_size)
+        self.gru = nn.GRU(input_size=1 + (time_dim if self.use_time else 0), hidden_size=self.hidden_size,
+                          num_layers=num_layers, batch_first=True, dropout=dropout if num_layers > 1 else 0.0)
+
+    def forward(self, r: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
+        B, L, S = r.shape
+        seq = r.transpose(1, 2).reshape(B * S, L, 1)  # sequence index = b*S + s
+        if self.use_time:
+            if tfeat is None:
+                raise ValueError("tfeat required when use_time=True")
+            tf = tfeat.unsqueeze(1).expand(B, S, L, tfeat.shape[-1]).reshape(B * S, L, -1)
+            seq = torch.cat([seq, tf], dim=-1)
+        out, _ = self.gru(seq)
+        return out[:, -1, :].view(B, S, -1)
+
+
+class EdgeHead(nn.Module):
+    def __init__(self, node_dim: int, hidden_dim: int = 128, dropout: float = 0.1) -> None:
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(node_dim * 3, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+                                 nn.Linear(hidden_dim, 1))
+
+    def forward(self, h_u: torch.Tensor, h_v: torch.Tensor) -> torch.Tensor:
+        return self.forward_feat(torch.cat([h_u, h_v, (h_u - h_v).abs()], dim=-1))
+
+    def forward_feat(self, feat: torch.Tensor) -> torch.Tensor:
+        """feat = cat[h_u, h_v, |h_u - h_v|] already built (by lg_pipe_gather_fwd)."""
+        return self.mlp(feat).squeeze(-1)
+
+
+class NoLeakHead(nn.Module):
+    def __init__(self, node_dim: int, hidden_dim: int = 128, dropout: float = 0.1) -> None:
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(node_dim, hidden_dim), nn.ReLU(), nn.Dropout(dropout),
+                                 nn.Linear(hidden_dim, 1))
+
+    def forward(self, pooled: torch.Tensor) -> torch.Tensor:
+        return self.mlp(pooled).squeeze(-1)
+
+
+def _batchify_edge_index(edge_index_single: torch.Tensor, num_nodes: int, batch_size: int) -> torch.Tensor:
+    """(2, E) -> (2, E*B) disjoint union, column b*E + e = edge e offset by b*N (detector.py:105-114).
+    Runs on the device (lg_batchify_edge_index); bit-exact."""
+    return ops.batchify_edge_index(edge_index_single, num_nodes, batch_size)
+
+
+class LeakDetector(nn.Module):
+    """residual (B, L_det, S), tfeat (B, L_det, 9) -> logits (B, num_pipes + 1); class P = no leak."""
+
+    def __init__(self, inp_path: str | Path, sensor_node_ids: Sequence[str], pipe_ids_in_order: Sequence[str],
+                 sensor_hidden: int = 64, node_hidden: int = 64, gnn_layers: int = 2, dropout: float = 0.1,
+                 use_time: bool = True, include_links: Sequence[str] = ("PIPES", "PUMPS", "VALVES")) -> None:
+        super().__init__()
+        self.graph: WDNGraph = build_wdn_graph_from_inp(inp_path=inp_path, sensor_node_ids=sensor_node_ids,
+                                                        pipe_ids_in_order=pipe_ids_in_order,
+                                                        include_links=include_links, add_self_loops=False,
+                                                        make_undirected=True)
+        self.node_names = self.graph.node_names
+        self.node_to_idx = self.graph.node_to_idx
+        self.pipe_ids = self.graph.pipe_ids
+        self.pipe_to_idx = self.graph.pipe_to_idx
+        self.pipe_ends = torch.tensor(self.graph.pipe_ends, dtype=torch.long)
+        self.edge_index_single = self.graph.edge_index
+        self.sensor_node_ids = list(sensor_node_ids)
+        self.sensor_node_idx = torch.tensor([self.node_to_idx[n] for n in self.sensor_node_ids], dtype=torch.long)
+
+        self.sensor_encoder = SharedSensorGRUEncoder(hidden_size=sensor_hidden, use_time=use_time)
+        self.sensor_to_node = nn.Linear(sensor_hidden + 1, node_hidden)
+        self.convs = nn.ModuleList(
+            [GCNConv(node_hidden, node_hidden, add_self_loops=True, normalize=True) for _ in range(gnn_layers)])
+        self.dropout = nn.Dropout(dropout)
+        self.edge_head = EdgeHead(node_hidden, hidden_dim=128, dropout=dropout)
+        self.noleak_head = NoLeakHead(node_hidden, hidden_dim=128, dropout=dropout)
+        self._dev_state: Dict[torch.device, tuple] = {}
+
+    # -- device-resident graph state (built once per device; not part of state_dict)
+    def _device_state(self, device: torch.device):
+        st = self._dev_state.get(device)
+        if st is None:
+            N = len(self.node_names)
+            graph = ops.GCNGraph.build(self.edge_index_single, N, device, add_self_loops=True, normalize=True)
+            inc = ops.Incidence.build(self.pipe_ends, N, device)
+            slot = torch.full((N,), -1, dtype=torch.int32)
+            for s, n in enumerate(self.sensor_node_idx.tolist()):
+                slot[n] = s  # duplicate sensor ids: last write wins, as h0[:, idx] = h_s does
+            live = torch.tensor([float(slot[n] == s) for s, n in enumerate(self.sensor_node_idx.tolist())])
+            nonsensor = torch.nonzero(slot < 0).flatten()
+            st = (graph, inc, slot.to(device), self.sensor_node_idx.to(device),
+                  None if bool(live.all()) else live.to(device), nonsensor.to(device))
+            self._dev_state[device] = st
+        return st
+
+    def forward(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if not residual.is_cuda:
+            raise RuntimeError("LeakDetector runs on a ROCm GPU only (libleakgnn has no CPU path)")
+        B, L, S = residual.shape
+        graph, inc, slot, sensor_idx, slot_live, nonsensor = self._device_state(residual.device)
+
+        h_s = self.sensor_encoder(residual, tfeat)                        # (B, S, Ds)
+        Ds = h_s.shape[-1]
+        Wn, bn = self.sensor_to_node.weight, self.sensor_to_node.bias     # (D, Ds+1), (D,)
+        # rows with a sensor: [h_s, 1] W^T + b ; rows without: [0, 0] W^T + b = b
+        proj = torch.addmm(Wn[:, Ds] + bn, h_s.reshape(B * S, Ds), Wn[:, :Ds].t()).view(B, S, -1)
+        wb = []
+        for conv in self.convs:
+            wb += [conv.lin.weight, conv.bias]
+        cfg = ops.TrunkConfig(graph=graph, sensor_slot=slot, sensor_idx=sensor_idx, slot_live=slot_live,
+                              nonsensor_idx=nonsensor,
+                              dropout_p=float(self.dropout.p), training=self.training)
+        h_nodes = ops.GNNTrunkFn.apply(cfg, proj, bn, *wb)               # (B, N, D)
+        feat, pooled = ops.PipeHeadsFn.apply(h_nodes, inc)              # (B, P, 3D), (B, D)
+        pipe_logits = self.edge_head.forward_feat(feat)                   # (B, P)
+        noleak_logit = self.noleak_head(pooled).unsqueeze(-1)             # (B, 1)
+        return torch.cat([pipe_logits, noleak_logit], dim=-1)

@@ -1,0 +1,405 @@
+"""Autograd-level operators over libleakgnn (HIP kernels for gfx950).
+
+Graph state lives on the device once per graph:
+  * ``GCNGraph``   - gcn_norm'ed CSR keyed by destination and its transpose
+                     (lg_graph_build; replaces PyG gcn_norm, recomputed per call in
+                     the reference because GCNConv is built with cached=False,
+                     detector.py:163,199).
+  * ``Incidence``  - pipe-endpoint incidence CSR (lg_incidence_build) for the
+                     deterministic backward of the EdgeHead gathers (detector.py:206-210).
+
+Autograd functions:
+  * ``GCNLayerFn``    - one GCNConv (lin -> propagate -> +bias), PyG semantics.
+  * ``GNNTrunkFn``    - LeakDetector node init + all conv/relu/dropout layers
+                        (detector.py:178-201) as one fused forward / backward chain.
+  * ``PipeHeadsFn``   - pipe endpoint features + per-window mean pool
+                        (detector.py:206-215), backward fused into one kernel.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _native as nat
+from ._native import check, load_library, ptr, require_device, stream_of
+
+SUPPORTED_D = (32, 64)
+
+
+# ----------------------------------------------------------------------------- timing hook
+class KernelTimer:
+    """Optional HIP-event bracketing of named kernel launches (used by bench.py).
+
+    Events are recorded on the stream the kernel is enqueued on (torch's current
+    stream), so elapsed times are the device-side durations of those launches.
+    """
+
+    def __init__(self, names: Sequence[str]):
+        self.names = set(names)
+        self.events: dict = {n: [] for n in names}
+        self.enabled = False
+
+    def wrap(self, name: str, device: torch.device):
+        timer = self
+
+        class _Ctx:
+            def __enter__(self_inner):
+                if timer.enabled and name in timer.names:
+                    s = torch.cuda.current_stream(device)
+                    self_inner.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    self_inner.ev[0].record(s)
+                else:
+                    self_inner.ev = None
+                return self_inner
+
+            def __exit__(self_inner, *exc):
+                if self_inner.ev is not None:
+                    self_inner.ev[1].record(torch.cuda.current_stream(device))
+                    timer.events[name].append(self_inner.ev)
+                return False
+
+        return _Ctx()
+
+    def mean_ms(self, name: str) -> Optional[float]:
+        evs = self.events.get(name, [])
+        if not evs:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+
+    def count(self, name: str) -> int:
+        return len(self.events.get(name, []))
+
+    def reset(self) -> None:
+        for n in self.events:
+            self.events[n] = []
+
+
+_TIMER: Optional[KernelTimer] = None
+
+
+def set_kernel_timer(timer: Optional[KernelTimer]) -> None:
+    global _TIMER
+    _TIMER = timer
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def _timed(name: str, device: torch.device):
+    if _TIMER is None:
+        return _NullCtx()
+    return _TIMER.wrap(name, device)
+
+
+# ----------------------------------------------------------------------------- graph state
+def _validate_edge_index(edge_index: torch.Tensor, num_nodes: int) -> None:
+    if edge_index.dim() != 2 or edge_index.size(0) != 2:
+        raise ValueError(f"edge_index must be (2, E), got {tuple(edge_index.shape)}")
+    if edge_index.dtype != torch.long:
+        raise TypeError("edge_index must be int64")
+    if edge_index.numel() and not edge_index.is_cuda:
+        lo, hi = int(edge_index.min()), int(edge_index.max())
+        if lo < 0 or hi >= num_nodes:
+            raise IndexError(f"edge_index values must lie in [0, {num_nodes}), got [{lo}, {hi}]")
+
+
+@dataclass
+class GCNGraph:
+    num_nodes: int
+    num_edges: int
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    w: torch.Tensor
+    rowptr_t: torch.Tensor
+    col_t: torch.Tensor
+    w_t: torch.Tensor
+
+    @staticmethod
+    def build(edge_index: torch.Tensor, num_nodes: int, device: torch.device, add_self_loops: bool = True,
+              normalize: bool = True, improved: bool = False) -> "GCNGraph":
+        """gcn_norm + CSR on the device (lg_graph_build)."""
+        lib = load_library()
+        _validate_edge_index(edge_index, num_nodes)
+        ei = edge_index.to(device=device, dtype=torch.long).contiguous()
+        E, N = int(ei.size(1)), int(num_nodes)
+        cap = E + N
+        i32 = dict(device=device, dtype=torch.int32)
+        f32 = dict(device=device, dtype=torch.float32)
+        g = GCNGraph(N, E, torch.empty(N + 1, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32),
+                     torch.empty(N + 1, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32))
+        ws = torch.empty(int(lib.lg_graph_workspace_bytes(E, N)), device=device, dtype=torch.uint8)
+        fill = 2.0 if improved else 1.0
+        check(lib.lg_graph_build(ptr(ei), E, N, int(add_self_loops), int(normalize), fill, ptr(g.rowptr),
+                                 ptr(g.col), ptr(g.w), ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(ws),
+                                 stream_of(ei)), "lg_graph_build")
+        g._keepalive = (ei, ws)  # freed after the stream consumes them
+        return g
+
+
+@dataclass
+class Incidence:
+    num_nodes: int
+    num_pipes: int
+    ends: torch.Tensor      # int64 (P, 2) device
+    rowptr: torch.Tensor    # int32 (N+1,)
+    item: torch.Tensor      # int32 (2P,)
+
+    @staticmethod
+    def build(pipe_ends: torch.Tensor, num_nodes: int, device: torch.device) -> "Incidence":
+        lib = load_library()
+        ends = pipe_ends.to(device=device, dtype=torch.long).contiguous()
+        P, N = int(ends.size(0)), int(num_nodes)
+        if P and not pipe_ends.is_cuda:
+            lo, hi = int(pipe_ends.min()), int(pipe_ends.max())
+            if lo < 0 or hi >= N:
+                raise IndexError(f"pipe_ends values must lie in [0, {N}), got [{lo}, {hi}]")
+        inc = Incidence(N, P, ends, torch.empty(N + 1, device=device, dtype=torch.int32),
+                        torch.empty(max(2 * P, 1), device=device, dtype=torch.int32))
+        ws = torch.empty(int(lib.lg_incidence_workspace_bytes(P, N)), device=device, dtype=torch.uint8)
+        check(lib.lg_incidence_build(ptr(ends), P, N, ptr(inc.rowptr), ptr(inc.item), ptr(ws), stream_of(ends)),
+              "lg_incidence_build")
+        inc._keepalive = ws
+        return inc
+
+
+def batchify_edge_index(edge_index_single: torch.Tensor, num_nodes: int, batch_size: int) -> torch.Tensor:
+    """Disjoint union of B copies (bit-exact with detector.py:105-114), on the device."""
+    require_device(edge_index_single)
+    lib = load_library()
+    ei = edge_index_single.to(torch.long).contiguous()
+    E = int(ei.size(1))
+    out = torch.empty(2, E * batch_size, device=ei.device, dtype=torch.long)
+    check(lib.lg_batchify_edge_index(ptr(ei), E, int(num_nodes), int(batch_size), ptr(out), stream_of(ei)),
+          "lg_batchify_edge_index")
+    return out
+
+
+def _new_seed() -> int:
+    # drawn from torch's CPU generator: reproducible under torch.manual_seed, no device sync
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())
+
+
+def _check_d(D: int) -> None:
+    if D not in SUPPORTED_D:
+        raise NotImplementedError(f"feature width {D} not supported by the HIP kernels (supported: {SUPPORTED_D})")
+
+
+# ----------------------------------------------------------------------------- GCNConv
+class GCNLayerFn(torch.autograd.Function):
+    """y = Ahat (x W^T) + b for one graph (B=1 view of the kernels)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, graph: GCNGraph):
+        lib = load_library()
+        x = x.contiguous()
+        weight = weight.contiguous()
+        require_device(x, weight, bias)
+        Ntot, D = x.shape
+        _check_d(D)
+        if weight.shape != (D, D):
+            raise NotImplementedError("GCNConv kernels need in_channels == out_channels")
+        y = torch.empty_like(x)
+        flags = nat.LG_F_BIAS if bias is not None else 0
+        with _timed("gcn_fwd", x.device):
+            check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(weight), ptr(bias),
+                                 ptr(y), 1, Ntot, D, flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
+        ctx.graph = graph
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = load_library()
+        x, weight = ctx.saved_tensors
+        g = ctx.graph
+        dy = dy.contiguous()
+        Ntot, D = x.shape
+        dx = torch.empty_like(x)
+        dW = torch.empty_like(weight)
+        db = torch.empty(D, device=x.device, dtype=x.dtype)
+        ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
+        with _timed("gcn_bwd", x.device):
+            check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), None, ptr(x), ptr(weight),
+                                 ptr(dx), ptr(dW), ptr(db), 1, Ntot, D, 0, 1.0, 1.0, ptr(ws), stream_of(x)),
+                  "lg_gcn_bwd")
+        return dx, dW, (db if ctx.has_bias else None), None
+
+
+# ----------------------------------------------------------------------------- detector trunk
+@dataclass
+class TrunkConfig:
+    graph: GCNGraph
+    sensor_slot: torch.Tensor      # int32 (N,), -1 for non-sensor nodes
+    sensor_idx: torch.Tensor       # int64 (S,): node row of sensor slot s
+    slot_live: Optional[torch.Tensor]  # float (S,) 1 where slot s owns its node (None: all unique)
+    nonsensor_idx: torch.Tensor    # int64 (N - #sensors,)
+    dropout_p: float
+    training: bool
+
+
+class GNNTrunkFn(torch.autograd.Function):
+    """Node init (detector.py:178-190) + L x [GCNConv, ReLU, Dropout] (detector.py:198-201).
+
+    Forward:  x0 = dropout(relu(slot>=0 ? proj[b, slot] : node_bias))        (lg_node_init_fwd)
+              x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                   (lg_gcn_fwd, fused)
+    Backward: one lg_gcn_bwd per layer; the ReLU/dropout masks of a layer's
+              output and of its input are applied inside the kernel, read back
+              from the saved activations ([x > 0]), so no mask is stored.
+    """
+
+    @staticmethod
+    def forward(ctx, cfg: TrunkConfig, proj, node_bias, *wb):
+        lib = load_library()
+        proj = proj.contiguous()
+        require_device(proj, node_bias)
+        B, S, D = proj.shape
+        _check_d(D)
+        N = cfg.graph.num_nodes
+        L = len(wb) // 2
+        drop = cfg.training and cfg.dropout_p > 0.0
+        p = float(cfg.dropout_p) if drop else 0.0
+        seed = _new_seed() if drop else 0
+        dflag = nat.LG_F_DROPOUT if drop else 0
+        st = stream_of(proj)
+        x0 = torch.empty(B, N, D, device=proj.device, dtype=torch.float32)
+        with _timed("node_init", proj.device):
+            check(lib.lg_node_init_fwd(ptr(cfg.sensor_slot), ptr(proj), ptr(node_bias.contiguous()), ptr(x0), B, N,
+                                       S, D, dflag, p, seed, 0, st), "lg_node_init_fwd")
+        xs = [x0]
+        g = cfg.graph
+        for l in range(L):
+            W, b = wb[2 * l].contiguous(), wb[2 * l + 1].contiguous()
+            require_device(W, b)
+            y = torch.empty_like(x0)
+            with _timed("gcn_fwd", proj.device):
+                check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
+                                     D, nat.LG_F_BIAS | nat.LG_F_RELU | dflag, p, seed, l + 1, st), "lg_gcn_fwd")
+            xs.append(y)
+        ctx.cfg = cfg
+        ctx.scale = 1.0 / (1.0 - p) if drop else 1.0
+        ctx.dims = (B, S, N, D, L)
+        ctx.save_for_backward(*xs, *[t.contiguous() for t in wb[0::2]])
+        return xs[-1]
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        lib = load_library()
+        cfg = ctx.cfg
+        B, S, N, D, L = ctx.dims
+        saved = ctx.saved_tensors
+        xs, Ws = saved[:L + 1], saved[L + 1:]
+        g = cfg.graph
+        st = stream_of(xs[0])
+        dy = grad_out.contiguous()
+        ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dy.device, dtype=torch.uint8)
+        grads_wb: List[Optional[torch.Tensor]] = [None] * (2 * L)
+        for l in range(L - 1, -1, -1):
+            flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0)
+            dx = torch.empty_like(dy)
+            dW = torch.empty(D, D, device=dy.device, dtype=torch.float32)
+            db = torch.empty(D, device=dy.device, dtype=torch.float32)
+            with _timed("gcn_bwd", dy.device):
+                check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), B, N, D, flags, ctx.scale, ctx.scale,
+                                     ptr(ws), st), "lg_gcn_bwd")
+            grads_wb[2 * l], grads_wb[2 * l + 1] = dW, db
+            dy = dx  # already masked by the previous op's relu/dropout
+        dproj = dy.index_select(1, cfg.sensor_idx)
+        if cfg.slot_live is not None:
+            dproj = dproj * cfg.slot_live.view(1, -1, 1)
+        dbias = dy.index_select(1, cfg.nonsensor_idx).sum(dim=(0, 1))
+        return (None, dproj, dbias, *grads_wb)
+
+
+class PipeHeadsFn(torch.autograd.Function):
+    """feat = cat[h_u, h_v, |h_u - h_v|] per pipe and pooled = mean_n h (detector.py:87, 206-215)."""
+
+    @staticmethod
+    def forward(ctx, h, inc: Incidence):
+        lib = load_library()
+        h = h.contiguous()
+        require_device(h)
+        B, N, D = h.shape
+        _check_d(D)
+        P = inc.num_pipes
+        st = stream_of(h)
+        feat = torch.empty(B, P, 3 * D, device=h.device, dtype=torch.float32)
+        pooled = torch.empty(B, D, device=h.device, dtype=torch.float32)
+        with _timed("pipe_gather", h.device):
+            check(lib.lg_pipe_gather_fwd(ptr(inc.ends), ptr(h), ptr(feat), B, N, P, D, st), "lg_pipe_gather_fwd")
+        with _timed("mean_pool", h.device):
+            check(lib.lg_mean_pool_fwd(ptr(h), ptr(pooled), B, N, D, st), "lg_mean_pool_fwd")
+        ctx.inc = inc
+        ctx.save_for_backward(h)
+        return feat, pooled
+
+    @staticmethod
+    def backward(ctx, dfeat, dpool):
+        lib = load_library()
+        (h,) = ctx.saved_tensors
+        inc = ctx.inc
+        B, N, D = h.shape
+        P = inc.num_pipes
+        dh = torch.empty_like(h)
+        if dfeat is None:
+            dfeat = torch.zeros(B, P, 3 * D, device=h.device, dtype=h.dtype)
+        dfeat = dfeat.contiguous()
+        dpool = dpool.contiguous() if dpool is not None else None
+        with _timed("pipe_scatter", h.device):
+            check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(inc.ends), ptr(h), ptr(dfeat),
+                                          ptr(dpool), ptr(dh), B, N, P, D, stream_of(h)), "lg_pipe_scatter_bwd")
+        return dh, None
+
+
+class MeanPoolWindowsFn(torch.autograd.Function):
+    """global_mean_pool for B equal windows of N rows (batch = arange(B).repeat_interleave(N))."""
+
+    @staticmethod
+    def forward(ctx, x, B: int, N: int):
+        lib = load_library()
+        x = x.contiguous()
+        require_device(x)
+        D = x.shape[-1]
+        _check_d(D)
+        out = torch.empty(B, D, device=x.device, dtype=torch.float32)
+        check(lib.lg_mean_pool_fwd(ptr(x), ptr(out), B, N, D, stream_of(x)), "lg_mean_pool_fwd")
+        ctx.dims = (B, N)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, N = ctx.dims
+        return (dout / float(N)).unsqueeze(1).expand(B, N, dout.shape[-1]).reshape(B * N, -1), None, None
+
+
+def spmm(graph: GCNGraph, x: torch.Tensor, B: int = 1) -> torch.Tensor:
+    """y = Ahat x (PyG propagate with gcn_norm weights) for B stacked windows; no autograd."""
+    lib = load_library()
+    x = x.contiguous()
+    require_device(x)
+    D = x.shape[-1]
+    _check_d(D)
+    y = torch.empty_like(x)
+    with _timed("spmm", x.device):
+        check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, graph.num_nodes, D,
+                          stream_of(x)), "lg_spmm")
+    return y
+
+
+def wall_ms(fn, iters: int = 10) -> float:
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / iters

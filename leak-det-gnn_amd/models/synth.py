@@ -1,0 +1,101 @@
+"""Synthetic pipe-network graphs (configs C4 / C5 of BASELINE.json) and an EPANET
+.inp writer, so LeakDetector(inp_path, ...) is constructed unchanged.
+
+Topology: nodes on a jittered sqrt(N) x sqrt(N) grid; a random spanning tree of
+the 4-neighbour grid (Kruskal on random weights) plus loop chords drawn from the
+remaining grid edges, degree capped at 5; all seeded.  Node ids n{i}, pipe ids
+p{i}; the last node is the reservoir.  Generated because the reference's data
+generators need `wntr` (absent) — SURVEY §8(d) C4/C5.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+def _find(parent: np.ndarray, i: int) -> int:
+    root = i
+    while parent[root] != root:
+        root = parent[root]
+    while parent[i] != root:
+        parent[i], i = root, parent[i]
+    return root
+
+
+def synthetic_pipe_ends(num_nodes: int, num_pipes: int, seed: int = 0, max_degree: int = 5) -> np.ndarray:
+    N, P = int(num_nodes), int(num_pipes)
+    if P < N - 1:
+        raise ValueError("need at least N-1 pipes for a connected network")
+    rng = np.random.default_rng(seed)
+    W = int(np.ceil(np.sqrt(N)))
+    ids = np.arange(N)
+    x, y = ids % W, ids // W
+    right = ids[(x + 1 < W) & (ids + 1 < N)]
+    down = ids[ids + W < N]
+    cand = np.concatenate([np.stack([right, right + 1], 1), np.stack([down, down + W], 1)])
+    cand = cand[rng.permutation(len(cand))]
+    parent = np.arange(N)
+    deg = np.zeros(N, dtype=np.int64)
+    tree, rest = [], []
+    for a, b in cand:
+        ra, rb = _find(parent, a), _find(parent, b)
+        if ra != rb:
+            parent[ra] = rb
+            tree.append((a, b))
+            deg[a] += 1
+            deg[b] += 1
+        else:
+            rest.append((a, b))
+    if len(tree) != N - 1:
+        raise RuntimeError("grid spanning tree failed")
+    chords = []
+    need = P - (N - 1)
+    for a, b in rest:
+        if len(chords) >= need:
+            break
+        if deg[a] < max_degree and deg[b] < max_degree:
+            chords.append((a, b))
+            deg[a] += 1
+            deg[b] += 1
+    if len(chords) < need:
+        raise ValueError(f"cannot place {P} pipes on {N} grid nodes with degree <= {max_degree}")
+    ends = np.array(tree + chords, dtype=np.int64)
+    flip = rng.random(len(ends)) < 0.5
+    ends[flip] = ends[flip][:, ::-1]
+    return ends[rng.permutation(len(ends))]
+
+
+def synthetic_pipe_graph(num_nodes: int, num_pipes: int, seed: int = 0) -> Tuple[torch.Tensor, np.ndarray]:
+    """(edge_index (2, 2P) with columns [u->v, v->u] per pipe, pipe_ends (P, 2)) in generator numbering."""
+    ends = synthetic_pipe_ends(num_nodes, num_pipes, seed)
+    src = np.stack([ends[:, 0], ends[:, 1]], 1).reshape(-1)
+    dst = np.stack([ends[:, 1], ends[:, 0]], 1).reshape(-1)
+    return torch.from_numpy(np.stack([src, dst])), ends
+
+
+def write_synthetic_inp(path: str | Path, num_nodes: int, num_pipes: int, seed: int = 0) -> Tuple[list, list]:
+    """Write an EPANET .inp with the synthetic topology; returns (node_ids, pipe_ids)."""
+    ends = synthetic_pipe_ends(num_nodes, num_pipes, seed)
+    N = int(num_nodes)
+    rng = np.random.default_rng(seed + 1)
+    W = int(np.ceil(np.sqrt(N)))
+    node_ids = [f"n{i}" for i in range(N)]
+    pipe_ids = [f"p{i}" for i in range(len(ends))]
+    lines = ["[TITLE]", f"synthetic pipe network N={N} P={len(ends)} seed={seed}", "", "[JUNCTIONS]"]
+    lines += [f" {node_ids[i]} 50.0 0.1" for i in range(N - 1)]
+    lines += ["", "[RESERVOIRS]", f" {node_ids[N - 1]} 100", "", "[PIPES]"]
+    lines += [f" {pipe_ids[k]} {node_ids[a]} {node_ids[b]} 50.0 150 120 0 Open" for k, (a, b) in enumerate(ends)]
+    lines += ["", "[COORDINATES]"]
+    jit = rng.uniform(-0.3, 0.3, size=(N, 2))
+    lines += [f"{node_ids[i]} {100.0 * (i % W + jit[i, 0]):.3f} {100.0 * (i // W + jit[i, 1]):.3f}" for i in range(N)]
+    lines += ["", "[END]"]
+    Path(path).write_text("\n".join(lines) + "\n", encoding="utf-8")
+    return node_ids, pipe_ids
+
+
+def pick_sensors(node_ids: Sequence[str], count: int = 29, seed: int = 0) -> list:
+    rng = np.random.default_rng(seed + 2)
+    return [node_ids[i] for i in sorted(rng.choice(len(node_ids) - 1, size=count, replace=False))]

@@ -1,0 +1,164 @@
+"""ORACLE fixture generator (test infrastructure only; container-side).
+
+Runs the REFERENCE code from /root/reference (read-only) and freezes its outputs
+as small fixtures under tests/golden/, plus a minimal topology .inp (only the
+sections the graph builder reads) under leak-det-gnn_amd/data/ so the GPU box,
+which has no /root/reference, can construct the L-TOWN-A detector.
+
+  python oracle/make_golden.py [--ref /root/reference]
+
+Reference modules imported as-is: models/utils.py, models/predictor.py.
+models/detector.py imports torch_geometric (absent, unpinned); it is run with
+the independent dense formulation oracle/dense_ref.py supplied as
+torch_geometric.nn, so every non-PyG step of the fixture is the reference's own
+code and the PyG steps are the dense restatement (recorded in meta).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+GOLD = REPO / "tests" / "golden"
+DATA = REPO / "leak-det-gnn_amd" / "data"
+SENSORS = ['n54', 'n105', 'n114', 'n163', 'n188', 'n229', 'n288', 'n296', 'n332', 'n342', 'n410', 'n415', 'n429',
+           'n458', 'n469', 'n495', 'n506', 'n516', 'n519', 'n549', 'n613', 'n636', 'n644', 'n679', 'n722', 'n726',
+           'n740', 'n752', 'n769']  # configs/sim_LTA.yaml:21
+
+
+def _import_reference(ref: Path):
+    sys.path.insert(0, str(REPO))
+    from oracle import dense_ref  # noqa: E402
+    tg = types.ModuleType("torch_geometric")
+    tgnn = types.ModuleType("torch_geometric.nn")
+    tgnn.GCNConv = dense_ref.GCNConv
+    tgnn.global_mean_pool = dense_ref.global_mean_pool
+    tg.nn = tgnn
+    sys.modules["torch_geometric"] = tg
+    sys.modules["torch_geometric.nn"] = tgnn
+    sys.path.insert(0, str(ref))
+    import models.utils as rutils  # noqa: E402
+    import models.predictor as rpred  # noqa: E402
+    import models.detector as rdet  # noqa: E402
+    return rutils, rpred, rdet
+
+
+def write_topology_inp(rutils, src: Path, dst: Path) -> None:
+    sec = rutils.parse_epanet_inp(src)
+    keep = ["JUNCTIONS", "RESERVOIRS", "TANKS", "PIPES", "PUMPS", "VALVES"]
+    lines = [f"[TITLE]", f"topology extracted from {src.name} by oracle/make_golden.py (ids and link endpoints only)",
+             ""]
+    for s in keep:
+        lines.append(f"[{s}]")
+        for ln in sec.get(s, []):
+            tok = ln.split()
+            lines.append(" ".join(tok[:3]) if s in ("PIPES", "PUMPS", "VALVES") else tok[0])
+        lines.append("")
+    lines.append("[END]")
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    dst.write_text("\n".join(lines) + "\n", encoding="utf-8")
+
+
+def graph_fixture(rutils, rdet, inp: Path, sensors, out: Path) -> dict:
+    sec = rutils.parse_epanet_inp(inp)
+    pipe_ids = sorted(rutils._parse_links(sec["PIPES"]).keys())  # all pipes, dataset order (datasets.py:353)
+    node_set = set()
+    for s in ("JUNCTIONS", "RESERVOIRS", "TANKS"):
+        node_set.update(rutils._parse_nodes(sec.get(s, [])))
+    sensors = [s for s in sensors if s in node_set]
+    g = rutils.build_wdn_graph_from_inp(inp, sensors, pipe_ids, add_self_loops=False, make_undirected=True)
+    ei = g.edge_index
+    bat = rdet._batchify_edge_index(ei, len(g.node_names), 3)
+    g2 = rutils.build_wdn_graph_from_inp(inp, sensors, pipe_ids, add_self_loops=True, make_undirected=False)
+    np.savez_compressed(out, node_names=np.array(g.node_names), pipe_ids=np.array(pipe_ids),
+                        sensor_ids=np.array(sensors), edge_index=ei.numpy(), pipe_ends=g.pipe_ends,
+                        sensor_node_idx=np.array([g.node_to_idx[s] for s in sensors], dtype=np.int64),
+                        batchified_b3=bat.numpy(), edge_index_loops_directed=g2.edge_index.numpy())
+    return {"nodes": len(g.node_names), "edges": int(ei.shape[1]), "pipes": len(pipe_ids)}
+
+
+def detector_fixture(rdet, inp: Path, pipe_ids, B: int, out: Path, with_state: bool, with_trace: bool) -> None:
+    torch.manual_seed(0)
+    model = rdet.LeakDetector(inp, SENSORS, pipe_ids, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
+                              use_time=True)
+    model.eval()
+    trace = {}
+    hooks = [model.sensor_to_node.register_forward_hook(lambda m, i, o: trace.__setitem__("node_init", torch.relu(o)))]
+    for k, conv in enumerate(model.convs):
+        hooks.append(conv.register_forward_hook(lambda m, i, o, k=k: trace.__setitem__(f"conv{k}", torch.relu(o))))
+    g = torch.Generator().manual_seed(1000 + B)
+    residual = torch.randn(B, 36, len(SENSORS), generator=g).requires_grad_(True)
+    tfeat = torch.randn(B, 36, 9, generator=g)
+    label = torch.randint(0, len(pipe_ids) + 1, (B,), generator=g)
+    logits = model(residual, tfeat)
+    loss = torch.nn.functional.cross_entropy(logits, label)
+    loss.backward()
+    for h in hooks:
+        h.remove()
+    arrs = dict(residual=residual.detach().numpy(), tfeat=tfeat.numpy(), label=label.numpy(),
+                logits=logits.detach().numpy(), loss=np.array(loss.item(), dtype=np.float32),
+                grad_residual=residual.grad.numpy())
+    for name, p in model.named_parameters():
+        arrs["grad." + name] = p.grad.numpy()
+        if with_state:
+            arrs["param." + name] = p.detach().numpy()
+    if with_trace:
+        for k, v in trace.items():
+            arrs["trace." + k] = v.detach().reshape(B, -1, v.shape[-1]).numpy()
+    np.savez_compressed(out, **arrs)
+
+
+def predictor_fixture(rutils, rpred, out: Path) -> None:
+    torch.manual_seed(0)
+    tcn = rpred.NormalPredictorTCN(num_sensors=29, time_dim=9).eval()
+    torch.manual_seed(0)
+    gru = rpred.NormalPredictorGRU(num_sensors=29, time_dim=9).eval()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 36, 29, generator=g)
+    xt = torch.randn(4, 36, 9, generator=g)
+    seg = torch.randn(2, 72, 29, generator=g)
+    tseg = torch.randn(2, 72, 9, generator=g)
+    with torch.no_grad():
+        y_tcn = tcn(x, xt)
+        y_gru = gru(x, xt)
+        res = rutils.build_residual_sequence_from_segment(tcn, seg, tseg, l_pred=36, l_det=36)
+    arrs = dict(x=x.numpy(), x_time=xt.numpy(), y_tcn=y_tcn.numpy(), y_gru=y_gru.numpy(), seg=seg.numpy(),
+                tseg=tseg.numpy(), residual=res.numpy())
+    for n, p in tcn.state_dict().items():
+        arrs["tcn." + n] = p.numpy()
+    for n, p in gru.state_dict().items():
+        arrs["gru." + n] = p.numpy()
+    np.savez_compressed(out, **arrs)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    args = ap.parse_args()
+    ref = Path(args.ref)
+    rutils, rpred, rdet = _import_reference(ref)
+    GOLD.mkdir(parents=True, exist_ok=True)
+    lta = ref / "data/raw/L-TOWN-A/L-TOWN_AreaA.inp"
+    lt = ref / "data/raw/L-TOWN/L-TOWN.inp"
+    write_topology_inp(rutils, lta, DATA / "L-TOWN-A.inp")
+    meta = {"generator": "oracle/make_golden.py", "reference": str(ref),
+            "pyg": "absent/unpinned; detector fixtures use oracle/dense_ref.py as torch_geometric.nn",
+            "torch": torch.__version__}
+    meta["graph_ltown_a"] = graph_fixture(rutils, rdet, lta, SENSORS, GOLD / "graph_ltown_a.npz")
+    meta["graph_ltown"] = graph_fixture(rutils, rdet, lt, SENSORS, GOLD / "graph_ltown.npz")
+    pipe_ids = [str(p) for p in np.load(GOLD / "graph_ltown_a.npz")["pipe_ids"]]
+    detector_fixture(rdet, lta, pipe_ids, 2, GOLD / "detector_b2.npz", with_state=True, with_trace=True)
+    detector_fixture(rdet, lta, pipe_ids, 8, GOLD / "detector_b8.npz", with_state=False, with_trace=False)
+    predictor_fixture(rutils, rpred, GOLD / "predictor.npz")
+    (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
+    print(json.dumps(meta, indent=2))
+
+
+if __name__ == "__main__":
+    main()

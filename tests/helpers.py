@@ -1,0 +1,40 @@
+"""Shared test helpers: fixture loading and the tolerance rules used everywhere."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from conftest import GOLD, LTA_INP  # noqa: F401
+
+# fp32 tolerance (north star: "within 1e-5 relative fp32"): an output matches when
+#   max|a - b| <= RTOL * max|b| + ATOL
+# i.e. relative to the tensor's own scale, so near-zero entries do not make the
+# element-wise ratio meaningless.  Integer/index outputs are compared bit-exactly.
+RTOL = 1e-5
+ATOL = 1e-7
+
+
+def load(name: str) -> dict:
+    with np.load(GOLD / name, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def rel_err(a, b) -> float:
+    a = torch.as_tensor(np.asarray(a) if not torch.is_tensor(a) else a.detach().cpu()).double()
+    b = torch.as_tensor(np.asarray(b) if not torch.is_tensor(b) else b.detach().cpu()).double()
+    scale = b.abs().max().item()
+    return (a - b).abs().max().item() / max(scale, 1e-30)
+
+
+def assert_close(a, b, rtol: float = RTOL, atol: float = ATOL, what: str = "") -> None:
+    a = a.detach().cpu().double() if torch.is_tensor(a) else torch.as_tensor(np.asarray(a)).double()
+    b = b.detach().cpu().double() if torch.is_tensor(b) else torch.as_tensor(np.asarray(b)).double()
+    assert a.shape == b.shape, f"{what}: shape {tuple(a.shape)} vs {tuple(b.shape)}"
+    err = (a - b).abs().max().item() if a.numel() else 0.0
+    lim = rtol * (b.abs().max().item() if b.numel() else 0.0) + atol
+    assert err <= lim, f"{what}: max abs err {err:.3e} > {lim:.3e} (rtol {rtol}, atol {atol})"
+
+
+def lta_ids():
+    g = load("graph_ltown_a.npz")
+    return [str(s) for s in g["sensor_ids"]], [str(p) for p in g["pipe_ids"]]

@@ -1,0 +1,129 @@
+"""Host side of the product (CPU): graph builder parity with the reference,
+module / state-dict boundary, residual builder and predictors, and the C ABI
+(library loads and exports every symbol include/leakgnn.h declares)."""
+from __future__ import annotations
+
+import ctypes
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG, REPO
+from helpers import LTA_INP, assert_close, load, lta_ids
+
+
+def test_product_graph_builder_bit_exact():
+    from models.utils import build_wdn_graph_from_inp
+    g = load("graph_ltown_a.npz")
+    sensors, pipes = lta_ids()
+    wg = build_wdn_graph_from_inp(LTA_INP, sensors, pipes, add_self_loops=False, make_undirected=True)
+    assert wg.node_names == [str(n) for n in g["node_names"]]
+    assert wg.edge_index.dtype == torch.long
+    np.testing.assert_array_equal(wg.edge_index.numpy(), g["edge_index"])
+    np.testing.assert_array_equal(wg.pipe_ends, g["pipe_ends"])
+    wg2 = build_wdn_graph_from_inp(LTA_INP, sensors, pipes, add_self_loops=True, make_undirected=False)
+    np.testing.assert_array_equal(wg2.edge_index.numpy(), g["edge_index_loops_directed"])
+    with pytest.raises(ValueError):
+        build_wdn_graph_from_inp(LTA_INP, sensors, ["no_such_pipe"])
+
+
+def test_parse_epanet_edge_cases(tmp_path):
+    from models.utils import parse_epanet_inp
+    from oracle.graph_ref import parse_inp
+    p = tmp_path / "t.inp"
+    p.write_text("junk before\n[junctions]\n a 1 ; c\n;only comment\n\n [PIPES] \np1 a b 3\n[PIPES] ;x\n[]\n")
+    assert parse_epanet_inp(p) == parse_inp(p)
+    assert parse_epanet_inp(p)["JUNCTIONS"] == ["a 1"]
+
+
+def test_detector_boundary_state_dict():
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    m = LeakDetector(LTA_INP, sensors, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1)
+    fx = load("detector_b2.npz")
+    ref = {k[len("param."):]: v for k, v in fx.items() if k.startswith("param.")}
+    sd = m.state_dict()
+    assert sorted(sd) == sorted(ref)
+    for k, v in ref.items():
+        assert tuple(sd[k].shape) == v.shape, k
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in ref.items()}, strict=True)
+    # public attributes used by the callers
+    g = load("graph_ltown_a.npz")
+    assert m.sensor_node_ids == sensors
+    np.testing.assert_array_equal(m.sensor_node_idx.numpy(), g["sensor_node_idx"])
+    np.testing.assert_array_equal(m.pipe_ends.numpy(), g["pipe_ends"])
+    np.testing.assert_array_equal(m.edge_index_single.numpy(), g["edge_index"])
+    assert m.pipe_ids == pipes and m.pipe_to_idx[pipes[5]] == 5
+    assert len(m.node_names) == 661 and m.node_to_idx[m.node_names[7]] == 7
+    with pytest.raises(RuntimeError):  # no CPU path
+        m(torch.zeros(1, 36, 29), torch.zeros(1, 36, 9))
+
+
+def test_predictors_and_residual_builder_match_reference():
+    from models.predictor import NormalPredictorGRU, NormalPredictorTCN
+    from models.utils import build_residual_sequence_from_segment
+    fx = load("predictor.npz")
+    tcn = NormalPredictorTCN(29, 9).eval()
+    tcn.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("tcn.")}, strict=True)
+    gru = NormalPredictorGRU(29, 9).eval()
+    gru.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("gru.")}, strict=True)
+    x, xt = torch.from_numpy(fx["x"]), torch.from_numpy(fx["x_time"])
+    with torch.no_grad():
+        assert_close(tcn(x, xt), fx["y_tcn"], what="tcn")
+        assert_close(gru(x, xt), fx["y_gru"], what="gru")
+        res = build_residual_sequence_from_segment(tcn, torch.from_numpy(fx["seg"]), torch.from_numpy(fx["tseg"]),
+                                                   36, 36)
+        assert_close(res, fx["residual"], what="residual")
+        one = build_residual_sequence_from_segment(tcn, torch.from_numpy(fx["seg"][0]),
+                                                   torch.from_numpy(fx["tseg"][0]), 36, 36)
+        assert_close(one, fx["residual"][0], what="residual 2-D input")
+
+
+def _header_symbols():
+    text = (REPO / "include" / "leakgnn.h").read_text()
+    return sorted(set(re.findall(r"\b(lg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_c_abi_exports_every_declared_symbol():
+    from models import _native
+    lib = _native.load_library()
+    syms = _header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in leakgnn.h but not exported"
+        assert s in _native.SIGNATURES, f"{s} has no ctypes signature"
+    assert set(_native.SIGNATURES) == set(syms)
+    raw = ctypes.CDLL(str(_native.LIB_PATH))
+    for s in syms:
+        getattr(raw, s)
+
+
+def test_c_abi_host_only_calls():
+    """Entry points that do not touch the GPU: version, error strings, workspace
+    sizes and argument validation (returns LG_EINVAL before any HIP call)."""
+    from models import _native
+    lib = _native.load_library()
+    assert lib.lg_abi_version() == 1
+    assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
+    assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * 1532)
+    assert lib.lg_graph_workspace_bytes(-1, 5) == -1
+    assert lib.lg_incidence_workspace_bytes(764, 661) >= 8 * 661
+    assert lib.lg_gcn_bwd_workspace_bytes(48) == -2
+    assert lib.lg_gcn_fwd(None, None, None, None, None, None, None, 1, 661, 64, 0, 0.0, 0, 0, None) == -1
+    assert lib.lg_gcn_bwd(None, None, None, None, None, None, None, None, None, None, 1, 661, 64, 0, 1.0, 1.0,
+                          None, None) == -1
+    assert lib.lg_graph_build(None, 5, 0, 1, 1, 1.0, None, None, None, None, None, None, None, None) == -1
+    assert lib.lg_pipe_gather_fwd(None, None, None, 1, 10, 5, 64, None) == -1
+    assert lib.lg_mean_pool_fwd(None, None, 2, 10, 64, None) == -1
+
+
+def test_library_built_for_gfx950_only():
+    import subprocess
+    lib = PKG / "lib" / "libleakgnn.so"
+    out = subprocess.run(["/opt/rocm/bin/roc-obj-ls", str(lib)], capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("roc-obj-ls unavailable")
+    targets = set(re.findall(r"gfx\d+", out.stdout))
+    assert targets == {"gfx950"}, targets
