@@ -86,7 +86,11 @@ __global__ void k_finalize(const int64_t* __restrict__ ei, int64_t E, int64_t N,
         insertion_sort(item_t + rowptr_t[n], cnt_t[n]);
         // deg = scatter_add(edge_weight, dst): unit weights plus the loop's fill value.
         const float deg = static_cast<float>(cnt[n]) + (add_loops ? fill : 0.0f);
-        dis[n] = deg > 0.0f ? __fdiv_rn(1.0f, __fsqrt_rn(deg)) : 0.0f;  // deg.pow(-0.5), inf -> 0
+        // deg.pow(-0.5) as torch evaluates it in fp32: sqrt rounded to fp32, then 1/x rounded
+        // to fp32.  Each step is done in fp64 and rounded once, which is exact for fp32
+        // sqrt and division (53 >= 2*24 + 2), so dis is bit-identical to the CPU reference.
+        const float sq = static_cast<float>(sqrt(static_cast<double>(deg)));
+        dis[n] = deg > 0.0f ? static_cast<float>(1.0 / static_cast<double>(sq)) : 0.0f;  // inf -> 0
         return;
     }
     // phase 1: all dis[] are final.
@@ -156,8 +160,9 @@ inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
 extern "C" int64_t lg_graph_workspace_bytes(int64_t E, int64_t N) {
     if (E < 0 || N < 0) return LG_EINVAL;
-    // cnt, cnt_t, cur, cur_t, dis : N each; item, item_t : E each
-    return align256(4 * (5 * N + 2 * E) + 64);
+    // cnt, cnt_t, cur, cur_t, dis : N each; item, item_t : E + N each (indexed by CSR
+    // position, which includes the self-loop slot of every row)
+    return align256(4 * (5 * N + 2 * (E + N)) + 64);
 }
 
 extern "C" int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int add_self_loops, int normalize,
@@ -173,7 +178,7 @@ extern "C" int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N, i
     int32_t* cur_t = cur + N;
     float* dis = reinterpret_cast<float*>(cur_t + N);
     int32_t* item = reinterpret_cast<int32_t*>(dis + N);
-    int32_t* item_t = item + E;
+    int32_t* item_t = item + (E + N);
     if (hipMemsetAsync(cnt, 0, sizeof(int32_t) * 4 * N, s) != hipSuccess) return LG_EHIP;
     const int drop = add_self_loops ? 1 : 0;
     if (E > 0) {

@@ -51,7 +51,17 @@ class SharedSensorGRUEncoder(nn.Module):
                 raise ValueError("tfeat required when use_time=True")
             tf = tfeat.unsqueeze(1).expand(B, S, L, tfeat.shape[-1]).reshape(B * S, L, -1)
             seq = torch.cat([seq, tf], dim=-1)
-        out, _ = self.gru(seq)
+        gru = self.gru
+        if not gru.training and torch.is_grad_enabled() and gru.num_layers == 1:
+            # MIOpen has no eval-mode RNN backward; for one layer (no inter-layer
+            # dropout) train and eval compute the same function, so run it in train mode.
+            gru.training = True
+            try:
+                out, _ = gru(seq)
+            finally:
+                gru.training = False
+        else:
+            out, _ = gru(seq)
         return out[:, -1, :].view(B, S, -1)
 
 

@@ -245,6 +245,7 @@ class TrunkConfig:
     nonsensor_idx: torch.Tensor    # int64 (N - #sensors,)
     dropout_p: float
     training: bool
+    capture: Optional[list] = None     # tests: receives the saved activations x_0 .. x_L
 
 
 class GNNTrunkFn(torch.autograd.Function):
@@ -285,6 +286,8 @@ class GNNTrunkFn(torch.autograd.Function):
                 check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
                                      D, nat.LG_F_BIAS | nat.LG_F_RELU | dflag, p, seed, l + 1, st), "lg_gcn_fwd")
             xs.append(y)
+        if cfg.capture is not None:
+            cfg.capture.extend(t.detach().clone() for t in xs)
         ctx.cfg = cfg
         ctx.scale = 1.0 / (1.0 - p) if drop else 1.0
         ctx.dims = (B, S, N, D, L)

@@ -38,3 +38,21 @@ def assert_close(a, b, rtol: float = RTOL, atol: float = ATOL, what: str = "") -
 def lta_ids():
     g = load("graph_ltown_a.npz")
     return [str(s) for s in g["sensor_ids"]], [str(p) for p in g["pipe_ids"]]
+
+
+def assert_grads_close(named_grads, ref_grads: dict, rtol: float = RTOL, prefix: str = "grad ") -> None:
+    """Parameter gradients: ||g - g_ref||_inf <= rtol * ||g_ref||_inf over the WHOLE
+    parameter-gradient vector (every tensor judged against the model's gradient scale).
+    Per-tensor relative bounds are meaningless for sums with heavy cancellation, e.g.
+    the last EdgeHead bias grad = sum over all (window, pipe) softmax terms, which is
+    ~1e-2 while its terms are ~1; the reduction order of torch on GPU vs CPU alone
+    moves it by ~1e-7 absolute."""
+    refs = {n: (torch.as_tensor(np.asarray(v)) if not torch.is_tensor(v) else v.detach().cpu()).double()
+            for n, v in ref_grads.items()}
+    scale = max(r.abs().max().item() for r in refs.values())
+    for n, g in named_grads:
+        r = refs[n]
+        g = g.detach().cpu().double()
+        assert g.shape == r.shape, n
+        err = (g - r).abs().max().item()
+        assert err <= rtol * scale + ATOL, f"{prefix}{n}: max abs err {err:.3e} > {rtol * scale + ATOL:.3e}"

@@ -1,0 +1,104 @@
+"""Multi-process (world_size 2, gloo, CPU) check of the data-parallel step:
+each rank takes its contiguous shard of the global batch, computes the mean loss
+on it, GradAllReduce averages the gradients; the result must equal the
+single-process gradient of the whole global batch, and after clip + AdamW the
+parameters must agree on both ranks and with the single-process run.
+
+The model is the oracle's CPU LeakDetector restatement (the product model has no
+CPU path); GradAllReduce / shard_range are the product's own code
+(leak-det-gnn_amd/models/ddp.py), device-agnostic."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model_and_batch():
+    sys.path[:0] = [str(REPO), str(PKG)]
+    from helpers import LTA_INP, lta_ids
+    from oracle.detector_ref import LeakDetectorRef
+    sensors, pipes = lta_ids()
+    torch.manual_seed(0)
+    m = LeakDetectorRef(LTA_INP, sensors, pipes).eval()  # eval: dropout off -> exact comparison
+    g = torch.Generator().manual_seed(3)
+    B = 8
+    r = torch.randn(B, 36, 29, generator=g)
+    tf = torch.randn(B, 36, 9, generator=g)
+    lab = torch.randint(0, len(pipes) + 1, (B,), generator=g)
+    return m, r, tf, lab
+
+
+def _step(m, r, tf, lab, allreduce=None):
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    opt.zero_grad(set_to_none=True)
+    torch.nn.functional.cross_entropy(m(r, tf), lab).backward()
+    if allreduce is not None:
+        allreduce()
+    grads = [p.grad.clone() for p in m.parameters()]
+    torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+    opt.step()
+    return grads, [p.detach().clone() for p in m.parameters()]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [str(REPO), str(PKG), str(REPO / "tests")]
+    from models.ddp import GradAllReduce, init_distributed, shard_range
+    torch.set_num_threads(2)
+    init_distributed("gloo")
+    m, r, tf, lab = _model_and_batch()
+    sl = shard_range(r.shape[0], rank, world)
+    idx = torch.tensor(list(sl))
+    grads, params = _step(m, r[idx], tf[idx], lab[idx], GradAllReduce(m.parameters()))
+    q.put((rank, [g.numpy() for g in grads], [p.numpy() for p in params]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gradient_allreduce_matches_single_process():
+    sys.path.insert(0, str(REPO / "tests"))
+    torch.set_num_threads(4)
+    m, r, tf, lab = _model_and_batch()
+    g1, p1 = _step(m, r, tf, lab)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(k, 2, port, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        k, g, prm = q.get(timeout=300)
+        res[k] = (g, prm)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in (0, 1):
+        for a, b in zip(res[k][0], g1):
+            torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-5, atol=1e-7)
+        for a, b in zip(res[k][1], p1):
+            torch.testing.assert_close(torch.from_numpy(a), b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a == b).all(), "ranks diverged after the step"
+
+
+def test_shard_range():
+    from models.ddp import shard_range
+    assert list(shard_range(512, 3, 8)) == list(range(192, 256))
+    with pytest.raises(ValueError):
+        shard_range(10, 0, 3)

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import LTA_INP, RTOL, assert_close, load, lta_ids
+from helpers import LTA_INP, RTOL, assert_close, assert_grads_close, load, lta_ids
 from oracle import gcn_ref, graph_ref
 
 pytestmark = pytest.mark.gpu
@@ -145,8 +145,8 @@ def test_detector_vs_reference_fixture(fixture):
     assert_close(logits, fx["logits"], what="logits")
     assert abs(loss.item() - float(fx["loss"])) <= RTOL * abs(float(fx["loss"]))
     assert_close(residual.grad, fx["grad_residual"], what="grad residual")
-    for name, p in m.named_parameters():
-        assert_close(p.grad, fx["grad." + name], what="grad " + name)
+    assert_grads_close([(n, p.grad) for n, p in m.named_parameters()],
+                       {n: fx["grad." + n] for n, _ in m.named_parameters()})
 
 
 def test_detector_vs_oracle_b64_random_weights():
@@ -170,9 +170,9 @@ def test_detector_vs_oracle_b64_random_weights():
     lg = m(r.to(DEV), tf.to(DEV))
     torch.nn.functional.cross_entropy(lg, lab.to(DEV)).backward()
     assert_close(lg, lc, what="logits B=64")
-    for (n, p), (n2, q) in zip(m.named_parameters(), ref.named_parameters()):
-        assert n == n2
-        assert_close(p.grad, q.grad, what="grad " + n)
+    assert [n for n, _ in m.named_parameters()] == [n for n, _ in ref.named_parameters()]
+    assert_grads_close([(n, p.grad) for n, p in m.named_parameters()],
+                       {n: q.grad for n, q in ref.named_parameters()})
 
 
 def test_detector_train_mode_dropout():
@@ -220,20 +220,19 @@ def test_detector_train_mode_grad_matches_autograd_of_masks():
     # replay: same seed -> same masks; re-derive them with the GPU forward and apply via torch ops
     m.zero_grad()
     torch.manual_seed(9)
-    cache = {}
-    orig = ops.GNNTrunkFn.forward
+    xs = []
+    orig_apply = ops.GNNTrunkFn.apply
 
-    def spy(ctx, cfg, proj, nb, *wb):
-        y = orig(ctx, cfg, proj, nb, *wb)
-        cache["xs"] = [t.detach().clone() for t in ctx.saved_tensors[: len(wb) // 2 + 1]]
-        return y
+    def capturing_apply(cfg, *args):
+        cfg.capture = xs
+        return orig_apply(cfg, *args)
 
-    ops.GNNTrunkFn.forward = staticmethod(spy)
+    ops.GNNTrunkFn.apply = capturing_apply
     try:
         m(r, tf)
     finally:
-        ops.GNNTrunkFn.forward = staticmethod(orig)
-    xs = cache["xs"]
+        del ops.GNNTrunkFn.apply  # back to torch.autograd.Function.apply
+    assert len(xs) == 3
     # torch-only trunk with explicit masks (mask_l = x_l > 0, scale 1/(1-p))
     from oracle import gcn_ref
     sc = 1 / 0.9
@@ -260,8 +259,7 @@ def test_detector_train_mode_grad_matches_autograd_of_masks():
     out2 = torch.cat([pl, nl], -1)
     assert_close(out2, out, rtol=1e-5, what="train-mode replay forward")
     out2.square().sum().backward()
-    for n, p in m.named_parameters():
-        assert_close(grads[n], p.grad, rtol=2e-5, what="train grad " + n)
+    assert_grads_close(list(grads.items()), {n: p.grad for n, p in m.named_parameters()}, prefix="train grad ")
 
 
 def test_pipe_heads_and_pool_vs_torch():
