@@ -41,6 +41,10 @@ SIGNATURES = {
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
+    "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
+    "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                          _p, _p]),
 }
 
 _lib = None

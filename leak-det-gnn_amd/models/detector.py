@@ -44,25 +44,17 @@ class SharedSensorGRUEncoder(nn.Module):
                           num_layers=num_layers, batch_first=True, dropout=dropout if num_layers > 1 else 0.0)
 
     def forward(self, r: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
-        B, L, S = r.shape
-        seq = r.transpose(1, 2).reshape(B * S, L, 1)  # sequence index = b*S + s
-        if self.use_time:
-            if tfeat is None:
-                raise ValueError("tfeat required when use_time=True")
-            tf = tfeat.unsqueeze(1).expand(B, S, L, tfeat.shape[-1]).reshape(B * S, L, -1)
-            seq = torch.cat([seq, tf], dim=-1)
-        gru = self.gru
-        if not gru.training and torch.is_grad_enabled() and gru.num_layers == 1:
-            # MIOpen has no eval-mode RNN backward; for one layer (no inter-layer
-            # dropout) train and eval compute the same function, so run it in train mode.
-            gru.training = True
-            try:
-                out, _ = gru(seq)
-            finally:
-                gru.training = False
-        else:
-            out, _ = gru(seq)
-        return out[:, -1, :].view(B, S, -1)
+        """(B, L, S) residuals (+ (B, L, 9) time features) -> (B, S, hidden): h_L of the shared GRU
+        over the B*S sensor sequences, on the fused HIP GRU (lg_gru_fwd / lg_gru_bwd)."""
+        if self.use_time and tfeat is None:
+            raise ValueError("tfeat required when use_time=True")
+        if not r.is_cuda:
+            raise RuntimeError("SharedSensorGRUEncoder runs on a ROCm GPU only (libleakgnn has no CPU path)")
+        g = self.gru
+        if g.num_layers != 1 or g.hidden_size != 64 or g.bidirectional or not g.bias:
+            raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 64, bias")
+        return ops.GRUEncoderFn.apply(r, tfeat if self.use_time else None, g.weight_ih_l0, g.weight_hh_l0,
+                                      g.bias_ih_l0, g.bias_hh_l0)
 
 
 class EdgeHead(nn.Module):

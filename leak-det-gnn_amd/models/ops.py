@@ -385,6 +385,54 @@ class MeanPoolWindowsFn(torch.autograd.Function):
         return (dout / float(N)).unsqueeze(1).expand(B, N, dout.shape[-1]).reshape(B * N, -1), None, None
 
 
+class GRUEncoderFn(torch.autograd.Function):
+    """SharedSensorGRUEncoder core (detector.py:60-73): h_L of nn.GRU over the B*S sensor
+    sequences, x_t = [residual[b, t, s], tfeat[b, t, :]] read in place (lg_gru_fwd / lg_gru_bwd)."""
+
+    @staticmethod
+    def forward(ctx, residual, tfeat, w_ih, w_hh, b_ih, b_hh):
+        lib = load_library()
+        residual = residual.contiguous().float()
+        tfeat = tfeat.contiguous().float() if tfeat is not None else None
+        require_device(residual, tfeat, w_ih, w_hh, b_ih, b_hh)
+        B, L, S = residual.shape
+        G, I = w_ih.shape
+        H = w_hh.shape[1]
+        if tfeat is not None and tuple(tfeat.shape) != (B, L, 9):
+            raise ValueError(f"tfeat must be (B, L, 9), got {tuple(tfeat.shape)}")
+        need_bwd = any(ctx.needs_input_grad)
+        h_seq = torch.empty(L, B * S, H, device=residual.device) if need_bwd else None
+        h_last = torch.empty(B * S, H, device=residual.device)
+        with _timed("gru_fwd", residual.device):
+            check(lib.lg_gru_fwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(h_seq),
+                                 ptr(h_last), B, L, S, I, H, stream_of(residual)), "lg_gru_fwd")
+        ctx.dims = (B, L, S, I, H)
+        ctx.save_for_backward(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq)
+        return h_last.view(B, S, H)
+
+    @staticmethod
+    def backward(ctx, dh):
+        lib = load_library()
+        residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq = ctx.saved_tensors
+        B, L, S, I, H = ctx.dims
+        dev = residual.device
+        need_dx = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        dx = torch.empty(B * S, L, I, device=dev) if need_dx else None
+        dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+        db_ih, db_hh = torch.empty_like(b_ih), torch.empty_like(b_hh)
+        ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I)), device=dev, dtype=torch.uint8)
+        with _timed("gru_bwd", dev):
+            check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(h_seq),
+                                 ptr(dh.contiguous()), ptr(dx), ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L,
+                                 S, I, H, ptr(ws), stream_of(residual)), "lg_gru_bwd")
+        dres = dtf = None
+        if ctx.needs_input_grad[0]:
+            dres = dx[..., 0].reshape(B, S, L).transpose(1, 2)
+        if tfeat is not None and ctx.needs_input_grad[1]:
+            dtf = dx[..., 1:].reshape(B, S, L, I - 1).sum(dim=1)
+        return dres, dtf, dw_ih, dw_hh, db_ih, db_hh
+
+
 def spmm(graph: GCNGraph, x: torch.Tensor, B: int = 1) -> torch.Tensor:
     """y = Ahat x (PyG propagate with gcn_norm weights) for B stacked windows; no autograd."""
     lib = load_library()

@@ -61,3 +61,37 @@ def assert_grads_close(named_grads, ref_grads: dict, rtol: float = RTOL, rtol_in
         assert gs[n].shape == r.shape, n
         err = (gs[n] - r).abs().max().item()
         assert err <= rtol_inf * scale + ATOL, f"{prefix}{n}: max abs err {err:.3e} > {rtol_inf * scale:.3e}"
+
+
+def oracle_grads(state: dict, residual, tfeat, label, dtype) -> tuple:
+    """CPU oracle (oracle/detector_ref.py) logits and parameter grads in `dtype` on the given inputs."""
+    from oracle.detector_ref import LeakDetectorRef
+    sensors, pipes = lta_ids()
+    m = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
+    m.load_state_dict(state)
+    m = m.to(dtype)
+    out = m(torch.as_tensor(residual).to(dtype), torch.as_tensor(tfeat).to(dtype))
+    torch.nn.functional.cross_entropy(out, torch.as_tensor(label)).backward()
+    return out.detach(), {n: p.grad.detach() for n, p in m.named_parameters()}
+
+
+def assert_grads_match_truth(gpu: dict, cpu32: dict, cpu64: dict, slack: float = 4.0, rtol: float = RTOL) -> None:
+    """Backward bar (the north star bounds the fp32 FORWARD at 1e-5; for gradients the
+    reference's own fp32 CPU path is itself ~1e-5 off in norm because some parameter
+    grads are sums with heavy cancellation).  Against an fp64 run of the oracle, every
+    tensor's GPU error must be within `slack` x the CPU fp32 error or within rtol of the
+    tensor's scale, and likewise for the whole-vector 2-norm."""
+    g64 = {n: v.double().cpu() for n, v in cpu64.items()}
+    e_gpu2 = e_cpu2 = n2 = 0.0
+    for n, t in g64.items():
+        g = gpu[n].detach().double().cpu()
+        c = cpu32[n].detach().double().cpu()
+        eg = (g - t).abs().max().item()
+        ec = (c - t).abs().max().item()
+        lim = max(slack * ec, rtol * t.abs().max().item()) + 1e-12
+        assert eg <= lim, f"grad {n}: gpu err {eg:.3e} > {lim:.3e} (cpu fp32 err {ec:.3e})"
+        e_gpu2 += ((g - t) ** 2).sum().item()
+        e_cpu2 += ((c - t) ** 2).sum().item()
+        n2 += (t ** 2).sum().item()
+    e_gpu2, e_cpu2, n2 = e_gpu2 ** 0.5, e_cpu2 ** 0.5, n2 ** 0.5
+    assert e_gpu2 <= max(slack * e_cpu2, rtol * n2), f"grad vector: gpu {e_gpu2:.3e}, cpu32 {e_cpu2:.3e}, |g| {n2:.3e}"

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import LTA_INP, RTOL, assert_close, assert_grads_close, load, lta_ids
+from helpers import (LTA_INP, RTOL, assert_close, assert_grads_close, assert_grads_match_truth, load, lta_ids,
+                     oracle_grads)
 from oracle import gcn_ref, graph_ref
 
 pytestmark = pytest.mark.gpu
@@ -135,6 +136,7 @@ def _product_model(state: dict, B_dropout=0.1):
 
 @pytest.mark.parametrize("fixture", ["detector_b2.npz", "detector_b8.npz"])
 def test_detector_vs_reference_fixture(fixture):
+    """Eval-mode forward within 1e-5 of the reference fixture; grads vs fp64 truth (helpers)."""
     state = load("detector_b2.npz")
     fx = load(fixture)
     m = _product_model(state).eval()
@@ -145,34 +147,38 @@ def test_detector_vs_reference_fixture(fixture):
     assert_close(logits, fx["logits"], what="logits")
     assert abs(loss.item() - float(fx["loss"])) <= RTOL * abs(float(fx["loss"]))
     assert_close(residual.grad, fx["grad_residual"], what="grad residual")
-    assert_grads_close([(n, p.grad) for n, p in m.named_parameters()],
-                       {n: fx["grad." + n] for n, _ in m.named_parameters()})
+    sd = {k[len("param."):]: torch.from_numpy(v) for k, v in state.items() if k.startswith("param.")}
+    args = (fx["residual"], fx["tfeat"], fx["label"])
+    _, g32 = oracle_grads(sd, *(torch.from_numpy(a) for a in args), torch.float32)
+    _, g64 = oracle_grads(sd, *(torch.from_numpy(a) for a in args), torch.float64)
+    for n in g32:  # the fixture (reference code, fp32) and the oracle fp32 agree
+        assert_close(g32[n], fx["grad." + n], what="oracle vs fixture grad " + n)
+    assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64)
 
 
 def test_detector_vs_oracle_b64_random_weights():
-    from oracle.detector_ref import LeakDetectorRef
     sensors, pipes = lta_ids()
+    from oracle.detector_ref import LeakDetectorRef
     torch.manual_seed(11)
     ref = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
     with torch.no_grad():
         for c in ref.convs:
             c.bias.normal_(0, 0.1)
+    sd = {k: v.clone() for k, v in ref.state_dict().items()}
     from models.detector import LeakDetector
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
-    m.load_state_dict(ref.state_dict())
+    m.load_state_dict(sd)
     B = 64
     gen = torch.Generator().manual_seed(12)
     r = torch.randn(B, 36, 29, generator=gen)
     tf = torch.randn(B, 36, 9, generator=gen)
     lab = torch.randint(0, 765, (B,), generator=gen)
-    lc = ref(r, tf)
-    torch.nn.functional.cross_entropy(lc, lab).backward()
+    l32, g32 = oracle_grads(sd, r, tf, lab, torch.float32)
+    _, g64 = oracle_grads(sd, r, tf, lab, torch.float64)
     lg = m(r.to(DEV), tf.to(DEV))
     torch.nn.functional.cross_entropy(lg, lab.to(DEV)).backward()
-    assert_close(lg, lc, what="logits B=64")
-    assert [n for n, _ in m.named_parameters()] == [n for n, _ in ref.named_parameters()]
-    assert_grads_close([(n, p.grad) for n, p in m.named_parameters()],
-                       {n: q.grad for n, q in ref.named_parameters()})
+    assert_close(lg, l32, what="logits B=64")
+    assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64)
 
 
 def test_detector_train_mode_dropout():
@@ -306,3 +312,35 @@ def test_full_size_properties_c5():
     k1 = torch.sort(rows * 100_000 + c).values
     k2 = torch.sort(rows * 100_000 + ct).values
     assert torch.equal(k1, k2)
+
+
+@pytest.mark.parametrize("use_time", [True, False])
+@pytest.mark.parametrize("B", [5, 64])
+def test_gru_encoder_vs_torch_cpu(use_time, B):
+    """Fused HIP GRU vs nn.GRU on the CPU (the reference's own op), fwd h_L and all grads."""
+    from models.detector import SharedSensorGRUEncoder
+    from oracle.detector_ref import _GRUEncoder
+    torch.manual_seed(B)
+    ref = _GRUEncoder(64, use_time=use_time)
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.uniform_(-0.3, 0.3)
+    enc = SharedSensorGRUEncoder(hidden_size=64, use_time=use_time)
+    enc.gru.load_state_dict(ref.gru.state_dict())
+    enc = enc.to(DEV)
+    gen = torch.Generator().manual_seed(3)
+    r = torch.randn(B, 36, 29, generator=gen)
+    tf = torch.randn(B, 36, 9, generator=gen)
+    gy = torch.randn(B, 29, 64, generator=gen)
+    rc, tc = r.clone().requires_grad_(True), tf.clone().requires_grad_(use_time)
+    yc = ref(rc, tc if use_time else None)
+    (yc * gy).sum().backward()
+    rg, tg = r.to(DEV).requires_grad_(True), tf.to(DEV).requires_grad_(use_time)
+    yg = enc(rg, tg if use_time else None)
+    (yg * gy.to(DEV)).sum().backward()
+    assert_close(yg, yc, what="GRU h_L")
+    assert_close(rg.grad, rc.grad, what="GRU d residual")
+    if use_time:
+        assert_close(tg.grad, tc.grad, what="GRU d tfeat")
+    assert_grads_close([(n, p.grad) for n, p in enc.gru.named_parameters()],
+                       {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")

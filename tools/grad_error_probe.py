@@ -1,0 +1,41 @@
+"""Diagnostic: per-tensor gradient error of the GPU path and of the CPU fp32 oracle,
+both against the CPU oracle run in float64 (the closest thing to ground truth)."""
+import sys
+from pathlib import Path
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / "leak-det-gnn_amd"), str(REPO / "tests")]
+import torch
+from helpers import LTA_INP, load, lta_ids
+from oracle.detector_ref import LeakDetectorRef
+from models.detector import LeakDetector
+
+sensors, pipes = lta_ids()
+fx = load("detector_b8.npz")
+st = load("detector_b2.npz")
+sd = {k[6:]: torch.from_numpy(v) for k, v in st.items() if k.startswith("param.")}
+r, tf, lab = (torch.from_numpy(fx[k]) for k in ("residual", "tfeat", "label"))
+
+def cpu(dtype):
+    m = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
+    m.load_state_dict(sd)
+    m = m.to(dtype)
+    out = m(r.to(dtype), tf.to(dtype))
+    torch.nn.functional.cross_entropy(out, lab).backward()
+    return out.detach().double(), {n: p.grad.double() for n, p in m.named_parameters()}
+
+l64, g64 = cpu(torch.float64)
+l32, g32 = cpu(torch.float32)
+m = LeakDetector(LTA_INP, sensors, pipes).cuda().eval()
+m.load_state_dict(sd)
+out = m(r.cuda(), tf.cuda())
+torch.nn.functional.cross_entropy(out, lab.cuda()).backward()
+gg = {n: p.grad.double().cpu() for n, p in m.named_parameters()}
+print("logits max err  gpu %.3e  cpu32 %.3e  (scale %.3e)" % ((out.double().cpu() - l64).abs().max(),
+      (l32 - l64).abs().max(), l64.abs().max()))
+tot_g = sum(((gg[n] - g64[n]) ** 2).sum() for n in g64) ** 0.5
+tot_c = sum(((g32[n] - g64[n]) ** 2).sum() for n in g64) ** 0.5
+norm = sum((g64[n] ** 2).sum() for n in g64) ** 0.5
+print("grad 2-norm rel err  gpu %.3e  cpu32 %.3e" % (tot_g / norm, tot_c / norm))
+for n in g64:
+    print("%-40s gpu %.3e  cpu32 %.3e  scale %.3e" % (n, (gg[n] - g64[n]).abs().max(), (g32[n] - g64[n]).abs().max(),
+                                                     g64[n].abs().max()))
