@@ -133,7 +133,8 @@ def main() -> None:
 
     for _ in range(args.warmup):
         step()
-    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "pipe_gather", "pipe_scatter", "mean_pool"])
+    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "gru_fwd", "gru_bwd", "edge_fwd", "edge_bwd",
+                             "pipe_scatter", "mean_pool"])
     ops.set_kernel_timer(timer)
 
     def barrier():

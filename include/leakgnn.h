@@ -155,14 +155,35 @@ int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* feat,
 
 /* K8 backward + K10 backward, fused: deterministic segmented reduce over the
  * incidence CSR (no atomics):
- *   dh[b][n] = dpool[b]/N + sum over incidences (p, role) of n, in item order, of
- *              role==u ? dfeat_u + dfeat_abs*sgn : dfeat_v - dfeat_abs*sgn,
- *   sgn = sign(h[b][u] - h[b][v]).  dpool may be NULL.
- * Replaces: autograd of h_nodes[:, u], h_nodes[:, v], cat, abs (detector.py:87,
- * 209-210) and of global_mean_pool (detector.py:215). */
-int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const int64_t* ends,
-                        const float* h, const float* dfeat, const float* dpool, float* dh,
+ *   dh[b][n] = dpool[b]/N + sum over incidences (p, role) of n, in item order, of dpipe[b][p][role]
+ * where dpipe[b][p][0] / [1] are the gradients w.r.t. h_u / h_v of pipe p (from
+ * lg_edge_head_bwd).  dpool may be NULL.
+ * Replaces: autograd of h_nodes[:, u], h_nodes[:, v] (detector.py:209-210) and of
+ * global_mean_pool (detector.py:215).   dpipe : fp32 [B][P][2][D];  dh : fp32 [B][N][D] */
+int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const float* dpipe,
+                        const float* dpool, float* dh,
                         int64_t B, int64_t N, int64_t P, int64_t D, lg_stream_t stream);
+
+/* K8 + K9 fused EdgeHead forward (detector.py:76-88 applied at :206-211):
+ *   logits[b][p] = W2 . dropout(relu(W1 [h_u, h_v, |h_u - h_v|] + b1)) + b2
+ * feat (B,P,3D) and the hidden layer are never materialised.  W1 : fp32 [hidden][3D]
+ * (edge_head.mlp.0.weight), b1 [hidden], W2 [hidden] (mlp.3.weight), b2 [1];
+ * logits : fp32 [B][P].  hidden must be 128; D in {32, 64}.  Dropout as lg_gcn_fwd,
+ * index (b*P + p)*hidden + unit. */
+int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
+                     const float* w2, const float* b2, float* logits,
+                     int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
+                     int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+/* Backward of lg_edge_head_fwd (same flags/seed/salt): dlogits fp32 [B][P] ->
+ * dpipe fp32 [B][P][2][D] (grads w.r.t. h_u, h_v per pipe), dw1/db1/dw2/db2
+ * (overwritten; deterministic fixed-order reduction of per-workgroup slabs). */
+int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden);
+int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
+                     const float* w2, const float* dlogits, float* dpipe,
+                     float* dw1, float* db1, float* dw2, float* db2,
+                     int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
+                     int flags, float dropout_p, uint64_t seed, uint32_t salt,
+                     void* workspace, lg_stream_t stream);
 
 /* K10 forward: per-window mean over the N node rows.
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)

@@ -13,6 +13,7 @@
 // Waves never wait for each other inside the tile loop (no workgroup barrier),
 // so the gather of one wave overlaps the MFMA phase of its neighbours.
 #include "common.h"
+#include "reduce.h"
 
 namespace {
 
@@ -298,19 +299,6 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
     for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
 }
 
-__global__ void k_slab_reduce(const float* __restrict__ slab, int G, int D, float* __restrict__ dW,
-                              float* __restrict__ db) {
-    const int L = D * D + D;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= L) return;
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += slab[static_cast<int64_t>(g) * L + i];
-    if (i < D * D)
-        dW[i] = s;
-    else if (db)
-        db[i - D * D] = s;
-}
-
 // ------------------------------------------------------------------ plain propagate
 template <int D>
 __global__ void __launch_bounds__(256)
@@ -422,8 +410,8 @@ extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const f
     }
 #undef LG_BWD_LAUNCH
     LG_RET_IF_LAUNCH_FAILED();
-    const int L = static_cast<int>(D * D + D);
-    k_slab_reduce<<<(L + 255) / 256, 256, 0, s>>>(slab, grid, static_cast<int>(D), dW, db);
-    LG_RET_IF_LAUNCH_FAILED();
-    return LG_OK;
+    const int64_t L = D * D + D;
+    int rc = lg_launch_slab_reduce(slab, grid, L, D * D, dW, s);
+    if (rc == LG_OK && db) rc = lg_launch_slab_reduce(slab + D * D, grid, L, D, db, s);
+    return rc;
 }

@@ -23,6 +23,7 @@
 // fixed order -> deterministic.
 #include <algorithm>
 #include "common.h"
+#include "reduce.h"
 
 namespace {
 
@@ -335,23 +336,6 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     }
 }
 
-__global__ void k_gru_reduce(const float* __restrict__ slab, int nslab, int len, float* __restrict__ dWih,
-                             float* __restrict__ dWhh, float* __restrict__ dbih, float* __restrict__ dbhh, int I) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= len) return;
-    float acc = 0.f;
-    for (int g = 0; g < nslab; ++g) acc += slab[static_cast<int64_t>(g) * len + i];
-    const int nWhh = G3 * H, nWih = G3 * I;
-    if (i < nWhh)
-        dWhh[i] = acc;
-    else if (i < nWhh + nWih)
-        dWih[i - nWhh] = acc;
-    else if (i < nWhh + nWih + G3)
-        dbih[i - nWhh - nWih] = acc;
-    else
-        dbhh[i - nWhh - nWih - G3] = acc;
-}
-
 inline int64_t nblocks_seq(int64_t nseq) { return (nseq + TS - 1) / TS; }
 
 }  // namespace
@@ -409,8 +393,11 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
 #undef LG_GRU_BWD
         LG_RET_IF_LAUNCH_FAILED();
     }
-    k_gru_reduce<<<(len + 255) / 256, 256, 0, s>>>(slab, B == 0 ? 1 : nb, len, dw_ih, dw_hh, db_ih, db_hh,
-                                                   static_cast<int>(I));
-    LG_RET_IF_LAUNCH_FAILED();
-    return LG_OK;
+    const int G = B == 0 ? 1 : nb;
+    const int64_t nWhh = G3 * H, nWih = G3 * I;
+    int rc = lg_launch_slab_reduce(slab, G, len, nWhh, dw_hh, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh, G, len, nWih, dw_ih, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih, G, len, G3, db_ih, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih + G3, G, len, G3, db_hh, s);
+    return rc;
 }

@@ -51,40 +51,27 @@ k_pipe_gather(const int64_t* __restrict__ ends, const float* __restrict__ h, flo
     }
 }
 
-__device__ __forceinline__ float sgnf(float d) { return d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f); }
-
+// dh[b][n] = dpool[b]/N + sum over incidences (p, role) of n, in item order, of dpipe[b][p][role]
 template <int D>
 __global__ void __launch_bounds__(256)
 k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict__ inc_item,
-               const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ dfeat,
-               const float* __restrict__ dpool, float* __restrict__ dh, int64_t N, int64_t P, int64_t R) {
+               const float* __restrict__ dpipe, const float* __restrict__ dpool, float* __restrict__ dh, int64_t N,
+               int64_t P, int64_t R) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-    const float invN = static_cast<float>(N);
+    const float fN = static_cast<float>(N);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
         const int64_t b = r / N, n = r - b * N;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         if (dpool) {
             const f32x4 g = ld4(dpool + b * D + 4 * fg);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] = g[k] / invN;
+            for (int k = 0; k < 4; ++k) acc[k] = g[k] / fN;
         }
         const int32_t e0 = inc_rowptr[n], e1 = inc_rowptr[n + 1];
         for (int32_t e = e0; e < e1; ++e) {
-            const int32_t it = inc_item[e];
-            const int64_t p = it >> 1;
-            const int role = it & 1;
-            const int64_t u = ends[2 * p], v = ends[2 * p + 1];
-            const float* df = dfeat + (b * P + p) * (3 * D) + 4 * fg;
-            const f32x4 hu = ld4(h + (b * N + u) * D + 4 * fg);
-            const f32x4 hv = ld4(h + (b * N + v) * D + 4 * fg);
-            const f32x4 dself = ld4(df + role * D);
-            const f32x4 dabs = ld4(df + 2 * D);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float sg = sgnf(hu[k] - hv[k]);
-                acc[k] += role == 0 ? dself[k] + dabs[k] * sg : dself[k] - dabs[k] * sg;
-            }
+            const int32_t it = inc_item[e];  // 2*p + role
+            acc += ld4(dpipe + ((b * P + (it >> 1)) * 2 + (it & 1)) * D + 4 * fg);
         }
         st4(dh + r * D + 4 * fg, acc);
     }
@@ -162,25 +149,18 @@ extern "C" int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* fe
     return LG_OK;
 }
 
-extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const int64_t* ends,
-                                   const float* h, const float* dfeat, const float* dpool, float* dh, int64_t B,
-                                   int64_t N, int64_t P, int64_t D, lg_stream_t stream) {
+extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const float* dpipe,
+                                   const float* dpool, float* dh, int64_t B, int64_t N, int64_t P, int64_t D,
+                                   lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
-    if (!inc_rowptr || !h || !dh || (P > 0 && (!inc_item || !ends || !dfeat))) return LG_EINVAL;
+    if (!inc_rowptr || !dh || (P > 0 && (!inc_item || !dpipe))) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64:
-            k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, ends, h, dfeat, dpool, dh, N, P,
-                                                               R);
-            break;
-        case 32:
-            k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, ends, h, dfeat, dpool, dh, N, P,
-                                                               R);
-            break;
-        default:
-            return LG_EUNSUPPORTED;
+        case 64: k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, P, R); break;
+        case 32: k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, P, R); break;
+        default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;

@@ -11,12 +11,14 @@ and models/window_evaluator.py use it unchanged:
   noleak_head.mlp.{0,3}.*           NoLeakHead                (detector.py:91-102)
 
 What runs where (forward + backward):
-  * GRU sensor encoder, the 29-row sensor projection, the EdgeHead / NoLeakHead
-    MLPs and the loss: stock PyTorch-ROCm (MIOpen / hipBLASLt).
-  * Node init, every GCNConv + ReLU + dropout, the pipe-endpoint gather and the
-    per-window mean pool: libleakgnn HIP kernels (ops.GNNTrunkFn, ops.PipeHeadsFn)
-    over ONE device-resident single-graph CSR; the (2, B*E) batchified
-    edge_index of the reference (detector.py:195-196) is never built.
+  * The 29-row sensor projection (one small GEMM), the NoLeakHead MLP on the
+    (B, 64) pooled vector and the loss: stock PyTorch-ROCm.
+  * The GRU sensor encoder, node init, every GCNConv + ReLU + dropout, the fused
+    EdgeHead (endpoint gather -> MLP -> logit, never materialising the (B,P,3D)
+    features) and the per-window mean pool: libleakgnn HIP kernels
+    (ops.GRUEncoderFn, ops.GNNTrunkFn, ops.HeadsFn) over ONE device-resident
+    single-graph CSR; the (2, B*E) batchified edge_index of the reference
+    (detector.py:195-196) is never built.
 There is no CPU path: forward raises on CPU tensors.
 """
 from __future__ import annotations
@@ -151,7 +153,9 @@ class LeakDetector(nn.Module):
                               nonsensor_idx=nonsensor,
                               dropout_p=float(self.dropout.p), training=self.training)
         h_nodes = ops.GNNTrunkFn.apply(cfg, proj, bn, *wb)               # (B, N, D)
-        feat, pooled = ops.PipeHeadsFn.apply(h_nodes, inc)              # (B, P, 3D), (B, D)
-        pipe_logits = self.edge_head.forward_feat(feat)                   # (B, P)
+        mlp = self.edge_head.mlp  # Linear(3D,128), ReLU, Dropout, Linear(128,1)
+        hcfg = ops.HeadsConfig(inc=inc, dropout_p=float(mlp[2].p), training=self.training)
+        pipe_logits, pooled = ops.HeadsFn.apply(hcfg, h_nodes, mlp[0].weight, mlp[0].bias, mlp[3].weight,
+                                                mlp[3].bias)              # (B, P), (B, D)
         noleak_logit = self.noleak_head(pooled).unsqueeze(-1)             # (B, 1)
         return torch.cat([pipe_logits, noleak_logit], dim=-1)

@@ -12,8 +12,10 @@ Autograd functions:
   * ``GCNLayerFn``    - one GCNConv (lin -> propagate -> +bias), PyG semantics.
   * ``GNNTrunkFn``    - LeakDetector node init + all conv/relu/dropout layers
                         (detector.py:178-201) as one fused forward / backward chain.
-  * ``PipeHeadsFn``   - pipe endpoint features + per-window mean pool
-                        (detector.py:206-215), backward fused into one kernel.
+  * ``HeadsFn``       - fused EdgeHead over every pipe + per-window mean pool
+                        (detector.py:76-88, 206-215); backward ends in one
+                        deterministic incidence reduce.
+  * ``GRUEncoderFn``  - SharedSensorGRUEncoder's GRU (detector.py:28-73).
 """
 from __future__ import annotations
 
@@ -324,44 +326,90 @@ class GNNTrunkFn(torch.autograd.Function):
         return (None, dproj, dbias, *grads_wb)
 
 
-class PipeHeadsFn(torch.autograd.Function):
-    """feat = cat[h_u, h_v, |h_u - h_v|] per pipe and pooled = mean_n h (detector.py:87, 206-215)."""
+EDGE_HEAD_SALT = 101  # dropout stream of the EdgeHead hidden layer (trunk layers use salts 0..L)
+
+
+@dataclass
+class HeadsConfig:
+    inc: Incidence
+    dropout_p: float
+    training: bool
+
+
+class HeadsFn(torch.autograd.Function):
+    """EdgeHead over every pipe + per-window mean pool (detector.py:87-88, 206-215).
+
+    forward:  pipe_logits (B, P) = lg_edge_head_fwd (gather -> MFMA MLP -> dot, fused),
+              pooled (B, D)      = lg_mean_pool_fwd
+    backward: lg_edge_head_bwd -> per-pipe endpoint grads, then ONE deterministic
+              incidence reduce (lg_pipe_scatter_bwd) that also adds dpooled / N.
+    """
 
     @staticmethod
-    def forward(ctx, h, inc: Incidence):
+    def forward(ctx, cfg: HeadsConfig, h, w1, b1, w2, b2):
         lib = load_library()
         h = h.contiguous()
-        require_device(h)
+        require_device(h, w1, b1, w2, b2)
         B, N, D = h.shape
         _check_d(D)
+        hidden = w1.shape[0]
+        inc = cfg.inc
         P = inc.num_pipes
+        drop = cfg.training and cfg.dropout_p > 0.0
+        p = float(cfg.dropout_p) if drop else 0.0
+        seed = _new_seed() if drop else 0
+        flags = nat.LG_F_DROPOUT if drop else 0
         st = stream_of(h)
-        feat = torch.empty(B, P, 3 * D, device=h.device, dtype=torch.float32)
+        logits = torch.empty(B, P, device=h.device, dtype=torch.float32)
         pooled = torch.empty(B, D, device=h.device, dtype=torch.float32)
-        with _timed("pipe_gather", h.device):
-            check(lib.lg_pipe_gather_fwd(ptr(inc.ends), ptr(h), ptr(feat), B, N, P, D, st), "lg_pipe_gather_fwd")
+        w1c, w2c = w1.contiguous(), w2.contiguous()
+        with _timed("edge_fwd", h.device):
+            check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits), B, N,
+                                       P, D, hidden, flags, p, seed, EDGE_HEAD_SALT, st), "lg_edge_head_fwd")
         with _timed("mean_pool", h.device):
             check(lib.lg_mean_pool_fwd(ptr(h), ptr(pooled), B, N, D, st), "lg_mean_pool_fwd")
-        ctx.inc = inc
-        ctx.save_for_backward(h)
-        return feat, pooled
+        ctx.cfg, ctx.p, ctx.seed, ctx.flags = cfg, p, seed, flags
+        ctx.save_for_backward(h, w1c, b1, w2c)
+        return logits, pooled
 
     @staticmethod
-    def backward(ctx, dfeat, dpool):
+    def backward(ctx, dlogits, dpooled):
         lib = load_library()
-        (h,) = ctx.saved_tensors
-        inc = ctx.inc
+        h, w1, b1, w2 = ctx.saved_tensors
+        inc = ctx.cfg.inc
         B, N, D = h.shape
-        P = inc.num_pipes
+        P, hidden = inc.num_pipes, w1.shape[0]
+        dev = h.device
+        st = stream_of(h)
+        if dlogits is None:
+            dlogits = torch.zeros(B, P, device=dev)
+        dpipe = torch.empty(B, P, 2, D, device=dev)
+        dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
+        dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
+        ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
+        with _timed("edge_bwd", dev):
+            check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(dlogits.contiguous()),
+                                       ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden,
+                                       ctx.flags, ctx.p, ctx.seed, EDGE_HEAD_SALT, ptr(ws), st), "lg_edge_head_bwd")
         dh = torch.empty_like(h)
-        if dfeat is None:
-            dfeat = torch.zeros(B, P, 3 * D, device=h.device, dtype=h.dtype)
-        dfeat = dfeat.contiguous()
-        dpool = dpool.contiguous() if dpool is not None else None
-        with _timed("pipe_scatter", h.device):
-            check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(inc.ends), ptr(h), ptr(dfeat),
-                                          ptr(dpool), ptr(dh), B, N, P, D, stream_of(h)), "lg_pipe_scatter_bwd")
-        return dh, None
+        with _timed("pipe_scatter", dev):
+            check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe),
+                                          ptr(dpooled.contiguous() if dpooled is not None else None), ptr(dh), B, N,
+                                          P, D, st), "lg_pipe_scatter_bwd")
+        return None, dh, dw1, db1, dw2, db2
+
+
+def pipe_features(h: torch.Tensor, inc: Incidence) -> torch.Tensor:
+    """feat = cat[h_u, h_v, |h_u - h_v|] per pipe (lg_pipe_gather_fwd); no autograd."""
+    lib = load_library()
+    h = h.contiguous()
+    require_device(h)
+    B, N, D = h.shape
+    _check_d(D)
+    feat = torch.empty(B, inc.num_pipes, 3 * D, device=h.device)
+    check(lib.lg_pipe_gather_fwd(ptr(inc.ends), ptr(h), ptr(feat), B, N, inc.num_pipes, D, stream_of(h)),
+          "lg_pipe_gather_fwd")
+    return feat
 
 
 class MeanPoolWindowsFn(torch.autograd.Function):

@@ -210,84 +210,112 @@ def test_detector_train_mode_dropout():
     assert_close(x0[x0 > 0], torch.full_like(x0[x0 > 0], 1 / 0.9), what="dropout scale")
 
 
-def test_detector_train_mode_grad_matches_autograd_of_masks():
-    """Train-mode backward: the kernels rebuild relu/dropout masks from [y > 0].
-    Check against torch autograd of the same forward with the masks made explicit."""
+def _masks(seed: int, salt: int, shape, p: float, dev=DEV) -> torch.Tensor:
+    from oracle.dropout_ref import keep_mask
+    idx = np.arange(int(np.prod(shape)), dtype=np.uint64).reshape(shape)
+    return torch.from_numpy(keep_mask(seed, salt, idx, p).astype(np.float32)).to(dev)
+
+
+def test_detector_train_mode_replay_with_oracle_masks():
+    """Train mode end to end: every dropout mask of the HIP path (node init, both GCN
+    layers, EdgeHead hidden) is regenerated on the host by oracle/dropout_ref.py and the
+    whole detector is replayed with explicit torch ops; forward and all grads must agree."""
+    from models import ops
     state = load("detector_b2.npz")
     m = _product_model(state).train()
-    from models import ops
-    B = 8
+    B, N, D, P = 6, 661, 64, 764
     r = torch.randn(B, 36, 29, device=DEV)
     tf = torch.randn(B, 36, 9, device=DEV)
     torch.manual_seed(9)
     out = m(r, tf)
     out.square().sum().backward()
     grads = {n: p.grad.clone() for n, p in m.named_parameters()}
-    # replay: same seed -> same masks; re-derive them with the GPU forward and apply via torch ops
     m.zero_grad()
     torch.manual_seed(9)
-    xs = []
-    orig_apply = ops.GNNTrunkFn.apply
-
-    def capturing_apply(cfg, *args):
-        cfg.capture = xs
-        return orig_apply(cfg, *args)
-
-    ops.GNNTrunkFn.apply = capturing_apply
-    try:
-        m(r, tf)
-    finally:
-        del ops.GNNTrunkFn.apply  # back to torch.autograd.Function.apply
-    assert len(xs) == 3
-    # torch-only trunk with explicit masks (mask_l = x_l > 0, scale 1/(1-p))
-    from oracle import gcn_ref
-    sc = 1 / 0.9
-    ei = torch.from_numpy(graph_ref.batchify(m.edge_index_single.numpy(), 661, B))
+    seed_t = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # GNNTrunkFn draw
+    seed_h = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # HeadsFn draw
+    sc = 1.0 / 0.9
+    R = B * N
+    mk = [_masks(seed_t, l, (R, D), 0.1) for l in range(3)]
+    me = _masks(seed_h, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1)
+    ei = torch.from_numpy(graph_ref.batchify(m.edge_index_single.numpy(), N, B))
+    row, col, w = (t.to(DEV) for t in gcn_ref.gcn_norm(ei, R))
     h_s = m.sensor_encoder(r, tf)
     Wn, bn = m.sensor_to_node.weight, m.sensor_to_node.bias
-    h0 = torch.zeros(B, 661, 64, device=DEV)
+    h0 = torch.zeros(B, N, 64, device=DEV)
     h0[:, m.sensor_node_idx.to(DEV)] = h_s
-    mask = torch.zeros(661, 1, device=DEV)
+    mask = torch.zeros(N, 1, device=DEV)
     mask[m.sensor_node_idx.to(DEV)] = 1
-    h = torch.relu(torch.cat([h0, mask.expand(B, -1, -1)], -1) @ Wn.t() + bn)
-    x = (h * (xs[0] > 0) * sc).reshape(B * 661, 64)
+    x = (torch.relu(torch.cat([h0, mask.expand(B, -1, -1)], -1) @ Wn.t() + bn).reshape(R, D)) * mk[0] * sc
     for l, conv in enumerate(m.convs):
-        row, col, w = gcn_ref.gcn_norm(ei, B * 661)
         hh = x @ conv.lin.weight.t()
-        agg = torch.zeros_like(hh).index_add_(0, col.to(DEV), w.to(DEV).view(-1, 1) * hh[row.to(DEV)])
-        x = torch.relu(agg + conv.bias) * (xs[l + 1].reshape(B * 661, 64) > 0) * sc
-    hn = x.view(B, 661, 64)
+        agg = torch.zeros_like(hh).index_add_(0, col, w.view(-1, 1) * hh[row])
+        x = torch.relu(agg + conv.bias) * mk[l + 1] * sc
+    hn = x.view(B, N, D)
     u, v = m.pipe_ends[:, 0].to(DEV), m.pipe_ends[:, 1].to(DEV)
-    feat = torch.cat([hn[:, u], hn[:, v], (hn[:, u] - hn[:, v]).abs()], -1)
-    torch.manual_seed(9)  # head dropouts draw from the CUDA generator: same masks as the product forward
-    pl = m.edge_head.forward_feat(feat)
-    nl = m.noleak_head(hn.mean(1)).unsqueeze(-1)
+    feat = torch.cat([hn[:, u], hn[:, v], (hn[:, u] - hn[:, v]).abs()], -1).reshape(B * P, 3 * D)
+    mlp = m.edge_head.mlp
+    hid = torch.relu(feat @ mlp[0].weight.t() + mlp[0].bias) * me * sc
+    pl = (hid @ mlp[3].weight.t() + mlp[3].bias).view(B, P)
+    nl = m.noleak_head(hn.mean(1)).unsqueeze(-1)   # torch dropout: same CUDA RNG stream as the product
     out2 = torch.cat([pl, nl], -1)
-    assert_close(out2, out, rtol=1e-5, what="train-mode replay forward")
+    assert_close(out, out2, what="train-mode forward replay")
     out2.square().sum().backward()
-    assert_grads_close(list(grads.items()), {n: p.grad for n, p in m.named_parameters()}, prefix="train grad ")
+    # both sides are fp32 GPU with different summation orders; a mask/structure bug is O(1)
+    assert_grads_close(list(grads.items()), {n: p.grad for n, p in m.named_parameters()}, rtol=1e-4,
+                       prefix="train grad ")
 
 
-def test_pipe_heads_and_pool_vs_torch():
-    from models.ops import Incidence, PipeHeadsFn
+@pytest.mark.parametrize("train", [False, True])
+@pytest.mark.parametrize("D", [64, 32])
+def test_fused_heads_vs_torch(train, D):
+    """HeadsFn (fused EdgeHead + mean pool, incidence-reduced backward) vs float64 torch."""
+    from models import ops
+    from models.ops import HeadsConfig, HeadsFn, Incidence
+    g = load("graph_ltown_a.npz")
+    ends = torch.from_numpy(g["pipe_ends"])
+    inc = Incidence.build(ends, 661, DEV)
+    B, N, P = 5, 661, 764
+    gen = torch.Generator().manual_seed(D + train)
+    h = torch.randn(B, N, D, generator=gen)
+    h[0, :40] = 0.25  # ties -> |h_u - h_v| = 0, sign 0
+    W1 = torch.randn(128, 3 * D, generator=gen) / 8
+    b1 = torch.randn(128, generator=gen) / 4
+    W2 = torch.randn(1, 128, generator=gen) / 8
+    b2 = torch.randn(1, generator=gen)
+    dl = torch.randn(B, P, generator=gen)
+    dp = torch.randn(B, D, generator=gen)
+    params = [t.to(DEV).requires_grad_(True) for t in (h, W1, b1, W2, b2)]
+    torch.manual_seed(77)
+    logits, pooled = HeadsFn.apply(HeadsConfig(inc, 0.1, train), *params)
+    ((logits * dl.to(DEV)).sum() + (pooled * dp.to(DEV)).sum()).backward()
+    # float64 reference with the same dropout mask
+    ref = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2)]
+    hr, W1r, b1r, W2r, b2r = ref
+    u, v = ends[:, 0], ends[:, 1]
+    feat = torch.cat([hr[:, u], hr[:, v], (hr[:, u] - hr[:, v]).abs()], -1)
+    hid = torch.relu(feat @ W1r.t() + b1r)
+    if train:
+        torch.manual_seed(77)
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())
+        hid = hid * _masks(seed, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1, dev="cpu").double().view(B, P, 128) / 0.9
+    lr = (hid @ W2r.t()).squeeze(-1) + b2r
+    pr = hr.mean(1)
+    ((lr * dl.double()).sum() + (pr * dp.double()).sum()).backward()
+    assert_close(logits, lr, what="edge logits")
+    assert_close(pooled, pr, what="pooled")
+    for a, b, n in zip(params, ref, ("dh", "dW1", "db1", "dW2", "db2")):
+        assert_close(a.grad, b.grad, rtol=2e-5, what=n)
+
+
+def test_pipe_features_kernel():
+    from models.ops import Incidence, pipe_features
     g = load("graph_ltown_a.npz")
     inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV)
-    B = 5
-    h = torch.randn(B, 661, 64, device=DEV)
-    h[0, :10] = 0.5  # ties: |h_u - h_v| at 0 (sign 0)
-    hg = h.clone().requires_grad_(True)
-    feat, pooled = PipeHeadsFn.apply(hg, inc)
-    ht = h.clone().requires_grad_(True)
+    h = torch.randn(3, 661, 64, device=DEV)
     e = torch.from_numpy(g["pipe_ends"]).to(DEV)
-    hu, hv = ht[:, e[:, 0]], ht[:, e[:, 1]]
-    ft = torch.cat([hu, hv, (hu - hv).abs()], -1)
-    pt = ht.mean(1)
-    assert torch.equal(feat, ft)
-    assert_close(pooled, pt, what="mean pool")
-    df, dp = torch.randn_like(ft), torch.randn_like(pt)
-    (feat * df).sum().add((pooled * dp).sum()).backward()
-    (ft * df).sum().add((pt * dp).sum()).backward()
-    assert_close(hg.grad, ht.grad, what="pipe scatter + pool bwd")
+    hu, hv = h[:, e[:, 0]], h[:, e[:, 1]]
+    assert torch.equal(pipe_features(h, inc), torch.cat([hu, hv, (hu - hv).abs()], -1))
 
 
 def test_full_size_properties_c5():
