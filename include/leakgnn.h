@@ -105,27 +105,32 @@ int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float*
                      int64_t B, int64_t N, int64_t S, int64_t D,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 
-/* K5+K6+K7  fused GCN layer forward (one launch).
+/* nnz_cap (lg_gcn_fwd / lg_spmm / lg_gcn_bwd): capacity of col/w as allocated for
+ * lg_graph_build (E + N).  It sizes the on-chip copy of the CSR: when
+ * 4*(N+1) + 8*nnz_cap <= 48 KiB every workgroup stages the CSR in LDS once.
+ *
+ * K5+K6+K7  fused GCN layer forward (one launch).
  * Replaces: GCNConv.forward (lin -> propagate -> +bias, detector.py:199) and the
  * following F.relu + dropout (detector.py:200-201):
  *   y = dropout(relu( Ahat (x W^T) + b ))  computed as  (Ahat x) W^T + b
- * Each 64-lane wavefront owns a 16-row tile: CSR gather + segmented reduce of the
- * neighbour rows (fp32), the tile staged in LDS, then the 16 x D x D product on
- * MFMA (v_mfma_f32_16x16x4_f32, exact fp32), bias/ReLU/dropout epilogue, and a
- * coalesced row store.
+ * Each 64-lane wavefront owns a 16-row tile and computes it transposed,
+ * y^T = W (Ahat x)^T: every lane gathers (CSR segmented reduce, fp32) exactly the
+ * MFMA B-operand fragment of its row, the D x D product runs on MFMA
+ * (v_mfma_f32_16x16x4_f32, exact fp32) with W in registers, and the accumulator is
+ * already in row-store layout for the bias/ReLU/dropout epilogue.
  *   rowptr/col/w : CSR from lg_graph_build;  x, y : fp32 [B][N][D];  W : fp32 [D][D]
  *   (nn.Linear layout [out][in]);  bias : fp32 [D] or NULL.
  *   Dropout: keep element (row, c) iff hash(seed, salt, row*D + c) >= p, scale 1/(1-p).
  *   x and y must not alias. */
 int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
                const float* x, const float* W, const float* bias, float* y,
-               int64_t B, int64_t N, int64_t D,
+               int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 
 /* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
  * weights; no transform).  Used for the HBM-roofline stress case (config C5). */
 int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,
-            const float* x, float* y, int64_t B, int64_t N, int64_t D, lg_stream_t stream);
+            const float* x, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, lg_stream_t stream);
 
 /* Fused GCN layer backward (one main launch + one deterministic slab reduction).
  * Given dy = dL/dy of this layer's output:
@@ -143,7 +148,7 @@ int64_t lg_gcn_bwd_workspace_bytes(int64_t D);
 int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t,
                const float* dy, const float* y, const float* x, const float* W,
                float* dx_out, float* dW, float* db,
-               int64_t B, int64_t N, int64_t D,
+               int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                int flags, float scale_in, float scale_out,
                void* workspace, lg_stream_t stream);
 

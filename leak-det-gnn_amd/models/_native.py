@@ -34,10 +34,11 @@ SIGNATURES = {
     "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
     "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),
     "lg_node_init_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
-    "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
-    "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _p]),
+    "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_gcn_bwd_workspace_bytes": (_i64, [_i64]),
-    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p, _p]),
+    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32, _p,
+                          _p]),
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_edge_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32,

@@ -138,6 +138,7 @@ class GCNGraph:
         f32 = dict(device=device, dtype=torch.float32)
         g = GCNGraph(N, E, torch.empty(N + 1, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32),
                      torch.empty(N + 1, **i32), torch.empty(cap, **i32), torch.empty(cap, **f32))
+        g.nnz_cap = cap
         ws = torch.empty(int(lib.lg_graph_workspace_bytes(E, N)), device=device, dtype=torch.uint8)
         fill = 2.0 if improved else 1.0
         check(lib.lg_graph_build(ptr(ei), E, N, int(add_self_loops), int(normalize), fill, ptr(g.rowptr),
@@ -213,7 +214,7 @@ class GCNLayerFn(torch.autograd.Function):
         flags = nat.LG_F_BIAS if bias is not None else 0
         with _timed("gcn_fwd", x.device):
             check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(weight), ptr(bias),
-                                 ptr(y), 1, Ntot, D, flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
+                                 ptr(y), 1, Ntot, D, graph.nnz_cap, flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
         ctx.graph = graph
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight)
@@ -232,7 +233,7 @@ class GCNLayerFn(torch.autograd.Function):
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
         with _timed("gcn_bwd", x.device):
             check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), None, ptr(x), ptr(weight),
-                                 ptr(dx), ptr(dW), ptr(db), 1, Ntot, D, 0, 1.0, 1.0, ptr(ws), stream_of(x)),
+                                 ptr(dx), ptr(dW), ptr(db), 1, Ntot, D, g.nnz_cap, 0, 1.0, 1.0, ptr(ws), stream_of(x)),
                   "lg_gcn_bwd")
         return dx, dW, (db if ctx.has_bias else None), None
 
@@ -286,7 +287,8 @@ class GNNTrunkFn(torch.autograd.Function):
             y = torch.empty_like(x0)
             with _timed("gcn_fwd", proj.device):
                 check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
-                                     D, nat.LG_F_BIAS | nat.LG_F_RELU | dflag, p, seed, l + 1, st), "lg_gcn_fwd")
+                                     D, g.nnz_cap, nat.LG_F_BIAS | nat.LG_F_RELU | dflag, p, seed, l + 1, st),
+                      "lg_gcn_fwd")
             xs.append(y)
         if cfg.capture is not None:
             cfg.capture.extend(t.detach().clone() for t in xs)
@@ -315,8 +317,8 @@ class GNNTrunkFn(torch.autograd.Function):
             db = torch.empty(D, device=dy.device, dtype=torch.float32)
             with _timed("gcn_bwd", dy.device):
                 check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
-                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), B, N, D, flags, ctx.scale, ctx.scale,
-                                     ptr(ws), st), "lg_gcn_bwd")
+                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), B, N, D, g.nnz_cap, flags, ctx.scale,
+                                     ctx.scale, ptr(ws), st), "lg_gcn_bwd")
             grads_wb[2 * l], grads_wb[2 * l + 1] = dW, db
             dy = dx  # already masked by the previous op's relu/dropout
         dproj = dy.index_select(1, cfg.sensor_idx)
@@ -491,7 +493,7 @@ def spmm(graph: GCNGraph, x: torch.Tensor, B: int = 1) -> torch.Tensor:
     y = torch.empty_like(x)
     with _timed("spmm", x.device):
         check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, graph.num_nodes, D,
-                          stream_of(x)), "lg_spmm")
+                          graph.nnz_cap, stream_of(x)), "lg_spmm")
     return y
 
 

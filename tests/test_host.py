@@ -111,8 +111,8 @@ def test_c_abi_host_only_calls():
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1
     assert lib.lg_incidence_workspace_bytes(764, 661) >= 8 * 661
     assert lib.lg_gcn_bwd_workspace_bytes(48) == -2
-    assert lib.lg_gcn_fwd(None, None, None, None, None, None, None, 1, 661, 64, 0, 0.0, 0, 0, None) == -1
-    assert lib.lg_gcn_bwd(None, None, None, None, None, None, None, None, None, None, 1, 661, 64, 0, 1.0, 1.0,
+    assert lib.lg_gcn_fwd(None, None, None, None, None, None, None, 1, 661, 64, 2193, 0, 0.0, 0, 0, None) == -1
+    assert lib.lg_gcn_bwd(None, None, None, None, None, None, None, None, None, None, 1, 661, 64, 2193, 0, 1.0, 1.0,
                           None, None) == -1
     assert lib.lg_graph_build(None, 5, 0, 1, 1, 1.0, None, None, None, None, None, None, None, None) == -1
     assert lib.lg_pipe_gather_fwd(None, None, None, 1, 10, 5, 64, None) == -1
