@@ -22,22 +22,33 @@ static inline int lg_num_cus() {
     return cus;
 }
 
-// Counter-based dropout RNG: a pure function of (seed, salt, element index), so
-// the forward mask never has to be stored (backward reads the mask back as
-// [y > 0]).  splitmix64 finaliser; top 24 bits -> uniform in [0, 1).
-__device__ __forceinline__ uint32_t lg_hash(uint64_t seed, uint32_t salt, uint64_t idx) {
-    uint64_t z = seed ^ (static_cast<uint64_t>(salt) << 32) ^ (idx * 0x9E3779B97F4A7C15ull);
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    z ^= z >> 31;
-    return static_cast<uint32_t>(z >> 40);  // 24 bits
+// Counter-based dropout RNG: a pure function of (seed, salt, element index), so the
+// forward mask never has to be stored (the backward reads it back as [y > 0] or
+// recomputes it).  32-bit "lowbias32" finaliser (~10 VALU ops per element); the
+// per-call key folds the 64-bit seed and the call-site salt once per thread.
+// keep <=> (h >> 8) * 2^-24 >= p, kept values scaled by 1 / (1 - p).
+// Restated for the tests in oracle/dropout_ref.py.
+__host__ __device__ __forceinline__ uint32_t lg_mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
 }
 
-__device__ __forceinline__ float lg_dropout(float v, float p, float scale, uint64_t seed, uint32_t salt,
-                                            uint64_t idx) {
-    const float u = static_cast<float>(lg_hash(seed, salt, idx)) * (1.0f / 16777216.0f);
-    return u >= p ? v * scale : 0.0f;
+__host__ __device__ __forceinline__ uint32_t lg_dropout_key(uint64_t seed, uint32_t salt) {
+    return lg_mix32(static_cast<uint32_t>(seed) ^ lg_mix32(static_cast<uint32_t>(seed >> 32) ^ (salt * 0x9E3779B9U)));
+}
+
+__device__ __forceinline__ bool lg_keep(uint32_t key, uint64_t idx, float p) {
+    const uint32_t h = lg_mix32((static_cast<uint32_t>(idx) * 0x9E3779B9U) ^ key ^
+                                (static_cast<uint32_t>(idx >> 32) * 0x85EBCA6BU));
+    return static_cast<float>(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+__device__ __forceinline__ float lg_dropout(float v, float p, float scale, uint32_t key, uint64_t idx) {
+    return lg_keep(key, idx, p) ? v * scale : 0.0f;
 }
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

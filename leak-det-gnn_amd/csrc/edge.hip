@@ -85,10 +85,6 @@ __device__ __forceinline__ float feat1(const float* __restrict__ ft, int row, in
     return fabsf(ft[row * G::FS + (k - 2 * D)] - ft[row * G::FS + (k - D)]);
 }
 
-__device__ __forceinline__ bool keep_elem(float p, uint64_t seed, uint32_t salt, uint64_t idx) {
-    return static_cast<float>(lg_hash(seed, salt, idx)) * (1.0f / 16777216.0f) >= p;
-}
-
 // hid^T tile rows n = 16w + 4q + reg for feat row j, bias included
 template <int D>
 __device__ __forceinline__ f32x4 hidden_tile(const float* __restrict__ ft, const float (&aw)[EG<D>::KS], f32x4 acc,
@@ -122,6 +118,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         w2v[reg] = W2[16 * w + 4 * q + reg];
     }
     const float bias2 = b2[0];
+    const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
         gather_tile<D>(ends, h, ft, row0, BP, P, N);
@@ -131,7 +128,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
             float v = fmaxf(acc[reg], 0.f);
-            if (dropout) v = lg_dropout(v, p_drop, dscale, seed, salt, (row0 + j) * HID + 16 * w + 4 * q + reg);
+            if (dropout) v = lg_dropout(v, p_drop, dscale, key, (row0 + j) * HID + 16 * w + 4 * q + reg);
             s = fmaf(v, w2v[reg], s);
         }
         s += __shfl_xor(s, 16);
@@ -186,6 +183,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     for (int mt = 0; mt < G::MT; ++mt) dwt[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 dw2 = f32x4{0.f, 0.f, 0.f, 0.f}, db1 = f32x4{0.f, 0.f, 0.f, 0.f};
     double db2 = 0.0;  // sum of all dlogits: heavy cancellation, kept in fp64 end to end
+    const uint32_t key = lg_dropout_key(seed, salt);
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
@@ -199,7 +197,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             const int n = 16 * w + 4 * q + reg;
             const float pre = acc[reg];
             float m = pre > 0.f ? 1.f : 0.f;
-            if (dropout) m = keep_elem(p_drop, seed, salt, (row0 + j) * HID + n) ? m * dscale : 0.f;
+            if (dropout) m = lg_keep(key, (row0 + j) * HID + n, p_drop) ? m * dscale : 0.f;
             dw2[reg] = fmaf(dl, pre * m, dw2[reg]);
             const float g = dl * w2v[reg] * m;
             db1[reg] += g;

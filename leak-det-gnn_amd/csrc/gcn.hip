@@ -25,7 +25,7 @@
 
 namespace {
 
-constexpr int kWaves = 4;      // waves per workgroup
+constexpr int kWaves = 8;      // waves per workgroup
 constexpr int kTileRows = 16;  // rows per wave tile (MFMA N)
 constexpr int64_t kCsrLdsMax = 48 * 1024;
 
@@ -90,130 +90,193 @@ __device__ __forceinline__ Csr stage_csr(char* smem, const int32_t* __restrict__
     return Csr{srp, scol, sw};
 }
 
-// Row j of the tile: acc[a][i] = sum_e w_e * src[(b*N + col_e)][16a + 4q + i]  (in CSR order).
-// MASK: the gathered values are dy * scale * [m > 0] (ReLU/dropout backward).
-template <int D, bool MASK>
-__device__ __forceinline__ void gather_row(const Csr& g, const float* __restrict__ src, const float* __restrict__ msk,
-                                           float mscale, int64_t r, bool valid, int64_t N, int q,
-                                           f32x4 (&acc)[Geo<D>::A4]) {
+// Coalesced row gather ("16 lanes per row"): lane (rl = lane>>4, fg = lane&15) owns
+// feature float4 fg of rows 4k + rl of an 8-row group; each wave-instruction reads
+// four whole 4*D-byte rows.  Two rows x two neighbours in flight per lane.  Row r sums
+// w_e * src[b*N + col_e] over its CSR entries in order (fp32 fma).  MASK: gathered
+// values are dy * scale * [m > 0] (ReLU/dropout backward of the gathered tensor).
+// Measured on MI355X (tools/spmm_lab.hip, L-TOWN-A shape, B = 256): 4.3-4.5 TB/s for
+// this layout vs 3.0 TB/s for quarter-row lanes; stream copy 6.4 TB/s.
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+template <int D, bool MASK, typename Hook = NoHook>
+__device__ __forceinline__ void gather8(const Csr& g, const float* __restrict__ src, const float* __restrict__ msk,
+                                        float mscale, int64_t rbase, int64_t R, int64_t N, int lane,
+                                        f32x4 (&acc)[2], Hook&& hook = Hook{}) {
+    constexpr int LPR = D / 4;  // lanes per row
+    constexpr int RPI = 64 / LPR;  // rows per instruction
+    const int rl = lane / LPR, fg = lane % LPR;
+    int e0[2], e1[2];
+    int64_t off[2];
+    int maxd = 0;
 #pragma unroll
-    for (int a = 0; a < Geo<D>::A4; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (!valid) return;
-    const int64_t b = r / N, n = r - b * N;
-    const int32_t e0 = g.rp[n], e1 = g.rp[n + 1];
-    const float* base = src + b * N * D + 4 * q;
-    const float* mbase = MASK ? msk + b * N * D + 4 * q : nullptr;
-    int32_t e = e0;
-    for (; e + 1 < e1; e += 2) {  // two neighbours in flight
-        const int32_t s0 = g.col[e], s1 = g.col[e + 1];
-        const float w0 = g.w[e], w1 = g.w[e + 1];
-        f32x4 v0[Geo<D>::A4], v1[Geo<D>::A4];
-#pragma unroll
-        for (int a = 0; a < Geo<D>::A4; ++a) {
-            v0[a] = ld4(base + static_cast<int64_t>(s0) * D + 16 * a);
-            v1[a] = ld4(base + static_cast<int64_t>(s1) * D + 16 * a);
+    for (int k = 0; k < 2; ++k) {
+        acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int64_t r = rbase + RPI * k + rl;
+        if (r < R) {
+            const int64_t b = r / N, n = r - b * N;
+            e0[k] = g.rp[n];
+            e1[k] = g.rp[n + 1];
+            off[k] = b * N * D + 4 * fg;
+        } else {
+            e0[k] = e1[k] = 0;
+            off[k] = 4 * fg;
         }
-        if constexpr (MASK) {
+        maxd = max(maxd, e1[k] - e0[k]);
+    }
+    // wave-uniform trip count: the hook (MFMA) must run with every lane active
 #pragma unroll
-            for (int a = 0; a < Geo<D>::A4; ++a) {
-                const f32x4 m0 = ld4(mbase + static_cast<int64_t>(s0) * D + 16 * a);
-                const f32x4 m1 = ld4(mbase + static_cast<int64_t>(s1) * D + 16 * a);
+    for (int o = 32; o >= 1; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o));
+    maxd = __builtin_amdgcn_readfirstlane(maxd);
+    for (int d = 0; d < maxd; d += 2) {
+        f32x4 v[2][2];
+        float ww[2][2];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    v0[a][i] = m0[i] > 0.f ? v0[a][i] * mscale : 0.f;
-                    v1[a][i] = m1[i] > 0.f ? v1[a][i] * mscale : 0.f;
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = e0[k] + d + u;
+                const bool ok = e < e1[k];
+                const int32_t s = ok ? g.col[e] : 0;
+                ww[k][u] = ok ? g.w[e] : 0.f;
+                const int64_t o = off[k] + static_cast<int64_t>(s) * D;
+                v[k][u] = ld4(src + o);
+                if constexpr (MASK) {
+                    const f32x4 m = ld4(msk + o);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[k][u][i] = m[i] > 0.f ? v[k][u][i] * mscale : 0.f;
                 }
             }
-        }
+        hook();  // independent work (e.g. the previous tile's MFMAs) under the load latency
 #pragma unroll
-        for (int a = 0; a < Geo<D>::A4; ++a)
+        for (int k = 0; k < 2; ++k)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[a][i] = fmaf(w1, v1[a][i], fmaf(w0, v0[a][i], acc[a][i]));
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(ww[k][u], v[k][u][i], acc[k][i]);
     }
-    if (e < e1) {
-        const int32_t s0 = g.col[e];
-        const float w0 = g.w[e];
+}
+
+// Gather the 16-row tile at r0 into tl[row][feature] (row stride S).
+template <int D, bool MASK, typename Hook = NoHook>
+__device__ __forceinline__ void gather_tile(const Csr& g, const float* __restrict__ src,
+                                            const float* __restrict__ msk, float mscale, int64_t r0, int64_t R,
+                                            int64_t N, int lane, float* __restrict__ tl, Hook&& hook = Hook{}) {
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    const int rl = lane / LPR, fg = lane % LPR;
 #pragma unroll
-        for (int a = 0; a < Geo<D>::A4; ++a) {
-            f32x4 v = ld4(base + static_cast<int64_t>(s0) * D + 16 * a);
-            if constexpr (MASK) {
-                const f32x4 m = ld4(mbase + static_cast<int64_t>(s0) * D + 16 * a);
+    for (int pass = 0; pass < kTileRows / (2 * RPI); ++pass) {
+        f32x4 acc[2];
+        gather8<D, MASK>(g, src, msk, mscale, r0 + pass * 2 * RPI, R, N, lane, acc, hook);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = m[i] > 0.f ? v[i] * mscale : 0.f;
-            }
+        for (int k = 0; k < 2; ++k) st4(tl + (pass * 2 * RPI + RPI * k + rl) * Geo<D>::S + 4 * fg, acc[k]);
+    }
+}
+
+// Store the 16-row tile tl[row][feature] to dst rows r0.. as whole rows.
+template <int D>
+__device__ __forceinline__ void store_tile(const float* __restrict__ tl, float* __restrict__ dst, int64_t r0,
+                                           int64_t R, int lane) {
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    const int rl = lane / LPR, fg = lane % LPR;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[a][i] = fmaf(w0, v[i], acc[a][i]);
-        }
+    for (int k = 0; k < kTileRows / RPI; ++k) {
+        const int row = RPI * k + rl;
+        if (r0 + row < R) st4(dst + (r0 + row) * D + 4 * fg, ld4(tl + row * Geo<D>::S + 4 * fg));
     }
 }
 
 // ------------------------------------------------------------------ forward
+// y^T = W (Ahat x)^T: B operand = the gathered tile (LDS), A operand = W (LDS).
+// Software pipeline per wave: the tile is double-buffered in LDS and the MFMA
+// chunks of tile i run between issuing and consuming each gather round of tile
+// i+1, so the matrix pipe works under the memory latency of the next gather.
+constexpr int kFwdWaves = 12;  // one 768-thread workgroup per CU: 12 x 8.7 KB tiles + W + CSR in LDS
+
 template <int D, bool CSR_LDS>
-__global__ void __launch_bounds__(64 * kWaves, 4)
+__global__ void __launch_bounds__(64 * kFwdWaves)
 k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
           const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
           float* __restrict__ y, int64_t N, int64_t R, int64_t ntiles, int flags, float p_drop, float dscale,
           uint64_t seed, uint32_t salt, int64_t csr_bytes) {
     using G = Geo<D>;
+    constexpr int TILE = kTileRows * G::S;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* wl = reinterpret_cast<float*>(smem + (CSR_LDS ? csr_bytes : 0));  // W [out][in], stride S
-    for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)),
-                                                                  ld4(W + 4 * i));
+    float* tiles = wl + D * G::S;
+    for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x)
+        st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), ld4(W + 4 * i));
     const Csr g = CSR_LDS ? stage_csr(smem, rowptr, col, wgt, N) : Csr{rowptr, col, wgt};
     if (!CSR_LDS) __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    float* buf0 = tiles + wave * 2 * TILE;
+    const uint32_t key = lg_dropout_key(seed, salt);
     f32x4 bv[G::MT];
 #pragma unroll
     for (int mt = 0; mt < G::MT; ++mt)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) bv[mt][reg] = (flags & LG_F_BIAS) ? bias[16 * mt + 4 * q + reg] : 0.f;
 
-    const TileRange tr = xcd_tiles(ntiles, wave, kWaves);
-    for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
-        const int64_t r = tile * kTileRows + j;
-        const bool valid = r < R;
-        f32x4 acc[G::A4];
-        gather_row<D, false>(g, x, nullptr, 1.f, r, valid, N, q, acc);
-        asm volatile("" ::: "memory");  // keep the W reads below in the loop (no 64-VGPR hoist)
+    const TileRange tr = xcd_tiles(ntiles, wave, kFwdWaves);
+    if (tr.first < tr.end) gather_tile<D, false>(g, x, nullptr, 1.f, tr.first * kTileRows, R, N, lane, buf0);
+    int cur = 0;
+    for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride, cur ^= 1) {
+        float* cb = buf0 + cur * TILE;
+        float* nb = buf0 + (cur ^ 1) * TILE;
+        wave_lds_sync();
         f32x4 o[G::MT];
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) o[mt] = bv[mt];
+        int chunk = 0;
+        auto mfma_chunk = [&]() {
+            if (chunk < G::KS / 4) {
+                const f32x4 bt = ld4(cb + j * G::S + 16 * chunk + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
 #pragma unroll
-        for (int a = 0; a < G::KS / 4; ++a)
+                for (int mt = 0; mt < G::MT; ++mt) {
+                    const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * chunk + 4 * q);  // W[16mt + j][..]
 #pragma unroll
-            for (int mt = 0; mt < G::MT; ++mt) {
-                // A operand W[16mt + j][fk(4a + i, q)] = W[16mt + j][16a + 4q + i]
-                const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * a + 4 * q);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) o[mt] = mfma(wa[i], acc[a][i], o[mt]);
-            }
-        if (valid) {
-#pragma unroll
-            for (int mt = 0; mt < G::MT; ++mt) {
-                f32x4 v = o[mt];
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) {
-                    float t = v[reg];
-                    if (flags & LG_F_RELU) t = fmaxf(t, 0.f);
-                    if (flags & LG_F_DROPOUT) t = lg_dropout(t, p_drop, dscale, seed, salt, r * D + 16 * mt + 4 * q + reg);
-                    v[reg] = t;
+                    for (int i = 0; i < 4; ++i) o[mt] = mfma(wa[i], bt[i], o[mt]);
                 }
-                st4(y + r * D + 16 * mt + 4 * q, v);
+                ++chunk;
             }
+        };
+        const int64_t next = tile + tr.stride;
+        if (next < tr.end) gather_tile<D, false>(g, x, nullptr, 1.f, next * kTileRows, R, N, lane, nb, mfma_chunk);
+        while (chunk < G::KS / 4) mfma_chunk();
+        const int64_t r0 = tile * kTileRows, r = r0 + j;
+#pragma unroll
+        for (int mt = 0; mt < G::MT; ++mt) {
+            f32x4 v = o[mt];
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float t = v[reg];
+                if (flags & LG_F_RELU) t = fmaxf(t, 0.f);
+                if (flags & LG_F_DROPOUT) t = lg_dropout(t, p_drop, dscale, key, r * D + 16 * mt + 4 * q + reg);
+                v[reg] = t;
+            }
+            o[mt] = v;
         }
+        wave_lds_sync();
+#pragma unroll
+        for (int mt = 0; mt < G::MT; ++mt) st4(cb + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_lds_sync();
+        store_tile<D>(cb, y, r0, R, lane);
     }
 }
 
 // ------------------------------------------------------------------ backward
 // dz = MASK_IN ? dy*scale_in*[y>0] : dy ; t = Ahat^T dz ; dx = t W ; dW += t^T x ; db += sum dz
 template <int D, bool MASK_IN, bool CSR_LDS>
-__global__ void __launch_bounds__(64 * kWaves)
+__global__ void __launch_bounds__(64 * kWaves, 2)
 k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
           const float* __restrict__ dy, const float* __restrict__ yv, const float* __restrict__ x,
           const float* __restrict__ W, float* __restrict__ dxo, float* __restrict__ slab, int64_t N, int64_t R,
           int64_t ntiles, int mask_out, float scale_in, float scale_out, int64_t csr_bytes) {
     using G = Geo<D>;
-    constexpr int SW = D + 4;               // W rows in LDS, conflict-free column reads
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    constexpr int SW = D + 4;  // W rows in LDS, conflict-free column reads
     constexpr int WBUF = 2 * kTileRows * G::S;
     constexpr int L = D * D + D;
     static_assert(kWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
@@ -222,7 +285,8 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
     float* lds = reinterpret_cast<float*>(smem + (CSR_LDS ? csr_bytes : 0));
     float* wl = lds + kWaves * WBUF;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    float* tl = lds + wave * WBUF;   // t tile [row][feature]
+    const int rl = lane / LPR, fg = lane % LPR;
+    float* tl = lds + wave * WBUF;      // t tile [row][feature], later dx
     float* xl = tl + kTileRows * G::S;  // x tile [row][feature]
     for (int i = threadIdx.x; i < D * D; i += blockDim.x) wl[(i / D) * SW + (i % D)] = W[i];
     __syncthreads();
@@ -232,54 +296,30 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
     for (int a = 0; a < G::MT; ++a)
 #pragma unroll
         for (int b = 0; b < G::MT; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 dbacc[G::A4];
-#pragma unroll
-    for (int a = 0; a < G::A4; ++a) dbacc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // features 4fg..4fg+3, summed over this lane's rows
 
     const TileRange tr = xcd_tiles(ntiles, wave, kWaves);
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
-        const int64_t r = tile * kTileRows + j;
-        const bool valid = r < R;
-        f32x4 t[G::A4];
-        gather_row<D, MASK_IN>(g, dy, yv, scale_in, r, valid, N, q, t);
-        f32x4 xv[G::A4];
+        const int64_t r0 = tile * kTileRows;
+        gather_tile<D, MASK_IN>(g, dy, yv, scale_in, r0, R, N, lane, tl);
+        // own rows (coalesced): dz for db, x for dW and the output mask
 #pragma unroll
-        for (int a = 0; a < G::A4; ++a) {
-            xv[a] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (valid) {
-                const int64_t off = r * D + 16 * a + 4 * q;
+        for (int k = 0; k < kTileRows / RPI; ++k) {
+            const int row = RPI * k + rl;
+            const int64_t r = r0 + row;
+            f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (r < R) {
+                const int64_t off = r * D + 4 * fg;
                 f32x4 dz = ld4(dy + off);
                 if constexpr (MASK_IN) {
                     const f32x4 m = ld4(yv + off);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) dz[i] = m[i] > 0.f ? dz[i] * scale_in : 0.f;
                 }
-                dbacc[a] += dz;
-                xv[a] = ld4(x + off);
+                dbacc += dz;
+                xv = ld4(x + off);
             }
-            st4(tl + j * G::S + 16 * a + 4 * q, t[a]);
-            st4(xl + j * G::S + 16 * a + 4 * q, xv[a]);
-        }
-        // dx^T[i][row] = sum_o W[o][i] t[row][o]  : A = W^T from LDS, B = t (lane-local)
-        f32x4 o[G::MT];
-#pragma unroll
-        for (int mt = 0; mt < G::MT; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-            const float bt = t[ks >> 2][ks & 3];
-#pragma unroll
-            for (int mt = 0; mt < G::MT; ++mt) o[mt] = mfma(wl[fk(ks, q) * SW + 16 * mt + j], bt, o[mt]);
-        }
-        if (valid) {
-#pragma unroll
-            for (int mt = 0; mt < G::MT; ++mt) {
-                f32x4 v = o[mt];
-                if (mask_out) {
-#pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) v[reg] = xv[mt][reg] > 0.f ? v[reg] * scale_out : 0.f;
-                }
-                st4(dxo + r * D + 16 * mt + 4 * q, v);
-            }
+            st4(xl + row * G::S + 4 * fg, xv);
         }
         wave_lds_sync();
         // dW[o][i] += sum_rows t[row][o] x[row][i]   (rows = 4q + kk on the K index)
@@ -297,16 +337,41 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
                 for (int ni = 0; ni < G::MT; ++ni) dw[mo][ni] = mfma(ta[mo], xb[ni], dw[mo][ni]);
         }
+        // dx^T[i][row] = sum_o W[o][i] t[row][o] : A = W^T (LDS), B = t tile (LDS)
+        f32x4 o[G::MT];
+#pragma unroll
+        for (int mt = 0; mt < G::MT; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < G::KS / 4; ++a) {
+            const f32x4 bt = ld4(tl + j * G::S + 16 * a + 4 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ko = 16 * a + 4 * q + i;
+#pragma unroll
+                for (int mt = 0; mt < G::MT; ++mt) o[mt] = mfma(wl[ko * SW + 16 * mt + j], bt[i], o[mt]);
+            }
+        }
+        if (mask_out) {
+#pragma unroll
+            for (int mt = 0; mt < G::MT; ++mt) {
+                const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
+            }
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int mt = 0; mt < G::MT; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_lds_sync();
+        store_tile<D>(tl, dxo, r0, R, lane);
         wave_lds_sync();
     }
 
     // ---- per-block reduction of dW / db (fixed wave order -> deterministic)
 #pragma unroll
-    for (int off = 1; off < 16; off <<= 1)
+    for (int off = LPR; off < 64; off <<= 1)
 #pragma unroll
-        for (int a = 0; a < G::A4; ++a)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dbacc[a][i] += __shfl_xor(dbacc[a][i], off);
+        for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
     __syncthreads();
     float* red = lds;  // reuse the tile buffers
     for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
@@ -320,11 +385,9 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg)
                         red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
-            if (j == 0)
+            if (lane < LPR)
 #pragma unroll
-                for (int a = 0; a < G::A4; ++a)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) red[D * D + 16 * a + 4 * q + i] += dbacc[a][i];
+                for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
         }
     }
     __syncthreads();
@@ -337,19 +400,20 @@ template <int D, bool CSR_LDS>
 __global__ void __launch_bounds__(256)
 k_spmm(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
        const float* __restrict__ x, float* __restrict__ y, int64_t N, int64_t R, int64_t ntiles) {
-    using G = Geo<D>;
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Csr g = CSR_LDS ? stage_csr(smem, rowptr, col, wgt, N) : Csr{rowptr, col, wgt};
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const TileRange tr = xcd_tiles(ntiles, wave, 4);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int rl = lane / LPR, fg = lane % LPR;
+    const TileRange tr = xcd_tiles(ntiles, wave, 4);  // a "tile" here is 2*RPI rows
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
-        const int64_t r = tile * kTileRows + j;
-        const bool valid = r < R;
-        f32x4 acc[G::A4];
-        gather_row<D, false>(g, x, nullptr, 1.f, r, valid, N, q, acc);
-        if (valid) {
+        const int64_t rb = tile * 2 * RPI;
+        f32x4 acc[2];
+        gather8<D, false>(g, x, nullptr, 1.f, rb, R, N, lane, acc);
 #pragma unroll
-            for (int a = 0; a < G::A4; ++a) st4(y + r * D + 16 * a + 4 * q, acc[a]);
+        for (int k = 0; k < 2; ++k) {
+            const int64_t r = rb + RPI * k + rl;
+            if (r < R) st4(y + r * D + 4 * fg, acc[k]);
         }
     }
 }
@@ -362,9 +426,10 @@ inline int64_t csr_lds_bytes(int64_t N, int64_t nnz_cap) {
     return b <= kCsrLdsMax ? b : 0;
 }
 
-int bwd_grid(int64_t ntiles) {
+int bwd_grid(int64_t ntiles, int64_t dyn_lds) {
     const int64_t want = ceil_div(ntiles, kWaves);
-    const int64_t cap = 2 * static_cast<int64_t>(lg_num_cus());
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, (160 * 1024) / dyn_lds));
+    const int64_t cap = per_cu * static_cast<int64_t>(lg_num_cus());
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(want, cap)));
 }
 
@@ -384,15 +449,20 @@ extern "C" int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float
     if (R == 0) return LG_OK;
     const int64_t ntiles = ceil_div(R, kTileRows);
     const int64_t csr = csr_lds_bytes(N, nnz_cap);
-    const int64_t dyn = csr + static_cast<int64_t>(sizeof(float)) * D * (D + 4);
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(8, (160 * 1024) / dyn));
-    const unsigned grid =
-        static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntiles, kWaves), per_cu * lg_num_cus())));
+    const int64_t dyn = csr + static_cast<int64_t>(sizeof(float)) * (D + 2 * kFwdWaves * kTileRows) * (D + 4);
+    const unsigned grid = static_cast<unsigned>(
+        std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntiles, kFwdWaves), lg_num_cus())));
     const float scale = (flags & LG_F_DROPOUT) ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
-#define LG_FWD(DD, CL)                                                                                             \
-    k_gcn_fwd<DD, CL><<<grid, 64 * kWaves, dyn, s>>>(rowptr, col, w, x, W, bias, y, N, R, ntiles, flags, dropout_p, \
-                                                    scale, seed, salt, csr)
+#define LG_FWD(DD, CL)                                                                                        \
+    do {                                                                                                      \
+        if (dyn > 64 * 1024 &&                                                                                \
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gcn_fwd<DD, CL>),                            \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn)) != hipSuccess) \
+            return LG_EHIP;                                                                                   \
+        k_gcn_fwd<DD, CL><<<grid, 64 * kFwdWaves, dyn, s>>>(rowptr, col, w, x, W, bias, y, N, R, ntiles, flags, \
+                                                        dropout_p, scale, seed, salt, csr);                   \
+    } while (0)
     if (D == 64) {
         if (csr) LG_FWD(64, true); else LG_FWD(64, false);
     } else {
@@ -410,7 +480,7 @@ extern "C" int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
-    const int64_t ntiles = ceil_div(R, kTileRows);
+    const int64_t ntiles = ceil_div(R, 2 * (64 / (D / 4)));
     const int64_t lds = csr_lds_bytes(N, nnz_cap);
     const int64_t per_cu = lds ? std::max<int64_t>(1, std::min<int64_t>(8, (160 * 1024) / lds)) : 8;
     const unsigned grid =
@@ -443,13 +513,13 @@ extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const f
     const int64_t R = B * N;
     hipStream_t s = lg_stream(stream);
     const int64_t ntiles = ceil_div(R, kTileRows);
-    const int grid = bwd_grid(ntiles);
     float* slab = static_cast<float*>(workspace);
     const int mask_out = (flags & LG_F_MASK_OUT) ? 1 : 0;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     const int64_t csr = csr_lds_bytes(N, nnz_cap);
     const int64_t tiles_lds = static_cast<int64_t>(sizeof(float)) *
                               (kWaves * 2 * kTileRows * (D + 4) + D * (D + 4));
+    const int grid = bwd_grid(ntiles, csr + tiles_lds);
 #define LG_BWD(DD, MI, CL)                                                                                        \
     do {                                                                                                          \
         const int64_t dyn = (CL ? csr : 0) + tiles_lds;                                                           \

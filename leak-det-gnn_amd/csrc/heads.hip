@@ -16,6 +16,7 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
             uint64_t seed, uint32_t salt) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
         const int64_t b = r / N, n = r - b * N;
         const int32_t s = slot[n];
@@ -23,7 +24,7 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = fmaxf(v[i], 0.f);
-            if (dropout) t = lg_dropout(t, p, scale, seed, salt, r * D + 4 * fg + i);
+            if (dropout) t = lg_dropout(t, p, scale, key, r * D + 4 * fg + i);
             v[i] = t;
         }
         st4(x0 + r * D + 4 * fg, v);

@@ -1,0 +1,134 @@
+"""Kernel micro-benchmark (GPU): times individual libleakgnn kernels in isolation with
+HIP events on the launch stream.  Used for tuning and under rocprofv3 --pmc.
+
+  python tools/kbench.py [--which gcn_fwd,gcn_bwd,spmm,edge_fwd,edge_bwd,gru_fwd,gru_bwd] [--B 256] [--iters 50]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO), str(REPO / "leak-det-gnn_amd")]
+import numpy as np
+import torch
+
+from models import _native as nat
+from models import ops
+from models.ops import GCNGraph, Incidence, check, ptr
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / iters  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,spmm,edge_fwd,edge_bwd,gru_fwd,gru_bwd")
+    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    lib = nat.load_library()
+    dev = torch.device("cuda:0")
+    g = np.load(REPO / "tests/golden/graph_ltown_a.npz")
+    ei = torch.from_numpy(g["edge_index"])
+    N, D, B = 661, 64, args.B
+    graph = GCNGraph.build(ei, N, dev)
+    inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), N, dev)
+    P = inc.num_pipes
+    st = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(B, N, D, device=dev)
+    y = torch.empty_like(x)
+    W = torch.randn(D, D, device=dev) / 8
+    bias = torch.randn(D, device=dev)
+    res = {}
+    E1 = graph.nnz_cap
+    fwd_bytes = 8 * B * N * D + 4 * (N + 1) + 8 * E1
+    which = args.which.split(",")
+    if "gcn_fwd" in which:
+        f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
+                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU, 0.0, 0, 0, st), "fwd")
+        t = timeit(f, args.iters)
+        res["gcn_fwd"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    if "gcn_fwd_train" in which:
+        f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
+                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT, 0.1,
+                                         123, 1, st), "fwd")
+        t = timeit(f, args.iters)
+        res["gcn_fwd_train"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    if "spmm" in which:
+        f = lambda: check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, N, D, E1,
+                                      st), "spmm")
+        t = timeit(f, args.iters)
+        res["spmm"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    if "gcn_bwd" in which:
+        dy = torch.randn_like(x)
+        yy = torch.relu(torch.randn_like(x))
+        dx = torch.empty_like(x)
+        dW = torch.empty(D, D, device=dev)
+        db = torch.empty(D, device=dev)
+        ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
+        f = lambda: check(lib.lg_gcn_bwd(ptr(graph.rowptr_t), ptr(graph.col_t), ptr(graph.w_t), ptr(dy), ptr(yy),
+                                         ptr(x), ptr(W), ptr(dx), ptr(dW), ptr(db), B, N, D, E1,
+                                         nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), st), "bwd")
+        t = timeit(f, args.iters)
+        res["gcn_bwd"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
+    if "edge_fwd" in which or "edge_bwd" in which:
+        W1 = torch.randn(128, 3 * D, device=dev) / 16
+        b1 = torch.randn(128, device=dev)
+        W2 = torch.randn(1, 128, device=dev) / 8
+        b2 = torch.randn(1, device=dev)
+        lo = torch.empty(B, P, device=dev)
+        if "edge_fwd" in which:
+            f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), B,
+                                                   N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, st), "edge fwd")
+            t = timeit(f, args.iters)
+            res["edge_fwd"] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
+        if "edge_bwd" in which:
+            dl = torch.randn(B, P, device=dev)
+            dpipe = torch.empty(B, P, 2, D, device=dev)
+            dW1, db1, dW2, db2 = (torch.empty_like(t) for t in (W1, b1, W2, b2))
+            ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=dev, dtype=torch.uint8)
+            f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(dl),
+                                                   ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
+                                                   nat.LG_F_DROPOUT, 0.1, 5, 101, ptr(ws), st), "edge bwd")
+            t = timeit(f, args.iters)
+            res["edge_bwd"] = {"us": t, "TFLOPs": 3 * 2 * B * P * 3 * D * 128 / t / 1e6}
+    if "gru_fwd" in which or "gru_bwd" in which:
+        S, L = 29, 36
+        r = torch.randn(B, L, S, device=dev)
+        tf = torch.randn(B, L, 9, device=dev)
+        wih = torch.randn(192, 10, device=dev) / 4
+        whh = torch.randn(192, 64, device=dev) / 8
+        bih, bhh = torch.randn(192, device=dev) / 4, torch.randn(192, device=dev) / 4
+        hs = torch.empty(L, B * S, 64, device=dev)
+        hl = torch.empty(B * S, 64, device=dev)
+        f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(hl), B,
+                                         L, S, 10, 64, st), "gru fwd")
+        t = timeit(f, args.iters)
+        flops = 2 * B * S * L * 192 * (64 + 10)
+        res["gru_fwd"] = {"us": t, "TFLOPs": flops / t / 1e6}
+        if "gru_bwd" in which:
+            dh = torch.randn(B * S, 64, device=dev)
+            dws = [torch.empty_like(t) for t in (wih, whh, bih, bhh)]
+            ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, 10)), device=dev, dtype=torch.uint8)
+            f = lambda: check(lib.lg_gru_bwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(dh),
+                                             None, ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), B, L, S, 10, 64,
+                                             ptr(ws), st), "gru bwd")
+            t = timeit(f, args.iters)
+            res["gru_bwd"] = {"us": t, "TFLOPs": 3 * flops / t / 1e6}
+    for k, v in res.items():
+        print(k, json.dumps({a: round(b, 2) for a, b in v.items()}))
+
+
+if __name__ == "__main__":
+    main()
