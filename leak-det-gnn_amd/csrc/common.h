@@ -51,5 +51,28 @@ __device__ __forceinline__ float lg_dropout(float v, float p, float scale, uint3
     return lg_keep(key, idx, p) ? v * scale : 0.0f;
 }
 
+// Division by a runtime divisor that is fixed per launch (N nodes, P pipes, S sensors):
+// magic multiplier computed on the host (Granlund & Montgomery 1994, round-up
+// variant), so a row index splits into (window, node) with one v_mul_hi_u32 and
+// three cheap ops instead of a ~130-instruction 64-bit division.  Exact for every
+// dividend n < 2^32; kernels using it require B*N < 2^31 (checked at the API).
+struct lg_fastdiv {
+    uint32_t d, m, s1, s2;
+};
+
+static inline lg_fastdiv lg_make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (uint64_t{1} << l) < d) ++l;  // l = ceil(log2 d)
+    const uint64_t m = ((uint64_t{1} << 32) * ((uint64_t{1} << l) - d)) / d + 1;
+    return lg_fastdiv{d, static_cast<uint32_t>(m), l < 1 ? l : 1u, l > 0 ? l - 1 : 0u};
+}
+
+__device__ __forceinline__ uint32_t lg_div(uint32_t n, const lg_fastdiv& f) {
+    const uint32_t t = __umulhi(n, f.m);
+    return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
+constexpr int64_t kLgMaxRows = int64_t{1} << 31;  // row-index space of the fast-division kernels
+
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }

@@ -50,7 +50,8 @@ struct EG {
 // Gather the two endpoint rows of 16 pipe rows into ft[16][FS] (u at [0,D), v at [D,2D)).
 template <int D>
 __device__ __forceinline__ void gather_tile(const int64_t* __restrict__ ends, const float* __restrict__ h,
-                                            float* __restrict__ ft, int64_t row0, int64_t BP, int64_t P, int64_t N) {
+                                            float* __restrict__ ft, int64_t row0, int64_t BP, const lg_fastdiv& fdP,
+                                            int64_t N) {
     using G = EG<D>;
     const int t = threadIdx.x;
     if (t < TR * 2 * G::F4) {
@@ -58,9 +59,9 @@ __device__ __forceinline__ void gather_tile(const int64_t* __restrict__ ends, co
         const int64_t gr = row0 + row;
         f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
         if (gr < BP) {
-            const int64_t b = gr / P, p = gr - b * P;
+            const uint32_t b = lg_div(static_cast<uint32_t>(gr), fdP), p = static_cast<uint32_t>(gr) - b * fdP.d;
             const int64_t node = ends[2 * p + side];
-            v = ld4(h + (b * N + node) * D + 4 * f4);
+            v = ld4(h + (static_cast<int64_t>(b) * N + node) * D + 4 * f4);
         }
         st4(ft + row * G::FS + side * D + 4 * f4, v);
     }
@@ -102,7 +103,7 @@ template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-           float* __restrict__ logit, int64_t N, int64_t P, int64_t BP, int64_t ntiles, int dropout, float p_drop,
+           float* __restrict__ logit, int64_t N, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout, float p_drop,
            float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
     __shared__ __attribute__((aligned(16))) float ft[TR * G::FS];
@@ -121,7 +122,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, P, N);
+        gather_tile<D>(ends, h, ft, row0, BP, fdP, N);
         __syncthreads();
         const f32x4 acc = hidden_tile<D>(ft, aw, b1v, j, q);
         float s = 0.f;
@@ -151,7 +152,7 @@ template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ dlogit,
-           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t N, int64_t P,
+           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t N, lg_fastdiv fdP,
            int64_t BP, int64_t ntiles, int dropout, float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
     constexpr int HS = HID + 4;
@@ -187,7 +188,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, P, N);
+        gather_tile<D>(ends, h, ft, row0, BP, fdP, N);
         const bool rv = row0 + j < BP;
         const float dl = rv ? dlogit[row0 + j] : 0.f;
         __syncthreads();
@@ -310,15 +311,17 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     const int64_t BP = B * P;
     if (BP == 0) return LG_OK;
     if (!ends || !h || !w1 || !b1 || !w2 || !b2 || !logits) return LG_EINVAL;
+    if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
     const int64_t ntiles = cdiv(BP, TR);
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ntiles, 4LL * lg_num_cus()));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     if (D == 64)
-        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, P, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     else
-        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, P, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
@@ -343,6 +346,8 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     if (!h || !w1 || !b1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !workspace) return LG_EINVAL;
     const int64_t BP = B * P;
     if (BP > 0 && (!ends || !dlogits || !dpipe)) return LG_EINVAL;
+    if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(std::max<int64_t>(P, 1)));
     const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), TR);
     const int grid = bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
@@ -354,10 +359,10 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else if (D == 64) {
-        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, P, BP, ntiles, dropout,
+        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     } else {
-        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, P, BP, ntiles, dropout,
+        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     }
     LG_RET_IF_LAUNCH_FAILED();

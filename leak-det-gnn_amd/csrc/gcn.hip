@@ -1,33 +1,42 @@
-// K5+K6+K7: fused GCN layer forward / backward on gfx950.
+// K5+K6+K7: fused GCN layer forward / backward and the plain propagate, gfx950.
 //
-// Layout: node features fp32 [B][N][D], one single-graph CSR shared by all B
-// windows (row r = b*N + n gathers rows b*N + col[e]).  When the CSR is small
-// (L-TOWN-A: 20 KB) every workgroup stages it in LDS once and then walks it from
-// there; large graphs (C5, 100k nodes) read it from L2.
+// Layout: node features fp32 [B][N][D] (row r = b*N + n), one single-graph CSR
+// (rowptr / col / w, self loop last in each row) shared by all B windows: row r
+// gathers rows b*N + col[e].  When the CSR fits (L-TOWN-A: 20 KB) every workgroup
+// stages it in LDS once; large graphs (C5, 100k nodes) read it through L2.
 //
-// Work unit: a 16-row "wave tile" owned by ONE 64-lane wavefront.  The layer is
-// computed transposed, y^T (D x 16 rows) = W (D x D) * (Ahat x)^T, on
-// v_mfma_f32_16x16x4_f32 (exact fp32).  With the K index permuted as
-// k = fk(ks, q) = 16*(ks>>2) + 4q + (ks&3), lane (j, q) of the wave gathers exactly
-// the B-operand fragment it needs — features {16a + 4q .. 16a + 4q + 3} of row j —
-// as float4 loads of the neighbour rows, and the accumulator comes out in the same
-// per-lane layout, so the forward needs no LDS for operands or for the store:
-//   1. CSR segmented reduce of row j over its entries in order (fp32 fma), 4 float4
-//      loads per neighbour per lane (D = 64), neighbour rows are L2-resident;
-//   2. D/16 x D/4 MFMAs with W held in registers (A operand), bias as the initial
-//      accumulator;
-//   3. ReLU / dropout epilogue and float4 row stores (each row's 256 B written by
-//      four lanes of one instruction group).
-// Waves never wait for each other inside the tile loop.
+// Work unit: a 16-row "wave tile" owned by one wavefront, tiles dealt XCD-aware
+// (xcd_tiles) to a persistent grid.  Per tile:
+//   gather   16 lanes per row (D = 64), lane = one float4 of features; all 16 rows
+//            in one round with U neighbours each, so K*U float4 loads per lane are
+//            in flight; neighbour rows are read with buffer loads whose offset is
+//            pushed out of range for padded slots (the hardware returns 0 and
+//            issues no memory request), so the loop has no branches and all CSR
+//            reads of a round are issued before any row load;
+//   MFMA     the layer is computed transposed, y^T (D x 16) = W (D x D) (Ahat x)^T
+//            on v_mfma_f32_16x16x4_f32 (exact fp32); A = W from LDS, B = the
+//            gathered tile from LDS; the k-chunks of tile i run between the row
+//            loads of tile i+1 and their use (software pipeline, one LDS tile per
+//            wave: the next tile is held in registers until the MFMAs are done);
+//   epilogue bias (initial accumulator), ReLU as max(t, floor), counter-hash
+//            dropout, then rows are written back whole through the LDS tile.
+// Backward: dz = MASK_IN ? dy*scale*[y>0] : dy; t = Ahat^T dz (transposed CSR);
+// dx = t W (MFMA), dW = t^T x and db = sum dz accumulated per wave, reduced per
+// block in a fixed order, then across blocks by the shared slab reducer.
+// All offsets are 32-bit byte offsets: the API splits launches over windows so that
+// each launch's [rows][D] tensors stay below 4 GiB.
 #include <algorithm>
 #include "common.h"
 #include "reduce.h"
 
 namespace {
 
-constexpr int kWaves = 8;      // waves per workgroup
 constexpr int kTileRows = 16;  // rows per wave tile (MFMA N)
+constexpr int kBwdWaves = 8;
+constexpr int kSpmmWaves = 4;
 constexpr int64_t kCsrLdsMax = 48 * 1024;
+constexpr uint32_t kOob = 0xFFFFFFF0u;             // beyond every descriptor: loads read 0, stores drop
+constexpr int64_t kMaxLaunchBytes = 0xFFFFFF00LL;  // per-launch tensor size limit (32-bit offsets)
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -39,15 +48,39 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q + (ks & 3); }
 
 template <int D>
 struct Geo {
-    static constexpr int A4 = D / 16;  // float4 groups per lane per row
-    static constexpr int KS = D / 4;   // k-steps of one contraction
-    static constexpr int MT = D / 16;  // 16-row output tiles
-    static constexpr int S = D + 4;    // padded LDS row stride (floats)
+    static constexpr int LPR = D / 4;           // lanes per row in the gather
+    static constexpr int RPI = 64 / LPR;        // rows per wave instruction
+    static constexpr int K = kTileRows / RPI;   // row groups per tile
+    static constexpr int KS = D / 4;            // k-steps of one contraction
+    static constexpr int CH = KS / 4;           // k-chunks (4 k-steps, one float4 of B)
+    static constexpr int MT = D / 16;           // 16-row output tiles
+    static constexpr int S = D + 4;             // padded LDS row stride (floats)
+    static constexpr int TILE = kTileRows * S;  // floats per LDS tile
 };
+
+// fp32 rows [rows][D] behind a buffer descriptor (built from kernel arguments, so it
+// lives in SGPRs).  ok == false turns the access into a no-op (load returns 0).
+template <int D>
+struct Rows {
+    __amdgpu_buffer_rsrc_t rs;
+    __device__ __forceinline__ f32x4 ld(uint32_t row, int fg, bool ok) const {
+        const uint32_t off = ok ? row * (4u * D) + 16u * fg : kOob;
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+    __device__ __forceinline__ void st(uint32_t row, int fg, bool ok, f32x4 v) const {
+        const uint32_t off = ok ? row * (4u * D) + 16u * fg : kOob;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rs,
+                                               off, 0, 0);
+    }
+};
+template <int D>
+__device__ __forceinline__ Rows<D> rows_of(const float* p, uint32_t rows) {
+    return Rows<D>{__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0),
+                                                     static_cast<int>(rows * (4u * D)), 0x00020000)};
+}
 
 // XCD-aware tile schedule.  Workgroups are dealt round-robin over the 8 XCDs, so
 // blocks b and b+8 share one L2 (MI355X_MICROARCH.md, dispatch/XCD placement).  The
@@ -74,222 +107,265 @@ struct Csr {
     const float* w;
 };
 
-// Stage rowptr / col / w into LDS (dynamic shared memory) for the whole block.
-__device__ __forceinline__ Csr stage_csr(char* smem, const int32_t* __restrict__ rowptr,
-                                         const int32_t* __restrict__ col, const float* __restrict__ w, int64_t N) {
-    int32_t* srp = reinterpret_cast<int32_t*>(smem);
-    const int32_t nnz = rowptr[N];
-    int32_t* scol = srp + ((N + 1 + 3) & ~3LL);
-    float* sw = reinterpret_cast<float*>(scol + ((nnz + 3) & ~3));
-    for (int64_t i = threadIdx.x; i <= N; i += blockDim.x) srp[i] = rowptr[i];
-    for (int32_t i = threadIdx.x; i < nnz; i += blockDim.x) {
-        scol[i] = col[i];
-        sw[i] = w[i];
-    }
-    __syncthreads();
-    return Csr{srp, scol, sw};
+// CSR words in LDS, contiguous: rowptr [0, N+1), col [N+1, N+1+nnz), w after col.
+inline int64_t csr_lds_bytes(int64_t N, int64_t nnz_cap) {
+    const int64_t b = 4 * (N + 1 + 2 * nnz_cap);
+    return b <= kCsrLdsMax ? b : 0;
 }
 
-// Coalesced row gather ("16 lanes per row"): lane (rl = lane>>4, fg = lane&15) owns
-// feature float4 fg of rows 4k + rl of an 8-row group; each wave-instruction reads
-// four whole 4*D-byte rows.  Two rows x two neighbours in flight per lane.  Row r sums
-// w_e * src[b*N + col_e] over its CSR entries in order (fp32 fma).  MASK: gathered
-// values are dy * scale * [m > 0] (ReLU/dropout backward of the gathered tensor).
-// Measured on MI355X (tools/spmm_lab.hip, L-TOWN-A shape, B = 256): 4.3-4.5 TB/s for
-// this layout vs 3.0 TB/s for quarter-row lanes; stream copy 6.4 TB/s.
+// Stage the CSR into LDS: every thread issues all of its loads (clamped indices, no
+// branches) before its first LDS store, so the prologue costs one memory round trip
+// per 8*blockDim words instead of one per word-loop iteration.  Caller syncs.
+__device__ __forceinline__ Csr stage_csr(uint32_t* s, const int32_t* __restrict__ rowptr,
+                                         const int32_t* __restrict__ col, const float* __restrict__ w, uint32_t N) {
+    const uint32_t n1 = N + 1, nnz = static_cast<uint32_t>(rowptr[N]), total = n1 + 2 * nnz;
+    const uint32_t* rp = reinterpret_cast<const uint32_t*>(rowptr);
+    const uint32_t* cp = reinterpret_cast<const uint32_t*>(col);
+    const uint32_t* wp = reinterpret_cast<const uint32_t*>(w);
+    constexpr int PER = 8;
+    for (uint32_t base = 0; base < total; base += blockDim.x * PER) {
+        uint32_t v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = min(base + u * blockDim.x + threadIdx.x, total - 1);
+            const uint32_t* p = i < n1 ? rp + i : (i < n1 + nnz ? cp + (i - n1) : wp + (i - n1 - nnz));
+            v[u] = *p;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const uint32_t i = base + u * blockDim.x + threadIdx.x;
+            if (i < total) s[i] = v[u];
+        }
+    }
+    return Csr{reinterpret_cast<const int32_t*>(s), reinterpret_cast<const int32_t*>(s + n1),
+               reinterpret_cast<const float*>(s + n1 + nnz)};
+}
+
 struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
+    __device__ __forceinline__ void operator()(int, int) const {}
 };
 
-template <int D, bool MASK, typename Hook = NoHook>
-__device__ __forceinline__ void gather8(const Csr& g, const float* __restrict__ src, const float* __restrict__ msk,
-                                        float mscale, int64_t rbase, int64_t R, int64_t N, int lane,
-                                        f32x4 (&acc)[2], Hook&& hook = Hook{}) {
-    constexpr int LPR = D / 4;  // lanes per row
-    constexpr int RPI = 64 / LPR;  // rows per instruction
-    const int rl = lane / LPR, fg = lane % LPR;
-    int e0[2], e1[2];
-    int64_t off[2];
+// Whole-tile gather: acc[k] = row (r0 + RPI*k + rl), features 4fg..4fg+3, summed over
+// the row's CSR entries in order (fp32 fma; w * v[s] per entry).  MASK: gathered values
+// are v * mscale * [m > 0] (ReLU / dropout backward of the gathered tensor).  The trip
+// count is the tile's wave-uniform max degree so hook(round, rounds) — independent
+// work such as the previous tile's MFMAs — runs with every lane active, between the
+// issue of a round's loads and their use.
+template <int D, bool MASK, int U, typename Hook = NoHook>
+__device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const Rows<D>& msk, float mscale,
+                                         uint32_t r0, uint32_t R, const lg_fastdiv& fdN, int lane,
+                                         f32x4 (&acc)[Geo<D>::K], Hook&& hook = Hook{}) {
+    using G = Geo<D>;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    int e0[G::K], e1[G::K];
+    uint32_t base[G::K];
     int maxd = 0;
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < G::K; ++k) {
         acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int64_t r = rbase + RPI * k + rl;
-        if (r < R) {
-            const int64_t b = r / N, n = r - b * N;
-            e0[k] = g.rp[n];
-            e1[k] = g.rp[n + 1];
-            off[k] = b * N * D + 4 * fg;
-        } else {
-            e0[k] = e1[k] = 0;
-            off[k] = 4 * fg;
-        }
+        const uint32_t r = r0 + G::RPI * k + rl;
+        const bool valid = r < R;
+        const uint32_t rr = valid ? r : 0u;
+        const uint32_t n = rr - lg_div(rr, fdN) * fdN.d;
+        e0[k] = g.rp[n];
+        e1[k] = valid ? g.rp[n + 1] : e0[k];
+        base[k] = rr - n;
         maxd = max(maxd, e1[k] - e0[k]);
     }
-    // wave-uniform trip count: the hook (MFMA) must run with every lane active
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o));
     maxd = __builtin_amdgcn_readfirstlane(maxd);
-    for (int d = 0; d < maxd; d += 2) {
-        f32x4 v[2][2];
-        float ww[2][2];
+    const int rounds = (maxd + U - 1) / U;
+    for (int rd = 0; rd < rounds; ++rd) {
+        int32_t s[G::K][U];
+        float ww[G::K][U];
+        bool ok[G::K][U];
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < G::K; ++k)
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int e = e0[k] + d + u;
-                const bool ok = e < e1[k];
-                const int32_t s = ok ? g.col[e] : 0;
-                ww[k][u] = ok ? g.w[e] : 0.f;
-                const int64_t o = off[k] + static_cast<int64_t>(s) * D;
-                v[k][u] = ld4(src + o);
-                if constexpr (MASK) {
-                    const f32x4 m = ld4(msk + o);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v[k][u][i] = m[i] > 0.f ? v[k][u][i] * mscale : 0.f;
-                }
+            for (int u = 0; u < U; ++u) {
+                const int e = e0[k] + rd * U + u;
+                ok[k][u] = e < e1[k];
+                const int ei = ok[k][u] ? e : 0;  // maxd > 0 implies nnz > 0, so entry 0 exists
+                s[k][u] = g.col[ei];
+                ww[k][u] = g.w[ei];
             }
-        hook();  // independent work (e.g. the previous tile's MFMAs) under the load latency
+        f32x4 v[G::K][U], m[G::K][U];
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < G::K; ++k)
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < U; ++u) {
+                v[k][u] = src.ld(base[k] + static_cast<uint32_t>(s[k][u]), fg, ok[k][u]);
+                if constexpr (MASK) m[k][u] = msk.ld(base[k] + static_cast<uint32_t>(s[k][u]), fg, ok[k][u]);
+            }
+        hook(rd, rounds);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(ww[k][u], v[k][u][i], acc[k][i]);
+        for (int k = 0; k < G::K; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                f32x4 t = v[k][u];
+                if constexpr (MASK) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) t[i] = m[k][u][i] > 0.f ? t[i] * mscale : 0.f;
+                }
+                const float wv = ok[k][u] ? ww[k][u] : 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(wv, t[i], acc[k][i]);
+            }
     }
 }
 
-// Gather the 16-row tile at r0 into tl[row][feature] (row stride S).
-template <int D, bool MASK, typename Hook = NoHook>
-__device__ __forceinline__ void gather_tile(const Csr& g, const float* __restrict__ src,
-                                            const float* __restrict__ msk, float mscale, int64_t r0, int64_t R,
-                                            int64_t N, int lane, float* __restrict__ tl, Hook&& hook = Hook{}) {
-    constexpr int LPR = D / 4, RPI = 64 / LPR;
-    const int rl = lane / LPR, fg = lane % LPR;
-#pragma unroll
-    for (int pass = 0; pass < kTileRows / (2 * RPI); ++pass) {
-        f32x4 acc[2];
-        gather8<D, MASK>(g, src, msk, mscale, r0 + pass * 2 * RPI, R, N, lane, acc, hook);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) st4(tl + (pass * 2 * RPI + RPI * k + rl) * Geo<D>::S + 4 * fg, acc[k]);
-    }
-}
-
-// Store the 16-row tile tl[row][feature] to dst rows r0.. as whole rows.
 template <int D>
-__device__ __forceinline__ void store_tile(const float* __restrict__ tl, float* __restrict__ dst, int64_t r0,
-                                           int64_t R, int lane) {
-    constexpr int LPR = D / 4, RPI = 64 / LPR;
-    const int rl = lane / LPR, fg = lane % LPR;
+__device__ __forceinline__ void put_tile(float* __restrict__ tl, const f32x4 (&acc)[Geo<D>::K], int lane) {
+    using G = Geo<D>;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
 #pragma unroll
-    for (int k = 0; k < kTileRows / RPI; ++k) {
-        const int row = RPI * k + rl;
-        if (r0 + row < R) st4(dst + (r0 + row) * D + 4 * fg, ld4(tl + row * Geo<D>::S + 4 * fg));
+    for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+}
+
+// Write the 16-row LDS tile tl[row][feature] to rows r0.. as whole rows.
+template <int D>
+__device__ __forceinline__ void store_tile(const float* __restrict__ tl, const Rows<D>& dst, uint32_t r0, uint32_t R,
+                                           int lane) {
+    using G = Geo<D>;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    f32x4 v[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) v[k] = ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg);
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) {
+        const uint32_t r = r0 + G::RPI * k + rl;
+        dst.st(r, fg, r < R, v[k]);
     }
 }
 
 // ------------------------------------------------------------------ forward
-// y^T = W (Ahat x)^T: B operand = the gathered tile (LDS), A operand = W (LDS).
-// Software pipeline per wave: the tile is double-buffered in LDS and the MFMA
-// chunks of tile i run between issuing and consuming each gather round of tile
-// i+1, so the matrix pipe works under the memory latency of the next gather.
-constexpr int kFwdWaves = 12;  // one 768-thread workgroup per CU: 12 x 8.7 KB tiles + W + CSR in LDS
-
-template <int D, bool CSR_LDS>
-__global__ void __launch_bounds__(64 * kFwdWaves)
+template <int D, int NW, bool CSR_LDS, bool DROP>
+__global__ void __launch_bounds__(64 * NW)
 k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
           const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-          float* __restrict__ y, int64_t N, int64_t R, int64_t ntiles, int flags, float p_drop, float dscale,
-          uint64_t seed, uint32_t salt, int64_t csr_bytes) {
+          float* __restrict__ y, uint32_t N, lg_fastdiv fdN, uint32_t R, int64_t ntiles, float relu_floor,
+          float p_drop, float dscale, uint64_t seed, uint32_t salt, uint64_t row_offset, int csr_words) {
     using G = Geo<D>;
-    constexpr int TILE = kTileRows * G::S;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* wl = reinterpret_cast<float*>(smem + (CSR_LDS ? csr_bytes : 0));  // W [out][in], stride S
-    float* tiles = wl + D * G::S;
-    for (int i = threadIdx.x; i < D * D / 4; i += blockDim.x)
-        st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), ld4(W + 4 * i));
-    const Csr g = CSR_LDS ? stage_csr(smem, rowptr, col, wgt, N) : Csr{rowptr, col, wgt};
-    if (!CSR_LDS) __syncthreads();
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    float* buf0 = tiles + wave * 2 * TILE;
-    const uint32_t key = lg_dropout_key(seed, salt);
-    f32x4 bv[G::MT];
-#pragma unroll
-    for (int mt = 0; mt < G::MT; ++mt)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) bv[mt][reg] = (flags & LG_F_BIAS) ? bias[16 * mt + 4 * q + reg] : 0.f;
+    float* wl = reinterpret_cast<float*>(smem) + (CSR_LDS ? ((csr_words + 3) & ~3) : 0);  // W [out][in], stride S
+    float* bl = wl + D * G::S;                                                          // bias [D]
+    float* tiles = bl + D;
+    const Rows<D> xs = rows_of<D>(x, R), ys = rows_of<D>(y, R);
 
-    const TileRange tr = xcd_tiles(ntiles, wave, kFwdWaves);
-    if (tr.first < tr.end) gather_tile<D, false>(g, x, nullptr, 1.f, tr.first * kTileRows, R, N, lane, buf0);
-    int cur = 0;
-    for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride, cur ^= 1) {
-        float* cb = buf0 + cur * TILE;
-        float* nb = buf0 + (cur ^ 1) * TILE;
+    // prologue: W and bias loads first, then the CSR staging, then the LDS stores
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * NW - 1) / (64 * NW);
+    f32x4 wv[WPER];
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * NW + threadIdx.x, W4 - 1));
+    const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+    const Csr g = CSR_LDS ? stage_csr(reinterpret_cast<uint32_t*>(smem), rowptr, col, wgt, N)
+                          : Csr{rowptr, col, wgt};
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+        const int i = u * 64 * NW + threadIdx.x;
+        if (i < W4) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), wv[u]);
+    }
+    if (threadIdx.x < D) bl[threadIdx.x] = bb;
+    __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    float* tl = tiles + wave * G::TILE;
+    const uint32_t key = lg_dropout_key(seed, salt);
+
+    const TileRange tr = xcd_tiles(ntiles, wave, NW);
+    f32x4 acc[G::K];
+    if (tr.first < tr.end) {
+        gather16<D, false, 2>(g, xs, xs, 1.f, static_cast<uint32_t>(tr.first * kTileRows), R, fdN, lane, acc);
+        put_tile<D>(tl, acc, lane);
+    }
+    for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
         wave_lds_sync();
         f32x4 o[G::MT];
 #pragma unroll
-        for (int mt = 0; mt < G::MT; ++mt) o[mt] = bv[mt];
+        for (int mt = 0; mt < G::MT; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
         int chunk = 0;
         auto mfma_chunk = [&]() {
-            if (chunk < G::KS / 4) {
-                const f32x4 bt = ld4(cb + j * G::S + 16 * chunk + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
+            const f32x4 bt = ld4(tl + j * G::S + 16 * chunk + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
 #pragma unroll
-                for (int mt = 0; mt < G::MT; ++mt) {
-                    const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * chunk + 4 * q);  // W[16mt + j][..]
+            for (int mt = 0; mt < G::MT; ++mt) {
+                const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * chunk + 4 * q);  // W[16mt + j][..]
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) o[mt] = mfma(wa[i], bt[i], o[mt]);
-                }
-                ++chunk;
+                for (int i = 0; i < 4; ++i) o[mt] = mfma(wa[i], bt[i], o[mt]);
             }
+            ++chunk;
+        };
+        // spread the k-chunks over the next tile's gather rounds
+        auto hook = [&](int rd, int rounds) {
+            const int target = (G::CH * (rd + 1) + rounds - 1) / rounds;
+            while (chunk < target) mfma_chunk();
         };
         const int64_t next = tile + tr.stride;
-        if (next < tr.end) gather_tile<D, false>(g, x, nullptr, 1.f, next * kTileRows, R, N, lane, nb, mfma_chunk);
-        while (chunk < G::KS / 4) mfma_chunk();
-        const int64_t r0 = tile * kTileRows, r = r0 + j;
+        const bool more = next < tr.end;
+        if (more)
+            gather16<D, false, 2>(g, xs, xs, 1.f, static_cast<uint32_t>(next * kTileRows), R, fdN, lane, acc, hook);
+        while (chunk < G::CH) mfma_chunk();
+
+        const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
+        const uint64_t rg = row_offset + r0 + j;  // global row: the dropout stream ignores launch splits
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) {
-            f32x4 v = o[mt];
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                float t = v[reg];
-                if (flags & LG_F_RELU) t = fmaxf(t, 0.f);
-                if (flags & LG_F_DROPOUT) t = lg_dropout(t, p_drop, dscale, key, r * D + 16 * mt + 4 * q + reg);
-                v[reg] = t;
+                float t = fmaxf(o[mt][reg], relu_floor);
+                if constexpr (DROP) t = lg_dropout(t, p_drop, dscale, key, rg * D + 16 * mt + 4 * q + reg);
+                o[mt][reg] = t;
             }
-            o[mt] = v;
         }
         wave_lds_sync();
 #pragma unroll
-        for (int mt = 0; mt < G::MT; ++mt) st4(cb + j * G::S + 16 * mt + 4 * q, o[mt]);
+        for (int mt = 0; mt < G::MT; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
         wave_lds_sync();
-        store_tile<D>(cb, y, r0, R, lane);
+        store_tile<D>(tl, ys, r0, R, lane);
+        if (more) {
+            wave_lds_sync();
+            put_tile<D>(tl, acc, lane);
+        }
     }
 }
 
 // ------------------------------------------------------------------ backward
 // dz = MASK_IN ? dy*scale_in*[y>0] : dy ; t = Ahat^T dz ; dx = t W ; dW += t^T x ; db += sum dz
 template <int D, bool MASK_IN, bool CSR_LDS>
-__global__ void __launch_bounds__(64 * kWaves, 2)
+__global__ void __launch_bounds__(64 * kBwdWaves, 2)
 k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
           const float* __restrict__ dy, const float* __restrict__ yv, const float* __restrict__ x,
-          const float* __restrict__ W, float* __restrict__ dxo, float* __restrict__ slab, int64_t N, int64_t R,
-          int64_t ntiles, int mask_out, float scale_in, float scale_out, int64_t csr_bytes) {
+          const float* __restrict__ W, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N, lg_fastdiv fdN,
+          uint32_t R, int64_t ntiles, int mask_out, float scale_in, float scale_out, int csr_words, int accumulate) {
     using G = Geo<D>;
-    constexpr int LPR = D / 4, RPI = 64 / LPR;
     constexpr int SW = D + 4;  // W rows in LDS, conflict-free column reads
-    constexpr int WBUF = 2 * kTileRows * G::S;
+    constexpr int WBUF = 2 * G::TILE;
     constexpr int L = D * D + D;
-    static_assert(kWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
+    static_assert(kBwdWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Csr g = CSR_LDS ? stage_csr(smem, rowptr, col, wgt, N) : Csr{rowptr, col, wgt};
-    float* lds = reinterpret_cast<float*>(smem + (CSR_LDS ? csr_bytes : 0));
-    float* wl = lds + kWaves * WBUF;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / LPR, fg = lane % LPR;
-    float* tl = lds + wave * WBUF;      // t tile [row][feature], later dx
-    float* xl = tl + kTileRows * G::S;  // x tile [row][feature]
-    for (int i = threadIdx.x; i < D * D; i += blockDim.x) wl[(i / D) * SW + (i % D)] = W[i];
+    const Rows<D> dys = rows_of<D>(dy, R), ms = rows_of<D>(MASK_IN ? yv : dy, R), xs = rows_of<D>(x, R),
+                  dxs = rows_of<D>(dxo, R);
+    float* lds = reinterpret_cast<float*>(smem) + (CSR_LDS ? ((csr_words + 3) & ~3) : 0);
+    float* wl = lds + kBwdWaves * WBUF;
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kBwdWaves - 1) / (64 * kBwdWaves);
+    f32x4 wv[WPER];
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kBwdWaves + threadIdx.x, W4 - 1));
+    const Csr g = CSR_LDS ? stage_csr(reinterpret_cast<uint32_t*>(smem), rowptr, col, wgt, N)
+                          : Csr{rowptr, col, wgt};
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+        const int i = u * 64 * kBwdWaves + threadIdx.x;
+        if (i < W4) st4(wl + (i / (D / 4)) * SW + 4 * (i % (D / 4)), wv[u]);
+    }
     __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = lds + wave * WBUF;  // t tile [row][feature], later dx
+    float* xl = tl + G::TILE;       // x tile [row][feature]
 
     f32x4 dw[G::MT][G::MT];  // dW tile (mo, ni): rows o = 16mo + 4q + reg, cols i = 16ni + j
 #pragma unroll
@@ -298,28 +374,29 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
         for (int b = 0; b < G::MT; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // features 4fg..4fg+3, summed over this lane's rows
 
-    const TileRange tr = xcd_tiles(ntiles, wave, kWaves);
+    const TileRange tr = xcd_tiles(ntiles, wave, kBwdWaves);
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
-        const int64_t r0 = tile * kTileRows;
-        gather_tile<D, MASK_IN>(g, dy, yv, scale_in, r0, R, N, lane, tl);
-        // own rows (coalesced): dz for db, x for dW and the output mask
+        const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
+        // own rows (coalesced): dz for db, x for dW and the output mask — issued first
+        f32x4 dz[G::K], mz[G::K], xv[G::K];
 #pragma unroll
-        for (int k = 0; k < kTileRows / RPI; ++k) {
-            const int row = RPI * k + rl;
-            const int64_t r = r0 + row;
-            f32x4 xv = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (r < R) {
-                const int64_t off = r * D + 4 * fg;
-                f32x4 dz = ld4(dy + off);
-                if constexpr (MASK_IN) {
-                    const f32x4 m = ld4(yv + off);
+        for (int k = 0; k < G::K; ++k) {
+            const uint32_t r = r0 + G::RPI * k + rl;
+            dz[k] = dys.ld(r, fg, r < R);
+            if constexpr (MASK_IN) mz[k] = ms.ld(r, fg, r < R);
+            xv[k] = xs.ld(r, fg, r < R);
+        }
+        f32x4 acc[G::K];
+        gather16<D, MASK_IN, 1>(g, dys, ms, scale_in, r0, R, fdN, lane, acc);
+        put_tile<D>(tl, acc, lane);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) dz[i] = m[i] > 0.f ? dz[i] * scale_in : 0.f;
-                }
-                dbacc += dz;
-                xv = ld4(x + off);
+        for (int k = 0; k < G::K; ++k) {
+            if constexpr (MASK_IN) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dz[k][i] = mz[k][i] > 0.f ? dz[k][i] * scale_in : 0.f;
             }
-            st4(xl + row * G::S + 4 * fg, xv);
+            dbacc += dz[k];
+            st4(xl + (G::RPI * k + rl) * G::S + 4 * fg, xv[k]);
         }
         wave_lds_sync();
         // dW[o][i] += sum_rows t[row][o] x[row][i]   (rows = 4q + kk on the K index)
@@ -342,7 +419,7 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int a = 0; a < G::KS / 4; ++a) {
+        for (int a = 0; a < G::CH; ++a) {
             const f32x4 bt = ld4(tl + j * G::S + 16 * a + 4 * q);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -363,21 +440,21 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
         wave_lds_sync();
-        store_tile<D>(tl, dxo, r0, R, lane);
+        store_tile<D>(tl, dxs, r0, R, lane);
         wave_lds_sync();
     }
 
     // ---- per-block reduction of dW / db (fixed wave order -> deterministic)
 #pragma unroll
-    for (int off = LPR; off < 64; off <<= 1)
+    for (int off = G::LPR; off < 64; off <<= 1)
 #pragma unroll
         for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
     __syncthreads();
     float* red = lds;  // reuse the tile buffers
     for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
-    for (int wv = 0; wv < kWaves; ++wv) {
+    for (int wv2 = 0; wv2 < kBwdWaves; ++wv2) {
         __syncthreads();
-        if (wave == wv) {
+        if (wave == wv2) {
 #pragma unroll
             for (int mo = 0; mo < G::MT; ++mo)
 #pragma unroll
@@ -385,52 +462,146 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg)
                         red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
-            if (lane < LPR)
+            if (lane < G::LPR)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
         }
     }
     __syncthreads();
     float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
-    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
+    if (accumulate)
+        for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] += red[i];
+    else
+        for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
 }
 
 // ------------------------------------------------------------------ plain propagate
 template <int D, bool CSR_LDS>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64 * kSpmmWaves)
 k_spmm(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
-       const float* __restrict__ x, float* __restrict__ y, int64_t N, int64_t R, int64_t ntiles) {
-    constexpr int LPR = D / 4, RPI = 64 / LPR;
+       const float* __restrict__ x, float* __restrict__ y, uint32_t N, lg_fastdiv fdN, uint32_t R, int64_t ntiles) {
+    using G = Geo<D>;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const Csr g = CSR_LDS ? stage_csr(smem, rowptr, col, wgt, N) : Csr{rowptr, col, wgt};
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int rl = lane / LPR, fg = lane % LPR;
-    const TileRange tr = xcd_tiles(ntiles, wave, 4);  // a "tile" here is 2*RPI rows
+    const Csr g = CSR_LDS ? stage_csr(reinterpret_cast<uint32_t*>(smem), rowptr, col, wgt, N)
+                          : Csr{rowptr, col, wgt};
+    __syncthreads();
+    const Rows<D> xs = rows_of<D>(x, R), ys = rows_of<D>(y, R);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, rl = lane / G::LPR, fg = lane % G::LPR;
+    const TileRange tr = xcd_tiles(ntiles, wave, kSpmmWaves);
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
-        const int64_t rb = tile * 2 * RPI;
-        f32x4 acc[2];
-        gather8<D, false>(g, x, nullptr, 1.f, rb, R, N, lane, acc);
+        const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
+        f32x4 acc[G::K];
+        gather16<D, false, 2>(g, xs, xs, 1.f, r0, R, fdN, lane, acc);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int64_t r = rb + RPI * k + rl;
-            if (r < R) st4(y + r * D + 4 * fg, acc[k]);
+        for (int k = 0; k < G::K; ++k) {
+            const uint32_t r = r0 + G::RPI * k + rl;
+            ys.st(r, fg, r < R, acc[k]);
         }
     }
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// LDS bytes to stage the CSR (rowptr + col + w, each padded to 16 B), or 0 if too big.
-inline int64_t csr_lds_bytes(int64_t N, int64_t nnz_cap) {
-    const int64_t b = 4 * ((N + 1 + 3) & ~3LL) + 8 * ((nnz_cap + 3) & ~3LL);
-    return b <= kCsrLdsMax ? b : 0;
+// Windows per launch so that one launch's [rows][D] fp32 tensor stays below 4 GiB.
+inline int64_t windows_per_launch(int64_t N, int64_t D) { return kMaxLaunchBytes / (4 * D * N); }
+
+// Persistent grid: as many blocks as are co-resident (registers and LDS both count),
+// capped at `cap_per_cu` per CU and at the work available.
+template <typename Kern>
+int resident_grid(Kern kernel, int threads, int64_t dyn_lds, int64_t want, int cap_per_cu) {
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, static_cast<size_t>(dyn_lds)) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const int64_t cap = std::min(cap_per_cu, per_cu) * static_cast<int64_t>(lg_num_cus());
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(want, cap)));
 }
 
-int bwd_grid(int64_t ntiles, int64_t dyn_lds) {
-    const int64_t want = ceil_div(ntiles, kWaves);
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, (160 * 1024) / dyn_lds));
-    const int64_t cap = per_cu * static_cast<int64_t>(lg_num_cus());
-    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(want, cap)));
+template <typename Kern>
+bool allow_lds(Kern kernel, int64_t dyn) {
+    return dyn <= 64 * 1024 || hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   static_cast<int>(dyn)) == hipSuccess;
+}
+
+constexpr int kFwdWaves = 16;
+
+template <int D, bool CL, bool DROP>
+int launch_fwd(const int32_t* rowptr, const int32_t* col, const float* w, const float* x, const float* W,
+               const float* bias, float* y, int64_t Bc, int64_t N, int64_t csr_bytes, float relu_floor, float p,
+               float scale, uint64_t seed, uint32_t salt, uint64_t row_offset, hipStream_t s) {
+    using G = Geo<D>;
+    const int64_t R = Bc * N, ntiles = ceil_div(R, kTileRows);
+    const int64_t csr_words = CL ? csr_bytes / 4 : 0;
+    const int64_t dyn = 4 * (((csr_words + 3) & ~3LL) + D * G::S + D + kFwdWaves * G::TILE);
+    auto kern = k_gcn_fwd<D, kFwdWaves, CL, DROP>;
+    if (!allow_lds(kern, dyn)) return LG_EHIP;
+    const int grid = resident_grid(kern, 64 * kFwdWaves, dyn, ceil_div(ntiles, kFwdWaves), 2);
+    kern<<<grid, 64 * kFwdWaves, dyn, s>>>(rowptr, col, w, x, W, bias, y, static_cast<uint32_t>(N),
+                                            lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
+                                            ntiles, relu_floor, p, scale, seed, salt, row_offset,
+                                            static_cast<int>(csr_words));
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+template <int D>
+int fwd_dispatch(bool cl, bool drop, const int32_t* rowptr, const int32_t* col, const float* w, const float* x,
+                 const float* W, const float* bias, float* y, int64_t Bc, int64_t N, int64_t csr_bytes,
+                 float relu_floor, float p, float scale, uint64_t seed, uint32_t salt, uint64_t row_offset,
+                 hipStream_t s) {
+#define LG_FWD_ARGS rowptr, col, w, x, W, bias, y, Bc, N, csr_bytes, relu_floor, p, scale, seed, salt, row_offset, s
+    if (cl) return drop ? launch_fwd<D, true, true>(LG_FWD_ARGS) : launch_fwd<D, true, false>(LG_FWD_ARGS);
+    return drop ? launch_fwd<D, false, true>(LG_FWD_ARGS) : launch_fwd<D, false, false>(LG_FWD_ARGS);
+#undef LG_FWD_ARGS
+}
+
+template <int D, bool MI, bool CL>
+int launch_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy, const float* y,
+               const float* x, const float* W, float* dx, float* slab, int64_t Bc, int64_t N, int64_t csr_bytes,
+               int mask_out, float scale_in, float scale_out, int accumulate, int* grid_io, hipStream_t s) {
+    using G = Geo<D>;
+    const int64_t R = Bc * N, ntiles = ceil_div(R, kTileRows);
+    const int64_t csr_words = CL ? csr_bytes / 4 : 0;
+    const int64_t dyn = 4 * (((csr_words + 3) & ~3LL) + kBwdWaves * 2 * G::TILE + D * (D + 4));
+    auto kern = k_gcn_bwd<D, MI, CL>;
+    if (!allow_lds(kern, dyn)) return LG_EHIP;
+    // every chunk of a split launch uses the first chunk's grid (the slab rows it accumulates into)
+    if (*grid_io == 0) *grid_io = resident_grid(kern, 64 * kBwdWaves, dyn, ceil_div(ntiles, kBwdWaves), 2);
+    kern<<<*grid_io, 64 * kBwdWaves, dyn, s>>>(rowptr_t, col_t, w_t, dy, y, x, W, dx, slab, static_cast<uint32_t>(N),
+                                                lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
+                                                ntiles, mask_out, scale_in, scale_out, static_cast<int>(csr_words),
+                                                accumulate);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+template <int D>
+int bwd_dispatch(bool mi, bool cl, const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy,
+                 const float* y, const float* x, const float* W, float* dx, float* slab, int64_t Bc, int64_t N,
+                 int64_t csr_bytes, int mask_out, float scale_in, float scale_out, int accumulate, int* grid_io,
+                 hipStream_t s) {
+#define LG_BWD_ARGS \
+    rowptr_t, col_t, w_t, dy, y, x, W, dx, slab, Bc, N, csr_bytes, mask_out, scale_in, scale_out, accumulate, grid_io, s
+    if (mi) return cl ? launch_bwd<D, true, true>(LG_BWD_ARGS) : launch_bwd<D, true, false>(LG_BWD_ARGS);
+    return cl ? launch_bwd<D, false, true>(LG_BWD_ARGS) : launch_bwd<D, false, false>(LG_BWD_ARGS);
+#undef LG_BWD_ARGS
+}
+
+template <int D, bool CL>
+int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* w, const float* x, float* y, int64_t Bc,
+                int64_t N, int64_t csr_bytes, hipStream_t s) {
+    const int64_t R = Bc * N, ntiles = ceil_div(R, kTileRows);
+    const int64_t dyn = CL ? csr_bytes : 0;
+    auto kern = k_spmm<D, CL>;
+    const int grid = resident_grid(kern, 64 * kSpmmWaves, dyn, ceil_div(ntiles, kSpmmWaves), 8);
+    kern<<<grid, 64 * kSpmmWaves, dyn, s>>>(rowptr, col, w, x, y, static_cast<uint32_t>(N),
+                                             lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
+                                             ntiles);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
 }
 
 int bwd_grid_max() { return 2 * lg_num_cus(); }
@@ -443,33 +614,26 @@ extern "C" int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float
     if (B < 0 || N <= 0 || nnz_cap < 0) return LG_EINVAL;
     if (!rowptr || !col || !w || !x || !W || !y || x == y) return LG_EINVAL;
     if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
-    if ((flags & LG_F_DROPOUT) && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    const bool drop = (flags & LG_F_DROPOUT) != 0;
+    if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
-    const int64_t R = B * N;
-    if (R == 0) return LG_OK;
-    const int64_t ntiles = ceil_div(R, kTileRows);
+    if (B == 0) return LG_OK;
+    const int64_t wpl = windows_per_launch(N, D);
+    if (wpl < 1) return LG_EUNSUPPORTED;
     const int64_t csr = csr_lds_bytes(N, nnz_cap);
-    const int64_t dyn = csr + static_cast<int64_t>(sizeof(float)) * (D + 2 * kFwdWaves * kTileRows) * (D + 4);
-    const unsigned grid = static_cast<unsigned>(
-        std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntiles, kFwdWaves), lg_num_cus())));
-    const float scale = (flags & LG_F_DROPOUT) ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    const float relu_floor = (flags & LG_F_RELU) ? 0.f : -__builtin_huge_valf();
+    const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    const float* bp = (flags & LG_F_BIAS) ? bias : nullptr;
     hipStream_t s = lg_stream(stream);
-#define LG_FWD(DD, CL)                                                                                        \
-    do {                                                                                                      \
-        if (dyn > 64 * 1024 &&                                                                                \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gcn_fwd<DD, CL>),                            \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn)) != hipSuccess) \
-            return LG_EHIP;                                                                                   \
-        k_gcn_fwd<DD, CL><<<grid, 64 * kFwdWaves, dyn, s>>>(rowptr, col, w, x, W, bias, y, N, R, ntiles, flags, \
-                                                        dropout_p, scale, seed, salt, csr);                   \
-    } while (0)
-    if (D == 64) {
-        if (csr) LG_FWD(64, true); else LG_FWD(64, false);
-    } else {
-        if (csr) LG_FWD(32, true); else LG_FWD(32, false);
+    for (int64_t b0 = 0; b0 < B; b0 += wpl) {
+        const int64_t Bc = std::min(wpl, B - b0), off = b0 * N * D;
+        const uint64_t row_off = static_cast<uint64_t>(b0 * N);
+        const int rc = D == 64 ? fwd_dispatch<64>(csr != 0, drop, rowptr, col, w, x + off, W, bp, y + off, Bc, N, csr,
+                                                  relu_floor, dropout_p, scale, seed, salt, row_off, s)
+                               : fwd_dispatch<32>(csr != 0, drop, rowptr, col, w, x + off, W, bp, y + off, Bc, N, csr,
+                                                  relu_floor, dropout_p, scale, seed, salt, row_off, s);
+        if (rc != LG_OK) return rc;
     }
-#undef LG_FWD
-    LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
 
@@ -478,22 +642,22 @@ extern "C" int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w
     if (B < 0 || N <= 0 || nnz_cap < 0) return LG_EINVAL;
     if (!rowptr || !col || !w || !x || !y || x == y) return LG_EINVAL;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
-    const int64_t R = B * N;
-    if (R == 0) return LG_OK;
-    const int64_t ntiles = ceil_div(R, 2 * (64 / (D / 4)));
-    const int64_t lds = csr_lds_bytes(N, nnz_cap);
-    const int64_t per_cu = lds ? std::max<int64_t>(1, std::min<int64_t>(8, (160 * 1024) / lds)) : 8;
-    const unsigned grid =
-        static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntiles, 4), per_cu * lg_num_cus())));
+    if (B == 0) return LG_OK;
+    const int64_t wpl = windows_per_launch(N, D);
+    if (wpl < 1) return LG_EUNSUPPORTED;
+    const int64_t csr = csr_lds_bytes(N, nnz_cap);
     hipStream_t s = lg_stream(stream);
-#define LG_SPMM(DD, CL) k_spmm<DD, CL><<<grid, 256, CL ? lds : 0, s>>>(rowptr, col, w, x, y, N, R, ntiles)
-    if (D == 64) {
-        if (lds) LG_SPMM(64, true); else LG_SPMM(64, false);
-    } else {
-        if (lds) LG_SPMM(32, true); else LG_SPMM(32, false);
+    for (int64_t b0 = 0; b0 < B; b0 += wpl) {
+        const int64_t Bc = std::min(wpl, B - b0), off = b0 * N * D;
+        int rc;
+        if (D == 64)
+            rc = csr ? launch_spmm<64, true>(rowptr, col, w, x + off, y + off, Bc, N, csr, s)
+                     : launch_spmm<64, false>(rowptr, col, w, x + off, y + off, Bc, N, csr, s);
+        else
+            rc = csr ? launch_spmm<32, true>(rowptr, col, w, x + off, y + off, Bc, N, csr, s)
+                     : launch_spmm<32, false>(rowptr, col, w, x + off, y + off, Bc, N, csr, s);
+        if (rc != LG_OK) return rc;
     }
-#undef LG_SPMM
-    LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
 
@@ -508,43 +672,29 @@ extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const f
                           float scale_out, void* workspace, lg_stream_t stream) {
     if (B < 0 || N <= 0 || nnz_cap < 0) return LG_EINVAL;
     if (!rowptr_t || !col_t || !w_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
-    if ((flags & LG_F_MASK_IN) && !y) return LG_EINVAL;
+    const bool mask_in = (flags & LG_F_MASK_IN) != 0;
+    if (mask_in && !y) return LG_EINVAL;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
-    const int64_t R = B * N;
+    const int64_t wpl = windows_per_launch(N, D);
+    if (wpl < 1) return LG_EUNSUPPORTED;
     hipStream_t s = lg_stream(stream);
-    const int64_t ntiles = ceil_div(R, kTileRows);
     float* slab = static_cast<float*>(workspace);
     const int mask_out = (flags & LG_F_MASK_OUT) ? 1 : 0;
-    const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     const int64_t csr = csr_lds_bytes(N, nnz_cap);
-    const int64_t tiles_lds = static_cast<int64_t>(sizeof(float)) *
-                              (kWaves * 2 * kTileRows * (D + 4) + D * (D + 4));
-    const int grid = bwd_grid(ntiles, csr + tiles_lds);
-#define LG_BWD(DD, MI, CL)                                                                                        \
-    do {                                                                                                          \
-        const int64_t dyn = (CL ? csr : 0) + tiles_lds;                                                           \
-        if (dyn > 64 * 1024 &&                                                                                    \
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gcn_bwd<DD, MI, CL>),                            \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(dyn)) != hipSuccess) \
-            return LG_EHIP;                                                                                       \
-        k_gcn_bwd<DD, MI, CL><<<grid, 64 * kWaves, dyn, s>>>(rowptr_t, col_t, w_t, dy, y, x, W, dx_out, slab, N, \
-                                                             R, ntiles, mask_out, scale_in, scale_out, csr);      \
-    } while (0)
-    if (D == 64) {
-        if (mask_in) {
-            if (csr) LG_BWD(64, true, true); else LG_BWD(64, true, false);
-        } else {
-            if (csr) LG_BWD(64, false, true); else LG_BWD(64, false, false);
-        }
-    } else {
-        if (mask_in) {
-            if (csr) LG_BWD(32, true, true); else LG_BWD(32, true, false);
-        } else {
-            if (csr) LG_BWD(32, false, true); else LG_BWD(32, false, false);
-        }
+    int grid = 0;
+    // B == 0 still runs one (empty) launch so the slab holds zeros
+    for (int64_t b0 = 0; b0 < std::max<int64_t>(B, 1); b0 += wpl) {
+        const int64_t Bc = std::min(wpl, B - b0), off = b0 * N * D;
+        const float* yc = y ? y + off : nullptr;
+        const int accumulate = b0 > 0 ? 1 : 0;
+        const int rc = D == 64 ? bwd_dispatch<64>(mask_in, csr != 0, rowptr_t, col_t, w_t, dy + off, yc, x + off, W,
+                                                  dx_out + off, slab, Bc, N, csr, mask_out, scale_in, scale_out,
+                                                  accumulate, &grid, s)
+                               : bwd_dispatch<32>(mask_in, csr != 0, rowptr_t, col_t, w_t, dy + off, yc, x + off, W,
+                                                  dx_out + off, slab, Bc, N, csr, mask_out, scale_in, scale_out,
+                                                  accumulate, &grid, s);
+        if (rc != LG_OK) return rc;
     }
-#undef LG_BWD
-    LG_RET_IF_LAUNCH_FAILED();
     const int64_t L = D * D + D;
     int rc = lg_launch_slab_reduce(slab, grid, L, D * D, dW, s);
     if (rc == LG_OK && db) rc = lg_launch_slab_reduce(slab + D * D, grid, L, D, db, s);

@@ -12,15 +12,15 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 template <int D>
 __global__ void __launch_bounds__(256)
 k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, const float* __restrict__ bias,
-            float* __restrict__ x0, int64_t N, int64_t S, int64_t R, int dropout, float p, float scale,
+            float* __restrict__ x0, int64_t N, lg_fastdiv fdN, int64_t S, int64_t R, int dropout, float p, float scale,
             uint64_t seed, uint32_t salt) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
-        const int64_t b = r / N, n = r - b * N;
+        const uint32_t b = lg_div(static_cast<uint32_t>(r), fdN), n = static_cast<uint32_t>(r) - b * fdN.d;
         const int32_t s = slot[n];
-        f32x4 v = s >= 0 ? ld4(proj + (b * S + s) * D + 4 * fg) : ld4(bias + 4 * fg);
+        f32x4 v = s >= 0 ? ld4(proj + (static_cast<int64_t>(b) * S + s) * D + 4 * fg) : ld4(bias + 4 * fg);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = fmaxf(v[i], 0.f);
@@ -34,14 +34,14 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
 template <int D>
 __global__ void __launch_bounds__(256)
 k_pipe_gather(const int64_t* __restrict__ ends, const float* __restrict__ h, float* __restrict__ feat, int64_t N,
-              int64_t P, int64_t BP) {
+              lg_fastdiv fdP, int64_t BP) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * RPB + rl; i < BP; i += static_cast<int64_t>(gridDim.x) * RPB) {
-        const int64_t b = i / P, p = i - b * P;
+        const uint32_t b = lg_div(static_cast<uint32_t>(i), fdP), p = static_cast<uint32_t>(i) - b * fdP.d;
         const int64_t u = ends[2 * p], v = ends[2 * p + 1];
-        const f32x4 hu = ld4(h + (b * N + u) * D + 4 * fg);
-        const f32x4 hv = ld4(h + (b * N + v) * D + 4 * fg);
+        const f32x4 hu = ld4(h + (static_cast<int64_t>(b) * N + u) * D + 4 * fg);
+        const f32x4 hv = ld4(h + (static_cast<int64_t>(b) * N + v) * D + 4 * fg);
         f32x4 ad;
 #pragma unroll
         for (int k = 0; k < 4; ++k) ad[k] = fabsf(hu[k] - hv[k]);
@@ -57,12 +57,13 @@ template <int D>
 __global__ void __launch_bounds__(256)
 k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict__ inc_item,
                const float* __restrict__ dpipe, const float* __restrict__ dpool, float* __restrict__ dh, int64_t N,
-               int64_t P, int64_t R) {
+               lg_fastdiv fdN, int64_t P, int64_t R) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const float fN = static_cast<float>(N);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
-        const int64_t b = r / N, n = r - b * N;
+        const uint32_t bu = lg_div(static_cast<uint32_t>(r), fdN), n = static_cast<uint32_t>(r) - bu * fdN.d;
+        const int64_t b = bu;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         if (dpool) {
             const f32x4 g = ld4(dpool + b * D + 4 * fg);
@@ -116,15 +117,17 @@ extern "C" int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, c
     if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
+    if (R >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const lg_fastdiv fdN = lg_make_fastdiv(static_cast<uint32_t>(N));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     switch (D) {
         case 64:
-            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, S, R, dropout, dropout_p,
+            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdN, S, R, dropout, dropout_p,
                                                             scale, seed, salt);
             break;
         case 32:
-            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, S, R, dropout, dropout_p,
+            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdN, S, R, dropout, dropout_p,
                                                             scale, seed, salt);
             break;
         default:
@@ -140,10 +143,12 @@ extern "C" int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* fe
     const int64_t BP = B * P;
     if (BP == 0) return LG_OK;
     if (!ends || !h || !feat) return LG_EINVAL;
+    if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64: k_pipe_gather<64><<<row_grid(BP, 64), 256, 0, s>>>(ends, h, feat, N, P, BP); break;
-        case 32: k_pipe_gather<32><<<row_grid(BP, 32), 256, 0, s>>>(ends, h, feat, N, P, BP); break;
+        case 64: k_pipe_gather<64><<<row_grid(BP, 64), 256, 0, s>>>(ends, h, feat, N, fdP, BP); break;
+        case 32: k_pipe_gather<32><<<row_grid(BP, 32), 256, 0, s>>>(ends, h, feat, N, fdP, BP); break;
         default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();
@@ -157,10 +162,12 @@ extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
     if (!inc_rowptr || !dh || (P > 0 && (!inc_item || !dpipe))) return LG_EINVAL;
+    if (R >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const lg_fastdiv fdN = lg_make_fastdiv(static_cast<uint32_t>(N));
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64: k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, P, R); break;
-        case 32: k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, P, R); break;
+        case 64: k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdN, P, R); break;
+        case 32: k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdN, P, R); break;
         default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();

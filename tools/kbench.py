@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,spmm,edge_fwd,edge_bwd,gru_fwd,gru_bwd")
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
     args = ap.parse_args()
     lib = nat.load_library()
     dev = torch.device("cuda:0")
@@ -65,6 +66,10 @@ def main():
                                          123, 1, st), "fwd")
         t = timeit(f, args.iters)
         res["gcn_fwd_train"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    for lab in [int(v) for v in args.lab.split(",") if v]:
+        f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
+                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | lab, 0.0, 0, 0, st), "fwd")
+        res[f"gcn_fwd_lab{lab >> 20}"] = {"us": timeit(f, args.iters)}
     if "spmm" in which:
         f = lambda: check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, N, D, E1,
                                       st), "spmm")
