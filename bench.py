@@ -16,14 +16,22 @@ model and is not part of the detector step).  Weak scaling: B windows per rank.
 Roofline: the dominant HIP kernel is the fused GCN layer (lg_gcn_fwd, the
 scatter-aggregate).  Its algorithmic bytes per launch follow SURVEY §8(d):
 8*B*N*D + 4*(N+1) + 8*E'  (read x once, write y once, single-graph CSR), timed with
-HIP events on the launch stream over the timed steps.
+HIP events on the launch stream over the timed steps.  `traffic` is the measured HBM
+traffic of one such launch: two child `rocprofv3 --pmc` passes (FETCH_SIZE, then
+WRITE_SIZE; kernel trace only) over tools/kbench.py's identical train-mode launch,
+corrected as MI355X_MICROARCH.md prescribes for gfx950 (2 x FETCH_SIZE + WRITE_SIZE,
+KiB).  The plain propagate (lg_spmm, K6 alone) is timed beside it on the same graph.
 """
 from __future__ import annotations
 
 import argparse
+import csv
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -87,6 +95,62 @@ def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
                       f"{med * 1e3:.1f} ms/step (oracle/detector_ref.py on torch CPU, {threads} threads)"}
 
 
+def pmc_traffic(batch: int) -> dict | None:
+    """Per-launch HBM bytes of the train-mode lg_gcn_fwd from rocprofv3 PMC counters.
+
+    Runs as child processes (never exec): one counter per pass, kernel trace only.
+    Returns None when rocprofv3 is unavailable or a pass fails.
+    """
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    vals = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir="/tmp") as d:
+            cmd = [prof, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv", "--",
+                   sys.executable, str(REPO / "tools" / "kbench.py"), "--which", "gcn_fwd_train", "--B", str(batch),
+                   "--iters", "20"]
+            try:
+                subprocess.run(cmd, env=env, cwd=str(REPO), timeout=300, check=True, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL)
+            except (subprocess.SubprocessError, OSError):
+                return None
+            per = {}
+            for f in Path(d).rglob("*counter_collection.csv"):
+                for r in csv.DictReader(open(f)):
+                    if "k_gcn_fwd" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+            if not per:
+                return None
+            vals[counter] = sum(per.values()) / len(per)
+    return {"bytes": (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, "FETCH_SIZE_KiB": vals["FETCH_SIZE"],
+            "WRITE_SIZE_KiB": vals["WRITE_SIZE"]}
+
+
+def time_propagate(graph, B: int, N: int, D: int, dev, iters: int = 50) -> float:
+    """Mean device time (ms) of lg_spmm (K6 alone) on [B, N, D], HIP events on the launch stream."""
+    from models import _native as nat
+    from models.ops import check, ptr
+    lib = nat.load_library()
+    x = torch.randn(B, N, D, device=dev)
+    y = torch.empty_like(x)
+    st = torch.cuda.current_stream(dev)
+
+    def f():
+        check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, N, D, graph.nnz_cap,
+                          st.cuda_stream), "lg_spmm")
+    for _ in range(5):
+        f()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(st)
+    for _ in range(iters):
+        f()
+    b.record(st)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +159,7 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=256, help="windows per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline sampling")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     args = ap.parse_args()
 
     from models import ops
@@ -173,6 +238,10 @@ def main() -> None:
     fwd_bytes = 8 * B * N * D + 4 * (N + 1) + 8 * E1
     fwd_ms = kms["gcn_fwd"]
     achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    graph = model._device_state(dev)[0]
+    prop_ms = time_propagate(graph, B, N, D, dev)
+    prop_gbs = fwd_bytes / (prop_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(B) if (world == 1 and not args.no_pmc) else None
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -184,8 +253,14 @@ def main() -> None:
                    "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode"},
         "roofline": {"kernel": "lg_gcn_fwd (fused gather-aggregate + MFMA transform)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": round(traffic["bytes"]) if traffic else None,
+                     "traffic_source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, "
+                                        "2*FETCH+WRITE (gfx950)") if traffic else None,
                      "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
+        "roofline_propagate": {"kernel": "lg_spmm (K6 alone, same graph and shape)", "bound": "hbm",
+                               "achieved": round(prop_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(prop_gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(prop_ms * 1e3, 2)},
         "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
         "final_loss": round(final_loss, 4),
     }

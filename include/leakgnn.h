@@ -25,6 +25,9 @@
  *    CSR and offsets rows by b·N itself, so the (2, B·E) batchified edge_index is
  *    never materialised on the hot path.
  *  - Supported feature widths D: 32, 64 (LG_EUNSUPPORTED otherwise).
+ *  - Row indices (b·N + n, b·P + p) are 32-bit inside the kernels: B·N and B·P must
+ *    be < 2^31 (LG_EUNSUPPORTED otherwise).  Feature tensors larger than 4 GiB are
+ *    fine: the GCN entry points split the launch over windows internally.
  */
 #ifndef LEAKGNN_H
 #define LEAKGNN_H
@@ -196,23 +199,26 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
 int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N, int64_t D, lg_stream_t stream);
 
 /* ---------------------------------------------------------------------------
- * SharedSensorGRUEncoder (detector.py:28-73): one nn.GRU(1 [+9], 64) over the
+ * SharedSensorGRUEncoder (detector.py:28-73): one nn.GRU(1 [+9], H) over the
  * B*S sensor sequences (q = b*S + s), L steps, output h_L.  PyTorch gate order
  * (r, z, n) and formulas; weights in nn.GRU layout (weight_ih_l0 [3H][I],
  * weight_hh_l0 [3H][H]).  x_t = [residual[b][t][s], tfeat[b][t][0..8]] is read in
  * place — the (B*S, L, 10) concatenation of detector.py:62-67 is never built.
  *   residual : fp32 [B][L][S];  tfeat : fp32 [B][L][9] (I = 10) or NULL (I = 1)
  *   h_seq    : fp32 [L][B*S][H] every step's h (for the backward) or NULL
+ *   gates    : fp32 [L][B*S][4][H] per step (r, z, n, W_hn h + b_hn) for the
+ *              backward, or NULL (inference); non-NULL requires h_seq
  *   h_last   : fp32 [B*S][H]  (= h_s of detector.py:176 as [B][S][H])
- * Only H = 64, I in {1, 10} (use_time False/True), one layer.
- * Backward (BPTT, gates recomputed from h_seq): dh_last -> dx (fp32 [B*S][L][I],
- * may be NULL), dW_ih, dW_hh, db_ih, db_hh (overwritten, deterministic). */
+ * H in {32, 64}, I in {1, 10} (use_time False/True), one layer.
+ * Backward (BPTT from the saved gates, no recompute): dh_last -> dx (fp32
+ * [B*S][L][I], may be NULL), dW_ih, dW_hh, db_ih, db_hh (overwritten,
+ * deterministic). */
 int lg_gru_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
-               const float* b_ih, const float* b_hh, float* h_seq, float* h_last,
+               const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last,
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H, lg_stream_t stream);
-int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I);
+int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H);
 int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
-               const float* b_ih, const float* b_hh, const float* h_seq, const float* dh_last,
+               const float* h_seq, const float* gates, const float* dh_last,
                float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H,
                void* workspace, lg_stream_t stream);

@@ -1,70 +1,102 @@
 // SharedSensorGRUEncoder (reference detector.py:28-73) as two fused HIP kernels.
 //
-// One nn.GRU(input 1 [+9 time features], hidden 64, 1 layer) runs over B*S
+// One nn.GRU(input 1 [+9 time features], hidden H in {32, 64}, 1 layer) runs over B*S
 // independent sequences (sequence q = b*S + s) of L steps; the encoder keeps h_L.
 // PyTorch gate order / formulas:
 //   r = sig(W_ir x + b_ir + W_hr h + b_hr)     z = sig(W_iz x + b_iz + W_hz h + b_hz)
 //   n = tanh(W_in x + b_in + r * (W_hn h + b_hn))     h' = (1 - z) * n + z * h
 //
-// Work split: one 256-thread workgroup = 16 sequences; wave w owns hidden units
-// [16w, 16w+16), i.e. gate rows {w, 4+w, 8+w} of the 12 16-row tiles.  Gates are
-// computed transposed, G^T (192 x 16 seq) = W (192 x K) * [h;x]^T, with
-// v_mfma_f32_16x16x4_f32 (exact fp32).  With the K index permuted as
-// k = f(ks, q) = 16*(ks>>2) + 4q + (ks&3), the accumulator layout of the new h IS
-// the B-operand layout of the next step's h, so the recurrence stays in registers;
-// the four waves swap their quarters of h through a 4 KiB LDS slot once per step.
-// The input projection is folded into the same accumulators (K = 10 padded to 12),
-// so x = [residual, tfeat] is read straight from (B, L, S) / (B, L, 9) — the
-// (B*S, L, 10) concatenation of the reference (detector.py:62-67) is never built.
+// Work split: one workgroup = 16 sequences x H/16 waves; wave w owns hidden units
+// [16w, 16w+16), i.e. one 16-row tile of each gate.  Gates are computed transposed,
+// G^T (3H x 16 seq) = W (3H x K) [h; x]^T on v_mfma_f32_16x16x4_f32 (exact fp32).
+// With the K index permuted as k = fk(ks, q) = 16*(ks>>2) + 4q + (ks&3), the
+// accumulator layout of the new h IS the B-operand layout of the next step's h, so
+// the recurrence stays in registers; waves swap their quarters of h through LDS once
+// per step.  x = [residual, tfeat] is staged into LDS 32 steps at a time straight
+// from (B, L, S) / (B, L, 9) (the (B*S, L, 10) concatenation of detector.py:62-67 is
+// never built) with a constant-1 column that the backward uses for the bias sums.
 //
-// Backward (BPTT) recomputes the gates from the saved h_{t-1}, exchanges dG^T
-// through LDS, and accumulates dW_hh / dW_ih / db in registers per wave (each wave
-// owns disjoint gate rows), written once per workgroup to a slab and reduced in
-// fixed order -> deterministic.
+// Training forward also stores the gate values (r, z, n, W_hn h + b_hn) per step, so
+// the backward does not recompute them: its serial critical path per step is the
+// elementwise gate backward, one LDS exchange and the dh MFMAs (W_hh^T fragments held
+// in registers, four independent accumulator chains).  dW_hh / dW_ih / db are
+// accumulated in the same loop from the exchanged dG (the MFMA pipe fills the
+// recurrence's bubbles), gates and h_{t-1} are prefetched two steps ahead, and each
+// workgroup writes its partial sums once to a slab reduced in fixed order
+// (deterministic).
 #include <algorithm>
 #include "common.h"
 #include "reduce.h"
 
 namespace {
 
-constexpr int H = 64;
-constexpr int G3 = 3 * H;
 constexpr int TS = 16;  // sequences per workgroup
+constexpr int kLC = 32;  // x staging chunk (steps), forward
+constexpr int kLB = 16;  // x staging chunk (steps), backward (keeps 2 workgroups/CU in LDS)
 
 __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q + (ks & 3); }
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-template <bool USE_TIME>
-__device__ __forceinline__ float load_x(const float* __restrict__ resid, const float* __restrict__ tfeat, int64_t b,
-                                        int64_t s, int t, int k, int L, int S, bool valid) {
-    if (!valid) return 0.f;
-    if (k == 0) return resid[(b * L + t) * S + s];
-    if (USE_TIME && k <= 9) return tfeat[(b * L + t) * 9 + (k - 1)];
-    return 0.f;
+// xs[tt][seq][16] = [x_0 .. x_{I-1}, 0.., 1 (col 10), 0..] for steps t0 .. t0+nt-1 of the
+// block's 16 sequences (all zero for padded sequences).  All loads are issued before
+// the first LDS store of each batch.
+template <bool UT>
+__device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __restrict__ resid,
+                                        const float* __restrict__ tfeat, int t0, int nt, uint32_t seq0,
+                                        uint32_t Nseq, int L, int S, const lg_fastdiv& fdS) {
+    constexpr int PER = 8;
+    const int total = nt * TS * 16;
+    for (int base = 0; base < total; base += blockDim.x * PER) {
+        float v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = base + u * blockDim.x + threadIdx.x;
+            const int tt = idx >> 8, sq = (idx >> 4) & 15, k = idx & 15;
+            const uint32_t sg = seq0 + sq;
+            const bool ok = idx < total && sg < Nseq;
+            const uint32_t sgc = ok ? sg : 0u;
+            const uint32_t b = lg_div(sgc, fdS), s = sgc - b * fdS.d;
+            const int64_t row = static_cast<int64_t>(b) * L + (t0 + (ok ? tt : 0));
+            float x = 0.f;
+            if (k == 0) x = resid[row * S + s];
+            else if (UT && k <= 9) x = tfeat[row * 9 + (k - 1)];
+            else if (k == 10) x = 1.f;
+            v[u] = ok ? x : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int idx = base + u * blockDim.x + threadIdx.x;
+            if (idx < total) xs[idx] = v[u];
+        }
+    }
 }
 
-template <bool USE_TIME>
-__global__ void __launch_bounds__(256)
+// ------------------------------------------------------------------ forward
+// gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
+template <int H, bool UT, bool SAVE>
+__global__ void __launch_bounds__(4 * H)
 k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Wih,
           const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
-          float* __restrict__ hs, float* __restrict__ hout, int B, int L, int S) {
-    constexpr int I = USE_TIME ? 10 : 1;
-    __shared__ __attribute__((aligned(16))) float hx[2][64][16];
-    const int64_t Nseq = static_cast<int64_t>(B) * S;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int64_t seq = static_cast<int64_t>(blockIdx.x) * TS + j;
+          float* __restrict__ hs, float* __restrict__ gates, float* __restrict__ hout, uint32_t Nseq, int L, int S,
+          lg_fastdiv fdS) {
+    constexpr int NW = H / 16, KH = H / 4, I = UT ? 10 : 1;
+    __shared__ __attribute__((aligned(16))) float xs[kLC * TS * 16];
+    __shared__ __attribute__((aligned(16))) float hx[2][64][4 * NW];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const uint32_t seq0 = blockIdx.x * TS, seq = seq0 + j;
     const bool valid = seq < Nseq;
-    const int64_t b = valid ? seq / S : 0, s = valid ? seq - b * S : 0;
 
-    float ah[3][16], ax[3][3];
+    float ah[3][KH], ax[3][3];
 #pragma unroll
     for (int gi = 0; gi < 3; ++gi) {
         const int row = gi * H + 16 * w + j;  // A-operand row of this lane
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) ah[gi][ks] = Whh[row * H + fk(ks, q)];
+        for (int ks = 0; ks < KH; ++ks) ah[gi][ks] = Whh[row * H + fk(ks, q)];
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const int k = 4 * kx + q;
@@ -80,225 +112,238 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
         bhn[reg] = bhh[2 * H + c];
         bin[reg] = bih[2 * H + c];
     }
-    float hf[16];
+    float hf[KH];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) hf[i] = 0.f;
+    for (int i = 0; i < KH; ++i) hf[i] = 0.f;
 
-    float xv[3];
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) xv[kx] = load_x<USE_TIME>(resid, tfeat, b, s, 0, 4 * kx + q, L, S, valid);
-
-    for (int t = 0; t < L; ++t) {
-        f32x4 ar = br, az = bz, ahn = bhn, ain = bin;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            ar = mfma(ax[0][kx], xv[kx], ar);
-            az = mfma(ax[1][kx], xv[kx], az);
-            ain = mfma(ax[2][kx], xv[kx], ain);
-        }
-        if (t + 1 < L) {  // prefetch next step's inputs under the MFMA chain
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx)
-                xv[kx] = load_x<USE_TIME>(resid, tfeat, b, s, t + 1, 4 * kx + q, L, S, valid);
-        }
-#pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-            ar = mfma(ah[0][ks], hf[ks], ar);
-            az = mfma(ah[1][ks], hf[ks], az);
-            ahn = mfma(ah[2][ks], hf[ks], ahn);
-        }
-        f32x4 hn;
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const float r = sigm(ar[reg]);
-            const float z = sigm(az[reg]);
-            const float n = tanhf(ain[reg] + r * ahn[reg]);
-            hn[reg] = (1.f - z) * n + z * hf[4 * w + reg];
-        }
-        st4(&hx[t & 1][lane][4 * w], hn);
-        if (hs && valid) st4(hs + ((static_cast<int64_t>(t) * Nseq + seq) * H + 16 * w + 4 * q), hn);
+    for (int t0 = 0; t0 < L; t0 += kLC) {
+        const int nt = min(kLC, L - t0);
         __syncthreads();
+        stage_x<UT>(xs, resid, tfeat, t0, nt, seq0, Nseq, L, S, fdS);
+        __syncthreads();
+        for (int tt = 0; tt < nt; ++tt) {
+            const int t = t0 + tt;
+            f32x4 ar = br, az = bz, ahn = bhn, ain = bin;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            const f32x4 v = ld4(&hx[t & 1][lane][4 * a]);
+            for (int kx = 0; kx < 3; ++kx) {
+                const float xv = xs[(tt * TS + j) * 16 + 4 * kx + q];
+                ar = mfma(ax[0][kx], xv, ar);
+                az = mfma(ax[1][kx], xv, az);
+                ain = mfma(ax[2][kx], xv, ain);
+            }
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
+            for (int ks = 0; ks < KH; ++ks) {
+                ar = mfma(ah[0][ks], hf[ks], ar);
+                az = mfma(ah[1][ks], hf[ks], az);
+                ahn = mfma(ah[2][ks], hf[ks], ahn);
+            }
+            f32x4 hn, rr, zz, nn;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                rr[reg] = sigm(ar[reg]);
+                zz[reg] = sigm(az[reg]);
+                nn[reg] = tanhf(ain[reg] + rr[reg] * ahn[reg]);
+                hn[reg] = (1.f - zz[reg]) * nn[reg] + zz[reg] * hf[4 * w + reg];
+            }
+            st4(&hx[t & 1][lane][4 * w], hn);
+            if (valid) {
+                const int64_t row = static_cast<int64_t>(t) * Nseq + seq;
+                if (hs) st4(hs + row * H + 16 * w + 4 * q, hn);
+                if constexpr (SAVE) {
+                    float* g = gates + row * 4 * H + 16 * w + 4 * q;
+                    st4(g, rr);
+                    st4(g + H, zz);
+                    st4(g + 2 * H, nn);
+                    st4(g + 3 * H, ahn);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int a = 0; a < NW; ++a) {
+                const f32x4 v = ld4(&hx[t & 1][lane][4 * a]);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
+            }
         }
     }
     if (valid) {
         f32x4 v;
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) v[reg] = hf[4 * w + reg];
-        st4(hout + seq * H + 16 * w + 4 * q, v);
+        st4(hout + static_cast<int64_t>(seq) * H + 16 * w + 4 * q, v);
     }
 }
 
-// slab layout per workgroup: [dWhh 192*64][dWih 192*I][dbih 192][dbhh 192]
-template <bool USE_TIME, bool NEED_DX>
-__global__ void __launch_bounds__(256)
+// ------------------------------------------------------------------ backward
+// slab layout per workgroup: [dWhh 3H*H][dWih 3H*I][dbih 3H][dbhh 3H]
+template <int H>
+struct GB {
+    static constexpr int NW = H / 16;
+    static constexpr int RW = 16 * NW;     // dG floats per lane row: 4 gates x NW waves x 4 regs
+    static constexpr int DS = RW + 4;      // dg row stride (16 B aligned rows)
+    static constexpr int HS = H + 16;      // h tile row stride (== 16 mod 64: conflict-free B' reads)
+    static constexpr int KG = 3 * H / 4;   // k-steps of the dh contraction (3H gate rows)
+};
+
+// Physical column of logical dG column c in the row of lane `src`: a 16-float rotation by
+// (src >> 4) keeps the cross-lane dW operand reads bank-conflict free.
+template <int H>
+__device__ __forceinline__ int dg_col(int src, int c) {
+    return (c + 16 * ((src >> 4) & 3)) & (GB<H>::RW - 1);
+}
+
+template <int H, bool UT, bool NEED_DX>
+__global__ void __launch_bounds__(4 * H)
 k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Wih,
-          const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
-          const float* __restrict__ hs, const float* __restrict__ dhL, float* __restrict__ dx,
-          float* __restrict__ slab, int B, int L, int S) {
-    constexpr int I = USE_TIME ? 10 : 1;
-    constexpr int SWH = H + 1;
+          const float* __restrict__ Whh, const float* __restrict__ hs, const float* __restrict__ gates,
+          const float* __restrict__ dhL, float* __restrict__ dx, float* __restrict__ slab, uint32_t Nseq, int L,
+          int S, lg_fastdiv fdS) {
+    using G = GB<H>;
+    constexpr int NW = G::NW, I = UT ? 10 : 1, G3 = 3 * H;
     constexpr int SLAB = G3 * H + G3 * I + 2 * G3;
-    __shared__ __attribute__((aligned(16))) float whh[G3 * SWH];
-    __shared__ __attribute__((aligned(16))) float wih[G3 * 16];
-    __shared__ __attribute__((aligned(16))) float dg[64][64 + 4];
-    const int64_t Nseq = static_cast<int64_t>(B) * S;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int64_t seq0 = static_cast<int64_t>(blockIdx.x) * TS;
-    const int64_t seq = seq0 + j;
+    constexpr int NTH = 64 * NW;
+    __shared__ __attribute__((aligned(16))) float xs[kLB * TS * 16];
+    __shared__ __attribute__((aligned(16))) float hl[3][TS * G::HS];
+    __shared__ __attribute__((aligned(16))) float dg[2][64 * G::DS];
+    __shared__ __attribute__((aligned(16))) float wih[NEED_DX ? G3 * 16 : 1];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const uint32_t seq0 = blockIdx.x * TS, seq = seq0 + j;
     const bool valid = seq < Nseq;
-    const int64_t b = valid ? seq / S : 0, s = valid ? seq - b * S : 0;
+    const uint32_t seqc = valid ? seq : 0u;
 
-    for (int i = threadIdx.x; i < G3 * H; i += 256) whh[(i / H) * SWH + (i % H)] = Whh[i];
-    for (int i = threadIdx.x; i < G3 * 16; i += 256) wih[i] = (i % 16) < I ? Wih[(i / 16) * I + (i % 16)] : 0.f;
-    __syncthreads();
+    if constexpr (NEED_DX) {
+        for (int i = threadIdx.x; i < G3 * 16; i += NTH) wih[i] = (i % 16) < I ? Wih[(i / 16) * I + (i % 16)] : 0.f;
+    }
+    // W_hh^T fragments: A[row j = unit 16w + j][k = gate row fk(ks, q)]
+    float at[G::KG];
+#pragma unroll
+    for (int ks = 0; ks < G::KG; ++ks) at[ks] = Whh[fk(ks, q) * H + 16 * w + j];
 
-    float ah[3][16], ax[3][3];
+    // h_{t-1} tile rows: thread -> (row = seq, float4 column)
+    const int hrow = threadIdx.x / (H / 4), hc4 = threadIdx.x % (H / 4);
+    const uint32_t hseq = seq0 + hrow;
+    const bool hvalid = hseq < Nseq;
+    auto load_h = [&](int t) -> f32x4 {  // h_t row of this thread (zero for t < 0 / padded)
+        if (t < 0) return zero4();
+        const f32x4 v = ld4(hs + (static_cast<int64_t>(t) * Nseq + (hvalid ? hseq : 0u)) * H + 4 * hc4);
+        return hvalid ? v : zero4();
+    };
+    auto load_g = [&](int t, f32x4 (&g)[4]) {  // gates of step t for this lane's 4 units
+        const float* p = gates + (static_cast<int64_t>(t) * Nseq + seqc) * 4 * H + 16 * w + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] = valid ? ld4(p + k * H) : zero4();
+    };
+
+    f32x4 dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + 16 * w + 4 * q) : zero4();
+    f32x4 dwh[3][NW], dwx[3], dbhn = zero4();
 #pragma unroll
     for (int gi = 0; gi < 3; ++gi) {
-        const int row = gi * H + 16 * w + j;
+        dwx[gi] = zero4();
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) ah[gi][ks] = whh[row * SWH + fk(ks, q)];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) ax[gi][kx] = wih[row * 16 + 4 * kx + q];
-    }
-    f32x4 br, bz, bhn, bin;
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        const int c = 16 * w + 4 * q + reg;
-        br[reg] = bih[c] + bhh[c];
-        bz[reg] = bih[H + c] + bhh[H + c];
-        bhn[reg] = bhh[2 * H + c];
-        bin[reg] = bih[2 * H + c];
+        for (int nt = 0; nt < NW; ++nt) dwh[gi][nt] = zero4();
     }
 
-    f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (valid) dh = ld4(dhL + seq * H + 16 * w + 4 * q);
-
-    f32x4 dwh[3][4], dwi[3], dbg[3], dbin;
-#pragma unroll
-    for (int gi = 0; gi < 3; ++gi) {
-        dwi[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
-        dbg[gi] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) dwh[gi][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    dbin = f32x4{0.f, 0.f, 0.f, 0.f};
+    // prologue: hl for step L-1 (= h_{L-2}), prefetch h_{L-3}, h_{L-4}; gates of L-1, L-2
+    f32x4 g_cur[4], g_n1[4];
+    load_g(L - 1, g_cur);
+    if (L >= 2) load_g(L - 2, g_n1);
+    f32x4 h_n1 = load_h(L - 3), h_n2 = load_h(L - 4);
+    st4(&hl[(L - 1) % 3][hrow * G::HS + 4 * hc4], load_h(L - 2));
 
     for (int t = L - 1; t >= 0; --t) {
-        // h_{t-1} in B layout (lane-local) and x_t
-        float hf[16];
-        if (t > 0 && valid) {
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const f32x4 v = ld4(hs + ((static_cast<int64_t>(t - 1) * Nseq + seq) * H + 16 * a + 4 * q));
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) hf[i] = 0.f;
+        if (t == L - 1 || t % kLB == kLB - 1) {  // stage the x chunk containing t (descending)
+            const int t0 = t - t % kLB;
+            __syncthreads();
+            stage_x<UT>(xs, resid, tfeat, t0, min(kLB, L - t0), seq0, Nseq, L, S, fdS);
         }
-        float xv[3];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) xv[kx] = load_x<USE_TIME>(resid, tfeat, b, s, t, 4 * kx + q, L, S, valid);
-
-        f32x4 ar = br, az = bz, ahn = bhn, ain = bin;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            ar = mfma(ax[0][kx], xv[kx], ar);
-            az = mfma(ax[1][kx], xv[kx], az);
-            ain = mfma(ax[2][kx], xv[kx], ain);
-        }
-#pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-            ar = mfma(ah[0][ks], hf[ks], ar);
-            az = mfma(ah[1][ks], hf[ks], az);
-            ahn = mfma(ah[2][ks], hf[ks], ahn);
-        }
+        const int tt = t % kLB;
+        // One barrier per step (below).  hl[t%3] and this step's x were published by the
+        // previous step's barrier (or the staging barrier); hl[(t-1)%3] and dg[t&1] were
+        // last read two steps ago, which every wave finished before that barrier.
+        // (b) h tile for step t-1 (= h_{t-2}) into the buffer nobody can be reading
+        if (t >= 1) st4(&hl[(t - 1) % 3][hrow * G::HS + 4 * hc4], h_n1);
+        // (a) elementwise gate backward for this lane's 4 units
+        const f32x4 hp = ld4(&hl[t % 3][j * G::HS + 16 * w + 4 * q]);
+        const f32x4 r = g_cur[0], z = g_cur[1], n = g_cur[2], hnp = g_cur[3];
         f32x4 gr, gz, ghn, gin, dhp;
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
-            const float r = sigm(ar[reg]);
-            const float z = sigm(az[reg]);
-            const float n = tanhf(ain[reg] + r * ahn[reg]);
-            const float hp = hf[4 * w + reg];
             const float d = dh[reg];
-            const float dn = d * (1.f - z);
-            const float dz = d * (hp - n);
-            dhp[reg] = d * z;
-            const float dnp = dn * (1.f - n * n);
+            const float dn = d * (1.f - z[reg]);
+            const float dzv = d * (hp[reg] - n[reg]);
+            dhp[reg] = d * z[reg];
+            const float dnp = dn * (1.f - n[reg] * n[reg]);
             gin[reg] = dnp;
-            ghn[reg] = dnp * r;
-            const float drr = dnp * ahn[reg];
-            gr[reg] = drr * r * (1.f - r);
-            gz[reg] = dz * z * (1.f - z);
+            ghn[reg] = dnp * r[reg];
+            gr[reg] = dnp * hnp[reg] * r[reg] * (1.f - r[reg]);
+            gz[reg] = dzv * z[reg] * (1.f - z[reg]);
         }
-        dbg[0] += gr;
-        dbg[1] += gz;
-        dbg[2] += ghn;
-        dbin += gin;
-        __syncthreads();  // previous step's readers of dg are done
-        st4(&dg[lane][4 * w], gr);
-        st4(&dg[lane][16 + 4 * w], gz);
-        st4(&dg[lane][32 + 4 * w], ghn);
-        st4(&dg[lane][48 + 4 * w], gin);
-        __syncthreads();
+        dbhn += ghn;
+        float* dgb = dg[t & 1];
+        st4(&dgb[lane * G::DS + dg_col<H>(lane, 4 * (0 * NW + w))], gr);
+        st4(&dgb[lane * G::DS + dg_col<H>(lane, 4 * (1 * NW + w))], gz);
+        st4(&dgb[lane * G::DS + dg_col<H>(lane, 4 * (2 * NW + w))], ghn);
+        st4(&dgb[lane * G::DS + dg_col<H>(lane, 4 * (3 * NW + w))], gin);
+        // prefetch: gates of t-2, h_{t-4} (consumed two iterations from now)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g_cur[k] = g_n1[k];
+        if (t >= 2) load_g(t - 2, g_n1);
+        h_n1 = h_n2;
+        h_n2 = load_h(t - 4);
+        __syncthreads();  // dG of all waves visible
 
-        // dh_{t-1}[c'] = dh*z + sum_g W_hh[g][c'] dgh[g]   (rows c' = 16w + 4q + reg)
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        // dh_{t-1}[c] = dh z + sum_g W_hh[g][c] dG_h[g]   (4 independent chains)
+        f32x4 acc[4] = {zero4(), zero4(), zero4(), zero4()};
 #pragma unroll
-        for (int ks = 0; ks < 48; ++ks) acc = mfma(whh[fk(ks, q) * SWH + 16 * w + j], dg[lane][ks], acc);
-        dh = dhp + acc;
+        for (int a = 0; a < G::KG / 4; ++a) {
+            const f32x4 bv = ld4(&dgb[lane * G::DS + dg_col<H>(lane, 4 * a)]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = mfma(at[4 * a + i], bv[i], acc[i]);
+        }
+        dh = dhp + ((acc[0] + acc[1]) + (acc[2] + acc[3]));
 
-        // dW_hh[g][c] += sum_seq dgh[g][seq] h_{t-1}[seq][c],  dW_ih likewise with dgi, x
-        // A[g_local = j][k = seq 4q+kk] was written by lane (seq) + 16*(j>>2) at entry 16gi + 4w + (j&3)
+        // dW over this step's 16 sequences: A'[unit j][seq 4ks + q] from the exchanged dG
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int src = (4 * q + kk) + 16 * (j >> 2);
-            const float a0 = dg[src][4 * w + (j & 3)];
-            const float a1 = dg[src][16 + 4 * w + (j & 3)];
-            const float a2 = dg[src][32 + 4 * w + (j & 3)];
-            const float a2i = dg[src][48 + 4 * w + (j & 3)];
-            const int64_t sq = seq0 + 4 * q + kk;
-            const bool v2 = sq < Nseq && t > 0;
+        for (int ks = 0; ks < 4; ++ks) {
+            const int src = (4 * ks + q) + 16 * (j >> 2);
+            const float* row = &dgb[src * G::DS];
+            const float a0 = row[dg_col<H>(src, 4 * (0 * NW + w) + (j & 3))];
+            const float a1 = row[dg_col<H>(src, 4 * (1 * NW + w) + (j & 3))];
+            const float a2 = row[dg_col<H>(src, 4 * (2 * NW + w) + (j & 3))];
+            const float a3 = row[dg_col<H>(src, 4 * (3 * NW + w) + (j & 3))];
+            const float* hrow_p = &hl[t % 3][(4 * ks + q) * G::HS];
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const float hb = v2 ? hs[(static_cast<int64_t>(t - 1) * Nseq + sq) * H + 16 * nt + j] : 0.f;
+            for (int nt = 0; nt < NW; ++nt) {
+                const float hb = hrow_p[16 * nt + j];
                 dwh[0][nt] = mfma(a0, hb, dwh[0][nt]);
                 dwh[1][nt] = mfma(a1, hb, dwh[1][nt]);
                 dwh[2][nt] = mfma(a2, hb, dwh[2][nt]);
             }
-            const bool vx = sq < Nseq;
-            const int64_t bb = vx ? sq / S : 0, ss = vx ? sq - bb * S : 0;
-            const float xb = j < I ? load_x<USE_TIME>(resid, tfeat, bb, ss, t, j, L, S, vx) : 0.f;
-            dwi[0] = mfma(a0, xb, dwi[0]);
-            dwi[1] = mfma(a1, xb, dwi[1]);
-            dwi[2] = mfma(a2i, xb, dwi[2]);
+            const float xb = xs[(tt * TS + 4 * ks + q) * 16 + j];
+            dwx[0] = mfma(a0, xb, dwx[0]);
+            dwx[1] = mfma(a1, xb, dwx[1]);
+            dwx[2] = mfma(a3, xb, dwx[2]);
         }
         if (NEED_DX && w == 0) {
-            // dx^T[k][seq] = sum_g W_ih[g][k] dgi[g][seq]   (k = 4q + reg < I)
-            f32x4 dxa = f32x4{0.f, 0.f, 0.f, 0.f};
+            // dx^T[k][seq] = sum_g W_ih[g][k] dG_i[g][seq]   (gates r, z, in; k = 4q + reg < I)
+            f32x4 dxa = zero4();
 #pragma unroll
-            for (int ks = 0; ks < 48; ++ks) {
-                const float bv = ks < 32 ? dg[lane][ks] : dg[lane][ks + 16];
-                dxa = mfma(wih[fk(ks, q) * 16 + j], bv, dxa);
+            for (int ks = 0; ks < G::KG; ++ks) {
+                const int c = ks < 2 * 4 * NW ? ks : ks + 4 * NW;  // skip the hn block
+                dxa = mfma(wih[fk(ks, q) * 16 + j], dgb[lane * G::DS + dg_col<H>(lane, c)], dxa);
             }
             if (valid) {
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {
                     const int k = 4 * q + reg;
-                    if (k < I) dx[(seq * L + t) * I + k] = dxa[reg];
+                    if (k < I) dx[(static_cast<int64_t>(seq) * L + t) * I + k] = dxa[reg];
                 }
             }
         }
     }
 
-    // per-workgroup slab: waves own disjoint gate rows, no cross-wave reduction needed
+    // per-workgroup slab: waves own disjoint gate rows
     float* out = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
     float* oWhh = out;
     float* oWih = out + G3 * H;
@@ -310,94 +355,117 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
         for (int reg = 0; reg < 4; ++reg) {
             const int g = gi * H + 16 * w + 4 * q + reg;
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) oWhh[g * H + 16 * nt + j] = dwh[gi][nt][reg];
-            if (j < I) oWih[g * I + j] = dwi[gi][reg];
+            for (int nt = 0; nt < NW; ++nt) oWhh[g * H + 16 * nt + j] = dwh[gi][nt][reg];
+            if (j < I) oWih[g * I + j] = dwx[gi][reg];
+            if (j == 10) obih[g] = dwx[gi][reg];             // constant-1 column: sum of dG_i
+            if (j == 10 && gi < 2) obhh[g] = dwx[gi][reg];   // r, z: dG_h == dG_i
         }
-    // biases: sum the 16 sequence lanes (same q) of each lane-local row
+    // db_hh(n) = sum over sequences of dG_hn: fold the 16 sequence lanes of each row
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-#pragma unroll
-            for (int gi = 0; gi < 3; ++gi) dbg[gi][reg] += __shfl_xor(dbg[gi][reg], off);
-            dbin[reg] += __shfl_xor(dbin[reg], off);
-        }
+        for (int reg = 0; reg < 4; ++reg) dbhn[reg] += __shfl_xor(dbhn[reg], off);
     if (j == 0) {
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int c = 16 * w + 4 * q + reg;
-            obhh[c] = dbg[0][reg];
-            obhh[H + c] = dbg[1][reg];
-            obhh[2 * H + c] = dbg[2][reg];
-            obih[c] = dbg[0][reg];
-            obih[H + c] = dbg[1][reg];
-            obih[2 * H + c] = dbin[reg];
-        }
+        for (int reg = 0; reg < 4; ++reg) obhh[2 * H + 16 * w + 4 * q + reg] = dbhn[reg];
     }
 }
 
 inline int64_t nblocks_seq(int64_t nseq) { return (nseq + TS - 1) / TS; }
 
-}  // namespace
-
-extern "C" int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I) {
-    if (B < 0 || S < 0 || (I != 1 && I != 10)) return LG_EINVAL;
-    const int64_t slab = G3 * H + G3 * I + 2 * G3;
-    return std::max<int64_t>(1, nblocks_seq(B * S)) * slab * static_cast<int64_t>(sizeof(float));
-}
-
-extern "C" int lg_gru_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
-                          const float* b_ih, const float* b_hh, float* h_seq, float* h_last, int64_t B, int64_t L,
-                          int64_t S, int64_t I, int64_t Hd, lg_stream_t stream) {
-    if (B < 0 || L <= 0 || S <= 0 || L > INT32_MAX || S > INT32_MAX || B * S > INT32_MAX / 2) return LG_EINVAL;
-    if (Hd != H || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
-    if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
-    if (B == 0) return LG_OK;
+template <int H>
+int launch_fwd(bool ut, bool save, const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+               const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last, int64_t B,
+               int64_t L, int64_t S, hipStream_t s) {
+    const uint32_t Nseq = static_cast<uint32_t>(B * S);
     const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
-    hipStream_t s = lg_stream(stream);
-    if (I == 10)
-        k_gru_fwd<true><<<grid, 256, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, h_last, (int)B, (int)L,
-                                              (int)S);
-    else
-        k_gru_fwd<false><<<grid, 256, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, h_last, (int)B, (int)L,
-                                               (int)S);
+    const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
+#define LG_GRU_FWD(UT, SV)                                                                                        \
+    k_gru_fwd<H, UT, SV><<<grid, 4 * H, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, h_last,   \
+                                                 Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+    if (ut) {
+        if (save) LG_GRU_FWD(true, true); else LG_GRU_FWD(true, false);
+    } else {
+        if (save) LG_GRU_FWD(false, true); else LG_GRU_FWD(false, false);
+    }
+#undef LG_GRU_FWD
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
 
+template <int H>
+int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat, const float* w_ih,
+               const float* w_hh, const float* h_seq, const float* gates, const float* dh_last, float* dx,
+               float* slab, int64_t B, int64_t L, int64_t S, hipStream_t s) {
+    const uint32_t Nseq = static_cast<uint32_t>(B * S);
+    const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
+    const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
+#define LG_GRU_BWD(UT, DX)                                                                                       \
+    k_gru_bwd<H, UT, DX><<<grid, 4 * H, 0, s>>>(residual, tfeat, w_ih, w_hh, h_seq, gates, dh_last, dx, slab,   \
+                                                 Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+    if (ut) {
+        if (need_dx) LG_GRU_BWD(true, true); else LG_GRU_BWD(true, false);
+    } else {
+        if (need_dx) LG_GRU_BWD(false, true); else LG_GRU_BWD(false, false);
+    }
+#undef LG_GRU_BWD
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+bool dims_ok(int64_t B, int64_t L, int64_t S) {
+    return B >= 0 && L > 0 && S > 0 && L <= INT32_MAX && S <= INT32_MAX && B * S < (int64_t{1} << 31);
+}
+
+}  // namespace
+
+extern "C" int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H) {
+    if (B < 0 || S < 0 || (I != 1 && I != 10) || (H != 32 && H != 64)) return LG_EINVAL;
+    const int64_t slab = 3 * H * H + 3 * H * I + 6 * H;
+    return std::max<int64_t>(1, nblocks_seq(B * S)) * slab * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int lg_gru_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+                          const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last, int64_t B,
+                          int64_t L, int64_t S, int64_t I, int64_t H, lg_stream_t stream) {
+    if (!dims_ok(B, L, S)) return LG_EINVAL;
+    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
+    if (gates && !h_seq) return LG_EINVAL;  // the backward needs both
+    if (B == 0) return LG_OK;
+    hipStream_t s = lg_stream(stream);
+    return H == 64 ? launch_fwd<64>(I == 10, gates != nullptr, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates,
+                                    h_last, B, L, S, s)
+                   : launch_fwd<32>(I == 10, gates != nullptr, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates,
+                                    h_last, B, L, S, s);
+}
+
 extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
-                          const float* b_ih, const float* b_hh, const float* h_seq, const float* dh_last, float* dx,
-                          float* dw_ih, float* dw_hh, float* db_ih, float* db_hh, int64_t B, int64_t L, int64_t S,
-                          int64_t I, int64_t Hd, void* workspace, lg_stream_t stream) {
-    if (B < 0 || L <= 0 || S <= 0 || L > INT32_MAX || S > INT32_MAX || B * S > INT32_MAX / 2) return LG_EINVAL;
-    if (Hd != H || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
-    if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_seq || !dh_last || !dw_ih || !dw_hh || !db_ih ||
-        !db_hh || !workspace || (I == 10 && !tfeat))
+                          const float* h_seq, const float* gates, const float* dh_last, float* dx, float* dw_ih,
+                          float* dw_hh, float* db_ih, float* db_hh, int64_t B, int64_t L, int64_t S, int64_t I,
+                          int64_t H, void* workspace, lg_stream_t stream) {
+    if (!dims_ok(B, L, S)) return LG_EINVAL;
+    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (!residual || !w_ih || !w_hh || !h_seq || !gates || !dh_last || !dw_ih || !dw_hh || !db_ih || !db_hh ||
+        !workspace || (I == 10 && !tfeat))
         return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     const int nb = static_cast<int>(std::max<int64_t>(1, nblocks_seq(B * S)));
     float* slab = static_cast<float*>(workspace);
-    const int len = static_cast<int>(G3 * H + G3 * I + 2 * G3);
+    const int64_t G3 = 3 * H, len = G3 * H + G3 * I + 2 * G3;
     if (B == 0) {
         if (hipMemsetAsync(slab, 0, sizeof(float) * len, s) != hipSuccess) return LG_EHIP;
     } else {
-        const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
-#define LG_GRU_BWD(UT, DX)                                                                                        \
-    k_gru_bwd<UT, DX><<<grid, 256, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, dh_last, dx, slab,     \
-                                           (int)B, (int)L, (int)S)
-        if (I == 10) {
-            if (dx) LG_GRU_BWD(true, true); else LG_GRU_BWD(true, false);
-        } else {
-            if (dx) LG_GRU_BWD(false, true); else LG_GRU_BWD(false, false);
-        }
-#undef LG_GRU_BWD
-        LG_RET_IF_LAUNCH_FAILED();
+        const int rc = H == 64 ? launch_bwd<64>(I == 10, dx != nullptr, residual, tfeat, w_ih, w_hh, h_seq, gates,
+                                                dh_last, dx, slab, B, L, S, s)
+                               : launch_bwd<32>(I == 10, dx != nullptr, residual, tfeat, w_ih, w_hh, h_seq, gates,
+                                                dh_last, dx, slab, B, L, S, s);
+        if (rc != LG_OK) return rc;
     }
-    const int G = B == 0 ? 1 : nb;
     const int64_t nWhh = G3 * H, nWih = G3 * I;
-    int rc = lg_launch_slab_reduce(slab, G, len, nWhh, dw_hh, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh, G, len, nWih, dw_ih, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih, G, len, G3, db_ih, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih + G3, G, len, G3, db_hh, s);
+    int rc = lg_launch_slab_reduce(slab, nb, len, nWhh, dw_hh, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh, nb, len, nWih, dw_ih, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih, nb, len, G3, db_ih, s);
+    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih + G3, nb, len, G3, db_hh, s);
     return rc;
 }

@@ -188,7 +188,7 @@ extern "C" int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N
     return LG_OK;
 }
 
-extern "C" int lg_abi_version(void) { return 1; }
+extern "C" int lg_abi_version(void) { return 2; }
 
 extern "C" const char* lg_strerror(int code) {
     switch (code) {

@@ -47,10 +47,9 @@ SIGNATURES = {
     "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32,
                                 _u64, _u32, _p, _p]),
     "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
-    "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
-    "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64]),
-    "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64,
-                          _p, _p]),
+    "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
+    "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
 }
 
 _lib = None

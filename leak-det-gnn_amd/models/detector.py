@@ -53,8 +53,8 @@ class SharedSensorGRUEncoder(nn.Module):
         if not r.is_cuda:
             raise RuntimeError("SharedSensorGRUEncoder runs on a ROCm GPU only (libleakgnn has no CPU path)")
         g = self.gru
-        if g.num_layers != 1 or g.hidden_size != 64 or g.bidirectional or not g.bias:
-            raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 64, bias")
+        if g.num_layers != 1 or g.hidden_size not in (32, 64) or g.bidirectional or not g.bias:
+            raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 32/64, bias")
         return ops.GRUEncoderFn.apply(r, tfeat if self.use_time else None, g.weight_ih_l0, g.weight_hh_l0,
                                       g.bias_ih_l0, g.bias_hh_l0)
 

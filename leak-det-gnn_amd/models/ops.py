@@ -451,28 +451,30 @@ class GRUEncoderFn(torch.autograd.Function):
         if tfeat is not None and tuple(tfeat.shape) != (B, L, 9):
             raise ValueError(f"tfeat must be (B, L, 9), got {tuple(tfeat.shape)}")
         need_bwd = any(ctx.needs_input_grad)
-        h_seq = torch.empty(L, B * S, H, device=residual.device) if need_bwd else None
-        h_last = torch.empty(B * S, H, device=residual.device)
-        with _timed("gru_fwd", residual.device):
+        dev = residual.device
+        h_seq = torch.empty(L, B * S, H, device=dev) if need_bwd else None
+        gates = torch.empty(L, B * S, 4, H, device=dev) if need_bwd else None
+        h_last = torch.empty(B * S, H, device=dev)
+        with _timed("gru_fwd", dev):
             check(lib.lg_gru_fwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(h_seq),
-                                 ptr(h_last), B, L, S, I, H, stream_of(residual)), "lg_gru_fwd")
+                                 ptr(gates), ptr(h_last), B, L, S, I, H, stream_of(residual)), "lg_gru_fwd")
         ctx.dims = (B, L, S, I, H)
-        ctx.save_for_backward(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq)
+        ctx.save_for_backward(residual, tfeat, w_ih, w_hh, h_seq, gates)
         return h_last.view(B, S, H)
 
     @staticmethod
     def backward(ctx, dh):
         lib = load_library()
-        residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq = ctx.saved_tensors
+        residual, tfeat, w_ih, w_hh, h_seq, gates = ctx.saved_tensors
         B, L, S, I, H = ctx.dims
         dev = residual.device
         need_dx = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
         dx = torch.empty(B * S, L, I, device=dev) if need_dx else None
         dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
-        db_ih, db_hh = torch.empty_like(b_ih), torch.empty_like(b_hh)
-        ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I)), device=dev, dtype=torch.uint8)
+        db_ih, db_hh = torch.empty(3 * H, device=dev), torch.empty(3 * H, device=dev)
+        ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I, H)), device=dev, dtype=torch.uint8)
         with _timed("gru_bwd", dev):
-            check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh), ptr(h_seq),
+            check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates),
                                  ptr(dh.contiguous()), ptr(dx), ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L,
                                  S, I, H, ptr(ws), stream_of(residual)), "lg_gru_bwd")
         dres = dtf = None

@@ -116,21 +116,22 @@ def main():
         whh = torch.randn(192, 64, device=dev) / 8
         bih, bhh = torch.randn(192, device=dev) / 4, torch.randn(192, device=dev) / 4
         hs = torch.empty(L, B * S, 64, device=dev)
+        gt = torch.empty(L, B * S, 4, 64, device=dev)
         hl = torch.empty(B * S, 64, device=dev)
-        f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(hl), B,
-                                         L, S, 10, 64, st), "gru fwd")
+        f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(gt),
+                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd")
         t = timeit(f, args.iters)
         flops = 2 * B * S * L * 192 * (64 + 10)
         res["gru_fwd"] = {"us": t, "TFLOPs": flops / t / 1e6}
         if "gru_bwd" in which:
             dh = torch.randn(B * S, 64, device=dev)
             dws = [torch.empty_like(t) for t in (wih, whh, bih, bhh)]
-            ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, 10)), device=dev, dtype=torch.uint8)
-            f = lambda: check(lib.lg_gru_bwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(dh),
-                                             None, ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), B, L, S, 10, 64,
+            ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)), device=dev, dtype=torch.uint8)
+            f = lambda: check(lib.lg_gru_bwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(hs), ptr(gt), ptr(dh), None,
+                                             ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), B, L, S, 10, 64,
                                              ptr(ws), st), "gru bwd")
             t = timeit(f, args.iters)
-            res["gru_bwd"] = {"us": t, "TFLOPs": 3 * flops / t / 1e6}
+            res["gru_bwd"] = {"us": t, "TFLOPs": 2 * flops / t / 1e6}
     for k, v in res.items():
         print(k, json.dumps({a: round(b, 2) for a, b in v.items()}))
 
