@@ -116,11 +116,11 @@ int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float*
  * Replaces: GCNConv.forward (lin -> propagate -> +bias, detector.py:199) and the
  * following F.relu + dropout (detector.py:200-201):
  *   y = dropout(relu( Ahat (x W^T) + b ))  computed as  (Ahat x) W^T + b
- * Each 64-lane wavefront owns a 16-row tile and computes it transposed,
- * y^T = W (Ahat x)^T: every lane gathers (CSR segmented reduce, fp32) exactly the
- * MFMA B-operand fragment of its row, the D x D product runs on MFMA
- * (v_mfma_f32_16x16x4_f32, exact fp32) with W in registers, and the accumulator is
- * already in row-store layout for the bias/ReLU/dropout epilogue.
+ * Each 64-lane wavefront owns 16-row tiles of a persistent, XCD-aware schedule:
+ * it gathers a whole tile (CSR segmented reduce in entry order, fp32, 16 lanes per
+ * row) into LDS, computes it transposed, y^T = W (Ahat x)^T, on MFMA
+ * (v_mfma_f32_16x16x4_f32, exact fp32) while the next tile's row loads are in
+ * flight, and applies bias/ReLU/dropout before whole-row stores.
  *   rowptr/col/w : CSR from lg_graph_build;  x, y : fp32 [B][N][D];  W : fp32 [D][D]
  *   (nn.Linear layout [out][in]);  bias : fp32 [D] or NULL.
  *   Dropout: keep element (row, c) iff hash(seed, salt, row*D + c) >= p, scale 1/(1-p).
@@ -145,12 +145,16 @@ int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,
  *   dx_out = LG_F_MASK_OUT ? dx * scale_out * [x > 0] : dx
  * Replaces: the autograd backward of GCNConv (lin, propagate, bias) and of the
  * relu/dropout pairs around it (detector.py:189-190, 198-201).
+ *   dnode_bias = sum over rows b*N + n with node_slot[n] < 0 of dx_out
+ *              (the node-init bias gradient, detector.py:184-190: rows without a
+ *              sensor are relu(bias)); node_slot / dnode_bias both NULL to skip.
  *   y may be NULL unless LG_F_MASK_IN;  db may be NULL.
  *   workspace : lg_gcn_bwd_workspace_bytes(D) bytes. */
 int64_t lg_gcn_bwd_workspace_bytes(int64_t D);
 int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t,
                const float* dy, const float* y, const float* x, const float* W,
                float* dx_out, float* dW, float* db,
+               const int32_t* node_slot, float* dnode_bias,
                int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                int flags, float scale_in, float scale_out,
                void* workspace, lg_stream_t stream);
@@ -176,18 +180,19 @@ int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, cons
  *   logits[b][p] = W2 . dropout(relu(W1 [h_u, h_v, |h_u - h_v|] + b1)) + b2
  * feat (B,P,3D) and the hidden layer are never materialised.  W1 : fp32 [hidden][3D]
  * (edge_head.mlp.0.weight), b1 [hidden], W2 [hidden] (mlp.3.weight), b2 [1];
- * logits : fp32 [B][P].  hidden must be 128; D in {32, 64}.  Dropout as lg_gcn_fwd,
- * index (b*P + p)*hidden + unit. */
+ * logits : fp32, element (b, p) at logits[b*ldo + p] (ldo >= P; ldo = P+1 writes the
+ * pipe columns of detector.py:216's (B, P+1) output in place).  hidden must be 128;
+ * D in {32, 64}.  Dropout as lg_gcn_fwd, index (b*P + p)*hidden + unit. */
 int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                     const float* w2, const float* b2, float* logits,
+                     const float* w2, const float* b2, float* logits, int64_t ldo,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
-/* Backward of lg_edge_head_fwd (same flags/seed/salt): dlogits fp32 [B][P] ->
+/* Backward of lg_edge_head_fwd (same flags/seed/salt): dlogits (row stride ldo) ->
  * dpipe fp32 [B][P][2][D] (grads w.r.t. h_u, h_v per pipe), dw1/db1/dw2/db2
  * (overwritten; deterministic fixed-order reduction of per-workgroup slabs). */
 int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden);
 int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                     const float* w2, const float* dlogits, float* dpipe,
+                     const float* w2, const float* dlogits, int64_t ldo, float* dpipe,
                      float* dw1, float* db1, float* dw2, float* db2,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt,
@@ -197,6 +202,28 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)
  * (detector.py:214-215).   x : fp32 [B][N][D];  out : fp32 [B][D] */
 int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N, int64_t D, lg_stream_t stream);
+
+/* K10 + NoLeakHead fused (detector.py:91-102 applied at :214-216):
+ *   pooled[b] = mean_n x[b][n]                                  (global_mean_pool)
+ *   hid[b]    = dropout(relu(pooled[b] W1^T + b1))              (noleak_head.mlp.0-2)
+ *   logits[b*ldo + col] = hid[b] . w2 + b2                      (mlp.3, squeeze)
+ * x : fp32 [B][N][D];  w1 [hidden][D], b1 [hidden], w2 [hidden], b2 [1];
+ * pooled [B][D] and hid [B][hidden] are outputs saved for the backward.  hidden must
+ * be 128; D in {32, 64}; dropout index b*hidden + unit.  With col = P and ldo = P+1
+ * this writes the no-leak column of the (B, P+1) logits in place. */
+int lg_pool_head_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                     float* pooled, float* hid, float* logits, int64_t ldo, int64_t col,
+                     int64_t B, int64_t N, int64_t D, int64_t hidden,
+                     int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+/* Backward: dlogits[b*ldo + col] -> dpooled fp32 [B][D] (pass to lg_pipe_scatter_bwd as
+ * dpool), dw1/db1/dw2/db2 (overwritten; deterministic; db2 summed in fp64).  The ReLU /
+ * dropout masks are read back from hid (> 0), scaled by 1/(1-p) under LG_F_DROPOUT. */
+int64_t lg_pool_head_bwd_workspace_bytes(int64_t B, int64_t D, int64_t hidden);
+int lg_pool_head_bwd(const float* pooled, const float* hid, const float* w1, const float* w2,
+                     const float* dlogits, int64_t ldo, int64_t col, float* dpooled,
+                     float* dw1, float* db1, float* dw2, float* db2,
+                     int64_t B, int64_t D, int64_t hidden, int flags, float dropout_p,
+                     void* workspace, lg_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * SharedSensorGRUEncoder (detector.py:28-73): one nn.GRU(1 [+9], H) over the

@@ -34,6 +34,11 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q + (ks & 3); }
+// row r = b*P + p of the (B, P) logit space -> element (b, p) of a buffer with row stride ldo
+__device__ __forceinline__ int64_t lg_row_index(int64_t r, const lg_fastdiv& fdP, int64_t ldo) {
+    const uint32_t b = lg_div(static_cast<uint32_t>(r), fdP);
+    return static_cast<int64_t>(b) * ldo + (static_cast<uint32_t>(r) - b * fdP.d);
+}
 
 template <int D>
 struct EG {
@@ -103,8 +108,8 @@ template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-           float* __restrict__ logit, int64_t N, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout, float p_drop,
-           float dscale, uint64_t seed, uint32_t salt) {
+           float* __restrict__ logit, int64_t ldo, int64_t N, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout,
+           float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
     __shared__ __attribute__((aligned(16))) float ft[TR * G::FS];
     __shared__ float part[NW][TR];
@@ -141,7 +146,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             float tot = part[0][threadIdx.x];
 #pragma unroll
             for (int i = 1; i < NW; ++i) tot += part[i][threadIdx.x];
-            if (r < BP) logit[r] = tot + bias2;
+            if (r < BP) logit[lg_row_index(r, fdP, ldo)] = tot + bias2;
         }
         __syncthreads();
     }
@@ -151,7 +156,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
-           const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ dlogit,
+           const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ dlogit, int64_t ldo,
            float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t N, lg_fastdiv fdP,
            int64_t BP, int64_t ntiles, int dropout, float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
@@ -190,7 +195,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         const int64_t row0 = tile * TR;
         gather_tile<D>(ends, h, ft, row0, BP, fdP, N);
         const bool rv = row0 + j < BP;
-        const float dl = rv ? dlogit[row0 + j] : 0.f;
+        const float dl = rv ? dlogit[lg_row_index(row0 + j, fdP, ldo)] : 0.f;
         __syncthreads();
         const f32x4 acc = hidden_tile<D>(ft, aw, b1v, j, q);
 #pragma unroll
@@ -286,14 +291,6 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     if (w == 0 && lane == 0) db2slab[blockIdx.x] = db2;
 }
 
-__global__ void k_sum_f64(const double* __restrict__ v, int n, float* __restrict__ out) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        double s = 0.0;
-        for (int i = 0; i < n; ++i) s += v[i];
-        out[0] = static_cast<float>(s);
-    }
-}
-
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 int bwd_grid(int64_t ntiles) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ntiles, lg_num_cus()))); }
@@ -301,7 +298,8 @@ int bwd_grid(int64_t ntiles) { return static_cast<int>(std::max<int64_t>(1, std:
 }  // namespace
 
 extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                                const float* w2, const float* b2, float* logits, int64_t B, int64_t N, int64_t P,
+                                const float* w2, const float* b2, float* logits, int64_t ldo, int64_t B, int64_t N,
+                                int64_t P,
                                 int64_t D, int64_t hidden, int flags, float dropout_p, uint64_t seed, uint32_t salt,
                                 lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
@@ -310,7 +308,7 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
     const int64_t BP = B * P;
     if (BP == 0) return LG_OK;
-    if (!ends || !h || !w1 || !b1 || !w2 || !b2 || !logits) return LG_EINVAL;
+    if (!ends || !h || !w1 || !b1 || !w2 || !b2 || !logits || ldo < P) return LG_EINVAL;
     if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
     const int64_t ntiles = cdiv(BP, TR);
@@ -318,10 +316,10 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     if (D == 64)
-        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, fdP, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, N, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     else
-        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, N, fdP, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, N, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
@@ -335,7 +333,8 @@ extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_
 }
 
 extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                                const float* w2, const float* dlogits, float* dpipe, float* dw1, float* db1,
+                                const float* w2, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
+                                float* db1,
                                 float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                                 int flags, float dropout_p, uint64_t seed, uint32_t salt, void* workspace,
                                 lg_stream_t stream) {
@@ -345,7 +344,7 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
     if (!h || !w1 || !b1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !workspace) return LG_EINVAL;
     const int64_t BP = B * P;
-    if (BP > 0 && (!ends || !dlogits || !dpipe)) return LG_EINVAL;
+    if (BP > 0 && (!ends || !dlogits || !dpipe || ldo < P)) return LG_EINVAL;
     if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(std::max<int64_t>(P, 1)));
     const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), TR);
@@ -359,19 +358,14 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else if (D == 64) {
-        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
+        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     } else {
-        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
+        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     }
     LG_RET_IF_LAUNCH_FAILED();
     const int64_t K3 = 3 * D;
-    int rc = lg_launch_slab_reduce(slab, grid, SL, HID * K3, dw1, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + HID * K3, grid, SL, HID, db1, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + HID * K3 + HID, grid, SL, HID, dw2, s);
-    if (rc != LG_OK) return rc;
-    k_sum_f64<<<1, 64, 0, s>>>(dslab, grid, db2);
-    LG_RET_IF_LAUNCH_FAILED();
-    return LG_OK;
+    const LgSlabSeg segs[3] = {{0, HID * K3, dw1}, {HID * K3, HID, db1}, {HID * K3 + HID, HID, dw2}};
+    return lg_launch_slab_reduce_multi(slab, grid, SL, segs, 3, dslab, db2, s);
 }

@@ -332,16 +332,19 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 
 // ------------------------------------------------------------------ backward
 // dz = MASK_IN ? dy*scale_in*[y>0] : dy ; t = Ahat^T dz ; dx = t W ; dW += t^T x ; db += sum dz
-template <int D, bool MASK_IN, bool CSR_LDS>
+// NB: also sum dx_out over the rows whose node has node_slot < 0 (the node-init bias
+// gradient, detector.py:184-190: rows without a sensor are relu(bias) + dropout).
+template <int D, bool MASK_IN, bool CSR_LDS, bool NB>
 __global__ void __launch_bounds__(64 * kBwdWaves, 2)
 k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, const float* __restrict__ wgt,
           const float* __restrict__ dy, const float* __restrict__ yv, const float* __restrict__ x,
-          const float* __restrict__ W, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N, lg_fastdiv fdN,
-          uint32_t R, int64_t ntiles, int mask_out, float scale_in, float scale_out, int csr_words, int accumulate) {
+          const float* __restrict__ W, const int32_t* __restrict__ node_slot, float* __restrict__ dxo,
+          float* __restrict__ slab, uint32_t N, lg_fastdiv fdN, uint32_t R, int64_t ntiles, int mask_out,
+          float scale_in, float scale_out, int csr_words, int accumulate) {
     using G = Geo<D>;
     constexpr int SW = D + 4;  // W rows in LDS, conflict-free column reads
     constexpr int WBUF = 2 * G::TILE;
-    constexpr int L = D * D + D;
+    constexpr int L = D * D + 2 * D;  // slab row: dW, db, d(node bias)
     static_assert(kBwdWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const Rows<D> dys = rows_of<D>(dy, R), ms = rows_of<D>(MASK_IN ? yv : dy, R), xs = rows_of<D>(x, R),
@@ -373,6 +376,9 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 #pragma unroll
         for (int b = 0; b < G::MT; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // features 4fg..4fg+3, summed over this lane's rows
+    f32x4 nbacc[NB ? G::MT : 1];              // NB: features 16mt + 4q + reg over this lane's rows j
+#pragma unroll
+    for (int mt = 0; mt < (NB ? G::MT : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const TileRange tr = xcd_tiles(ntiles, wave, kBwdWaves);
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
@@ -436,12 +442,28 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
                 for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
             }
         }
+        if constexpr (NB) {
+            const uint32_t r = r0 + j;
+            const uint32_t rr = r < R ? r : 0u;
+            const bool bias_row = r < R && node_slot[rr - lg_div(rr, fdN) * fdN.d] < 0;
+#pragma unroll
+            for (int mt = 0; mt < G::MT; ++mt)
+                if (bias_row) nbacc[mt] += o[mt];
+        }
         wave_lds_sync();
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
         wave_lds_sync();
         store_tile<D>(tl, dxs, r0, R, lane);
         wave_lds_sync();
+    }
+    if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+            for (int mt = 0; mt < G::MT; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
     }
 
     // ---- per-block reduction of dW / db (fixed wave order -> deterministic)
@@ -465,6 +487,11 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
             if (lane < G::LPR)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
+            if (NB && j == 0)
+#pragma unroll
+                for (int mt = 0; mt < G::MT; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
         }
     }
     __syncthreads();
@@ -558,19 +585,21 @@ int fwd_dispatch(bool cl, bool drop, const int32_t* rowptr, const int32_t* col, 
 #undef LG_FWD_ARGS
 }
 
-template <int D, bool MI, bool CL>
+template <int D, bool MI, bool CL, bool NB>
 int launch_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy, const float* y,
-               const float* x, const float* W, float* dx, float* slab, int64_t Bc, int64_t N, int64_t csr_bytes,
-               int mask_out, float scale_in, float scale_out, int accumulate, int* grid_io, hipStream_t s) {
+               const float* x, const float* W, const int32_t* node_slot, float* dx, float* slab, int64_t Bc,
+               int64_t N, int64_t csr_bytes, int mask_out, float scale_in, float scale_out, int accumulate,
+               int* grid_io, hipStream_t s) {
     using G = Geo<D>;
     const int64_t R = Bc * N, ntiles = ceil_div(R, kTileRows);
     const int64_t csr_words = CL ? csr_bytes / 4 : 0;
     const int64_t dyn = 4 * (((csr_words + 3) & ~3LL) + kBwdWaves * 2 * G::TILE + D * (D + 4));
-    auto kern = k_gcn_bwd<D, MI, CL>;
+    auto kern = k_gcn_bwd<D, MI, CL, NB>;
     if (!allow_lds(kern, dyn)) return LG_EHIP;
     // every chunk of a split launch uses the first chunk's grid (the slab rows it accumulates into)
     if (*grid_io == 0) *grid_io = resident_grid(kern, 64 * kBwdWaves, dyn, ceil_div(ntiles, kBwdWaves), 2);
-    kern<<<*grid_io, 64 * kBwdWaves, dyn, s>>>(rowptr_t, col_t, w_t, dy, y, x, W, dx, slab, static_cast<uint32_t>(N),
+    kern<<<*grid_io, 64 * kBwdWaves, dyn, s>>>(rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab,
+                                                static_cast<uint32_t>(N),
                                                 lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
                                                 ntiles, mask_out, scale_in, scale_out, static_cast<int>(csr_words),
                                                 accumulate);
@@ -578,16 +607,29 @@ int launch_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, 
     return LG_OK;
 }
 
+template <int D, bool NB>
+int bwd_dispatch_nb(bool mi, bool cl, const int32_t* rowptr_t, const int32_t* col_t, const float* w_t,
+                    const float* dy, const float* y, const float* x, const float* W, const int32_t* node_slot,
+                    float* dx, float* slab, int64_t Bc, int64_t N, int64_t csr_bytes, int mask_out, float scale_in,
+                    float scale_out, int accumulate, int* grid_io, hipStream_t s) {
+#define LG_BWD_ARGS                                                                                                 \
+    rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab, Bc, N, csr_bytes, mask_out, scale_in, scale_out, accumulate, \
+        grid_io, s
+    if (mi) return cl ? launch_bwd<D, true, true, NB>(LG_BWD_ARGS) : launch_bwd<D, true, false, NB>(LG_BWD_ARGS);
+    return cl ? launch_bwd<D, false, true, NB>(LG_BWD_ARGS) : launch_bwd<D, false, false, NB>(LG_BWD_ARGS);
+#undef LG_BWD_ARGS
+}
+
 template <int D>
 int bwd_dispatch(bool mi, bool cl, const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy,
-                 const float* y, const float* x, const float* W, float* dx, float* slab, int64_t Bc, int64_t N,
-                 int64_t csr_bytes, int mask_out, float scale_in, float scale_out, int accumulate, int* grid_io,
-                 hipStream_t s) {
-#define LG_BWD_ARGS \
-    rowptr_t, col_t, w_t, dy, y, x, W, dx, slab, Bc, N, csr_bytes, mask_out, scale_in, scale_out, accumulate, grid_io, s
-    if (mi) return cl ? launch_bwd<D, true, true>(LG_BWD_ARGS) : launch_bwd<D, true, false>(LG_BWD_ARGS);
-    return cl ? launch_bwd<D, false, true>(LG_BWD_ARGS) : launch_bwd<D, false, false>(LG_BWD_ARGS);
-#undef LG_BWD_ARGS
+                 const float* y, const float* x, const float* W, const int32_t* node_slot, float* dx, float* slab,
+                 int64_t Bc, int64_t N, int64_t csr_bytes, int mask_out, float scale_in, float scale_out,
+                 int accumulate, int* grid_io, hipStream_t s) {
+    if (node_slot)
+        return bwd_dispatch_nb<D, true>(mi, cl, rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab, Bc, N,
+                                        csr_bytes, mask_out, scale_in, scale_out, accumulate, grid_io, s);
+    return bwd_dispatch_nb<D, false>(mi, cl, rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab, Bc, N, csr_bytes,
+                                     mask_out, scale_in, scale_out, accumulate, grid_io, s);
 }
 
 template <int D, bool CL>
@@ -663,15 +705,17 @@ extern "C" int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w
 
 extern "C" int64_t lg_gcn_bwd_workspace_bytes(int64_t D) {
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
-    return static_cast<int64_t>(bwd_grid_max()) * (D * D + D) * static_cast<int64_t>(sizeof(float));
+    return static_cast<int64_t>(bwd_grid_max()) * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));
 }
 
 extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy,
                           const float* y, const float* x, const float* W, float* dx_out, float* dW, float* db,
-                          int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags, float scale_in,
-                          float scale_out, void* workspace, lg_stream_t stream) {
+                          const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
+                          int64_t nnz_cap, int flags, float scale_in, float scale_out, void* workspace,
+                          lg_stream_t stream) {
     if (B < 0 || N <= 0 || nnz_cap < 0) return LG_EINVAL;
     if (!rowptr_t || !col_t || !w_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
+    if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     if (mask_in && !y) return LG_EINVAL;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
@@ -688,15 +732,14 @@ extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const f
         const float* yc = y ? y + off : nullptr;
         const int accumulate = b0 > 0 ? 1 : 0;
         const int rc = D == 64 ? bwd_dispatch<64>(mask_in, csr != 0, rowptr_t, col_t, w_t, dy + off, yc, x + off, W,
-                                                  dx_out + off, slab, Bc, N, csr, mask_out, scale_in, scale_out,
-                                                  accumulate, &grid, s)
+                                                  node_slot, dx_out + off, slab, Bc, N, csr, mask_out, scale_in,
+                                                  scale_out, accumulate, &grid, s)
                                : bwd_dispatch<32>(mask_in, csr != 0, rowptr_t, col_t, w_t, dy + off, yc, x + off, W,
-                                                  dx_out + off, slab, Bc, N, csr, mask_out, scale_in, scale_out,
-                                                  accumulate, &grid, s);
+                                                  node_slot, dx_out + off, slab, Bc, N, csr, mask_out, scale_in,
+                                                  scale_out, accumulate, &grid, s);
         if (rc != LG_OK) return rc;
     }
-    const int64_t L = D * D + D;
-    int rc = lg_launch_slab_reduce(slab, grid, L, D * D, dW, s);
-    if (rc == LG_OK && db) rc = lg_launch_slab_reduce(slab + D * D, grid, L, D, db, s);
-    return rc;
+    const int64_t L = D * D + 2 * D;
+    const LgSlabSeg segs[3] = {{0, D * D, dW}, {D * D, D, db}, {D * D + D, D, dnode_bias}};
+    return lg_launch_slab_reduce_multi(slab, grid, L, segs, 3, nullptr, nullptr, s);
 }

@@ -463,9 +463,7 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
         if (rc != LG_OK) return rc;
     }
     const int64_t nWhh = G3 * H, nWih = G3 * I;
-    int rc = lg_launch_slab_reduce(slab, nb, len, nWhh, dw_hh, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh, nb, len, nWih, dw_ih, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih, nb, len, G3, db_ih, s);
-    if (rc == LG_OK) rc = lg_launch_slab_reduce(slab + nWhh + nWih + G3, nb, len, G3, db_hh, s);
-    return rc;
+    const LgSlabSeg segs[4] = {{0, nWhh, dw_hh}, {nWhh, nWih, dw_ih}, {nWhh + nWih, G3, db_ih},
+                               {nWhh + nWih + G3, G3, db_hh}};
+    return lg_launch_slab_reduce_multi(slab, nb, len, segs, 4, nullptr, nullptr, s);
 }

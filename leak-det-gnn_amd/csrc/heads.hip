@@ -79,28 +79,6 @@ k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict
     }
 }
 
-// One block per window: 256 threads = RPB row groups x LPR lanes; LDS fold of the groups.
-template <int D>
-__global__ void __launch_bounds__(256)
-k_mean_pool(const float* __restrict__ x, float* __restrict__ out, int64_t N) {
-    constexpr int LPR = D / 4, RPB = 256 / LPR;
-    __shared__ f32x4 part[256];
-    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-    const int64_t b = blockIdx.x;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t n = rl; n < N; n += RPB) acc += ld4(x + (b * N + n) * D + 4 * fg);
-    part[threadIdx.x] = acc;
-    __syncthreads();
-    if (rl == 0) {
-        f32x4 s = part[fg];
-        for (int g = 1; g < RPB; ++g) s += part[g * LPR + fg];
-        const float cnt = static_cast<float>(N);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] = s[k] / cnt;
-        st4(out + b * D + 4 * fg, s);
-    }
-}
-
 inline unsigned row_grid(int64_t rows, int D) {
     const int64_t rpb = 256 / (D / 4);
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, rpb), 16LL * lg_num_cus())));
@@ -174,21 +152,7 @@ extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc
     return LG_OK;
 }
 
-extern "C" int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N, int64_t D, lg_stream_t stream) {
-    if (B < 0 || N <= 0) return LG_EINVAL;
-    if (B == 0) return LG_OK;
-    if (!x || !out || B > INT32_MAX) return LG_EINVAL;
-    hipStream_t s = lg_stream(stream);
-    switch (D) {
-        case 64: k_mean_pool<64><<<static_cast<unsigned>(B), 256, 0, s>>>(x, out, N); break;
-        case 32: k_mean_pool<32><<<static_cast<unsigned>(B), 256, 0, s>>>(x, out, N); break;
-        default: return LG_EUNSUPPORTED;
-    }
-    LG_RET_IF_LAUNCH_FAILED();
-    return LG_OK;
-}
-
-extern "C" int lg_abi_version(void) { return 2; }
+extern "C" int lg_abi_version(void) { return 3; }
 
 extern "C" const char* lg_strerror(int code) {
     switch (code) {

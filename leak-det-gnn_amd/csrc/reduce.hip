@@ -1,49 +1,98 @@
 // Deterministic slab reduction shared by the backward kernels:
-// out[i] = sum_g slab[g * stride + i], i < len
-// in a fixed order.  One 1024-thread block per 64 columns: wave w sums slabs
-// g = w, w + 16, ... for its column (one column per lane, coalesced rows), then the
-// 16 wave partials are added in wave order through LDS.  Per-column work and the
-// combine order depend only on (G, len), never on scheduling.
+//   seg k:  out_k[i] = sum_g slab[g * stride + off_k + i],  i < len_k
+// in a fixed order, all segments of one backward op in ONE launch.  One 1024-thread
+// block per 64 columns of a segment: wave w sums slabs g = w, w + 16, ... for its
+// column (one column per lane, coalesced rows), then the 16 wave partials are added
+// in wave order through LDS.  An optional fp64 column (sum of G doubles, used for
+// the cancellation-heavy output-bias gradients) is reduced by one extra block as a
+// fixed-shape tree.  Per-column work and the combine order depend only on (G, len),
+// never on scheduling.
 #include "common.h"
 #include "reduce.h"
 
 namespace {
 
-__global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ slab, int G, int64_t stride,
-                                                      int64_t len, float* __restrict__ out) {
-    __shared__ float part[16][64];
+struct Segs {
+    int64_t off[kLgMaxSlabSegs];
+    int64_t len[kLgMaxSlabSegs];
+    float* out[kLgMaxSlabSegs];
+    int first[kLgMaxSlabSegs + 1];  // first block of each segment; first[n] = total column blocks
+    int n;
+};
+
+__global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ slab, int G, int64_t stride, Segs sg,
+                                                      const double* __restrict__ dslab, float* __restrict__ dout) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t col = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+    const int b = blockIdx.x;
+    if (b >= sg.first[sg.n]) {  // fp64 column: 1024 strided partials, then a fixed tree
+        __shared__ double dp[1024];
+        double acc = 0.0;
+        for (int g = threadIdx.x; g < G; g += 1024) acc += dslab[g];
+        dp[threadIdx.x] = acc;
+        __syncthreads();
+        for (int h = 512; h > 0; h >>= 1) {
+            if (threadIdx.x < h) dp[threadIdx.x] += dp[threadIdx.x + h];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) dout[0] = static_cast<float>(dp[0]);
+        return;
+    }
+    int k = 0;
+    while (k + 1 < sg.n && b >= sg.first[k + 1]) ++k;
+    const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 64 + lane;
+    const int64_t len = sg.len[k];
+    const float* src = slab + sg.off[k];
+    __shared__ float part[16][64];
     float acc = 0.f;
     if (col < len) {
         int g = w;
         for (; g + 48 < G; g += 64) {  // four independent loads in flight
-            const float a = slab[static_cast<int64_t>(g) * stride + col];
-            const float b = slab[static_cast<int64_t>(g + 16) * stride + col];
-            const float c = slab[static_cast<int64_t>(g + 32) * stride + col];
-            const float d = slab[static_cast<int64_t>(g + 48) * stride + col];
+            const float a = src[static_cast<int64_t>(g) * stride + col];
+            const float bb = src[static_cast<int64_t>(g + 16) * stride + col];
+            const float c = src[static_cast<int64_t>(g + 32) * stride + col];
+            const float d = src[static_cast<int64_t>(g + 48) * stride + col];
             acc += a;
-            acc += b;
+            acc += bb;
             acc += c;
             acc += d;
         }
-        for (; g < G; g += 16) acc += slab[static_cast<int64_t>(g) * stride + col];
+        for (; g < G; g += 16) acc += src[static_cast<int64_t>(g) * stride + col];
     }
     part[w][lane] = acc;
     __syncthreads();
     if (w == 0 && col < len) {
         float s = part[0][lane];
         for (int i = 1; i < 16; ++i) s += part[i][lane];
-        out[col] = s;
+        sg.out[k][col] = s;
     }
 }
 
 }  // namespace
 
-int lg_launch_slab_reduce(const float* slab, int G, int64_t stride, int64_t len, float* out, hipStream_t s) {
-    if (len <= 0) return LG_OK;
-    const unsigned grid = static_cast<unsigned>((len + 63) / 64);
-    k_slab_reduce<<<grid, 1024, 0, s>>>(slab, G, stride, len, out);
+int lg_launch_slab_reduce_multi(const float* slab, int G, int64_t stride, const LgSlabSeg* segs, int nseg,
+                                const double* dslab, float* dout, hipStream_t s) {
+    if (nseg < 0 || nseg > kLgMaxSlabSegs || G < 0 || (dslab && !dout)) return LG_EINVAL;
+    Segs sg{};
+    int blocks = 0, n = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (segs[i].out == nullptr || segs[i].len <= 0) continue;
+        sg.off[n] = segs[i].off;
+        sg.len[n] = segs[i].len;
+        sg.out[n] = segs[i].out;
+        sg.first[n] = blocks;
+        blocks += static_cast<int>((segs[i].len + 63) / 64);
+        ++n;
+    }
+    sg.first[n] = blocks;
+    sg.n = n;
+    const int total = blocks + (dslab ? 1 : 0);
+    if (total == 0) return LG_OK;
+    k_slab_reduce<<<total, 1024, 0, s>>>(slab, G, stride, sg, dslab, dout);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
+}
+
+int lg_launch_slab_reduce(const float* slab, int G, int64_t stride, int64_t len, float* out, hipStream_t s) {
+    const LgSlabSeg seg{0, len, out};
+    return lg_launch_slab_reduce_multi(slab, G, stride, &seg, 1, nullptr, nullptr, s);
 }

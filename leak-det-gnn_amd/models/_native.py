@@ -37,16 +37,21 @@ SIGNATURES = {
     "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_gcn_bwd_workspace_bytes": (_i64, [_i64]),
-    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32, _p,
-                          _p]),
+    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32,
+                          _p, _p]),
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
-    "lg_edge_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32,
-                                _p]),
+    "lg_edge_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64,
+                                _u32, _p]),
     "lg_edge_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
-    "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32,
-                                _u64, _u32, _p, _p]),
+    "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32,
+                                _f32, _u64, _u32, _p, _p]),
     "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
+    "lg_pool_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64,
+                                _u32, _p]),
+    "lg_pool_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "lg_pool_head_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p,
+                                _p]),
     "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _p]),

@@ -54,24 +54,20 @@ class GradAllReduce:
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
             return
         world = dist.get_world_size(self.group)
+        # one gather into the bucket, one collective, gradients re-pointed at the bucket
+        grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
+                 for p in self.params]
+        torch.cat(grads, out=self.flat)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:  # gloo has no AVG
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat.div_(world)
         off = 0
-        views = []
         for p in self.params:
             n = p.numel()
-            v = self.flat[off:off + n].view_as(p)
-            if p.grad is None:
-                v.zero_()
-            else:
-                v.copy_(p.grad)
-            views.append(v)
+            p.grad = self.flat[off:off + n].view_as(p)
             off += n
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.div_(world)
-        for p, v in zip(self.params, views):
-            if p.grad is None:
-                p.grad = v.clone()
-            else:
-                p.grad.copy_(v)
 
 
 def shard_range(global_batch: int, rank: int, world: int) -> range:

@@ -233,7 +233,8 @@ class GCNLayerFn(torch.autograd.Function):
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
         with _timed("gcn_bwd", x.device):
             check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), None, ptr(x), ptr(weight),
-                                 ptr(dx), ptr(dW), ptr(db), 1, Ntot, D, g.nnz_cap, 0, 1.0, 1.0, ptr(ws), stream_of(x)),
+                                 ptr(dx), ptr(dW), ptr(db), None, None, 1, Ntot, D, g.nnz_cap, 0, 1.0, 1.0, ptr(ws),
+                                 stream_of(x)),
                   "lg_gcn_bwd")
         return dx, dW, (db if ctx.has_bias else None), None
 
@@ -310,95 +311,115 @@ class GNNTrunkFn(torch.autograd.Function):
         dy = grad_out.contiguous()
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dy.device, dtype=torch.uint8)
         grads_wb: List[Optional[torch.Tensor]] = [None] * (2 * L)
+        dbias = torch.empty(D, device=dy.device, dtype=torch.float32)
         for l in range(L - 1, -1, -1):
             flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0)
             dx = torch.empty_like(dy)
             dW = torch.empty(D, D, device=dy.device, dtype=torch.float32)
             db = torch.empty(D, device=dy.device, dtype=torch.float32)
+            first = l == 0  # layer 0's dx is the node-init gradient: its bias rows are summed in-kernel
             with _timed("gcn_bwd", dy.device):
                 check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
-                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), B, N, D, g.nnz_cap, flags, ctx.scale,
-                                     ctx.scale, ptr(ws), st), "lg_gcn_bwd")
+                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), ptr(cfg.sensor_slot) if first else None,
+                                     ptr(dbias) if first else None, B, N, D, g.nnz_cap, flags, ctx.scale, ctx.scale,
+                                     ptr(ws), st), "lg_gcn_bwd")
             grads_wb[2 * l], grads_wb[2 * l + 1] = dW, db
             dy = dx  # already masked by the previous op's relu/dropout
         dproj = dy.index_select(1, cfg.sensor_idx)
         if cfg.slot_live is not None:
             dproj = dproj * cfg.slot_live.view(1, -1, 1)
-        dbias = dy.index_select(1, cfg.nonsensor_idx).sum(dim=(0, 1))
+        if L == 0:
+            dbias = dy.index_select(1, cfg.nonsensor_idx).sum(dim=(0, 1))
         return (None, dproj, dbias, *grads_wb)
 
 
-EDGE_HEAD_SALT = 101  # dropout stream of the EdgeHead hidden layer (trunk layers use salts 0..L)
+EDGE_HEAD_SALT = 101    # dropout stream of the EdgeHead hidden layer (trunk layers use salts 0..L)
+NOLEAK_HEAD_SALT = 102  # dropout stream of the NoLeakHead hidden layer
 
 
 @dataclass
 class HeadsConfig:
     inc: Incidence
-    dropout_p: float
+    dropout_p: float         # EdgeHead dropout (edge_head.mlp[2].p)
     training: bool
+    noleak_p: Optional[float] = None  # NoLeakHead dropout (noleak_head.mlp[2].p); None -> dropout_p
 
 
 class HeadsFn(torch.autograd.Function):
-    """EdgeHead over every pipe + per-window mean pool (detector.py:87-88, 206-215).
+    """EdgeHead over every pipe + mean pool + NoLeakHead (detector.py:87-102, 206-216).
 
-    forward:  pipe_logits (B, P) = lg_edge_head_fwd (gather -> MFMA MLP -> dot, fused),
-              pooled (B, D)      = lg_mean_pool_fwd
-    backward: lg_edge_head_bwd -> per-pipe endpoint grads, then ONE deterministic
-              incidence reduce (lg_pipe_scatter_bwd) that also adds dpooled / N.
+    forward:  logits (B, P+1) written in place: columns [0, P) by lg_edge_head_fwd (gather
+              -> MFMA MLP -> dot, fused), column P by lg_pool_head_fwd (mean pool +
+              NoLeakHead) — the torch.cat of detector.py:216 is never a separate copy.
+    backward: lg_edge_head_bwd -> per-pipe endpoint grads; lg_pool_head_bwd -> dpooled and
+              the NoLeakHead weight grads; ONE deterministic incidence reduce
+              (lg_pipe_scatter_bwd) adds dpooled / N to every node row.
     """
 
     @staticmethod
-    def forward(ctx, cfg: HeadsConfig, h, w1, b1, w2, b2):
+    def forward(ctx, cfg: HeadsConfig, h, w1, b1, w2, b2, nw1, nb1, nw2, nb2):
         lib = load_library()
         h = h.contiguous()
-        require_device(h, w1, b1, w2, b2)
+        require_device(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
         B, N, D = h.shape
         _check_d(D)
-        hidden = w1.shape[0]
+        hidden, nhidden = w1.shape[0], nw1.shape[0]
         inc = cfg.inc
         P = inc.num_pipes
-        drop = cfg.training and cfg.dropout_p > 0.0
-        p = float(cfg.dropout_p) if drop else 0.0
-        seed = _new_seed() if drop else 0
-        flags = nat.LG_F_DROPOUT if drop else 0
+        pe = float(cfg.dropout_p) if cfg.training else 0.0
+        pn = float(cfg.dropout_p if cfg.noleak_p is None else cfg.noleak_p) if cfg.training else 0.0
+        seed = _new_seed() if (pe > 0.0 or pn > 0.0) else 0
+        fe = nat.LG_F_DROPOUT if pe > 0.0 else 0
+        fn = nat.LG_F_DROPOUT if pn > 0.0 else 0
         st = stream_of(h)
-        logits = torch.empty(B, P, device=h.device, dtype=torch.float32)
+        logits = torch.empty(B, P + 1, device=h.device, dtype=torch.float32)
         pooled = torch.empty(B, D, device=h.device, dtype=torch.float32)
-        w1c, w2c = w1.contiguous(), w2.contiguous()
+        hid = torch.empty(B, nhidden, device=h.device, dtype=torch.float32)
+        w1c, w2c, nw1c, nw2c = w1.contiguous(), w2.contiguous(), nw1.contiguous(), nw2.contiguous()
         with _timed("edge_fwd", h.device):
-            check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits), B, N,
-                                       P, D, hidden, flags, p, seed, EDGE_HEAD_SALT, st), "lg_edge_head_fwd")
-        with _timed("mean_pool", h.device):
-            check(lib.lg_mean_pool_fwd(ptr(h), ptr(pooled), B, N, D, st), "lg_mean_pool_fwd")
-        ctx.cfg, ctx.p, ctx.seed, ctx.flags = cfg, p, seed, flags
-        ctx.save_for_backward(h, w1c, b1, w2c)
-        return logits, pooled
+            check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits),
+                                       P + 1, B, N, P, D, hidden, fe, pe, seed, EDGE_HEAD_SALT, st),
+                  "lg_edge_head_fwd")
+        with _timed("pool_head", h.device):
+            check(lib.lg_pool_head_fwd(ptr(h), ptr(nw1c), ptr(nb1), ptr(nw2c), ptr(nb2), ptr(pooled), ptr(hid),
+                                       ptr(logits), P + 1, P, B, N, D, nhidden, fn, pn, seed, NOLEAK_HEAD_SALT, st),
+                  "lg_pool_head_fwd")
+        ctx.cfg, ctx.drop = cfg, (pe, fe, pn, fn, seed)
+        ctx.save_for_backward(h, w1c, b1, w2c, pooled, hid, nw1c, nw2c)
+        return logits
 
     @staticmethod
-    def backward(ctx, dlogits, dpooled):
+    def backward(ctx, dlogits):
         lib = load_library()
-        h, w1, b1, w2 = ctx.saved_tensors
+        h, w1, b1, w2, pooled, hid, nw1, nw2 = ctx.saved_tensors
+        pe, fe, pn, fn, seed = ctx.drop
         inc = ctx.cfg.inc
         B, N, D = h.shape
-        P, hidden = inc.num_pipes, w1.shape[0]
+        P, hidden, nhidden = inc.num_pipes, w1.shape[0], nw1.shape[0]
         dev = h.device
         st = stream_of(h)
-        if dlogits is None:
-            dlogits = torch.zeros(B, P, device=dev)
+        dl = dlogits.contiguous()
         dpipe = torch.empty(B, P, 2, D, device=dev)
         dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
         dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
         ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
         with _timed("edge_bwd", dev):
-            check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(dlogits.contiguous()),
-                                       ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden,
-                                       ctx.flags, ctx.p, ctx.seed, EDGE_HEAD_SALT, ptr(ws), st), "lg_edge_head_bwd")
+            check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(dl), P + 1, ptr(dpipe),
+                                       ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, pe, seed,
+                                       EDGE_HEAD_SALT, ptr(ws), st), "lg_edge_head_bwd")
+        dpooled = torch.empty(B, D, device=dev)
+        ndw1, ndb1 = torch.empty_like(nw1), torch.empty(nhidden, device=dev)
+        ndw2, ndb2 = torch.empty_like(nw2), torch.empty(1, device=dev)
+        wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
+        with _timed("pool_head_bwd", dev):
+            check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
+                                       ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, pn, ptr(wsn),
+                                       st), "lg_pool_head_bwd")
         dh = torch.empty_like(h)
         with _timed("pipe_scatter", dev):
-            check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe),
-                                          ptr(dpooled.contiguous() if dpooled is not None else None), ptr(dh), B, N,
-                                          P, D, st), "lg_pipe_scatter_bwd")
-        return None, dh, dw1, db1, dw2, db2
+            check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P,
+                                          D, st), "lg_pipe_scatter_bwd")
+        return None, dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 
 def pipe_features(h: torch.Tensor, inc: Incidence) -> torch.Tensor:

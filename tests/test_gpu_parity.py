@@ -321,7 +321,9 @@ def test_detector_train_mode_replay_with_oracle_masks():
     mlp = m.edge_head.mlp
     hid = torch.relu(feat @ mlp[0].weight.t() + mlp[0].bias) * me * sc
     pl = (hid @ mlp[3].weight.t() + mlp[3].bias).view(B, P)
-    nl = m.noleak_head(hn.mean(1)).unsqueeze(-1)   # torch dropout: same CUDA RNG stream as the product
+    mn = _masks(seed_h, ops.NOLEAK_HEAD_SALT, (B, 128), 0.1)
+    nm = m.noleak_head.mlp
+    nl = (torch.relu(hn.mean(1) @ nm[0].weight.t() + nm[0].bias) * mn * sc) @ nm[3].weight.t() + nm[3].bias
     out2 = torch.cat([pl, nl], -1)
     assert_close(out, out2, what="train-mode forward replay")
     out2.square().sum().backward()
@@ -333,7 +335,8 @@ def test_detector_train_mode_replay_with_oracle_masks():
 @pytest.mark.parametrize("train", [False, True])
 @pytest.mark.parametrize("D", [64, 32])
 def test_fused_heads_vs_torch(train, D):
-    """HeadsFn (fused EdgeHead + mean pool, incidence-reduced backward) vs float64 torch."""
+    """HeadsFn (fused EdgeHead, mean pool + NoLeakHead, one (B, P+1) output, incidence-reduced
+    backward) vs float64 torch with the same dropout masks (oracle/dropout_ref.py)."""
     from models import ops
     from models.ops import HeadsConfig, HeadsFn, Incidence
     g = load("graph_ltown_a.npz")
@@ -347,28 +350,32 @@ def test_fused_heads_vs_torch(train, D):
     b1 = torch.randn(128, generator=gen) / 4
     W2 = torch.randn(1, 128, generator=gen) / 8
     b2 = torch.randn(1, generator=gen)
-    dl = torch.randn(B, P, generator=gen)
-    dp = torch.randn(B, D, generator=gen)
-    params = [t.to(DEV).requires_grad_(True) for t in (h, W1, b1, W2, b2)]
+    V1 = torch.randn(128, D, generator=gen) / 8
+    c1 = torch.randn(128, generator=gen) / 4
+    V2 = torch.randn(1, 128, generator=gen) / 8
+    c2 = torch.randn(1, generator=gen)
+    dl = torch.randn(B, P + 1, generator=gen)
+    params = [t.to(DEV).requires_grad_(True) for t in (h, W1, b1, W2, b2, V1, c1, V2, c2)]
     torch.manual_seed(77)
-    logits, pooled = HeadsFn.apply(HeadsConfig(inc, 0.1, train), *params)
-    ((logits * dl.to(DEV)).sum() + (pooled * dp.to(DEV)).sum()).backward()
-    # float64 reference with the same dropout mask
-    ref = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2)]
-    hr, W1r, b1r, W2r, b2r = ref
+    logits = HeadsFn.apply(HeadsConfig(inc, 0.1, train), *params)
+    (logits * dl.to(DEV)).sum().backward()
+    # float64 reference with the same dropout masks
+    ref = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2, V1, c1, V2, c2)]
+    hr, W1r, b1r, W2r, b2r, V1r, c1r, V2r, c2r = ref
     u, v = ends[:, 0], ends[:, 1]
     feat = torch.cat([hr[:, u], hr[:, v], (hr[:, u] - hr[:, v]).abs()], -1)
     hid = torch.relu(feat @ W1r.t() + b1r)
+    pooled = hr.mean(1)
+    nhid = torch.relu(pooled @ V1r.t() + c1r)
     if train:
         torch.manual_seed(77)
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())
         hid = hid * _masks(seed, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1, dev="cpu").double().view(B, P, 128) / 0.9
-    lr = (hid @ W2r.t()).squeeze(-1) + b2r
-    pr = hr.mean(1)
-    ((lr * dl.double()).sum() + (pr * dp.double()).sum()).backward()
-    assert_close(logits, lr, what="edge logits")
-    assert_close(pooled, pr, what="pooled")
-    for a, b, n in zip(params, ref, ("dh", "dW1", "db1", "dW2", "db2")):
+        nhid = nhid * _masks(seed, ops.NOLEAK_HEAD_SALT, (B, 128), 0.1, dev="cpu").double() / 0.9
+    lr = torch.cat([(hid @ W2r.t()).squeeze(-1) + b2r, nhid @ V2r.t() + c2r], -1)
+    (lr * dl.double()).sum().backward()
+    assert_close(logits, lr, what="head logits")
+    for a, b, n in zip(params, ref, ("dh", "dW1", "db1", "dW2", "db2", "dV1", "dc1", "dV2", "dc2")):
         assert_close(a.grad, b.grad, rtol=2e-5, what=n)
 
 

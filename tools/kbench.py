@@ -83,7 +83,7 @@ def main():
         db = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
         f = lambda: check(lib.lg_gcn_bwd(ptr(graph.rowptr_t), ptr(graph.col_t), ptr(graph.w_t), ptr(dy), ptr(yy),
-                                         ptr(x), ptr(W), ptr(dx), ptr(dW), ptr(db), B, N, D, E1,
+                                         ptr(x), ptr(W), ptr(dx), ptr(dW), ptr(db), None, None, B, N, D, E1,
                                          nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), st), "bwd")
         t = timeit(f, args.iters)
         res["gcn_bwd"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
@@ -94,7 +94,7 @@ def main():
         b2 = torch.randn(1, device=dev)
         lo = torch.empty(B, P, device=dev)
         if "edge_fwd" in which:
-            f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), B,
+            f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), P, B,
                                                    N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, st), "edge fwd")
             t = timeit(f, args.iters)
             res["edge_fwd"] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
@@ -103,7 +103,7 @@ def main():
             dpipe = torch.empty(B, P, 2, D, device=dev)
             dW1, db1, dW2, db2 = (torch.empty_like(t) for t in (W1, b1, W2, b2))
             ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=dev, dtype=torch.uint8)
-            f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(dl),
+            f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(dl), P,
                                                    ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
                                                    nat.LG_F_DROPOUT, 0.1, 5, 101, ptr(ws), st), "edge bwd")
             t = timeit(f, args.iters)
