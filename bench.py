@@ -200,7 +200,7 @@ def main() -> None:
     for _ in range(args.warmup):
         step()
     timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "gru_fwd", "gru_bwd", "edge_fwd", "edge_bwd",
-                             "pipe_scatter", "pool_head", "pool_head_bwd"])
+                             "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)
 
     def barrier():

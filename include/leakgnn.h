@@ -108,6 +108,18 @@ int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float*
                      int64_t B, int64_t N, int64_t S, int64_t D,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 
+/* K2 backward (node init Linear(Ds+1 -> D), detector.py:160, 184-189), weight side:
+ * for sensor rows the Linear input is [h_s, 1], so with dy = d(proj) [K][M] (K = B*S rows)
+ * and x = h_s [K][N]:
+ *   dw[m][n] = sum_k dy[k][m] x[k][n]  (n < N),   dw[m][N] = sum_k dy[k][m]
+ *   db[m]    = sum_k dy[k][m]            (db may be NULL)
+ * dw is [M][N+1], the nn.Linear weight layout.  M, N in {32, 64}.  Split-K over
+ * workgroups, fixed-order reduction (deterministic).  Replaces the skinny-K
+ * (K = 7,424) torch.mm of the autograd of torch.addmm. */
+int64_t lg_linear_dw_workspace_bytes(int64_t K, int64_t M, int64_t N);
+int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t M, int64_t N,
+                 float* dw, float* db, void* workspace, lg_stream_t stream);
+
 /* nnz_cap (lg_gcn_fwd / lg_spmm / lg_gcn_bwd): capacity of col/w as allocated for
  * lg_graph_build (E + N).  It sizes the on-chip copy of the CSR: when
  * 4*(N+1) + 8*nnz_cap <= 48 KiB every workgroup stages the CSR in LDS once.

@@ -3,6 +3,7 @@
 // and written as whole 4*D-byte lines.
 #include <algorithm>
 #include "common.h"
+#include "reduce.h"
 
 namespace {
 
@@ -79,6 +80,54 @@ k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict
     }
 }
 
+
+// Weight gradient of a Linear whose input rows are [x_k, 1]:
+//   slab row g: [M][N+1] block partial of dW[m][n] = sum_k dy[k][m] x[k][n], dW[m][N] = sum_k dy[k][m],
+//   then [M] the same column sums (the bias gradient).  One wave per 16-row m-tile; K split
+//   over blocks of kLinRows rows; v_mfma_f32_16x16x4_f32 with the column sums as an extra
+//   MFMA against a constant-1 B operand.  Split-K partials are reduced in fixed order.
+constexpr int kLinRows = 32;  // 8 k-steps per block: every operand load is issued before the MFMAs
+
+template <int M, int N>
+__global__ void __launch_bounds__(64 * (M / 16))
+k_linear_dw(const float* __restrict__ dy, const float* __restrict__ x, int64_t K, float* __restrict__ slab) {
+    constexpr int NT = N / 16, SL = M * (N + 1) + M, KS = kLinRows / 4;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int64_t k0 = static_cast<int64_t>(blockIdx.x) * kLinRows;
+    float a[KS], bv[KS][NT];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        const int64_t kr = k0 + 4 * ks + q;
+        const bool ok = kr < K;
+        const int64_t kc = ok ? kr : 0;
+        a[ks] = ok ? dy[kc * M + 16 * w + j] : 0.f;  // A[m = j][k = q]
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) bv[ks][nt] = ok ? x[kc * N + 16 * nt + j] : 0.f;  // B[k = q][n = j]
+    }
+    f32x4 acc[NT], cs = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ks], bv[ks][nt], acc[nt], 0, 0, 0);
+        cs = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ks], 1.f, cs, 0, 0, 0);
+    }
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int m = 16 * w + 4 * q + reg;  // D layout: row 4q + reg, column j
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) out[m * (N + 1) + 16 * nt + j] = acc[nt][reg];
+        if (j == 0) {
+            out[m * (N + 1) + N] = cs[reg];
+            out[M * (N + 1) + m] = cs[reg];
+        }
+    }
+}
+
+int linear_dw_grid(int64_t K) { return static_cast<int>(std::max<int64_t>(1, ceil_div(K, kLinRows))); }
+
 inline unsigned row_grid(int64_t rows, int D) {
     const int64_t rpb = 256 / (D / 4);
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, rpb), 16LL * lg_num_cus())));
@@ -150,6 +199,35 @@ extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc
     }
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
+}
+
+extern "C" int64_t lg_linear_dw_workspace_bytes(int64_t K, int64_t M, int64_t N) {
+    if (K < 0 || (M != 32 && M != 64) || (N != 32 && N != 64)) return LG_EUNSUPPORTED;
+    return static_cast<int64_t>(linear_dw_grid(K)) * (M * (N + 1) + M) * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t M, int64_t N, float* dw, float* db,
+                            void* workspace, lg_stream_t stream) {
+    if (K < 0 || !dw || !workspace || (K > 0 && (!dy || !x))) return LG_EINVAL;
+    if ((M != 32 && M != 64) || (N != 32 && N != 64)) return LG_EUNSUPPORTED;
+    hipStream_t s = lg_stream(stream);
+    const int G = linear_dw_grid(K);
+    float* slab = static_cast<float*>(workspace);
+    const int64_t SL = M * (N + 1) + M;
+    if (K == 0) {
+        if (hipMemsetAsync(slab, 0, SL * sizeof(float), s) != hipSuccess) return LG_EHIP;
+    } else {
+#define LG_LDW(MM, NN) k_linear_dw<MM, NN><<<G, 64 * (MM / 16), 0, s>>>(dy, x, K, slab)
+        if (M == 64) {
+            if (N == 64) LG_LDW(64, 64); else LG_LDW(64, 32);
+        } else {
+            if (N == 64) LG_LDW(32, 64); else LG_LDW(32, 32);
+        }
+#undef LG_LDW
+        LG_RET_IF_LAUNCH_FAILED();
+    }
+    const LgSlabSeg segs[2] = {{0, M * (N + 1), dw}, {M * (N + 1), M, db}};
+    return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
 extern "C" int lg_abi_version(void) { return 3; }

@@ -93,9 +93,12 @@ k_pool_head_bwd(const float* __restrict__ pooled, const float* __restrict__ hid,
                 float* __restrict__ dpooled, float* __restrict__ slab, double* __restrict__ dslab, int64_t B,
                 float scale) {
     constexpr int SL = kHid * D + 2 * kHid;
+    constexpr int WS = D + 1;  // W1 / dW1 rows in LDS (odd stride: conflict-free row-per-thread access)
+    __shared__ float w1l[kHid * WS];
     __shared__ float pl[D];
     __shared__ float dh[kHid];
     const int k = threadIdx.x;
+    for (int i = k; i < kHid * D; i += kHid) w1l[(i / D) * WS + (i % D)] = W1[i];
     const float w2k = w2[k];
     float dw1[D];
 #pragma unroll
@@ -111,19 +114,23 @@ k_pool_head_bwd(const float* __restrict__ pooled, const float* __restrict__ hid,
         db1 += dhk;
         dw2 = fmaf(dout, hk, dw2);
         if (k == 0) db2 += static_cast<double>(dout);
-        __syncthreads();
+        __syncthreads();  // pl, dh (and on the first pass w1l) visible
 #pragma unroll
         for (int d = 0; d < D; ++d) dw1[d] = fmaf(dhk, pl[d], dw1[d]);
         if (k < D) {
             float s = 0.f;
-            for (int kk = 0; kk < kHid; ++kk) s = fmaf(dh[kk], W1[kk * D + k], s);
+#pragma unroll 16
+            for (int kk = 0; kk < kHid; ++kk) s = fmaf(dh[kk], w1l[kk * WS + k], s);
             dpooled[b * D + k] = s;
         }
         __syncthreads();
     }
-    float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
+    // dW1 rows through LDS (reusing the W1 copy) so the slab store is coalesced
 #pragma unroll
-    for (int d = 0; d < D; ++d) out[k * D + d] = dw1[d];
+    for (int d = 0; d < D; ++d) w1l[k * WS + d] = dw1[d];
+    __syncthreads();
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
+    for (int i = k; i < kHid * D; i += kHid) out[i] = w1l[(i / D) * WS + (i % D)];
     out[kHid * D + k] = db1;
     out[kHid * D + kHid + k] = dw2;
     if (k == 0) dslab[blockIdx.x] = db2;

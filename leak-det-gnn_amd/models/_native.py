@@ -33,6 +33,8 @@ SIGNATURES = {
     "lg_incidence_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
     "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),
+    "lg_linear_dw_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "lg_linear_dw": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
     "lg_node_init_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),

@@ -145,7 +145,7 @@ class LeakDetector(nn.Module):
         Ds = h_s.shape[-1]
         Wn, bn = self.sensor_to_node.weight, self.sensor_to_node.bias     # (D, Ds+1), (D,)
         # rows with a sensor: [h_s, 1] W^T + b ; rows without: [0, 0] W^T + b = b
-        proj = torch.addmm(Wn[:, Ds] + bn, h_s.reshape(B * S, Ds), Wn[:, :Ds].t()).view(B, S, -1)
+        proj = ops.SensorProjFn.apply(h_s, Wn, bn)                        # (B, S, D)
         wb = []
         for conv in self.convs:
             wb += [conv.lin.weight, conv.bias]

@@ -252,6 +252,40 @@ class TrunkConfig:
     capture: Optional[list] = None     # tests: receives the saved activations x_0 .. x_L
 
 
+class SensorProjFn(torch.autograd.Function):
+    """sensor_to_node on the rows that carry a sensor (detector.py:160, 184-189): their
+    Linear input is [h_s, 1], so proj = h_s W[:, :Ds]^T + (W[:, Ds] + b) — one addmm.
+    Backward: dh_s = dproj W[:, :Ds] (torch mm); dW (incl. the mask column) and db in one
+    split-K MFMA kernel (lg_linear_dw) instead of autograd's skinny-K (K = B*S) mm."""
+
+    @staticmethod
+    def forward(ctx, h_s, W, b):
+        B, S, Ds = h_s.shape
+        D = W.shape[0]
+        h2 = h_s.reshape(B * S, Ds).contiguous()
+        proj = torch.addmm(W[:, Ds] + b, h2, W[:, :Ds].t()).view(B, S, D)
+        ctx.save_for_backward(h2, W)
+        ctx.shape = (B, S)
+        return proj
+
+    @staticmethod
+    def backward(ctx, dproj):
+        lib = load_library()
+        h2, W = ctx.saved_tensors
+        B, S = ctx.shape
+        K, Ds = h2.shape
+        D = W.shape[0]
+        d2 = dproj.reshape(K, D).contiguous()
+        dh = (d2 @ W[:, :Ds]).view(B, S, Ds) if ctx.needs_input_grad[0] else None
+        dW = torch.empty(D, Ds + 1, device=d2.device, dtype=torch.float32)
+        db = torch.empty(D, device=d2.device, dtype=torch.float32)
+        ws = torch.empty(int(lib.lg_linear_dw_workspace_bytes(K, D, Ds)), device=d2.device, dtype=torch.uint8)
+        with _timed("linear_dw", d2.device):
+            check(lib.lg_linear_dw(ptr(d2), ptr(h2), K, D, Ds, ptr(dW), ptr(db), ptr(ws), stream_of(d2)),
+                  "lg_linear_dw")
+        return dh, dW, db
+
+
 class GNNTrunkFn(torch.autograd.Function):
     """Node init (detector.py:178-190) + L x [GCNConv, ReLU, Dropout] (detector.py:198-201).
 

@@ -450,3 +450,22 @@ def test_gru_encoder_vs_torch_cpu(use_time, B):
         assert_close(tg.grad, tc.grad, what="GRU d tfeat")
     assert_grads_close([(n, p.grad) for n, p in enc.gru.named_parameters()],
                        {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
+
+
+@pytest.mark.parametrize("K,M,N", [(7424, 64, 64), (1857, 32, 32), (3, 64, 32), (250, 32, 64)])
+def test_linear_dw_vs_fp64(K, M, N):
+    """lg_linear_dw (node-init Linear weight grad on [x, 1] rows) vs float64 torch, ragged K."""
+    from models import ops
+    lib = ops.load_library()
+    gen = torch.Generator().manual_seed(K + M + N)
+    dy = torch.randn(K, M, generator=gen)
+    x = torch.randn(K, N, generator=gen)
+    dw = torch.empty(M, N + 1, device=DEV)
+    db = torch.empty(M, device=DEV)
+    ws = torch.empty(int(lib.lg_linear_dw_workspace_bytes(K, M, N)), device=DEV, dtype=torch.uint8)
+    dyg, xg = dy.to(DEV), x.to(DEV)
+    ops.check(lib.lg_linear_dw(ops.ptr(dyg), ops.ptr(xg), K, M, N, ops.ptr(dw), ops.ptr(db), ops.ptr(ws),
+                               ops.stream_of(dyg)), "lg_linear_dw")
+    ref = torch.cat([dy.double().t() @ x.double(), dy.double().sum(0, keepdim=True).t()], 1)
+    assert_close(dw, ref, what="dW")
+    assert_close(db, ref[:, N], what="db")

@@ -119,6 +119,8 @@ def test_c_abi_host_only_calls():
     assert lib.lg_pipe_gather_fwd(None, None, None, 1, 10, 5, 64, None) == -1
     assert lib.lg_mean_pool_fwd(None, None, 2, 10, 64, None) == -1
     assert lib.lg_pool_head_bwd_workspace_bytes(256, 64, 64) == -2   # hidden must be 128
+    assert lib.lg_linear_dw_workspace_bytes(7424, 64, 48) == -2
+    assert lib.lg_linear_dw(None, None, 7424, 64, 64, None, None, None, None) == -1
     assert lib.lg_pool_head_fwd(None, None, None, None, None, None, None, None, 765, 764, 2, 661, 64, 128, 0, 0.0, 0,
                                 102, None) == -1
     assert lib.lg_edge_head_fwd(None, None, None, None, None, None, None, 764, 2, 661, 764, 64, 128, 0, 0.0, 0, 101,
