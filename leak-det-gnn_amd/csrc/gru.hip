@@ -41,14 +41,15 @@ __device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// xs[tt][seq][16] = [x_0 .. x_{I-1}, 0.., 1 (col 10), 0..] for steps t0 .. t0+nt-1 of the
-// block's 16 sequences (all zero for padded sequences).  All loads are issued before
-// the first LDS store of each batch.
-template <bool UT>
+// xs[tt][seq][0..15] (row stride XR) = [x_0 .. x_{I-1}, 0.., 1 (col 10), 0..] for steps
+// t0 .. t0+nt-1 of the block's 16 sequences (all zero for padded sequences).  The odd
+// row stride keeps the per-lane (seq, k) reads of both kernels bank-conflict free.  All
+// loads are issued before the first LDS store of each batch.
+constexpr int XR = 17;
+template <bool UT, int PER = 8>
 __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __restrict__ resid,
                                         const float* __restrict__ tfeat, int t0, int nt, uint32_t seq0,
                                         uint32_t Nseq, int L, int S, const lg_fastdiv& fdS) {
-    constexpr int PER = 8;
     const int total = nt * TS * 16;
     for (int base = 0; base < total; base += blockDim.x * PER) {
         float v[PER];
@@ -70,108 +71,112 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __r
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const int idx = base + u * blockDim.x + threadIdx.x;
-            if (idx < total) xs[idx] = v[u];
+            if (idx < total) xs[(idx >> 4) * XR + (idx & 15)] = v[u];
         }
     }
 }
 
 // ------------------------------------------------------------------ forward
+// One wave per 16-row gate tile: 3 * H/16 waves per 16 sequences (12 at H = 64), so each
+// wave issues only 3 + H/4 MFMAs per step (x part; h part split over two accumulator
+// chains) and ~5 waves share a SIMD to hide the recurrence's latency.  Wave (g, u),
+// g in {r, z, n}, u = unit group: the r and z waves post sigma(.) tiles to LDS; the n
+// wave u keeps W_in x + b_in and W_hn h + b_hn, forms n = tanh(.), h' = (1-z) n + z h
+// for units [16u, 16u+16) and posts h' to LDS, from where every wave reads the next
+// step's B operand.  Exchanges use lane-major slots (the reader lane is the writer
+// lane), so every LDS access is a conflict-free b128.  Two barriers per step.
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
 template <int H, bool UT, bool SAVE>
-__global__ void __launch_bounds__(4 * H)
+__global__ void __launch_bounds__(12 * H) __attribute__((amdgpu_waves_per_eu(6, 8)))  // 2 workgroups / CU
 k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Wih,
           const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
           float* __restrict__ hs, float* __restrict__ gates, float* __restrict__ hout, uint32_t Nseq, int L, int S,
           lg_fastdiv fdS) {
-    constexpr int NW = H / 16, KH = H / 4, I = UT ? 10 : 1;
-    __shared__ __attribute__((aligned(16))) float xs[kLC * TS * 16];
-    __shared__ __attribute__((aligned(16))) float hx[2][64][4 * NW];
+    constexpr int NU = H / 16, KH = H / 4, I = UT ? 10 : 1;
+    __shared__ __attribute__((aligned(16))) float xs[kLC * TS * XR];
+    __shared__ __attribute__((aligned(16))) f32x4 grz[2][NU][64];  // [r|z][unit group][lane]: sigma tiles
+    __shared__ __attribute__((aligned(16))) f32x4 hb[NU][64];      // h_t tiles, lane-major
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = w / NU, u = w % NU;  // gate (0 r, 1 z, 2 n), unit group
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const uint32_t seq0 = blockIdx.x * TS, seq = seq0 + j;
     const bool valid = seq < Nseq;
 
-    float ah[3][KH], ax[3][3];
+    const int row = g * H + 16 * u + j;  // A-operand row of this lane
+    float ah[KH], ax[3];
 #pragma unroll
-    for (int gi = 0; gi < 3; ++gi) {
-        const int row = gi * H + 16 * w + j;  // A-operand row of this lane
+    for (int ks = 0; ks < KH; ++ks) ah[ks] = Whh[row * H + fk(ks, q)];
 #pragma unroll
-        for (int ks = 0; ks < KH; ++ks) ah[gi][ks] = Whh[row * H + fk(ks, q)];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const int k = 4 * kx + q;
-            ax[gi][kx] = k < I ? Wih[row * I + k] : 0.f;
-        }
+    for (int kx = 0; kx < 3; ++kx) {
+        const int k = 4 * kx + q;
+        ax[kx] = k < I ? Wih[row * I + k] : 0.f;
     }
-    f32x4 br, bz, bhn, bin;  // D-layout rows 4q+reg of each gate tile
+    f32x4 bx, bh;  // x-side / h-side biases of rows 4q+reg (r, z: both folded into bx)
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
-        const int c = 16 * w + 4 * q + reg;
-        br[reg] = bih[c] + bhh[c];
-        bz[reg] = bih[H + c] + bhh[H + c];
-        bhn[reg] = bhh[2 * H + c];
-        bin[reg] = bih[2 * H + c];
+        const int c = g * H + 16 * u + 4 * q + reg;
+        bx[reg] = g < 2 ? bih[c] + bhh[c] : bih[c];
+        bh[reg] = g < 2 ? 0.f : bhh[c];
     }
     float hf[KH];
 #pragma unroll
     for (int i = 0; i < KH; ++i) hf[i] = 0.f;
+    if (g == 2) hb[u][lane] = zero4();  // h_{-1}; each n wave reads its own slot back as h_{t-1}
 
     for (int t0 = 0; t0 < L; t0 += kLC) {
         const int nt = min(kLC, L - t0);
         __syncthreads();
-        stage_x<UT>(xs, resid, tfeat, t0, nt, seq0, Nseq, L, S, fdS);
+        stage_x<UT, 2>(xs, resid, tfeat, t0, nt, seq0, Nseq, L, S, fdS);
         __syncthreads();
         for (int tt = 0; tt < nt; ++tt) {
             const int t = t0 + tt;
-            f32x4 ar = br, az = bz, ahn = bhn, ain = bin;
+            f32x4 a0 = bx, a1 = bh, a2 = zero4();  // a0: x part, a1 + a2: h part
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                const float xv = xs[(tt * TS + j) * 16 + 4 * kx + q];
-                ar = mfma(ax[0][kx], xv, ar);
-                az = mfma(ax[1][kx], xv, az);
-                ain = mfma(ax[2][kx], xv, ain);
-            }
+            for (int kx = 0; kx < 3; ++kx) a0 = mfma(ax[kx], xs[(tt * TS + j) * XR + 4 * kx + q], a0);
 #pragma unroll
-            for (int ks = 0; ks < KH; ++ks) {
-                ar = mfma(ah[0][ks], hf[ks], ar);
-                az = mfma(ah[1][ks], hf[ks], az);
-                ahn = mfma(ah[2][ks], hf[ks], ahn);
+            for (int ks = 0; ks < KH; ks += 2) {
+                a1 = mfma(ah[ks], hf[ks], a1);
+                a2 = mfma(ah[ks + 1], hf[ks + 1], a2);
             }
-            f32x4 hn, rr, zz, nn;
+            const f32x4 hp = a1 + a2;
+            if (g < 2) {
+                f32x4 sg;
 #pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                rr[reg] = sigm(ar[reg]);
-                zz[reg] = sigm(az[reg]);
-                nn[reg] = tanhf(ain[reg] + rr[reg] * ahn[reg]);
-                hn[reg] = (1.f - zz[reg]) * nn[reg] + zz[reg] * hf[4 * w + reg];
+                for (int reg = 0; reg < 4; ++reg) sg[reg] = sigm(a0[reg] + hp[reg]);
+                grz[g][u][lane] = sg;
             }
-            st4(&hx[t & 1][lane][4 * w], hn);
-            if (valid) {
-                const int64_t row = static_cast<int64_t>(t) * Nseq + seq;
-                if (hs) st4(hs + row * H + 16 * w + 4 * q, hn);
-                if constexpr (SAVE) {
-                    float* g = gates + row * 4 * H + 16 * w + 4 * q;
-                    st4(g, rr);
-                    st4(g + H, zz);
-                    st4(g + 2 * H, nn);
-                    st4(g + 3 * H, ahn);
+            __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hb
+            if (g == 2) {
+                const f32x4 r = grz[0][u][lane], z = grz[1][u][lane], hprev = hb[u][lane];
+                f32x4 n, hn;
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    n[reg] = tanhf(a0[reg] + r[reg] * hp[reg]);
+                    hn[reg] = (1.f - z[reg]) * n[reg] + z[reg] * hprev[reg];
+                }
+                hb[u][lane] = hn;
+                if (valid) {
+                    const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
+                    if (hs) st4(hs + rw * H + 16 * u + 4 * q, hn);
+                    if constexpr (SAVE) {
+                        float* gp = gates + rw * 4 * H + 16 * u + 4 * q;
+                        st4(gp, r);
+                        st4(gp + H, z);
+                        st4(gp + 2 * H, n);
+                        st4(gp + 3 * H, hp);
+                    }
                 }
             }
-            __syncthreads();
+            __syncthreads();  // (B) h_t posted; sigma slots free again
 #pragma unroll
-            for (int a = 0; a < NW; ++a) {
-                const f32x4 v = ld4(&hx[t & 1][lane][4 * a]);
+            for (int a = 0; a < NU; ++a) {
+                const f32x4 v = hb[a][lane];
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
             }
         }
     }
-    if (valid) {
-        f32x4 v;
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) v[reg] = hf[4 * w + reg];
-        st4(hout + static_cast<int64_t>(seq) * H + 16 * w + 4 * q, v);
-    }
+    if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hb[u][lane]);
 }
 
 // ------------------------------------------------------------------ backward
@@ -202,7 +207,7 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     constexpr int NW = G::NW, I = UT ? 10 : 1, G3 = 3 * H;
     constexpr int SLAB = G3 * H + G3 * I + 2 * G3;
     constexpr int NTH = 64 * NW;
-    __shared__ __attribute__((aligned(16))) float xs[kLB * TS * 16];
+    __shared__ __attribute__((aligned(16))) float xs[kLB * TS * XR];
     __shared__ __attribute__((aligned(16))) float hl[3][TS * G::HS];
     __shared__ __attribute__((aligned(16))) float dg[2][64 * G::DS];
     __shared__ __attribute__((aligned(16))) float wih[NEED_DX ? G3 * 16 : 1];
@@ -320,7 +325,7 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                 dwh[1][nt] = mfma(a1, hb, dwh[1][nt]);
                 dwh[2][nt] = mfma(a2, hb, dwh[2][nt]);
             }
-            const float xb = xs[(tt * TS + 4 * ks + q) * 16 + j];
+            const float xb = xs[(tt * TS + 4 * ks + q) * XR + j];
             dwx[0] = mfma(a0, xb, dwx[0]);
             dwx[1] = mfma(a1, xb, dwx[1]);
             dwx[2] = mfma(a3, xb, dwx[2]);
@@ -381,7 +386,7 @@ int launch_fwd(bool ut, bool save, const float* residual, const float* tfeat, co
     const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
     const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
 #define LG_GRU_FWD(UT, SV)                                                                                        \
-    k_gru_fwd<H, UT, SV><<<grid, 4 * H, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, h_last,   \
+    k_gru_fwd<H, UT, SV><<<grid, 12 * H, 0, s>>>(residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, h_last,   \
                                                  Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
     if (ut) {
         if (save) LG_GRU_FWD(true, true); else LG_GRU_FWD(true, false);

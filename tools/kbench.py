@@ -123,6 +123,12 @@ def main():
         t = timeit(f, args.iters)
         flops = 2 * B * S * L * 192 * (64 + 10)
         res["gru_fwd"] = {"us": t, "TFLOPs": flops / t / 1e6}
+        f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), None, None,
+                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd eval")
+        res["gru_fwd_eval"] = {"us": timeit(f, args.iters)}
+        f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), None,
+                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd hs only")
+        res["gru_fwd_hs"] = {"us": timeit(f, args.iters)}
         if "gru_bwd" in which:
             dh = torch.randn(B * S, 64, device=dev)
             dws = [torch.empty_like(t) for t in (wih, whh, bih, bhh)]
