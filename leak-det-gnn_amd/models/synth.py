@@ -9,8 +9,9 @@ generators need `wntr` (absent) — SURVEY §8(d) C4/C5.
 """
 from __future__ import annotations
 
+import json
 from pathlib import Path
-from typing import Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -99,3 +100,84 @@ def write_synthetic_inp(path: str | Path, num_nodes: int, num_pipes: int, seed: 
 def pick_sensors(node_ids: Sequence[str], count: int = 29, seed: int = 0) -> list:
     rng = np.random.default_rng(seed + 2)
     return [node_ids[i] for i in sorted(rng.choice(len(node_ids) - 1, size=count, replace=False))]
+
+
+# ------------------------------------------------------------------ sensor data sets
+def _sensor_frame(sensor_ids: Sequence[str], T: int, rng: np.random.Generator, start: str,
+                  drop: Optional[np.ndarray] = None):
+    """(clean, noisy) DataFrames in the reference layout (index 'datetime' at 5 min, one
+    column per sensor): 40 + 5 sin(t/20 + phase) + N(0, 1) per sensor (SURVEY §8 d, C1),
+    multiplicative noise N(1, 2.5e-4); `drop` (T, S) is subtracted from the clean signal."""
+    import pandas as pd
+    S = len(sensor_ids)
+    t = np.arange(T, dtype=np.float64)[:, None]
+    phase = rng.uniform(0, 2 * np.pi, size=(1, S))
+    clean = 40.0 + 5.0 * np.sin(t / 20.0 + phase) + rng.normal(0.0, 1.0, size=(T, S))
+    if drop is not None:
+        clean = clean - drop
+    noisy = clean * rng.normal(1.0, 2.5e-4, size=(T, S))
+    idx = pd.date_range(start, periods=T, freq="5min", name="datetime")
+    return (pd.DataFrame(clean, index=idx, columns=list(sensor_ids)),
+            pd.DataFrame(noisy, index=idx, columns=list(sensor_ids)))
+
+
+def write_synthetic_normal_set(root: str | Path, sensor_ids: Sequence[str], n_windows: int = 12, T: int = 577,
+                               seed: int = 0) -> List[str]:
+    """No-leak set in the reference format (datasets.py:72-111, 200-257): manifest.jsonl rows
+    {"window_id", "status": "ok"}, <id>/sensors.csv (noisy) and <id>/sensors_gt.csv."""
+    root = Path(root)
+    root.mkdir(parents=True, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    ids = [f"w{i:05d}" for i in range(n_windows)]
+    for i, wid in enumerate(ids):
+        (root / wid).mkdir(exist_ok=True)
+        gt, noisy = _sensor_frame(sensor_ids, T, rng, start=f"2024-01-{1 + i % 28:02d} 00:00")
+        noisy.to_csv(root / wid / "sensors.csv")
+        gt.to_csv(root / wid / "sensors_gt.csv")
+    with open(root / "manifest.jsonl", "w", encoding="utf-8") as f:
+        for wid in ids:
+            f.write(json.dumps({"window_id": wid, "status": "ok"}) + "\n")
+    return ids
+
+
+def write_synthetic_leak_set(root: str | Path, sensor_ids: Sequence[str], pipe_ids: Sequence[str],
+                             scenes_per_pipe: int = 2, n_noleak: int = 6, T: int = 400, seed: int = 0) -> dict:
+    """Abrupt-leak set in the reference format (datasets.py:282-435, leak_generation.py):
+    manifest rows {"scenario_id": "NNNNNN_<pipe>_abrupt_rK", "status", "kind": "leak",
+    "leak_type": "abrupt", "pipe_id"} plus no-leak rows {"scenario_id", "kind": "noleak"};
+    each leak scene has leak_flow_m3h.csv (column = pipe id, 0 before the onset) and a
+    pressure drop after the onset.  One row is marked status "failed" (filtered out)."""
+    import pandas as pd
+    root = Path(root)
+    root.mkdir(parents=True, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    rows = []
+    k = 0
+    for pid in pipe_ids:
+        for r in range(scenes_per_pipe):
+            sid = f"{k:06d}_{pid}_abrupt_r{r + 1}"
+            k += 1
+            tau = int(rng.integers(100, T - 60))
+            drop = np.zeros((T, len(sensor_ids)))
+            drop[tau:] = rng.uniform(0.05, 0.5, size=(1, len(sensor_ids)))
+            (root / sid).mkdir(exist_ok=True)
+            gt, noisy = _sensor_frame(sensor_ids, T, rng, start=f"2024-02-{1 + k % 28:02d} 00:00", drop=drop)
+            noisy.to_csv(root / sid / "sensors.csv")
+            gt.to_csv(root / sid / "sensors_gt.csv")
+            q = np.zeros(T)
+            q[tau:] = rng.uniform(1.0, 5.0)
+            pd.DataFrame({pid: q}, index=gt.index).to_csv(root / sid / "leak_flow_m3h.csv")
+            rows.append({"scenario_id": sid, "status": "ok", "kind": "leak", "leak_type": "abrupt", "pipe_id": pid})
+    for j in range(n_noleak):
+        sid = f"{k:06d}_noleak"
+        k += 1
+        (root / sid).mkdir(exist_ok=True)
+        gt, noisy = _sensor_frame(sensor_ids, T, rng, start=f"2024-03-{1 + j % 28:02d} 00:00")
+        noisy.to_csv(root / sid / "sensors.csv")
+        gt.to_csv(root / sid / "sensors_gt.csv")
+        rows.append({"scenario_id": sid, "status": "ok", "kind": "noleak"})
+    rows.append({"scenario_id": "999999_failed", "status": "failed", "kind": "noleak"})
+    with open(root / "manifest.jsonl", "w", encoding="utf-8") as f:
+        for row in rows:
+            f.write(json.dumps(row) + "\n")
+    return {"rows": rows}

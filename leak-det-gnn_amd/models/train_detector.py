@@ -1,0 +1,276 @@
+"""Train + evaluate the leak detector on abrupt single-pipe leak scenarios (+ no-leak)
+(reference models/train_detector.py): same CLI flags (:133-155), scenario splits
+(:41-109), frozen-predictor loading (:112-128), loop order (:296-317), evaluation and
+checkpoint schema (:346-353).
+
+  python -m models.train_detector --leak_root DATA --inp_path L-TOWN-A.inp \\
+         --predictor_ckpt OUT/predictor_best.ckpt --out_dir OUT [...]
+
+The detector is this package's LeakDetector (HIP GRU / GCN / heads kernels); batches
+come from datasets.DeviceBatchLoader (--loader torch restores the DataLoader path);
+the optimizer is AdamW(fused=True) on the GPU.  Checkpoints load with
+torch.load(weights_only=True).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+from collections import defaultdict
+from dataclasses import asdict
+from pathlib import Path
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .datasets import AbruptLeakDetectorDataset, SensorStandardizer
+from .detector import LeakDetector
+from .predictor import NormalPredictorGRU, NormalPredictorTCN
+from .train_predictor import make_loader, pick_device, set_seed
+from .utils import build_residual_sequence_from_segment, now
+from .window_evaluator import DetectorEvaluator
+
+
+def scenario_to_pipe_id(sid: str) -> str:
+    """train_detector.py:41-45: '001927_p534_abrupt_r1' -> 'p534'."""
+    parts = sid.split("_")
+    if len(parts) < 2:
+        raise ValueError(f"Bad scenario_id format: {sid}")
+    return parts[1]
+
+
+def split_leak_scenids(leak_scene_ids: List[str], seed: int, ratio=(0.8, 0.1, 0.1)) -> Tuple[List[str], ...]:
+    """train_detector.py:47-96: every pipe keeps one scene in train; val / test are
+    filled round-robin across pipes from the rest; random.Random(seed) throughout."""
+    rng = random.Random(seed)
+    pipe2scenes = defaultdict(list)
+    for sid in leak_scene_ids:
+        pipe2scenes[scenario_to_pipe_id(sid)].append(sid)
+    train_ids: List[str] = []
+    pipe2rest = {}
+    for pid, scenes in pipe2scenes.items():
+        scenes = list(scenes)
+        rng.shuffle(scenes)
+        train_ids.append(scenes[0])
+        pipe2rest[pid] = scenes[1:]
+    rest_total = sum(len(v) for v in pipe2rest.values())
+    r_train, r_val, r_test = ratio
+    denom = float(r_train + r_val + r_test)
+    val_target = int(round(rest_total * (r_val / denom)))
+    test_target = int(round(rest_total * (r_test / denom)))
+    pipe_keys = list(pipe2rest.keys())
+    rng.shuffle(pipe_keys)
+
+    def pop_one_round_robin(target_n: int) -> List[str]:
+        out: List[str] = []
+        while len(out) < target_n:
+            progressed = False
+            for pid in pipe_keys:
+                if len(out) >= target_n:
+                    break
+                lst = pipe2rest[pid]
+                if lst:
+                    out.append(lst.pop())
+                    progressed = True
+            if not progressed:
+                break
+        return out
+
+    val_ids = pop_one_round_robin(val_target)
+    test_ids = pop_one_round_robin(test_target)
+    for pid in pipe_keys:
+        train_ids.extend(pipe2rest[pid])
+    rng.shuffle(train_ids)
+    rng.shuffle(val_ids)
+    rng.shuffle(test_ids)
+    return train_ids, val_ids, test_ids
+
+
+def split_normal_scenids(ids: List[str], seed: int, ratios=(0.8, 0.1, 0.1)) -> Tuple[List[str], ...]:
+    """train_detector.py:98-109."""
+    assert abs(sum(ratios) - 1.0) < 1e-6
+    rng = random.Random(seed)
+    ids = list(ids)
+    rng.shuffle(ids)
+    n = len(ids)
+    n_train, n_val = int(n * ratios[0]), int(n * ratios[1])
+    return ids[:n_train], ids[n_train:n_train + n_val], ids[n_train + n_val:]
+
+
+def _load_ckpt(path: str | Path, device: torch.device) -> Dict:
+    """Checkpoints written by this package load with weights_only=True.  One written by
+    another trainer with numpy arrays inside needs LEAKGNN_TRUST_CKPT=1 (explicit opt-in
+    to a full unpickle of a file the user vouches for)."""
+    try:
+        return torch.load(path, map_location=device, weights_only=True)
+    except Exception:
+        if os.environ.get("LEAKGNN_TRUST_CKPT") == "1":
+            return torch.load(path, map_location=device, weights_only=False)
+        raise
+
+
+def load_predictor(ckpt_path: str | Path, device: torch.device) -> Tuple[nn.Module, Dict]:
+    """Frozen predictor (train_detector.py:112-128)."""
+    ckpt = _load_ckpt(ckpt_path, device)
+    S = len(ckpt["sensor_ids"])
+    model = NormalPredictorGRU(num_sensors=S, time_dim=9) if ckpt.get("arch", "tcn") == "gru" else \
+        NormalPredictorTCN(num_sensors=S, time_dim=9)
+    model.load_state_dict(ckpt["model_state"])
+    model.to(device)
+    model.eval()
+    for p in model.parameters():
+        p.requires_grad_(False)
+    return model, ckpt
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--leak_root", type=str, required=True, help="Path to leak dataset root")
+    ap.add_argument("--inp_path", type=str, required=True, help="Path to EPANET .inp file")
+    ap.add_argument("--predictor_ckpt", type=str, required=True, help="Path to trained predictor checkpoint")
+    ap.add_argument("--out_dir", type=str, required=True, help="Output directory for detector checkpoints/logs")
+    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--steps_per_epoch", type=int, default=120000)
+    ap.add_argument("--val_steps", type=int, default=10000)
+    ap.add_argument("--test_steps", type=int, default=10000)
+    ap.add_argument("--batch_size", type=int, default=128)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--weight_decay", type=float, default=1e-4)
+    ap.add_argument("--grad_clip", type=float, default=1.0)
+    ap.add_argument("--l_pred", type=int, default=36)
+    ap.add_argument("--l_det", type=int, default=36)
+    ap.add_argument("--topk", type=int, default=5)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--device", type=str, default="auto")
+    ap.add_argument("--num_workers", type=int, default=0)
+    ap.add_argument("--log_every", type=int, default=50)
+    ap.add_argument("--loader", type=str, default="device", choices=["device", "torch"])
+    args = ap.parse_args(argv)
+
+    out_dir = Path(args.out_dir)
+    out_dir.mkdir(parents=True, exist_ok=True)
+    set_seed(args.seed)
+    device = pick_device(args.device)
+    print(f"{now()} [detector] device={device} seed={args.seed}")
+    print(f"{now()} [detector] leak_root={args.leak_root}")
+    print(f"{now()} [detector] inp_path={args.inp_path}")
+    print(f"{now()} [detector] predictor_ckpt={args.predictor_ckpt}")
+
+    predictor, predictor_ckpt = load_predictor(args.predictor_ckpt, device)
+    sensor_ids: List[str] = list(predictor_ckpt["sensor_ids"])
+    std_mean, std_std = predictor_ckpt.get("standardizer_mean"), predictor_ckpt.get("standardizer_std")
+    if std_mean is None or std_std is None:
+        raise ValueError("Error: predictor ckpt missing standardizer stats.")
+    stdzr = SensorStandardizer(mean=np.asarray(std_mean.cpu() if torch.is_tensor(std_mean) else std_mean,
+                                               dtype=np.float32),
+                               std=np.asarray(std_std.cpu() if torch.is_tensor(std_std) else std_std,
+                                              dtype=np.float32))
+
+    base_ds = AbruptLeakDetectorDataset(leak_root=args.leak_root, steps_per_epoch=1, seed=args.seed,
+                                        standardizer=stdzr)
+    if sensor_ids != base_ds.get_sensor_node_ids():
+        raise ValueError("Sensor IDs do not match between the normal and abrupt datasets.")
+    pipe_ids_in_order = base_ds.get_pipe_ids_in_order()
+    leak_train, leak_val, leak_test = split_leak_scenids(base_ds.leak_scene_ids, args.seed, ratio=(0.8, 0.1, 0.1))
+    nl_train, nl_val, nl_test = split_normal_scenids(base_ds.noleak_scene_ids, args.seed + 11,
+                                                     ratios=(0.8, 0.1, 0.1))
+    train_pipes, all_pipes = {scenario_to_pipe_id(s) for s in leak_train}, set(pipe_ids_in_order)
+    missing = all_pipes - train_pipes
+    if missing:
+        raise RuntimeError(f"Train split missing {len(missing)} pipes, e.g. {sorted(list(missing))[:10]}")
+    print(f"{now()} [detector] train dataset covers leak pipes: {len(train_pipes)}/{len(all_pipes)}")
+    print(f"{now()} [detector] leak scenes: total={len(base_ds.leak_scene_ids)} train={len(leak_train)} "
+          f"val={len(leak_val)} test={len(leak_test)}")
+    print(f"{now()} [detector] noleak scenes: total={len(base_ds.noleak_scene_ids)} train={len(nl_train)} "
+          f"val={len(nl_val)} test={len(nl_test)}")
+    print(f"{now()} [detector] classes: num_pipes={base_ds.num_pipes} num_classes={base_ds.num_pipes + 1}")
+
+    def mk(steps, seed, cache, leak_ids, nl_ids):
+        ds = AbruptLeakDetectorDataset(leak_root=args.leak_root, l_pred_steps=args.l_pred, l_det_steps=args.l_det,
+                                       steps_per_epoch=steps, seed=seed, sensor_ids=sensor_ids, standardizer=stdzr,
+                                       cache_size=cache)
+        ds.leak_scene_ids, ds.noleak_scene_ids = leak_ids, nl_ids
+        return ds, make_loader(ds, args.batch_size, device, args.loader, args.num_workers)
+
+    train_ds, train_loader = mk(args.steps_per_epoch, args.seed, 4096, leak_train, nl_train)
+    _, val_loader = mk(args.val_steps, args.seed + 1, 2048, leak_val, nl_val)
+    _, test_loader = mk(args.test_steps, args.seed + 2, 2048, leak_test, nl_test)
+
+    detector = LeakDetector(inp_path=args.inp_path, sensor_node_ids=sensor_ids, pipe_ids_in_order=pipe_ids_in_order,
+                            sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1, use_time=True).to(device)
+    opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay,
+                            fused=(device.type == "cuda"))
+    loss_fn = nn.CrossEntropyLoss()
+    evaluator = DetectorEvaluator(predictor=predictor, detector=detector, device=device, l_pred=args.l_pred,
+                                  l_det=args.l_det,
+                                  metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
+                                  topk=args.topk, inp_path=args.inp_path, pipe_ids_in_order=pipe_ids_in_order)
+
+    best_acc = -1.0
+    best_path, last_path = out_dir / "detector_best.ckpt", out_dir / "detector_last.ckpt"
+    meta = {
+        "inp_path": str(args.inp_path), "predictor_ckpt": str(args.predictor_ckpt), "sensor_ids": sensor_ids,
+        "pipe_ids_in_order": pipe_ids_in_order, "num_classes": int(base_ds.num_pipes + 1),
+        "sampling_config": asdict(train_ds.cfg),
+        "split": {"leak_train": leak_train, "leak_val": leak_val, "leak_test": leak_test,
+                  "noleak_train": nl_train, "noleak_val": nl_val, "noleak_test": nl_test},
+        "args": vars(args),
+    }
+    (out_dir / "detector_meta.json").write_text(json.dumps(meta, indent=2, ensure_ascii=False), encoding="utf-8")
+
+    def report(tag: str, m: Dict[str, float]) -> None:
+        line = (f"{now()} [detector] {tag} leak_ar={m['ar_mean']:.4f} "
+                f"leak_hit@{args.topk}={m[f'leak_acc_top{args.topk}']:.4f} det_f1={m.get('det_f1', 0.0):.4f} "
+                f"det_p={m.get('det_precision', 0.0):.4f} det_r={m.get('det_recall', 0.0):.4f} "
+                f"ATD={m['atd_mean_m']:.4f}")
+        line += "".join(f" success_at_{int(r)}={m[f'success_at_{int(r)}']:.4f}" for r in evaluator.success_radii_m)
+        line += "".join(f" accuracy_{int(i)}={m[f'accuracy_{int(i)}']:.4f}" for i in evaluator.accuracy_is)
+        print(line)
+
+    print(f"{now()} [detector] start training: epochs={args.epochs}, steps/epoch={args.steps_per_epoch}, "
+          f"batch={args.batch_size}")
+    for epoch in range(1, args.epochs + 1):
+        detector.train()
+        running = torch.zeros((), dtype=torch.float64, device=device)
+        seen = 0
+        for it, batch in enumerate(train_loader, start=1):
+            noisy_seg = batch["noisy_seg"].to(device)
+            time_seg = batch["time_seg"].to(device)
+            label = torch.as_tensor(batch["label"], device=device, dtype=torch.long)
+            with torch.no_grad():
+                residual = build_residual_sequence_from_segment(predictor, noisy_seg, time_seg, l_pred=args.l_pred,
+                                                                l_det=args.l_det, device=device)
+            logits = detector(residual, time_seg[:, args.l_pred:, :])
+            loss = loss_fn(logits, label)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            if args.grad_clip and args.grad_clip > 0:
+                torch.nn.utils.clip_grad_norm_(detector.parameters(), args.grad_clip)
+            opt.step()
+            running += loss.detach().double() * noisy_seg.size(0)
+            seen += noisy_seg.size(0)
+            if (it % args.log_every) == 0:
+                print(f"{now()} [detector][epoch {epoch:02d}] step {it:05d}/{len(train_loader):05d} "
+                      f"loss={running.item() / max(seen, 1):.6f}")
+        val_metrics = evaluator.evaluate(val_loader)
+        report(f"[epoch {epoch:02d}] done. train_loss={running.item() / max(seen, 1):.6f}", val_metrics)
+        ckpt = {"epoch": epoch, "detector_state": detector.state_dict(), "sensor_ids": sensor_ids,
+                "pipe_ids_in_order": pipe_ids_in_order, "num_classes": int(len(pipe_ids_in_order) + 1),
+                "predictor_ckpt": str(args.predictor_ckpt), "args": vars(args)}
+        torch.save(ckpt, last_path)
+        if val_metrics["acc_top1"] > best_acc:
+            best_acc = val_metrics["acc_top1"]
+            torch.save(ckpt, best_path)
+            print(f"{now()} [detector] new best: acc_top1={best_acc:.4f} -> {best_path.name}")
+
+    best_ckpt = torch.load(best_path, map_location=device, weights_only=True)
+    detector.load_state_dict(best_ckpt["detector_state"])
+    report("TEST:", evaluator.evaluate(test_loader))
+    print(f"{now()} [detector] saved: {best_path.name}, {last_path.name}, meta.json")
+
+
+if __name__ == "__main__":
+    main()

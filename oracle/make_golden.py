@@ -52,13 +52,15 @@ def _import_reference(ref: Path):
 def write_topology_inp(rutils, src: Path, dst: Path) -> None:
     sec = rutils.parse_epanet_inp(src)
     keep = ["JUNCTIONS", "RESERVOIRS", "TANKS", "PIPES", "PUMPS", "VALVES"]
-    lines = [f"[TITLE]", f"topology extracted from {src.name} by oracle/make_golden.py (ids and link endpoints only)",
-             ""]
+    lines = [f"[TITLE]", f"topology extracted from {src.name} by oracle/make_golden.py (ids, link endpoints and "
+             f"pipe lengths only)", ""]
     for s in keep:
         lines.append(f"[{s}]")
         for ln in sec.get(s, []):
             tok = ln.split()
-            lines.append(" ".join(tok[:3]) if s in ("PIPES", "PUMPS", "VALVES") else tok[0])
+            # pipes keep their length (distance metrics, window_evaluator.py:76-110)
+            lines.append(" ".join(tok[:4]) if s == "PIPES" else " ".join(tok[:3]) if s in ("PUMPS", "VALVES")
+                         else tok[0])
         lines.append("")
     lines.append("[END]")
     dst.parent.mkdir(parents=True, exist_ok=True)
@@ -137,6 +139,87 @@ def predictor_fixture(rutils, rpred, out: Path) -> None:
     np.savez_compressed(out, **arrs)
 
 
+class FixedLogitsDetector(torch.nn.Module):
+    """Deterministic stand-in detector for the evaluator fixture (weights stored in the
+    fixture): logits = 3 tanh(mean_t(residual) A + mean_t(tfeat) Bm) + c."""
+
+    def __init__(self, A, Bm, c):
+        super().__init__()
+        self.A, self.Bm, self.c = (torch.as_tensor(v, dtype=torch.float32) for v in (A, Bm, c))
+
+    def forward(self, residual, tfeat):
+        dev = residual.device
+        return 3.0 * torch.tanh(residual.mean(1) @ self.A.to(dev) + tfeat.mean(1) @ self.Bm.to(dev)) + self.c.to(dev)
+
+
+def harness_fixture(ref: Path, rpred, lta_inp: Path, pipe_pool, out_npz: Path, out_json: Path) -> dict:
+    """Data-pipeline / trainer-split / evaluator fixtures: the reference's own
+    models/datasets.py, train_detector.py split functions and window_evaluator.py run on
+    a seeded synthetic data set written by models/synth.py (regenerated by the tests)."""
+    import importlib.util
+    import tempfile
+    # the product's data writer, loaded standalone (both code bases name their package `models`)
+    spec = importlib.util.spec_from_file_location("lg_synth", REPO / "leak-det-gnn_amd" / "models" / "synth.py")
+    lg_synth = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lg_synth)
+    write_synthetic_leak_set, write_synthetic_normal_set = lg_synth.write_synthetic_leak_set, \
+        lg_synth.write_synthetic_normal_set
+    import models.datasets as rds  # the reference's
+    import models.train_detector as rtd
+    import models.window_evaluator as rwe
+    assert str(ref) in rds.__file__, rds.__file__
+    pipes = [pipe_pool[i] for i in (3, 50, 120, 333, 500, 700)]
+    arrs, info = {}, {"pipes": pipes, "sensors": SENSORS}
+    with tempfile.TemporaryDirectory() as d:
+        d = Path(d)
+        write_synthetic_normal_set(d / "normal", SENSORS, n_windows=12, T=577, seed=0)
+        write_synthetic_leak_set(d / "leak", SENSORS, pipes, scenes_per_pipe=2, n_noleak=6, T=400, seed=0)
+        st = rds.compute_sensor_stats_from_normal(d / "normal")
+        arrs["std_mean"], arrs["std_std"] = st.mean, st.std
+        nds = rds.NormalPredictorDataset(d / "normal", steps_per_epoch=50, seed=42, standardizer=st)
+        info["normal_samples"] = []
+        for i in range(8):
+            smp = nds[i]
+            info["normal_samples"].append({"scene_id": str(smp["scene_id"]), "t": smp["t"]})
+            for k in ("x", "x_time", "y"):
+                arrs[f"normal.{i}.{k}"] = smp[k].numpy()
+        lds = rds.AbruptLeakDetectorDataset(d / "leak", steps_per_epoch=64, seed=123, standardizer=st,
+                                            sensor_ids=SENSORS)
+        info["leak_scene_ids"] = [str(x) for x in lds.leak_scene_ids]
+        info["noleak_scene_ids"] = [str(x) for x in lds.noleak_scene_ids]
+        info["pipe_ids_in_order"] = lds.get_pipe_ids_in_order()
+        info["bucket_sizes"] = {sid: {b: int(v.size) for b, v in bt.items()} for sid, bt in lds._bucket_times.items()}
+        info["leak_samples"] = []
+        for i in range(24):
+            smp = lds[i]
+            info["leak_samples"].append({k: (str(v) if k in ("scenario_id", "bucket", "t", "pipe_id") else int(v))
+                                         for k, v in smp.items() if k not in ("noisy_seg", "time_seg")})
+            arrs[f"leak.{i}.noisy_seg"] = smp["noisy_seg"].numpy()
+            arrs[f"leak.{i}.time_seg"] = smp["time_seg"].numpy()
+        # trainer splits on a larger id list
+        fake = [f"{k:06d}_p{k % 12}_abrupt_r{k // 12 + 1}" for k in range(50)]
+        info["split_leak"] = [list(x) for x in rtd.split_leak_scenids(fake, 42, ratio=(0.8, 0.1, 0.1))]
+        info["split_normal"] = [list(x) for x in rtd.split_normal_scenids([f"w{k}" for k in range(23)], 53)]
+        # evaluator on a fixed predictor + stand-in detector
+        torch.manual_seed(0)
+        tcn = rpred.NormalPredictorTCN(num_sensors=29, time_dim=9).eval()
+        g = torch.Generator().manual_seed(11)
+        P1 = len(pipes) + 1
+        A, Bm, c = torch.randn(29, P1, generator=g), torch.randn(9, P1, generator=g), torch.randn(P1, generator=g)
+        arrs["eval.A"], arrs["eval.Bm"], arrs["eval.c"] = A.numpy(), Bm.numpy(), c.numpy()
+        det = FixedLogitsDetector(A, Bm, c)
+        eds = rds.AbruptLeakDetectorDataset(d / "leak", steps_per_epoch=48, seed=7, standardizer=st,
+                                            sensor_ids=SENSORS)
+        ev = rwe.DetectorEvaluator(tcn, det, torch.device("cpu"), l_pred=36, l_det=36, topk=5,
+                                   metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
+                                   inp_path=lta_inp, pipe_ids_in_order=lds.get_pipe_ids_in_order())
+        from torch.utils.data import DataLoader
+        info["eval_metrics"] = {k: float(v) for k, v in ev.evaluate(DataLoader(eds, batch_size=16)).items()}
+    np.savez_compressed(out_npz, **arrs)
+    out_json.write_text(json.dumps(info, indent=1) + "\n")
+    return {"normal_samples": 8, "leak_samples": 24, "eval_metrics": len(info["eval_metrics"])}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -156,6 +239,7 @@ def main() -> None:
     detector_fixture(rdet, lta, pipe_ids, 2, GOLD / "detector_b2.npz", with_state=True, with_trace=True)
     detector_fixture(rdet, lta, pipe_ids, 8, GOLD / "detector_b8.npz", with_state=False, with_trace=False)
     predictor_fixture(rutils, rpred, GOLD / "predictor.npz")
+    meta["harness"] = harness_fixture(ref, rpred, lta, pipe_ids, GOLD / "harness.npz", GOLD / "harness.json")
     (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
     print(json.dumps(meta, indent=2))
 

@@ -1,0 +1,82 @@
+"""GPU side of the harness (SURVEY §8 b, f-3): the HBM-resident batch path equals the
+reference-style DataLoader path, and train_predictor / train_detector run end to end on
+the synthetic data set with the reference CLI flags."""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import GOLD, LTA_INP
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+INFO = json.loads((GOLD / "harness.json").read_text())
+
+
+@pytest.fixture(scope="module")
+def data(tmp_path_factory):
+    from models.synth import write_synthetic_leak_set, write_synthetic_normal_set
+    d = tmp_path_factory.mktemp("synthds_gpu")
+    write_synthetic_normal_set(d / "normal", INFO["sensors"], n_windows=12, T=577, seed=0)
+    write_synthetic_leak_set(d / "leak", INFO["sensors"], INFO["pipes"], scenes_per_pipe=2, n_noleak=6, T=400, seed=0)
+    return d
+
+
+def _same_batch(a: dict, b: dict):
+    assert set(a) == set(b)
+    for k in a:
+        if torch.is_tensor(b[k]):
+            assert torch.equal(a[k].cpu(), b[k].cpu()), k
+        else:
+            assert list(a[k]) == list(b[k]), k
+
+
+def test_device_loader_equals_dataloader(data):
+    from torch.utils.data import DataLoader
+    from models.datasets import (AbruptLeakDetectorDataset, DeviceBatchLoader, NormalPredictorDataset,
+                                 compute_sensor_stats_from_normal)
+    st = compute_sensor_stats_from_normal(data / "normal")
+    dds = AbruptLeakDetectorDataset(data / "leak", steps_per_epoch=37, seed=5, standardizer=st,
+                                    sensor_ids=INFO["sensors"])
+    ref = list(DataLoader(dds, batch_size=8))
+    got = list(DeviceBatchLoader(dds, 8, DEV))
+    assert len(ref) == len(got) == 5
+    for a, b in zip(got, ref):
+        assert a["noisy_seg"].device.type == "cuda"
+        _same_batch(a, b)
+    nds = NormalPredictorDataset(data / "normal", steps_per_epoch=20, seed=3, standardizer=st)
+    for a, b in zip(DeviceBatchLoader(nds, 8, DEV), DataLoader(nds, batch_size=8)):
+        _same_batch(a, b)
+
+
+def test_train_predictor_and_detector_cli(data, tmp_path, capsys):
+    """Reference CLI flags end to end.  The leak set here has enough scenes for non-empty
+    80/10/10 splits (the reference trainer needs >= 1 scene per split)."""
+    from models import train_detector, train_predictor
+    from models.synth import write_synthetic_leak_set
+    write_synthetic_leak_set(tmp_path / "leak", INFO["sensors"], INFO["pipes"], scenes_per_pipe=4, n_noleak=12,
+                             T=300, seed=1)
+    out = tmp_path / "out"
+    train_predictor.main(["--normal_root", str(data / "normal"), "--out_dir", str(out), "--epochs", "1",
+                          "--steps_per_epoch", "32", "--val_steps", "16", "--test_steps", "16", "--batch_size", "8",
+                          "--device", "cuda", "--log_every", "2"])
+    ck = torch.load(out / "predictor_best.ckpt", weights_only=True)
+    assert ck["sensor_ids"] == INFO["sensors"] and ck["arch"] == "tcn"
+    assert set(ck) == {"epoch", "arch", "model_state", "standardizer_mean", "standardizer_std", "sensor_ids", "args"}
+    train_detector.main(["--leak_root", str(tmp_path / "leak"), "--inp_path", str(LTA_INP), "--predictor_ckpt",
+                         str(out / "predictor_best.ckpt"), "--out_dir", str(out), "--epochs", "2",
+                         "--steps_per_epoch", "16", "--val_steps", "16", "--test_steps", "16", "--batch_size", "8",
+                         "--device", "cuda", "--log_every", "1"])
+    ck = torch.load(out / "detector_best.ckpt", weights_only=True)
+    assert ck["pipe_ids_in_order"] == INFO["pipe_ids_in_order"] and ck["num_classes"] == len(INFO["pipes"]) + 1
+    assert set(ck) == {"epoch", "detector_state", "sensor_ids", "pipe_ids_in_order", "num_classes",
+                       "predictor_ckpt", "args"}
+    meta = json.loads((out / "detector_meta.json").read_text())
+    assert meta["sampling_config"]["p_early"] == 0.3
+    log = capsys.readouterr().out
+    assert "[detector] TEST:" in log and "ATD=" in log and "loss=" in log
+    losses = [float(l.split("loss=")[1].split()[0]) for l in log.splitlines() if "[detector][epoch" in l and "loss=" in l]
+    assert all(np.isfinite(losses)) and len(losses) >= 2

@@ -1,0 +1,119 @@
+"""Caller-harness counterparts (SURVEY §8 b) and the data pipeline (§8 f rank 3) against
+fixtures produced by the reference's own models/datasets.py, train_detector.py split
+functions and window_evaluator.py (oracle/make_golden.py: harness_fixture) on a seeded
+synthetic data set in the reference on-disk format, regenerated here by models/synth.py.
+
+Bars: sampled indices / ids / labels / buckets / timestamps exact; window arrays and the
+standardizer bit-exact (same float32 arithmetic); evaluator metrics exact for counts and
+rates and within 1e-9 relative for the distance means.
+"""
+from __future__ import annotations
+
+import json
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import GOLD, LTA_INP, lta_ids
+
+SENSORS = json.loads((GOLD / "harness.json").read_text())["sensors"]
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return json.loads((GOLD / "harness.json").read_text()), np.load(GOLD / "harness.npz")
+
+
+@pytest.fixture(scope="module")
+def data(tmp_path_factory, fx):
+    from models.synth import write_synthetic_leak_set, write_synthetic_normal_set
+    info, _ = fx
+    d = tmp_path_factory.mktemp("synthds")
+    write_synthetic_normal_set(d / "normal", SENSORS, n_windows=12, T=577, seed=0)
+    write_synthetic_leak_set(d / "leak", SENSORS, info["pipes"], scenes_per_pipe=2, n_noleak=6, T=400, seed=0)
+    return d
+
+
+def test_standardizer_and_predictor_samples(fx, data):
+    from models.datasets import NormalPredictorDataset, compute_sensor_stats_from_normal
+    info, arrs = fx
+    st = compute_sensor_stats_from_normal(data / "normal")
+    assert np.array_equal(st.mean, arrs["std_mean"]) and np.array_equal(st.std, arrs["std_std"])
+    ds = NormalPredictorDataset(data / "normal", steps_per_epoch=50, seed=42, standardizer=st)
+    for i, ref in enumerate(info["normal_samples"]):
+        s = ds[i]
+        assert (s["scene_id"], s["t"]) == (ref["scene_id"], ref["t"]), i
+        for k in ("x", "x_time", "y"):
+            assert np.array_equal(s[k].numpy(), arrs[f"normal.{i}.{k}"]), (i, k)
+
+
+def test_detector_dataset_samples(fx, data):
+    from models.datasets import AbruptLeakDetectorDataset, SensorStandardizer
+    info, arrs = fx
+    st = SensorStandardizer(arrs["std_mean"], arrs["std_std"])
+    ds = AbruptLeakDetectorDataset(data / "leak", steps_per_epoch=64, seed=123, standardizer=st, sensor_ids=SENSORS)
+    assert ds.leak_scene_ids == info["leak_scene_ids"]
+    assert ds.noleak_scene_ids == info["noleak_scene_ids"]   # the "failed" manifest row is filtered out
+    assert ds.get_pipe_ids_in_order() == info["pipe_ids_in_order"]
+    assert {sid: {b: int(v.size) for b, v in bt.items()} for sid, bt in ds._bucket_times.items()} == \
+        info["bucket_sizes"]
+    buckets = set()
+    for i, ref in enumerate(info["leak_samples"]):
+        s = ds[i]
+        got = {k: (str(v) if k in ("scenario_id", "bucket", "t", "pipe_id") else int(v))
+               for k, v in s.items() if k not in ("noisy_seg", "time_seg")}
+        assert got == ref, i
+        assert np.array_equal(s["noisy_seg"].numpy(), arrs[f"leak.{i}.noisy_seg"]), i
+        assert np.array_equal(s["time_seg"].numpy(), arrs[f"leak.{i}.time_seg"]), i
+        buckets.add(ref["bucket"])
+    assert buckets == {"early", "late", "pre", "noleak"}  # every sampling bucket is exercised
+
+
+def test_trainer_splits(fx):
+    from models.train_detector import split_leak_scenids, split_normal_scenids
+    info, _ = fx
+    fake = [f"{k:06d}_p{k % 12}_abrupt_r{k // 12 + 1}" for k in range(50)]
+    assert [list(x) for x in split_leak_scenids(fake, 42, ratio=(0.8, 0.1, 0.1))] == info["split_leak"]
+    assert [list(x) for x in split_normal_scenids([f"w{k}" for k in range(23)], 53)] == info["split_normal"]
+
+
+def _fixed_detector(arrs):
+    class FixedLogitsDetector(torch.nn.Module):
+        def forward(self, residual, tfeat):
+            dev = residual.device
+            A, Bm, c = (torch.from_numpy(arrs[f"eval.{k}"]).to(dev) for k in ("A", "Bm", "c"))
+            return 3.0 * torch.tanh(residual.mean(1) @ A + tfeat.mean(1) @ Bm) + c
+    return FixedLogitsDetector()
+
+
+def _tcn():
+    from models.predictor import NormalPredictorTCN
+    p = np.load(GOLD / "predictor.npz")
+    m = NormalPredictorTCN(num_sensors=29, time_dim=9).eval()
+    m.load_state_dict({k[4:]: torch.from_numpy(p[k]) for k in p.files if k.startswith("tcn.")})
+    return m
+
+
+def _check_metrics(got: dict, ref: dict):
+    assert set(got) == set(ref), set(got) ^ set(ref)
+    for k, v in ref.items():
+        g = got[k]
+        if math.isinf(v):
+            assert math.isinf(g), k
+        else:
+            assert abs(g - v) <= 1e-9 * max(1.0, abs(v)), (k, g, v)
+
+
+def test_window_evaluator_matches_reference(fx, data):
+    from torch.utils.data import DataLoader
+    from models.datasets import AbruptLeakDetectorDataset, SensorStandardizer
+    from models.window_evaluator import DetectorEvaluator
+    info, arrs = fx
+    st = SensorStandardizer(arrs["std_mean"], arrs["std_std"])
+    eds = AbruptLeakDetectorDataset(data / "leak", steps_per_epoch=48, seed=7, standardizer=st, sensor_ids=SENSORS)
+    ev = DetectorEvaluator(_tcn(), _fixed_detector(arrs), torch.device("cpu"), l_pred=36, l_det=36, topk=5,
+                           metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
+                           inp_path=LTA_INP, pipe_ids_in_order=info["pipe_ids_in_order"])
+    _check_metrics(ev.evaluate(DataLoader(eds, batch_size=16)), info["eval_metrics"])
