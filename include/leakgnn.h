@@ -262,6 +262,25 @@ int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, con
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H,
                void* workspace, lg_stream_t stream);
 
+/* ---- Frozen-predictor residual builder (SURVEY 8 f rank 1) ----------------------
+ * Replaces the per-window NormalPredictorTCN passes of
+ * build_residual_sequence_from_segment (reference models/utils.py:169-216, TCN
+ * models/predictor.py:17-81) with ONE pass per segment over the shared-window row plan
+ * of models/tcn_plan.py: output row r of a conv layer reads input rows plan[r].x/.y/.z
+ * (taps t, t-d, t-2d; -1 = zero padding) and, for a block's second conv, adds block-input
+ * row plan[r].w (-1 = none).  Rows are segment-local; tensors are [nseg][rows][C].
+ * C must be 128 (the TCN default, LG_EUNSUPPORTED otherwise); rows_out <= 2048.
+ *   lg_tcn_pack_weight   Conv1d weight [C][C][3] -> packed fragment order
+ *                        (lg_tcn_packed_weight_floats(C) floats), once per weight.
+ *   lg_tcn_conv_fwd      y = LayerNorm(conv(x) + bias) -> ReLU (-> + residual), exact
+ *                        fp32 (MFMA f32); blk = NULL for a block's first conv.  */
+int64_t lg_tcn_packed_weight_floats(int64_t C);
+int lg_tcn_pack_weight(const float* weight, float* packed, int64_t C, lg_stream_t stream);
+int lg_tcn_conv_fwd(const float* in, const float* blk, const int32_t* plan, const float* packed_weight,
+                    const float* bias, const float* ln_w, const float* ln_b, float eps, float* out,
+                    int64_t nseg, int64_t rows_in, int64_t rows_blk, int64_t rows_out, int64_t C,
+                    lg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

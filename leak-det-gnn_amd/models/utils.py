@@ -16,6 +16,7 @@ device by libleakgnn.
 """
 from __future__ import annotations
 
+import os
 import re
 from dataclasses import dataclass
 from datetime import datetime
@@ -24,6 +25,8 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+
+from . import tcn_plan
 
 _SECTION = re.compile(r"^\s*\[(.+?)\]\s*$")
 
@@ -132,6 +135,10 @@ def build_wdn_graph_from_inp(
                     pipe_ends=pipe_ends, edge_index=edge_index)
 
 
+# LEAKGNN_RESIDUAL=stock keeps the per-window module calls (for A/B timing).
+RESIDUAL_FAST_PATH = os.environ.get("LEAKGNN_RESIDUAL", "fast") != "stock"
+
+
 def build_residual_sequence_from_segment(predictor: Any, noisy_seg: Any, time_seg: Any, l_pred: int, l_det: int,
                                          device: Optional[Any] = None) -> Any:
     """residual[b, k] = noisy[b, l_pred+k] - predictor(noisy[b, k:k+l_pred], time[b, k:k+l_pred]).
@@ -145,6 +152,11 @@ def build_residual_sequence_from_segment(predictor: Any, noisy_seg: Any, time_se
     assert T == l_pred + l_det, (T, l_pred, l_det)
     if device is not None:
         noisy_seg, time_seg = noisy_seg.to(device), time_seg.to(device)
+    if noisy_seg.is_cuda and RESIDUAL_FAST_PATH and tcn_plan.fast_path_eligible(predictor):
+        # frozen default TCN on the GPU: one shared-window pass per segment (HIP,
+        # lg_tcn_conv_fwd); same values as the per-window passes below within fp32 rounding
+        res = tcn_plan.tcn_residual(predictor, noisy_seg.float(), time_seg.float(), l_pred, l_det)
+        return res.squeeze(0) if squeeze else res
     # (l_det, B, l_pred, C) windows via unfold: window k covers [k, k + l_pred)
     xw = noisy_seg.unfold(1, l_pred, 1)[:, :l_det].permute(1, 0, 3, 2).reshape(l_det * B, l_pred, S)
     tw = time_seg.unfold(1, l_pred, 1)[:, :l_det].permute(1, 0, 3, 2).reshape(l_det * B, l_pred, -1)

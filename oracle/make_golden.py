@@ -220,13 +220,47 @@ def harness_fixture(ref: Path, rpred, lta_inp: Path, pipe_pool, out_npz: Path, o
     return {"normal_samples": 8, "leak_samples": 24, "eval_metrics": len(info["eval_metrics"])}
 
 
+RESIDUAL_CASES = ((36, 36, 3), (12, 20, 2), (64, 8, 2), (40, 1, 2))  # (l_pred, l_det, B)
+
+
+def residual_fixture(rutils, rpred, out: Path) -> dict:
+    """Residual builder (utils.py:169-216) on a TCN with non-trivial LayerNorm affine and
+    conv biases, at several (l_pred, l_det): pins the shared-window row plan beyond the
+    default 36/36 case."""
+    torch.manual_seed(3)
+    tcn = rpred.NormalPredictorTCN(num_sensors=29, time_dim=9).eval()
+    g = torch.Generator().manual_seed(5)
+    with torch.no_grad():
+        for blk in tcn.tcn:
+            for norm in (blk.norm1, blk.norm2):
+                norm.weight.copy_(1.0 + 0.5 * torch.randn(norm.weight.shape, generator=g))
+                norm.bias.copy_(0.3 * torch.randn(norm.bias.shape, generator=g))
+    arrs = {"tcn." + n: p.numpy() for n, p in tcn.state_dict().items()}
+    arrs["cases"] = np.array(RESIDUAL_CASES, dtype=np.int64)
+    for i, (lp, ld, B) in enumerate(RESIDUAL_CASES):
+        seg = torch.randn(B, lp + ld, 29, generator=g)
+        tseg = torch.randn(B, lp + ld, 9, generator=g)
+        with torch.no_grad():
+            res = rutils.build_residual_sequence_from_segment(tcn, seg, tseg, l_pred=lp, l_det=ld)
+        arrs[f"seg{i}"], arrs[f"tseg{i}"], arrs[f"res{i}"] = seg.numpy(), tseg.numpy(), res.numpy()
+    np.savez_compressed(out, **arrs)
+    return {"cases": [list(c) for c in RESIDUAL_CASES]}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", choices=["residual"], default=None,
+                    help="regenerate one fixture only (leaves the others byte-identical)")
     args = ap.parse_args()
     ref = Path(args.ref)
     rutils, rpred, rdet = _import_reference(ref)
     GOLD.mkdir(parents=True, exist_ok=True)
+    if args.only == "residual":
+        meta = json.loads((GOLD / "meta.json").read_text())
+        meta["residual"] = residual_fixture(rutils, rpred, GOLD / "residual.npz")
+        (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
+        return
     lta = ref / "data/raw/L-TOWN-A/L-TOWN_AreaA.inp"
     lt = ref / "data/raw/L-TOWN/L-TOWN.inp"
     write_topology_inp(rutils, lta, DATA / "L-TOWN-A.inp")
@@ -239,6 +273,7 @@ def main() -> None:
     detector_fixture(rdet, lta, pipe_ids, 2, GOLD / "detector_b2.npz", with_state=True, with_trace=True)
     detector_fixture(rdet, lta, pipe_ids, 8, GOLD / "detector_b8.npz", with_state=False, with_trace=False)
     predictor_fixture(rutils, rpred, GOLD / "predictor.npz")
+    meta["residual"] = residual_fixture(rutils, rpred, GOLD / "residual.npz")
     meta["harness"] = harness_fixture(ref, rpred, lta, pipe_ids, GOLD / "harness.npz", GOLD / "harness.json")
     (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
     print(json.dumps(meta, indent=2))

@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == 3
+    assert lib.lg_abi_version() == 4
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
     assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * (1532 + 661))
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1

@@ -138,6 +138,42 @@ def main():
                                              ptr(ws), st), "gru bwd")
             t = timeit(f, args.iters)
             res["gru_bwd"] = {"us": t, "TFLOPs": 2 * flops / t / 1e6}
+    if "tcn" in which:
+        # frozen-predictor residual builder, B segments of l_pred + l_det = 72 steps
+        from models import tcn_plan
+        from models import utils as mutils
+        from models.predictor import NormalPredictorTCN
+        torch.manual_seed(0)
+        m = NormalPredictorTCN(29, 9).eval().to(dev)
+        seg, tseg = torch.randn(B, 72, 29, device=dev), torch.randn(B, 72, 9, device=dev)
+        plan = tcn_plan.plan_for(36, 36)
+        conv_flops = sum(cp.rows for cp in plan.convs) * B * 2 * 128 * 384
+        with torch.no_grad():
+            f = lambda: tcn_plan.tcn_residual(m, seg, tseg, 36, 36)
+            t = timeit(f, args.iters)
+            res["tcn_residual"] = {"us": t, "conv_TFLOPs": conv_flops / t / 1e6, "segments_per_s": B / t * 1e6}
+            # one conv layer alone (the widest: rows 252)
+            li = max(range(8), key=lambda i: plan.convs[i].rows)
+            cp = plan.convs[li]
+            rows_prev = plan.convs[li - 1].rows
+            xin = torch.randn(B * rows_prev, 128, device=dev)
+            blk_in = torch.randn(B * plan.convs[li - 2].rows, 128, device=dev) if li % 2 == 1 else None
+            out = torch.empty(B * cp.rows, 128, device=dev)
+            dp = tcn_plan._DevicePlan(plan, dev)
+            packed = tcn_plan._packed_weights(m, dev)
+            blk = m.tcn[li // 2]
+            conv, norm = (blk.conv1.conv, blk.norm1) if li % 2 == 0 else (blk.conv2.conv, blk.norm2)
+            f = lambda: check(lib.lg_tcn_conv_fwd(ptr(xin), ptr(blk_in), ptr(dp.tables[li]), ptr(packed[li]),
+                                                  ptr(conv.bias), ptr(norm.weight), ptr(norm.bias), 1e-5, ptr(out), B,
+                                                  rows_prev, plan.convs[li - 2].rows if li % 2 == 1 else 0, cp.rows,
+                                                  128, st), "tcn conv")
+            t = timeit(f, args.iters)
+            res[f"tcn_conv_l{li}"] = {"us": t, "TFLOPs": B * cp.rows * 2 * 128 * 384 / t / 1e6}
+            mutils.RESIDUAL_FAST_PATH = False
+            f = lambda: mutils.build_residual_sequence_from_segment(m, seg, tseg, 36, 36)
+            t = timeit(f, max(3, args.iters // 10))
+            res["tcn_residual_stock"] = {"us": t, "segments_per_s": B / t * 1e6}
+            mutils.RESIDUAL_FAST_PATH = True
     for k, v in res.items():
         print(k, json.dumps({a: round(b, 2) for a, b in v.items()}))
 
