@@ -151,6 +151,100 @@ def time_propagate(graph, B: int, N: int, D: int, dev, iters: int = 50) -> float
     return a.elapsed_time(b) / iters
 
 
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense fp32
+
+
+def e2e_training(model, opt, allreduce, label, B: int, steps: int, dev) -> dict:
+    """Detector training steps INCLUDING the frozen-predictor residual build from raw
+    (B, 72, 29) segments (train_detector.py:296-317 loop order; SURVEY §8 d: reported
+    separately from graphs/s).  Residual build = the HIP shared-window TCN path; the
+    stock per-window module path (what the reference runs) is timed beside it."""
+    from models import tcn_plan
+    from models import utils as mutils
+    from models.predictor import NormalPredictorTCN
+    torch.manual_seed(7)
+    predictor = NormalPredictorTCN(len(SENSORS), 9).to(dev).eval()
+    gen = torch.Generator().manual_seed(4321)
+    seg = torch.randn(B, 72, len(SENSORS), generator=gen).to(dev)
+    tseg = time_features(B, 72, gen).to(dev)
+    loss_fn = torch.nn.CrossEntropyLoss()
+
+    def step():
+        with torch.no_grad():
+            residual = mutils.build_residual_sequence_from_segment(predictor, seg, tseg, 36, 36, device=dev)
+        logits = model(residual, tseg[:, 36:, :])
+        loss = loss_fn(logits, label)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        allreduce()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    e2e_s = (time.perf_counter() - t0) / steps
+    with torch.no_grad():
+        fast_ms = _event_ms(lambda: tcn_plan.tcn_residual(predictor, seg, tseg, 36, 36), 20)
+        mutils.RESIDUAL_FAST_PATH = False
+        try:
+            stock_ms = _event_ms(lambda: mutils.build_residual_sequence_from_segment(predictor, seg, tseg, 36, 36), 3)
+        finally:
+            mutils.RESIDUAL_FAST_PATH = True
+    plan = tcn_plan.plan_for(36, 36)
+    conv_flop = sum(cp.rows for cp in plan.convs) * B * 2 * 128 * 384
+    conv_ms = _conv_ms(predictor, plan, B, dev)
+    conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
+    return {"value": round(B / e2e_s, 2), "unit": "windows/s", "ms_per_step": round(e2e_s * 1e3, 4),
+            "step": "residual build (frozen TCN, 36 windows of 36 steps per segment) + detector fwd+CE+bwd+AdamW",
+            "residual_ms": round(fast_ms, 4), "residual_ms_stock_module": round(stock_ms, 4),
+            "residual_speedup": round(stock_ms / fast_ms, 2),
+            "tcn_conv": {"kernel": "lg_tcn_conv_fwd x8 (shared-window rows)", "bound": "mfma",
+                         "achieved": round(conv_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(conv_tf / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_call": conv_flop,
+                         "ms_per_call": round(conv_ms, 4)}}
+
+
+def _event_ms(fn, iters: int) -> float:
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def _conv_ms(predictor, plan, B: int, dev) -> float:
+    """Summed HIP-event time of the 8 conv launches of one residual build."""
+    from models import _native as nat
+    from models import tcn_plan
+    lib = nat.load_library()
+    dp = tcn_plan._DevicePlan(plan, dev)
+    packed = tcn_plan._packed_weights(predictor, dev)
+    bufs = [(torch.randn(B * plan.seg_len, 128, device=dev), plan.seg_len)]
+    for cp in plan.convs:
+        bufs.append((torch.empty(B * cp.rows, 128, device=dev), cp.rows))
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        for li, cp in enumerate(plan.convs):
+            blk = predictor.tcn[li // 2]
+            conv, norm = (blk.conv1.conv, blk.norm1) if li % 2 == 0 else (blk.conv2.conv, blk.norm2)
+            prev, rp = bufs[li]
+            bi, rb = bufs[li - 1] if li % 2 == 1 else (None, 0)
+            nat.check(lib.lg_tcn_conv_fwd(nat.ptr(prev), nat.ptr(bi), nat.ptr(dp.tables[li]), nat.ptr(packed[li]),
+                                          nat.ptr(conv.bias), nat.ptr(norm.weight), nat.ptr(norm.bias), 1e-5,
+                                          nat.ptr(bufs[li + 1][0]), B, rp, rb, cp.rows, 128, st), "lg_tcn_conv_fwd")
+    return _event_ms(run, 20)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,6 +359,8 @@ def main() -> None:
         "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
         "final_loss": round(final_loss, 4),
     }
+    if world == 1:
+        out["e2e_training"] = e2e_training(model, opt, allreduce, label, B, max(5, args.steps // 2), dev)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(B, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
     print(json.dumps(out), flush=True)

@@ -15,6 +15,8 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
+ABI_VERSION = 4  # lg_abi_version() of the libleakgnn.so these signatures describe
+
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
 LG_F_DROPOUT = 0x04
@@ -74,6 +76,10 @@ def load_library() -> ctypes.CDLL:
                 f"libleakgnn.so not found at {LIB_PATH}; build it with `make -C {_PKG_ROOT}` "
                 "(or __graft_entry__.build()). The GNN hot path has no CPU fallback.")
         lib = ctypes.CDLL(str(LIB_PATH))
+        lib.lg_abi_version.restype = ctypes.c_int
+        if lib.lg_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH} has ABI {lib.lg_abi_version()}, the bindings expect {ABI_VERSION}; "
+                              f"rebuild with `make -C {_PKG_ROOT}`")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

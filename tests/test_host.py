@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == 4
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 4
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
     assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * (1532 + 661))
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1
@@ -138,3 +138,9 @@ def test_library_built_for_gfx950_only():
     blob = (PKG / "lib" / "libleakgnn.so").read_bytes()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
     assert targets == {b"gfx950"}, targets
+
+
+def test_graft_entry_build():
+    """The driver's build check: make (no-op when up to date) + import + ABI match."""
+    import __graft_entry__ as ge
+    ge.build()
