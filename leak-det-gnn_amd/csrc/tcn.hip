@@ -12,22 +12,30 @@
 // computed in exact fp32 on v_mfma_f32_16x16x4_f32 (LayerNorm needs whole rows, so a
 // workgroup owns all 128 output channels of its rows).
 //
-// Weight-stationary, one 16-row tile at a time:
+// Weight-stationary, one 16-row tile at a time, persistent grid:
 //   * wave w of 4 owns output channels [32w, 32w + 32): its 32 x 384 weight slice
-//     sits in 192 VGPRs for the whole (persistent) kernel, pre-packed by
-//     lg_tcn_pack_weight into fragment order so it loads as 48 coalesced float4;
-//   * the tile's gathered rows arrive in LDS by LDS-DMA (global_load_lds_dwordx4,
-//     no VGPR staging): K chunk q (16 k) of the 16 rows is one 1 KiB piece whose
-//     lane l holds row l % 16, k = 16q + 4(l / 16) .. +3 — exactly the A fragment
-//     of four k-steps, so the MFMA loop reads it back with one linear,
-//     conflict-free ds_read_b128 per lane and chunk; the k order inside a chunk is
-//     the same permuted order the packed weights use;
-//   * double-buffered: the pieces of tile i+1 are in flight during tile i's 192
-//     MFMAs per wave; a zero tap reads a static zero row;
-//   * epilogue: bias, two-pass LayerNorm over the 128 channels (16-lane shuffles
-//     inside a wave, a 4-wave exchange through LDS), ReLU, + residual row, store.
-// Tiles are dealt to a persistent grid, XCD-aware (contiguous tile ranges per XCD
-// group, so the rows a segment's tiles share stay in one L2).
+//     sits in 192 VGPRs for the whole kernel, pre-packed by lg_tcn_pack_weight into
+//     fragment order so it loads as 48 coalesced float4;
+//   * the tile's gathered rows arrive in LDS by LDS-DMA (buffer_load ... lds, no VGPR
+//     staging): K chunk q (16 k) of the 16 rows is one 1 KiB piece whose lane l holds
+//     row l % 16, k = 16q + 4(l / 16) .. +3 — exactly the A fragment of four k-steps,
+//     so the MFMA loop reads it back with one linear, conflict-free ds_read_b128 per
+//     lane and chunk (the packed weights use the same permuted k order); the tile's
+//     16 residual rows ride along as 8 more pieces; zero taps / missing rows are
+//     out-of-range buffer offsets, which read zeros;
+//   * two LDS tile buffers: tile j+1's pieces are issued during tile j's MFMAs;
+//   * epilogue: bias (initial accumulator), two-pass LayerNorm over the 128 channels
+//     (DPP inside a wave, Chan's merge of the 4 waves' partials through LDS),
+//     ReLU, + residual, store; tile j's normalisation and stores run inside tile
+//     j+1's K loop, between its MFMAs.
+// All K-loop LDS reads are inline asm with explicit lgkmcnt waits: a compiler-visible
+// ds_read after an LDS-DMA gets a conservative vmcnt(0), which would serialise the
+// next tile's gather with this tile's MFMAs.
+// Tiles are dealt XCD-aware (contiguous tile ranges per XCD group, so the rows a
+// segment's tiles share stay in one L2).
+// Measured (MI355X, B = 256 segments, widest layer): 70-72 us = 88-91 TFLOP/s, 0.56-0.58
+// of the fp32 MFMA peak; the K loop runs at the MFMA rate, the remainder is the
+// epilogue / side work a single wave per SIMD cannot fully overlap (tools/tcn_prof.cpp).
 #include <algorithm>
 #include <utility>
 #include "common.h"
@@ -39,11 +47,12 @@ constexpr int kK = 3 * kC;          // contraction: 3 taps x C
 constexpr int kQ = kK / 16;         // 16-k chunks
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kPieces = kQ / kWaves;    // LDS-DMA pieces issued per wave and tile
-constexpr int kTileFloats = kQ * 256;   // 16 rows x 384 k
+constexpr int kPieces = kQ / kWaves;    // tap pieces issued per wave and tile
+constexpr int kResPieces = kC / 16 / kWaves;  // residual pieces per wave and tile
+constexpr int kTileFloats = (kQ + kC / 16) * 256;  // 16 rows x (384 k of taps + 128 residual channels)
+constexpr uint32_t kOobOff = 0xFFFF0000u;  // beyond every descriptor (launches stay below 2 GiB per tensor)
 constexpr int kPlanMaxRows = 2048;      // LDS-resident plan table (32 KiB)
 
-__device__ __attribute__((aligned(16))) const float kZeroRow[kC] = {};
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -79,7 +88,7 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
 // Sum over the 16 lanes of a DPP row (= one MFMA output column group), result in every
 // lane: xor 1, xor 2 (quad_perm), then half-row and row mirrors — VALU only, no LDS.
@@ -118,61 +127,33 @@ struct ConvArgs {
     uint32_t rows_in, rows_blk, rows_out;
     lg_fastdiv seg_of;    // row -> segment (divisor rows_out)
     uint32_t ntiles;
-    uint32_t blk_bytes;   // nseg * rows_blk * C * 4 (< 4 GiB per launch)
+    uint32_t in_bytes;    // nseg * rows_in * C * 4 (< 2 GiB per launch)
+    uint32_t blk_bytes;   // nseg * rows_blk * C * 4, 0 without a residual
 };
 
-// Source rows of this lane's row (l % 16) of tile `tile` for the three taps; the static
-// zero row for zero padding, for a missing row past the end and for tile >= ntiles.
-struct TapSrc {
-    const float *s0, *s1, *s2;
-};
-__device__ __forceinline__ TapSrc tap_sources(const ConvArgs& a, const int4* plan_s, uint32_t tile, int lane) {
-    const uint32_t row = tile * 16 + (lane & 15);
-    const bool ok = tile < a.ntiles && row < a.total_rows;
-    const uint32_t rc = ok ? row : 0u;
-    const uint32_t seg = lg_div(rc, a.seg_of);
-    const int4 p = plan_s[rc - seg * a.rows_out];
-    const float* base = a.in + static_cast<uint64_t>(seg) * a.rows_in * kC;
-    TapSrc t;
-    t.s0 = ok && p.x >= 0 ? base + static_cast<uint64_t>(p.x) * kC : kZeroRow;
-    t.s1 = ok && p.y >= 0 ? base + static_cast<uint64_t>(p.y) * kC : kZeroRow;
-    t.s2 = ok && p.z >= 0 ? base + static_cast<uint64_t>(p.z) * kC : kZeroRow;
-    return t;
-}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
-// This wave's LDS-DMA pieces of one tile into `buf` (piece q: tap q / 8,
-// channels 16 (q % 8) + 4 (l / 16) .. +3 of row l % 16, landing at lane l of the piece).
-__device__ __forceinline__ void issue_pieces(const TapSrc& t, float* buf, int w, int lane) {
-    const int g = lane >> 4;
-#pragma unroll
-    for (int u = 0; u < kPieces; ++u) {
-        const int q = w * kPieces + u;
-        const int tap = q >> 3;  // wave-uniform; mask selects keep the pointers out of scratch
-        const uint64_t m0 = 0 - static_cast<uint64_t>(tap == 0), m1 = 0 - static_cast<uint64_t>(tap == 1),
-                       m2 = 0 - static_cast<uint64_t>(tap == 2);
-        const uint64_t sp = (reinterpret_cast<uint64_t>(t.s0) & m0) | (reinterpret_cast<uint64_t>(t.s1) & m1) |
-                            (reinterpret_cast<uint64_t>(t.s2) & m2);
-        const float* s = reinterpret_cast<const float*>(sp) + 16 * (q & 7) + 4 * g;
-        __builtin_amdgcn_global_load_lds(s, (lds_ptr_t)(buf + q * 256), 16, 0, 0);
-    }
+// Side-work LDS reads inside the K loop, also in asm (see ds_read16): issued in chunk q,
+// retired by the lgkmcnt(1) wait at the end of chunk q + 1 (LDS returns in order and a
+// newer ring read is outstanding by then), tied there and consumed from chunk q + 2.
+__device__ __forceinline__ f32x4 ds_read16v(uint32_t addr) {
+    f32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
 }
-
-// Residual (block-input) values of this lane's 4 output rows of `tile`, channels
-// 32w + c16 and 32w + 16 + c16, through a buffer descriptor: absent rows get an
-// out-of-range offset and read 0.  Branch-free.
-__device__ __forceinline__ void load_resid(const ConvArgs& a, __amdgpu_buffer_rsrc_t brs, const int4* plan_s,
-                                           uint32_t tile, int w, int g, int c16, float (&res)[4][2]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t orow = tile * 16 + 4 * g + i;
-        const uint32_t rc = min(orow, a.total_rows - 1);
-        const uint32_t seg = lg_div(rc, a.seg_of);
-        const int rr = plan_s[rc - seg * a.rows_out].w;
-        const bool ok = a.blk != nullptr && orow < a.total_rows && rr >= 0;
-        const uint32_t off = ok ? ((seg * a.rows_blk + static_cast<uint32_t>(rr)) * kC + 32 * w + c16) * 4u : 0xFFFFFF00u;
-        res[i][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, off, 0, 0));
-        res[i][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, off + 64u, 0, 0));
-    }
+__device__ __forceinline__ i32x4 ds_read16i(uint32_t addr) {
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+__device__ __forceinline__ int ds_read4i(uint32_t addr) {
+    int v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ void tie(T& v) {
+    asm volatile("" : "+v"(v));
 }
 
 // Output rows through a buffer descriptor: a row past the end gets an out-of-range
@@ -192,9 +173,19 @@ struct Pending {
     bool live;
 };
 
+#ifdef TCN_PROF
+__device__ unsigned long long g_tcn_prof[4096][8];  // per workgroup: K-loop, between, prologue, tiles, partials, barrier
+#endif
+
 __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
+#ifdef TCN_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long t_k = 0, t_b = 0, t_mark = 0, n_t = 0, t_p = 0, t_w = 0;
+#endif
+    // tiles[b]: pieces 0..23 = the gathered tap rows (A fragments), pieces 24..31 = the
+    // tile's 16 residual rows (block input) in the same fragment layout
     __shared__ __attribute__((aligned(16))) float tiles[2][kTileFloats];
-    __shared__ float red[2][2][kWaves][16];  // [tile parity][mean, M2][wave][row]
+    __shared__ __attribute__((aligned(16))) float red[2][16][2][kWaves];  // [tile parity][row][mean, M2][wave]
     extern __shared__ int4 plan_s[];
 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c16 = lane & 15;
@@ -215,21 +206,73 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
     }
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         a.out, static_cast<short>(0), static_cast<int>(a.total_rows * (4u * kC)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.in), static_cast<short>(0), static_cast<int>(a.in_bytes), 0x00020000);
     const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(a.blk), static_cast<short>(0), static_cast<int>(a.blk_bytes), 0x00020000);
+    const uint32_t plan_lds = lds_addr(reinterpret_cast<const float*>(plan_s));
+    const uint32_t red_lds = lds_addr(&red[0][0][0][0]);
     __syncthreads();  // plan table staged
 
-    // Schedule (one barrier per tile): tiles i and i+1 are resident or in flight while
-    // tile i computes; each wave retires its DMA pieces (vmcnt) just before tile i's
-    // barrier, so after it tile i+1 has landed for everyone and tiles[buf] (tile i) is
-    // free for tile i+2's pieces.  Between two K loops only the LayerNorm partial sums
-    // and the barrier run; tile i's normalisation and stores, tile i's residual loads
-    // and tile i+2's DMA addresses are interleaved with tile i+1's / i's MFMAs.  The
-    // loop never waits on its own output stores (vmcnt counts stores on gfx9).
+    // ---- LDS-DMA of one tile: this wave's 6 tap pieces (q = 6w + u: tap q / 8,
+    // channels 16 (q % 8) + 4 (l / 16) .. +3 of row l % 16) and 2 residual pieces
+    // (channels 16 (2w + v) + 4 (l / 16) .. +3).  Byte offsets into `in` / `blk`; a zero
+    // tap, a missing residual or a row past the end reads out of range, i.e. zeros.
+    uint32_t doff[kPieces + kResPieces];
+    auto dma_offsets = [&](bool ok, uint32_t seg, i32x4 p) {
+        const uint32_t row_in = seg * a.rows_in, row_blk = seg * a.rows_blk;
+        const uint32_t o0 = ok && p.x >= 0 ? (row_in + p.x) * (4u * kC) : kOobOff;
+        const uint32_t o1 = ok && p.y >= 0 ? (row_in + p.y) * (4u * kC) : kOobOff;
+        const uint32_t o2 = ok && p.z >= 0 ? (row_in + p.z) * (4u * kC) : kOobOff;
+        const uint32_t orr = ok && p.w >= 0 ? (row_blk + p.w) * (4u * kC) : kOobOff;
+#pragma unroll
+        for (int u = 0; u < kPieces; ++u) {
+            const int q = w * kPieces + u;
+            const int tap = q >> 3;  // wave-uniform; mask selects keep this out of scratch
+            const uint32_t ot = (o0 & (0u - (tap == 0))) | (o1 & (0u - (tap == 1))) | (o2 & (0u - (tap == 2)));
+            doff[u] = ot + (16 * (q & 7) + 4 * g) * 4;
+        }
+#pragma unroll
+        for (int v = 0; v < kResPieces; ++v) doff[kPieces + v] = orr + (16 * (kResPieces * w + v) + 4 * g) * 4;
+    };
+    auto issue_piece = [&](float* buf, int u) {  // u < kPieces: tap piece, else residual piece
+        if (u < kPieces)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(irs, (lds_ptr_t)(buf + (w * kPieces + u) * 256), 16, doff[u], 0,
+                                                     0, 0);
+        else
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                brs, (lds_ptr_t)(buf + (kQ + kResPieces * w + (u - kPieces)) * 256), 16, doff[u], 0, 0, 0);
+    };
+    // plan row of this lane's DMA row (l % 16) in tile `tile`; ok = a real row
+    auto dma_row = [&](uint32_t tile, bool& ok, uint32_t& seg) -> uint32_t {
+        const uint32_t row = tile * 16 + (lane & 15);
+        ok = tile < a.ntiles && row < a.total_rows;
+        const uint32_t rc = ok ? row : 0u;
+        seg = lg_div(rc, a.seg_of);
+        return rc - seg * a.rows_out;
+    };
+
+    // Schedule (one barrier per tile, two LDS tile buffers): tile j's K loop reads
+    // tiles[j % 2] while the pieces of tile j+1 are issued into tiles[(j+1) % 2], one
+    // per chunk over the first chunks of the loop (that buffer held tile j-1, which
+    // every wave finished before barrier j-1).  Each wave retires its pieces (vmcnt)
+    // before barrier j, so tile j+1 has landed for everyone after it.  Between two K
+    // loops only the LayerNorm partial sums and the barrier run; tile j-1's
+    // normalisation and stores, the read of tile j's residual rows and tile j+2's DMA
+    // offsets are side work inside tile j's K loop.  The loop never waits on its own
+    // output stores (vmcnt counts stores on gfx9): they retire during later MFMAs.
     const TileRange tr = xcd_tiles(a.ntiles);
-    if (tr.first < tr.end) issue_pieces(tap_sources(a, plan_s, tr.first, lane), tiles[0], w, lane);
-    if (tr.first + tr.stride < tr.end)
-        issue_pieces(tap_sources(a, plan_s, tr.first + tr.stride, lane), tiles[1], w, lane);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t t = tr.first + k * tr.stride;
+        bool ok;
+        uint32_t seg;
+        const uint32_t pr = dma_row(t, ok, seg);
+        dma_offsets(ok && t < tr.end, seg, *reinterpret_cast<const i32x4*>(&plan_s[pr]));
+        if (k == 0 && t < tr.end)
+#pragma unroll
+            for (int u = 0; u < kPieces + kResPieces; ++u) issue_piece(tiles[0], u);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
@@ -240,41 +283,62 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) pd.v0[i] = pd.v1[i] = pd.res[i][0] = pd.res[i][1] = 0.f;
 
-    // Epilogue of the pending tile, in two parts: LayerNorm statistics from the four
-    // waves' partials, then normalise / ReLU / + residual / store one row.
-    float mean[4], rstd[4];
-    auto ln_stats = [&]() {
+    float lsc[4][2], lsh[4][2];  // folded LayerNorm affine of the pending rows: y = v * lsc + lsh
+    f32x4 rsum[4], rm2[4];       // the 4 waves' (mean, M2) partials of the pending tile's rows 4g+i
+    auto read_stats = [&]() {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            const float(*rm)[16] = red[pd.par][0];
-            const float(*rq)[16] = red[pd.par][1];
-            const float a0 = rm[0][r], a1 = rm[1][r], a2 = rm[2][r], a3 = rm[3][r];
-            const float mu = 0.25f * ((a0 + a1) + (a2 + a3));
-            const float e0 = a0 - mu, e1 = a1 - mu, e2 = a2 - mu, e3 = a3 - mu;
-            const float M2 = ((rq[0][r] + rq[1][r]) + (rq[2][r] + rq[3][r])) +
-                             32.0f * ((e0 * e0 + e1 * e1) + (e2 * e2 + e3 * e3));
-            mean[i] = mu;
-            rstd[i] = rsqrtf(M2 * (1.0f / kC) + a.eps);
+            const uint32_t ad = red_lds + ((pd.par * 16 + 4 * g + i) * 2 * kWaves) * 4;
+            rsum[i] = ds_read16v(ad);
+            rm2[i] = ds_read16v(ad + 16);
+        }
+    };
+    auto tie_stats = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            tie(rsum[i]);
+            tie(rm2[i]);
+        }
+    };
+    auto ln_stats = [&](int i) {  // Chan's parallel merge of the four waves' (mean, M2)
+        const f32x4 m = rsum[i], q2 = rm2[i];
+        const float mu = 0.25f * ((m[0] + m[1]) + (m[2] + m[3]));
+        const float e0 = m[0] - mu, e1 = m[1] - mu, e2 = m[2] - mu, e3 = m[3] - mu;
+        const float M2 = ((q2[0] + q2[1]) + (q2[2] + q2[3])) + 32.0f * ((e0 * e0 + e1 * e1) + (e2 * e2 + e3 * e3));
+        const float rs = rsqrtf(M2 * (1.0f / kC) + a.eps);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            lsc[i][c] = rs * gam[c];
+            lsh[i][c] = bet[c] - mu * lsc[i][c];
         }
     };
     auto finish_row = [&](int i) {
         const uint32_t orow = pd.tile * 16 + 4 * g + i;
         const bool ok = pd.live && orow < a.total_rows;
-        const float y0 = fmaxf((pd.v0[i] - mean[i]) * rstd[i] * gam[0] + bet[0], 0.f) + pd.res[i][0];
-        const float y1 = fmaxf((pd.v1[i] - mean[i]) * rstd[i] * gam[1] + bet[1], 0.f) + pd.res[i][1];
+        const float y0 = fmaxf(fmaf(pd.v0[i], lsc[i][0], lsh[i][0]), 0.f) + pd.res[i][0];
+        const float y1 = fmaxf(fmaf(pd.v1[i], lsc[i][1], lsh[i][1]), 0.f) + pd.res[i][1];
         store_out(ors, orow, ok, 32 * w + c16, y0);
         store_out(ors, orow, ok, 32 * w + 16 + c16, y1);
     };
 
     int buf = 0;
+#ifdef TCN_PROF
+    const unsigned long long t_pro = __builtin_amdgcn_s_memtime() - t_start;
+    t_mark = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t tile = tr.first; tile < tr.end; tile += tr.stride, buf ^= 1) {
         float res[4][2];
-        TapSrc src2;
+        i32x4 dplan;
+        bool dok = false;
+        uint32_t dseg = 0;
         // K loop: chunk q's A fragment (1 KiB piece q of the tile) is read two chunks
         // ahead into a 3-register ring; the wait after step q's MFMAs retires chunk q + 1
-        // only.  Hooks between chunks carry the interleaved side work.
+        // (and every older LDS read).  Side work is hooked between chunks.
         const uint32_t abase = lds_addr(tiles[buf]) + lane * 16;
+        // residual of this lane's (row 4g+i, channel 32w + 16c + c16) in the fragment
+        // layout of pieces 24..31
+        const uint32_t rbase = lds_addr(tiles[buf]) + (kQ + 2 * w) * 1024 + (16 * (c16 >> 2) + 4 * g) * 16 +
+                               (c16 & 3) * 4;
         f32x4 acc0 = {bias[0], bias[0], bias[0], bias[0]};
         f32x4 acc1 = {bias[1], bias[1], bias[1], bias[1]};
         f32x4 ring[3];
@@ -291,17 +355,54 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
                     acc0 = mfma(av[j], wr[q][0][j], acc0);
                     acc1 = mfma(av[j], wr[q][1][j], acc1);
                 }
-                if constexpr (q == 0) ln_stats();
-                if constexpr (q >= 1 && q <= 4) finish_row(q - 1);
-                if constexpr (q == 6) load_resid(a, brs, plan_s, tile, w, g, c16, res);
-                if constexpr (q == 9) src2 = tap_sources(a, plan_s, tile + 2 * tr.stride, lane);
+                // ---- side work ----
+#ifndef TCN_NOHOOK
+                if constexpr (q < kPieces + kResPieces) issue_piece(tiles[buf ^ 1], q);  // tile j+1
+                if constexpr (q == 0) read_stats();
+                if constexpr (q >= 2 && q <= 5) ln_stats(q - 2);
+                if constexpr (q >= 3 && q <= 6) finish_row(q - 3);
+                if constexpr (q == 8) {
+                    const uint32_t pr = dma_row(tile + 2 * tr.stride, dok, dseg);
+                    dok = dok && tile + 2 * tr.stride < tr.end;  // else all pieces read zeros (unused)
+                    dplan = ds_read16i(plan_lds + pr * 16);
+                }
+                if constexpr (q == 10) dma_offsets(dok, dseg, dplan);
+                if constexpr (q == 14) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        res[i][0] = __builtin_bit_cast(float, ds_read4i(rbase + i * 16));
+                        res[i][1] = __builtin_bit_cast(float, ds_read4i(rbase + 1024 + i * 16));
+                    }
+                }
+#endif
+                // ---- waits ----
                 if constexpr (q + 2 < kQ)
                     lgkm_wait_but1(ring[(q + 1) % 3]);  // chunk q + 2 may stay in flight
                 else if constexpr (q + 1 < kQ)
                     lgkm_wait_all(ring[(q + 1) % 3]);
+#ifndef TCN_NOHOOK
+                if constexpr (q == 1) tie_stats();
+                if constexpr (q == 9) tie(dplan);
+                if constexpr (q == 10)
+#pragma unroll
+                    for (int u = 0; u < kPieces + kResPieces; ++u) tie(doff[u]);  // computed here, not sunk
+                if constexpr (q == 15)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        tie(res[i][0]);
+                        tie(res[i][1]);
+                    }
+#endif
             },
             std::make_integer_sequence<int, kQ>{});
-
+#ifdef TCN_PROF
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            t_k += t - t_mark;
+            t_mark = t;
+            ++n_t;
+        }
+#endif
         // LayerNorm partials of this tile: each wave reduces its 32 channels exactly
         // (two-pass mean / M2 inside the wave, DPP only); the four waves' (mean, M2)
         // are merged by ln_stats with Chan's parallel formula.
@@ -316,8 +417,8 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
         if (c16 == 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                red[buf][0][w][4 * g + i] = mw[i];
-                red[buf][1][w][4 * g + i] = m2[i];
+                red[buf][4 * g + i][0][w] = mw[i];
+                red[buf][4 * g + i][1][w] = m2[i];
             }
         }
 #pragma unroll
@@ -330,18 +431,45 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
         pd.tile = tile;
         pd.par = buf;
         pd.live = true;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile i+1, residual loads
-#pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(pd.res[i][0]), "+v"(pd.res[i][1]));
+#ifdef TCN_PROF
+        const unsigned long long t_p0 = __builtin_amdgcn_s_memtime();
+#endif
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile j+1
         __syncthreads();
-        if (tile + 2 * tr.stride < tr.end) issue_pieces(src2, tiles[buf], w, lane);
+#ifdef TCN_PROF
+        const unsigned long long t_p1 = __builtin_amdgcn_s_memtime();
+        t_p += t_p0 - t_mark;
+        t_w += t_p1 - t_p0;
+#endif
+#ifdef TCN_PROF
+        {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            t_b += t - t_mark;
+            t_mark = t;
+        }
+#endif
     }
     if (pd.live) {
-        ln_stats();
+        read_stats();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tie_stats();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) finish_row(i);
+        for (int i = 0; i < 4; ++i) {
+            ln_stats(i);
+            finish_row(i);
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
+#ifdef TCN_PROF
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {
+        g_tcn_prof[blockIdx.x][0] = t_k;
+        g_tcn_prof[blockIdx.x][1] = t_b;
+        g_tcn_prof[blockIdx.x][2] = t_pro;
+        g_tcn_prof[blockIdx.x][3] = n_t;
+        g_tcn_prof[blockIdx.x][4] = t_p;
+        g_tcn_prof[blockIdx.x][5] = t_w;
+    }
+#endif
 }
 
 // Packed weight: wpk[w][q][c][lane][j] = W[co][ci][2 - tap] with co = 32w + 16c + lane % 16,
@@ -383,8 +511,11 @@ int lg_tcn_conv_fwd(const float* in, const float* blk, const int32_t* plan, cons
     if (nseg * rows_in >= kLgMaxRows || nseg * std::max<int64_t>(rows_blk, 0) >= kLgMaxRows) return LG_EUNSUPPORTED;
     // output rows are stored through a buffer descriptor (32-bit byte offsets): split
     // the segments so that each launch's output stays below 4 GiB
-    const int64_t seg_cap = std::max<int64_t>(
-        1, int64_t{0xFFFFF000} / (std::max<int64_t>(rows_out, std::max<int64_t>(rows_blk, 0)) * kC * 4));
+    // rows are addressed through buffer descriptors (32-bit byte offsets, out-of-range
+    // offsets read zero / drop the store): split the segments so that each launch's
+    // tensors stay below 2 GiB
+    const int64_t widest = std::max(std::max(rows_out, rows_in), std::max<int64_t>(rows_blk, 0));
+    const int64_t seg_cap = std::max<int64_t>(1, (int64_t{1} << 31) / (widest * kC * 4));
     const size_t dyn = static_cast<size_t>(rows_out) * sizeof(int4);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tcn_conv, kThreads, dyn) != hipSuccess || per_cu < 1)
@@ -408,6 +539,7 @@ int lg_tcn_conv_fwd(const float* in, const float* blk, const int32_t* plan, cons
         a.rows_out = static_cast<uint32_t>(rows_out);
         a.seg_of = lg_make_fastdiv(static_cast<uint32_t>(rows_out));
         a.ntiles = static_cast<uint32_t>((total + 15) / 16);
+        a.in_bytes = static_cast<uint32_t>(ns * rows_in * kC * 4);
         a.blk_bytes = blk != nullptr ? static_cast<uint32_t>(ns * rows_blk * kC * 4) : 0u;
         const int64_t grid = std::min<int64_t>(a.ntiles, int64_t{per_cu} * lg_num_cus());
         k_tcn_conv<<<static_cast<unsigned>(grid), kThreads, dyn, lg_stream(stream)>>>(a);
