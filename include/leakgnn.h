@@ -53,6 +53,12 @@ enum {
 #define LG_F_DROPOUT   0x04  /* fwd: inverted dropout after ReLU (nn.Dropout, detector.py:201) */
 #define LG_F_MASK_IN   0x08  /* bwd: dz = dy * scale_in * [y > 0]  (ReLU/dropout backward of THIS layer's output) */
 #define LG_F_MASK_OUT  0x10  /* bwd: dx_out = dx * scale_out * [x > 0] (ReLU/dropout backward of the PREVIOUS op) */
+/* Node-feature layout for lg_node_init_fwd / lg_pipe_scatter_bwd / lg_edge_head_* /
+ * lg_pool_head_fwd: without it node rows are window-major [B][N][D] (row b*N + n, the
+ * reference's disjoint-union order, detector.py:105-114, 192-196); with it they are
+ * node-major [N][B][D] (row n*B + b), the layout of lg_gcn_fwd_nm / lg_gcn_bwd_nm.
+ * Dropout masks are indexed by the window-major row in both layouts. */
+#define LG_F_NODE_MAJOR 0x20
 
 int lg_abi_version(void);
 const char* lg_strerror(int code);
@@ -142,6 +148,26 @@ int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
                int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 
+/* Node-major fused GCN layer (LG_F_NODE_MAJOR layout, x, y : fp32 [N][B][D]).
+ * Same math, flags and results as lg_gcn_fwd on the transposed layout: rows n*B + b.
+ * Every window shares the graph, so a 16-row tile is one node and 16 consecutive
+ * windows, and each CSR entry (m, w) names one contiguous 16 x D block of x — the
+ * entry is wave-uniform and the row loads need no per-lane index arithmetic.
+ *   pairs : int32 [2 * nnz] interleaved (col, float_as_int(w)) of the lg_graph_build CSR.
+ *   Dropout: row-stream masks indexed by the window-major row b*N + n (the mask of
+ *   lg_gcn_fwd for the same seed/salt).
+ *   Requires N*B*D*4 <= 0xFFFFFF00 bytes (LG_EUNSUPPORTED otherwise). */
+int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
+                  const float* bias, float* y, int64_t B, int64_t N, int64_t D,
+                  int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+/* Backward of lg_gcn_fwd_nm: lg_gcn_bwd's contract on the node-major layout, over the
+ * transposed CSR given as rowptr_t + pairs_t.  workspace: lg_gcn_bwd_nm_workspace_bytes(D). */
+int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D);
+int lg_gcn_bwd_nm(const int32_t* rowptr_t, const int32_t* pairs_t, const float* dy, const float* y,
+                  const float* x, const float* W, float* dx_out, float* dW, float* db,
+                  const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
+                  int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream);
+
 /* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
  * weights; no transform).  Used for the HBM-roofline stress case (config C5). */
 int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,
@@ -186,7 +212,7 @@ int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* feat,
  * global_mean_pool (detector.py:215).   dpipe : fp32 [B][P][2][D];  dh : fp32 [B][N][D] */
 int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const float* dpipe,
                         const float* dpool, float* dh,
-                        int64_t B, int64_t N, int64_t P, int64_t D, lg_stream_t stream);
+                        int64_t B, int64_t N, int64_t P, int64_t D, int flags, lg_stream_t stream);
 
 /* K8 + K9 fused EdgeHead forward (detector.py:76-88 applied at :206-211):
  *   logits[b][p] = W2 . dropout(relu(W1 [h_u, h_v, |h_u - h_v|] + b1)) + b2

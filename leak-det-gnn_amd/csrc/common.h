@@ -51,6 +51,32 @@ __device__ __forceinline__ float lg_dropout(float v, float p, float scale, uint3
     return lg_keep(key, idx, p) ? v * scale : 0.0f;
 }
 
+// Row-stream variant (fused GCN forward, whose backward reads the mask back as [y > 0]):
+// one seed per (global row, lane group q) from two lowbias32 rounds, then one xorshift32
+// step per PAIR of the lane's channels 16 mt + 4 q + reg, in (mt, reg) order: the low
+// 16 bits decide the even reg, the high 16 bits the odd one (lg_keep_threshold16) —
+// ~3 full-rate VALU per channel instead of a 4-multiply hash.
+// Restated in oracle/dropout_ref.py (row_stream_mask).
+__host__ __device__ __forceinline__ uint32_t lg_row_stream_seed(uint32_t key, uint64_t row, uint32_t q) {
+    const uint32_t a = lg_mix32((static_cast<uint32_t>(row) * 0x9E3779B9U) ^ key);
+    const uint32_t s = lg_mix32(a ^ (static_cast<uint32_t>(row >> 32) * 0x85EBCA6BU) ^ (q * 0x632BE5ABU));
+    return s ? s : 0x6D2B79F5U;
+}
+__host__ __device__ __forceinline__ uint32_t lg_xorshift32(uint32_t s) {
+    s ^= s << 13;
+    s ^= s >> 17;
+    s ^= s << 5;
+    return s;
+}
+__device__ __forceinline__ bool lg_keep_u(uint32_t s, float p) {
+    return static_cast<float>(s >> 8) * (1.0f / 16777216.0f) >= p;
+}
+// 16-bit keep threshold of the fused GCN forward: keep <=> u16 >= rint(p * 2^16)
+// (p quantised to 1/65536), two decisions per xorshift step.
+__host__ __device__ __forceinline__ uint32_t lg_keep_threshold16(float p) {
+    return static_cast<uint32_t>(rintf(p * 65536.0f));
+}
+
 // Division by a runtime divisor that is fixed per launch (N nodes, P pipes, S sensors):
 // magic multiplier computed on the host (Granlund & Montgomery 1994, round-up
 // variant), so a row index splits into (window, node) with one v_mul_hi_u32 and

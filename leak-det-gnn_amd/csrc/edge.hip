@@ -56,7 +56,7 @@ struct EG {
 template <int D>
 __device__ __forceinline__ void gather_tile(const int64_t* __restrict__ ends, const float* __restrict__ h,
                                             float* __restrict__ ft, int64_t row0, int64_t BP, const lg_fastdiv& fdP,
-                                            int64_t N) {
+                                            int64_t sb, int64_t sn) {
     using G = EG<D>;
     const int t = threadIdx.x;
     if (t < TR * 2 * G::F4) {
@@ -66,7 +66,7 @@ __device__ __forceinline__ void gather_tile(const int64_t* __restrict__ ends, co
         if (gr < BP) {
             const uint32_t b = lg_div(static_cast<uint32_t>(gr), fdP), p = static_cast<uint32_t>(gr) - b * fdP.d;
             const int64_t node = ends[2 * p + side];
-            v = ld4(h + (static_cast<int64_t>(b) * N + node) * D + 4 * f4);
+            v = ld4(h + (static_cast<int64_t>(b) * sb + node * sn) * D + 4 * f4);  // row of (window b, node)
         }
         st4(ft + row * G::FS + side * D + 4 * f4, v);
     }
@@ -108,7 +108,7 @@ template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-           float* __restrict__ logit, int64_t ldo, int64_t N, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout,
+           float* __restrict__ logit, int64_t ldo, int64_t sb, int64_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout,
            float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
     __shared__ __attribute__((aligned(16))) float ft[TR * G::FS];
@@ -127,7 +127,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, fdP, N);
+        gather_tile<D>(ends, h, ft, row0, BP, fdP, sb, sn);
         __syncthreads();
         const f32x4 acc = hidden_tile<D>(ft, aw, b1v, j, q);
         float s = 0.f;
@@ -157,7 +157,8 @@ template <int D>
 __global__ void __launch_bounds__(64 * NW)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ dlogit, int64_t ldo,
-           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t N, lg_fastdiv fdP,
+           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t sb, int64_t sn,
+           lg_fastdiv fdP,
            int64_t BP, int64_t ntiles, int dropout, float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     using G = EG<D>;
     constexpr int HS = HID + 4;
@@ -193,7 +194,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, fdP, N);
+        gather_tile<D>(ends, h, ft, row0, BP, fdP, sb, sn);
         const bool rv = row0 + j < BP;
         const float dl = rv ? dlogit[lg_row_index(row0 + j, fdP, ldo)] : 0.f;
         __syncthreads();
@@ -311,15 +312,17 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     if (!ends || !h || !w1 || !b1 || !w2 || !b2 || !logits || ldo < P) return LG_EINVAL;
     if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
+    const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // h is [N][B][D] instead of [B][N][D]
+    const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
     const int64_t ntiles = cdiv(BP, TR);
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ntiles, 4LL * lg_num_cus()));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     if (D == 64)
-        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, N, fdP, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, sb, sn, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     else
-        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, N, fdP, BP, ntiles, dropout, dropout_p,
+        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, sb, sn, fdP, BP, ntiles, dropout, dropout_p,
                                                 scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
@@ -347,6 +350,8 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     if (BP > 0 && (!ends || !dlogits || !dpipe || ldo < P)) return LG_EINVAL;
     if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(std::max<int64_t>(P, 1)));
+    const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // h is [N][B][D] instead of [B][N][D]
+    const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
     const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), TR);
     const int grid = bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
@@ -358,10 +363,10 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else if (D == 64) {
-        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
+        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     } else {
-        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, N, fdP, BP, ntiles, dropout,
+        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP, ntiles, dropout,
                                                 dropout_p, scale, seed, salt);
     }
     LG_RET_IF_LAUNCH_FAILED();

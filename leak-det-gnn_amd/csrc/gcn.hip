@@ -101,24 +101,39 @@ __device__ __forceinline__ TileRange xcd_tiles(int64_t ntiles, int wave, int wav
     return TileRange{begin + k * waves + wave, end, nbx * waves};
 }
 
+// Single-graph CSR.  Global form: rowptr / col / w arrays.  LDS form (PAIRS): rowptr
+// [0, N+1), padded to an even word count, then one (col, w) pair per entry, so a
+// neighbour slot costs one 64-bit LDS read; `col` then points at the pairs.
 struct Csr {
     const int32_t* rp;
     const int32_t* col;
     const float* w;
 };
+template <bool PAIRS>
+__device__ __forceinline__ void csr_at(const Csr& g, int e, int32_t& c, float& w) {
+    if constexpr (PAIRS) {
+        const int2 v = *reinterpret_cast<const int2*>(g.col + 2 * e);
+        c = v.x;
+        w = __int_as_float(v.y);
+    } else {
+        c = g.col[e];
+        w = g.w[e];
+    }
+}
 
-// CSR words in LDS, contiguous: rowptr [0, N+1), col [N+1, N+1+nnz), w after col.
+// CSR words in LDS (pair layout), or 0 when it does not fit.
 inline int64_t csr_lds_bytes(int64_t N, int64_t nnz_cap) {
-    const int64_t b = 4 * (N + 1 + 2 * nnz_cap);
+    const int64_t b = 4 * (((N + 2) & ~int64_t{1}) + 2 * nnz_cap);
     return b <= kCsrLdsMax ? b : 0;
 }
 
-// Stage the CSR into LDS: every thread issues all of its loads (clamped indices, no
-// branches) before its first LDS store, so the prologue costs one memory round trip
-// per 8*blockDim words instead of one per word-loop iteration.  Caller syncs.
+// Stage the CSR into LDS in the pair layout: every thread issues all of its loads
+// (clamped indices, no branches) before its first LDS store, so the prologue costs one
+// memory round trip per 8*blockDim words instead of one per word-loop iteration.
+// Caller syncs.
 __device__ __forceinline__ Csr stage_csr(uint32_t* s, const int32_t* __restrict__ rowptr,
                                          const int32_t* __restrict__ col, const float* __restrict__ w, uint32_t N) {
-    const uint32_t n1 = N + 1, nnz = static_cast<uint32_t>(rowptr[N]), total = n1 + 2 * nnz;
+    const uint32_t n1 = N + 1, n1p = (N + 2) & ~1u, nnz = static_cast<uint32_t>(rowptr[N]), total = n1p + 2 * nnz;
     const uint32_t* rp = reinterpret_cast<const uint32_t*>(rowptr);
     const uint32_t* cp = reinterpret_cast<const uint32_t*>(col);
     const uint32_t* wp = reinterpret_cast<const uint32_t*>(w);
@@ -128,8 +143,16 @@ __device__ __forceinline__ Csr stage_csr(uint32_t* s, const int32_t* __restrict_
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
             const uint32_t i = min(base + u * blockDim.x + threadIdx.x, total - 1);
-            const uint32_t* p = i < n1 ? rp + i : (i < n1 + nnz ? cp + (i - n1) : wp + (i - n1 - nnz));
-            v[u] = *p;
+            const uint32_t j = i - n1p, e = j >> 1;
+            // one mask-selected address and one load (no branches, so all PER loads are in
+            // flight); the pad word between rowptr and the pairs copies rowptr[N] (never read)
+            const uint32_t ec = min(e, nnz > 0 ? nnz - 1 : 0u);
+            const uint64_t mr = 0 - static_cast<uint64_t>(i < n1p);
+            const uint64_t mw = 0 - static_cast<uint64_t>(i >= n1p && (j & 1));
+            const uint64_t mc = ~(mr | mw);
+            const uint64_t ad = (reinterpret_cast<uint64_t>(rp + min(i, n1 - 1)) & mr) |
+                                (reinterpret_cast<uint64_t>(wp + ec) & mw) | (reinterpret_cast<uint64_t>(cp + ec) & mc);
+            v[u] = *reinterpret_cast<const uint32_t*>(ad);
         }
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
@@ -137,9 +160,18 @@ __device__ __forceinline__ Csr stage_csr(uint32_t* s, const int32_t* __restrict_
             if (i < total) s[i] = v[u];
         }
     }
-    return Csr{reinterpret_cast<const int32_t*>(s), reinterpret_cast<const int32_t*>(s + n1),
-               reinterpret_cast<const float*>(s + n1 + nnz)};
+    return Csr{reinterpret_cast<const int32_t*>(s), reinterpret_cast<const int32_t*>(s + n1p), nullptr};
 }
+
+#ifdef GCN_PROF
+// lab build only (tools/gcn_prof.cpp): per wave s_memtime cycles
+// [0 -, 1 csr+issue, 2 hook, 3 wait+fma, 4 tail MFMA, 5 epilogue+stores, 6 tiles, 7 rounds]
+__device__ unsigned long long g_gcn_prof[65536][8];
+__device__ unsigned long long* gcn_prof_slot() {
+    return g_gcn_prof[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)];
+}
+#define GCN_T() __builtin_amdgcn_s_memtime()
+#endif
 
 struct NoHook {
     __device__ __forceinline__ void operator()(int, int) const {}
@@ -151,7 +183,7 @@ struct NoHook {
 // count is the tile's wave-uniform max degree so hook(round, rounds) — independent
 // work such as the previous tile's MFMAs — runs with every lane active, between the
 // issue of a round's loads and their use.
-template <int D, bool MASK, int U, typename Hook = NoHook>
+template <int D, bool MASK, int U, bool PAIRS, typename Hook = NoHook>
 __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const Rows<D>& msk, float mscale,
                                          uint32_t r0, uint32_t R, const lg_fastdiv& fdN, int lane,
                                          f32x4 (&acc)[Geo<D>::K], Hook&& hook = Hook{}) {
@@ -160,26 +192,36 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
     int e0[G::K], e1[G::K];
     uint32_t base[G::K];
     int maxd = 0;
+    // node of the tile's first row by one (wave-uniform) division; the other rows add
+    // their offset (< 16) and wrap once (N >= 16; tiny graphs divide per row)
+    const uint32_t n0 = r0 - lg_div(r0, fdN) * fdN.d;
 #pragma unroll
     for (int k = 0; k < G::K; ++k) {
         acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         const uint32_t r = r0 + G::RPI * k + rl;
         const bool valid = r < R;
         const uint32_t rr = valid ? r : 0u;
-        const uint32_t n = rr - lg_div(rr, fdN) * fdN.d;
+        uint32_t n;
+        if (fdN.d >= 16) {
+            const uint32_t t = n0 + G::RPI * k + rl;
+            n = valid ? (t >= fdN.d ? t - fdN.d : t) : 0u;
+        } else {
+            n = rr - lg_div(rr, fdN) * fdN.d;
+        }
         e0[k] = g.rp[n];
         e1[k] = valid ? g.rp[n + 1] : e0[k];
         base[k] = rr - n;
         maxd = max(maxd, e1[k] - e0[k]);
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o));
-    maxd = __builtin_amdgcn_readfirstlane(maxd);
-    const int rounds = (maxd + U - 1) / U;
-    for (int rd = 0; rd < rounds; ++rd) {
-        int32_t s[G::K][U];
-        float ww[G::K][U];
-        bool ok[G::K][U];
+    // rounds = wave max of ceil(maxd / U): a few ballots (SALU) instead of a shuffle tree
+    int rounds = 0;
+    while (__builtin_amdgcn_ballot_w64(maxd > rounds * U) != 0) ++rounds;
+    // CSR entries of round rd + 1 are read (LDS) while round rd's rows are in flight, so
+    // the LDS latency is off the round's critical path (read -> address -> load issue).
+    int32_t s[G::K][U];
+    float ww[G::K][U];
+    bool ok[G::K][U];
+    auto read_entries = [&](int rd) {
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
 #pragma unroll
@@ -187,9 +229,14 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
                 const int e = e0[k] + rd * U + u;
                 ok[k][u] = e < e1[k];
                 const int ei = ok[k][u] ? e : 0;  // maxd > 0 implies nnz > 0, so entry 0 exists
-                s[k][u] = g.col[ei];
-                ww[k][u] = g.w[ei];
+                csr_at<PAIRS>(g, ei, s[k][u], ww[k][u]);
             }
+    };
+    if (rounds > 0) read_entries(0);
+    for (int rd = 0; rd < rounds; ++rd) {
+#ifdef GCN_PROF
+        const unsigned long long pt0 = GCN_T();
+#endif
         f32x4 v[G::K][U], m[G::K][U];
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
@@ -198,7 +245,19 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
                 v[k][u] = src.ld(base[k] + static_cast<uint32_t>(s[k][u]), fg, ok[k][u]);
                 if constexpr (MASK) m[k][u] = msk.ld(base[k] + static_cast<uint32_t>(s[k][u]), fg, ok[k][u]);
             }
+        float wv[G::K][U];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u) wv[k][u] = ok[k][u] ? ww[k][u] : 0.f;
+        if (rd + 1 < rounds) read_entries(rd + 1);
+#ifdef GCN_PROF
+        const unsigned long long pt1 = GCN_T();
+#endif
         hook(rd, rounds);
+#ifdef GCN_PROF
+        const unsigned long long pt2 = GCN_T();
+#endif
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
 #pragma unroll
@@ -208,10 +267,20 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
 #pragma unroll
                     for (int i = 0; i < 4; ++i) t[i] = m[k][u][i] > 0.f ? t[i] * mscale : 0.f;
                 }
-                const float wv = ok[k][u] ? ww[k][u] : 0.f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(wv, t[i], acc[k][i]);
+                for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(wv[k][u], t[i], acc[k][i]);
             }
+#ifdef GCN_PROF
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[G::K - 1][3]));
+        const unsigned long long pt3 = GCN_T();
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long* ps = gcn_prof_slot();
+            ps[1] += pt1 - pt0;
+            ps[2] += pt2 - pt1;
+            ps[3] += pt3 - pt2;
+            ps[7] += 1;
+        }
+#endif
     }
 }
 
@@ -261,12 +330,14 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
     const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
     const Csr g = CSR_LDS ? stage_csr(reinterpret_cast<uint32_t*>(smem), rowptr, col, wgt, N)
                           : Csr{rowptr, col, wgt};
+    // dropout's 1 / (1 - p) is folded into W and b: relu(s z) = s relu(z) for s > 0
+    const float fold = DROP ? dscale : 1.0f;
 #pragma unroll
     for (int u = 0; u < WPER; ++u) {
         const int i = u * 64 * NW + threadIdx.x;
-        if (i < W4) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), wv[u]);
+        if (i < W4) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), wv[u] * fold);
     }
-    if (threadIdx.x < D) bl[threadIdx.x] = bb;
+    if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
     __syncthreads();
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -276,8 +347,11 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 
     const TileRange tr = xcd_tiles(ntiles, wave, NW);
     f32x4 acc[G::K];
+#ifdef GCN_PROF
+    unsigned long long tm = GCN_T();
+#endif
     if (tr.first < tr.end) {
-        gather16<D, false, 2>(g, xs, xs, 1.f, static_cast<uint32_t>(tr.first * kTileRows), R, fdN, lane, acc);
+        gather16<D, false, 2, CSR_LDS>(g, xs, xs, 1.f, static_cast<uint32_t>(tr.first * kTileRows), R, fdN, lane, acc);
         put_tile<D>(tl, acc, lane);
     }
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
@@ -304,29 +378,59 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
         const int64_t next = tile + tr.stride;
         const bool more = next < tr.end;
         if (more)
-            gather16<D, false, 2>(g, xs, xs, 1.f, static_cast<uint32_t>(next * kTileRows), R, fdN, lane, acc, hook);
+            gather16<D, false, 2, CSR_LDS>(g, xs, xs, 1.f, static_cast<uint32_t>(next * kTileRows), R, fdN, lane, acc,
+                                           hook);
+#ifdef GCN_PROF
+        tm = GCN_T();
+#endif
         while (chunk < G::CH) mfma_chunk();
+#ifdef GCN_PROF
+        {
+            asm volatile("" ::"v"(o[0][0]), "v"(o[G::MT - 1][3]));
+            const unsigned long long t = GCN_T();
+            if (lane == 0) gcn_prof_slot()[4] += t - tm;
+            tm = t;
+        }
+#endif
 
         const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
-        const uint64_t rg = row_offset + r0 + j;  // global row: the dropout stream ignores launch splits
+        // row-stream dropout (common.h): seeded by the global row (launch splits do not
+        // change it) and the lane group q; each xorshift step decides two channels
+        // (16-bit halves against rint(p 2^16)), in (mt, reg) order
+        uint32_t st = 0, thr = 0;
+        if constexpr (DROP) {
+            st = lg_row_stream_seed(key, row_offset + r0 + j, static_cast<uint32_t>(q));
+            thr = lg_keep_threshold16(p_drop);
+        }
+        const uint32_t r = r0 + j;
 #pragma unroll
         for (int mt = 0; mt < G::MT; ++mt) {
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
                 float t = fmaxf(o[mt][reg], relu_floor);
-                if constexpr (DROP) t = lg_dropout(t, p_drop, dscale, key, rg * D + 16 * mt + 4 * q + reg);
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    t = u16 >= thr ? t : 0.0f;
+                }
                 o[mt][reg] = t;
             }
+            // D fragment: row r0 + j, channels 16 mt + 4q .. +3 -> one float4 per block
+            ys.st(r, 4 * mt + q, r < R, o[mt]);
         }
-        wave_lds_sync();
-#pragma unroll
-        for (int mt = 0; mt < G::MT; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
-        wave_lds_sync();
-        store_tile<D>(tl, ys, r0, R, lane);
         if (more) {
             wave_lds_sync();
             put_tile<D>(tl, acc, lane);
         }
+#ifdef GCN_PROF
+        {
+            const unsigned long long t = GCN_T();
+            if (lane == 0) {
+                gcn_prof_slot()[5] += t - tm;
+                gcn_prof_slot()[6] += 1;
+            }
+        }
+#endif
     }
 }
 
@@ -393,7 +497,7 @@ k_gcn_bwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
             xv[k] = xs.ld(r, fg, r < R);
         }
         f32x4 acc[G::K];
-        gather16<D, MASK_IN, 1>(g, dys, ms, scale_in, r0, R, fdN, lane, acc);
+        gather16<D, MASK_IN, 1, CSR_LDS>(g, dys, ms, scale_in, r0, R, fdN, lane, acc);
         put_tile<D>(tl, acc, lane);
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
@@ -519,7 +623,7 @@ k_spmm(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, cons
     for (int64_t tile = tr.first; tile < tr.end; tile += tr.stride) {
         const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
         f32x4 acc[G::K];
-        gather16<D, false, 2>(g, xs, xs, 1.f, r0, R, fdN, lane, acc);
+        gather16<D, false, 2, CSR_LDS>(g, xs, xs, 1.f, r0, R, fdN, lane, acc);
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
             const uint32_t r = r0 + G::RPI * k + rl;

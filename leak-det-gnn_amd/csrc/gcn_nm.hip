@@ -1,0 +1,513 @@
+// Fused GCN layer forward / backward in the NODE-MAJOR layout of the LeakDetector trunk.
+//
+// Layout: node features [N][B][D] (row r = n*B + b): the B windows of one node are
+// contiguous.  Every window carries the same graph, so a 16-row tile is ONE node n and 16
+// consecutive windows b0..b0+15 (a "window group"), and its aggregation
+//     (Ahat x)[n][b0..b0+15][:] = sum_{m in N(n)} w_nm x[m][b0..b0+15][:]
+// reads one contiguous 16 x D block per neighbour (4 KiB at D = 64):
+//   * the CSR entry (m, w_nm) is wave-uniform (scalar loads of (col, w) pairs),
+//   * the degree is uniform (no padded neighbour slots),
+//   * row loads are buffer loads with a scalar base and a per-lane constant offset —
+//     no per-lane index or address arithmetic; a ragged last window group masks rows.
+// Compared with the window-major kernels (gcn.hip) this removes most of the per-row VALU
+// work that bounded them (measured: 35.7 -> 24.4 us per train-mode layer at B = 256, and
+// 0.57 of the HBM peak at B = 1024).
+//
+// Forward: aggregate -> LDS -> MFMA B operand, y^T = W (Ahat x)^T on
+// v_mfma_f32_16x16x4_f32 (exact fp32), bias as the initial accumulator, ReLU, row-stream
+// dropout with the 1/(1-p) scale folded into W and b, rows written back through LDS as
+// one contiguous block with non-temporal stores (y is not re-read by this launch).
+// Backward: t = Ahat^T dz (transposed CSR, dz = dy * s * [y > 0] when MASK_IN), dx = t W
+// (MFMA, masked by the input's [x > 0] * s), dW += t^T x and db += sum dz accumulated per
+// wave and reduced per block in a fixed order (deterministic), then by the slab reducer.
+// Tiles are ordered window-group-major and dealt XCD-aware.
+#include <algorithm>
+#include "common.h"
+#include "reduce.h"
+
+namespace {
+
+constexpr int kNmFwdWaves = 8;
+constexpr int kNmBwdWaves = 8;
+constexpr uint32_t kNmOob = 0xFFFFFFF0u;
+
+__device__ __forceinline__ f32x4 mfma_nm(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void wave_sync_nm() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
+}
+
+template <int D>
+struct NmGeo {
+    static constexpr int LPR = D / 4;     // lanes per row (one float4 each)
+    static constexpr int RPI = 64 / LPR;  // rows per wave instruction
+    static constexpr int K = 16 / RPI;    // instructions per 16-row block
+    static constexpr int CH = D / 16;     // MFMA k chunks = output blocks
+    static constexpr int S = D + 4;       // LDS row stride (floats)
+    static constexpr int TILE = 16 * S;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nm_rsrc(const float* p, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), static_cast<short>(0), static_cast<int>(bytes),
+                                             0x00020000);
+}
+
+// The block base goes into the VGPR offset, not soffset: a masked lane's offset must stay
+// beyond num_records after the whole address sum, so nothing may be added to kNmOob.
+template <int D>
+__device__ __forceinline__ f32x4 nm_ld(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, bool ok, uint32_t base) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? lane_off + base : kNmOob, 0, 0));
+}
+
+template <int AUX>
+__device__ __forceinline__ void nm_st(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, bool ok, uint32_t base, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rs,
+                                           ok ? lane_off + base : kNmOob, 0, AUX);
+}
+
+// Tile -> (node, window group) and the XCD-aware persistent schedule over groups * N tiles.
+struct NmSched {
+    int64_t first, end, stride;
+};
+__device__ __forceinline__ NmSched nm_sched(int64_t ntiles, int wave, int waves) {
+    const int64_t G = gridDim.x, b = blockIdx.x;
+    if (G < 8) return NmSched{b * waves + wave, ntiles, G * waves};
+    const int64_t x = b % 8, k = b / 8, nbx = (G - x + 7) / 8, chunk = (ntiles + 7) / 8;
+    return NmSched{x * chunk + k * waves + wave, std::min<int64_t>(ntiles, x * chunk + chunk), nbx * waves};
+}
+
+// acc[k] (gather layout: row RPI k + rl of the block, channels 4 fg..) =
+//   sum over CSR row n of w * src[m][b0..b0+15]   (MASK: src * mscale * [msk > 0]),
+// entries in CSR order, fp32 fma.  Two neighbours' blocks are in flight at a time.
+template <int D, bool MASK>
+__device__ __forceinline__ void gather_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
+                                          __amdgpu_buffer_rsrc_t src, __amdgpu_buffer_rsrc_t msk, float mscale,
+                                          uint32_t n, uint32_t B, uint32_t b0, const uint32_t (&loff)[NmGeo<D>::K],
+                                          const bool (&rv)[NmGeo<D>::K], f32x4 (&acc)[NmGeo<D>::K]) {
+    using G = NmGeo<D>;
+    const int e0 = __builtin_amdgcn_readfirstlane(rowptr[n]);
+    const int e1 = __builtin_amdgcn_readfirstlane(rowptr[n + 1]);
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto contrib = [&](float w, const f32x4& v, const f32x4& m, f32x4& a) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = v[i];
+            if constexpr (MASK) t = m[i] > 0.f ? t * mscale : 0.f;
+            a[i] = fmaf(w, t, a[i]);
+        }
+    };
+    int e = e0;
+    for (; e + 1 < e1; e += 2) {
+        const int2 pa = pairs[e], pb = pairs[e + 1];  // wave-uniform: scalar loads
+        const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+        const uint32_t bbase = (static_cast<uint32_t>(pb.x) * B + b0) * (4u * D);
+        f32x4 va[G::K], vb[G::K], ma[G::K], mb[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            va[k] = nm_ld<D>(src, loff[k], rv[k], ba);
+            vb[k] = nm_ld<D>(src, loff[k], rv[k], bbase);
+            if constexpr (MASK) {
+                ma[k] = nm_ld<D>(msk, loff[k], rv[k], ba);
+                mb[k] = nm_ld<D>(msk, loff[k], rv[k], bbase);
+            }
+        }
+        const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            contrib(wa, va[k], ma[k], acc[k]);
+            contrib(wb, vb[k], mb[k], acc[k]);
+        }
+    }
+    if (e < e1) {
+        const int2 pa = pairs[e];
+        const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+        f32x4 va[G::K], ma[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            va[k] = nm_ld<D>(src, loff[k], rv[k], ba);
+            if constexpr (MASK) ma[k] = nm_ld<D>(msk, loff[k], rv[k], ba);
+        }
+        const float wa = __int_as_float(pa.y);
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) contrib(wa, va[k], ma[k], acc[k]);
+    }
+}
+
+// ------------------------------------------------------------------ forward
+template <int D, bool DROP>
+__global__ void __launch_bounds__(64 * kNmFwdWaves)
+k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ x,
+             const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
+             uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
+             uint64_t seed, uint32_t salt) {
+    using G = NmGeo<D>;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* wl = reinterpret_cast<float*>(smem);  // W [out][in] * fold, stride S
+    float* bl = wl + D * G::S;                   // bias * fold
+    float* tiles = bl + D;
+
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmFwdWaves - 1) / (64 * kNmFwdWaves);
+    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
+    f32x4 wv[WPER];
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmFwdWaves + threadIdx.x, W4 - 1));
+    const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+        const int i = u * 64 * kNmFwdWaves + threadIdx.x;
+        if (i < W4) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), wv[u] * fold);
+    }
+    if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
+    __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = tiles + wave * G::TILE;
+    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p_drop);
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmFwdWaves);
+    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
+        const uint32_t t32 = static_cast<uint32_t>(tile);
+        const uint32_t grp = lg_div(t32, fdN), n = t32 - grp * N, b0 = grp * 16;
+        const uint32_t nb = min(16u, B - b0);  // windows in this group (the last may be ragged)
+        bool rv[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
+        f32x4 acc[G::K];
+        gather_nm<D, false>(rowptr, pairs, xrs, xrs, 1.f, n, B, b0, loff, rv, acc);
+
+        // gather layout -> LDS -> MFMA B operand
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+        wave_sync_nm();
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
+#pragma unroll
+        for (int c = 0; c < G::CH; ++c) {
+            const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);  // W[16mt + j][16c + 4q + i]
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[mt] = mfma_nm(wa[i], bt[i], o[mt]);
+            }
+        }
+        // epilogue: ReLU, row-stream dropout (two channels per step) seeded with the window-major
+        // row id (b0 + j) N + n, so both layouts draw the same mask
+        uint32_t st = 0;
+        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float t = fmaxf(o[mt][reg], relu_floor);
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    t = u16 >= thr ? t : 0.0f;
+                }
+                o[mt][reg] = t;
+            }
+        }
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_sync_nm();
+        const uint32_t ob = (n * B + b0) * (4u * D);
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) nm_st<2>(yrs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
+    }
+}
+
+// ------------------------------------------------------------------ backward
+template <int D, bool MASK_IN, bool NB>
+__global__ void __launch_bounds__(64 * kNmBwdWaves, 2)
+k_gcn_bwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ dy,
+             const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
+             const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
+             uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out) {
+    using G = NmGeo<D>;
+    constexpr int SW = D + 4;
+    constexpr int WBUF = 2 * G::TILE;
+    constexpr int L = D * D + 2 * D;  // slab row: dW, db, d(node bias)
+    static_assert(kNmBwdWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    float* wl = lds + kNmBwdWaves * WBUF;
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves - 1) / (64 * kNmBwdWaves);
+    f32x4 wv[WPER];
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves + threadIdx.x, W4 - 1));
+#pragma unroll
+    for (int u = 0; u < WPER; ++u) {
+        const int i = u * 64 * kNmBwdWaves + threadIdx.x;
+        if (i < W4) st4(wl + (i / (D / 4)) * SW + 4 * (i % (D / 4)), wv[u]);
+    }
+    __syncthreads();
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = lds + wave * WBUF;  // t tile [row][feature], later dx
+    float* xl = tl + G::TILE;       // x tile [row][feature]
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MASK_IN ? yv : dy, bytes),
+                                 xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+
+    f32x4 dw[G::CH][G::CH];  // dW tile (mo, ni): rows o = 16mo + 4q + reg, cols i = 16ni + j
+#pragma unroll
+    for (int a = 0; a < G::CH; ++a)
+#pragma unroll
+        for (int b = 0; b < G::CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // channels 4fg..4fg+3, summed over this lane's rows
+    f32x4 nbacc[NB ? G::CH : 1];              // NB: channels 16mt + 4q + reg over this lane's rows j
+#pragma unroll
+    for (int mt = 0; mt < (NB ? G::CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmBwdWaves);
+    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
+        const uint32_t t32 = static_cast<uint32_t>(tile);
+        const uint32_t grp = lg_div(t32, fdN), n = t32 - grp * N, b0 = grp * 16;
+        const uint32_t nb = min(16u, B - b0);
+        bool rv[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
+        const uint32_t ob = (n * B + b0) * (4u * D);
+        // own rows (one contiguous block): dz for db, x for dW and the output mask
+        f32x4 dz[G::K], mz[G::K], xv[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            dz[k] = nm_ld<D>(dys, loff[k], rv[k], ob);
+            if constexpr (MASK_IN) mz[k] = nm_ld<D>(ms, loff[k], rv[k], ob);
+            xv[k] = nm_ld<D>(xs, loff[k], rv[k], ob);
+        }
+        f32x4 acc[G::K];
+        gather_nm<D, MASK_IN>(rowptr, pairs, dys, ms, scale_in, n, B, b0, loff, rv, acc);
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+            if constexpr (MASK_IN) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dz[k][i] = mz[k][i] > 0.f ? dz[k][i] * scale_in : 0.f;
+            }
+            dbacc += dz[k];
+            st4(xl + (G::RPI * k + rl) * G::S + 4 * fg, xv[k]);
+        }
+        wave_sync_nm();
+        // dW[o][i] += sum_rows t[row][o] x[row][i]   (rows = 4q + kk on the K index)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int row = 4 * q + kk;
+            float ta[G::CH], xb[G::CH];
+#pragma unroll
+            for (int m = 0; m < G::CH; ++m) {
+                ta[m] = tl[row * G::S + 16 * m + j];
+                xb[m] = xl[row * G::S + 16 * m + j];
+            }
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo)
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni) dw[mo][ni] = mfma_nm(ta[mo], xb[ni], dw[mo][ni]);
+        }
+        // dx^T[i][row] = sum_o W[o][i] t[row][o] : A = W^T (LDS), B = t tile (LDS)
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < G::CH; ++a) {
+            const f32x4 bt = ld4(tl + j * G::S + 16 * a + 4 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ko = 16 * a + 4 * q + i;
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) o[mt] = mfma_nm(wl[ko * SW + 16 * mt + j], bt[i], o[mt]);
+            }
+        }
+        if (mask_out) {
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
+            }
+        }
+        if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
+            if (node_slot[n] < 0)
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) nbacc[mt] += o[mt];
+        }
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) nm_st<0>(dxs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
+        wave_sync_nm();
+    }
+    if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
+    }
+    // ---- per-block reduction of dW / db / node bias (fixed wave order -> deterministic)
+#pragma unroll
+    for (int off = G::LPR; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
+    __syncthreads();
+    float* red = lds;  // reuse the tile buffers
+    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
+    for (int wv2 = 0; wv2 < kNmBwdWaves; ++wv2) {
+        __syncthreads();
+        if (wave == wv2) {
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo)
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg)
+                        red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
+            if (lane < G::LPR)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
+            if (NB && j == 0)
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
+        }
+    }
+    __syncthreads();
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
+}
+
+template <typename Kern>
+int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int cap_per_cu) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        static_cast<int>(dyn));
+    int per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, dyn) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const int64_t want = (ntiles + waves - 1) / waves;
+    const int64_t cap = static_cast<int64_t>(std::min(per_cu, cap_per_cu)) * lg_num_cus();
+    return static_cast<int>(std::max<int64_t>(1, std::min(want, cap)));
+}
+
+bool nm_fits(int64_t B, int64_t N, int64_t D) { return N * B * D * 4 <= int64_t{0xFFFFFF00}; }
+
+}  // namespace
+
+extern "C" int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
+                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int flags,
+                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || !rowptr || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
+    if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
+    const bool drop = (flags & LG_F_DROPOUT) != 0;
+    if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    if (D != 32 && D != 64) return LG_EUNSUPPORTED;
+    if (B == 0) return LG_OK;
+    if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const int64_t ngroups = (B + 15) / 16, ntiles = ngroups * N;
+    const float relu_floor = (flags & LG_F_RELU) ? 0.f : -__builtin_huge_valf();
+    const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    const float* bp = (flags & LG_F_BIAS) ? bias : nullptr;
+    const size_t dyn = 4 * static_cast<size_t>(D * (D + 4) + D + kNmFwdWaves * 16 * (D + 4));
+    const int2* pr = reinterpret_cast<const int2*>(pairs);
+    const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
+    hipStream_t s = lg_stream(stream);
+#define LG_NM_FWD(DD, DR)                                                                                          \
+    do {                                                                                                           \
+        auto kern = k_gcn_fwd_nm<DD, DR>;                                                                          \
+        const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn, ntiles, kNmFwdWaves, 4);                             \
+        kern<<<grid, 64 * kNmFwdWaves, dyn, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),                \
+                                                 static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,     \
+                                                 relu_floor, dropout_p, scale, seed, salt);                        \
+    } while (0)
+    if (D == 64) {
+        if (drop) LG_NM_FWD(64, true);
+        else LG_NM_FWD(64, false);
+    } else {
+        if (drop) LG_NM_FWD(32, true);
+        else LG_NM_FWD(32, false);
+    }
+#undef LG_NM_FWD
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D) {
+    if (D != 32 && D != 64) return LG_EUNSUPPORTED;
+    return static_cast<int64_t>(2) * lg_num_cus() * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int lg_gcn_bwd_nm(const int32_t* rowptr_t, const int32_t* pairs_t, const float* dy, const float* y,
+                             const float* x, const float* W, float* dx_out, float* dW, float* db,
+                             const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
+                             float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || !rowptr_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
+    if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
+    const bool mask_in = (flags & LG_F_MASK_IN) != 0;
+    if (mask_in && !y) return LG_EINVAL;
+    if (D != 32 && D != 64) return LG_EUNSUPPORTED;
+    if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const int64_t ngroups = (B + 15) / 16, ntiles = std::max<int64_t>(ngroups * N, 0);
+    const int mask_out = (flags & LG_F_MASK_OUT) ? 1 : 0;
+    const size_t dyn = 4 * static_cast<size_t>(kNmBwdWaves * 2 * 16 * (D + 4) + D * (D + 4));
+    const int2* pr = reinterpret_cast<const int2*>(pairs_t);
+    const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
+    float* slab = static_cast<float*>(workspace);
+    hipStream_t s = lg_stream(stream);
+    int grid = 1;
+    // B == 0 still runs one (empty) launch so the slab holds zeros
+#define LG_NM_BWD(DD, MI, NBB)                                                                                     \
+    do {                                                                                                           \
+        auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                     \
+        grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),  \
+                             2 * lg_num_cus());                                                                    \
+        kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(rowptr_t, pr, dy, y, x, W, node_slot, dx_out, slab,               \
+                                                 static_cast<uint32_t>(N), static_cast<uint32_t>(B),               \
+                                                 static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,           \
+                                                 scale_out);                                                       \
+    } while (0)
+#define LG_NM_BWD_D(DD)                                  \
+    do {                                                 \
+        if (mask_in) {                                   \
+            if (node_slot) LG_NM_BWD(DD, true, true);    \
+            else LG_NM_BWD(DD, true, false);             \
+        } else {                                         \
+            if (node_slot) LG_NM_BWD(DD, false, true);   \
+            else LG_NM_BWD(DD, false, false);            \
+        }                                                \
+    } while (0)
+    if (D == 64) LG_NM_BWD_D(64);
+    else LG_NM_BWD_D(32);
+#undef LG_NM_BWD_D
+#undef LG_NM_BWD
+    LG_RET_IF_LAUNCH_FAILED();
+    const int64_t L = D * D + 2 * D;
+    const LgSlabSeg segs[3] = {{0, D * D, dW}, {D * D, D, db}, {D * D + D, D, dnode_bias}};
+    return lg_launch_slab_reduce_multi(slab, grid, L, segs, 3, nullptr, nullptr, s);
+}

@@ -12,20 +12,25 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // One row group of LPR lanes per (b, n) row.
 template <int D>
 __global__ void __launch_bounds__(256)
+// Output row r of x0: window-major r = b N + n, node-major (nm) r = n B + b; fdM divides by
+// the fast index's extent (N, resp. B).  The dropout index is always the window-major one,
+// so both layouts draw the same mask.
 k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, const float* __restrict__ bias,
-            float* __restrict__ x0, int64_t N, lg_fastdiv fdN, int64_t S, int64_t R, int dropout, float p, float scale,
-            uint64_t seed, uint32_t salt) {
+            float* __restrict__ x0, int64_t N, lg_fastdiv fdM, int nm, int64_t S, int64_t R, int dropout, float p,
+            float scale, uint64_t seed, uint32_t salt) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const uint32_t key = lg_dropout_key(seed, salt);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
-        const uint32_t b = lg_div(static_cast<uint32_t>(r), fdN), n = static_cast<uint32_t>(r) - b * fdN.d;
+        const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
+        const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
         const int32_t s = slot[n];
         f32x4 v = s >= 0 ? ld4(proj + (static_cast<int64_t>(b) * S + s) * D + 4 * fg) : ld4(bias + 4 * fg);
+        const int64_t rw = static_cast<int64_t>(b) * N + n;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float t = fmaxf(v[i], 0.f);
-            if (dropout) t = lg_dropout(t, p, scale, key, r * D + 4 * fg + i);
+            if (dropout) t = lg_dropout(t, p, scale, key, rw * D + 4 * fg + i);
             v[i] = t;
         }
         st4(x0 + r * D + 4 * fg, v);
@@ -58,13 +63,14 @@ template <int D>
 __global__ void __launch_bounds__(256)
 k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict__ inc_item,
                const float* __restrict__ dpipe, const float* __restrict__ dpool, float* __restrict__ dh, int64_t N,
-               lg_fastdiv fdN, int64_t P, int64_t R) {
+               lg_fastdiv fdM, int nm, int64_t P, int64_t R) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const float fN = static_cast<float>(N);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
-        const uint32_t bu = lg_div(static_cast<uint32_t>(r), fdN), n = static_cast<uint32_t>(r) - bu * fdN.d;
-        const int64_t b = bu;
+        const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
+        const int64_t b = nm ? lo : hi;
+        const uint32_t n = nm ? hi : lo;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         if (dpool) {
             const f32x4 g = ld4(dpool + b * D + 4 * fg);
@@ -145,17 +151,18 @@ extern "C" int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, c
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
     if (R >= kLgMaxRows) return LG_EUNSUPPORTED;
-    const lg_fastdiv fdN = lg_make_fastdiv(static_cast<uint32_t>(N));
+    const int nm = (flags & LG_F_NODE_MAJOR) ? 1 : 0;
+    const lg_fastdiv fdM = lg_make_fastdiv(static_cast<uint32_t>(nm ? B : N));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     switch (D) {
         case 64:
-            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdN, S, R, dropout, dropout_p,
-                                                            scale, seed, salt);
+            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+                                                            dropout_p, scale, seed, salt);
             break;
         case 32:
-            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdN, S, R, dropout, dropout_p,
-                                                            scale, seed, salt);
+            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+                                                            dropout_p, scale, seed, salt);
             break;
         default:
             return LG_EUNSUPPORTED;
@@ -184,17 +191,22 @@ extern "C" int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* fe
 
 extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, const float* dpipe,
                                    const float* dpool, float* dh, int64_t B, int64_t N, int64_t P, int64_t D,
-                                   lg_stream_t stream) {
+                                   int flags, lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     const int64_t R = B * N;
     if (R == 0) return LG_OK;
     if (!inc_rowptr || !dh || (P > 0 && (!inc_item || !dpipe))) return LG_EINVAL;
     if (R >= kLgMaxRows) return LG_EUNSUPPORTED;
-    const lg_fastdiv fdN = lg_make_fastdiv(static_cast<uint32_t>(N));
+    const int nm = (flags & LG_F_NODE_MAJOR) ? 1 : 0;
+    const lg_fastdiv fdM = lg_make_fastdiv(static_cast<uint32_t>(nm ? B : N));
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64: k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdN, P, R); break;
-        case 32: k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdN, P, R); break;
+        case 64:
+            k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
+            break;
+        case 32:
+            k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
+            break;
         default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();
@@ -230,7 +242,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 4; }
+extern "C" int lg_abi_version(void) { return 5; }
 
 extern "C" const char* lg_strerror(int code) {
     switch (code) {

@@ -20,20 +20,22 @@ namespace {
 constexpr int kPoolThreads = 1024;
 constexpr int kHid = 128;
 
-// pooled_lds[d] = mean over the N rows of window b (all threads participate).
+// pooled_lds[d] = mean over the N rows of window b (all threads participate).  Row of
+// (window b, node n) = b * sb + n * sn: (N, 1) window-major, (1, B) node-major.
 template <int D>
-__device__ __forceinline__ void pool_window(const float* __restrict__ x, int64_t b, int64_t N,
+__device__ __forceinline__ void pool_window(const float* __restrict__ x, int64_t b, int64_t N, int64_t sb, int64_t sn,
                                             f32x4* __restrict__ part, float* __restrict__ pooled_lds) {
     constexpr int LPR = D / 4, G = kPoolThreads / LPR;
     const int g = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-    const float* xb = x + b * N * D + 4 * fg;
+    const float* xb = x + b * sb * D + 4 * fg;
+    const int64_t step = sn * D;
     f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
     int64_t n = g;
     for (; n + G < N; n += 2 * G) {  // two independent loads in flight per lane
-        a0 += ld4(xb + n * D);
-        a1 += ld4(xb + (n + G) * D);
+        a0 += ld4(xb + n * step);
+        a1 += ld4(xb + (n + G) * step);
     }
-    if (n < N) a0 += ld4(xb + n * D);
+    if (n < N) a0 += ld4(xb + n * step);
     part[threadIdx.x] = a0 + a1;
     __syncthreads();
     if (threadIdx.x < D) {
@@ -51,7 +53,7 @@ __global__ void __launch_bounds__(kPoolThreads) k_mean_pool(const float* __restr
     __shared__ f32x4 part[kPoolThreads];
     __shared__ float pooled[D];
     const int64_t b = blockIdx.x;
-    pool_window<D>(x, b, N, part, pooled);
+    pool_window<D>(x, b, N, N, 1, part, pooled);
     if (threadIdx.x < D) out[b * D + threadIdx.x] = pooled[threadIdx.x];
 }
 
@@ -60,12 +62,12 @@ __global__ void __launch_bounds__(kPoolThreads)
 k_pool_head_fwd(const float* __restrict__ x, const float* __restrict__ W1, const float* __restrict__ b1,
                 const float* __restrict__ w2, const float* __restrict__ b2, float* __restrict__ pooled_out,
                 float* __restrict__ hid_out, float* __restrict__ logits, int64_t ldo, int64_t col, int64_t N,
-                float p_drop, float dscale, uint64_t seed, uint32_t salt) {
+                int64_t sb, int64_t sn, float p_drop, float dscale, uint64_t seed, uint32_t salt) {
     __shared__ f32x4 part[kPoolThreads];
     __shared__ float pooled[D];
     __shared__ float red[kHid];
     const int64_t b = blockIdx.x;
-    pool_window<D>(x, b, N, part, pooled);
+    pool_window<D>(x, b, N, sb, sn, part, pooled);
     const int t = threadIdx.x;
     if (t < D) pooled_out[b * D + t] = pooled[t];
     if (t < kHid) {
@@ -169,9 +171,11 @@ extern "C" int lg_pool_head_fwd(const float* x, const float* w1, const float* b1
     const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     const unsigned grid = static_cast<unsigned>(B);
+    const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // x is [N][B][D] instead of [B][N][D]
+    const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
 #define LG_PH(DD, DR)                                                                                             \
     k_pool_head_fwd<DD, DR><<<grid, kPoolThreads, 0, s>>>(x, w1, b1, w2, b2, pooled, hid, logits, ldo, col, N,    \
-                                                           dropout_p, scale, seed, salt)
+                                                           sb, sn, dropout_p, scale, seed, salt)
     if (D == 64) {
         if (drop) LG_PH(64, true); else LG_PH(64, false);
     } else {

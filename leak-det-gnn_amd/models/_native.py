@@ -15,13 +15,14 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 4  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 5  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
 LG_F_DROPOUT = 0x04
 LG_F_MASK_IN = 0x08
 LG_F_MASK_OUT = 0x10
+LG_F_NODE_MAJOR = 0x20
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)
@@ -44,7 +45,11 @@ SIGNATURES = {
     "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32,
                           _p, _p]),
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
-    "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),
+    "lg_gcn_fwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_gcn_bwd_nm_workspace_bytes": (_i64, [_i64]),
+    "lg_gcn_bwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p,
+                             _p]),
     "lg_edge_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64,
                                 _u32, _p]),
     "lg_edge_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),

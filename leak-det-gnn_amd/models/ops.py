@@ -19,6 +19,7 @@ Autograd functions:
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -29,6 +30,14 @@ from . import _native as nat
 from ._native import check, load_library, ptr, require_device, stream_of
 
 SUPPORTED_D = (32, 64)
+
+# Layout of the LeakDetector node features between GNNTrunkFn and HeadsFn.  "node"
+# (default): [N][B][D], row n*B + b — the B windows of a node are contiguous, so a GCN
+# tile (1 node x 16 windows) gathers one contiguous block per neighbour (lg_gcn_fwd_nm /
+# lg_gcn_bwd_nm).  "window": the reference's disjoint-union order [B][N][D]
+# (detector.py:105-114, 192-196) through lg_gcn_fwd / lg_gcn_bwd.  Both give the same
+# results (same dropout masks); only the memory order differs.
+TRUNK_NODE_MAJOR = os.environ.get("LEAKGNN_LAYOUT", "node") != "window"
 
 
 # ----------------------------------------------------------------------------- timing hook
@@ -124,6 +133,8 @@ class GCNGraph:
     rowptr_t: torch.Tensor
     col_t: torch.Tensor
     w_t: torch.Tensor
+    pairs: Optional[torch.Tensor] = None    # int32 (cap, 2): (col, float bits of w), node-major kernels
+    pairs_t: Optional[torch.Tensor] = None  # same for the transposed CSR
 
     @staticmethod
     def build(edge_index: torch.Tensor, num_nodes: int, device: torch.device, add_self_loops: bool = True,
@@ -145,6 +156,8 @@ class GCNGraph:
                                  ptr(g.col), ptr(g.w), ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(ws),
                                  stream_of(ei)), "lg_graph_build")
         g._keepalive = (ei, ws)  # freed after the stream consumes them
+        g.pairs = torch.stack([g.col, g.w.view(torch.int32)], dim=1).contiguous()
+        g.pairs_t = torch.stack([g.col_t, g.w_t.view(torch.int32)], dim=1).contiguous()
         return g
 
 
@@ -249,7 +262,8 @@ class TrunkConfig:
     nonsensor_idx: torch.Tensor    # int64 (N - #sensors,)
     dropout_p: float
     training: bool
-    capture: Optional[list] = None     # tests: receives the saved activations x_0 .. x_L
+    capture: Optional[list] = None     # tests: receives the saved activations x_0 .. x_L, as (B, N, D)
+    node_major: bool = False           # True: node features [N][B][D] (see TRUNK_NODE_MAJOR)
 
 
 class SensorProjFn(torch.autograd.Function):
@@ -294,6 +308,8 @@ class GNNTrunkFn(torch.autograd.Function):
     Backward: one lg_gcn_bwd per layer; the ReLU/dropout masks of a layer's
               output and of its input are applied inside the kernel, read back
               from the saved activations ([x > 0]), so no mask is stored.
+    cfg.node_major: the same chain on [N][B][D] features (lg_gcn_fwd_nm / lg_gcn_bwd_nm);
+    the output is then (N, B, D).
     """
 
     @staticmethod
@@ -309,24 +325,30 @@ class GNNTrunkFn(torch.autograd.Function):
         p = float(cfg.dropout_p) if drop else 0.0
         seed = _new_seed() if drop else 0
         dflag = nat.LG_F_DROPOUT if drop else 0
+        nm = bool(cfg.node_major)
         st = stream_of(proj)
-        x0 = torch.empty(B, N, D, device=proj.device, dtype=torch.float32)
+        x0 = torch.empty((N, B, D) if nm else (B, N, D), device=proj.device, dtype=torch.float32)
         with _timed("node_init", proj.device):
             check(lib.lg_node_init_fwd(ptr(cfg.sensor_slot), ptr(proj), ptr(node_bias.contiguous()), ptr(x0), B, N,
-                                       S, D, dflag, p, seed, 0, st), "lg_node_init_fwd")
+                                       S, D, dflag | (nat.LG_F_NODE_MAJOR if nm else 0), p, seed, 0, st),
+                  "lg_node_init_fwd")
         xs = [x0]
         g = cfg.graph
         for l in range(L):
             W, b = wb[2 * l].contiguous(), wb[2 * l + 1].contiguous()
             require_device(W, b)
             y = torch.empty_like(x0)
+            flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag
             with _timed("gcn_fwd", proj.device):
-                check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
-                                     D, g.nnz_cap, nat.LG_F_BIAS | nat.LG_F_RELU | dflag, p, seed, l + 1, st),
-                      "lg_gcn_fwd")
+                if nm:
+                    check(lib.lg_gcn_fwd_nm(ptr(g.rowptr), ptr(g.pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
+                                            flags, p, seed, l + 1, st), "lg_gcn_fwd_nm")
+                else:
+                    check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B,
+                                         N, D, g.nnz_cap, flags, p, seed, l + 1, st), "lg_gcn_fwd")
             xs.append(y)
         if cfg.capture is not None:
-            cfg.capture.extend(t.detach().clone() for t in xs)
+            cfg.capture.extend((t.transpose(0, 1) if nm else t).detach().clone() for t in xs)
         ctx.cfg = cfg
         ctx.scale = 1.0 / (1.0 - p) if drop else 1.0
         ctx.dims = (B, S, N, D, L)
@@ -343,7 +365,9 @@ class GNNTrunkFn(torch.autograd.Function):
         g = cfg.graph
         st = stream_of(xs[0])
         dy = grad_out.contiguous()
-        ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dy.device, dtype=torch.uint8)
+        nm = bool(cfg.node_major)
+        wsb = lib.lg_gcn_bwd_nm_workspace_bytes(D) if nm else lib.lg_gcn_bwd_workspace_bytes(D)
+        ws = torch.empty(int(wsb), device=dy.device, dtype=torch.uint8)
         grads_wb: List[Optional[torch.Tensor]] = [None] * (2 * L)
         dbias = torch.empty(D, device=dy.device, dtype=torch.float32)
         for l in range(L - 1, -1, -1):
@@ -352,18 +376,26 @@ class GNNTrunkFn(torch.autograd.Function):
             dW = torch.empty(D, D, device=dy.device, dtype=torch.float32)
             db = torch.empty(D, device=dy.device, dtype=torch.float32)
             first = l == 0  # layer 0's dx is the node-init gradient: its bias rows are summed in-kernel
+            slot_p, dbias_p = (ptr(cfg.sensor_slot), ptr(dbias)) if first else (None, None)
             with _timed("gcn_bwd", dy.device):
-                check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
-                                     ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), ptr(cfg.sensor_slot) if first else None,
-                                     ptr(dbias) if first else None, B, N, D, g.nnz_cap, flags, ctx.scale, ctx.scale,
-                                     ptr(ws), st), "lg_gcn_bwd")
+                if nm:
+                    check(lib.lg_gcn_bwd_nm(ptr(g.rowptr_t), ptr(g.pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                                            ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D, flags,
+                                            ctx.scale, ctx.scale, ptr(ws), st), "lg_gcn_bwd_nm")
+                else:
+                    check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), ptr(xs[l + 1]),
+                                         ptr(xs[l]), ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
+                                         g.nnz_cap, flags, ctx.scale, ctx.scale, ptr(ws), st), "lg_gcn_bwd")
             grads_wb[2 * l], grads_wb[2 * l + 1] = dW, db
             dy = dx  # already masked by the previous op's relu/dropout
-        dproj = dy.index_select(1, cfg.sensor_idx)
+        if nm:
+            dproj = dy.index_select(0, cfg.sensor_idx).transpose(0, 1)
+        else:
+            dproj = dy.index_select(1, cfg.sensor_idx)
         if cfg.slot_live is not None:
             dproj = dproj * cfg.slot_live.view(1, -1, 1)
         if L == 0:
-            dbias = dy.index_select(1, cfg.nonsensor_idx).sum(dim=(0, 1))
+            dbias = dy.index_select(0 if nm else 1, cfg.nonsensor_idx).sum(dim=(0, 1))
         return (None, dproj, dbias, *grads_wb)
 
 
@@ -377,6 +409,7 @@ class HeadsConfig:
     dropout_p: float         # EdgeHead dropout (edge_head.mlp[2].p)
     training: bool
     noleak_p: Optional[float] = None  # NoLeakHead dropout (noleak_head.mlp[2].p); None -> dropout_p
+    node_major: bool = False          # h is (N, B, D) (GNNTrunkFn with node_major) instead of (B, N, D)
 
 
 class HeadsFn(torch.autograd.Function):
@@ -395,7 +428,9 @@ class HeadsFn(torch.autograd.Function):
         lib = load_library()
         h = h.contiguous()
         require_device(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
-        B, N, D = h.shape
+        nm = bool(cfg.node_major)
+        N, B, D = h.shape if nm else (h.shape[1], h.shape[0], h.shape[2])
+        lay = nat.LG_F_NODE_MAJOR if nm else 0
         _check_d(D)
         hidden, nhidden = w1.shape[0], nw1.shape[0]
         inc = cfg.inc
@@ -412,11 +447,12 @@ class HeadsFn(torch.autograd.Function):
         w1c, w2c, nw1c, nw2c = w1.contiguous(), w2.contiguous(), nw1.contiguous(), nw2.contiguous()
         with _timed("edge_fwd", h.device):
             check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits),
-                                       P + 1, B, N, P, D, hidden, fe, pe, seed, EDGE_HEAD_SALT, st),
+                                       P + 1, B, N, P, D, hidden, fe | lay, pe, seed, EDGE_HEAD_SALT, st),
                   "lg_edge_head_fwd")
         with _timed("pool_head", h.device):
             check(lib.lg_pool_head_fwd(ptr(h), ptr(nw1c), ptr(nb1), ptr(nw2c), ptr(nb2), ptr(pooled), ptr(hid),
-                                       ptr(logits), P + 1, P, B, N, D, nhidden, fn, pn, seed, NOLEAK_HEAD_SALT, st),
+                                       ptr(logits), P + 1, P, B, N, D, nhidden, fn | lay, pn, seed, NOLEAK_HEAD_SALT,
+                                       st),
                   "lg_pool_head_fwd")
         ctx.cfg, ctx.drop = cfg, (pe, fe, pn, fn, seed)
         ctx.save_for_backward(h, w1c, b1, w2c, pooled, hid, nw1c, nw2c)
@@ -428,7 +464,9 @@ class HeadsFn(torch.autograd.Function):
         h, w1, b1, w2, pooled, hid, nw1, nw2 = ctx.saved_tensors
         pe, fe, pn, fn, seed = ctx.drop
         inc = ctx.cfg.inc
-        B, N, D = h.shape
+        nm = bool(ctx.cfg.node_major)
+        N, B, D = h.shape if nm else (h.shape[1], h.shape[0], h.shape[2])
+        lay = nat.LG_F_NODE_MAJOR if nm else 0
         P, hidden, nhidden = inc.num_pipes, w1.shape[0], nw1.shape[0]
         dev = h.device
         st = stream_of(h)
@@ -439,7 +477,7 @@ class HeadsFn(torch.autograd.Function):
         ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
         with _timed("edge_bwd", dev):
             check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(dl), P + 1, ptr(dpipe),
-                                       ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, pe, seed,
+                                       ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe | lay, pe, seed,
                                        EDGE_HEAD_SALT, ptr(ws), st), "lg_edge_head_bwd")
         dpooled = torch.empty(B, D, device=dev)
         ndw1, ndb1 = torch.empty_like(nw1), torch.empty(nhidden, device=dev)
@@ -452,7 +490,7 @@ class HeadsFn(torch.autograd.Function):
         dh = torch.empty_like(h)
         with _timed("pipe_scatter", dev):
             check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P,
-                                          D, st), "lg_pipe_scatter_bwd")
+                                          D, lay, st), "lg_pipe_scatter_bwd")
         return None, dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 

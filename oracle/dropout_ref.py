@@ -41,3 +41,44 @@ def keep_mask(seed: int, salt: int, idx: np.ndarray, p: float) -> np.ndarray:
     h = _mix32(x)
     u = (h >> np.uint64(8)).astype(np.float64) / 16777216.0
     return u.astype(np.float32) >= np.float32(p)
+
+
+# ---- row-stream dropout of the fused GCN forward (common.h lg_row_stream_seed) ----
+#   seed(row, q) = mix32(mix32(lo32(row) * 0x9E3779B9 ^ key) ^ hi32(row) * 0x85EBCA6B ^ q * 0x632BE5AB),
+#                  0 replaced by 0x6D2B79F5
+#   lane group q of a row owns channels 16 mt + 4 q + reg (t = 4 mt + reg); its stream
+#   steps xorshift32 (s ^= s<<13; s ^= s>>17; s ^= s<<5) once per channel PAIR (t >> 1);
+#   channel t keeps iff its 16-bit half (low for even t, high for odd t) >= rint(p * 2^16).
+def _xorshift32(s: np.ndarray) -> np.ndarray:
+    s = s ^ ((s << np.uint64(13)) & _M)
+    s = s ^ (s >> np.uint64(17))
+    return s ^ ((s << np.uint64(5)) & _M)
+
+
+def row_stream_seed(key: int, rows: np.ndarray, q: int) -> np.ndarray:
+    rows = rows.astype(np.uint64)
+    lo, hi = rows & _M, rows >> np.uint64(32)
+    a = _mix32(((lo * np.uint64(0x9E3779B9)) & _M) ^ np.uint64(key))
+    s = _mix32(a ^ ((hi * np.uint64(0x85EBCA6B)) & _M) ^ np.uint64((q * 0x632BE5AB) & 0xFFFFFFFF))
+    return np.where(s == 0, np.uint64(0x6D2B79F5), s)
+
+
+def keep_threshold16(p: float) -> int:
+    """rint(float32(p) * 2^16) (round half to even, as rintf)."""
+    return int(np.rint(np.float32(p) * np.float32(65536.0)))
+
+
+def row_stream_mask(seed: int, salt: int, rows: np.ndarray, D: int, p: float) -> np.ndarray:
+    """Keep mask [len(rows), D] of the fused GCN forward for the given global rows."""
+    key = dropout_key(seed, salt)
+    thr = np.uint64(keep_threshold16(p))
+    rows = np.asarray(rows, dtype=np.uint64).reshape(-1)
+    out = np.zeros((rows.size, D), dtype=bool)
+    for q in range(4):
+        s = row_stream_seed(key, rows, q)
+        for t in range(D // 16 * 4):
+            if t % 2 == 0:
+                s = _xorshift32(s)
+            u16 = (s & np.uint64(0xFFFF)) if t % 2 == 0 else (s >> np.uint64(16))
+            out[:, 16 * (t // 4) + 4 * q + (t % 4)] = u16 >= thr
+    return out

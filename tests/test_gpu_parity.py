@@ -300,7 +300,10 @@ def test_detector_train_mode_replay_with_oracle_masks():
     seed_h = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # HeadsFn draw
     sc = 1.0 / 0.9
     R = B * N
-    mk = [_masks(seed_t, l, (R, D), 0.1) for l in range(3)]
+    from oracle.dropout_ref import row_stream_mask
+    mk = [_masks(seed_t, 0, (R, D), 0.1)] + [   # node init: per-element hash; GCN layers: row streams
+        torch.from_numpy(row_stream_mask(seed_t, l, np.arange(R), D, 0.1).astype(np.float32)).to(DEV)
+        for l in (1, 2)]
     me = _masks(seed_h, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1)
     ei = torch.from_numpy(graph_ref.batchify(m.edge_index_single.numpy(), N, B))
     row, col, w = (t.to(DEV) for t in gcn_ref.gcn_norm(ei, R))
@@ -332,9 +335,90 @@ def test_detector_train_mode_replay_with_oracle_masks():
                        prefix="train grad ")
 
 
+@pytest.mark.parametrize("B", [1, 37, 256])
+@pytest.mark.parametrize("D", [64, 32])
+@pytest.mark.parametrize("drop", [False, True])
+def test_gcn_node_major_matches_window_major(B, D, drop):
+    """lg_gcn_fwd_nm / lg_gcn_bwd_nm on [N][B][D] vs lg_gcn_fwd / lg_gcn_bwd on [B][N][D]
+    (themselves oracle-checked above).  Forward bit-exact (same entry order, same MFMA
+    order, same row-stream dropout masks); backward dx bit-exact-or-1e-5, dW / db / node
+    bias (different reduction trees) within 1e-5.  B = 37 leaves a ragged window group."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    g = load("graph_ltown_a.npz")
+    N = 661
+    graph = GCNGraph.build(torch.from_numpy(g["edge_index"]), N, DEV)
+    gen = torch.Generator().manual_seed(B * 7 + D + drop)
+    x = torch.randn(B, N, D, generator=gen).relu().to(DEV)  # trunk inputs are post-ReLU
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    b = (torch.randn(D, generator=gen) / 4).to(DEV)
+    flags = ops.nat.LG_F_BIAS | ops.nat.LG_F_RELU | (ops.nat.LG_F_DROPOUT if drop else 0)
+    p, seed, salt = (0.1 if drop else 0.0), 987654321, 2
+    st = ops.stream_of(x)
+    y = torch.empty_like(x)
+    ops.check(lib.lg_gcn_fwd(ops.ptr(graph.rowptr), ops.ptr(graph.col), ops.ptr(graph.w), ops.ptr(x), ops.ptr(W),
+                             ops.ptr(b), ops.ptr(y), B, N, D, graph.nnz_cap, flags, p, seed, salt, st), "fwd")
+    xn = x.transpose(0, 1).contiguous()
+    yn = torch.empty_like(xn)
+    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                ops.ptr(yn), B, N, D, flags, p, seed, salt, st), "fwd_nm")
+    assert torch.equal(yn.transpose(0, 1), y), "node-major forward must match the window-major kernel bit for bit"
+    # backward with both masks and the node-bias sum
+    slot = torch.full((N,), -1, dtype=torch.int32)
+    slot[torch.randperm(N, generator=gen)[:29]] = torch.arange(29, dtype=torch.int32)
+    slot = slot.to(DEV)
+    dy = torch.randn(B, N, D, generator=gen).to(DEV)
+    sc = 1.0 / 0.9 if drop else 1.0
+    bflags = ops.nat.LG_F_MASK_IN | ops.nat.LG_F_MASK_OUT
+    outs = []
+    for nm in (False, True):
+        xx, yy, dd = (xn, yn, dy.transpose(0, 1).contiguous()) if nm else (x, y, dy)
+        dx = torch.empty_like(xx)
+        dW, db, dnb = (torch.empty(D, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV))
+        if nm:
+            ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+            ops.check(lib.lg_gcn_bwd_nm(ops.ptr(graph.rowptr_t), ops.ptr(graph.pairs_t), ops.ptr(dd), ops.ptr(yy),
+                                        ops.ptr(xx), ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db),
+                                        ops.ptr(slot), ops.ptr(dnb), B, N, D, bflags, sc, sc, ops.ptr(ws), st),
+                      "bwd_nm")
+            dx = dx.transpose(0, 1)
+        else:
+            ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+            ops.check(lib.lg_gcn_bwd(ops.ptr(graph.rowptr_t), ops.ptr(graph.col_t), ops.ptr(graph.w_t), ops.ptr(dd),
+                                     ops.ptr(yy), ops.ptr(xx), ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db),
+                                     ops.ptr(slot), ops.ptr(dnb), B, N, D, graph.nnz_cap, bflags, sc, sc,
+                                     ops.ptr(ws), st), "bwd")
+        outs.append((dx, dW, db, dnb))
+    for a, r, n in zip(outs[1], outs[0], ("dx", "dW", "db", "dnode_bias")):
+        assert_close(a, r, what=f"node-major {n}")
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_detector_node_major_matches_window_major(train, monkeypatch):
+    """The whole detector (train mode: same dropout masks) in both trunk layouts."""
+    from models import ops
+    state = load("detector_b2.npz")
+    m = _product_model(state).train(train)
+    B = 40
+    r = torch.randn(B, 36, 29, device=DEV)
+    tf = torch.randn(B, 36, 9, device=DEV)
+    res = []
+    for nm in (False, True):
+        monkeypatch.setattr(ops, "TRUNK_NODE_MAJOR", nm)
+        m.zero_grad()
+        torch.manual_seed(3)
+        out = m(r, tf)
+        out.square().sum().backward()
+        res.append((out.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert_close(res[1][0], res[0][0], what="logits node-major vs window-major")
+    assert_grads_close(list(res[1][1].items()), res[0][1], prefix="layout grad ")
+
+
+@pytest.mark.parametrize("nm", [False, True])
 @pytest.mark.parametrize("train", [False, True])
 @pytest.mark.parametrize("D", [64, 32])
-def test_fused_heads_vs_torch(train, D):
+def test_fused_heads_vs_torch(train, D, nm):
     """HeadsFn (fused EdgeHead, mean pool + NoLeakHead, one (B, P+1) output, incidence-reduced
     backward) vs float64 torch with the same dropout masks (oracle/dropout_ref.py)."""
     from models import ops
@@ -356,8 +440,10 @@ def test_fused_heads_vs_torch(train, D):
     c2 = torch.randn(1, generator=gen)
     dl = torch.randn(B, P + 1, generator=gen)
     params = [t.to(DEV).requires_grad_(True) for t in (h, W1, b1, W2, b2, V1, c1, V2, c2)]
+    if nm:  # node-major input (N, B, D): the grad is compared in the same layout below
+        params[0] = h.transpose(0, 1).contiguous().to(DEV).requires_grad_(True)
     torch.manual_seed(77)
-    logits = HeadsFn.apply(HeadsConfig(inc, 0.1, train), *params)
+    logits = HeadsFn.apply(HeadsConfig(inc, 0.1, train, node_major=nm), *params)
     (logits * dl.to(DEV)).sum().backward()
     # float64 reference with the same dropout masks
     ref = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2, V1, c1, V2, c2)]
@@ -376,7 +462,8 @@ def test_fused_heads_vs_torch(train, D):
     (lr * dl.double()).sum().backward()
     assert_close(logits, lr, what="head logits")
     for a, b, n in zip(params, ref, ("dh", "dW1", "db1", "dW2", "db2", "dV1", "dc1", "dV2", "dc2")):
-        assert_close(a.grad, b.grad, rtol=2e-5, what=n)
+        ga = a.grad.transpose(0, 1) if (nm and n == "dh") else a.grad
+        assert_close(ga, b.grad, rtol=2e-5, what=n)
 
 
 def test_pipe_features_kernel():

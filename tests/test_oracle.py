@@ -113,3 +113,39 @@ def test_state_dict_keys_match_reference():
     ref_keys = sorted(k[len("param."):] for k in fx if k.startswith("param."))
     assert ref_keys == sorted(n for n, _ in _ref_model().named_parameters())
     assert sum(fx["param." + k].size for k in ref_keys) == 60418
+
+
+def test_row_stream_dropout_oracle_matches_scalar_restatement():
+    """oracle/dropout_ref.row_stream_mask (vectorised) vs a scalar transcription of
+    common.h lg_row_stream_seed / lg_xorshift32 / lg_keep_threshold16; and the keep rate."""
+    from oracle.dropout_ref import dropout_key, row_stream_mask
+
+    def mix32(x):
+        x &= 0xFFFFFFFF
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & 0xFFFFFFFF
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & 0xFFFFFFFF
+        return x ^ (x >> 16)
+
+    seed, salt, p, D = 0x1234_5678_9ABC_DEF0, 2, 0.1, 64
+    key = dropout_key(seed, salt)
+    rows = [0, 1, 17, 660, 169215, (1 << 33) + 5]
+    got = row_stream_mask(seed, salt, np.array(rows), D, p)
+    for ri, row in enumerate(rows):
+        for q in range(4):
+            a = mix32(((row & 0xFFFFFFFF) * 0x9E3779B9) ^ key)
+            s = mix32(a ^ (((row >> 32) * 0x85EBCA6B) & 0xFFFFFFFF) ^ ((q * 0x632BE5AB) & 0xFFFFFFFF)) or 0x6D2B79F5
+            thr = int(round(p * 65536))  # 6554 for p = 0.1 (no tie)
+            for t in range(D // 16 * 4):
+                if t % 2 == 0:
+                    s ^= (s << 13) & 0xFFFFFFFF
+                    s ^= s >> 17
+                    s ^= (s << 5) & 0xFFFFFFFF
+                u16 = s & 0xFFFF if t % 2 == 0 else s >> 16
+                assert got[ri, 16 * (t // 4) + 4 * q + t % 4] == (u16 >= thr)
+    big = row_stream_mask(7, 1, np.arange(20000), D, p)
+    assert abs(big.mean() - 0.9) < 0.003
+    # neighbouring channels / rows are not trivially correlated
+    assert abs(np.corrcoef(big[:, 0], big[:, 1])[0, 1]) < 0.03
+    assert abs(np.corrcoef(big[:-1, 5], big[1:, 5])[0, 1]) < 0.03

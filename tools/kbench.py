@@ -33,7 +33,8 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,spmm,edge_fwd,edge_bwd,gru_fwd,gru_bwd")
+    ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,gcn_fwd_nm,gcn_fwd_nm_train,gcn_bwd_nm,spmm,"
+                                       "edge_fwd,edge_bwd,gru_fwd,gru_bwd")
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
@@ -70,6 +71,26 @@ def main():
         f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
                                          ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | lab, 0.0, 0, 0, st), "fwd")
         res[f"gcn_fwd_lab{lab >> 20}"] = {"us": timeit(f, args.iters)}
+    # node-major kernels (x, y as [N][B][D]; same bytes)
+    for name, fl in (("gcn_fwd_nm", 0), ("gcn_fwd_nm_train", nat.LG_F_DROPOUT)):
+        if name in which:
+            f = lambda fl=fl: check(lib.lg_gcn_fwd_nm(ptr(graph.rowptr), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias),
+                                                      ptr(y), B, N, D, nat.LG_F_BIAS | nat.LG_F_RELU | fl, 0.1, 123,
+                                                      1, st), name)
+            t = timeit(f, args.iters)
+            res[name] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    if "gcn_bwd_nm" in which:
+        dy = torch.randn_like(x)
+        yy = torch.relu(torch.randn_like(x))
+        dx = torch.empty_like(x)
+        dW = torch.empty(D, D, device=dev)
+        db = torch.empty(D, device=dev)
+        ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
+        f = lambda: check(lib.lg_gcn_bwd_nm(ptr(graph.rowptr_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
+                                            ptr(dx), ptr(dW), ptr(db), None, None, B, N, D,
+                                            nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), st), "bwd_nm")
+        t = timeit(f, args.iters)
+        res["gcn_bwd_nm"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
     if "spmm" in which:
         f = lambda: check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, N, D, E1,
                                       st), "spmm")
