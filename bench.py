@@ -95,7 +95,7 @@ def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
                       f"{med * 1e3:.1f} ms/step (oracle/detector_ref.py on torch CPU, {threads} threads)"}
 
 
-def pmc_traffic(batch: int) -> dict | None:
+def pmc_traffic(batch: int, node_major: bool) -> dict | None:
     """Per-launch HBM bytes of the train-mode lg_gcn_fwd from rocprofv3 PMC counters.
 
     Runs as child processes (never exec): one counter per pass, kernel trace only.
@@ -106,10 +106,11 @@ def pmc_traffic(batch: int) -> dict | None:
         return None
     vals = {}
     env = dict(os.environ, TMPDIR="/tmp")
+    which, kname = ("gcn_fwd_nm_train", "k_gcn_fwd_nm") if node_major else ("gcn_fwd_train", "k_gcn_fwd<")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory(dir="/tmp") as d:
             cmd = [prof, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv", "--",
-                   sys.executable, str(REPO / "tools" / "kbench.py"), "--which", "gcn_fwd_train", "--B", str(batch),
+                   sys.executable, str(REPO / "tools" / "kbench.py"), "--which", which, "--B", str(batch),
                    "--iters", "20"]
             try:
                 subprocess.run(cmd, env=env, cwd=str(REPO), timeout=300, check=True, stdout=subprocess.DEVNULL,
@@ -119,7 +120,7 @@ def pmc_traffic(batch: int) -> dict | None:
             per = {}
             for f in Path(d).rglob("*counter_collection.csv"):
                 for r in csv.DictReader(open(f)):
-                    if "k_gcn_fwd" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                    if kname in r["Kernel_Name"] and r["Counter_Name"] == counter:
                         per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
             if not per:
                 return None
@@ -336,7 +337,7 @@ def main() -> None:
     graph = model._device_state(dev)[0]
     prop_ms = time_propagate(graph, B, N, D, dev)
     prop_gbs = fwd_bytes / (prop_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(B) if (world == 1 and not args.no_pmc) else None
+    traffic = pmc_traffic(B, ops.TRUNK_NODE_MAJOR) if (world == 1 and not args.no_pmc) else None
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -346,7 +347,8 @@ def main() -> None:
                    "nodes": N, "edge_columns": E1 - N, "pipes": P, "windows_per_rank": B,
                    "global_batch": B * world, "feat": D, "gnn_layers": 2, "parallelism": f"dp{world}",
                    "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode"},
-        "roofline": {"kernel": "lg_gcn_fwd (fused gather-aggregate + MFMA transform)", "bound": "hbm",
+        "roofline": {"kernel": ("lg_gcn_fwd_nm" if ops.TRUNK_NODE_MAJOR else "lg_gcn_fwd")
+                     + " (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(traffic["bytes"]) if traffic else None,

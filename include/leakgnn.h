@@ -59,6 +59,16 @@ enum {
  * node-major [N][B][D] (row n*B + b), the layout of lg_gcn_fwd_nm / lg_gcn_bwd_nm.
  * Dropout masks are indexed by the window-major row in both layouts. */
 #define LG_F_NODE_MAJOR 0x20
+/* Tuning bits of lg_gcn_fwd_nm (kernel lab, tools/kbench.py): they pick a schedule and never
+ * change results.  LG_F_LAB_V1: the one-tile-per-wave kernel; bits 24..27: workgroups of
+ * 4 waves per CU for the software-pipelined kernel (0 = default). */
+#define LG_F_LAB_V1        0x00800000
+/* lg_gcn_fwd_nm transform: by default on bf16 MFMA with 3-way split fp32 operands
+ * (|error| <= ~2^-23 relative per product, fp32 accumulate: fp32-level accuracy, not
+ * bit-identical to lg_gcn_fwd); LG_F_F32_MFMA = exact v_mfma_f32_16x16x4_f32, bit-identical
+ * to lg_gcn_fwd on the transposed layout. */
+#define LG_F_F32_MFMA      0x00400000
+#define LG_F_LAB_BPC_SHIFT 24
 
 int lg_abi_version(void);
 const char* lg_strerror(int code);
@@ -158,7 +168,7 @@ int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
  *   lg_gcn_fwd for the same seed/salt).
  *   Requires N*B*D*4 <= 0xFFFFFF00 bytes (LG_EUNSUPPORTED otherwise). */
 int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
-                  const float* bias, float* y, int64_t B, int64_t N, int64_t D,
+                  const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                   int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 /* Backward of lg_gcn_fwd_nm: lg_gcn_bwd's contract on the node-major layout, over the
  * transposed CSR given as rowptr_t + pairs_t.  workspace: lg_gcn_bwd_nm_workspace_bytes(D). */

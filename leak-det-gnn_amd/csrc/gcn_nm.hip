@@ -234,6 +234,309 @@ k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
     }
 }
 
+// ------------------------------------------------------------------ forward, software-pipelined
+// Same math and bit-identical results as k_gcn_fwd_nm, reorganised so the HBM stream and
+// the MFMA transform overlap inside every wave: while tile i is transformed (64 MFMAs at
+// D = 64), the blocks of tile i+1's first NPF neighbours are already in flight in
+// registers (NPF x 16 rows x D floats = 16 KiB per wave at D = 64, NPF = 4).  Fewer waves
+// per CU (2-3 per SIMD) each walk ~5-8 tiles, so the pipeline reaches a steady state; the
+// one-tile-per-wave schedule of k_gcn_fwd_nm instead ran every wave's gather, then every
+// wave's MFMA burst, in lock step.  Neighbours past the NPF prefetched ones (degree > NPF)
+// are loaded in place, two at a time.  Accumulation order = CSR order in both kernels.
+constexpr int kNm2Waves = 4;
+
+// ---- 3-way bf16 split of fp32 operands (SPLIT transform) --------------------------------
+// x = x0 + x1 + x2 with x_i = bf16_rne(x - x0 - ... ): |x - (x0 + x1 + x2)| <= 2^-24 |x|.
+// A product x w is then sum_{i+j<=2} x_i w_j (6 bf16 MFMAs, each product exact in fp32,
+// fp32 accumulate); the dropped terms are <= 2^-24 |x w|: fp32-level accuracy at 6/16 of
+// the f32-MFMA issue time (v_mfma_f32_16x16x32_bf16: 16 cyc per 16x16x32 vs 32 cyc per
+// 16x16x4 for v_mfma_f32_16x16x4_f32).
+typedef __bf16 lg_bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float lg_f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t lg_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const lg_f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_bf16x2));
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+// 8 floats (two f32x4) -> three bf16x8 fragments (hi, mid, lo)
+__device__ __forceinline__ void split3_x8(const f32x4& u, const f32x4& v, lg_bf16x8& f0, lg_bf16x8& f1,
+                                          lg_bf16x8& f2) {
+    lg_u32x4 p0, p1, p2;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const float a = h < 2 ? u[2 * h] : v[2 * h - 4], b = h < 2 ? u[2 * h + 1] : v[2 * h - 3];
+        p0[h] = pk_bf16(a, b);
+        const float ra = a - bf_lo(p0[h]), rb = b - bf_hi(p0[h]);
+        p1[h] = pk_bf16(ra, rb);
+        p2[h] = pk_bf16(ra - bf_lo(p1[h]), rb - bf_hi(p1[h]));
+    }
+    f0 = __builtin_bit_cast(lg_bf16x8, p0);
+    f1 = __builtin_bit_cast(lg_bf16x8, p1);
+    f2 = __builtin_bit_cast(lg_bf16x8, p2);
+}
+__device__ __forceinline__ f32x4 mfma_bf(const lg_bf16x8& a, const lg_bf16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// LAB (kernel-lab builds only, -DLG_KERNEL_LAB; results are WRONG when set): 1 = skip the
+// MFMA transform, 2 = skip the neighbour loads — the memory-only and compute-only floors.
+// SPLIT: the transform on bf16 MFMA with 3-way split operands (above) instead of
+//   v_mfma_f32_16x16x4_f32; W's three parts are staged once per workgroup in LDS.
+// Measured and dropped (B = 256, L-TOWN-A): two tiles in flight per wave at 2 waves/SIMD
+// (+15-25 %, occupancy), the CSR staged in LDS per workgroup (+3.5 us of prologue), the
+// MFMA-operand gather layout without the LDS transposes (16 rows x 64 B per instruction:
+// the load stream alone 15 -> 25 us).
+template <int D, bool SPLIT>
+struct Nm2Lds {  // dynamic LDS layout (floats)
+    static constexpr int SB = D + 8;  // bf16 row stride of the split W parts
+    static constexpr int WF = SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
+    static constexpr int TILES = WF + D;                                // after W and bias
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + kNm2Waves * NmGeo<D>::TILE);
+};
+
+template <int D, int NPF>
+struct NmSlot {  // one tile in flight: its CSR range, weights and first NPF neighbour blocks
+    f32x4 pf[NPF][NmGeo<D>::K];
+    float pw[NPF];
+    int e0, e1;
+    uint32_t n, b0, nb;
+};
+
+template <int D, bool DROP, int NPF, bool SPLIT, int LAB = 0>
+__global__ void __launch_bounds__(64 * kNm2Waves)
+k_gcn_fwd_nm2(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ x,
+              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
+              uint64_t seed, uint32_t salt) {
+    using G = NmGeo<D>;
+    using LY = Nm2Lds<D, SPLIT>;
+    constexpr int SB = LY::SB;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* wl = reinterpret_cast<float*>(smem);         // fp32: W [out][in] * fold, stride S
+    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB
+    float* bl = wl + LY::WF;                            // bias * fold
+    float* tiles = wl + LY::TILES;
+
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNm2Waves - 1) / (64 * kNm2Waves);
+    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
+    {
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNm2Waves + threadIdx.x, W4 - 1));
+        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i = u * 64 * kNm2Waves + threadIdx.x;
+            if (i >= W4) continue;
+            const int o = i / (D / 4), c4 = 4 * (i % (D / 4));
+            const f32x4 w = wv[u] * fold;
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t p0 = pk_bf16(w[2 * h], w[2 * h + 1]);
+                    const float ra = w[2 * h] - bf_lo(p0), rb = w[2 * h + 1] - bf_hi(p0);
+                    const uint32_t p1 = pk_bf16(ra, rb);
+                    const uint32_t p2 = pk_bf16(ra - bf_lo(p1), rb - bf_hi(p1));
+                    const int e = o * SB + c4 + 2 * h;
+                    *reinterpret_cast<uint32_t*>(wsl + e) = p0;
+                    *reinterpret_cast<uint32_t*>(wsl + D * SB + e) = p1;
+                    *reinterpret_cast<uint32_t*>(wsl + 2 * D * SB + e) = p2;
+                }
+            } else {
+                st4(wl + o * G::S + c4, w);
+            }
+        }
+        if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
+    }
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = tiles + wave * G::TILE;
+    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p_drop);
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+
+    auto csr_row = [&](uint32_t n, int& e0, int& e1) {  // wave-uniform: scalar loads
+        e0 = __builtin_amdgcn_readfirstlane(rowptr[n]);
+        e1 = __builtin_amdgcn_readfirstlane(rowptr[n + 1]);
+    };
+    auto csr_pair = [&](int e) -> int2 { return pairs[e]; };
+
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNm2Waves);
+
+    // Straight-line issue (no branch around the vector loads, so the compiler counts them
+    // statically and waits per neighbour with vmcnt(n)): slots past the degree, and every
+    // slot past the wave's last tile, load with an out-of-range offset (0, no request).
+    NmSlot<D, NPF> sl;
+    auto issue = [&](NmSlot<D, NPF>& S, int64_t tile) {
+        const bool valid = tile < sc.end;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        S.n = t32 - grp * N;
+        S.b0 = grp * 16;
+        S.nb = valid ? min(16u, B - S.b0) : 0u;
+        int e0 = 0, e1 = 0;
+        if (valid) csr_row(S.n, e0, e1);
+        S.e0 = e0;
+        S.e1 = e1;
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            const bool have = e0 + i < e1;
+            const int2 pa = have ? csr_pair(e0 + i) : int2{0, 0};
+            S.pw[i] = __int_as_float(pa.y);
+            const uint32_t base = (static_cast<uint32_t>(pa.x) * B + S.b0) * (4u * D);
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+                S.pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
+                                       : nm_ld<D>(xrs, loff[k], have && (G::RPI * k + rl) < static_cast<int>(S.nb),
+                                                  base);
+        }
+    };
+    issue(sl, sc.first);
+    __syncthreads();  // W / bias staged (after the first tile's loads are in flight)
+
+    auto process = [&](NmSlot<D, NPF>& S, int64_t tile) {
+        const uint32_t n = S.n, b0 = S.b0, nb = S.nb;
+        const int e0 = S.e0, e1 = S.e1;
+        bool rv[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
+        f32x4 acc[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            if (e0 + i < e1) {
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[k][c] = fmaf(S.pw[i], S.pf[i][k][c], acc[k][c]);
+            }
+        }
+        // neighbours beyond the prefetched ones: in place, two blocks in flight
+        int e = e0 + NPF;
+        for (; e + 1 < e1; e += 2) {
+            const int2 pa = csr_pair(e), pb = csr_pair(e + 1);
+            const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+            const uint32_t bbs = (static_cast<uint32_t>(pb.x) * B + b0) * (4u * D);
+            f32x4 va[G::K], vb[G::K];
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) {
+                va[k] = nm_ld<D>(xrs, loff[k], rv[k], ba);
+                vb[k] = nm_ld<D>(xrs, loff[k], rv[k], bbs);
+            }
+            const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    acc[k][c] = fmaf(wa, va[k][c], acc[k][c]);
+                    acc[k][c] = fmaf(wb, vb[k][c], acc[k][c]);
+                }
+        }
+        if (e < e1) {
+            const int2 pa = csr_pair(e);
+            const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+            f32x4 va[G::K];
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) va[k] = nm_ld<D>(xrs, loff[k], rv[k], ba);
+            const float wa = __int_as_float(pa.y);
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[k][c] = fmaf(wa, va[k][c], acc[k][c]);
+        }
+        // this slot's next tile goes in flight under this tile's transform
+        issue(S, tile + sc.stride);
+        __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting the W reads above the issue
+
+        // gather layout -> LDS -> MFMA B operand
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+        wave_sync_nm();
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
+        if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + j * G::S + 16 * mt + 4 * q);
+        } else if constexpr (SPLIT) {
+            // yT[out][row] += sum_k W[out][k] (Ahat x)[row][k], k-step s covers k = 32 s + 8 q + (0..7)
+            // (W fragments read per group: software-pipelining them costs registers, hence occupancy,
+            // and measured slower)
+#pragma unroll
+            for (int s2 = 0; s2 < D / 32; ++s2) {
+                lg_bf16x8 b0f, b1f, b2f;
+                split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f,
+                          b2f);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                    const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                    const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
+                    const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
+                    // smallest terms first
+                    o[mt] = mfma_bf(a2, b0f, o[mt]);
+                    o[mt] = mfma_bf(a1, b1f, o[mt]);
+                    o[mt] = mfma_bf(a0, b2f, o[mt]);
+                    o[mt] = mfma_bf(a1, b0f, o[mt]);
+                    o[mt] = mfma_bf(a0, b1f, o[mt]);
+                    o[mt] = mfma_bf(a0, b0f, o[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < G::CH; ++c) {
+                const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);  // W[16mt + j][16c + 4q + i]
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[mt] = mfma_nm(wa[i], bt[i], o[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);  // W reads per k chunk: bounded register footprint
+            }
+        }
+        // epilogue: ReLU, row-stream dropout (two channels per step) seeded with the window-major
+        // row id (b0 + j) N + n, so both layouts draw the same mask
+        uint32_t st = 0;
+        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float t = fmaxf(o[mt][reg], relu_floor);
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    t = u16 >= thr ? t : 0.0f;
+                }
+                o[mt][reg] = t;
+            }
+        }
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_sync_nm();
+        const uint32_t ob = (n * B + b0) * (4u * D);
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) nm_st<2>(yrs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
+    };
+
+    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) process(sl, tile);
+}
+
 // ------------------------------------------------------------------ backward
 template <int D, bool MASK_IN, bool NB>
 __global__ void __launch_bounds__(64 * kNmBwdWaves, 2)
@@ -418,10 +721,26 @@ int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int
 
 bool nm_fits(int64_t B, int64_t N, int64_t D) { return N * B * D * 4 <= int64_t{0xFFFFFF00}; }
 
+// Transform selection of lg_gcn_fwd_nm: split-bf16 MFMA by default, exact f32 MFMA under
+// LG_F_F32_MFMA (bit-identical to lg_gcn_fwd).  Lab builds add the LAB floors (bits 28-29).
+template <int D, bool DR>
+auto nm2_kernel(int flags) {
+    const bool split = (flags & LG_F_F32_MFMA) == 0;
+#ifdef LG_KERNEL_LAB
+    switch ((flags >> 28) & 3) {
+        case 1: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 1> : k_gcn_fwd_nm2<D, DR, 4, false, 1>;
+        case 2: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 2> : k_gcn_fwd_nm2<D, DR, 4, false, 2>;
+        case 3: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 3> : k_gcn_fwd_nm2<D, DR, 4, false, 3>;
+        default: break;
+    }
+#endif
+    return split ? k_gcn_fwd_nm2<D, DR, 4, true, 0> : k_gcn_fwd_nm2<D, DR, 4, false, 0>;
+}
+
 }  // namespace
 
 extern "C" int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
-                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int flags,
+                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
                              float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
     if (B < 0 || N <= 0 || !rowptr || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
     if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
@@ -434,17 +753,31 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const 
     const float relu_floor = (flags & LG_F_RELU) ? 0.f : -__builtin_huge_valf();
     const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const float* bp = (flags & LG_F_BIAS) ? bias : nullptr;
-    const size_t dyn = 4 * static_cast<size_t>(D * (D + 4) + D + kNmFwdWaves * 16 * (D + 4));
+    // tuning bits (no effect on results): LG_F_LAB_V1 = the one-tile-per-wave kernel,
+    // LG_F_LAB_BPC(n) = n workgroups of 4 waves per CU for the pipelined kernel
+    const bool lab_v1 = (flags & LG_F_LAB_V1) != 0;
+    const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 4;
+    (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
     hipStream_t s = lg_stream(stream);
 #define LG_NM_FWD(DD, DR)                                                                                          \
     do {                                                                                                           \
-        auto kern = k_gcn_fwd_nm<DD, DR>;                                                                          \
-        const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn, ntiles, kNmFwdWaves, 4);                             \
-        kern<<<grid, 64 * kNmFwdWaves, dyn, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),                \
-                                                 static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,     \
-                                                 relu_floor, dropout_p, scale, seed, salt);                        \
+        if (lab_v1) {                                                                                              \
+            auto kern = k_gcn_fwd_nm<DD, DR>;                                                                      \
+            const size_t dyn1 = 4 * static_cast<size_t>(DD * (DD + 4) + DD + kNmFwdWaves * 16 * (DD + 4));        \
+            const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn1, ntiles, kNmFwdWaves, 4);                        \
+            kern<<<grid, 64 * kNmFwdWaves, dyn1, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),           \
+                                                      static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,\
+                                                      relu_floor, dropout_p, scale, seed, salt);                   \
+        } else {                                                                                                   \
+            auto kern = nm2_kernel<DD, DR>(flags);                                                                 \
+            const size_t dyn2 = (flags & LG_F_F32_MFMA) ? Nm2Lds<DD, false>::BYTES : Nm2Lds<DD, true>::BYTES;      \
+            const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
+            kern<<<grid, 64 * kNm2Waves, dyn2, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),             \
+                                                    static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,  \
+                                                    relu_floor, dropout_p, scale, seed, salt);                     \
+        }                                                                                                          \
     } while (0)
     if (D == 64) {
         if (drop) LG_NM_FWD(64, true);

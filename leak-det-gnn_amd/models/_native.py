@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 5  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 6  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -23,6 +23,8 @@ LG_F_DROPOUT = 0x04
 LG_F_MASK_IN = 0x08
 LG_F_MASK_OUT = 0x10
 LG_F_NODE_MAJOR = 0x20
+LG_F_LAB_V1 = 0x00800000  # kernel-lab schedule bit of lg_gcn_fwd_nm (tools/kbench.py)
+LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 3-way split bf16 MFMA)
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)
@@ -46,7 +48,7 @@ SIGNATURES = {
                           _p, _p]),
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),
-    "lg_gcn_fwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_gcn_fwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_gcn_bwd_nm_workspace_bytes": (_i64, [_i64]),
     "lg_gcn_bwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p,
                              _p]),

@@ -38,6 +38,9 @@ SUPPORTED_D = (32, 64)
 # (detector.py:105-114, 192-196) through lg_gcn_fwd / lg_gcn_bwd.  Both give the same
 # results (same dropout masks); only the memory order differs.
 TRUNK_NODE_MAJOR = os.environ.get("LEAKGNN_LAYOUT", "node") != "window"
+# lg_gcn_fwd_nm schedule / transform bits (LG_F_F32_MFMA, LG_F_LAB_*; include/leakgnn.h) for A/B
+# timing of the trunk; the schedule bits never change results.
+GCN_FWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_NM_FLAGS", "0"), 0)
 
 
 # ----------------------------------------------------------------------------- timing hook
@@ -342,7 +345,8 @@ class GNNTrunkFn(torch.autograd.Function):
             with _timed("gcn_fwd", proj.device):
                 if nm:
                     check(lib.lg_gcn_fwd_nm(ptr(g.rowptr), ptr(g.pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
-                                            flags, p, seed, l + 1, st), "lg_gcn_fwd_nm")
+                                            g.nnz_cap, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed, l + 1, st),
+                          "lg_gcn_fwd_nm")
                 else:
                     check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B,
                                          N, D, g.nnz_cap, flags, p, seed, l + 1, st), "lg_gcn_fwd")

@@ -340,8 +340,9 @@ def test_detector_train_mode_replay_with_oracle_masks():
 @pytest.mark.parametrize("drop", [False, True])
 def test_gcn_node_major_matches_window_major(B, D, drop):
     """lg_gcn_fwd_nm / lg_gcn_bwd_nm on [N][B][D] vs lg_gcn_fwd / lg_gcn_bwd on [B][N][D]
-    (themselves oracle-checked above).  Forward bit-exact (same entry order, same MFMA
-    order, same row-stream dropout masks); backward dx bit-exact-or-1e-5, dW / db / node
+    (themselves oracle-checked above).  Forward with LG_F_F32_MFMA bit-exact (same entry
+    order, same MFMA order, same row-stream dropout masks), with the default split-bf16
+    transform within 1e-6 of the output scale; backward dx bit-exact-or-1e-5, dW / db / node
     bias (different reduction trees) within 1e-5.  B = 37 leaves a ragged window group."""
     from models import ops
     from models.ops import GCNGraph
@@ -361,9 +362,27 @@ def test_gcn_node_major_matches_window_major(B, D, drop):
                              ops.ptr(b), ops.ptr(y), B, N, D, graph.nnz_cap, flags, p, seed, salt, st), "fwd")
     xn = x.transpose(0, 1).contiguous()
     yn = torch.empty_like(xn)
+    F32 = ops.nat.LG_F_F32_MFMA
     ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
-                                ops.ptr(yn), B, N, D, flags, p, seed, salt, st), "fwd_nm")
-    assert torch.equal(yn.transpose(0, 1), y), "node-major forward must match the window-major kernel bit for bit"
+                                ops.ptr(yn), B, N, D, graph.nnz_cap, flags | F32, p, seed, salt, st), "fwd_nm")
+    assert torch.equal(yn.transpose(0, 1), y), "node-major forward (f32 MFMA) must match the window-major kernel bit for bit"
+    for lab in (ops.nat.LG_F_LAB_V1, F32 | (1 << 24), F32 | (3 << 24)):  # other schedules: same bits
+        y2 = torch.empty_like(xn)
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                    ops.ptr(y2), B, N, D, graph.nnz_cap, flags | lab, p, seed, salt, st), "fwd_nm lab")
+        assert torch.equal(y2, yn), f"schedule {lab:#x} changed the forward"
+    # default transform (3-way split bf16 MFMA): fp32-level accuracy, bar 1e-6 of the output scale
+    ys = torch.empty_like(xn)
+    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                ops.ptr(ys), B, N, D, graph.nnz_cap, flags, p, seed, salt, st), "fwd_nm split")
+    scale = yn.abs().amax().item()
+    err = (ys.double() - yn.double()).abs().max().item()
+    assert err <= 1e-6 * scale, f"split transform off by {err:.3e} (scale {scale:.3e})"
+    for lab in (1 << 24, 3 << 24):  # split schedules agree bit for bit
+        y2 = torch.empty_like(xn)
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                    ops.ptr(y2), B, N, D, graph.nnz_cap, flags | lab, p, seed, salt, st), "split lab")
+        assert torch.equal(y2, ys), f"split schedule {lab:#x} changed the forward"
     # backward with both masks and the node-bias sum
     slot = torch.full((N,), -1, dtype=torch.int32)
     slot[torch.randperm(N, generator=gen)[:29]] = torch.arange(29, dtype=torch.int32)
@@ -556,3 +575,37 @@ def test_linear_dw_vs_fp64(K, M, N):
     ref = torch.cat([dy.double().t() @ x.double(), dy.double().sum(0, keepdim=True).t()], 1)
     assert_close(dw, ref, what="dW")
     assert_close(db, ref[:, N], what="db")
+
+
+@pytest.mark.parametrize("D", [64, 32])
+def test_gcn_node_major_high_degree_graph(D):
+    """Node-major forward on a random graph with hubs (degree up to ~40, past the kernel's
+    prefetched neighbours), isolated nodes and duplicate edges: bit-exact with the
+    window-major kernel, which is oracle-checked on random graphs above."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    gen = torch.Generator().manual_seed(77 + D)
+    N, E, B = 300, 2400, 40
+    src = torch.randint(0, N - 20, (E,), generator=gen)
+    dst = torch.where(torch.rand(E, generator=gen) < 0.3, torch.randint(0, 5, (E,), generator=gen),
+                      torch.randint(0, N - 20, (E,), generator=gen))  # nodes 0..4 are hubs; N-20.. isolated
+    graph = GCNGraph.build(torch.stack([src, dst]), N, DEV)
+    x = torch.randn(B, N, D, generator=gen).to(DEV)
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    b = (torch.randn(D, generator=gen) / 4).to(DEV)
+    st = ops.stream_of(x)
+    for flags in (ops.nat.LG_F_BIAS | ops.nat.LG_F_RELU | ops.nat.LG_F_DROPOUT, ops.nat.LG_F_BIAS):
+        y = torch.empty_like(x)
+        ops.check(lib.lg_gcn_fwd(ops.ptr(graph.rowptr), ops.ptr(graph.col), ops.ptr(graph.w), ops.ptr(x), ops.ptr(W),
+                                 ops.ptr(b), ops.ptr(y), B, N, D, graph.nnz_cap, flags, 0.2, 5, 3, st), "fwd")
+        xn = x.transpose(0, 1).contiguous()
+        yn = torch.empty_like(xn)
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                    ops.ptr(yn), B, N, D, graph.nnz_cap, flags | ops.nat.LG_F_F32_MFMA, 0.2, 5, 3, st),
+                  "fwd_nm")
+        assert torch.equal(yn.transpose(0, 1), y)
+        ys = torch.empty_like(xn)
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+                                    ops.ptr(ys), B, N, D, graph.nnz_cap, flags, 0.2, 5, 3, st), "fwd_nm split")
+        assert (ys.double() - yn.double()).abs().max().item() <= 1e-6 * yn.abs().amax().item()

@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 5
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 6
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
     assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * (1532 + 661))
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1
@@ -116,7 +116,7 @@ def test_c_abi_host_only_calls():
                           1.0, 1.0,
                           None, None) == -1
     assert lib.lg_gcn_bwd_nm_workspace_bytes(48) == -2
-    assert lib.lg_gcn_fwd_nm(None, None, None, None, None, None, 16, 661, 64, 0, 0.0, 0, 0, None) == -1
+    assert lib.lg_gcn_fwd_nm(None, None, None, None, None, None, 16, 661, 64, 2193, 0, 0.0, 0, 0, None) == -1
     assert lib.lg_gcn_bwd_nm(None, None, None, None, None, None, None, None, None, None, None, 16, 661, 64, 0, 1.0,
                              1.0, None, None) == -1
     assert lib.lg_graph_build(None, 5, 0, 1, 1, 1.0, None, None, None, None, None, None, None, None) == -1

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
+    ap.add_argument("--nmlab", default="", help="comma list of lg_gcn_fwd_nm schedules: v1 or bpc<n> (train mode)")
     args = ap.parse_args()
     lib = nat.load_library()
     dev = torch.device("cuda:0")
@@ -75,10 +76,23 @@ def main():
     for name, fl in (("gcn_fwd_nm", 0), ("gcn_fwd_nm_train", nat.LG_F_DROPOUT)):
         if name in which:
             f = lambda fl=fl: check(lib.lg_gcn_fwd_nm(ptr(graph.rowptr), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias),
-                                                      ptr(y), B, N, D, nat.LG_F_BIAS | nat.LG_F_RELU | fl, 0.1, 123,
+                                                      ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | fl, 0.1, 123,
                                                       1, st), name)
             t = timeit(f, args.iters)
             res[name] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    for lab in [v for v in args.nmlab.split(",") if v]:
+        bits = 0
+        for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
+            bits |= {"v1": nat.LG_F_LAB_V1, "nomfma": 1 << 28, "noload": 2 << 28, "f32": nat.LG_F_F32_MFMA}.get(tok, 0)
+            if tok.startswith("bpc"):
+                bits |= int(tok[3:]) << 24
+        for mode, fl in (("eval", 0), ("train", nat.LG_F_DROPOUT)):
+            f = lambda fl=fl, bits=bits: check(lib.lg_gcn_fwd_nm(ptr(graph.rowptr), ptr(graph.pairs), ptr(x), ptr(W),
+                                                                 ptr(bias), ptr(y), B, N, D, E1,
+                                                                 nat.LG_F_BIAS | nat.LG_F_RELU | fl | bits, 0.1, 123,
+                                                                 1, st), "nmlab")
+            t = timeit(f, args.iters)
+            res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     if "gcn_bwd_nm" in which:
         dy = torch.randn_like(x)
         yy = torch.relu(torch.randn_like(x))

@@ -4,7 +4,7 @@
 # One rocprofv3 invocation per counter group (gfx950 cannot co-schedule them all);
 # kernel-trace only, never combined with sys/runtime tracing.
 set -e
-WHICH=${1:-gcn_fwd}; OUT=${2:-gpurun_out/pmc}; B=${3:-256}
+WHICH=${1:-gcn_fwd}; OUT=${2:-gpurun_out/pmc}; B=${3:-256}; shift 3; EXTRA="$@"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 i=0
@@ -14,6 +14,6 @@ for grp in \
   "FETCH_SIZE" "WRITE_SIZE" \
   "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_MFMA"; do
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace -d "$OUT/p$i" -o run --output-format csv -- \
-      python3 tools/kbench.py --which "$WHICH" --B "$B" --iters 20 > "$OUT/p$i.log" 2>&1
+      python3 tools/kbench.py --which "$WHICH" --B "$B" --iters 20 $EXTRA > "$OUT/p$i.log" 2>&1
   i=$((i+1))
 done

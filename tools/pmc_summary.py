@@ -9,7 +9,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
-        per[(r["Kernel_Name"][:40], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        per[(r["Kernel_Name"][28:60], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (k, d, c), v in per.items():
         acc[k][c].append(v)
 for k, cs in sorted(acc.items()):
