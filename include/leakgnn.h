@@ -230,21 +230,24 @@ int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, cons
  * (edge_head.mlp.0.weight), b1 [hidden], W2 [hidden] (mlp.3.weight), b2 [1];
  * logits : fp32, element (b, p) at logits[b*ldo + p] (ldo >= P; ldo = P+1 writes the
  * pipe columns of detector.py:216's (B, P+1) output in place).  hidden must be 128;
- * D in {32, 64}.  Dropout as lg_gcn_fwd, index (b*P + p)*hidden + unit. */
+ * D in {32, 64}.  Dropout as lg_gcn_fwd, index (b*P + p)*hidden + unit.
+ * hid: NULL, or fp32 [B*P][hidden] receiving the post-dropout hidden layer (what
+ * lg_edge_head_bwd needs; pass it in training).  The products run on bf16 MFMA with
+ * 3-way split fp32 operands (fp32-level accuracy, not bit-identical to an fp32 GEMM). */
 int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                     const float* w2, const float* b2, float* logits, int64_t ldo,
+                     const float* w2, const float* b2, float* logits, int64_t ldo, float* hid,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
-/* Backward of lg_edge_head_fwd (same flags/seed/salt): dlogits (row stride ldo) ->
- * dpipe fp32 [B][P][2][D] (grads w.r.t. h_u, h_v per pipe), dw1/db1/dw2/db2
- * (overwritten; deterministic fixed-order reduction of per-workgroup slabs). */
+/* Backward of lg_edge_head_fwd: hid (its hidden-layer output) and dlogits (row stride
+ * ldo) -> dpipe fp32 [B][P][2][D] (grads w.r.t. h_u, h_v per pipe), dw1/db1/dw2/db2
+ * (overwritten; deterministic fixed-order reduction of per-workgroup slabs).  flags and
+ * dropout_p as in the forward (the keep mask is read back as [hid > 0]). */
 int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden);
-int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                     const float* w2, const float* dlogits, int64_t ldo, float* dpipe,
+int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                     const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
                      float* dw1, float* db1, float* dw2, float* db2,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
-                     int flags, float dropout_p, uint64_t seed, uint32_t salt,
-                     void* workspace, lg_stream_t stream);
+                     int flags, float dropout_p, void* workspace, lg_stream_t stream);
 
 /* K10 forward: per-window mean over the N node rows.
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)

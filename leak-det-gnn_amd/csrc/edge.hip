@@ -4,305 +4,471 @@
 //   hid       = dropout(relu(W1 feat + b1))          (128)
 //   logit     = W2 hid + b2                          (1)
 //
-// The (B, P, 3D) feature tensor (150 MB at B=256) and the (B, P, 128) hidden
-// tensor are never written to HBM.  One 512-thread workgroup processes 16 pipe
-// rows at a time: the rows' endpoint features are gathered into LDS once, then
-// wave w (of 8) computes hidden units [16w, 16w+16) for all 16 rows as
-// hid^T = W1 feat^T on v_mfma_f32_16x16x4_f32 (exact fp32; its W1 slice lives in
-// registers), applies bias/ReLU/dropout, dots with W2 and the eight partial
-// logits are added in wave order.
+// The (B, P, 3D) feature tensor (150 MB at B=256) is never written to HBM.  Both kernels
+// run every product on v_mfma_f32_16x16x32_bf16 with 3-way split fp32 operands
+// (split_bf16.h: fp32-level accuracy at 6/16 of the f32-MFMA issue time).
 //
-// Backward recomputes hid, then per row tile:
-//   dhid  = dlogit * W2 * relu' * dropout mask                (lane-local)
-//   dW1^T += feat^T dhid   (MFMA, K = rows)   dW2 += dlogit*hid   db1 += dhid   db2 += dlogit
-//   dfeat^T = W1^T dhid^T  (MFMA, K = 128)     -> per-pipe endpoint grads
+// Forward: one 512-thread workgroup handles TR = 2048/D pipe rows per tile (32 at D=64):
+// each thread gathers one float4 of h_u and of h_v, and writes the three bf16 parts of
+// (h_u, h_v, |h_u - h_v|) into an LDS feature image.  Wave w (of 8) computes hidden units
+// [16w, 16w+16) for all rows as hid^T = W1 feat^T (its split W1 rows live in registers),
+// applies bias/ReLU/dropout, dots with W2; the eight partial logits are summed in wave order.
+// The next tile's endpoint rows are loaded into registers during the MFMA phase (and the
+// endpoint ids one tile further ahead).  In training the post-activation hidden layer is
+// written out (hid, fp32 [B*P][128]) for the backward.
+//
+// Backward (no recompute): from hid, dlogit:
+//   g     = dlogit * W2 * dropout_scale * [hid > 0]     (= d pre-activation)
+//   dW2  += dlogit * hid     db1 += g     db2 += dlogit  (fp64)
+//   dW1  += g^T feat         (MFMA, K = rows, both operands by ds_read_b64_tr_b16)
+//   dfeat^T = W1^T g^T       (MFMA, K = hidden; wave = 16 features x {u,v,|u-v|} x half the
+//                             hidden units; the two halves meet in LDS in a fixed order)
 //   dpipe[b,p,0] = dfeat_u + sgn*dfeat_abs,  dpipe[b,p,1] = dfeat_v - sgn*dfeat_abs,
-//   sgn = sign(h_u - h_v)  (torch abs backward).
+//   sgn = sign(h_u - h_v) from the fp32 difference (torch abs backward).
 // dpipe is then summed per node over the incidence CSR by lg_pipe_scatter_bwd
 // (deterministic, no atomics).  Weight grads: per-workgroup slabs + fixed-order reduce.
 #include <algorithm>
 #include "common.h"
 #include "reduce.h"
+#include "split_bf16.h"
 
 namespace {
 
 constexpr int HID = 128;
-constexpr int TR = 16;       // pipe rows per tile
 constexpr int NW = 8;        // waves per workgroup (= HID / 16)
+constexpr int NT = 64 * NW;
 
-__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q + (ks & 3); }
+template <int D>
+struct EG {
+    static constexpr int K3 = 3 * D;            // feature width
+    static constexpr int TR = 2048 / D;         // pipe rows per tile: one float4 of h_u and h_v per thread
+    static constexpr int RB = TR / 16;          // 16-row blocks per tile
+    static constexpr int KS = K3 / 32;          // k-steps of the feature contraction
+    static constexpr int F4 = D / 4;            // float4 per node row
+    static constexpr int FSB = K3 + 8;          // fwd feature image row stride (bf16): row reads conflict-free
+    static constexpr int FTB = K3 + 16;         // bwd feature image row stride: transposed reads conflict-free
+    static constexpr int GSB = HID + 8;         // bwd d-hidden image row stride
+    static constexpr int DT = D / 16;           // 16-feature tiles of one endpoint row
+    static constexpr int RG = NW / (2 * DT);    // row groups of the dfeat product
+    static constexpr int RBW = RB / RG;         // row blocks per wave in the dfeat product
+    static constexpr int KT = K3 / 16;          // 16-feature tiles of dW1
+    static constexpr int HPT = TR / 16;         // float4 of the hidden tile per thread
+    static constexpr int FPL = TR * FSB, FTPL = TR * FTB, GPL = TR * GSB;  // image plane strides
+    static constexpr int NROLE = DT * RG * RBW;  // dfeat output blocks (16 features x 16 rows) = NW
+    static constexpr int NRED = 2 * NROLE * 3;   // dfeat partials of both hidden halves (f32x4 x 64 lanes)
+    // forward workgroups resident per CU (VGPR-bound: 144 VGPRs of split W1 at D=64)
+    static constexpr int FWD_WG_PER_CU = 1;
+    static constexpr int64_t FWD_LDS = int64_t{2} * 2 * 3 * FPL + 4 * (2 * 4 * TR + 2 * HID);  // images, partials, b1/W2
+    static constexpr int64_t BWD_LDS = int64_t{2} * (3 * FTPL + 3 * GPL) + 2 * TR * D + 16 * 64 * NRED;
+};
+static_assert(EG<64>::RBW == 2 && EG<32>::RBW == 2, "dfeat wave split");
+static_assert(EG<64>::NROLE == NW && EG<32>::NROLE == NW, "one dfeat output block per wave");
+static_assert(EG<64>::BWD_LDS <= 160 * 1024 && EG<32>::BWD_LDS <= 160 * 1024, "LDS budget");
+
 // row r = b*P + p of the (B, P) logit space -> element (b, p) of a buffer with row stride ldo
 __device__ __forceinline__ int64_t lg_row_index(int64_t r, const lg_fastdiv& fdP, int64_t ldo) {
     const uint32_t b = lg_div(static_cast<uint32_t>(r), fdP);
     return static_cast<int64_t>(b) * ldo + (static_cast<uint32_t>(r) - b * fdP.d);
 }
 
-template <int D>
-struct EG {
-    static constexpr int K3 = 3 * D;       // feature width
-    static constexpr int KS = K3 / 4;      // k-steps of the feat contraction
-    static constexpr int FS = K3 + 4;      // LDS row stride of the feature tile
-    static constexpr int MT = K3 / 16;     // 16-row tiles of K3
-    static constexpr int DT = D / 16;      // 16-row tiles of D
-    static constexpr int F4 = D / 4;       // float4 per node row
-    static constexpr int NSPLIT = NW / DT; // waves sharing one k-triple of dfeat (split over hidden)
-    static constexpr int KPER = 32 / NSPLIT;  // k-steps (of 32 over hidden=128) per wave
-};
-
-// Gather the two endpoint rows of 16 pipe rows into ft[16][FS] (u at [0,D), v at [D,2D)).
-template <int D>
-__device__ __forceinline__ void gather_tile(const int64_t* __restrict__ ends, const float* __restrict__ h,
-                                            float* __restrict__ ft, int64_t row0, int64_t BP, const lg_fastdiv& fdP,
-                                            int64_t sb, int64_t sn) {
-    using G = EG<D>;
-    const int t = threadIdx.x;
-    if (t < TR * 2 * G::F4) {
-        const int row = t / (2 * G::F4), rem = t % (2 * G::F4), side = rem / G::F4, f4 = rem % G::F4;
-        const int64_t gr = row0 + row;
-        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (gr < BP) {
-            const uint32_t b = lg_div(static_cast<uint32_t>(gr), fdP), p = static_cast<uint32_t>(gr) - b * fdP.d;
-            const int64_t node = ends[2 * p + side];
-            v = ld4(h + (static_cast<int64_t>(b) * sb + node * sn) * D + 4 * f4);  // row of (window b, node)
-        }
-        st4(ft + row * G::FS + side * D + 4 * f4, v);
+// endpoint node ids of pipe row r (0, 0 past the end)
+__device__ __forceinline__ void load_ends(const int64_t* __restrict__ ends, int64_t r, int64_t BP,
+                                          const lg_fastdiv& fdP, uint32_t& nu, uint32_t& nv) {
+    nu = nv = 0;
+    if (r < BP) {
+        const uint32_t p = static_cast<uint32_t>(r) - lg_div(static_cast<uint32_t>(r), fdP) * fdP.d;
+        nu = static_cast<uint32_t>(ends[2 * p]);
+        nv = static_cast<uint32_t>(ends[2 * p + 1]);
     }
 }
-
-// feat[row][k] with the |u - v| third computed on the fly
+// float4 f of the two endpoint rows of pipe row r (zeros past the end); 32-bit element
+// offsets (the API requires N*B*D < 2^32)
 template <int D>
-__device__ __forceinline__ f32x4 feat4(const float* __restrict__ ft, int row, int k) {
-    using G = EG<D>;
-    if (k < 2 * D) return ld4(ft + row * G::FS + k);
-    const f32x4 u = ld4(ft + row * G::FS + (k - 2 * D));
-    const f32x4 v = ld4(ft + row * G::FS + (k - D));
-    f32x4 a;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = fabsf(u[i] - v[i]);
-    return a;
-}
-template <int D>
-__device__ __forceinline__ float feat1(const float* __restrict__ ft, int row, int k) {
-    using G = EG<D>;
-    if (k < 2 * D) return ft[row * G::FS + k];
-    return fabsf(ft[row * G::FS + (k - 2 * D)] - ft[row * G::FS + (k - D)]);
-}
-
-// hid^T tile rows n = 16w + 4q + reg for feat row j, bias included
-template <int D>
-__device__ __forceinline__ f32x4 hidden_tile(const float* __restrict__ ft, const float (&aw)[EG<D>::KS], f32x4 acc,
-                                             int j, int q) {
-#pragma unroll
-    for (int a = 0; a < EG<D>::KS / 4; ++a) {
-        const f32x4 v = feat4<D>(ft, j, 16 * a + 4 * q);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc = mfma(aw[4 * a + i], v[i], acc);
+__device__ __forceinline__ void load_rows(const float* __restrict__ h, int64_t r, int64_t BP, const lg_fastdiv& fdP,
+                                          uint32_t nu, uint32_t nv, uint32_t sb, uint32_t sn, int f, f32x4& u,
+                                          f32x4& v) {
+    u = v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (r < BP) {
+        const uint32_t b = lg_div(static_cast<uint32_t>(r), fdP);
+        u = ld4(h + ((b * sb + nu * sn) * D + 4 * f));
+        v = ld4(h + ((b * sb + nv * sn) * D + 4 * f));
     }
-    return acc;
+}
+// three bf16 parts of 4 floats -> 8-byte slots at img[off], img[pl + off], img[2 pl + off]
+__device__ __forceinline__ void st_split4(uint16_t* img, int pl, int off, const f32x4& x) {
+    lg_u32x2 a, b, c;
+    split3_x4(x, a, b, c);
+    *reinterpret_cast<lg_u32x2*>(img + off) = a;
+    *reinterpret_cast<lg_u32x2*>(img + pl + off) = b;
+    *reinterpret_cast<lg_u32x2*>(img + 2 * pl + off) = c;
 }
 
 template <int D>
-__global__ void __launch_bounds__(64 * NW)
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EG<D>::FWD_WG_PER_CU * 2, 4)))
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-           float* __restrict__ logit, int64_t ldo, int64_t sb, int64_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout,
-           float p_drop, float dscale, uint64_t seed, uint32_t salt) {
+           float* __restrict__ logit, int64_t ldo, float* __restrict__ hid_out, uint32_t sb, uint32_t sn,
+           lg_fastdiv fdP, int64_t BP, int64_t ntiles, int dropout, float p_drop, float dscale, uint64_t seed,
+           uint32_t salt) {
     using G = EG<D>;
-    __shared__ __attribute__((aligned(16))) float ft[TR * G::FS];
-    __shared__ float part[NW][TR];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    float aw[G::KS];
+    constexpr int RBF = G::RB / 2;  // row blocks per wave
+#ifdef LG_KERNEL_LAB
+    // kernel-lab builds only (results WRONG when set): 1 skip MFMA, 2 skip row loads, 4 skip split
+    const int lab = dropout >> 8;
+    dropout &= 1;
+#else
+    constexpr int lab = 0;
+#endif
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);                                  // [2][3][TR][FSB]
+    float(*part)[4][G::TR] = reinterpret_cast<float(*)[4][G::TR]>(fimg + 2 * 3 * G::FPL);  // [2][4][TR]
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    // wave = hidden units [32 nh, 32 nh + 32) (two 16-unit tiles: every feature fragment read
+    // from LDS feeds two MFMA chains) x row blocks [RBF rh, RBF rh + RBF)
+    const int nh = w & 3, rh = w >> 2;
+    // A operand: W1[n = 32 nh + 16 i + c][k = 32 ks + 8q + j], split once
+    lg_bf16x8 wa[2][G::KS][3];
 #pragma unroll
-    for (int ks = 0; ks < G::KS; ++ks) aw[ks] = W1[(16 * w + j) * G::K3 + fk(ks, q)];
-    f32x4 b1v, w2v;
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        b1v[reg] = b1[16 * w + 4 * q + reg];
-        w2v[reg] = W2[16 * w + 4 * q + reg];
+        for (int ks = 0; ks < G::KS; ++ks) {
+            const float* src = W1 + (32 * nh + 16 * i + c) * G::K3 + 32 * ks + 8 * q;
+            split3_x8(ld4(src), ld4(src + 4), wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
+        }
+    // b1 / W2 of hidden units n = 32 nh + 16 i + 4q + reg (the accumulator rows) are re-read
+    // from LDS per tile (VGPR budget)
+    float* bw = reinterpret_cast<float*>(part + 2);  // [2][HID]: b1, W2
+    if (threadIdx.x < HID) {
+        bw[threadIdx.x] = b1[threadIdx.x];
+        bw[HID + threadIdx.x] = W2[threadIdx.x];
     }
     const float bias2 = b2[0];
-    const uint32_t key = lg_dropout_key(seed, salt);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, fdP, sb, sn);
-        __syncthreads();
-        const f32x4 acc = hidden_tile<D>(ft, aw, b1v, j, q);
-        float s = 0.f;
+    const uint32_t key = lg_dropout_key(seed, salt), thr = lg_keep_threshold16(p_drop);
+    const int arow = threadIdx.x / G::F4, af = threadIdx.x % G::F4;  // gather slot of this thread
+    const int64_t step = gridDim.x;
+    // Software pipeline, one barrier per tile: while tile i's MFMAs run on feature image
+    // i&1, the wave splits tile i+1's endpoint rows into image (i+1)&1.  Rows are loaded
+    // three tiles ahead into two alternating register sets, node ids a tile before their rows.
+    uint32_t nu, nv;
+    f32x4 pu0, pv0, pu1, pv1;
+    auto rowof = [&](int64_t t) { return t * G::TR + arow; };
+    auto stage = [&](uint16_t* img, int part3, const f32x4& pu, const f32x4& pv) {  // a third of the slot
+        if (lab & 4) return;
+        if (part3 == 0) st_split4(img, G::FPL, arow * G::FSB + 4 * af, pu);
+        if (part3 == 1) st_split4(img, G::FPL, arow * G::FSB + D + 4 * af, pv);
+        if (part3 == 2) {
+            f32x4 a;
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            float v = fmaxf(acc[reg], 0.f);
-            if (dropout) v = lg_dropout(v, p_drop, dscale, key, (row0 + j) * HID + 16 * w + 4 * q + reg);
-            s = fmaf(v, w2v[reg], s);
+            for (int i = 0; i < 4; ++i) a[i] = fabsf(pu[i] - pv[i]);
+            st_split4(img, G::FPL, arow * G::FSB + 2 * D + 4 * af, a);
         }
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (q == 0) part[w][j] = s;
-        __syncthreads();
-        if (threadIdx.x < TR) {
-            const int64_t r = row0 + threadIdx.x;
-            float tot = part[0][threadIdx.x];
+    };
+    const int64_t t0 = blockIdx.x;
+    load_ends(ends, rowof(t0), BP, fdP, nu, nv);
+    load_rows<D>(h, rowof(t0), BP, fdP, nu, nv, sb, sn, af, pu0, pv0);
+    stage(fimg, 0, pu0, pv0);
+    stage(fimg, 1, pu0, pv0);
+    stage(fimg, 2, pu0, pv0);
+    load_ends(ends, rowof(t0 + step), BP, fdP, nu, nv);
+    load_rows<D>(h, rowof(t0 + step), BP, fdP, nu, nv, sb, sn, af, pu0, pv0);
+    load_ends(ends, rowof(t0 + 2 * step), BP, fdP, nu, nv);
+    load_rows<D>(h, rowof(t0 + 2 * step), BP, fdP, nu, nv, sb, sn, af, pu1, pv1);
+    load_ends(ends, rowof(t0 + 3 * step), BP, fdP, nu, nv);
+    __syncthreads();
+    // tile: this iteration's tile; (pu, pv): tile + step's rows, refilled with tile + 3 step's
+    auto body = [&](int64_t tile, int buf, f32x4& pu, f32x4& pv) {
+        const int64_t row0 = tile * G::TR;
+        const uint16_t* cur = fimg + buf * 3 * G::FPL;
+        uint16_t* nxt = fimg + (buf ^ 1) * 3 * G::FPL;
+        f32x4 acc[RBF][2];
 #pragma unroll
-            for (int i = 1; i < NW; ++i) tot += part[i][threadIdx.x];
+        for (int rb = 0; rb < RBF; ++rb) {
+            acc[rb][0] = ld4(bw + 32 * nh + 4 * q);
+            acc[rb][1] = ld4(bw + 32 * nh + 16 + 4 * q);
+        }
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+#pragma unroll
+            for (int rb = 0; rb < RBF; ++rb) {
+                const uint16_t* src = cur + (16 * (RBF * rh + rb) + c) * G::FSB + 32 * ks + 8 * q;
+                const lg_bf16x8 bf[3] = {lds_frag_row(src), lds_frag_row(src + G::FPL), lds_frag_row(src + 2 * G::FPL)};
+                if (lab & 1) {
+                    acc[rb][0][0] += bf[0][0];
+                    continue;
+                }
+                acc[rb][0] = mfma_split(wa[0][ks], bf, acc[rb][0]);
+                acc[rb][1] = mfma_split(wa[1][ks], bf, acc[rb][1]);
+            }
+            // the next tile's split, spread over the MFMA stream
+            if (ks * 3 / G::KS != (ks + 1) * 3 / G::KS) stage(nxt, ks * 3 / G::KS, pu, pv);
+        }
+        if (!(lab & 2)) {
+            load_rows<D>(h, rowof(tile + 3 * step), BP, fdP, nu, nv, sb, sn, af, pu, pv);
+            load_ends(ends, rowof(tile + 4 * step), BP, fdP, nu, nv);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RBF; ++rb) {
+            const int row = 16 * (RBF * rh + rb) + c;
+            const int64_t r = row0 + row;
+            // row-stream dropout (oracle/dropout_ref.py edge_stream_mask): one stream per
+            // (row, 4 nh + q), one xorshift step per pair of this lane's 8 units
+            uint32_t st = dropout ? lg_row_stream_seed(key, static_cast<uint64_t>(r), 4 * nh + q) : 0u;
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x4 hv;
+                const f32x4 w2v = ld4(bw + HID + 32 * nh + 16 * i + 4 * q);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    float v = fmaxf(acc[rb][i][reg], 0.f);
+                    if (dropout) {
+                        if ((reg & 1) == 0) st = lg_xorshift32(st);
+                        const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                        v = u16 >= thr ? v * dscale : 0.f;
+                    }
+                    hv[reg] = v;
+                    s = fmaf(v, w2v[reg], s);
+                }
+                if (hid_out && r < BP)
+                    st4(hid_out + (static_cast<uint32_t>(r) * HID + 32 * nh + 16 * i + 4 * q), hv);
+            }
+            s += __shfl_xor(s, 16);
+            s += __shfl_xor(s, 32);
+            if (q == 0) part[buf][nh][row] = s;
+        }
+        __syncthreads();  // image buf^1 complete, image buf free, partial logits of this tile posted
+        if (threadIdx.x < G::TR) {
+            const int64_t r = row0 + threadIdx.x;
+            const float(&pp)[4][G::TR] = part[buf];
+            const float tot = (pp[0][threadIdx.x] + pp[1][threadIdx.x]) + (pp[2][threadIdx.x] + pp[3][threadIdx.x]);
             if (r < BP) logit[lg_row_index(r, fdP, ldo)] = tot + bias2;
         }
-        __syncthreads();
+    };
+    for (int64_t tile = t0; tile < ntiles; tile += 2 * step) {
+        body(tile, 0, pu0, pv0);
+        if (tile + step < ntiles) body(tile + step, 1, pu1, pv1);
     }
 }
 
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
 template <int D>
-__global__ void __launch_bounds__(64 * NW)
+__global__ void __launch_bounds__(NT)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
-           const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ dlogit, int64_t ldo,
-           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, int64_t sb, int64_t sn,
-           lg_fastdiv fdP,
-           int64_t BP, int64_t ntiles, int dropout, float p_drop, float dscale, uint64_t seed, uint32_t salt) {
+           const float* __restrict__ W2, const float* __restrict__ hid, const float* __restrict__ dlogit, int64_t ldo,
+           float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, uint32_t sb,
+           uint32_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, float dscale) {
     using G = EG<D>;
-    constexpr int HS = HID + 4;
     constexpr int SL = HID * G::K3 + 2 * HID + 1;
-    __shared__ __attribute__((aligned(16))) float ft[TR * G::FS];
-    __shared__ __attribute__((aligned(16))) float dh[TR * HS];  // dhid[row][n]
-    __shared__ __attribute__((aligned(16))) float red[(G::NSPLIT - 1) * G::DT][64][12];  // dfeat partials
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    // dfeat: wave w handles k-triple kt = w % DT (k-tiles kt, kt+DT, kt+2DT = the u, v, |u-v|
-    // columns of the same node feature) over hidden slice hh = w / DT; partials meet in LDS.
-    const int kt = w % G::DT, hh = w / G::DT;
-    float aw[G::KS];
-#pragma unroll
-    for (int ks = 0; ks < G::KS; ++ks) aw[ks] = W1[(16 * w + j) * G::K3 + fk(ks, q)];
-    float wt[3][G::KPER];  // W1^T fragments: A[k = 16*(kt + s3*DT) + j][n = fk(hh*KPER + ks, q)]
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);     // [3][TR][FTB]  feat parts
+    uint16_t* gimg = fimg + 3 * G::FTPL;                     // [3][TR][GSB]  g parts
+    int8_t* sgn = reinterpret_cast<int8_t*>(gimg + 3 * G::GPL);  // [2][TR][D]  sign(h_u - h_v), by tile parity
+    f32x4* red = reinterpret_cast<f32x4*>(sgn + 2 * G::TR * D);  // [2][NROLE][3][64] dfeat partials
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int tq = (lane >> 2) & 3, tp = lane & 3;  // transposed-read address slot of this lane
+    // dfeat roles: features 16 kt + [0,16) of u, v, |u-v|, hidden half hh, row group rg
+    const int kt = w % G::DT, hh = (w / G::DT) & 1, rg = w / (2 * G::DT);
+    // A operand of dfeat^T = W1^T g^T: A[k = 16(kt + DT s3) + c][n = 64hh + 32ks + 8q + j] = W1[n][k]
+    lg_bf16x8 wt[3][2][3];
 #pragma unroll
     for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
-        for (int ks = 0; ks < G::KPER; ++ks)
-            wt[s3][ks] = W1[fk(hh * G::KPER + ks, q) * G::K3 + 16 * (kt + s3 * G::DT) + j];
-    f32x4 b1v, w2v;
+        for (int ks = 0; ks < 2; ++ks) {
+            f32x4 x0, x1;
+            const float* src = W1 + (64 * hh + 32 * ks + 8 * q) * G::K3 + 16 * (kt + G::DT * s3) + c;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        b1v[reg] = b1[16 * w + 4 * q + reg];
-        w2v[reg] = W2[16 * w + 4 * q + reg];
-    }
-    f32x4 dwt[G::MT];
+            for (int j = 0; j < 4; ++j) {
+                x0[j] = src[j * G::K3];
+                x1[j] = src[(j + 4) * G::K3];
+            }
+            split3_x8(x0, x1, wt[s3][ks][0], wt[s3][ks][1], wt[s3][ks][2]);
+        }
+    const int arow = threadIdx.x / G::F4, af = threadIdx.x % G::F4;  // feature gather slot
+    const int n4 = threadIdx.x & 31, hrow = threadIdx.x >> 5;        // hidden slot: rows hrow + 16 i
+    const f32x4 w2g = ld4(W2 + 4 * n4);
+    f32x4 dwa[G::KT];
 #pragma unroll
-    for (int mt = 0; mt < G::MT; ++mt) dwt[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 dw2 = f32x4{0.f, 0.f, 0.f, 0.f}, db1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < G::KT; ++i) dwa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dw2a = f32x4{0.f, 0.f, 0.f, 0.f}, db1a = dw2a;
     double db2 = 0.0;  // sum of all dlogits: heavy cancellation, kept in fp64 end to end
-    const uint32_t key = lg_dropout_key(seed, salt);
 
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t row0 = tile * TR;
-        gather_tile<D>(ends, h, ft, row0, BP, fdP, sb, sn);
-        const bool rv = row0 + j < BP;
-        const float dl = rv ? dlogit[lg_row_index(row0 + j, fdP, ldo)] : 0.f;
-        __syncthreads();
-        const f32x4 acc = hidden_tile<D>(ft, aw, b1v, j, q);
+    const int64_t step = gridDim.x;
+    int64_t tile = blockIdx.x;
+    uint32_t nu, nv;
+    f32x4 pu, pv, hp[G::HPT];
+    float dl[G::HPT];
+    auto load_hid = [&](int64_t t) {
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int n = 16 * w + 4 * q + reg;
-            const float pre = acc[reg];
-            float m = pre > 0.f ? 1.f : 0.f;
-            if (dropout) m = lg_keep(key, (row0 + j) * HID + n, p_drop) ? m * dscale : 0.f;
-            dw2[reg] = fmaf(dl, pre * m, dw2[reg]);
-            const float g = dl * w2v[reg] * m;
-            db1[reg] += g;
-            dh[j * HS + n] = g;
+        for (int i = 0; i < G::HPT; ++i) {
+            const int64_t r = t * G::TR + hrow + 16 * i;
+            hp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            dl[i] = 0.f;
+            if (r < BP) {
+                hp[i] = ld4(hid + (static_cast<uint32_t>(r) * HID + 4 * n4));
+                dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
+            }
         }
-        if (w == 0 && q == 0) db2 += static_cast<double>(dl);
-        __syncthreads();
-        // dW1^T[k][n] += sum_rows feat[row][k] * dhid[row][n]   (rows = 4q + kk)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int row = 4 * q + kk;
-            const float bv = dh[row * HS + 16 * w + j];
-#pragma unroll
-            for (int mt = 0; mt < G::MT; ++mt) dwt[mt] = mfma(feat1<D>(ft, row, 16 * mt + j), bv, dwt[mt]);
-        }
+    };
+    load_ends(ends, tile * G::TR + arow, BP, fdP, nu, nv);
+    load_rows<D>(h, tile * G::TR + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
+    load_hid(tile);
+    load_ends(ends, (tile + step) * G::TR + arow, BP, fdP, nu, nv);
+    int buf = 0;
+    for (; tile < ntiles; tile += step, buf ^= 1) {
+        const int64_t row0 = tile * G::TR;
+        int8_t* sgnb = sgn + buf * G::TR * D;
         {
-            // dfeat^T[k][row] = sum_n W1[n][k] dhid[row][n] over this wave's hidden slice
-            f32x4 cu = f32x4{0.f, 0.f, 0.f, 0.f}, cv = cu, ca = cu;
+            f32x4 a;
+            uint32_t sw = 0;
 #pragma unroll
-            for (int a = 0; a < G::KPER / 4; ++a) {
-                const f32x4 g4 = ld4(dh + j * HS + 16 * (hh * G::KPER / 4 + a) + 4 * q);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    cu = mfma(wt[0][4 * a + i], g4[i], cu);
-                    cv = mfma(wt[1][4 * a + i], g4[i], cv);
-                    ca = mfma(wt[2][4 * a + i], g4[i], ca);
-                }
+            for (int i = 0; i < 4; ++i) {
+                const float d = pu[i] - pv[i];
+                a[i] = fabsf(d);
+                sw |= static_cast<uint32_t>(static_cast<uint8_t>(d > 0.f ? 1 : (d < 0.f ? -1 : 0))) << (8 * i);
             }
-            if (hh > 0) {
-                float* rp = &red[(hh - 1) * G::DT + kt][lane][0];
-                st4(rp, cu);
-                st4(rp + 4, cv);
-                st4(rp + 8, ca);
-            }
-            __syncthreads();
-            if (hh == 0) {
+            st_split4(fimg, G::FTPL, arow * G::FTB + 4 * af, pu);
+            st_split4(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv);
+            st_split4(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a);
+            *reinterpret_cast<uint32_t*>(sgnb + arow * D + 4 * af) = sw;
+        }
 #pragma unroll
-                for (int o = 1; o < G::NSPLIT; ++o) {  // fixed order -> deterministic
-                    const float* rp = &red[(o - 1) * G::DT + kt][lane][0];
-                    cu += ld4(rp);
-                    cv += ld4(rp + 4);
-                    ca += ld4(rp + 8);
-                }
-                if (rv) {
-                    const int ku = 16 * kt + 4 * q;
-                    const f32x4 u = ld4(ft + j * G::FS + ku), v = ld4(ft + j * G::FS + D + ku);
-                    f32x4 du, dv;
+        for (int i = 0; i < G::HPT; ++i) {
+            f32x4 g;
 #pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) {
-                        const float d = u[reg] - v[reg];
-                        const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-                        du[reg] = cu[reg] + sg * ca[reg];
-                        dv[reg] = cv[reg] - sg * ca[reg];
-                    }
-                    float* o = dpipe + (row0 + j) * 2 * D + ku;
-                    st4(o, du);
-                    st4(o + D, dv);
-                }
+            for (int j = 0; j < 4; ++j) {
+                g[j] = hp[i][j] > 0.f ? dl[i] * w2g[j] * dscale : 0.f;
+                dw2a[j] = fmaf(dl[i], hp[i][j], dw2a[j]);
+                db1a[j] += g[j];
             }
+            if (n4 == 0) db2 += static_cast<double>(dl[i]);
+            st_split4(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
         }
         __syncthreads();
+        load_rows<D>(h, (tile + step) * G::TR + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
+        load_hid(tile + step);
+        load_ends(ends, (tile + 2 * step) * G::TR + arow, BP, fdP, nu, nv);
+
+        // dW1[n][k] += sum_rows g[row][n] feat[row][k]: n-tile w, every k-tile; the k (= row)
+        // order inside a step is 4q + (j & 3) + 16 (j >> 2) in both operands
+#pragma unroll
+        for (int ks = 0; ks < G::TR / 32; ++ks) {
+            const int r0 = 32 * ks + 4 * q + tq;
+            lg_bf16x8 ga[3];
+#pragma unroll
+            for (int pp = 0; pp < 3; ++pp) {
+                const uint16_t* src = gimg + pp * G::GPL + r0 * G::GSB + 16 * w + 4 * tp;
+                ga[pp] = lds_frag_tr16(src, src + 16 * G::GSB);
+            }
+#pragma unroll
+            for (int t = 0; t < G::KT; ++t) {
+                lg_bf16x8 fb[3];
+#pragma unroll
+                for (int pp = 0; pp < 3; ++pp) {
+                    const uint16_t* src = fimg + pp * G::FTPL + r0 * G::FTB + 16 * t + 4 * tp;
+                    fb[pp] = lds_frag_tr16(src, src + 16 * G::FTB);
+                }
+                dwa[t] = mfma_split(ga, fb, dwa[t]);
+            }
+        }
+        // dfeat^T[k][row] = sum_n W1[n][k] g[row][n] over this wave's hidden half; partial
+        // blocks role = (rg, kt, rbw) of both halves go to LDS
+#pragma unroll
+        for (int rbw = 0; rbw < G::RBW; ++rbw) {
+            const int rowb = 16 * (rg * G::RBW + rbw);
+            f32x4 cacc[3] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const uint16_t* src = gimg + (rowb + c) * G::GSB + 64 * hh + 32 * ks + 8 * q;
+                const lg_bf16x8 gb[3] = {lds_frag_row(src), lds_frag_row(src + G::GPL), lds_frag_row(src + 2 * G::GPL)};
+#pragma unroll
+                for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_split(wt[s3][ks], gb, cacc[s3]);
+            }
+            const int role = (rg * G::DT + kt) * G::RBW + rbw;
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3) red[((hh * G::NROLE + role) * 3 + s3) * 64 + lane] = cacc[s3];
+        }
+        __syncthreads();
+        {
+            // wave w finishes output block role = w: halves added in a fixed order
+            const int rbw = w % G::RBW, kt2 = (w / G::RBW) % G::DT, rg2 = w / (G::RBW * G::DT);
+            const int row = 16 * (rg2 * G::RBW + rbw) + c;
+            const int64_t r = row0 + row;
+            const f32x4* r0p = red + (w * 3) * 64 + lane;
+            const f32x4* r1p = red + ((G::NROLE + w) * 3) * 64 + lane;
+            const f32x4 cu = r0p[0] + r1p[0], cv = r0p[64] + r1p[64], ca = r0p[128] + r1p[128];
+            const int ku = 16 * kt2 + 4 * q;
+            const uint32_t sw = *reinterpret_cast<const uint32_t*>(sgnb + row * D + ku);
+            if (r < BP) {
+                f32x4 du, dv;
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {
+                    const float sg = static_cast<float>(static_cast<int8_t>(sw >> (8 * reg)));
+                    du[reg] = cu[reg] + sg * ca[reg];
+                    dv[reg] = cv[reg] - sg * ca[reg];
+                }
+                float* o = dpipe + (static_cast<uint32_t>(r) * 2 * D + ku);
+                st4(o, du);
+                st4(o + D, dv);
+            }
+        }
     }
 
     float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
 #pragma unroll
-    for (int mt = 0; mt < G::MT; ++mt)
+    for (int t = 0; t < G::KT; ++t)
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) out[(16 * w + j) * G::K3 + 16 * mt + 4 * q + reg] = dwt[mt][reg];
+        for (int reg = 0; reg < 4; ++reg) out[(16 * w + 4 * q + reg) * G::K3 + 16 * t + c] = dwa[t][reg];
+    // db1 / dW2: lanes l and l + 32 share n4, then the eight waves in order; db2 likewise
 #pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            dw2[reg] += __shfl_xor(dw2[reg], off);
-            db1[reg] += __shfl_xor(db1[reg], off);
-        }
-        db2 += __shfl_xor(db2, off);
+    for (int j = 0; j < 4; ++j) {
+        dw2a[j] += __shfl_xor(dw2a[j], 32);
+        db1a[j] += __shfl_xor(db1a[j], 32);
     }
-    if (j == 0) {
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            out[HID * G::K3 + 16 * w + 4 * q + reg] = db1[reg];
-            out[HID * G::K3 + HID + 16 * w + 4 * q + reg] = dw2[reg];
-        }
+    db2 += __shfl_xor(db2, 32);
+    __syncthreads();  // the last tile's LDS readers are done: reuse the partials area
+    float* fin = reinterpret_cast<float*>(red);
+    double* find = reinterpret_cast<double*>(fin + NW * 32 * 8);
+    if (lane < 32) {
+        st4(fin + (w * 32 + lane) * 8, db1a);
+        st4(fin + (w * 32 + lane) * 8 + 4, dw2a);
     }
-    if (w == 0 && lane == 0) db2slab[blockIdx.x] = db2;
+    if (lane == 0) find[w] = db2;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        f32x4 a = ld4(fin + threadIdx.x * 8), b = ld4(fin + threadIdx.x * 8 + 4);
+#pragma unroll
+        for (int i = 1; i < NW; ++i) {
+            a += ld4(fin + (i * 32 + threadIdx.x) * 8);
+            b += ld4(fin + (i * 32 + threadIdx.x) * 8 + 4);
+        }
+        st4(out + HID * G::K3 + 4 * threadIdx.x, a);
+        st4(out + HID * G::K3 + HID + 4 * threadIdx.x, b);
+    }
+    if (threadIdx.x == 0) {
+        double s = find[0];
+        for (int i = 1; i < NW; ++i) s += find[i];
+        db2slab[blockIdx.x] = s;
+    }
 }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+int64_t tile_rows(int64_t D) { return 2048 / D; }
 int bwd_grid(int64_t ntiles) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ntiles, lg_num_cus()))); }
+
+template <typename Kern>
+bool allow_lds(Kern kernel, int64_t dyn) {
+    return dyn <= 64 * 1024 || hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   static_cast<int>(dyn)) == hipSuccess;
+}
 
 }  // namespace
 
 extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                                const float* w2, const float* b2, float* logits, int64_t ldo, int64_t B, int64_t N,
-                                int64_t P,
-                                int64_t D, int64_t hidden, int flags, float dropout_p, uint64_t seed, uint32_t salt,
-                                lg_stream_t stream) {
+                                const float* w2, const float* b2, float* logits, int64_t ldo, float* hid,
+                                int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden, int flags,
+                                float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
@@ -310,20 +476,30 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     const int64_t BP = B * P;
     if (BP == 0) return LG_OK;
     if (!ends || !h || !w1 || !b1 || !w2 || !b2 || !logits || ldo < P) return LG_EINVAL;
-    if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
+    if (BP * HID >= (int64_t{1} << 32) || N * B * D >= (int64_t{1} << 32)) return LG_EUNSUPPORTED;  // 32-bit offsets
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
     const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // h is [N][B][D] instead of [B][N][D]
     const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
-    const int64_t ntiles = cdiv(BP, TR);
-    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ntiles, 4LL * lg_num_cus()));
+    const int64_t ntiles = cdiv(BP, tile_rows(D));
+    // persistent grid sized to residency (tiles are dealt statically)
+    const int64_t per_cu = D == 64 ? EG<64>::FWD_WG_PER_CU : EG<32>::FWD_WG_PER_CU;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ntiles, per_cu * lg_num_cus()));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
-    if (D == 64)
-        k_edge_fwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, sb, sn, fdP, BP, ntiles, dropout, dropout_p,
-                                                scale, seed, salt);
-    else
-        k_edge_fwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, sb, sn, fdP, BP, ntiles, dropout, dropout_p,
-                                                scale, seed, salt);
+#ifdef LG_KERNEL_LAB
+    const int dropout_arg = dropout | (((flags >> 28) & 7) << 8);
+#else
+    const int dropout_arg = dropout;
+#endif
+    if (D == 64) {
+        if (!allow_lds(k_edge_fwd<64>, EG<64>::FWD_LDS)) return LG_EHIP;
+        k_edge_fwd<64><<<grid, NT, EG<64>::FWD_LDS, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
+                                                         ntiles, dropout_arg, dropout_p, scale, seed, salt);
+    } else {
+        if (!allow_lds(k_edge_fwd<32>, EG<32>::FWD_LDS)) return LG_EHIP;
+        k_edge_fwd<32><<<grid, NT, EG<32>::FWD_LDS, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
+                                                         ntiles, dropout_arg, dropout_p, scale, seed, salt);
+    }
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
@@ -331,28 +507,26 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden) {
     if (B < 0 || P < 0 || hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int64_t SL = HID * 3 * D + 2 * HID + 1;
-    const int64_t G = bwd_grid(cdiv(std::max<int64_t>(B * P, 1), TR));
+    const int64_t G = bwd_grid(cdiv(std::max<int64_t>(B * P, 1), tile_rows(D)));
     return ((G * SL * 4 + 255) & ~int64_t(255)) + G * 8;
 }
 
-extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
-                                const float* w2, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
-                                float* db1,
-                                float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
-                                int flags, float dropout_p, uint64_t seed, uint32_t salt, void* workspace,
-                                lg_stream_t stream) {
+extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                                const float* hid, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
+                                float* db1, float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D,
+                                int64_t hidden, int flags, float dropout_p, void* workspace, lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
     if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
-    if (!h || !w1 || !b1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !workspace) return LG_EINVAL;
+    if (!h || !w1 || !w2 || !dw1 || !db1 || !dw2 || !db2 || !workspace) return LG_EINVAL;
     const int64_t BP = B * P;
-    if (BP > 0 && (!ends || !dlogits || !dpipe || ldo < P)) return LG_EINVAL;
-    if (BP >= kLgMaxRows) return LG_EUNSUPPORTED;
+    if (BP > 0 && (!ends || !hid || !dlogits || !dpipe || ldo < P)) return LG_EINVAL;
+    if (BP * HID >= (int64_t{1} << 32) || N * B * D >= (int64_t{1} << 32)) return LG_EUNSUPPORTED;  // 32-bit offsets
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(std::max<int64_t>(P, 1)));
     const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // h is [N][B][D] instead of [B][N][D]
     const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
-    const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), TR);
+    const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), tile_rows(D));
     const int grid = bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const int64_t SL = HID * 3 * D + 2 * HID + 1;
@@ -363,11 +537,15 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else if (D == 64) {
-        k_edge_bwd<64><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP, ntiles, dropout,
-                                                dropout_p, scale, seed, salt);
+        constexpr int64_t lds = EG<64>::BWD_LDS;
+        if (!allow_lds(k_edge_bwd<64>, lds)) return LG_EHIP;
+        k_edge_bwd<64><<<grid, NT, lds, s>>>(ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
+                                             ntiles, scale);
     } else {
-        k_edge_bwd<32><<<grid, 64 * NW, 0, s>>>(ends, h, w1, b1, w2, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP, ntiles, dropout,
-                                                dropout_p, scale, seed, salt);
+        constexpr int64_t lds = EG<32>::BWD_LDS;
+        if (!allow_lds(k_edge_bwd<32>, lds)) return LG_EHIP;
+        k_edge_bwd<32><<<grid, NT, lds, s>>>(ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
+                                             ntiles, scale);
     }
     LG_RET_IF_LAUNCH_FAILED();
     const int64_t K3 = 3 * D;

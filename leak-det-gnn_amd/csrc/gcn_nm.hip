@@ -24,6 +24,7 @@
 #include <algorithm>
 #include "common.h"
 #include "reduce.h"
+#include "split_bf16.h"
 
 namespace {
 
@@ -245,42 +246,7 @@ k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
 // are loaded in place, two at a time.  Accumulation order = CSR order in both kernels.
 constexpr int kNm2Waves = 4;
 
-// ---- 3-way bf16 split of fp32 operands (SPLIT transform) --------------------------------
-// x = x0 + x1 + x2 with x_i = bf16_rne(x - x0 - ... ): |x - (x0 + x1 + x2)| <= 2^-24 |x|.
-// A product x w is then sum_{i+j<=2} x_i w_j (6 bf16 MFMAs, each product exact in fp32,
-// fp32 accumulate); the dropped terms are <= 2^-24 |x w|: fp32-level accuracy at 6/16 of
-// the f32-MFMA issue time (v_mfma_f32_16x16x32_bf16: 16 cyc per 16x16x32 vs 32 cyc per
-// 16x16x4 for v_mfma_f32_16x16x4_f32).
-typedef __bf16 lg_bf16x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 lg_bf16x8 __attribute__((ext_vector_type(8)));
-typedef float lg_f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t lg_u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-    const lg_f32x2 v = {a, b};
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_bf16x2));
-}
-__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
-// 8 floats (two f32x4) -> three bf16x8 fragments (hi, mid, lo)
-__device__ __forceinline__ void split3_x8(const f32x4& u, const f32x4& v, lg_bf16x8& f0, lg_bf16x8& f1,
-                                          lg_bf16x8& f2) {
-    lg_u32x4 p0, p1, p2;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const float a = h < 2 ? u[2 * h] : v[2 * h - 4], b = h < 2 ? u[2 * h + 1] : v[2 * h - 3];
-        p0[h] = pk_bf16(a, b);
-        const float ra = a - bf_lo(p0[h]), rb = b - bf_hi(p0[h]);
-        p1[h] = pk_bf16(ra, rb);
-        p2[h] = pk_bf16(ra - bf_lo(p1[h]), rb - bf_hi(p1[h]));
-    }
-    f0 = __builtin_bit_cast(lg_bf16x8, p0);
-    f1 = __builtin_bit_cast(lg_bf16x8, p1);
-    f2 = __builtin_bit_cast(lg_bf16x8, p2);
-}
-__device__ __forceinline__ f32x4 mfma_bf(const lg_bf16x8& a, const lg_bf16x8& b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
+// ---- 3-way bf16 split of fp32 operands (SPLIT transform): split_bf16.h ----------------
 
 // LAB (kernel-lab builds only, -DLG_KERNEL_LAB; results are WRONG when set): 1 = skip the
 // MFMA transform, 2 = skip the neighbour loads — the memory-only and compute-only floors.

@@ -1,0 +1,87 @@
+// 3-way bf16 split of fp32 operands for bf16 MFMA at fp32-level accuracy (gfx950).
+//
+// x = x0 + x1 + x2 with x_i = bf16_rne(x - x0 - ...): |x - (x0 + x1 + x2)| <= 2^-24 |x|.
+// A product x w is then sum_{i+j<=2} x_i w_j (6 bf16 MFMAs, each product exact in fp32,
+// fp32 accumulate); the dropped terms are <= 2^-24 |x w|: fp32-level accuracy at 6/16 of
+// the f32-MFMA issue time (v_mfma_f32_16x16x32_bf16: 16 cyc per 16x16x32 vs 32 cyc per
+// 16x16x4 for v_mfma_f32_16x16x4_f32, i.e. 96 vs 256 cycles per K = 32).
+#pragma once
+#include "common.h"
+
+typedef __bf16 lg_bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lg_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float lg_f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t lg_u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t lg_u32x4 __attribute__((ext_vector_type(4)));
+typedef short lg_i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const lg_f32x2 v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_bf16x2));
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+
+// one pair of floats -> (hi, mid, lo) packed bf16 pairs
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+    p0 = pk_bf16(a, b);
+    const float ra = a - bf_lo(p0), rb = b - bf_hi(p0);
+    p1 = pk_bf16(ra, rb);
+    p2 = pk_bf16(ra - bf_lo(p1), rb - bf_hi(p1));
+}
+// 4 floats -> three 4 x bf16 parts (8 bytes each)
+__device__ __forceinline__ void split3_x4(const f32x4& u, lg_u32x2& f0, lg_u32x2& f1, lg_u32x2& f2) {
+    uint32_t a0, a1, a2, b0, b1, b2;
+    split3_pair(u[0], u[1], a0, a1, a2);
+    split3_pair(u[2], u[3], b0, b1, b2);
+    f0 = lg_u32x2{a0, b0};
+    f1 = lg_u32x2{a1, b1};
+    f2 = lg_u32x2{a2, b2};
+}
+// 8 floats (two f32x4) -> three bf16x8 fragments (hi, mid, lo)
+__device__ __forceinline__ void split3_x8(const f32x4& u, const f32x4& v, lg_bf16x8& f0, lg_bf16x8& f1,
+                                          lg_bf16x8& f2) {
+    lg_u32x4 p0, p1, p2;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const float a = h < 2 ? u[2 * h] : v[2 * h - 4], b = h < 2 ? u[2 * h + 1] : v[2 * h - 3];
+        uint32_t x0, x1, x2;
+        split3_pair(a, b, x0, x1, x2);
+        p0[h] = x0;
+        p1[h] = x1;
+        p2[h] = x2;
+    }
+    f0 = __builtin_bit_cast(lg_bf16x8, p0);
+    f1 = __builtin_bit_cast(lg_bf16x8, p1);
+    f2 = __builtin_bit_cast(lg_bf16x8, p2);
+}
+__device__ __forceinline__ f32x4 mfma_bf(const lg_bf16x8& a, const lg_bf16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// acc += a * b on split operands: the six terms with i + j <= 2, smallest first
+__device__ __forceinline__ f32x4 mfma_split(const lg_bf16x8 (&a)[3], const lg_bf16x8 (&b)[3], f32x4 c) {
+    c = mfma_bf(a[2], b[0], c);
+    c = mfma_bf(a[1], b[1], c);
+    c = mfma_bf(a[0], b[2], c);
+    c = mfma_bf(a[1], b[0], c);
+    c = mfma_bf(a[0], b[1], c);
+    return mfma_bf(a[0], b[0], c);
+}
+
+// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, columns 4p..4p+3
+// of a 4 x 16 block of 16-bit elements; lane i of the group receives column i (row q in
+// element q).  EXEC must be all ones.  p must be 8-byte aligned.
+__device__ __forceinline__ lg_u32x2 lds_read_tr16(const uint16_t* p) {
+    typedef __attribute__((address_space(3))) lg_i16x4 lds_i16x4;
+    const lg_i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p));
+    return __builtin_bit_cast(lg_u32x2, v);
+}
+// two transposed 4-row reads -> one bf16x8 fragment (elements 0..3 from r0, 4..7 from r1)
+__device__ __forceinline__ lg_bf16x8 lds_frag_tr16(const uint16_t* r0, const uint16_t* r1) {
+    const lg_u32x2 a = lds_read_tr16(r0), b = lds_read_tr16(r1);
+    const lg_u32x4 v = {a[0], a[1], b[0], b[1]};
+    return __builtin_bit_cast(lg_bf16x8, v);
+}
+__device__ __forceinline__ lg_bf16x8 lds_frag_row(const uint16_t* p) {
+    return *reinterpret_cast<const lg_bf16x8*>(p);
+}

@@ -449,9 +449,13 @@ class HeadsFn(torch.autograd.Function):
         pooled = torch.empty(B, D, device=h.device, dtype=torch.float32)
         hid = torch.empty(B, nhidden, device=h.device, dtype=torch.float32)
         w1c, w2c, nw1c, nw2c = w1.contiguous(), w2.contiguous(), nw1.contiguous(), nw2.contiguous()
+        # the EdgeHead hidden layer is kept for the backward (no recompute) when any grad is needed
+        keep = any(ctx.needs_input_grad[1:])
+        ehid = torch.empty(B * P, hidden, device=h.device, dtype=torch.float32) if keep else None
         with _timed("edge_fwd", h.device):
             check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits),
-                                       P + 1, B, N, P, D, hidden, fe | lay, pe, seed, EDGE_HEAD_SALT, st),
+                                       P + 1, ptr(ehid) if keep else None, B, N, P, D, hidden, fe | lay, pe, seed,
+                                       EDGE_HEAD_SALT, st),
                   "lg_edge_head_fwd")
         with _timed("pool_head", h.device):
             check(lib.lg_pool_head_fwd(ptr(h), ptr(nw1c), ptr(nb1), ptr(nw2c), ptr(nb2), ptr(pooled), ptr(hid),
@@ -459,13 +463,13 @@ class HeadsFn(torch.autograd.Function):
                                        st),
                   "lg_pool_head_fwd")
         ctx.cfg, ctx.drop = cfg, (pe, fe, pn, fn, seed)
-        ctx.save_for_backward(h, w1c, b1, w2c, pooled, hid, nw1c, nw2c)
+        ctx.save_for_backward(h, w1c, w2c, ehid, pooled, hid, nw1c, nw2c)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         lib = load_library()
-        h, w1, b1, w2, pooled, hid, nw1, nw2 = ctx.saved_tensors
+        h, w1, w2, ehid, pooled, hid, nw1, nw2 = ctx.saved_tensors
         pe, fe, pn, fn, seed = ctx.drop
         inc = ctx.cfg.inc
         nm = bool(ctx.cfg.node_major)
@@ -476,13 +480,13 @@ class HeadsFn(torch.autograd.Function):
         st = stream_of(h)
         dl = dlogits.contiguous()
         dpipe = torch.empty(B, P, 2, D, device=dev)
-        dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
+        dw1, db1 = torch.empty_like(w1), torch.empty(hidden, device=dev)
         dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
         ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
         with _timed("edge_bwd", dev):
-            check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(dl), P + 1, ptr(dpipe),
-                                       ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe | lay, pe, seed,
-                                       EDGE_HEAD_SALT, ptr(ws), st), "lg_edge_head_bwd")
+            check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
+                                       ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe | lay, pe,
+                                       ptr(ws), st), "lg_edge_head_bwd")
         dpooled = torch.empty(B, D, device=dev)
         ndw1, ndb1 = torch.empty_like(nw1), torch.empty(nhidden, device=dev)
         ndw2, ndb2 = torch.empty_like(nw2), torch.empty(1, device=dev)

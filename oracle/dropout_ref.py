@@ -82,3 +82,25 @@ def row_stream_mask(seed: int, salt: int, rows: np.ndarray, D: int, p: float) ->
             u16 = (s & np.uint64(0xFFFF)) if t % 2 == 0 else (s >> np.uint64(16))
             out[:, 16 * (t // 4) + 4 * q + (t % 4)] = u16 >= thr
     return out
+
+
+# ---- row-stream dropout of the fused EdgeHead forward (edge.hip k_edge_fwd) ----
+#   hidden block nh (units [32 nh, 32 nh + 32)) x lane group q of a row draws the stream
+#   row_stream_seed(key, row, 4 nh + q) and owns units 32 nh + 16 i + 4 q + reg in
+#   t = 4 i + reg order (i, reg < 2, 4); same xorshift / 16-bit-half rule as row_stream_mask.
+def edge_stream_mask(seed: int, salt: int, rows: np.ndarray, p: float, hidden: int = 128) -> np.ndarray:
+    """Keep mask [len(rows), hidden] of the EdgeHead hidden layer for the given pipe rows
+    (row = b * P + p)."""
+    key = dropout_key(seed, salt)
+    thr = np.uint64(keep_threshold16(p))
+    rows = np.asarray(rows, dtype=np.uint64).reshape(-1)
+    out = np.zeros((rows.size, hidden), dtype=bool)
+    for nh in range(hidden // 32):
+        for q in range(4):
+            s = row_stream_seed(key, rows, 4 * nh + q)
+            for t in range(8):
+                if t % 2 == 0:
+                    s = _xorshift32(s)
+                u16 = (s & np.uint64(0xFFFF)) if t % 2 == 0 else (s >> np.uint64(16))
+                out[:, 32 * nh + 16 * (t // 4) + 4 * q + (t % 4)] = u16 >= thr
+    return out

@@ -304,7 +304,9 @@ def test_detector_train_mode_replay_with_oracle_masks():
     mk = [_masks(seed_t, 0, (R, D), 0.1)] + [   # node init: per-element hash; GCN layers: row streams
         torch.from_numpy(row_stream_mask(seed_t, l, np.arange(R), D, 0.1).astype(np.float32)).to(DEV)
         for l in (1, 2)]
-    me = _masks(seed_h, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1)
+    from oracle.dropout_ref import edge_stream_mask
+    me = torch.from_numpy(edge_stream_mask(seed_h, ops.EDGE_HEAD_SALT, np.arange(B * P), 0.1)
+                          .astype(np.float32)).to(DEV)   # EdgeHead: row streams
     ei = torch.from_numpy(graph_ref.batchify(m.edge_index_single.numpy(), N, B))
     row, col, w = (t.to(DEV) for t in gcn_ref.gcn_norm(ei, R))
     h_s = m.sensor_encoder(r, tf)
@@ -440,12 +442,37 @@ def test_detector_node_major_matches_window_major(train, monkeypatch):
 def test_fused_heads_vs_torch(train, D, nm):
     """HeadsFn (fused EdgeHead, mean pool + NoLeakHead, one (B, P+1) output, incidence-reduced
     backward) vs float64 torch with the same dropout masks (oracle/dropout_ref.py)."""
+    _heads_case(train, D, nm, 5)
+
+
+@pytest.mark.parametrize("D", [64, 32])
+def test_fused_heads_multi_tile(D):
+    """B = 70 (53,480 pipe rows): every workgroup of both EdgeHead kernels runs several tiles
+    (prefetch pipeline, LDS buffer parity) and the last tile is ragged."""
+    _heads_case(True, D, True, 70)
+
+
+def test_edge_head_eval_without_hidden():
+    """No-grad forward passes hid = NULL (nothing kept for a backward); logits unchanged."""
+    from models.ops import HeadsConfig, HeadsFn, Incidence
+    g = load("graph_ltown_a.npz")
+    inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV)
+    gen = torch.Generator().manual_seed(3)
+    ps = [torch.randn(*s, generator=gen).to(DEV) / 8 for s in
+          ((4, 661, 64), (128, 192), (128,), (1, 128), (1,), (128, 64), (128,), (1, 128), (1,))]
+    a = HeadsFn.apply(HeadsConfig(inc, 0.1, False), *ps)
+    ps[1].requires_grad_(True)
+    b = HeadsFn.apply(HeadsConfig(inc, 0.1, False), *ps)
+    assert torch.equal(a, b.detach())
+
+
+def _heads_case(train, D, nm, B):
     from models import ops
     from models.ops import HeadsConfig, HeadsFn, Incidence
     g = load("graph_ltown_a.npz")
     ends = torch.from_numpy(g["pipe_ends"])
     inc = Incidence.build(ends, 661, DEV)
-    B, N, P = 5, 661, 764
+    N, P = 661, 764
     gen = torch.Generator().manual_seed(D + train)
     h = torch.randn(B, N, D, generator=gen)
     h[0, :40] = 0.25  # ties -> |h_u - h_v| = 0, sign 0
@@ -475,7 +502,9 @@ def test_fused_heads_vs_torch(train, D, nm):
     if train:
         torch.manual_seed(77)
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())
-        hid = hid * _masks(seed, ops.EDGE_HEAD_SALT, (B * P, 128), 0.1, dev="cpu").double().view(B, P, 128) / 0.9
+        from oracle.dropout_ref import edge_stream_mask
+        me = torch.from_numpy(edge_stream_mask(seed, ops.EDGE_HEAD_SALT, np.arange(B * P), 0.1))
+        hid = hid * me.double().view(B, P, 128) / 0.9
         nhid = nhid * _masks(seed, ops.NOLEAK_HEAD_SALT, (B, 128), 0.1, dev="cpu").double() / 0.9
     lr = torch.cat([(hid @ W2r.t()).squeeze(-1) + b2r, nhid @ V2r.t() + c2r], -1)
     (lr * dl.double()).sum().backward()

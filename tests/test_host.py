@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 6
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 7
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
     assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * (1532 + 661))
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1
@@ -127,8 +127,10 @@ def test_c_abi_host_only_calls():
     assert lib.lg_linear_dw(None, None, 7424, 64, 64, None, None, None, None) == -1
     assert lib.lg_pool_head_fwd(None, None, None, None, None, None, None, None, 765, 764, 2, 661, 64, 128, 0, 0.0, 0,
                                 102, None) == -1
-    assert lib.lg_edge_head_fwd(None, None, None, None, None, None, None, 764, 2, 661, 764, 64, 128, 0, 0.0, 0, 101,
-                                None) == -1
+    assert lib.lg_edge_head_fwd(None, None, None, None, None, None, None, 764, None, 2, 661, 764, 64, 128, 0, 0.0, 0,
+                                101, None) == -1
+    assert lib.lg_edge_head_bwd(None, None, None, None, None, None, 764, None, None, None, None, None, 2, 661, 764, 64,
+                                128, 0, 0.0, None, None) == -1
     # GRU: H in {32, 64}; the backward needs the saved gates; gates need h_seq
     assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 48) == -1
     assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 32) > 0

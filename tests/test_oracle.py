@@ -149,3 +149,40 @@ def test_row_stream_dropout_oracle_matches_scalar_restatement():
     # neighbouring channels / rows are not trivially correlated
     assert abs(np.corrcoef(big[:, 0], big[:, 1])[0, 1]) < 0.03
     assert abs(np.corrcoef(big[:-1, 5], big[1:, 5])[0, 1]) < 0.03
+
+
+def test_edge_stream_dropout_oracle_matches_scalar_restatement():
+    """oracle/dropout_ref.edge_stream_mask vs a scalar transcription of the EdgeHead
+    forward's stream (edge.hip: lg_row_stream_seed(key, row, 4 nh + q), units
+    32 nh + 16 i + 4 q + reg); and the keep rate."""
+    from oracle.dropout_ref import dropout_key, edge_stream_mask
+
+    def mix32(x):
+        x &= 0xFFFFFFFF
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & 0xFFFFFFFF
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & 0xFFFFFFFF
+        return x ^ (x >> 16)
+
+    seed, salt, p = 0x0F0E_0D0C_0B0A_0908, 101, 0.1
+    key = dropout_key(seed, salt)
+    rows = [0, 3, 764, 195583, (1 << 32) + 9]
+    got = edge_stream_mask(seed, salt, np.array(rows), p)
+    thr = int(round(p * 65536))
+    for ri, row in enumerate(rows):
+        for g in range(16):
+            nh, q = g // 4, g % 4
+            a = mix32(((row & 0xFFFFFFFF) * 0x9E3779B9) ^ key)
+            s = mix32(a ^ (((row >> 32) * 0x85EBCA6B) & 0xFFFFFFFF) ^ ((g * 0x632BE5AB) & 0xFFFFFFFF)) or 0x6D2B79F5
+            for t in range(8):
+                if t % 2 == 0:
+                    s ^= (s << 13) & 0xFFFFFFFF
+                    s ^= s >> 17
+                    s ^= (s << 5) & 0xFFFFFFFF
+                u16 = s & 0xFFFF if t % 2 == 0 else s >> 16
+                assert got[ri, 32 * nh + 16 * (t // 4) + 4 * q + t % 4] == (u16 >= thr)
+    big = edge_stream_mask(5, 101, np.arange(20000), p)
+    assert abs(big.mean() - 0.9) < 0.003
+    assert abs(np.corrcoef(big[:, 0], big[:, 1])[0, 1]) < 0.03
+    assert abs(np.corrcoef(big[:, 3], big[:, 35])[0, 1]) < 0.03

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--B", type=int, default=256)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
+    ap.add_argument("--edgelab", default="", help="comma list of lg_edge_head_fwd lab bits (1 nomfma, 2 noload, "
+                                                   "4 nosplit; LEAKGNN_LIB=lib/lab build only)")
     ap.add_argument("--nmlab", default="", help="comma list of lg_gcn_fwd_nm schedules: v1 or bpc<n> (train mode)")
     args = ap.parse_args()
     lib = nat.load_library()
@@ -128,21 +130,31 @@ def main():
         W2 = torch.randn(1, 128, device=dev) / 8
         b2 = torch.randn(1, device=dev)
         lo = torch.empty(B, P, device=dev)
+        hid = torch.empty(B * P, 128, device=dev)
+        f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), P,
+                                               ptr(hid), B, N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, st), "edge fwd")
         if "edge_fwd" in which:
-            f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), P, B,
-                                                   N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, st), "edge fwd")
             t = timeit(f, args.iters)
             res["edge_fwd"] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
+            labs = [(f"edge_fwd_eval_lab{v}", v << 28, None) for v in (int(x) for x in args.edgelab.split(",") if x)]
+            for name, fl, hp in [("edge_fwd_nohid", nat.LG_F_DROPOUT, None), ("edge_fwd_eval", 0, None)] + labs:
+                g = lambda fl=fl, hp=hp: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2),
+                                                                    ptr(b2), ptr(lo), P, hp, B, N, P, D, 128, fl, 0.1,
+                                                                    5, 101, st), name)
+                t = timeit(g, args.iters)
+                res[name] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
+        else:
+            f()
         if "edge_bwd" in which:
             dl = torch.randn(B, P, device=dev)
             dpipe = torch.empty(B, P, 2, D, device=dev)
             dW1, db1, dW2, db2 = (torch.empty_like(t) for t in (W1, b1, W2, b2))
             ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=dev, dtype=torch.uint8)
-            f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(dl), P,
+            f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(W2), ptr(hid), ptr(dl), P,
                                                    ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
-                                                   nat.LG_F_DROPOUT, 0.1, 5, 101, ptr(ws), st), "edge bwd")
+                                                   nat.LG_F_DROPOUT, 0.1, ptr(ws), st), "edge bwd")
             t = timeit(f, args.iters)
-            res["edge_bwd"] = {"us": t, "TFLOPs": 3 * 2 * B * P * 3 * D * 128 / t / 1e6}
+            res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
     if "gru_fwd" in which or "gru_bwd" in which:
         S, L = 29, 36
         r = torch.randn(B, L, S, device=dev)
