@@ -255,6 +255,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--eager", action="store_true", help="launch the step eagerly instead of replaying its HIP graph")
     args = ap.parse_args()
 
     from models import ops
@@ -270,8 +271,9 @@ def main() -> None:
     torch.manual_seed(0)
     model = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
                          use_time=True).to(dev).train()
-    # fused=True: one multi-tensor launch for the whole update (same AdamW math as the reference's)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, fused=True)
+    # fused=True: one multi-tensor launch for the whole update (same AdamW math as the reference's);
+    # capturable=True: device-side step counters, so the update can live inside the step graph
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
     allreduce = GradAllReduce(model.parameters())
     N = len(model.node_names)
     E1 = int(model.edge_index_single.shape[1]) + N  # E' = E + N self loops
@@ -294,6 +296,11 @@ def main() -> None:
 
     for _ in range(args.warmup):
         step()
+    eager_step = step
+    if not args.eager:
+        # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay)
+        from models.graph_step import CapturedTrainStep
+        step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=1.0, warmup=3)
     timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "gru_fwd", "gru_bwd", "edge_fwd", "edge_bwd",
                              "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)
@@ -314,10 +321,11 @@ def main() -> None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    # pass 2: per-kernel HIP-event durations over the same number of steps
+    # pass 2: per-kernel HIP-event durations over the same number of steps (eager launches:
+    # the events bracket each library call on its stream)
     timer.enabled = True
     for _ in range(args.steps):
-        step()
+        eager_step()
     barrier()
     timer.enabled = False
     kms = {k: timer.mean_ms(k) for k in timer.names}
@@ -346,7 +354,8 @@ def main() -> None:
         "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",
                    "nodes": N, "edge_columns": E1 - N, "pipes": P, "windows_per_rank": B,
                    "global_batch": B * world, "feat": D, "gnn_layers": 2, "parallelism": f"dp{world}",
-                   "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode"},
+                   "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode",
+                   "launch": "eager" if args.eager else "hipgraph (one replay per step, dropout re-drawn on device)"},
         "roofline": {"kernel": ("lg_gcn_fwd_nm" if ops.TRUNK_NODE_MAJOR else "lg_gcn_fwd")
                      + " (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -59,6 +59,11 @@ enum {
  * node-major [N][B][D] (row n*B + b), the layout of lg_gcn_fwd_nm / lg_gcn_bwd_nm.
  * Dropout masks are indexed by the window-major row in both layouts. */
 #define LG_F_NODE_MAJOR 0x20
+/* Dropout seeds: every forward entry point taking (seed, salt) reads `seed` as the address
+ * of a device-resident uint64 when salt has bit 31 set (the salt proper is bits 0..30).  A
+ * captured HIP graph of a training step then re-draws its dropout streams on each replay by
+ * refreshing that word on the device, with no host involvement. */
+#define LG_SALT_SEED_PTR 0x80000000u
 /* Tuning bits of lg_gcn_fwd_nm (kernel lab, tools/kbench.py): they pick a schedule and never
  * change results.  LG_F_LAB_V1: the one-tile-per-wave kernel; bits 24..27: workgroups of
  * 4 waves per CU for the software-pipelined kernel (0 = default). */

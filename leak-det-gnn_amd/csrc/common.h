@@ -41,6 +41,15 @@ __host__ __device__ __forceinline__ uint32_t lg_dropout_key(uint64_t seed, uint3
     return lg_mix32(static_cast<uint32_t>(seed) ^ lg_mix32(static_cast<uint32_t>(seed >> 32) ^ (salt * 0x9E3779B9U)));
 }
 
+// Salt bit 31 (LG_SALT_SEED_PTR, include/leakgnn.h): `seed` is then the device address of
+// the uint64 seed, read at launch — a captured HIP graph re-draws its dropout streams on
+// every replay by refreshing that word on the device.
+constexpr uint32_t kLgSaltSeedPtr = 0x80000000u;
+__device__ __forceinline__ uint32_t lg_dropout_key_dev(uint64_t seed, uint32_t salt) {
+    if (salt & kLgSaltSeedPtr) seed = *reinterpret_cast<const uint64_t*>(seed);
+    return lg_dropout_key(seed, salt & ~kLgSaltSeedPtr);
+}
+
 __device__ __forceinline__ bool lg_keep(uint32_t key, uint64_t idx, float p) {
     const uint32_t h = lg_mix32((static_cast<uint32_t>(idx) * 0x9E3779B9U) ^ key ^
                                 (static_cast<uint32_t>(idx >> 32) * 0x85EBCA6BU));

@@ -143,7 +143,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         bw[HID + threadIdx.x] = W2[threadIdx.x];
     }
     const float bias2 = b2[0];
-    const uint32_t key = lg_dropout_key(seed, salt), thr = lg_keep_threshold16(p_drop);
+    const uint32_t key = lg_dropout_key_dev(seed, salt), thr = lg_keep_threshold16(p_drop);
     const int arow = threadIdx.x / G::F4, af = threadIdx.x % G::F4;  // gather slot of this thread
     const int64_t step = gridDim.x;
     // Software pipeline, one barrier per tile: while tile i's MFMAs run on feature image

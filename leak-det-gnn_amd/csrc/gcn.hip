@@ -343,7 +343,7 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     float* tl = tiles + wave * G::TILE;
-    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
 
     const TileRange tr = xcd_tiles(ntiles, wave, NW);
     f32x4 acc[G::K];

@@ -171,7 +171,7 @@ k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const int rl = lane / G::LPR, fg = lane % G::LPR;
     float* tl = tiles + wave * G::TILE;
-    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p_drop);
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
@@ -323,7 +323,7 @@ k_gcn_fwd_nm2(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const int rl = lane / G::LPR, fg = lane % G::LPR;
     float* tl = tiles + wave * G::TILE;
-    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p_drop);
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);

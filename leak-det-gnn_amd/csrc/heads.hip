@@ -20,7 +20,7 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
             float scale, uint64_t seed, uint32_t salt) {
     constexpr int LPR = D / 4, RPB = 256 / LPR;
     const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-    const uint32_t key = lg_dropout_key(seed, salt);
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
     for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
         const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
         const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;

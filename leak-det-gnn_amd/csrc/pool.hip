@@ -75,7 +75,7 @@ k_pool_head_fwd(const float* __restrict__ x, const float* __restrict__ W1, const
 #pragma unroll 8
         for (int d = 0; d < D; ++d) pre = fmaf(W1[t * D + d], pooled[d], pre);
         float v = fmaxf(pre, 0.f);
-        if constexpr (DROP) v = lg_dropout(v, p_drop, dscale, lg_dropout_key(seed, salt), b * kHid + t);
+        if constexpr (DROP) v = lg_dropout(v, p_drop, dscale, lg_dropout_key_dev(seed, salt), b * kHid + t);
         hid_out[b * kHid + t] = v;
         red[t] = v * w2[t];
     }

@@ -202,9 +202,45 @@ def batchify_edge_index(edge_index_single: torch.Tensor, num_nodes: int, batch_s
     return out
 
 
-def _new_seed() -> int:
-    # drawn from torch's CPU generator: reproducible under torch.manual_seed, no device sync
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())
+class SeedSlots:
+    """Device-resident dropout seeds for a captured HIP graph (include/leakgnn.h
+    LG_SALT_SEED_PTR).  While installed (use_device_seeds), every forward that needs a
+    dropout seed takes the next slot and passes its ADDRESS with salt bit 31 set; the
+    kernels read the seed at launch.  refresh(), captured at the head of the step, re-draws
+    all slots from torch's CUDA generator (graph-safe), so every replay gets new masks."""
+
+    def __init__(self, device, n: int = 16):
+        self.buf = torch.zeros(n, dtype=torch.int64, device=device)
+        self.n, self.i = n, 0
+
+    def refresh(self) -> None:
+        self.buf.random_(0, 2 ** 62)
+        self.i = 0
+
+    def take(self) -> int:
+        if self.i >= self.n:
+            raise RuntimeError(f"more than {self.n} dropout seeds in one captured step")
+        addr = self.buf.data_ptr() + 8 * self.i
+        self.i += 1
+        return addr
+
+
+_SEED_SLOTS: Optional[SeedSlots] = None
+
+
+def use_device_seeds(slots: Optional[SeedSlots]) -> None:
+    """Install (or, with None, remove) the device seed source of a graph capture."""
+    global _SEED_SLOTS
+    _SEED_SLOTS = slots
+
+
+def _new_seed() -> tuple:
+    """(seed, salt bits) of one dropout call site.  Eager: drawn from torch's CPU generator
+    (reproducible under torch.manual_seed, no device sync), salt bits 0.  Under
+    use_device_seeds: a device seed slot's address and LG_SALT_SEED_PTR."""
+    if _SEED_SLOTS is not None:
+        return _SEED_SLOTS.take(), nat.LG_SALT_SEED_PTR
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item()), 0
 
 
 def _check_d(D: int) -> None:
@@ -326,14 +362,14 @@ class GNNTrunkFn(torch.autograd.Function):
         L = len(wb) // 2
         drop = cfg.training and cfg.dropout_p > 0.0
         p = float(cfg.dropout_p) if drop else 0.0
-        seed = _new_seed() if drop else 0
+        seed, sbit = _new_seed() if drop else (0, 0)
         dflag = nat.LG_F_DROPOUT if drop else 0
         nm = bool(cfg.node_major)
         st = stream_of(proj)
         x0 = torch.empty((N, B, D) if nm else (B, N, D), device=proj.device, dtype=torch.float32)
         with _timed("node_init", proj.device):
             check(lib.lg_node_init_fwd(ptr(cfg.sensor_slot), ptr(proj), ptr(node_bias.contiguous()), ptr(x0), B, N,
-                                       S, D, dflag | (nat.LG_F_NODE_MAJOR if nm else 0), p, seed, 0, st),
+                                       S, D, dflag | (nat.LG_F_NODE_MAJOR if nm else 0), p, seed, 0 | sbit, st),
                   "lg_node_init_fwd")
         xs = [x0]
         g = cfg.graph
@@ -345,11 +381,11 @@ class GNNTrunkFn(torch.autograd.Function):
             with _timed("gcn_fwd", proj.device):
                 if nm:
                     check(lib.lg_gcn_fwd_nm(ptr(g.rowptr), ptr(g.pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
-                                            g.nnz_cap, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed, l + 1, st),
+                                            g.nnz_cap, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed, (l + 1) | sbit, st),
                           "lg_gcn_fwd_nm")
                 else:
                     check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B,
-                                         N, D, g.nnz_cap, flags, p, seed, l + 1, st), "lg_gcn_fwd")
+                                         N, D, g.nnz_cap, flags, p, seed, (l + 1) | sbit, st), "lg_gcn_fwd")
             xs.append(y)
         if cfg.capture is not None:
             cfg.capture.extend((t.transpose(0, 1) if nm else t).detach().clone() for t in xs)
@@ -441,7 +477,7 @@ class HeadsFn(torch.autograd.Function):
         P = inc.num_pipes
         pe = float(cfg.dropout_p) if cfg.training else 0.0
         pn = float(cfg.dropout_p if cfg.noleak_p is None else cfg.noleak_p) if cfg.training else 0.0
-        seed = _new_seed() if (pe > 0.0 or pn > 0.0) else 0
+        seed, sbit = _new_seed() if (pe > 0.0 or pn > 0.0) else (0, 0)
         fe = nat.LG_F_DROPOUT if pe > 0.0 else 0
         fn = nat.LG_F_DROPOUT if pn > 0.0 else 0
         st = stream_of(h)
@@ -455,12 +491,12 @@ class HeadsFn(torch.autograd.Function):
         with _timed("edge_fwd", h.device):
             check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(h), ptr(w1c), ptr(b1), ptr(w2c), ptr(b2), ptr(logits),
                                        P + 1, ptr(ehid) if keep else None, B, N, P, D, hidden, fe | lay, pe, seed,
-                                       EDGE_HEAD_SALT, st),
+                                       EDGE_HEAD_SALT | sbit, st),
                   "lg_edge_head_fwd")
         with _timed("pool_head", h.device):
             check(lib.lg_pool_head_fwd(ptr(h), ptr(nw1c), ptr(nb1), ptr(nw2c), ptr(nb2), ptr(pooled), ptr(hid),
-                                       ptr(logits), P + 1, P, B, N, D, nhidden, fn | lay, pn, seed, NOLEAK_HEAD_SALT,
-                                       st),
+                                       ptr(logits), P + 1, P, B, N, D, nhidden, fn | lay, pn, seed,
+                                       NOLEAK_HEAD_SALT | sbit, st),
                   "lg_pool_head_fwd")
         ctx.cfg, ctx.drop = cfg, (pe, fe, pn, fn, seed)
         ctx.save_for_backward(h, w1c, w2c, ehid, pooled, hid, nw1c, nw2c)

@@ -150,3 +150,13 @@ def test_graft_entry_build():
     """The driver's build check: make (no-op when up to date) + import + ABI match."""
     import __graft_entry__ as ge
     ge.build()
+
+
+def test_seed_pointer_salt_bit_matches_header():
+    """The device-seed salt bit of the Python side is the header's LG_SALT_SEED_PTR."""
+    import re
+    from models import _native
+    from pathlib import Path
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "leakgnn.h").read_text()
+    m = re.search(r"#define LG_SALT_SEED_PTR (0x[0-9a-fA-F]+)u", hdr)
+    assert m and int(m.group(1), 16) == _native.LG_SALT_SEED_PTR == 1 << 31
