@@ -144,7 +144,7 @@ def write_synthetic_leak_set(root: str | Path, sensor_ids: Sequence[str], pipe_i
                              scenes_per_pipe: int = 2, n_noleak: int = 6, T: int = 400, seed: int = 0) -> dict:
     """Abrupt-leak set in the reference format (datasets.py:282-435, leak_generation.py):
     manifest rows {"scenario_id": "NNNNNN_<pipe>_abrupt_rK", "status", "kind": "leak",
-    "leak_type": "abrupt", "pipe_id"} plus no-leak rows {"scenario_id", "kind": "noleak"};
+    "leak_type": "abrupt", "pipe_id"} plus no-leak rows {"scenario_id", "kind": "no_leak"} (leak_generation.py:373);
     each leak scene has leak_flow_m3h.csv (column = pipe id, 0 before the onset) and a
     pressure drop after the onset.  One row is marked status "failed" (filtered out)."""
     import pandas as pd
@@ -175,8 +175,8 @@ def write_synthetic_leak_set(root: str | Path, sensor_ids: Sequence[str], pipe_i
         gt, noisy = _sensor_frame(sensor_ids, T, rng, start=f"2024-03-{1 + j % 28:02d} 00:00")
         noisy.to_csv(root / sid / "sensors.csv")
         gt.to_csv(root / sid / "sensors_gt.csv")
-        rows.append({"scenario_id": sid, "status": "ok", "kind": "noleak"})
-    rows.append({"scenario_id": "999999_failed", "status": "failed", "kind": "noleak"})
+        rows.append({"scenario_id": sid, "status": "ok", "kind": "no_leak"})
+    rows.append({"scenario_id": "999999_failed", "status": "failed", "kind": "no_leak"})
     with open(root / "manifest.jsonl", "w", encoding="utf-8") as f:
         for row in rows:
             f.write(json.dumps(row) + "\n")

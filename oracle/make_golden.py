@@ -220,6 +220,55 @@ def harness_fixture(ref: Path, rpred, lta_inp: Path, pipe_pool, out_npz: Path, o
     return {"normal_samples": 8, "leak_samples": 24, "eval_metrics": len(info["eval_metrics"])}
 
 
+NOLEAK_BIAS = (2.0, 3.0)
+
+
+def event_fixture(ref: Path, lta_inp: Path, out_json: Path) -> dict:
+    """Event-level evaluator fixture: the reference's eval/event_evaluator.py
+    (`evaluate_dataset_event_level`, B = 1 per stride step) on the synthetic leak set,
+    the seeded TCN of predictor.npz and the stand-in detector of harness.npz; records
+    the per-event jsonl and summary.json it writes."""
+    import importlib.util
+    import tempfile
+    spec = importlib.util.spec_from_file_location("lg_synth", REPO / "leak-det-gnn_amd" / "models" / "synth.py")
+    lg_synth = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lg_synth)
+    spec = importlib.util.spec_from_file_location("ref_event_evaluator", ref / "eval" / "event_evaluator.py")
+    rev = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rev)
+    import models.predictor as rpred  # the reference's (path set by _import_reference)
+    info = json.loads((GOLD / "harness.json").read_text())
+    h = np.load(GOLD / "harness.npz")
+    p = np.load(GOLD / "predictor.npz")
+    tcn = rpred.NormalPredictorTCN(num_sensors=29, time_dim=9).eval()
+    tcn.load_state_dict({k[4:]: torch.from_numpy(p[k]) for k in p.files if k.startswith("tcn.")})
+    std = rev.SensorStandardizer(mean=h["std_mean"], std=h["std_std"])
+    # noleak_bias lifts the stand-in's no-leak logit so alarms come late, or never
+    cases = [dict(stride_steps=3, agg_window_hours=1.0, include_noleak=True, max_leak_scens=8, max_noleak_scens=4),
+             dict(stride_steps=1, agg_window_hours=12.0, include_noleak=True, max_leak_scens=-1, max_noleak_scens=-1),
+             dict(stride_steps=2, agg_window_hours=2.0, include_noleak=True, max_leak_scens=-1, max_noleak_scens=-1,
+                  noleak_bias=NOLEAK_BIAS[0]),
+             dict(stride_steps=1, agg_window_hours=0.5, include_noleak=False, max_leak_scens=5, max_noleak_scens=2,
+                  noleak_bias=NOLEAK_BIAS[1])]
+    out = {"pipes": info["pipes"], "l_pred": 36, "l_det": 36, "cases": []}
+    with tempfile.TemporaryDirectory() as d:
+        d = Path(d)
+        lg_synth.write_synthetic_leak_set(d / "leak", SENSORS, info["pipes"], scenes_per_pipe=2, n_noleak=6, T=400,
+                                          seed=0)
+        for c in cases:
+            kw = {k: v for k, v in c.items() if k != "noleak_bias"}
+            cc = h["eval.c"].copy()
+            cc[-1] += np.float32(c.get("noleak_bias", 0.0))
+            det = FixedLogitsDetector(h["eval.A"], h["eval.Bm"], cc)
+            summary = rev.evaluate_dataset_event_level(
+                d / "leak", lta_inp, torch.device("cpu"), tcn, det, 36, 36, std, SENSORS, info["pipes"],
+                sample_seed=42, out_dir=d / "out", **kw)
+            events = [json.loads(ln) for ln in (d / "out" / "per_event.jsonl").read_text().splitlines() if ln]
+            out["cases"].append({"args": c, "summary": summary, "events": events})
+    out_json.write_text(json.dumps(out, indent=1) + "\n")
+    return {"cases": len(cases), "events": [len(c["events"]) for c in out["cases"]]}
+
+
 RESIDUAL_CASES = ((36, 36, 3), (12, 20, 2), (64, 8, 2), (40, 1, 2))  # (l_pred, l_det, B)
 
 
@@ -250,12 +299,17 @@ def residual_fixture(rutils, rpred, out: Path) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--only", choices=["residual"], default=None,
+    ap.add_argument("--only", choices=["residual", "event"], default=None,
                     help="regenerate one fixture only (leaves the others byte-identical)")
     args = ap.parse_args()
     ref = Path(args.ref)
     rutils, rpred, rdet = _import_reference(ref)
     GOLD.mkdir(parents=True, exist_ok=True)
+    if args.only == "event":
+        meta = json.loads((GOLD / "meta.json").read_text())
+        meta["event"] = event_fixture(ref, ref / "data/raw/L-TOWN-A/L-TOWN_AreaA.inp", GOLD / "event.json")
+        (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
+        return
     if args.only == "residual":
         meta = json.loads((GOLD / "meta.json").read_text())
         meta["residual"] = residual_fixture(rutils, rpred, GOLD / "residual.npz")
@@ -275,6 +329,7 @@ def main() -> None:
     predictor_fixture(rutils, rpred, GOLD / "predictor.npz")
     meta["residual"] = residual_fixture(rutils, rpred, GOLD / "residual.npz")
     meta["harness"] = harness_fixture(ref, rpred, lta, pipe_ids, GOLD / "harness.npz", GOLD / "harness.json")
+    meta["event"] = event_fixture(ref, lta, GOLD / "event.json")
     (GOLD / "meta.json").write_text(json.dumps(meta, indent=2) + "\n")
     print(json.dumps(meta, indent=2))
 

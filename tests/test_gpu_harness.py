@@ -80,3 +80,45 @@ def test_train_predictor_and_detector_cli(data, tmp_path, capsys):
     assert "[detector] TEST:" in log and "ATD=" in log and "loss=" in log
     losses = [float(l.split("loss=")[1].split()[0]) for l in log.splitlines() if "[detector][epoch" in l and "loss=" in l]
     assert all(np.isfinite(losses)) and len(losses) >= 2
+
+
+def test_event_evaluator_gpu_matches_reference(data):
+    """Event-level evaluator on the GPU (residuals from the HIP shared-window TCN over the
+    whole scenario, one batched detector call) == the reference's per-step CPU loop
+    (tests/golden/event.json): alarm times, predicted pipes, ATD and summary metrics."""
+    from test_harness import _check_events, _check_metrics, _event_cases, _run_event_case, _tcn
+    arrs = np.load(GOLD / "harness.npz")
+    for case in _event_cases()["cases"]:
+        summary, events = _run_event_case(case, data / "leak", arrs, DEV, _tcn())
+        _check_metrics(summary, case["summary"])
+        _check_events(events, [dict(e) for e in case["events"]])
+
+
+def test_event_windows_batched_equal_per_window_loop(data):
+    """scenario_window_logits on a LeakDetector == the reference's loop shape: per window,
+    build_residual_segment on its own (l_pred + l_det) segment and a B = 1 detector call
+    (`event_evaluator.py:476-492`), fp32 within 1e-5 relative of the logit scale."""
+    import pandas as pd
+    from models.datasets import SensorStandardizer, make_time_features
+    from models.detector import LeakDetector
+    from models.event_evaluator import load_sensors_csv, scenario_window_logits
+    from models.utils import build_residual_sequence_from_segment
+    from test_harness import _tcn
+    arrs = np.load(GOLD / "harness.npz")
+    sid = sorted(p.name for p in (data / "leak").iterdir() if p.is_dir() and "abrupt" in p.name)[0]
+    df = load_sensors_csv(data / "leak" / sid / "sensors.csv", INFO["sensors"])
+    std = SensorStandardizer(mean=arrs["std_mean"], std=arrs["std_std"])
+    pressure = std.transform(df.values.astype(np.float32))
+    tfeat = make_time_features(pd.to_datetime(df.index))
+    torch.manual_seed(0)
+    det = LeakDetector(LTA_INP, INFO["sensors"], INFO["pipes"]).to(DEV).eval()
+    tcn = _tcn().to(DEV)
+    logits, last = scenario_window_logits(tcn, det, pressure, tfeat, 36, 36, 5, DEV, window_batch=16)
+    assert logits.shape == (len(last), len(INFO["pipes"]) + 1) and len(last) > 40
+    p, tf = torch.from_numpy(pressure).to(DEV), torch.from_numpy(tfeat).to(DEV)
+    with torch.no_grad():
+        for w, end in enumerate(last):
+            t0 = int(end) - 36 + 1
+            res = build_residual_sequence_from_segment(tcn, p[t0 - 36:t0 + 36], tf[t0 - 36:t0 + 36], 36, 36)
+            ref = det(res[None], tf[None, t0:t0 + 36]).float().cpu()[0]
+            assert (logits[w] - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, w

@@ -117,3 +117,77 @@ def test_window_evaluator_matches_reference(fx, data):
                            metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
                            inp_path=LTA_INP, pipe_ids_in_order=info["pipe_ids_in_order"])
     _check_metrics(ev.evaluate(DataLoader(eds, batch_size=16)), info["eval_metrics"])
+
+
+# ------------------------------------------------------------------ event-level evaluator
+def _event_cases():
+    return json.loads((GOLD / "event.json").read_text())
+
+
+def _run_event_case(case, root, arrs, device, predictor):
+    from models.datasets import SensorStandardizer
+    from models.event_evaluator import evaluate_dataset_event_level
+    c = dict(case["args"])
+    bias = np.float32(c.pop("noleak_bias", 0.0))
+    cc = arrs["eval.c"].copy()
+    cc[-1] += bias
+    A, Bm, cv = (torch.from_numpy(v).to(device) for v in (arrs["eval.A"], arrs["eval.Bm"], cc))
+
+    class StandIn(torch.nn.Module):  # oracle/make_golden.py FixedLogitsDetector
+        def forward(self, residual, tfeat):
+            return 3.0 * torch.tanh(residual.mean(1) @ A + tfeat.mean(1) @ Bm) + cv
+
+    std = SensorStandardizer(mean=arrs["std_mean"], std=arrs["std_std"])
+    out = root / "out"
+    summary = evaluate_dataset_event_level(root, LTA_INP, device, predictor.to(device), StandIn(), 36, 36, std,
+                                           SENSORS, _event_cases()["pipes"], sample_seed=42, out_dir=out, **c)
+    events = [json.loads(ln) for ln in (out / "per_event.jsonl").read_text().splitlines() if ln]
+    return summary, events
+
+
+def _check_events(got, ref):
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        atd_g, atd_r = g.pop("atd_m"), r.pop("atd_m")
+        assert g == r
+        assert (atd_g is None) == (atd_r is None) and (atd_r is None or abs(atd_g - atd_r) <= 1e-9 * max(1.0, atd_r))
+
+
+@pytest.fixture(scope="module")
+def event_data(tmp_path_factory):
+    from models.synth import write_synthetic_leak_set
+    d = tmp_path_factory.mktemp("eventds") / "leak"
+    write_synthetic_leak_set(d, SENSORS, _event_cases()["pipes"], scenes_per_pipe=2, n_noleak=6, T=400, seed=0)
+    return d
+
+
+def test_event_evaluator_matches_reference(fx, event_data):
+    """Batched evaluator (one residual pass + one detector call per scenario) == the
+    reference's per-stride-step loop on CPU: selection order, tau, alarm time, predicted
+    pipe, ATD and every summary metric, over four argument sets (stride 1-3, aggregation
+    0.5-12 h, with and without no-leak scenarios, alarms that come late or never)."""
+    _, arrs = fx
+    cases = _event_cases()["cases"]
+    # the fixture covers events whose aggregated logits fall back to no-leak
+    assert any(e["is_leak_true"] and not e["is_leak_pred"] for c in cases for e in c["events"])
+    for case in cases:
+        summary, events = _run_event_case(case, event_data, arrs, torch.device("cpu"), _tcn())
+        _check_metrics(summary, case["summary"])
+        _check_events(events, [dict(e) for e in case["events"]])
+
+
+def test_event_trigger_and_aggregation_helpers():
+    """List-API helpers (`event_evaluator.py:327-342`) on hand-made records."""
+    import pandas as pd
+    from models.event_evaluator import aggregate_sum_logits, trigger_argmax
+    t = pd.date_range("2024-01-01", periods=6, freq="5min")
+    lg = [torch.tensor([0.0, 1.0]), torch.tensor([0.0, 2.0]), torch.tensor([3.0, 1.0]), torch.tensor([1.0, 0.5]),
+          torch.tensor([0.25, 4.0]), torch.tensor([9.0, 0.0])]
+    rec = list(zip(t, lg))
+    assert trigger_argmax(rec, noleak_class=1) == 2
+    assert trigger_argmax(rec[:2], noleak_class=1) is None
+    assert trigger_argmax([], noleak_class=1) is None
+    s = aggregate_sum_logits(rec, 2, pd.Timedelta(minutes=15))  # rows 2, 3, 4 (gap 15 min stops)
+    assert torch.equal(s, lg[2] + lg[3] + lg[4])
+    assert torch.equal(aggregate_sum_logits(rec, 5, pd.Timedelta(minutes=15)), lg[5])
+    assert torch.equal(aggregate_sum_logits(rec, 3, pd.Timedelta(0)), lg[3])
