@@ -85,6 +85,10 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __r
 // for units [16u, 16u+16) and posts h' to LDS, from where every wave reads the next
 // step's B operand.  Exchanges use lane-major slots (the reader lane is the writer
 // lane), so every LDS access is a conflict-free b128.  Two barriers per step.
+// Measured and dropped (MI355X, B = 256): the recurrent product on split-bf16
+// v_mfma_f32_16x16x32_bf16 (K permuted so each lane's two lane-major h tiles form its B
+// fragment, no extra exchange) ran 158 -> 165 us and doubled the W_ih gradient error —
+// the step is bound by its barriers / transcendentals / LDS round trip, not MFMA issue.
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
 template <int H, bool UT, bool SAVE>
 __global__ void __launch_bounds__(12 * H) __attribute__((amdgpu_waves_per_eu(6, 8)))  // 2 workgroups / CU
