@@ -385,9 +385,10 @@ def main() -> None:
     l_pred = int(round(float(args.l_pred_hours) * per_hour))
     l_det = int(round(float(args.l_det_hours) * per_hour))
     stride = max(1, int(round(float(args.stride_minutes) / float(args.step_minutes))))
-    # checkpoints written by our own train_* CLIs (reference schema); weights_only load
-    pck = torch.load(args.predictor_ckpt, map_location="cpu", weights_only=True)
-    dck = torch.load(args.detector_ckpt, map_location="cpu", weights_only=True)
+    # weights_only load; LEAKGNN_TRUST_CKPT=1 opts in to a trusted foreign checkpoint
+    from .train_detector import _load_ckpt
+    pck = _load_ckpt(args.predictor_ckpt, torch.device("cpu"))
+    dck = _load_ckpt(args.detector_ckpt, torch.device("cpu"))
     S = len(pck["sensor_ids"])
     pred_cls = NormalPredictorGRU if pck.get("arch", "tcn") == "gru" else NormalPredictorTCN
     predictor = pred_cls(num_sensors=S, time_dim=9)
