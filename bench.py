@@ -246,6 +246,51 @@ def _conv_ms(predictor, plan, B: int, dev) -> float:
     return _event_ms(run, 20)
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` without torchrun's environment: start N ranks (one process per GPU)
+    under torch.distributed.run as a CHILD process, before this process touches the GPU,
+    and return its exit code.  Rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve())] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """`--dry-run`: the multi-rank launch / barrier / max-over-ranks timing / JSON path on
+    CPU (gloo), with the step reduced to the detector's gradient all-reduce (60,418 fp32
+    values in one bucket).  For CI without a GPU; never a measurement."""
+    import torch.distributed as dist
+    from models.ddp import init_distributed
+    init_distributed(backend="gloo")
+    grad = torch.ones(60418) * (rank + 1)
+    for _ in range(args.warmup):
+        dist.all_reduce(grad)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(grad)
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": None, "unit": "windows/s",
+                          "n_gpus": world, "ranks_seen": dist.get_world_size(), "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(float(t.item()) * 1e3 / max(args.steps, 1), 4),
+                          "dry_run": True, "backend": "gloo",
+                          "config": {"workload": "gradient all-reduce only (no detector step)",
+                                     "parallelism": f"dp{world}"}}), flush=True)
+    dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,7 +301,23 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--eager", action="store_true", help="launch the step eagerly instead of replaying its HIP graph")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launch-path check (no GPU, no measurement)")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world_env = int(env_world or 1)
+    if world_env != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}; launch one rank per GPU")
+    if args.dry_run:
+        from models.ddp import dist_env
+        rank, _, world = dist_env()
+        dry_run(args, rank, world)
+        return
+    if torch.cuda.device_count() < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible")
 
     from models import ops
     from models.ddp import GradAllReduce, init_distributed
@@ -348,7 +409,7 @@ def main() -> None:
     traffic = pmc_traffic(B, ops.TRUNK_NODE_MAJOR) if (world == 1 and not args.no_pmc) else None
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "n_gpus": world, "ranks_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic residual windows (B,36,29) + time features, random-init weights",
         "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",

@@ -73,6 +73,12 @@ enum {
  * bit-identical to lg_gcn_fwd); LG_F_F32_MFMA = exact v_mfma_f32_16x16x4_f32, bit-identical
  * to lg_gcn_fwd on the transposed layout. */
 #define LG_F_F32_MFMA      0x00400000
+/* lg_gcn_fwd_nm schedule bits (kernel lab; results unchanged): LG_F_LAB_NM2 = the pipeline
+ * that walks rowptr per tile (round-1 kernel), LG_F_LAB_W8 = 8-wave workgroups. */
+#define LG_F_LAB_NM2       0x00200000
+#define LG_F_LAB_W8        0x00100000
+#define LG_F_LAB_DST       0x00080000  /* lab: epilogue stores straight from the MFMA layout */
+
 #define LG_F_LAB_BPC_SHIFT 24
 
 int lg_abi_version(void);
@@ -102,6 +108,15 @@ int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
                    int32_t* rowptr, int32_t* col, float* w,
                    int32_t* rowptr_t, int32_t* col_t, float* w_t,
                    void* workspace, lg_stream_t stream);
+
+/* Node table of the node-major kernels, once per graph (and once for the transposed CSR):
+ * one 64-byte record per node = {e0, e1, (col, float_as_int(w)) x 6, self, 0} so a tile
+ * reads its CSR row with ONE scalar load.  self = position (< 6) of the row's entry whose
+ * col is the node itself, -1 if none inline.
+ *   rowptr : int32 [N+1];  pairs : int32 [2 * nnz] (col, float_as_int(w));
+ *   nodetab : int32 [N][16] (64-byte aligned). */
+int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, int32_t* nodetab,
+                      lg_stream_t stream);
 
 /* Pipe-endpoint incidence CSR, once per model (backward of detector.py:206-210).
  *   ends : int64 [P][2] device (pipe_ends, utils.py:352-358)
@@ -168,17 +183,21 @@ int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
  * Every window shares the graph, so a 16-row tile is one node and 16 consecutive
  * windows, and each CSR entry (m, w) names one contiguous 16 x D block of x — the
  * entry is wave-uniform and the row loads need no per-lane index arithmetic.
+ *   nodetab : int32 [N][16] from lg_nm_table_build (one 64-byte record per node:
+ *             e0, e1, the first 6 (col, w) pairs of the row, self position);
  *   pairs : int32 [2 * nnz] interleaved (col, float_as_int(w)) of the lg_graph_build CSR.
  *   Dropout: row-stream masks indexed by the window-major row b*N + n (the mask of
  *   lg_gcn_fwd for the same seed/salt).
- *   Requires N*B*D*4 <= 0xFFFFFF00 bytes (LG_EUNSUPPORTED otherwise). */
-int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
+ *   Requires N*B*D*4 <= 0x7FFFF000 bytes (LG_EUNSUPPORTED otherwise; callers split
+ *   larger batches over windows). */
+int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                   const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                   int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 /* Backward of lg_gcn_fwd_nm: lg_gcn_bwd's contract on the node-major layout, over the
- * transposed CSR given as rowptr_t + pairs_t.  workspace: lg_gcn_bwd_nm_workspace_bytes(D). */
+ * transposed CSR given as nodetab_t (lg_nm_table_build of rowptr_t) + pairs_t.
+ * workspace: lg_gcn_bwd_nm_workspace_bytes(D). */
 int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D);
-int lg_gcn_bwd_nm(const int32_t* rowptr_t, const int32_t* pairs_t, const float* dy, const float* y,
+int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                   const float* x, const float* W, float* dx_out, float* dW, float* db,
                   const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
                   int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream);

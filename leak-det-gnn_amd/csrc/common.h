@@ -107,6 +107,8 @@ __device__ __forceinline__ uint32_t lg_div(uint32_t n, const lg_fastdiv& f) {
     return (t + ((n - t) >> f.s1)) >> f.s2;
 }
 
+constexpr int kLgNmInline = 6;  // CSR entries held inline in a node-table record (graph.hip k_nm_table)
+
 constexpr int64_t kLgMaxRows = int64_t{1} << 31;  // row-index space of the fast-division kernels
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }

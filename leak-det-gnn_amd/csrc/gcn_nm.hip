@@ -86,13 +86,13 @@ __device__ __forceinline__ NmSched nm_sched(int64_t ntiles, int wave, int waves)
 //   sum over CSR row n of w * src[m][b0..b0+15]   (MASK: src * mscale * [msk > 0]),
 // entries in CSR order, fp32 fma.  Two neighbours' blocks are in flight at a time.
 template <int D, bool MASK>
-__device__ __forceinline__ void gather_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
+__device__ __forceinline__ void gather_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs,
                                           __amdgpu_buffer_rsrc_t src, __amdgpu_buffer_rsrc_t msk, float mscale,
                                           uint32_t n, uint32_t B, uint32_t b0, const uint32_t (&loff)[NmGeo<D>::K],
                                           const bool (&rv)[NmGeo<D>::K], f32x4 (&acc)[NmGeo<D>::K]) {
     using G = NmGeo<D>;
-    const int e0 = __builtin_amdgcn_readfirstlane(rowptr[n]);
-    const int e1 = __builtin_amdgcn_readfirstlane(rowptr[n + 1]);
+    const int e0 = __builtin_amdgcn_readfirstlane(tab[16 * n]);
+    const int e1 = __builtin_amdgcn_readfirstlane(tab[16 * n + 1]);
 #pragma unroll
     for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
     auto contrib = [&](float w, const f32x4& v, const f32x4& m, f32x4& a) {
@@ -143,7 +143,7 @@ __device__ __forceinline__ void gather_nm(const int32_t* __restrict__ rowptr, co
 // ------------------------------------------------------------------ forward
 template <int D, bool DROP>
 __global__ void __launch_bounds__(64 * kNmFwdWaves)
-k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ x,
+k_gcn_fwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
              uint64_t seed, uint32_t salt) {
@@ -188,7 +188,7 @@ k_gcn_fwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
 #pragma unroll
         for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
         f32x4 acc[G::K];
-        gather_nm<D, false>(rowptr, pairs, xrs, xrs, 1.f, n, B, b0, loff, rv, acc);
+        gather_nm<D, false>(tab, pairs, xrs, xrs, 1.f, n, B, b0, loff, rv, acc);
 
         // gather layout -> LDS -> MFMA B operand
         wave_sync_nm();
@@ -274,7 +274,7 @@ struct NmSlot {  // one tile in flight: its CSR range, weights and first NPF nei
 
 template <int D, bool DROP, int NPF, bool SPLIT, int LAB = 0>
 __global__ void __launch_bounds__(64 * kNm2Waves)
-k_gcn_fwd_nm2(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ x,
+k_gcn_fwd_nm2(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
               uint64_t seed, uint32_t salt) {
@@ -332,8 +332,8 @@ k_gcn_fwd_nm2(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
 
     auto csr_row = [&](uint32_t n, int& e0, int& e1) {  // wave-uniform: scalar loads
-        e0 = __builtin_amdgcn_readfirstlane(rowptr[n]);
-        e1 = __builtin_amdgcn_readfirstlane(rowptr[n + 1]);
+        e0 = __builtin_amdgcn_readfirstlane(tab[16 * n]);
+        e1 = __builtin_amdgcn_readfirstlane(tab[16 * n + 1]);
     };
     auto csr_pair = [&](int e) -> int2 { return pairs[e]; };
 
@@ -503,10 +503,335 @@ k_gcn_fwd_nm2(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs
     for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) process(sl, tile);
 }
 
+
+// ------------------------------------------------------------------ forward, node-table pipeline
+// k_gcn_fwd_nm2's math with the CSR read from the node table (graph.hip k_nm_table): one
+// 64-byte record per node holds (e0, e1) and its first kLgNmInline (col, w) pairs, read by
+// a single scalar load.  nm2 walked rowptr -> pair -> pair ... as dependent scalar round
+// trips before each tile's row loads could issue, and the MFMA transform waited behind
+// them (SMEM and LDS share lgkmcnt).  Here the record of tile i+1 is requested at the top
+// of tile i and lands while tile i's rows are waited for and accumulated, so tile i+1's
+// NPF neighbour blocks issue at once, right before tile i's transform.  (A record carried
+// across the loop back edge in SGPRs is copied there, and the copy waits for the load.)
+constexpr int kNm3Npf = 4;
+
+struct NmRec {  // one node-table record (wave-uniform, SGPRs)
+    int e0, e1, self;
+    int2 p[kLgNmInline];
+};
+
+__device__ __forceinline__ NmRec nm_rec(const int32_t* __restrict__ tab, uint32_t n) {
+    const int4* t = reinterpret_cast<const int4*>(tab) + 4 * static_cast<size_t>(n);
+    const int4 a = t[0], b = t[1], c = t[2], d = t[3];
+    NmRec r;
+    r.e0 = a.x;
+    r.e1 = a.y;
+    r.p[0] = int2{a.z, a.w};
+    r.p[1] = int2{b.x, b.y};
+    r.p[2] = int2{b.z, b.w};
+    r.p[3] = int2{c.x, c.y};
+    r.p[4] = int2{c.z, c.w};
+    r.p[5] = int2{d.x, d.y};
+    r.self = d.z;
+    return r;
+}
+static_assert(kLgNmInline == 6, "nm_rec unpacks six inline pairs");
+
+template <int D, bool SPLIT, int WAVES>
+struct Nm3Lds {  // dynamic LDS layout (floats)
+    static constexpr int SB = D + 8;
+    static constexpr int WF = SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
+    static constexpr int TILES = WF + D;
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + WAVES * NmGeo<D>::TILE);
+};
+
+// acc += w * v on packed fp32 (v_pk_fma_f32: two lanes' worth of fma per instruction,
+// each element the same IEEE fma as fmaf)
+__device__ __forceinline__ void pk_fma4(f32x4& a, float w, const f32x4& v) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 ww = {w, w};
+    const f2 lo = __builtin_elementwise_fma(ww, f2{v[0], v[1]}, f2{a[0], a[1]});
+    const f2 hi = __builtin_elementwise_fma(ww, f2{v[2], v[3]}, f2{a[2], a[3]});
+    a = f32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
+// Out-of-range offsets of the nm3 addressing: a lane offset of a masked row is kNm3RowOob
+// and an absent neighbour's block base is kNm3BlkOob, so lane + base lands past
+// num_records (<= kNm3MaxBytes) with ONE v_add per load and no wrap-around.
+constexpr uint32_t kNm3RowOob = 0x80000000u;
+constexpr uint32_t kNm3BlkOob = 0x7FFFF000u;
+constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
+
+// LAB (kernel-lab builds only; results are WRONG when set): 1 = skip the MFMA transform,
+// 2 = skip the neighbour loads, 4 = skip the y stores (kept behind a runtime-false test so
+// the transform is not dead code).  DST: epilogue stores straight from the MFMA layout
+// (16 rows x 64 B per store) instead of through the LDS tile.
+template <int D, bool DROP, bool SPLIT, int WAVES, int LAB = 0, bool DST = false>
+__global__ void __launch_bounds__(64 * WAVES)
+k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
+              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
+              uint64_t seed, uint32_t salt) {
+    using G = NmGeo<D>;
+    using LY = Nm3Lds<D, SPLIT, WAVES>;
+    constexpr int SB = LY::SB;
+    constexpr int NPF = kNm3Npf;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* wl = reinterpret_cast<float*>(smem);         // fp32: W [out][in] * fold, stride S
+    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB
+    float* bl = wl + LY::WF;                            // bias * fold
+    float* tiles = wl + LY::TILES;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = tiles + wave * G::TILE;
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, WAVES);
+    const int64_t tend = sc.end;
+
+    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+        const bool valid = tile < tend;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        n = t32 - grp * N;
+        b0 = grp * 16;
+        nb = valid ? min(16u, B - b0) : 0u;
+    };
+    // tile in flight: its record, coordinates, lane offsets and first NPF neighbour blocks
+    f32x4 pf[NPF][G::K];
+    uint32_t lo[G::K];  // loff, or kNm3RowOob for rows past the tile's window count
+    NmRec cur;
+    uint32_t cn, cb0, cnb;
+    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+        cur = r;
+        cn = n;
+        cb0 = b0;
+        cnb = nb;
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            const bool have = r.e0 + i < r.e1;
+            const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : kNm3BlkOob;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+                pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
+                                     : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                     xrs, lo[k] + base, 0, 0));
+        }
+    };
+    const int64_t t0 = sc.first;
+    {
+        uint32_t n0, b00, nb00;
+        tile_coords(t0, n0, b00, nb00);
+        issue(nm_rec(tab, n0), n0, b00, nb00);
+    }
+
+    // W (x dropout scale fold) and bias to LDS, after the first tile's loads are out
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
+        const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
+        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i = u * 64 * WAVES + threadIdx.x;
+            if (i >= W4) continue;
+            const int o = i / (D / 4), c4 = 4 * (i % (D / 4));
+            const f32x4 w = wv[u] * fold;
+            if constexpr (SPLIT) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    uint32_t p0, p1, p2;
+                    split3_pair(w[2 * h], w[2 * h + 1], p0, p1, p2);
+                    const int e = o * SB + c4 + 2 * h;
+                    *reinterpret_cast<uint32_t*>(wsl + e) = p0;
+                    *reinterpret_cast<uint32_t*>(wsl + D * SB + e) = p1;
+                    *reinterpret_cast<uint32_t*>(wsl + 2 * D * SB + e) = p2;
+                }
+            } else {
+                st4(wl + o * G::S + c4, w);
+            }
+        }
+        if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
+    }
+    __syncthreads();
+
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p_drop);
+
+    for (int64_t tile = t0; tile < tend; tile += sc.stride) {
+        const uint32_t n = cn, b0 = cb0, nb = cnb;
+        const int e0 = cur.e0, e1 = cur.e1;
+        uint32_t tlo[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
+        // the next tile's record goes in flight while this tile's rows are waited for
+        uint32_t nn, nb0, nnb;
+        tile_coords(tile + sc.stride, nn, nb0, nnb);
+        const NmRec nxt = nm_rec(tab, nn);
+        asm volatile("" ::: "memory");  // keep the request here: the compiler would sink it to its use
+        f32x4 acc[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            if (e0 + i < e1) {
+                const float w = __int_as_float(cur.p[i].y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[i][k]);
+            }
+        }
+        // neighbours past the prefetched ones (degree > NPF): inline pairs, then the pair array
+        if (e0 + NPF < e1) {
+            int2 ip[kLgNmInline - NPF];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) ip[i] = cur.p[NPF + i];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) {
+                if (e0 + NPF + i < e1) {
+                    const uint32_t ba = (static_cast<uint32_t>(ip[i].x) * B + b0) * (4u * D);
+                    f32x4 va[G::K];
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k)
+                        va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
+                    const float wa = __int_as_float(ip[i].y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+                }
+            }
+            int e = e0 + kLgNmInline;
+            for (; e + 1 < e1; e += 2) {
+                const int2 pa = pairs[e], pb = pairs[e + 1];
+                const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                const uint32_t bbs = (static_cast<uint32_t>(pb.x) * B + b0) * (4u * D);
+                f32x4 va[G::K], vb[G::K];
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) {
+                    va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
+                    vb[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + bbs, 0, 0));
+                }
+                const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) {
+                    pk_fma4(acc[k], wa, va[k]);
+                    pk_fma4(acc[k], wb, vb[k]);
+                }
+            }
+            if (e < e1) {
+                const int2 pa = pairs[e];
+                const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                f32x4 va[G::K];
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
+                const float wa = __int_as_float(pa.y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+            }
+        }
+        // next tile's blocks go in flight under this tile's transform (its record landed meanwhile)
+        issue(nxt, nn, nb0, nnb);
+        __builtin_amdgcn_sched_barrier(0);
+
+        // gather layout -> LDS -> MFMA B operand
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+        wave_sync_nm();
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
+        if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + j * G::S + 16 * mt + 4 * q);
+        } else if constexpr (SPLIT) {
+#pragma unroll
+            for (int s2 = 0; s2 < D / 32; ++s2) {
+                lg_bf16x8 b0f, b1f, b2f;
+                split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f,
+                          b2f);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                    const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                    const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
+                    const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
+                    o[mt] = mfma_bf(a2, b0f, o[mt]);
+                    o[mt] = mfma_bf(a1, b1f, o[mt]);
+                    o[mt] = mfma_bf(a0, b2f, o[mt]);
+                    o[mt] = mfma_bf(a1, b0f, o[mt]);
+                    o[mt] = mfma_bf(a0, b1f, o[mt]);
+                    o[mt] = mfma_bf(a0, b0f, o[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < G::CH; ++c) {
+                const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[mt] = mfma_nm(wa[i], bt[i], o[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // epilogue: ReLU, row-stream dropout seeded with the window-major row id (b0 + j) N + n
+        uint32_t st = 0;
+        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float t = fmaxf(o[mt][reg], relu_floor);
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    t = u16 >= thr ? t : 0.0f;
+                }
+                o[mt][reg] = t;
+            }
+        }
+        const uint32_t ob = (n * B + b0) * (4u * D);
+        const bool do_store = (LAB & 4) == 0 || relu_floor == 1234.5f;
+        if constexpr (DST) {
+            // lane (j, q) holds row j, channels 16 mt + 4 q .. + 3
+            const uint32_t so = j < static_cast<int>(nb) ? static_cast<uint32_t>(j) * (4u * D) + 16u * q : kNm3RowOob;
+            if (do_store)
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, o[mt]),
+                                                           yrs, so + ob + 64u * mt, 0, 2);
+        } else {
+            wave_sync_nm();
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+            wave_sync_nm();
+            if (do_store)
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t,
+                                           ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg)),
+                        yrs, tlo[k] + ob, 0, 2);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ backward
 template <int D, bool MASK_IN, bool NB>
 __global__ void __launch_bounds__(64 * kNmBwdWaves, 2)
-k_gcn_bwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, const float* __restrict__ dy,
+k_gcn_bwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
              const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
              const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out) {
@@ -569,7 +894,7 @@ k_gcn_bwd_nm(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs,
             xv[k] = nm_ld<D>(xs, loff[k], rv[k], ob);
         }
         f32x4 acc[G::K];
-        gather_nm<D, MASK_IN>(rowptr, pairs, dys, ms, scale_in, n, B, b0, loff, rv, acc);
+        gather_nm<D, MASK_IN>(tab, pairs, dys, ms, scale_in, n, B, b0, loff, rv, acc);
         wave_sync_nm();
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
@@ -685,10 +1010,10 @@ int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int
     return static_cast<int>(std::max<int64_t>(1, std::min(want, cap)));
 }
 
-bool nm_fits(int64_t B, int64_t N, int64_t D) { return N * B * D * 4 <= int64_t{0xFFFFFF00}; }
+bool nm_fits(int64_t B, int64_t N, int64_t D) { return N * B * D * 4 <= static_cast<int64_t>(kNm3MaxBytes); }
 
-// Transform selection of lg_gcn_fwd_nm: split-bf16 MFMA by default, exact f32 MFMA under
-// LG_F_F32_MFMA (bit-identical to lg_gcn_fwd).  Lab builds add the LAB floors (bits 28-29).
+// Transform selection of the pipelined forward: split-bf16 MFMA by default, exact f32 MFMA
+// under LG_F_F32_MFMA (bit-identical to lg_gcn_fwd).  Lab builds add the LAB floors (bits 28-29).
 template <int D, bool DR>
 auto nm2_kernel(int flags) {
     const bool split = (flags & LG_F_F32_MFMA) == 0;
@@ -702,13 +1027,37 @@ auto nm2_kernel(int flags) {
 #endif
     return split ? k_gcn_fwd_nm2<D, DR, 4, true, 0> : k_gcn_fwd_nm2<D, DR, 4, false, 0>;
 }
+template <int D, bool DR, int WV>
+auto nm3_kernel(int flags) {
+    const bool split = (flags & LG_F_F32_MFMA) == 0;
+#ifdef LG_KERNEL_LAB
+    const bool dst = (flags & LG_F_LAB_DST) != 0;
+#define LG_NM3_LAB(L)                                                                                      \
+    case L:                                                                                                \
+        return split ? (dst ? k_gcn_fwd_nm3<D, DR, true, WV, L, true> : k_gcn_fwd_nm3<D, DR, true, WV, L>) \
+                     : (dst ? k_gcn_fwd_nm3<D, DR, false, WV, L, true> : k_gcn_fwd_nm3<D, DR, false, WV, L>);
+    switch ((flags >> 28) & 7) {
+        LG_NM3_LAB(0)
+        LG_NM3_LAB(1)
+        LG_NM3_LAB(2)
+        LG_NM3_LAB(3)
+        LG_NM3_LAB(4)
+        LG_NM3_LAB(5)
+        LG_NM3_LAB(6)
+        LG_NM3_LAB(7)
+        default: break;
+    }
+#undef LG_NM3_LAB
+#endif
+    return split ? k_gcn_fwd_nm3<D, DR, true, WV, 0> : k_gcn_fwd_nm3<D, DR, false, WV, 0>;
+}
 
 }  // namespace
 
-extern "C" int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const float* x, const float* W,
+extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                              const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
                              float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
-    if (B < 0 || N <= 0 || !rowptr || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
+    if (B < 0 || N <= 0 || !nodetab || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
     if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
     if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
@@ -719,30 +1068,44 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* rowptr, const int32_t* pairs, const 
     const float relu_floor = (flags & LG_F_RELU) ? 0.f : -__builtin_huge_valf();
     const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const float* bp = (flags & LG_F_BIAS) ? bias : nullptr;
-    // tuning bits (no effect on results): LG_F_LAB_V1 = the one-tile-per-wave kernel,
-    // LG_F_LAB_BPC(n) = n workgroups of 4 waves per CU for the pipelined kernel
-    const bool lab_v1 = (flags & LG_F_LAB_V1) != 0;
-    const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 4;
+    // schedule bits (never change results): LG_F_LAB_V1 = one tile per wave, LG_F_LAB_NM2 =
+    // the rowptr-walking pipeline, LG_F_LAB_W8 = 8-wave workgroups, LG_F_LAB_BPC(n) = at most
+    // n workgroups per CU
+    const bool lab_v1 = (flags & LG_F_LAB_V1) != 0, lab_nm2 = (flags & LG_F_LAB_NM2) != 0;
+    const bool w8 = (flags & LG_F_LAB_W8) != 0;
+    const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
     (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
+    const bool split = (flags & LG_F_F32_MFMA) == 0;
     hipStream_t s = lg_stream(stream);
+    const uint32_t N32 = static_cast<uint32_t>(N), B32 = static_cast<uint32_t>(B), G32 = static_cast<uint32_t>(ngroups);
 #define LG_NM_FWD(DD, DR)                                                                                          \
     do {                                                                                                           \
         if (lab_v1) {                                                                                              \
             auto kern = k_gcn_fwd_nm<DD, DR>;                                                                      \
             const size_t dyn1 = 4 * static_cast<size_t>(DD * (DD + 4) + DD + kNmFwdWaves * 16 * (DD + 4));        \
             const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn1, ntiles, kNmFwdWaves, 4);                        \
-            kern<<<grid, 64 * kNmFwdWaves, dyn1, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),           \
-                                                      static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,\
-                                                      relu_floor, dropout_p, scale, seed, salt);                   \
-        } else {                                                                                                   \
+            kern<<<grid, 64 * kNmFwdWaves, dyn1, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,     \
+                                                      dropout_p, scale, seed, salt);                               \
+        } else if (lab_nm2) {                                                                                      \
             auto kern = nm2_kernel<DD, DR>(flags);                                                                 \
-            const size_t dyn2 = (flags & LG_F_F32_MFMA) ? Nm2Lds<DD, false>::BYTES : Nm2Lds<DD, true>::BYTES;      \
+            const size_t dyn2 = split ? Nm2Lds<DD, true>::BYTES : Nm2Lds<DD, false>::BYTES;                        \
             const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
-            kern<<<grid, 64 * kNm2Waves, dyn2, s>>>(rowptr, pr, x, W, bp, y, static_cast<uint32_t>(N),             \
-                                                    static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd,  \
-                                                    relu_floor, dropout_p, scale, seed, salt);                     \
+            kern<<<grid, 64 * kNm2Waves, dyn2, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
+                                                    dropout_p, scale, seed, salt);                                 \
+        } else if (w8) {                                                                                           \
+            auto kern = nm3_kernel<DD, DR, 8>(flags);                                                              \
+            const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \
+            const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
+            kern<<<grid, 64 * 8, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor, dropout_p,    \
+                                            scale, seed, salt);                                                    \
+        } else {                                                                                                   \
+            auto kern = nm3_kernel<DD, DR, 4>(flags);                                                              \
+            const size_t dyn3 = split ? Nm3Lds<DD, true, 4>::BYTES : Nm3Lds<DD, false, 4>::BYTES;                  \
+            const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
+            kern<<<grid, 64 * 4, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor, dropout_p,    \
+                                            scale, seed, salt);                                                    \
         }                                                                                                          \
     } while (0)
     if (D == 64) {
@@ -762,11 +1125,11 @@ extern "C" int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D) {
     return static_cast<int64_t>(2) * lg_num_cus() * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));
 }
 
-extern "C" int lg_gcn_bwd_nm(const int32_t* rowptr_t, const int32_t* pairs_t, const float* dy, const float* y,
+extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                              const float* x, const float* W, float* dx_out, float* dW, float* db,
                              const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
                              float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
-    if (B < 0 || N <= 0 || !rowptr_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
+    if (B < 0 || N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
     if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     if (mask_in && !y) return LG_EINVAL;
@@ -786,7 +1149,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* rowptr_t, const int32_t* pairs_t, co
         auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                     \
         grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),  \
                              2 * lg_num_cus());                                                                    \
-        kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(rowptr_t, pr, dy, y, x, W, node_slot, dx_out, slab,               \
+        kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,               \
                                                  static_cast<uint32_t>(N), static_cast<uint32_t>(B),               \
                                                  static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,           \
                                                  scale_out);                                                       \

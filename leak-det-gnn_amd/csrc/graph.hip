@@ -153,6 +153,34 @@ __global__ void k_batchify(const int64_t* __restrict__ ei, int64_t E, int64_t N,
     out[B * E + i] = ei[E + e] + off;
 }
 
+// Node table of the node-major kernels: one 64-byte record per node, read by ONE scalar
+// load (s_load_dwordx16) per tile: {e0, e1, (col, w bits) x kLgNmInline, self, 0}.
+// self = position k < kLgNmInline of the entry whose col is the node itself (-1: none
+// inline); the backward reads that entry's block as the tile's own dz rows.
+__global__ void k_nm_table(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, int64_t N,
+                           int32_t* __restrict__ tab) {
+    const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const int e0 = rowptr[n], e1 = rowptr[n + 1];
+    int v[16];
+    v[0] = e0;
+    v[1] = e1;
+    int self = -1;
+#pragma unroll
+    for (int k = 0; k < kLgNmInline; ++k) {
+        const bool have = e0 + k < e1;
+        const int2 p = have ? pairs[e0 + k] : int2{0, 0};
+        v[2 + 2 * k] = p.x;
+        v[3 + 2 * k] = p.y;
+        if (have && self < 0 && p.x == static_cast<int>(n)) self = k;
+    }
+    v[2 + 2 * kLgNmInline] = self;
+    v[3 + 2 * kLgNmInline] = 0;
+    int4* o = reinterpret_cast<int4*>(tab + 16 * n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = int4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+}
+
 inline unsigned nblocks(int64_t n) { return static_cast<unsigned>((n + kThreads - 1) / kThreads); }
 inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
@@ -236,6 +264,15 @@ extern "C" int lg_batchify_edge_index(const int64_t* edge_index, int64_t E, int6
     if (E == 0 || B == 0) return LG_OK;
     if (!edge_index || !out) return LG_EINVAL;
     k_batchify<<<nblocks(B * E), kThreads, 0, lg_stream(stream)>>>(edge_index, E, N, B, out);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, int32_t* nodetab,
+                                 lg_stream_t stream) {
+    if (N <= 0 || N > INT32_MAX / 16 || !rowptr || !pairs || !nodetab) return LG_EINVAL;
+    k_nm_table<<<nblocks(N), kThreads, 0, lg_stream(stream)>>>(rowptr, reinterpret_cast<const int2*>(pairs), N,
+                                                               nodetab);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

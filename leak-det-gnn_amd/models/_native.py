@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 7  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 8  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -26,6 +26,8 @@ LG_F_NODE_MAJOR = 0x20
 LG_SALT_SEED_PTR = 0x80000000  # salt bit 31: `seed` is the address of a device-resident uint64
 LG_F_LAB_V1 = 0x00800000  # kernel-lab schedule bit of lg_gcn_fwd_nm (tools/kbench.py)
 LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 3-way split bf16 MFMA)
+LG_F_LAB_NM2 = 0x00200000  # lg_gcn_fwd_nm schedule: round-1 rowptr-walking pipeline (kernel lab)
+LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel lab)
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)
@@ -36,6 +38,7 @@ SIGNATURES = {
     "lg_strerror": (ctypes.c_char_p, [_i32]),
     "lg_graph_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "lg_nm_table_build": (_i32, [_p, _p, _i64, _p, _p]),
     "lg_incidence_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
     "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),

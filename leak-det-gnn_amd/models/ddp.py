@@ -54,10 +54,19 @@ class GradAllReduce:
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
             return
         world = dist.get_world_size(self.group)
-        # one gather into the bucket, one collective, gradients re-pointed at the bucket
-        grads = [p.grad.reshape(-1) if p.grad is not None else torch.zeros(p.numel(), device=self.flat.device)
-                 for p in self.params]
-        torch.cat(grads, out=self.flat)
+        # one gather into the bucket, one collective, gradients re-pointed at the bucket.  After
+        # the first call every p.grad is a view of the bucket; a caller that zeroes or
+        # accumulates in place (zero_grad(set_to_none=False), micro-batches) keeps it that way,
+        # and then the gradient is already in place: copy only the ones that are not.
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            view = self.flat[off:off + n]
+            if p.grad is None:
+                view.zero_()
+            elif not (p.grad.data_ptr() == view.data_ptr() and p.grad.is_contiguous()):
+                view.copy_(p.grad.reshape(-1))
+            off += n
         if dist.get_backend(self.group) == "nccl":
             dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
         else:  # gloo has no AVG

@@ -400,8 +400,10 @@ def main() -> None:
     detector.to(device).eval()
     if list(pck["sensor_ids"]) != list(dck["sensor_ids"]):
         raise ValueError("predictor and detector checkpoints disagree on sensor_ids")
-    std = SensorStandardizer(mean=torch.as_tensor(pck["standardizer_mean"]).numpy().astype(np.float32),
-                             std=torch.as_tensor(pck["standardizer_std"]).numpy().astype(np.float32))
+    def _stat(v):  # lists (this build), numpy arrays (reference) or tensors on any device
+        return np.asarray(v.detach().cpu() if torch.is_tensor(v) else v, dtype=np.float32)
+
+    std = SensorStandardizer(mean=_stat(pck["standardizer_mean"]), std=_stat(pck["standardizer_std"]))
     evaluate_dataset_event_level(
         args.dataset_root, args.inp_path, device, predictor, detector, l_pred, l_det, std, dck["sensor_ids"],
         dck["pipe_ids_in_order"], stride_steps=stride, agg_window_hours=args.agg_window_hours,

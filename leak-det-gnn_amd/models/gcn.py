@@ -13,9 +13,12 @@ reference; the semantics restated here are PyG 2.x's published ones:
 
 Here forward runs the fused HIP kernel lg_gcn_fwd ((Ahat x) W^T + b, one launch)
 and backward lg_gcn_bwd.  The gcn_norm'ed CSR is built on the device
-(lg_graph_build) and, unlike PyG with cached=False, re-used while the same
-edge_index tensor (same storage, shape and version) is passed again — the graph
-is a pure function of edge_index, so results are unchanged.
+(lg_graph_build) and, unlike PyG with cached=False, re-used while an edge_index
+with the SAME CONTENT is passed again (compared element-wise against a private
+copy, one device-side equality check per call) — the graph is a pure function of
+edge_index, so results are unchanged.  Keying on the storage address alone would
+reuse a stale CSR when the caching allocator hands a freed edge_index's address
+to a different graph of the same shape.
 """
 from __future__ import annotations
 
@@ -50,6 +53,7 @@ class GCNConv(nn.Module):
         else:
             self.register_parameter("bias", None)
         self._graph_key = None
+        self._graph_ei: Optional[torch.Tensor] = None  # private copy of the edge_index the CSR was built from
         self._graph: Optional[GCNGraph] = None
         self.reset_parameters()
 
@@ -59,14 +63,18 @@ class GCNConv(nn.Module):
             with torch.no_grad():
                 self.bias.zero_()
         self._graph_key = None
+        self._graph_ei = None
         self._graph = None
 
     def graph_for(self, edge_index: torch.Tensor, num_nodes: int, device: torch.device) -> GCNGraph:
-        key = (edge_index.data_ptr(), tuple(edge_index.shape), edge_index._version, int(num_nodes), device)
-        if self._graph is None or self._graph_key != key:
+        key = (tuple(edge_index.shape), edge_index.dtype, int(num_nodes), device)
+        ei = edge_index.to(device)
+        if (self._graph is None or self._graph_key != key or self._graph_ei is None
+                or not torch.equal(self._graph_ei, ei)):
             self._graph = GCNGraph.build(edge_index, num_nodes, device, add_self_loops=self.add_self_loops,
                                          normalize=self.normalize, improved=self.improved)
             self._graph_key = key
+            self._graph_ei = ei.clone()
         return self._graph
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor] = None):

@@ -138,6 +138,9 @@ class GCNGraph:
     w_t: torch.Tensor
     pairs: Optional[torch.Tensor] = None    # int32 (cap, 2): (col, float bits of w), node-major kernels
     pairs_t: Optional[torch.Tensor] = None  # same for the transposed CSR
+    nodetab: Optional[torch.Tensor] = None    # int32 (N, 16): node-major kernels' per-node record
+    nodetab_t: Optional[torch.Tensor] = None  # same for the transposed CSR
+
 
     @staticmethod
     def build(edge_index: torch.Tensor, num_nodes: int, device: torch.device, add_self_loops: bool = True,
@@ -161,6 +164,11 @@ class GCNGraph:
         g._keepalive = (ei, ws)  # freed after the stream consumes them
         g.pairs = torch.stack([g.col, g.w.view(torch.int32)], dim=1).contiguous()
         g.pairs_t = torch.stack([g.col_t, g.w_t.view(torch.int32)], dim=1).contiguous()
+        g.nodetab = torch.empty(N, 16, **i32)
+        g.nodetab_t = torch.empty(N, 16, **i32)
+        check(lib.lg_nm_table_build(ptr(g.rowptr), ptr(g.pairs), N, ptr(g.nodetab), stream_of(ei)), "lg_nm_table_build")
+        check(lib.lg_nm_table_build(ptr(g.rowptr_t), ptr(g.pairs_t), N, ptr(g.nodetab_t), stream_of(ei)),
+              "lg_nm_table_build")
         return g
 
 
@@ -234,13 +242,39 @@ def use_device_seeds(slots: Optional[SeedSlots]) -> None:
     _SEED_SLOTS = slots
 
 
-def _new_seed() -> tuple:
-    """(seed, salt bits) of one dropout call site.  Eager: drawn from torch's CPU generator
-    (reproducible under torch.manual_seed, no device sync), salt bits 0.  Under
-    use_device_seeds: a device seed slot's address and LG_SALT_SEED_PTR."""
+def _new_seed(device: torch.device) -> tuple:
+    """(seed, salt bits, keep-alive) of one dropout call site.
+
+    Eager: drawn from torch's CPU generator (reproducible under torch.manual_seed, no
+    device sync), salt bits 0.  Under use_device_seeds: a device seed slot's address and
+    LG_SALT_SEED_PTR.  Inside any other stream capture (a plain torch.cuda.graph or
+    torch.compile's cudagraphs) a host integer would be frozen into the graph and every
+    replay would reuse the same masks, so the seed is drawn on the device by torch's
+    graph-safe CUDA generator (a fresh draw per replay) and passed by address; the
+    returned tensor must stay referenced until the kernel has been enqueued."""
     if _SEED_SLOTS is not None:
-        return _SEED_SLOTS.take(), nat.LG_SALT_SEED_PTR
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item()), 0
+        return _SEED_SLOTS.take(), nat.LG_SALT_SEED_PTR, None
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        t = torch.randint(0, 2 ** 62, (1,), dtype=torch.long, device=device)
+        return t.data_ptr(), nat.LG_SALT_SEED_PTR, t
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item()), 0, None
+
+
+def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The kernels read fp32: a half/bf16 tensor (model.half(), or an autocast-produced
+    activation that reached an op outside its custom_fwd cast) is converted, never
+    reinterpreted.  Gradients come back as fp32 and autograd casts them to the input's
+    dtype."""
+    if t is None or t.dtype == torch.float32:
+        return t
+    if not t.is_floating_point():
+        raise TypeError(f"leakgnn ops take floating-point tensors, got {t.dtype}")
+    return t.float()
+
+
+# autocast: every op runs its fp32 kernels; floating inputs are cast to fp32 on entry
+_fwd32 = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+_bwd32 = torch.amp.custom_bwd(device_type="cuda")
 
 
 def _check_d(D: int) -> None:
@@ -253,10 +287,12 @@ class GCNLayerFn(torch.autograd.Function):
     """y = Ahat (x W^T) + b for one graph (B=1 view of the kernels)."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, x, weight, bias, graph: GCNGraph):
         lib = load_library()
-        x = x.contiguous()
-        weight = weight.contiguous()
+        x = _f32(x).contiguous()
+        weight = _f32(weight).contiguous()
+        bias = _f32(bias)
         require_device(x, weight, bias)
         Ntot, D = x.shape
         _check_d(D)
@@ -273,11 +309,12 @@ class GCNLayerFn(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dy):
         lib = load_library()
         x, weight = ctx.saved_tensors
         g = ctx.graph
-        dy = dy.contiguous()
+        dy = _f32(dy).contiguous()
         Ntot, D = x.shape
         dx = torch.empty_like(x)
         dW = torch.empty_like(weight)
@@ -312,7 +349,9 @@ class SensorProjFn(torch.autograd.Function):
     split-K MFMA kernel (lg_linear_dw) instead of autograd's skinny-K (K = B*S) mm."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, h_s, W, b):
+        h_s, W, b = _f32(h_s), _f32(W), _f32(b)
         B, S, Ds = h_s.shape
         D = W.shape[0]
         h2 = h_s.reshape(B * S, Ds).contiguous()
@@ -322,9 +361,11 @@ class SensorProjFn(torch.autograd.Function):
         return proj
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dproj):
         lib = load_library()
         h2, W = ctx.saved_tensors
+        dproj = _f32(dproj)
         B, S = ctx.shape
         K, Ds = h2.shape
         D = W.shape[0]
@@ -352,9 +393,12 @@ class GNNTrunkFn(torch.autograd.Function):
     """
 
     @staticmethod
+    @_fwd32
     def forward(ctx, cfg: TrunkConfig, proj, node_bias, *wb):
         lib = load_library()
-        proj = proj.contiguous()
+        proj = _f32(proj).contiguous()
+        node_bias = _f32(node_bias)
+        wb = tuple(_f32(t) for t in wb)
         require_device(proj, node_bias)
         B, S, D = proj.shape
         _check_d(D)
@@ -362,7 +406,7 @@ class GNNTrunkFn(torch.autograd.Function):
         L = len(wb) // 2
         drop = cfg.training and cfg.dropout_p > 0.0
         p = float(cfg.dropout_p) if drop else 0.0
-        seed, sbit = _new_seed() if drop else (0, 0)
+        seed, sbit, seed_keep = _new_seed(proj.device) if drop else (0, 0, None)
         dflag = nat.LG_F_DROPOUT if drop else 0
         nm = bool(cfg.node_major)
         st = stream_of(proj)
@@ -380,7 +424,7 @@ class GNNTrunkFn(torch.autograd.Function):
             flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag
             with _timed("gcn_fwd", proj.device):
                 if nm:
-                    check(lib.lg_gcn_fwd_nm(ptr(g.rowptr), ptr(g.pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
+                    check(lib.lg_gcn_fwd_nm(ptr(g.nodetab), ptr(g.pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
                                             g.nnz_cap, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed, (l + 1) | sbit, st),
                           "lg_gcn_fwd_nm")
                 else:
@@ -390,15 +434,18 @@ class GNNTrunkFn(torch.autograd.Function):
         if cfg.capture is not None:
             cfg.capture.extend((t.transpose(0, 1) if nm else t).detach().clone() for t in xs)
         ctx.cfg = cfg
+        ctx.seed_keep = seed_keep
         ctx.scale = 1.0 / (1.0 - p) if drop else 1.0
         ctx.dims = (B, S, N, D, L)
         ctx.save_for_backward(*xs, *[t.contiguous() for t in wb[0::2]])
         return xs[-1]
 
     @staticmethod
+    @_bwd32
     def backward(ctx, grad_out):
         lib = load_library()
         cfg = ctx.cfg
+        grad_out = _f32(grad_out)
         B, S, N, D, L = ctx.dims
         saved = ctx.saved_tensors
         xs, Ws = saved[:L + 1], saved[L + 1:]
@@ -419,7 +466,7 @@ class GNNTrunkFn(torch.autograd.Function):
             slot_p, dbias_p = (ptr(cfg.sensor_slot), ptr(dbias)) if first else (None, None)
             with _timed("gcn_bwd", dy.device):
                 if nm:
-                    check(lib.lg_gcn_bwd_nm(ptr(g.rowptr_t), ptr(g.pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                    check(lib.lg_gcn_bwd_nm(ptr(g.nodetab_t), ptr(g.pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                             ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D, flags,
                                             ctx.scale, ctx.scale, ptr(ws), st), "lg_gcn_bwd_nm")
                 else:
@@ -464,8 +511,10 @@ class HeadsFn(torch.autograd.Function):
     """
 
     @staticmethod
+    @_fwd32
     def forward(ctx, cfg: HeadsConfig, h, w1, b1, w2, b2, nw1, nb1, nw2, nb2):
         lib = load_library()
+        h, w1, b1, w2, b2, nw1, nb1, nw2, nb2 = (_f32(t) for t in (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2))
         h = h.contiguous()
         require_device(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
         nm = bool(cfg.node_major)
@@ -477,7 +526,7 @@ class HeadsFn(torch.autograd.Function):
         P = inc.num_pipes
         pe = float(cfg.dropout_p) if cfg.training else 0.0
         pn = float(cfg.dropout_p if cfg.noleak_p is None else cfg.noleak_p) if cfg.training else 0.0
-        seed, sbit = _new_seed() if (pe > 0.0 or pn > 0.0) else (0, 0)
+        seed, sbit, seed_keep = _new_seed(h.device) if (pe > 0.0 or pn > 0.0) else (0, 0, None)
         fe = nat.LG_F_DROPOUT if pe > 0.0 else 0
         fn = nat.LG_F_DROPOUT if pn > 0.0 else 0
         st = stream_of(h)
@@ -498,11 +547,12 @@ class HeadsFn(torch.autograd.Function):
                                        ptr(logits), P + 1, P, B, N, D, nhidden, fn | lay, pn, seed,
                                        NOLEAK_HEAD_SALT | sbit, st),
                   "lg_pool_head_fwd")
-        ctx.cfg, ctx.drop = cfg, (pe, fe, pn, fn, seed)
+        ctx.cfg, ctx.drop, ctx.seed_keep = cfg, (pe, fe, pn, fn, seed), seed_keep
         ctx.save_for_backward(h, w1c, w2c, ehid, pooled, hid, nw1c, nw2c)
         return logits
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dlogits):
         lib = load_library()
         h, w1, w2, ehid, pooled, hid, nw1, nw2 = ctx.saved_tensors
@@ -514,7 +564,7 @@ class HeadsFn(torch.autograd.Function):
         P, hidden, nhidden = inc.num_pipes, w1.shape[0], nw1.shape[0]
         dev = h.device
         st = stream_of(h)
-        dl = dlogits.contiguous()
+        dl = _f32(dlogits).contiguous()
         dpipe = torch.empty(B, P, 2, D, device=dev)
         dw1, db1 = torch.empty_like(w1), torch.empty(hidden, device=dev)
         dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
@@ -541,7 +591,7 @@ class HeadsFn(torch.autograd.Function):
 def pipe_features(h: torch.Tensor, inc: Incidence) -> torch.Tensor:
     """feat = cat[h_u, h_v, |h_u - h_v|] per pipe (lg_pipe_gather_fwd); no autograd."""
     lib = load_library()
-    h = h.contiguous()
+    h = _f32(h).contiguous()
     require_device(h)
     B, N, D = h.shape
     _check_d(D)
@@ -555,9 +605,10 @@ class MeanPoolWindowsFn(torch.autograd.Function):
     """global_mean_pool for B equal windows of N rows (batch = arange(B).repeat_interleave(N))."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, x, B: int, N: int):
         lib = load_library()
-        x = x.contiguous()
+        x = _f32(x).contiguous()
         require_device(x)
         D = x.shape[-1]
         _check_d(D)
@@ -567,6 +618,7 @@ class MeanPoolWindowsFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dout):
         B, N = ctx.dims
         return (dout / float(N)).unsqueeze(1).expand(B, N, dout.shape[-1]).reshape(B * N, -1), None, None
@@ -577,10 +629,12 @@ class GRUEncoderFn(torch.autograd.Function):
     sequences, x_t = [residual[b, t, s], tfeat[b, t, :]] read in place (lg_gru_fwd / lg_gru_bwd)."""
 
     @staticmethod
+    @_fwd32
     def forward(ctx, residual, tfeat, w_ih, w_hh, b_ih, b_hh):
         lib = load_library()
-        residual = residual.contiguous().float()
-        tfeat = tfeat.contiguous().float() if tfeat is not None else None
+        residual = _f32(residual).contiguous()
+        tfeat = _f32(tfeat).contiguous() if tfeat is not None else None
+        w_ih, w_hh, b_ih, b_hh = (_f32(t).contiguous() for t in (w_ih, w_hh, b_ih, b_hh))
         require_device(residual, tfeat, w_ih, w_hh, b_ih, b_hh)
         B, L, S = residual.shape
         G, I = w_ih.shape
@@ -600,9 +654,11 @@ class GRUEncoderFn(torch.autograd.Function):
         return h_last.view(B, S, H)
 
     @staticmethod
+    @_bwd32
     def backward(ctx, dh):
         lib = load_library()
         residual, tfeat, w_ih, w_hh, h_seq, gates = ctx.saved_tensors
+        dh = _f32(dh)
         B, L, S, I, H = ctx.dims
         dev = residual.device
         need_dx = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
@@ -625,7 +681,7 @@ class GRUEncoderFn(torch.autograd.Function):
 def spmm(graph: GCNGraph, x: torch.Tensor, B: int = 1) -> torch.Tensor:
     """y = Ahat x (PyG propagate with gcn_norm weights) for B stacked windows; no autograd."""
     lib = load_library()
-    x = x.contiguous()
+    x = _f32(x).contiguous()
     require_device(x)
     D = x.shape[-1]
     _check_d(D)

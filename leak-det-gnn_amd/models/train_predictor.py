@@ -6,8 +6,10 @@ models/train_predictor.py): same CLI flags (:95-109), split (:46-56), loop order
 
 Differences that do not change results: batches come from datasets.DeviceBatchLoader
 (scenes resident in HBM, one gather per batch; --loader torch restores the
-DataLoader path), and checkpoints store the standardizer as float32 tensors so they
-load with torch.load(weights_only=True).
+DataLoader path), and checkpoints store the standardizer as plain lists of floats: they
+load with torch.load(weights_only=True), and the reference's loaders
+(train_detector.py / event_evaluator.py: np.asarray(std_mean, dtype=np.float32) after a
+load with map_location=cuda) accept them on any device.
 """
 from __future__ import annotations
 
@@ -163,8 +165,8 @@ def main(argv=None) -> None:
         print(f"{now()} [predictor][epoch {epoch:02d}] done. train_loss={train_loss:.6f} "
               f"val_mae={val_metrics['mae']:.4f} val_rmse={val_metrics['rmse']:.4f}")
         ckpt = {"epoch": epoch, "arch": args.arch, "model_state": model.state_dict(),
-                "standardizer_mean": torch.from_numpy(stdzr.mean.copy()),
-                "standardizer_std": torch.from_numpy(stdzr.std.copy()),
+                "standardizer_mean": [float(v) for v in stdzr.mean],
+                "standardizer_std": [float(v) for v in stdzr.std],
                 "sensor_ids": sensor_ids, "args": vars(args)}
         torch.save(ckpt, last_path)
         if val_metrics["rmse"] < best_rmse:

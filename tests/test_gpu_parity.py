@@ -365,24 +365,24 @@ def test_gcn_node_major_matches_window_major(B, D, drop):
     xn = x.transpose(0, 1).contiguous()
     yn = torch.empty_like(xn)
     F32 = ops.nat.LG_F_F32_MFMA
-    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                 ops.ptr(yn), B, N, D, graph.nnz_cap, flags | F32, p, seed, salt, st), "fwd_nm")
     assert torch.equal(yn.transpose(0, 1), y), "node-major forward (f32 MFMA) must match the window-major kernel bit for bit"
     for lab in (ops.nat.LG_F_LAB_V1, F32 | (1 << 24), F32 | (3 << 24)):  # other schedules: same bits
         y2 = torch.empty_like(xn)
-        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                     ops.ptr(y2), B, N, D, graph.nnz_cap, flags | lab, p, seed, salt, st), "fwd_nm lab")
         assert torch.equal(y2, yn), f"schedule {lab:#x} changed the forward"
     # default transform (3-way split bf16 MFMA): fp32-level accuracy, bar 1e-6 of the output scale
     ys = torch.empty_like(xn)
-    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                 ops.ptr(ys), B, N, D, graph.nnz_cap, flags, p, seed, salt, st), "fwd_nm split")
     scale = yn.abs().amax().item()
     err = (ys.double() - yn.double()).abs().max().item()
     assert err <= 1e-6 * scale, f"split transform off by {err:.3e} (scale {scale:.3e})"
     for lab in (1 << 24, 3 << 24):  # split schedules agree bit for bit
         y2 = torch.empty_like(xn)
-        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                     ops.ptr(y2), B, N, D, graph.nnz_cap, flags | lab, p, seed, salt, st), "split lab")
         assert torch.equal(y2, ys), f"split schedule {lab:#x} changed the forward"
     # backward with both masks and the node-bias sum
@@ -399,7 +399,7 @@ def test_gcn_node_major_matches_window_major(B, D, drop):
         dW, db, dnb = (torch.empty(D, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV))
         if nm:
             ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
-            ops.check(lib.lg_gcn_bwd_nm(ops.ptr(graph.rowptr_t), ops.ptr(graph.pairs_t), ops.ptr(dd), ops.ptr(yy),
+            ops.check(lib.lg_gcn_bwd_nm(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t), ops.ptr(dd), ops.ptr(yy),
                                         ops.ptr(xx), ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db),
                                         ops.ptr(slot), ops.ptr(dnb), B, N, D, bflags, sc, sc, ops.ptr(ws), st),
                       "bwd_nm")
@@ -630,11 +630,11 @@ def test_gcn_node_major_high_degree_graph(D):
                                  ops.ptr(b), ops.ptr(y), B, N, D, graph.nnz_cap, flags, 0.2, 5, 3, st), "fwd")
         xn = x.transpose(0, 1).contiguous()
         yn = torch.empty_like(xn)
-        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                     ops.ptr(yn), B, N, D, graph.nnz_cap, flags | ops.nat.LG_F_F32_MFMA, 0.2, 5, 3, st),
                   "fwd_nm")
         assert torch.equal(yn.transpose(0, 1), y)
         ys = torch.empty_like(xn)
-        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                     ops.ptr(ys), B, N, D, graph.nnz_cap, flags, 0.2, 5, 3, st), "fwd_nm split")
         assert (ys.double() - yn.double()).abs().max().item() <= 1e-6 * yn.abs().amax().item()

@@ -92,7 +92,7 @@ def test_captured_forward_reads_device_seeds():
     orig = ops._new_seed
     for got, sd in zip(outs, seeds):
         it = iter(sd)
-        ops._new_seed = lambda: (next(it), 0)
+        ops._new_seed = lambda device=None: (next(it), 0, None)
         try:
             with torch.no_grad():
                 ref = m(r, tf)

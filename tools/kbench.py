@@ -18,10 +18,34 @@ from models import ops
 from models.ops import GCNGraph, Incidence, check, ptr
 
 
+GRAPH = True  # time iters launches captured in one HIP graph (host launch cost out of the loop)
+
+
 def timeit(fn, iters):
+    """Mean device time per call (us): `iters` back-to-back calls captured in one HIP graph
+    and replayed (so Python / ctypes launch overhead cannot starve the GPU between these
+    short kernels); eager launches with --eager."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    if GRAPH:
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(iters):
+                    fn()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(3):
+            g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) * 1e3 / (3 * iters)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(iters):
@@ -41,7 +65,10 @@ def main():
     ap.add_argument("--edgelab", default="", help="comma list of lg_edge_head_fwd lab bits (1 nomfma, 2 noload, "
                                                    "4 nosplit; LEAKGNN_LIB=lib/lab build only)")
     ap.add_argument("--nmlab", default="", help="comma list of lg_gcn_fwd_nm schedules: v1 or bpc<n> (train mode)")
+    ap.add_argument("--eager", action="store_true", help="time eager launches instead of a replayed HIP graph")
     args = ap.parse_args()
+    global GRAPH
+    GRAPH = not args.eager
     lib = nat.load_library()
     dev = torch.device("cuda:0")
     g = np.load(REPO / "tests/golden/graph_ltown_a.npz")
@@ -50,7 +77,8 @@ def main():
     graph = GCNGraph.build(ei, N, dev)
     inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), N, dev)
     P = inc.num_pipes
-    st = torch.cuda.current_stream().cuda_stream
+    def cs():  # launch stream = torch's current stream at CALL time (graph capture switches it)
+        return torch.cuda.current_stream().cuda_stream
     x = torch.randn(B, N, D, device=dev)
     y = torch.empty_like(x)
     W = torch.randn(D, D, device=dev) / 8
@@ -61,38 +89,39 @@ def main():
     which = args.which.split(",")
     if "gcn_fwd" in which:
         f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
-                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU, 0.0, 0, 0, st), "fwd")
+                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU, 0.0, 0, 0, cs()), "fwd")
         t = timeit(f, args.iters)
         res["gcn_fwd"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     if "gcn_fwd_train" in which:
         f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
                                          ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT, 0.1,
-                                         123, 1, st), "fwd")
+                                         123, 1, cs()), "fwd")
         t = timeit(f, args.iters)
         res["gcn_fwd_train"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     for lab in [int(v) for v in args.lab.split(",") if v]:
         f = lambda: check(lib.lg_gcn_fwd(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(W), ptr(bias),
-                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | lab, 0.0, 0, 0, st), "fwd")
+                                         ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | lab, 0.0, 0, 0, cs()), "fwd")
         res[f"gcn_fwd_lab{lab >> 20}"] = {"us": timeit(f, args.iters)}
     # node-major kernels (x, y as [N][B][D]; same bytes)
     for name, fl in (("gcn_fwd_nm", 0), ("gcn_fwd_nm_train", nat.LG_F_DROPOUT)):
         if name in which:
-            f = lambda fl=fl: check(lib.lg_gcn_fwd_nm(ptr(graph.rowptr), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias),
+            f = lambda fl=fl: check(lib.lg_gcn_fwd_nm(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias),
                                                       ptr(y), B, N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | fl, 0.1, 123,
-                                                      1, st), name)
+                                                      1, cs()), name)
             t = timeit(f, args.iters)
             res[name] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     for lab in [v for v in args.nmlab.split(",") if v]:
         bits = 0
         for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
-            bits |= {"v1": nat.LG_F_LAB_V1, "nomfma": 1 << 28, "noload": 2 << 28, "f32": nat.LG_F_F32_MFMA}.get(tok, 0)
+            bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "nomfma": 1 << 28,
+                     "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA}.get(tok, 0)
             if tok.startswith("bpc"):
                 bits |= int(tok[3:]) << 24
         for mode, fl in (("eval", 0), ("train", nat.LG_F_DROPOUT)):
-            f = lambda fl=fl, bits=bits: check(lib.lg_gcn_fwd_nm(ptr(graph.rowptr), ptr(graph.pairs), ptr(x), ptr(W),
+            f = lambda fl=fl, bits=bits: check(lib.lg_gcn_fwd_nm(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W),
                                                                  ptr(bias), ptr(y), B, N, D, E1,
                                                                  nat.LG_F_BIAS | nat.LG_F_RELU | fl | bits, 0.1, 123,
-                                                                 1, st), "nmlab")
+                                                                 1, cs()), "nmlab")
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     if "gcn_bwd_nm" in which:
@@ -102,14 +131,18 @@ def main():
         dW = torch.empty(D, D, device=dev)
         db = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
-        f = lambda: check(lib.lg_gcn_bwd_nm(ptr(graph.rowptr_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
+        f = lambda: check(lib.lg_gcn_bwd_nm(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
                                             ptr(dx), ptr(dW), ptr(db), None, None, B, N, D,
-                                            nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), st), "bwd_nm")
+                                            nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), cs()), "bwd_nm")
         t = timeit(f, args.iters)
         res["gcn_bwd_nm"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
+    if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
+        f = lambda: y.copy_(x)
+        t = timeit(f, args.iters)
+        res["copy"] = {"us": t, "GBps": 8 * B * N * D / t / 1e3}
     if "spmm" in which:
         f = lambda: check(lib.lg_spmm(ptr(graph.rowptr), ptr(graph.col), ptr(graph.w), ptr(x), ptr(y), B, N, D, E1,
-                                      st), "spmm")
+                                      cs()), "spmm")
         t = timeit(f, args.iters)
         res["spmm"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
     if "gcn_bwd" in which:
@@ -121,7 +154,7 @@ def main():
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
         f = lambda: check(lib.lg_gcn_bwd(ptr(graph.rowptr_t), ptr(graph.col_t), ptr(graph.w_t), ptr(dy), ptr(yy),
                                          ptr(x), ptr(W), ptr(dx), ptr(dW), ptr(db), None, None, B, N, D, E1,
-                                         nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), st), "bwd")
+                                         nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), cs()), "bwd")
         t = timeit(f, args.iters)
         res["gcn_bwd"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
     if "edge_fwd" in which or "edge_bwd" in which:
@@ -132,7 +165,7 @@ def main():
         lo = torch.empty(B, P, device=dev)
         hid = torch.empty(B * P, 128, device=dev)
         f = lambda: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(lo), P,
-                                               ptr(hid), B, N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, st), "edge fwd")
+                                               ptr(hid), B, N, P, D, 128, nat.LG_F_DROPOUT, 0.1, 5, 101, cs()), "edge fwd")
         if "edge_fwd" in which:
             t = timeit(f, args.iters)
             res["edge_fwd"] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
@@ -140,7 +173,7 @@ def main():
             for name, fl, hp in [("edge_fwd_nohid", nat.LG_F_DROPOUT, None), ("edge_fwd_eval", 0, None)] + labs:
                 g = lambda fl=fl, hp=hp: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2),
                                                                     ptr(b2), ptr(lo), P, hp, B, N, P, D, 128, fl, 0.1,
-                                                                    5, 101, st), name)
+                                                                    5, 101, cs()), name)
                 t = timeit(g, args.iters)
                 res[name] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
         else:
@@ -152,7 +185,7 @@ def main():
             ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=dev, dtype=torch.uint8)
             f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(W2), ptr(hid), ptr(dl), P,
                                                    ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
-                                                   nat.LG_F_DROPOUT, 0.1, ptr(ws), st), "edge bwd")
+                                                   nat.LG_F_DROPOUT, 0.1, ptr(ws), cs()), "edge bwd")
             t = timeit(f, args.iters)
             res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
     if "gru_fwd" in which or "gru_bwd" in which:
@@ -166,15 +199,15 @@ def main():
         gt = torch.empty(L, B * S, 4, 64, device=dev)
         hl = torch.empty(B * S, 64, device=dev)
         f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), ptr(gt),
-                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd")
+                                         ptr(hl), B, L, S, 10, 64, cs()), "gru fwd")
         t = timeit(f, args.iters)
         flops = 2 * B * S * L * 192 * (64 + 10)
         res["gru_fwd"] = {"us": t, "TFLOPs": flops / t / 1e6}
         f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), None, None,
-                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd eval")
+                                         ptr(hl), B, L, S, 10, 64, cs()), "gru fwd eval")
         res["gru_fwd_eval"] = {"us": timeit(f, args.iters)}
         f = lambda: check(lib.lg_gru_fwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(bih), ptr(bhh), ptr(hs), None,
-                                         ptr(hl), B, L, S, 10, 64, st), "gru fwd hs only")
+                                         ptr(hl), B, L, S, 10, 64, cs()), "gru fwd hs only")
         res["gru_fwd_hs"] = {"us": timeit(f, args.iters)}
         if "gru_bwd" in which:
             dh = torch.randn(B * S, 64, device=dev)
@@ -182,7 +215,7 @@ def main():
             ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)), device=dev, dtype=torch.uint8)
             f = lambda: check(lib.lg_gru_bwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(hs), ptr(gt), ptr(dh), None,
                                              ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), B, L, S, 10, 64,
-                                             ptr(ws), st), "gru bwd")
+                                             ptr(ws), cs()), "gru bwd")
             t = timeit(f, args.iters)
             res["gru_bwd"] = {"us": t, "TFLOPs": 2 * flops / t / 1e6}
     if "tcn" in which:
@@ -213,7 +246,7 @@ def main():
             f = lambda: check(lib.lg_tcn_conv_fwd(ptr(xin), ptr(blk_in), ptr(dp.tables[li]), ptr(packed[li]),
                                                   ptr(conv.bias), ptr(norm.weight), ptr(norm.bias), 1e-5, ptr(out), B,
                                                   rows_prev, plan.convs[li - 2].rows if li % 2 == 1 else 0, cp.rows,
-                                                  128, st), "tcn conv")
+                                                  128, cs()), "tcn conv")
             t = timeit(f, args.iters)
             res[f"tcn_conv_l{li}"] = {"us": t, "TFLOPs": B * cp.rows * 2 * 128 * 384 / t / 1e6}
             mutils.RESIDUAL_FAST_PATH = False
