@@ -66,37 +66,62 @@ def time_features(B: int, L: int, gen: torch.Generator) -> torch.Tensor:
                       torch.nn.functional.one_hot(dow, 7).float()], dim=-1)
 
 
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
-    """Time the oracle's CPU restatement of the same step on the host cores (reported only)."""
+    """The oracle's CPU restatement of the same step timed on the host cores (reported only,
+    BASELINE.md plan): eval-mode forward and train-mode fwd+CE+bwd, median of >= 10 timed
+    steps after 3 warm-ups each (more while within the budget)."""
     from oracle.detector_ref import LeakDetectorRef
     torch.set_num_threads(threads)
     pipes = all_pipe_ids(LTA_INP)
     torch.manual_seed(0)
-    m = LeakDetectorRef(LTA_INP, SENSORS, pipes).train()
+    m = LeakDetectorRef(LTA_INP, SENSORS, pipes)
     gen = torch.Generator().manual_seed(1234)
     r = torch.randn(batch, 36, 29, generator=gen)
     tf = time_features(batch, 36, gen)
     lab = torch.randint(0, len(pipes) + 1, (batch,), generator=gen)
 
-    def step():
+    def train_step():
         m.zero_grad(set_to_none=True)
         torch.nn.functional.cross_entropy(m(r, tf), lab).backward()
 
-    step()  # warm-up
-    times = []
-    t_end = time.perf_counter() + budget_s
-    while len(times) < 2 or (time.perf_counter() < t_end and len(times) < 20):
-        t0 = time.perf_counter()
-        step()
-        times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    return {"value": batch / med, "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} train-mode fwd+CE+bwd steps of B={batch} L-TOWN-A windows, median "
-                      f"{med * 1e3:.1f} ms/step (oracle/detector_ref.py on torch CPU, {threads} threads)"}
+    def eval_fwd():
+        with torch.no_grad():
+            m(r, tf)
+
+    def timed(fn, mode):
+        m.train(mode == "train")
+        for _ in range(3):
+            fn()
+        ts = []
+        t_end = time.perf_counter() + budget_s / 2
+        while len(ts) < 10 or (time.perf_counter() < t_end and len(ts) < 30):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), len(ts)
+
+    tr, ntr = timed(train_step, "train")
+    ev, nev = timed(eval_fwd, "eval")
+    return {"value": round(batch / tr, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "eval_forward_windows_per_s": round(batch / ev, 2),
+            "train_ms_per_step": round(tr * 1e3, 1), "eval_ms_per_step": round(ev * 1e3, 1),
+            "sample": f"median of {ntr} train-mode fwd+CE+bwd steps (value) and {nev} eval-mode forwards, each "
+                      f"after 3 warm-ups, B={batch} L-TOWN-A windows (oracle/detector_ref.py on torch CPU, "
+                      f"{threads} threads, {cpu_model()})"}
 
 
-def pmc_traffic(batch: int, node_major: bool) -> dict | None:
-    """Per-launch HBM bytes of the train-mode lg_gcn_fwd from rocprofv3 PMC counters.
+def pmc_traffic(which: str, kname: str, batch: int) -> dict | None:
+    """Per-launch HBM bytes of one kbench launch from rocprofv3 PMC counters.
 
     Runs as child processes (never exec): one counter per pass, kernel trace only.
     Returns None when rocprofv3 is unavailable or a pass fails.
@@ -106,12 +131,11 @@ def pmc_traffic(batch: int, node_major: bool) -> dict | None:
         return None
     vals = {}
     env = dict(os.environ, TMPDIR="/tmp")
-    which, kname = ("gcn_fwd_nm_train", "k_gcn_fwd_nm") if node_major else ("gcn_fwd_train", "k_gcn_fwd<")
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory(dir="/tmp") as d:
             cmd = [prof, "--pmc", counter, "--kernel-trace", "-d", d, "-o", "pmc", "--output-format", "csv", "--",
                    sys.executable, str(REPO / "tools" / "kbench.py"), "--which", which, "--B", str(batch),
-                   "--iters", "20"]
+                   "--iters", "20", "--eager"]
             try:
                 subprocess.run(cmd, env=env, cwd=str(REPO), timeout=300, check=True, stdout=subprocess.DEVNULL,
                                stderr=subprocess.DEVNULL)
@@ -127,6 +151,26 @@ def pmc_traffic(batch: int, node_major: bool) -> dict | None:
             vals[counter] = sum(per.values()) / len(per)
     return {"bytes": (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, "FETCH_SIZE_KiB": vals["FETCH_SIZE"],
             "WRITE_SIZE_KiB": vals["WRITE_SIZE"]}
+
+
+def stream_copy_peak(dev, nbytes: int = 2 << 30, iters: int = 10) -> dict:
+    """Measured copy bandwidth on this box: device copy of an nbytes fp32 buffer (past the
+    256 MiB Infinity Cache), read + write bytes over HIP-event time."""
+    x = torch.ones(nbytes // 4, device=dev)
+    y = torch.empty_like(x)
+    for _ in range(3):
+        y.copy_(x)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        y.copy_(x)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / iters
+    del x, y
+    torch.cuda.empty_cache()
+    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_moved": 2 * nbytes,
+            "method": f"torch copy_ of a {nbytes >> 20} MiB fp32 buffer (read + write), HIP events, mean of {iters}"}
 
 
 def time_propagate(graph, B: int, N: int, D: int, dev, iters: int = 50) -> float:
@@ -155,32 +199,41 @@ def time_propagate(graph, B: int, N: int, D: int, dev, iters: int = 50) -> float
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense fp32
 
 
-def e2e_training(model, opt, allreduce, label, B: int, steps: int, dev) -> dict:
+class ResidualDetector(torch.nn.Module):
+    """The reference's training forward from raw segments (train_detector.py:302-310):
+    residual build with the frozen predictor under no_grad, then the detector."""
+
+    def __init__(self, predictor, detector, l_pred: int = 36, l_det: int = 36):
+        super().__init__()
+        self.predictor, self.detector, self.l_pred, self.l_det = predictor, detector, l_pred, l_det
+
+    def forward(self, seg, tseg):
+        from models import utils as mutils
+        with torch.no_grad():
+            residual = mutils.build_residual_sequence_from_segment(self.predictor, seg, tseg, self.l_pred,
+                                                                   self.l_det, device=seg.device)
+        return self.detector(residual, tseg[:, self.l_pred:, :])
+
+
+def e2e_training(model, opt, label, B: int, steps: int, dev) -> dict:
     """Detector training steps INCLUDING the frozen-predictor residual build from raw
     (B, 72, 29) segments (train_detector.py:296-317 loop order; SURVEY §8 d: reported
-    separately from graphs/s).  Residual build = the HIP shared-window TCN path; the
-    stock per-window module path (what the reference runs) is timed beside it."""
+    separately from graphs/s), the whole step replayed as one HIP graph like the headline
+    step.  Residual build = the HIP shared-window TCN path; the stock per-window module
+    path (what the reference runs) is timed beside it."""
     from models import tcn_plan
     from models import utils as mutils
+    from models.graph_step import CapturedTrainStep
     from models.predictor import NormalPredictorTCN
     torch.manual_seed(7)
     predictor = NormalPredictorTCN(len(SENSORS), 9).to(dev).eval()
+    for p in predictor.parameters():
+        p.requires_grad_(False)
     gen = torch.Generator().manual_seed(4321)
     seg = torch.randn(B, 72, len(SENSORS), generator=gen).to(dev)
     tseg = time_features(B, 72, gen).to(dev)
-    loss_fn = torch.nn.CrossEntropyLoss()
-
-    def step():
-        with torch.no_grad():
-            residual = mutils.build_residual_sequence_from_segment(predictor, seg, tseg, 36, 36, device=dev)
-        logits = model(residual, tseg[:, 36:, :])
-        loss = loss_fn(logits, label)
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        allreduce()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
-
+    e2e = ResidualDetector(predictor, model).to(dev)
+    step = CapturedTrainStep(e2e, torch.nn.CrossEntropyLoss(), opt, (seg, tseg), label, clip=1.0, warmup=3)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -201,13 +254,73 @@ def e2e_training(model, opt, allreduce, label, B: int, steps: int, dev) -> dict:
     conv_ms = _conv_ms(predictor, plan, B, dev)
     conv_tf = conv_flop / (conv_ms * 1e-3) / 1e12
     return {"value": round(B / e2e_s, 2), "unit": "windows/s", "ms_per_step": round(e2e_s * 1e3, 4),
-            "step": "residual build (frozen TCN, 36 windows of 36 steps per segment) + detector fwd+CE+bwd+AdamW",
+            "step": "residual build (frozen TCN, 36 windows of 36 steps per segment) + detector fwd+CE+bwd+AdamW, "
+                    "one HIP-graph replay per step",
             "residual_ms": round(fast_ms, 4), "residual_ms_stock_module": round(stock_ms, 4),
             "residual_speedup": round(stock_ms / fast_ms, 2),
             "tcn_conv": {"kernel": "lg_tcn_conv_fwd x8 (shared-window rows)", "bound": "mfma",
                          "achieved": round(conv_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(conv_tf / FP32_MFMA_PEAK_TFLOPS, 4), "flop_per_call": conv_flop,
                          "ms_per_call": round(conv_ms, 4)}}
+
+
+def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
+    """BASELINE configs[3]: the detector training step on the synthetic 10k-node / 15k-pipe
+    network (30k edge columns, written as an EPANET .inp), node_hidden = sensor_hidden = 32,
+    64 windows per rank (global 512 at 8 GPUs), one HIP-graph replay per step, weak scaling.
+    Returns windows/s over all ranks (max time over ranks) and the C4 GCN forward roofline."""
+    from models import ops
+    from models.detector import LeakDetector
+    from models.graph_step import CapturedTrainStep
+    from models.synth import pick_sensors, write_synthetic_inp
+    N, P, D, B = 10_000, 15_000, 32, 64
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        inp = Path(d) / "c4.inp"
+        node_ids, pipe_ids = write_synthetic_inp(inp, N, P, seed=0)
+        sensors = pick_sensors(node_ids, 29, seed=0)
+        torch.manual_seed(0)
+        m = LeakDetector(inp, sensors, pipe_ids, sensor_hidden=D, node_hidden=D).to(dev).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    gen = torch.Generator().manual_seed(99 + rank)
+    r = torch.randn(B, 36, 29, generator=gen).to(dev)
+    tf = time_features(B, 36, gen).to(dev)
+    lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
+    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=1.0, warmup=3)
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    timer = ops.KernelTimer(["gcn_fwd"])
+    ops.set_kernel_timer(timer)
+    timer.enabled = True
+    for _ in range(5):
+        opt.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(m(r, tf), lab).backward()
+    timer.enabled = False
+    ops.set_kernel_timer(None)
+    fwd_ms = timer.mean_ms("gcn_fwd")
+    E1 = int(m.edge_index_single.shape[1]) + N
+    byts = 8 * B * N * D + 4 * (N + 1) + 8 * E1
+    gbs = byts / (fwd_ms * 1e-3) / 1e9
+    return {"metric": "windowed graphs/sec fwd+bwd, synthetic 10k nodes / 30k edge columns (BASELINE configs[3])",
+            "value": round(B * world * steps / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / steps, 4),
+            "windows_per_rank": B, "global_batch": B * world, "feat": D, "pipes": P, "scaling": "weak",
+            "roofline_gcn_fwd": {"kernel": "lg_gcn_fwd_nm (train mode)", "bound": "hbm",
+                                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": byts,
+                                 "avg_launch_us": round(fwd_ms * 1e3, 2)}}
 
 
 def _event_ms(fn, iters: int) -> float:
@@ -298,7 +411,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="windows per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline sampling")
+    ap.add_argument("--cpu-budget", type=float, default=24.0, help="seconds of CPU-baseline sampling")
+    ap.add_argument("--no-c4", action="store_true", help="skip the configs[3] (C4) leg")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--eager", action="store_true", help="launch the step eagerly instead of replaying its HIP graph")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launch-path check (no GPU, no measurement)")
@@ -362,8 +476,8 @@ def main() -> None:
         # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay)
         from models.graph_step import CapturedTrainStep
         step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=1.0, warmup=3)
-    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "node_init", "gru_fwd", "gru_bwd", "edge_fwd", "edge_bwd",
-                             "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
+    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "gcn_bwd_l0", "node_init", "gru_fwd", "gru_bwd", "edge_fwd",
+                             "edge_bwd", "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)
 
     def barrier():
@@ -382,6 +496,7 @@ def main() -> None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    final_loss = float(loss.item())
     # pass 2: per-kernel HIP-event durations over the same number of steps (eager launches:
     # the events bracket each library call on its stream)
     timer.enabled = True
@@ -389,27 +504,38 @@ def main() -> None:
         eager_step()
     barrier()
     timer.enabled = False
+    ops.set_kernel_timer(None)
     kms = {k: timer.mean_ms(k) for k in timer.names}
-    final_loss = float(loss.item())
+    # BASELINE configs[3] (C4) at every world size: 64 windows per rank, weak scaling
+    c4 = None if args.no_c4 else c4_leg(dev, max(10, args.steps // 2), 3, rank, world)
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
     ms_per_step = elapsed * 1e3 / args.steps
-    windows = B * world * args.steps
-    value = windows / elapsed
+    value = B * world * args.steps / elapsed
     D = 64
-    fwd_bytes = 8 * B * N * D + 4 * (N + 1) + 8 * E1
-    fwd_ms = kms["gcn_fwd"]
+    csr_bytes = 4 * (N + 1) + 8 * E1
+    fwd_bytes = 8 * B * N * D + csr_bytes           # read x once, write y once
+    bwd_bytes = 16 * B * N * D + csr_bytes          # layer-L-1 backward: read dy, y (mask), x; write dx
+    fwd_ms, bwd_ms = kms["gcn_fwd"], kms["gcn_bwd"]
     achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     graph = model._device_state(dev)[0]
     prop_ms = time_propagate(graph, B, N, D, dev)
     prop_gbs = fwd_bytes / (prop_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(B, ops.TRUNK_NODE_MAJOR) if (world == 1 and not args.no_pmc) else None
+    copy = stream_copy_peak(dev)
+    pmc = world == 1 and not args.no_pmc
+    traffic = pmc_traffic("gcn_fwd_nm_train", "k_gcn_fwd_nm", B) if pmc else None
+    traffic_bwd = pmc_traffic("gcn_bwd_nm", "k_gcn_bwd_nm", B) if pmc else None
+    gru_flop = 2 * B * len(SENSORS) * 36 * 192 * (64 + 10)
+    gru_tf = {k: gru_flop * (2 if k == "gru_bwd" else 1) / (kms[k] * 1e-3) / 1e12 for k in ("gru_fwd", "gru_bwd")}
+    src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, 2*FETCH+WRITE (gfx950)"
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
-        "n_gpus": world, "ranks_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "n_gpus": world, "ranks_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic residual windows (B,36,29) + time features, random-init weights",
         "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",
@@ -417,22 +543,33 @@ def main() -> None:
                    "global_batch": B * world, "feat": D, "gnn_layers": 2, "parallelism": f"dp{world}",
                    "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode",
                    "launch": "eager" if args.eager else "hipgraph (one replay per step, dropout re-drawn on device)"},
-        "roofline": {"kernel": ("lg_gcn_fwd_nm" if ops.TRUNK_NODE_MAJOR else "lg_gcn_fwd")
-                     + " (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
+        "roofline": {"kernel": "lg_gcn_fwd_nm (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(traffic["bytes"]) if traffic else None,
-                     "traffic_source": ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, "
-                                        "2*FETCH+WRITE (gfx950)") if traffic else None,
-                     "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
+                     "traffic_source": src if traffic else None,
+                     "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2),
+                     "frac_of_measured_copy": round(achieved / copy["GBps"], 4)},
+        "roofline_bwd": {"kernel": "lg_gcn_bwd_nm (layer 2: gather of dy * [y > 0] over the transposed CSR, "
+                                   "dx = t W, dW, db, masked by [x > 0])", "bound": "hbm",
+                         "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": round(traffic_bwd["bytes"]) if traffic_bwd else None,
+                         "traffic_source": src if traffic_bwd else None,
+                         "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2)},
         "roofline_propagate": {"kernel": "lg_spmm (K6 alone, same graph and shape)", "bound": "hbm",
                                "achieved": round(prop_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(prop_gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(prop_ms * 1e3, 2)},
+        "stream_copy": copy,
+        "gru_mfma": {k: {"achieved": round(v, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(v / FP32_MFMA_PEAK_TFLOPS, 4)} for k, v in gru_tf.items()},
         "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
         "final_loss": round(final_loss, 4),
     }
+    if c4 is not None:
+        out["c4"] = c4
     if world == 1:
-        out["e2e_training"] = e2e_training(model, opt, allreduce, label, B, max(5, args.steps // 2), dev)
+        out["e2e_training"] = e2e_training(model, opt, label, B, max(5, args.steps // 2), dev)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(B, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
     print(json.dumps(out), flush=True)

@@ -30,6 +30,7 @@ namespace {
 
 constexpr int kNmFwdWaves = 8;
 constexpr int kNmBwdWaves = 8;
+constexpr int kNmBwdWaves3 = 4;
 constexpr uint32_t kNmOob = 0xFFFFFFF0u;
 
 __device__ __forceinline__ f32x4 mfma_nm(float a, float b, f32x4 c) {
@@ -566,12 +567,12 @@ constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
 // 2 = skip the neighbour loads, 4 = skip the y stores (kept behind a runtime-false test so
 // the transform is not dead code).  DST: epilogue stores straight from the MFMA layout
 // (16 rows x 64 B per store) instead of through the LDS tile.
-template <int D, bool DROP, bool SPLIT, int WAVES, int LAB = 0, bool DST = false>
+template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false>
 __global__ void __launch_bounds__(64 * WAVES)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
-              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
-              uint64_t seed, uint32_t salt) {
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
+              uint32_t salt) {
     using G = NmGeo<D>;
     using LY = Nm3Lds<D, SPLIT, WAVES>;
     constexpr int SB = LY::SB;
@@ -678,11 +679,16 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         tile_coords(tile + sc.stride, nn, nb0, nnb);
         const NmRec nxt = nm_rec(tab, nn);
         asm volatile("" ::: "memory");  // keep the request here: the compiler would sink it to its use
+        // CSR order from 0: the first term is the product itself (an absent first neighbour
+        // loaded zeros, and its weight is taken as 0), the rest fma'd in
         f32x4 acc[G::K];
+        {
+            const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
 #pragma unroll
-        for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int k = 0; k < G::K; ++k) acc[k] = pf[0][k] * w;
+        }
 #pragma unroll
-        for (int i = 0; i < NPF; ++i) {
+        for (int i = 1; i < NPF; ++i) {
             if (e0 + i < e1) {
                 const float w = __int_as_float(cur.p[i].y);
 #pragma unroll
@@ -786,24 +792,27 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // epilogue: ReLU, row-stream dropout seeded with the window-major row id (b0 + j) N + n
+        // epilogue: ReLU, row-stream dropout seeded with the window-major row id (b0 + j) N + n,
+        // both as ONE select per element (no fmaxf: its NaN canonicalisation costs a VALU op)
         uint32_t st = 0;
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                float t = fmaxf(o[mt][reg], relu_floor);
+                const float v = o[mt][reg];
+                bool keep = true;
                 if constexpr (DROP) {
                     if ((reg & 1) == 0) st = lg_xorshift32(st);
                     const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
-                    t = u16 >= thr ? t : 0.0f;
+                    keep = u16 >= thr;
                 }
-                o[mt][reg] = t;
+                if constexpr (RELU) keep = keep && v > 0.f;
+                o[mt][reg] = keep ? v : 0.0f;
             }
         }
         const uint32_t ob = (n * B + b0) * (4u * D);
-        const bool do_store = (LAB & 4) == 0 || relu_floor == 1234.5f;
+        const bool do_store = (LAB & 4) == 0 || dscale == 1234.5f;
         if constexpr (DST) {
             // lane (j, q) holds row j, channels 16 mt + 4 q .. + 3
             const uint32_t so = j < static_cast<int>(nb) ? static_cast<uint32_t>(j) * (4u * D) + 16u * q : kNm3RowOob;
@@ -998,6 +1007,348 @@ k_gcn_bwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
 }
 
+
+// ------------------------------------------------------------------ backward, node-table pipeline
+// lg_gcn_bwd_nm on k_gcn_fwd_nm3's pipeline: the tile's CSR record (transposed CSR) is one
+// scalar load issued a tile ahead; the tile's NPF first neighbour dz blocks (MASK_IN: and
+// their y blocks for the [y > 0] mask) and its own x block are in flight under the previous
+// tile's MFMA work; the row's self entry (the node table's `self`) supplies the tile's own
+// dz rows for db, so the own dy / y blocks are not read twice.  Both GEMMs run on bf16
+// MFMA with 3-way split operands (split_bf16.h, fp32-level accuracy):
+//   dx^T = W^T t^T   (16x16x32, W^T split once per workgroup in LDS)
+//   dW  += t^T x     (16x16x16, K = the tile's 16 rows; t and x columns split per tile)
+// The round-1 kernel (k_gcn_bwd_nm) walked rowptr -> pair -> block as dependent round trips
+// and ran dW and dx on f32 MFMA (4096 cycles per tile against 1536 here).
+template <int D, bool MASK_IN>
+struct Nb3Lds {
+    static constexpr int SB = D + 8;
+    static constexpr int WF = (3 * D * SB) / 2;          // W^T split parts (bf16), in floats
+    static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
+    static constexpr int L = D * D + 2 * D;               // slab row: dW, db, d(node bias)
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L);
+};
+
+template <int D, bool MASK_IN, bool NB>
+__global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
+k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
+              const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
+              const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out) {
+    using G = NmGeo<D>;
+    using LY = Nb3Lds<D, MASK_IN>;
+    constexpr int SB = LY::SB;
+    constexpr int NPF = MASK_IN ? 2 : 4;
+    constexpr int L = LY::L;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // 3 x W^T [in][out] bf16, stride SB
+    float* tiles = reinterpret_cast<float*>(smem) + LY::WF;
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* tl = tiles + wave * LY::TL;  // t tile [row][feature], later dx
+    float* xl = tl + G::TILE;           // x tile [row][feature]
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MASK_IN ? yv : dy, bytes),
+                                 xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmBwdWaves3);
+    const int64_t tend = sc.end;
+
+    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+        const bool valid = tile < tend;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        n = t32 - grp * N;
+        b0 = grp * 16;
+        nb = valid ? min(16u, B - b0) : 0u;
+    };
+    auto ld = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    };
+    // dz of one loaded block: MASK_IN applies this layer's relu/dropout backward
+    auto dzf = [&](const f32x4& g, const f32x4& m) {
+        if constexpr (!MASK_IN) return g;
+        f32x4 r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) r[c] = m[c] > 0.f ? g[c] * scale_in : 0.f;
+        return r;
+    };
+
+    // tile in flight: record, coordinates, lane offsets, first NPF neighbour blocks, own x block
+    f32x4 pf[NPF][G::K], pm[MASK_IN ? NPF : 1][G::K], px[G::K];
+    uint32_t lo[G::K];
+    NmRec cur;
+    uint32_t cn, cb0;
+    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+        cur = r;
+        cn = n;
+        cb0 = b0;
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+        const uint32_t ob = nb ? (n * B + b0) * (4u * D) : kNm3BlkOob;
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            const bool have = r.e0 + i < r.e1;
+            const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : kNm3BlkOob;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) {
+                pf[i][k] = ld(dys, lo[k] + base);
+                if constexpr (MASK_IN) pm[i][k] = ld(ms, lo[k] + base);
+            }
+        }
+    };
+    {
+        uint32_t n0, b00, nb00;
+        tile_coords(sc.first, n0, b00, nb00);
+        issue(nm_rec(tab, n0), n0, b00, nb00);
+    }
+    // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
+            if (i4 >= W4) continue;
+            const int o = i4 / (D / 4), c4 = 4 * (i4 % (D / 4));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float w = wv[u][c];
+                const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
+                const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
+                const uint16_t h1 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r1));
+                const float r2 = r1 - __uint_as_float(static_cast<uint32_t>(h1) << 16);
+                const uint16_t h2 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r2));
+                const int e = (c4 + c) * SB + o;
+                wsl[e] = h0;
+                wsl[D * SB + e] = h1;
+                wsl[2 * D * SB + e] = h2;
+            }
+        }
+    }
+    __syncthreads();
+
+    f32x4 dw[G::CH][G::CH];  // dW tile (mo, ni): rows o = 16mo + 4q + reg, cols i = 16ni + j
+#pragma unroll
+    for (int a = 0; a < G::CH; ++a)
+#pragma unroll
+        for (int b = 0; b < G::CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // channels 4fg..4fg+3, summed over this lane's rows
+    f32x4 nbacc[NB ? G::CH : 1];              // NB: channels 16mt + 4q + reg over this lane's rows j
+#pragma unroll
+    for (int mt = 0; mt < (NB ? G::CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int64_t tile = sc.first; tile < tend; tile += sc.stride) {
+        const uint32_t n = cn, b0 = cb0;
+        const int e0 = cur.e0, e1 = cur.e1, self = cur.self;
+        uint32_t tlo[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
+        uint32_t nn, nb0, nnb;
+        tile_coords(tile + sc.stride, nn, nb0, nnb);
+        const NmRec nxt = nm_rec(tab, nn);
+        asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
+        f32x4 acc[G::K], xv[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            xv[k] = px[k];
+        }
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            if (e0 + i < e1) {
+                const float w = __int_as_float(cur.p[i].y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) {
+                    const f32x4 z = dzf(pf[i][k], MASK_IN ? pm[i < (MASK_IN ? NPF : 1) ? i : 0][k] : pf[i][k]);
+                    pk_fma4(acc[k], w, z);
+                    if (i == self) dbacc += z;
+                }
+            }
+        }
+        if (e0 + NPF < e1) {  // the rest of the row: inline pairs, then the pair array
+            int2 ip[kLgNmInline - NPF];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) ip[i] = cur.p[NPF + i];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) {
+                if (e0 + NPF + i < e1) {
+                    const uint32_t ba = (static_cast<uint32_t>(ip[i].x) * B + b0) * (4u * D);
+                    f32x4 va[G::K], vm[G::K];
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) {
+                        va[k] = ld(dys, tlo[k] + ba);
+                        vm[k] = MASK_IN ? ld(ms, tlo[k] + ba) : va[k];
+                    }
+                    const float wa = __int_as_float(ip[i].y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) {
+                        const f32x4 z = dzf(va[k], vm[k]);
+                        pk_fma4(acc[k], wa, z);
+                        if (NPF + i == self) dbacc += z;
+                    }
+                }
+            }
+            for (int e = e0 + kLgNmInline; e < e1; ++e) {
+                const int2 pa = pairs[e];
+                const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                f32x4 va[G::K], vm[G::K];
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) {
+                    va[k] = ld(dys, tlo[k] + ba);
+                    vm[k] = MASK_IN ? ld(ms, tlo[k] + ba) : va[k];
+                }
+                const float wa = __int_as_float(pa.y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, dzf(va[k], vm[k]));
+            }
+        }
+        if (self < 0) {  // no self entry among the inline pairs: the own dz rows explicitly
+            const uint32_t ob = (n * B + b0) * (4u * D);
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) dbacc += dzf(ld(dys, tlo[k] + ob), MASK_IN ? ld(ms, tlo[k] + ob) : f32x4{});
+        }
+        issue(nxt, nn, nb0, nnb);
+        __builtin_amdgcn_sched_barrier(0);
+
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+            st4(xl + (G::RPI * k + rl) * G::S + 4 * fg, xv[k]);
+        }
+        wave_sync_nm();
+        // dW += t^T x over the tile's 16 rows: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
+        {
+            lg_i16x4 xb[G::CH][3];
+#pragma unroll
+            for (int ni = 0; ni < G::CH; ++ni) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j];
+                lg_u32x2 f0, f1, f2;
+                split3_x4(v, f0, f1, f2);
+                xb[ni][0] = __builtin_bit_cast(lg_i16x4, f0);
+                xb[ni][1] = __builtin_bit_cast(lg_i16x4, f1);
+                xb[ni][2] = __builtin_bit_cast(lg_i16x4, f2);
+            }
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j];
+                lg_u32x2 f0, f1, f2;
+                split3_x4(v, f0, f1, f2);
+                const lg_i16x4 a0 = __builtin_bit_cast(lg_i16x4, f0), a1 = __builtin_bit_cast(lg_i16x4, f1),
+                                a2 = __builtin_bit_cast(lg_i16x4, f2);
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni) {
+                    f32x4 c = dw[mo][ni];
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, xb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, xb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, xb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][1], c, 0, 0, 0);
+                    dw[mo][ni] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][0], c, 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        // dx^T[i][row] = sum_o W^T[i][o] t[row][o]
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < D / 32; ++s2) {
+            lg_bf16x8 b0f, b1f, b2f;
+            split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f, b2f);
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
+                const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
+                o[mt] = mfma_bf(a2, b0f, o[mt]);
+                o[mt] = mfma_bf(a1, b1f, o[mt]);
+                o[mt] = mfma_bf(a0, b2f, o[mt]);
+                o[mt] = mfma_bf(a1, b0f, o[mt]);
+                o[mt] = mfma_bf(a0, b1f, o[mt]);
+                o[mt] = mfma_bf(a0, b0f, o[mt]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (mask_out) {
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
+            }
+        }
+        if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
+            if (node_slot[n] < 0)
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) nbacc[mt] += o[mt];
+        }
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        wave_sync_nm();
+        const uint32_t ob = (n * B + b0) * (4u * D);
+#pragma unroll
+        for (int k = 0; k < G::K; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg)),
+                dxs, tlo[k] + ob, 0, 0);
+    }
+    if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
+    }
+    // ---- per-block reduction of dW / db / node bias (fixed wave order -> deterministic)
+#pragma unroll
+    for (int off = G::LPR; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // reuse the whole LDS image
+    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
+    for (int wv2 = 0; wv2 < kNmBwdWaves3; ++wv2) {
+        __syncthreads();
+        if (wave == wv2) {
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo)
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg)
+                        red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
+            if (lane < G::LPR)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
+            if (NB && j == 0)
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
+        }
+    }
+    __syncthreads();
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
+}
+
 template <typename Kern>
 int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int cap_per_cu) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1027,15 +1378,15 @@ auto nm2_kernel(int flags) {
 #endif
     return split ? k_gcn_fwd_nm2<D, DR, 4, true, 0> : k_gcn_fwd_nm2<D, DR, 4, false, 0>;
 }
-template <int D, bool DR, int WV>
+template <int D, bool DR, bool RL, int WV>
 auto nm3_kernel(int flags) {
     const bool split = (flags & LG_F_F32_MFMA) == 0;
 #ifdef LG_KERNEL_LAB
     const bool dst = (flags & LG_F_LAB_DST) != 0;
-#define LG_NM3_LAB(L)                                                                                      \
-    case L:                                                                                                \
-        return split ? (dst ? k_gcn_fwd_nm3<D, DR, true, WV, L, true> : k_gcn_fwd_nm3<D, DR, true, WV, L>) \
-                     : (dst ? k_gcn_fwd_nm3<D, DR, false, WV, L, true> : k_gcn_fwd_nm3<D, DR, false, WV, L>);
+#define LG_NM3_LAB(L)                                                                                              \
+    case L:                                                                                                        \
+        return split ? (dst ? k_gcn_fwd_nm3<D, DR, RL, true, WV, L, true> : k_gcn_fwd_nm3<D, DR, RL, true, WV, L>) \
+                     : (dst ? k_gcn_fwd_nm3<D, DR, RL, false, WV, L, true> : k_gcn_fwd_nm3<D, DR, RL, false, WV, L>);
     switch ((flags >> 28) & 7) {
         LG_NM3_LAB(0)
         LG_NM3_LAB(1)
@@ -1049,7 +1400,7 @@ auto nm3_kernel(int flags) {
     }
 #undef LG_NM3_LAB
 #endif
-    return split ? k_gcn_fwd_nm3<D, DR, true, WV, 0> : k_gcn_fwd_nm3<D, DR, false, WV, 0>;
+    return split ? k_gcn_fwd_nm3<D, DR, RL, true, WV, 0> : k_gcn_fwd_nm3<D, DR, RL, false, WV, 0>;
 }
 
 }  // namespace
@@ -1073,6 +1424,7 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
     // n workgroups per CU
     const bool lab_v1 = (flags & LG_F_LAB_V1) != 0, lab_nm2 = (flags & LG_F_LAB_NM2) != 0;
     const bool w8 = (flags & LG_F_LAB_W8) != 0;
+    const bool relu = (flags & LG_F_RELU) != 0;
     const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
     (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
@@ -1095,17 +1447,17 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
             kern<<<grid, 64 * kNm2Waves, dyn2, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
                                                     dropout_p, scale, seed, salt);                                 \
         } else if (w8) {                                                                                           \
-            auto kern = nm3_kernel<DD, DR, 8>(flags);                                                              \
+            auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
-            kern<<<grid, 64 * 8, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor, dropout_p,    \
-                                            scale, seed, salt);                                                    \
+            kern<<<grid, 64 * 8, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
+                                            salt);                                                                 \
         } else {                                                                                                   \
-            auto kern = nm3_kernel<DD, DR, 4>(flags);                                                              \
+            auto kern = relu ? nm3_kernel<DD, DR, true, 4>(flags) : nm3_kernel<DD, DR, false, 4>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 4>::BYTES : Nm3Lds<DD, false, 4>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
-            kern<<<grid, 64 * 4, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor, dropout_p,    \
-                                            scale, seed, salt);                                                    \
+            kern<<<grid, 64 * 4, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
+                                            salt);                                                                 \
         }                                                                                                          \
     } while (0)
     if (D == 64) {
@@ -1146,13 +1498,25 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
     // B == 0 still runs one (empty) launch so the slab holds zeros
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
     do {                                                                                                           \
-        auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                     \
-        grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),  \
-                             2 * lg_num_cus());                                                                    \
-        kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,               \
-                                                 static_cast<uint32_t>(N), static_cast<uint32_t>(B),               \
-                                                 static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,           \
-                                                 scale_out);                                                       \
+        if (flags & LG_F_LAB_NM2) {                                                                                \
+            auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                 \
+            grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),\
+                                 2 * lg_num_cus());                                                                \
+            kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,          \
+                                                     static_cast<uint32_t>(N), static_cast<uint32_t>(B),           \
+                                                     static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
+                                                     scale_out);                                                   \
+        } else {                                                                                                   \
+            auto kern = k_gcn_bwd_nm3<DD, MI, NBB>;                                                                \
+            const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                             \
+            grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
+                                         2),                                                                       \
+                                 2 * lg_num_cus());                                                                \
+            kern<<<grid, 64 * kNmBwdWaves3, dyn3, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,        \
+                                                       static_cast<uint32_t>(N), static_cast<uint32_t>(B),         \
+                                                       static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,     \
+                                                       scale_out);                                                 \
+        }                                                                                                          \
     } while (0)
 #define LG_NM_BWD_D(DD)                                  \
     do {                                                 \

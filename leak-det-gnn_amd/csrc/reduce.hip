@@ -1,6 +1,8 @@
 // Deterministic slab reduction shared by the backward kernels:
 //   seg k:  out_k[i] = sum_g slab[g * stride + off_k + i],  i < len_k
-// in a fixed order, all segments of one backward op in ONE launch.  One 1024-thread
+// in a fixed order, all segments of one backward op in ONE launch, accumulated in fp64
+// (the bias gradients are sums with heavy cancellation over hundreds of block partials;
+// fp32 accumulation left them ~2e-5 of scale off at B = 256).  One 1024-thread
 // block per 64 columns of a segment: wave w sums slabs g = w, w + 16, ... for its
 // column (one column per lane, coalesced rows), then the 16 wave partials are added
 // in wave order through LDS.  An optional fp64 column (sum of G doubles, used for
@@ -42,8 +44,8 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ 
     const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 64 + lane;
     const int64_t len = sg.len[k];
     const float* src = slab + sg.off[k];
-    __shared__ float part[16][64];
-    float acc = 0.f;
+    __shared__ double part[16][64];
+    double acc = 0.0;
     if (col < len) {
         int g = w;
         for (; g + 48 < G; g += 64) {  // four independent loads in flight
@@ -61,9 +63,9 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ 
     part[w][lane] = acc;
     __syncthreads();
     if (w == 0 && col < len) {
-        float s = part[0][lane];
+        double s = part[0][lane];
         for (int i = 1; i < 16; ++i) s += part[i][lane];
-        sg.out[k][col] = s;
+        sg.out[k][col] = static_cast<float>(s);
     }
 }
 

@@ -23,7 +23,7 @@ from __future__ import annotations
 import json
 from dataclasses import dataclass
 from pathlib import Path
-from typing import Any, Dict, Iterable, Iterator, List, Optional, Sequence
+from typing import Any, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pandas as pd
@@ -439,10 +439,11 @@ class DeviceBatchLoader:
     order, windows gathered on ``device`` from HBM-resident scenes.  Equivalent to
     DataLoader(ds, batch_size, shuffle=False) + .to(device) of the tensor fields."""
 
-    def __init__(self, ds, batch_size: int, device: torch.device) -> None:
+    def __init__(self, ds, batch_size: int, device: torch.device, shard: Tuple[int, int] = (0, 1)) -> None:
         self.ds = ds
         self.batch_size = int(batch_size)
         self.device = torch.device(device)
+        self.rank, self.world = int(shard[0]), int(shard[1])  # data parallel: this rank's slice of each batch
         if isinstance(ds, AbruptLeakDetectorDataset):
             ids = list(dict.fromkeys(list(ds.leak_scene_ids) + list(ds.noleak_scene_ids)))
             self.bank = _DeviceBank(ds.store, ids, self.device)
@@ -490,4 +491,28 @@ class DeviceBatchLoader:
     def __iter__(self) -> Iterator[Dict[str, Any]]:
         make = self._detector_batch if isinstance(self.ds, AbruptLeakDetectorDataset) else self._predictor_batch
         for b0 in range(0, len(self.ds), self.batch_size):
-            yield make(range(b0, min(b0 + self.batch_size, len(self.ds))))
+            yield make(shard_slice(range(b0, min(b0 + self.batch_size, len(self.ds))), self.rank, self.world))
+
+
+def shard_slice(idxs: range, rank: int, world: int) -> range:
+    """Contiguous slice `rank` of `world` of one global batch's sample indices (sizes
+    differ by at most one on a ragged last batch).  Samples are seeded by seed + index
+    (datasets.py:236,490), so the union over ranks is the single-process batch."""
+    n = len(idxs)
+    lo = idxs.start + (n * rank) // world
+    hi = idxs.start + (n * (rank + 1)) // world
+    return range(lo, hi)
+
+
+class ShardBatchSampler:
+    """batch_sampler for torch's DataLoader: this rank's shard_slice of every global batch."""
+
+    def __init__(self, n: int, batch_size: int, rank: int, world: int) -> None:
+        self.n, self.bs, self.rank, self.world = int(n), int(batch_size), int(rank), int(world)
+
+    def __len__(self) -> int:
+        return (self.n + self.bs - 1) // self.bs
+
+    def __iter__(self):
+        for b0 in range(0, self.n, self.bs):
+            yield list(shard_slice(range(b0, min(b0 + self.bs, self.n)), self.rank, self.world))

@@ -149,15 +149,16 @@ class LeakDetector(nn.Module):
         wb = []
         for conv in self.convs:
             wb += [conv.lin.weight, conv.bias]
+        nm = ops.use_node_major(B, len(self.node_names), Wn.shape[0])
         cfg = ops.TrunkConfig(graph=graph, sensor_slot=slot, sensor_idx=sensor_idx, slot_live=slot_live,
                               nonsensor_idx=nonsensor,
                               dropout_p=float(self.dropout.p), training=self.training,
-                              node_major=ops.TRUNK_NODE_MAJOR)
+                              node_major=nm)
         h_nodes = ops.GNNTrunkFn.apply(cfg, proj, bn, *wb)               # (N, B, D) node-major, else (B, N, D)
         mlp = self.edge_head.mlp     # Linear(3D,128), ReLU, Dropout, Linear(128,1)
         nmlp = self.noleak_head.mlp  # Linear(D,128), ReLU, Dropout, Linear(128,1)
         hcfg = ops.HeadsConfig(inc=inc, dropout_p=float(mlp[2].p), training=self.training,
-                               noleak_p=float(nmlp[2].p), node_major=ops.TRUNK_NODE_MAJOR)
+                               noleak_p=float(nmlp[2].p), node_major=nm)
         # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-216)
         return ops.HeadsFn.apply(hcfg, h_nodes, mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
                                  nmlp[0].weight, nmlp[0].bias, nmlp[3].weight, nmlp[3].bias)

@@ -65,7 +65,10 @@ class CapturedTrainStep:
         try:
             with torch.cuda.graph(self.graph_a):
                 self.slots.refresh()
-                self.loss = self._forward_backward()
+                # detached: the static loss must not keep the capture-time autograd graph
+                # (and its AccumulateGrad nodes, bound to the capture stream) alive, or a
+                # later eager backward on another stream would sync on them
+                self.loss = self._forward_backward().detach()
                 if self.world == 1:
                     self._update()
                 else:

@@ -38,6 +38,16 @@ SUPPORTED_D = (32, 64)
 # (detector.py:105-114, 192-196) through lg_gcn_fwd / lg_gcn_bwd.  Both give the same
 # results (same dropout masks); only the memory order differs.
 TRUNK_NODE_MAJOR = os.environ.get("LEAKGNN_LAYOUT", "node") != "window"
+NM_MAX_BYTES = 0x7FFFF000  # lg_gcn_fwd_nm / lg_gcn_bwd_nm: one [N][B][D] activation per launch
+
+
+def use_node_major(B: int, N: int, D: int) -> bool:
+    """Trunk layout for a batch: node-major when a 16-window tile is mostly full (B >= 16)
+    and the activation fits one node-major launch; window-major otherwise (B = 1 graphs
+    such as C5, where a node-major tile would carry 1 window in 16)."""
+    return TRUNK_NODE_MAJOR and B >= 16 and N * B * D * 4 <= NM_MAX_BYTES
+
+
 # lg_gcn_fwd_nm schedule / transform bits (LG_F_F32_MFMA, LG_F_LAB_*; include/leakgnn.h) for A/B
 # timing of the trunk; the schedule bits never change results.
 GCN_FWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_NM_FLAGS", "0"), 0)
@@ -464,7 +474,7 @@ class GNNTrunkFn(torch.autograd.Function):
             db = torch.empty(D, device=dy.device, dtype=torch.float32)
             first = l == 0  # layer 0's dx is the node-init gradient: its bias rows are summed in-kernel
             slot_p, dbias_p = (ptr(cfg.sensor_slot), ptr(dbias)) if first else (None, None)
-            with _timed("gcn_bwd", dy.device):
+            with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dy.device):
                 if nm:
                     check(lib.lg_gcn_bwd_nm(ptr(g.nodetab_t), ptr(g.pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                             ptr(Ws[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D, flags,

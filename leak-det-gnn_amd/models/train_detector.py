@@ -10,10 +10,21 @@ The detector is this package's LeakDetector (HIP GRU / GCN / heads kernels); bat
 come from datasets.DeviceBatchLoader (--loader torch restores the DataLoader path);
 the optimizer is AdamW(fused=True) on the GPU.  Checkpoints load with
 torch.load(weights_only=True).
+
+Data parallel (not in the reference, which is single-device): launched under torchrun
+(one process per GPU; RANK / LOCAL_RANK / WORLD_SIZE from the environment),
+  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m models.train_detector ... --batch_size 512
+every rank takes its contiguous slice of each GLOBAL batch of --batch_size samples (the
+samples are seeded by seed + index, datasets.py:236,490, so the global batch is the
+single-process batch at any world size), scales its mean loss by its share of the batch,
+and one gradient all-reduce (models/ddp.py: RCCL over xGMI, gloo on CPU) averages the
+gradients before clipping, so every rank takes the single-process step.  Rank 0
+evaluates, logs and writes the checkpoints.
 """
 from __future__ import annotations
 
 import argparse
+import builtins
 import json
 import os
 import random
@@ -27,6 +38,7 @@ import torch
 import torch.nn as nn
 
 from .datasets import AbruptLeakDetectorDataset, SensorStandardizer
+from .ddp import GradAllReduce, dist_env, init_distributed
 from .detector import LeakDetector
 from .predictor import NormalPredictorGRU, NormalPredictorTCN
 from .train_predictor import make_loader, pick_device, set_seed
@@ -148,13 +160,28 @@ def main(argv=None) -> None:
     ap.add_argument("--num_workers", type=int, default=0)
     ap.add_argument("--log_every", type=int, default=50)
     ap.add_argument("--loader", type=str, default="device", choices=["device", "torch"])
+    ap.add_argument("--dist_backend", type=str, default="auto", choices=["auto", "nccl", "gloo"],
+                    help="data parallel under torchrun: nccl (= RCCL on ROCm) for GPUs, gloo for CPU / tests")
     args = ap.parse_args(argv)
 
+    rank, local_rank, world = dist_env()
+    if world > 1:
+        backend = None if args.dist_backend == "auto" else args.dist_backend
+        if backend is None:
+            backend = "nccl" if (args.device != "cpu" and torch.cuda.is_available()) else "gloo"
+        init_distributed(backend)
+    lead = rank == 0
     out_dir = Path(args.out_dir)
-    out_dir.mkdir(parents=True, exist_ok=True)
+    if lead:
+        out_dir.mkdir(parents=True, exist_ok=True)
     set_seed(args.seed)
     device = pick_device(args.device)
-    print(f"{now()} [detector] device={device} seed={args.seed}")
+    if world > 1 and device.type == "cuda":
+        device = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(device)
+    # one log (rank 0's); every rank runs the same steps
+    print = builtins.print if lead else (lambda *a, **k: None)  # noqa: A001
+    print(f"{now()} [detector] device={device} seed={args.seed} world={world}")
     print(f"{now()} [detector] leak_root={args.leak_root}")
     print(f"{now()} [detector] inp_path={args.inp_path}")
     print(f"{now()} [detector] predictor_ckpt={args.predictor_ckpt}")
@@ -188,14 +215,14 @@ def main(argv=None) -> None:
           f"val={len(nl_val)} test={len(nl_test)}")
     print(f"{now()} [detector] classes: num_pipes={base_ds.num_pipes} num_classes={base_ds.num_pipes + 1}")
 
-    def mk(steps, seed, cache, leak_ids, nl_ids):
+    def mk(steps, seed, cache, leak_ids, nl_ids, shard=(0, 1)):
         ds = AbruptLeakDetectorDataset(leak_root=args.leak_root, l_pred_steps=args.l_pred, l_det_steps=args.l_det,
                                        steps_per_epoch=steps, seed=seed, sensor_ids=sensor_ids, standardizer=stdzr,
                                        cache_size=cache)
         ds.leak_scene_ids, ds.noleak_scene_ids = leak_ids, nl_ids
-        return ds, make_loader(ds, args.batch_size, device, args.loader, args.num_workers)
+        return ds, make_loader(ds, args.batch_size, device, args.loader, args.num_workers, shard=shard)
 
-    train_ds, train_loader = mk(args.steps_per_epoch, args.seed, 4096, leak_train, nl_train)
+    train_ds, train_loader = mk(args.steps_per_epoch, args.seed, 4096, leak_train, nl_train, shard=(rank, world))
     _, val_loader = mk(args.val_steps, args.seed + 1, 2048, leak_val, nl_val)
     _, test_loader = mk(args.test_steps, args.seed + 2, 2048, leak_test, nl_test)
 
@@ -204,6 +231,7 @@ def main(argv=None) -> None:
     opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay,
                             fused=(device.type == "cuda"))
     loss_fn = nn.CrossEntropyLoss()
+    allreduce = GradAllReduce(detector.parameters())  # no-op at world 1
     evaluator = DetectorEvaluator(predictor=predictor, detector=detector, device=device, l_pred=args.l_pred,
                                   l_det=args.l_det,
                                   metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
@@ -219,7 +247,8 @@ def main(argv=None) -> None:
                   "noleak_train": nl_train, "noleak_val": nl_val, "noleak_test": nl_test},
         "args": vars(args),
     }
-    (out_dir / "detector_meta.json").write_text(json.dumps(meta, indent=2, ensure_ascii=False), encoding="utf-8")
+    if lead:
+        (out_dir / "detector_meta.json").write_text(json.dumps(meta, indent=2, ensure_ascii=False), encoding="utf-8")
 
     def report(tag: str, m: Dict[str, float]) -> None:
         line = (f"{now()} [detector] {tag} leak_ar={m['ar_mean']:.4f} "
@@ -232,10 +261,16 @@ def main(argv=None) -> None:
 
     print(f"{now()} [detector] start training: epochs={args.epochs}, steps/epoch={args.steps_per_epoch}, "
           f"batch={args.batch_size}")
+    def global_sum(v: torch.Tensor) -> torch.Tensor:
+        if world > 1:
+            v = v.clone()
+            torch.distributed.all_reduce(v)
+        return v
+
     for epoch in range(1, args.epochs + 1):
         detector.train()
         running = torch.zeros((), dtype=torch.float64, device=device)
-        seen = 0
+        seen = torch.zeros((), dtype=torch.float64, device=device)
         for it, batch in enumerate(train_loader, start=1):
             noisy_seg = batch["noisy_seg"].to(device)
             time_seg = batch["time_seg"].to(device)
@@ -246,30 +281,45 @@ def main(argv=None) -> None:
             logits = detector(residual, time_seg[:, args.l_pred:, :])
             loss = loss_fn(logits, label)
             opt.zero_grad(set_to_none=True)
-            loss.backward()
+            n_local = noisy_seg.size(0)
+            if world > 1:  # mean over the GLOBAL batch after the all-reduce's average over ranks
+                n_glob = min(args.batch_size, len(train_ds) - (it - 1) * args.batch_size)
+                (loss * (n_local * world / n_glob)).backward()
+                allreduce()
+            else:
+                loss.backward()
             if args.grad_clip and args.grad_clip > 0:
                 torch.nn.utils.clip_grad_norm_(detector.parameters(), args.grad_clip)
             opt.step()
-            running += loss.detach().double() * noisy_seg.size(0)
-            seen += noisy_seg.size(0)
+            running += loss.detach().double() * n_local
+            seen += n_local
             if (it % args.log_every) == 0:
+                r_, s_ = global_sum(running), global_sum(seen)
                 print(f"{now()} [detector][epoch {epoch:02d}] step {it:05d}/{len(train_loader):05d} "
-                      f"loss={running.item() / max(seen, 1):.6f}")
-        val_metrics = evaluator.evaluate(val_loader)
-        report(f"[epoch {epoch:02d}] done. train_loss={running.item() / max(seen, 1):.6f}", val_metrics)
-        ckpt = {"epoch": epoch, "detector_state": detector.state_dict(), "sensor_ids": sensor_ids,
-                "pipe_ids_in_order": pipe_ids_in_order, "num_classes": int(len(pipe_ids_in_order) + 1),
-                "predictor_ckpt": str(args.predictor_ckpt), "args": vars(args)}
-        torch.save(ckpt, last_path)
-        if val_metrics["acc_top1"] > best_acc:
-            best_acc = val_metrics["acc_top1"]
-            torch.save(ckpt, best_path)
-            print(f"{now()} [detector] new best: acc_top1={best_acc:.4f} -> {best_path.name}")
+                      f"loss={r_.item() / max(s_.item(), 1):.6f}")
+        r_, s_ = global_sum(running), global_sum(seen)
+        if lead:
+            val_metrics = evaluator.evaluate(val_loader)
+            report(f"[epoch {epoch:02d}] done. train_loss={r_.item() / max(s_.item(), 1):.6f}", val_metrics)
+            ckpt = {"epoch": epoch, "detector_state": detector.state_dict(), "sensor_ids": sensor_ids,
+                    "pipe_ids_in_order": pipe_ids_in_order, "num_classes": int(len(pipe_ids_in_order) + 1),
+                    "predictor_ckpt": str(args.predictor_ckpt), "args": vars(args)}
+            torch.save(ckpt, last_path)
+            if val_metrics["acc_top1"] > best_acc:
+                best_acc = val_metrics["acc_top1"]
+                torch.save(ckpt, best_path)
+                print(f"{now()} [detector] new best: acc_top1={best_acc:.4f} -> {best_path.name}")
+        if world > 1:
+            torch.distributed.barrier()
 
-    best_ckpt = torch.load(best_path, map_location=device, weights_only=True)
-    detector.load_state_dict(best_ckpt["detector_state"])
-    report("TEST:", evaluator.evaluate(test_loader))
-    print(f"{now()} [detector] saved: {best_path.name}, {last_path.name}, meta.json")
+    if lead:
+        best_ckpt = torch.load(best_path, map_location=device, weights_only=True)
+        detector.load_state_dict(best_ckpt["detector_state"])
+        report("TEST:", evaluator.evaluate(test_loader))
+        print(f"{now()} [detector] saved: {best_path.name}, {last_path.name}, meta.json")
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

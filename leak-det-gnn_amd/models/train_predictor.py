@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 from torch.utils.data import DataLoader
 
-from .datasets import DeviceBatchLoader, NormalPredictorDataset, compute_sensor_stats_from_normal
+from .datasets import DeviceBatchLoader, NormalPredictorDataset, ShardBatchSampler, compute_sensor_stats_from_normal
 from .predictor import NormalPredictorGRU, NormalPredictorTCN
 from .utils import now
 
@@ -54,9 +54,15 @@ def split_ids(ids: List[str], seed: int, ratios=(0.8, 0.1, 0.1)) -> Tuple[List[s
     return ids[:n_train], ids[n_train:n_train + n_val], ids[n_train + n_val:]
 
 
-def make_loader(ds, batch_size: int, device: torch.device, kind: str, num_workers: int = 0):
+def make_loader(ds, batch_size: int, device: torch.device, kind: str, num_workers: int = 0,
+                shard: Tuple[int, int] = (0, 1)):
+    """Batches of `batch_size` samples in index order; with shard = (rank, world) each rank
+    gets its contiguous slice of every global batch (data parallelism)."""
     if kind == "device" and device.type == "cuda":
-        return DeviceBatchLoader(ds, batch_size, device)
+        return DeviceBatchLoader(ds, batch_size, device, shard=shard)
+    if shard[1] > 1:
+        return DataLoader(ds, batch_sampler=ShardBatchSampler(len(ds), batch_size, *shard), num_workers=num_workers,
+                          pin_memory=(device.type == "cuda"))
     return DataLoader(ds, batch_size=batch_size, num_workers=num_workers, pin_memory=(device.type == "cuda"))
 
 

@@ -102,3 +102,55 @@ def test_shard_range():
     assert list(shard_range(512, 3, 8)) == list(range(192, 256))
     with pytest.raises(ValueError):
         shard_range(10, 0, 3)
+
+
+def _inplace_worker(rank, world, port, q):
+    """Two steps with zero_grad(set_to_none=False): after the first all-reduce every
+    p.grad is a view of the flat bucket, and the second step must still reduce correctly."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [str(REPO), str(PKG), str(REPO / "tests")]
+    from models.ddp import GradAllReduce, init_distributed
+    init_distributed("gloo")
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(7, 3)
+    ar = GradAllReduce(lin.parameters())
+    out = []
+    for step in range(2):
+        lin.zero_grad(set_to_none=False)
+        x = torch.full((4, 7), float(rank + 1 + step))
+        lin(x).sum().backward()
+        ar()
+        out.append([p.grad.clone().numpy() for p in lin.parameters()])
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_with_in_place_zero_grad():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inplace_worker, args=(k, 2, port, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for step in range(2):
+        # d/dW sum(W x + b) = 4 * x value per row; mean over ranks of (rank + 1 + step)
+        mean_x = ((1 + step) + (2 + step)) / 2.0
+        w, b = res[0][step]
+        assert abs(w[0, 0] - 4 * mean_x) < 1e-5 and abs(b[0] - 4.0) < 1e-6
+        for a, c in zip(res[0][step], res[1][step]):
+            assert (a == c).all()
+
+
+def test_shard_slices_cover_global_batch():
+    from models.datasets import ShardBatchSampler, shard_slice
+    for n, world in ((256, 8), (37, 4), (5, 8)):
+        parts = [shard_slice(range(100, 100 + n), r, world) for r in range(world)]
+        assert [i for p in parts for i in p] == list(range(100, 100 + n))
+    s = list(ShardBatchSampler(20, 8, 1, 2))
+    assert s == [[4, 5, 6, 7], [12, 13, 14, 15], [18, 19]]

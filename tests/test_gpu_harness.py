@@ -122,3 +122,63 @@ def test_event_windows_batched_equal_per_window_loop(data):
             res = build_residual_sequence_from_segment(tcn, p[t0 - 36:t0 + 36], tf[t0 - 36:t0 + 36], 36, 36)
             ref = det(res[None], tf[None, t0:t0 + 36]).float().cpu()[0]
             assert (logits[w] - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, w
+
+
+def _dp_trainer_worker(rank, world, port, argv):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from models import train_detector
+    from models.detector import LeakDetector
+
+    class NoDropout(LeakDetector):  # dropout off: masks are per-rank draws, the comparison must be exact
+        def __init__(self, *a, **k):
+            k["dropout"] = 0.0
+            super().__init__(*a, **k)
+    train_detector.LeakDetector = NoDropout
+    train_detector.main(argv)
+
+
+def test_train_detector_data_parallel_equals_single_process(data, tmp_path):
+    """train_detector under a 2-rank launch (torchrun environment, gloo, both ranks on this
+    GPU): each rank trains on its half of every global batch of --batch_size samples and the
+    gradients are all-reduced; rank 0's checkpoint equals a single-process run's on the same
+    global batches (dropout off on both sides)."""
+    import socket
+    import torch.multiprocessing as mp
+    from models import train_detector, train_predictor
+    from models.detector import LeakDetector
+    from models.synth import write_synthetic_leak_set
+    write_synthetic_leak_set(tmp_path / "leak", INFO["sensors"], INFO["pipes"], scenes_per_pipe=4, n_noleak=12,
+                             T=300, seed=1)
+    out = tmp_path / "pred"
+    train_predictor.main(["--normal_root", str(data / "normal"), "--out_dir", str(out), "--epochs", "1",
+                          "--steps_per_epoch", "16", "--val_steps", "8", "--test_steps", "8", "--batch_size", "8",
+                          "--device", "cuda"])
+
+    def argv(o):
+        return ["--leak_root", str(tmp_path / "leak"), "--inp_path", str(LTA_INP), "--predictor_ckpt",
+                str(out / "predictor_best.ckpt"), "--out_dir", str(o), "--epochs", "1", "--steps_per_epoch", "24",
+                "--val_steps", "8", "--test_steps", "8", "--batch_size", "8", "--device", "cuda",
+                "--dist_backend", "gloo"]
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    mp.start_processes(_dp_trainer_worker, args=(2, port, argv(tmp_path / "dp")), nprocs=2, start_method="spawn")
+
+    class NoDropout(LeakDetector):
+        def __init__(self, *a, **k):
+            k["dropout"] = 0.0
+            super().__init__(*a, **k)
+    orig = train_detector.LeakDetector
+    train_detector.LeakDetector = NoDropout
+    try:
+        train_detector.main(argv(tmp_path / "sp"))
+    finally:
+        train_detector.LeakDetector = orig
+    a = torch.load(tmp_path / "dp" / "detector_last.ckpt", weights_only=True)["detector_state"]
+    b = torch.load(tmp_path / "sp" / "detector_last.ckpt", weights_only=True)["detector_state"]
+    assert set(a) == set(b)
+    for k in b:
+        d = (a[k].double() - b[k].double()).abs().max().item()
+        assert d <= 2e-5 * max(b[k].abs().max().item(), 1e-3), f"{k}: {d:.3e}"

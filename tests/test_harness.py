@@ -191,3 +191,19 @@ def test_event_trigger_and_aggregation_helpers():
     assert torch.equal(s, lg[2] + lg[3] + lg[4])
     assert torch.equal(aggregate_sum_logits(rec, 5, pd.Timedelta(minutes=15)), lg[5])
     assert torch.equal(aggregate_sum_logits(rec, 3, pd.Timedelta(0)), lg[3])
+
+
+def test_train_predictor_cpu_plumbing(data, tmp_path):
+    """configs[0]: train_predictor on the CPU, 1 epoch, batch 1 (the reference's plumbing
+    run), reference flags; the checkpoint's standardizer stats are plain floats that the
+    reference loaders' np.asarray(std, dtype=float32) accepts after a weights_only load."""
+    from models import train_predictor
+    out = tmp_path / "out"
+    train_predictor.main(["--normal_root", str(data / "normal"), "--out_dir", str(out), "--epochs", "1",
+                          "--steps_per_epoch", "4", "--val_steps", "2", "--test_steps", "2", "--batch_size", "1",
+                          "--device", "cpu", "--log_every", "2"])
+    ck = torch.load(out / "predictor_best.ckpt", map_location="cpu", weights_only=True)
+    mean = np.asarray(ck["standardizer_mean"], dtype=np.float32)
+    std = np.asarray(ck["standardizer_std"], dtype=np.float32)
+    assert mean.shape == std.shape == (len(ck["sensor_ids"]),) and (std > 0).all()
+    assert (out / "predictor_last.ckpt").is_file() and (out / "predictor_meta.json").is_file()

@@ -124,18 +124,28 @@ def main():
                                                                  1, cs()), "nmlab")
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
-    if "gcn_bwd_nm" in which:
+    for name, fl, nbias in (("gcn_bwd_nm", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
+                            ("gcn_bwd_nm_old", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, False),
+                            ("gcn_bwd_nm_l0", nat.LG_F_MASK_OUT, True),
+                            ("gcn_bwd_nm_l0_old", nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, True)):
+        if name not in which:
+            continue
         dy = torch.randn_like(x)
         yy = torch.relu(torch.randn_like(x))
         dx = torch.empty_like(x)
         dW = torch.empty(D, D, device=dev)
         db = torch.empty(D, device=dev)
+        slot = torch.full((N,), -1, dtype=torch.int32, device=dev)
+        slot[:29] = torch.arange(29, dtype=torch.int32, device=dev)
+        dnb = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
-        f = lambda: check(lib.lg_gcn_bwd_nm(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
-                                            ptr(dx), ptr(dW), ptr(db), None, None, B, N, D,
-                                            nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), cs()), "bwd_nm")
+        f = lambda fl=fl, nbias=nbias, dy=dy, yy=yy, dx=dx, dW=dW, db=db, slot=slot, dnb=dnb, ws=ws: check(
+            lib.lg_gcn_bwd_nm(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W), ptr(dx),
+                              ptr(dW), ptr(db), ptr(slot) if nbias else None, ptr(dnb) if nbias else None, B, N, D,
+                              fl, 1.0, 1.0, ptr(ws), cs()), name)
         t = timeit(f, args.iters)
-        res["gcn_bwd_nm"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
+        byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
+        res[name] = {"us": t, "GBps": byts / t / 1e3}
     if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
         f = lambda: y.copy_(x)
         t = timeit(f, args.iters)
