@@ -15,10 +15,10 @@ What runs where (forward + backward):
     (B, 64) pooled vector and the loss: stock PyTorch-ROCm.
   * The GRU sensor encoder, node init, every GCNConv + ReLU + dropout, the fused
     EdgeHead (endpoint gather -> MLP -> logit, never materialising the (B,P,3D)
-    features) and the per-window mean pool: libleakgnn HIP kernels
-    (ops.GRUEncoderFn, ops.GNNTrunkFn, ops.HeadsFn) over ONE device-resident
-    single-graph CSR; the (2, B*E) batchified edge_index of the reference
-    (detector.py:195-196) is never built.
+    features) and the per-window mean pool: libleakgnn HIP kernels behind the
+    registered ops leakgnn::gru_encoder / sensor_proj / gnn_trunk / detector_heads
+    (models/library.py) over ONE device-resident single-graph CSR; the (2, B*E)
+    batchified edge_index of the reference (detector.py:195-196) is never built.
 There is no CPU path: forward raises on CPU tensors.
 """
 from __future__ import annotations
@@ -29,7 +29,7 @@ from typing import Dict, Optional, Sequence
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import library, ops
 from .gcn import GCNConv, global_mean_pool  # noqa: F401  (re-exported PyG-compatible API)
 from .utils import WDNGraph, build_wdn_graph_from_inp
 
@@ -55,8 +55,12 @@ class SharedSensorGRUEncoder(nn.Module):
         g = self.gru
         if g.num_layers != 1 or g.hidden_size not in (32, 64) or g.bidirectional or not g.bias:
             raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 32/64, bias")
-        return ops.GRUEncoderFn.apply(r, tfeat if self.use_time else None, g.weight_ih_l0, g.weight_hh_l0,
-                                      g.bias_ih_l0, g.bias_hh_l0)
+        f = ops._f32
+        ws = [f(t) for t in (g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)]
+        tf = f(tfeat) if self.use_time else None
+        r = f(r)
+        save = torch.is_grad_enabled() and any(t.requires_grad for t in [r, *ws] + ([tf] if tf is not None else []))
+        return torch.ops.leakgnn.gru_encoder(r, tf, *ws, save)[0]
 
 
 class EdgeHead(nn.Module):
@@ -142,23 +146,31 @@ class LeakDetector(nn.Module):
         graph, inc, slot, sensor_idx, slot_live, nonsensor = self._device_state(residual.device)
 
         h_s = self.sensor_encoder(residual, tfeat)                        # (B, S, Ds)
-        Ds = h_s.shape[-1]
-        Wn, bn = self.sensor_to_node.weight, self.sensor_to_node.bias     # (D, Ds+1), (D,)
+        f = ops._f32
+        Wn, bn = f(self.sensor_to_node.weight), f(self.sensor_to_node.bias)  # (D, Ds+1), (D,)
         # rows with a sensor: [h_s, 1] W^T + b ; rows without: [0, 0] W^T + b = b
-        proj = ops.SensorProjFn.apply(h_s, Wn, bn)                        # (B, S, D)
-        wb = []
-        for conv in self.convs:
-            wb += [conv.lin.weight, conv.bias]
-        nm = ops.use_node_major(B, len(self.node_names), Wn.shape[0])
-        cfg = ops.TrunkConfig(graph=graph, sensor_slot=slot, sensor_idx=sensor_idx, slot_live=slot_live,
-                              nonsensor_idx=nonsensor,
-                              dropout_p=float(self.dropout.p), training=self.training,
-                              node_major=nm)
-        h_nodes = ops.GNNTrunkFn.apply(cfg, proj, bn, *wb)               # (N, B, D) node-major, else (B, N, D)
+        proj = torch.ops.leakgnn.sensor_proj(h_s, Wn, bn)                  # (B, S, D)
+        N, D = len(self.node_names), Wn.shape[0]
+        nm = ops.use_node_major(B, N, D)
+        drop = self.training and float(self.dropout.p) > 0.0
+        g = graph
+        xs = torch.ops.leakgnn.gnn_trunk(
+            proj, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
+            nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
+            g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
+            library.seed_tensor(residual.device) if drop else _NO_SEED)
+        h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
         mlp = self.edge_head.mlp     # Linear(3D,128), ReLU, Dropout, Linear(128,1)
         nmlp = self.noleak_head.mlp  # Linear(D,128), ReLU, Dropout, Linear(128,1)
-        hcfg = ops.HeadsConfig(inc=inc, dropout_p=float(mlp[2].p), training=self.training,
-                               noleak_p=float(nmlp[2].p), node_major=nm)
-        # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-216)
-        return ops.HeadsFn.apply(hcfg, h_nodes, mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
-                                 nmlp[0].weight, nmlp[0].bias, nmlp[3].weight, nmlp[3].bias)
+        pe = float(mlp[2].p) if self.training else 0.0
+        pn = float(nmlp[2].p) if self.training else 0.0
+        hw = [f(t) for t in (mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
+                             nmlp[0].weight, nmlp[0].bias, nmlp[3].weight, nmlp[3].bias)]
+        keep = torch.is_grad_enabled() and (h_nodes.requires_grad or any(t.requires_grad for t in hw))
+        seed = library.seed_tensor(residual.device) if (pe > 0.0 or pn > 0.0) else _NO_SEED
+        # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-218)
+        return torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep,
+                                                seed)[0]
+
+
+_NO_SEED = torch.zeros(1, dtype=torch.long)  # seed argument of an op that draws no dropout mask

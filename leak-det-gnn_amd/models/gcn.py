@@ -11,8 +11,9 @@ reference; the semantics restated here are PyG 2.x's published ones:
      forward(x, edge_index) = propagate(gcn_norm(edge_index), lin(x)) + bias
   global_mean_pool(x, batch, size=None) = scatter(x, batch, reduce='mean')
 
-Here forward runs the fused HIP kernel lg_gcn_fwd ((Ahat x) W^T + b, one launch)
-and backward lg_gcn_bwd.  The gcn_norm'ed CSR is built on the device
+Here forward runs the registered op leakgnn::gcn_conv (models/library.py: the fused
+HIP kernel lg_gcn_fwd, (Ahat x) W^T + b in one launch) and its autograd formula
+leakgnn::gcn_conv_backward (lg_gcn_bwd).  The gcn_norm'ed CSR is built on the device
 (lg_graph_build) and, unlike PyG with cached=False, re-used while an edge_index
 with the SAME CONTENT is passed again (compared element-wise against a private
 copy, one device-side equality check per call) — the graph is a pure function of
@@ -28,7 +29,8 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from .ops import GCNGraph, GCNLayerFn, MeanPoolWindowsFn
+from . import library  # noqa: F401  (registers the leakgnn:: ops)
+from .ops import GCNGraph, _f32
 
 
 def _glorot_(t: torch.Tensor) -> None:
@@ -81,7 +83,8 @@ class GCNConv(nn.Module):
         if edge_weight is not None:
             raise NotImplementedError("edge_weight is not used on the Leak-det-gnn path")
         g = self.graph_for(edge_index, x.size(0), x.device)
-        return GCNLayerFn.apply(x, self.lin.weight, self.bias, g)
+        return torch.ops.leakgnn.gcn_conv(_f32(x), _f32(self.lin.weight), _f32(self.bias), g.rowptr, g.col, g.w,
+                                          g.rowptr_t, g.col_t, g.w_t)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"
@@ -98,5 +101,5 @@ def global_mean_pool(x: torch.Tensor, batch: Optional[torch.Tensor], size: Optio
         expected = torch.arange(B, device=batch.device).repeat_interleave(N)
         if not torch.equal(batch, expected):
             raise NotImplementedError("global_mean_pool kernels need batch = arange(B).repeat_interleave(N)")
-        return MeanPoolWindowsFn.apply(x, B, N)
+        return torch.ops.leakgnn.mean_pool(_f32(x), B, N)
     raise NotImplementedError("global_mean_pool kernels need equal-size windows")

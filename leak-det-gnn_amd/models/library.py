@@ -1,0 +1,573 @@
+"""torch.library registration of the libleakgnn operators (namespace ``leakgnn``).
+
+SURVEY §8(b): the hot path sits behind registered PyTorch operators whose bodies call
+the C ABI (include/leakgnn.h) on torch's current HIP stream, with autograd formulas in
+Python, so torch.compile / torch.export / any dispatcher-level caller sees them as
+ordinary ops (fake / meta implementations give output shapes without running kernels).
+
+  leakgnn::gcn_conv            PyG GCNConv.forward (detector.py:163,199): Ahat (x W^T) + b
+  leakgnn::mean_pool           PyG global_mean_pool over B equal windows (detector.py:215)
+  leakgnn::sensor_proj         sensor_to_node on the sensor rows (detector.py:184-189)
+  leakgnn::gru_encoder         SharedSensorGRUEncoder's GRU (detector.py:60-73)
+  leakgnn::gnn_trunk           node init + L x [GCNConv, ReLU, Dropout] (detector.py:178-201)
+  leakgnn::detector_heads      pipe gather + EdgeHead + mean pool + NoLeakHead
+                               (detector.py:76-102, 206-218)
+and one ``*_backward`` op per differentiable op (registered autograd formulas call them).
+
+Every op takes plain tensors (the graph CSR and its node tables are inputs, not Python
+objects) and fp32 CUDA tensors; there is no CPU kernel, so a CPU call raises.  Dropout
+seeds are a 1-element int64 tensor: a CPU tensor's value, or - under HIP-graph capture -
+a device tensor whose ADDRESS the kernels read at launch (LG_SALT_SEED_PTR), so replays
+draw fresh masks.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _native as nat
+from ._native import check, load_library, ptr, stream_of
+from .ops import EDGE_HEAD_SALT, GCN_FWD_NM_EXTRA_FLAGS, NOLEAK_HEAD_SALT, _check_d, _timed
+
+NS = "leakgnn"
+
+
+def _seed_args(seed: Tensor) -> Tuple[int, int]:
+    """(seed value or device address, salt bits) of a dropout seed tensor."""
+    if seed.is_cuda:
+        return seed.data_ptr(), nat.LG_SALT_SEED_PTR
+    return int(seed.item()), 0
+
+
+def _req(*ts: Optional[Tensor]) -> None:
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("leakgnn ops run only on a ROCm GPU (tensor on %s); there is no CPU path" % t.device)
+        if t.is_floating_point() and t.dtype != torch.float32:
+            raise TypeError(f"leakgnn ops compute in fp32, got {t.dtype} (cast the inputs with .float())")
+
+
+def _c(t: Optional[Tensor]) -> Optional[Tensor]:
+    return None if t is None else t.contiguous()
+
+
+# ============================================================================ gcn_conv
+@torch.library.custom_op(f"{NS}::gcn_conv", mutates_args=(), device_types="cuda")
+def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, col: Tensor, w: Tensor,
+             rowptr_t: Tensor, col_t: Tensor, w_t: Tensor) -> Tensor:
+    """y = Ahat (x W^T) + b on one graph (lg_gcn_fwd, B = 1).  (rowptr, col, w): the
+    gcn_norm'ed CSR of lg_graph_build; the transposed CSR is the backward's."""
+    lib = load_library()
+    x, weight, bias = _c(x), _c(weight), _c(bias)
+    _req(x, weight, bias)
+    Ntot, D = x.shape
+    _check_d(D)
+    if weight.shape != (D, D):
+        raise NotImplementedError("GCNConv kernels need in_channels == out_channels")
+    y = torch.empty_like(x)
+    flags = nat.LG_F_BIAS if bias is not None else 0
+    with _timed("gcn_fwd", x.device):
+        check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(x), ptr(weight), ptr(bias), ptr(y), 1, Ntot, D,
+                             col.numel(), flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
+    return y
+
+
+@gcn_conv.register_fake
+def _(x, weight, bias, rowptr, col, w, rowptr_t, col_t, w_t):
+    return torch.empty_like(x)
+
+
+@torch.library.custom_op(f"{NS}::gcn_conv_backward", mutates_args=(), device_types="cuda")
+def gcn_conv_backward(dy: Tensor, x: Tensor, weight: Tensor, rowptr_t: Tensor, col_t: Tensor,
+                      w_t: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """(dx, dW, db) of gcn_conv (lg_gcn_bwd over the transposed CSR)."""
+    lib = load_library()
+    dy, x, weight = _c(dy), _c(x), _c(weight)
+    _req(dy, x, weight)
+    Ntot, D = x.shape
+    dx = torch.empty_like(x)
+    dW = torch.empty_like(weight)
+    db = torch.empty(D, device=x.device, dtype=x.dtype)
+    ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
+    with _timed("gcn_bwd", x.device):
+        check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), None, ptr(x), ptr(weight), ptr(dx),
+                             ptr(dW), ptr(db), None, None, 1, Ntot, D, col_t.numel(), 0, 1.0, 1.0, ptr(ws),
+                             stream_of(x)), "lg_gcn_bwd")
+    return dx, dW, db
+
+
+@gcn_conv_backward.register_fake
+def _(dy, x, weight, rowptr_t, col_t, w_t):
+    return torch.empty_like(x), torch.empty_like(weight), x.new_empty(x.shape[1])
+
+
+def _gcn_conv_setup(ctx, inputs, output):
+    x, weight, bias, _, _, _, rowptr_t, col_t, w_t = inputs
+    ctx.has_bias = bias is not None
+    ctx.save_for_backward(x, weight, rowptr_t, col_t, w_t)
+
+
+def _gcn_conv_bwd(ctx, dy):
+    x, weight, rowptr_t, col_t, w_t = ctx.saved_tensors
+    dx, dW, db = torch.ops.leakgnn.gcn_conv_backward(dy, x, weight, rowptr_t, col_t, w_t)
+    return dx, dW, (db if ctx.has_bias else None), None, None, None, None, None, None
+
+
+gcn_conv.register_autograd(_gcn_conv_bwd, setup_context=_gcn_conv_setup)
+
+
+# ============================================================================ mean_pool
+@torch.library.custom_op(f"{NS}::mean_pool", mutates_args=(), device_types="cuda")
+def mean_pool(x: Tensor, B: int, N: int) -> Tensor:
+    """global_mean_pool for batch = arange(B).repeat_interleave(N) (lg_mean_pool_fwd)."""
+    lib = load_library()
+    x = _c(x)
+    _req(x)
+    D = x.shape[-1]
+    _check_d(D)
+    out = torch.empty(B, D, device=x.device, dtype=torch.float32)
+    check(lib.lg_mean_pool_fwd(ptr(x), ptr(out), B, N, D, stream_of(x)), "lg_mean_pool_fwd")
+    return out
+
+
+@mean_pool.register_fake
+def _(x, B, N):
+    return x.new_empty(B, x.shape[-1])
+
+
+def _mean_pool_setup(ctx, inputs, output):
+    ctx.BN = (inputs[1], inputs[2])
+
+
+def _mean_pool_bwd(ctx, dout):
+    B, N = ctx.BN
+    return (dout / float(N)).unsqueeze(1).expand(B, N, dout.shape[-1]).reshape(B * N, -1), None, None
+
+
+mean_pool.register_autograd(_mean_pool_bwd, setup_context=_mean_pool_setup)
+
+
+# ============================================================================ sensor_proj
+@torch.library.custom_op(f"{NS}::sensor_proj", mutates_args=(), device_types="cuda")
+def sensor_proj(h_s: Tensor, weight: Tensor, bias: Tensor) -> Tensor:
+    """sensor_to_node on the rows that carry a sensor (detector.py:160, 184-189): their
+    Linear input is [h_s, 1], so proj = h_s W[:, :Ds]^T + (W[:, Ds] + b), one GEMM."""
+    _req(h_s, weight, bias)
+    B, S, Ds = h_s.shape
+    D = weight.shape[0]
+    with torch.autocast("cuda", enabled=False):
+        return torch.addmm(weight[:, Ds] + bias, h_s.reshape(B * S, Ds), weight[:, :Ds].t()).view(B, S, D)
+
+
+@sensor_proj.register_fake
+def _(h_s, weight, bias):
+    return h_s.new_empty(h_s.shape[0], h_s.shape[1], weight.shape[0])
+
+
+@torch.library.custom_op(f"{NS}::sensor_proj_backward", mutates_args=(), device_types="cuda")
+def sensor_proj_backward(dproj: Tensor, h_s: Tensor, weight: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """dh_s = dproj W[:, :Ds] (GEMM); dW (incl. the mask column) and db in one split-K
+    MFMA kernel (lg_linear_dw) instead of a skinny-K (K = B*S) GEMM."""
+    lib = load_library()
+    dproj, h_s, weight = _c(dproj), _c(h_s), _c(weight)
+    _req(dproj, h_s, weight)
+    B, S, Ds = h_s.shape
+    D = weight.shape[0]
+    K = B * S
+    d2, h2 = dproj.view(K, D), h_s.view(K, Ds)
+    with torch.autocast("cuda", enabled=False):
+        dh = (d2 @ weight[:, :Ds]).view(B, S, Ds)
+    dW = torch.empty(D, Ds + 1, device=d2.device, dtype=torch.float32)
+    db = torch.empty(D, device=d2.device, dtype=torch.float32)
+    ws = torch.empty(int(lib.lg_linear_dw_workspace_bytes(K, D, Ds)), device=d2.device, dtype=torch.uint8)
+    with _timed("linear_dw", d2.device):
+        check(lib.lg_linear_dw(ptr(d2), ptr(h2), K, D, Ds, ptr(dW), ptr(db), ptr(ws), stream_of(d2)), "lg_linear_dw")
+    return dh, dW, db
+
+
+@sensor_proj_backward.register_fake
+def _(dproj, h_s, weight):
+    return torch.empty_like(h_s), weight.new_empty(weight.shape), weight.new_empty(weight.shape[0])
+
+
+def _sensor_proj_setup(ctx, inputs, output):
+    h_s, weight, _ = inputs
+    ctx.save_for_backward(h_s, weight)
+
+
+def _sensor_proj_bwd(ctx, dproj):
+    h_s, weight = ctx.saved_tensors
+    dh, dW, db = torch.ops.leakgnn.sensor_proj_backward(dproj, h_s, weight)
+    return (dh if ctx.needs_input_grad[0] else None), dW, db
+
+
+sensor_proj.register_autograd(_sensor_proj_bwd, setup_context=_sensor_proj_setup)
+
+
+# ============================================================================ gru_encoder
+@torch.library.custom_op(f"{NS}::gru_encoder", mutates_args=(), device_types="cuda")
+def gru_encoder(residual: Tensor, tfeat: Optional[Tensor], w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor,
+                save: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    """(h_L (B, S, H), h_seq, gates): nn.GRU over the B*S sensor sequences, x_t =
+    [residual[b, t, s], tfeat[b, t, :]] read in place (lg_gru_fwd).  save: keep h_t and
+    the gate values of every step for the backward (else both are empty)."""
+    lib = load_library()
+    residual, tfeat, w_ih, w_hh, b_ih, b_hh = (_c(t) for t in (residual, tfeat, w_ih, w_hh, b_ih, b_hh))
+    _req(residual, tfeat, w_ih, w_hh, b_ih, b_hh)
+    B, L, S = residual.shape
+    G, I = w_ih.shape
+    H = w_hh.shape[1]
+    if tfeat is not None and tuple(tfeat.shape) != (B, L, 9):
+        raise ValueError(f"tfeat must be (B, L, 9), got {tuple(tfeat.shape)}")
+    dev = residual.device
+    h_seq = torch.empty(L, B * S, H, device=dev) if save else torch.empty(0, device=dev)
+    gates = torch.empty(L, B * S, 4, H, device=dev) if save else torch.empty(0, device=dev)
+    h_last = torch.empty(B, S, H, device=dev)
+    with _timed("gru_fwd", dev):
+        check(lib.lg_gru_fwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh),
+                             ptr(h_seq) if save else None, ptr(gates) if save else None, ptr(h_last), B, L, S, I, H,
+                             stream_of(residual)), "lg_gru_fwd")
+    return h_last, h_seq, gates
+
+
+@gru_encoder.register_fake
+def _(residual, tfeat, w_ih, w_hh, b_ih, b_hh, save):
+    B, L, S = residual.shape
+    H = w_hh.shape[1]
+    if save:
+        return (residual.new_empty(B, S, H), residual.new_empty(L, B * S, H), residual.new_empty(L, B * S, 4, H))
+    return residual.new_empty(B, S, H), residual.new_empty(0), residual.new_empty(0)
+
+
+@torch.library.custom_op(f"{NS}::gru_encoder_backward", mutates_args=(), device_types="cuda")
+def gru_encoder_backward(dh: Tensor, residual: Tensor, tfeat: Optional[Tensor], w_ih: Tensor, w_hh: Tensor,
+                         h_seq: Tensor, gates: Tensor, need_dx: bool
+                         ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """(dx (B*S, L, I) or empty, dW_ih, dW_hh, db_ih, db_hh) by BPTT over the saved gates
+    (lg_gru_bwd)."""
+    lib = load_library()
+    dh, residual, tfeat, w_ih, w_hh = (_c(t) for t in (dh, residual, tfeat, w_ih, w_hh))
+    _req(dh, residual, tfeat, w_ih, w_hh)
+    if h_seq.numel() == 0 or gates.numel() == 0:
+        raise RuntimeError("gru_encoder was run with save=False; no backward")
+    B, L, S = residual.shape
+    G, I = w_ih.shape
+    H = w_hh.shape[1]
+    dev = residual.device
+    dx = torch.empty(B * S, L, I, device=dev) if need_dx else torch.empty(0, device=dev)
+    dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+    db_ih, db_hh = torch.empty(3 * H, device=dev), torch.empty(3 * H, device=dev)
+    ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I, H)), device=dev, dtype=torch.uint8)
+    with _timed("gru_bwd", dev):
+        check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates), ptr(dh),
+                             ptr(dx) if need_dx else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L, S, I,
+                             H, ptr(ws), stream_of(residual)), "lg_gru_bwd")
+    return dx, dw_ih, dw_hh, db_ih, db_hh
+
+
+@gru_encoder_backward.register_fake
+def _(dh, residual, tfeat, w_ih, w_hh, h_seq, gates, need_dx):
+    B, L, S = residual.shape
+    H = w_hh.shape[1]
+    dx = residual.new_empty(B * S, L, w_ih.shape[1]) if need_dx else residual.new_empty(0)
+    return dx, torch.empty_like(w_ih), torch.empty_like(w_hh), w_ih.new_empty(3 * H), w_ih.new_empty(3 * H)
+
+
+def _gru_setup(ctx, inputs, output):
+    residual, tfeat, w_ih, w_hh, _, _, _ = inputs
+    _, h_seq, gates = output
+    ctx.mark_non_differentiable(h_seq, gates)
+    ctx.has_tfeat = tfeat is not None
+    ctx.save_for_backward(residual, tfeat, w_ih, w_hh, h_seq, gates)
+
+
+def _gru_bwd(ctx, dh, _dhseq, _dgates):
+    residual, tfeat, w_ih, w_hh, h_seq, gates = ctx.saved_tensors
+    B, L, S = residual.shape
+    I = w_ih.shape[1]
+    need_dx = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+    dx, dw_ih, dw_hh, db_ih, db_hh = torch.ops.leakgnn.gru_encoder_backward(
+        dh.contiguous(), residual, tfeat if ctx.has_tfeat else None, w_ih, w_hh, h_seq, gates, need_dx)
+    dres = dtf = None
+    if ctx.needs_input_grad[0]:
+        dres = dx[..., 0].reshape(B, S, L).transpose(1, 2)
+    if ctx.has_tfeat and ctx.needs_input_grad[1]:
+        dtf = dx[..., 1:].reshape(B, S, L, I - 1).sum(dim=1)
+    return dres, dtf, dw_ih, dw_hh, db_ih, db_hh, None
+
+
+gru_encoder.register_autograd(_gru_bwd, setup_context=_gru_setup)
+
+
+# ============================================================================ gnn_trunk
+@torch.library.custom_op(f"{NS}::gnn_trunk", mutates_args=(), device_types="cuda")
+def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor], sensor_slot: Tensor,
+              sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab: Tensor, pairs: Tensor,
+              rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor,
+              col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor) -> List[Tensor]:
+    """[x_0, ..., x_L]: node init (detector.py:178-190) then L x dropout(relu(GCNConv)).
+
+      x_0     = dropout(relu(slot >= 0 ? proj[b, slot] : node_bias))     (lg_node_init_fwd)
+      x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                     (lg_gcn_fwd[_nm], fused)
+    node_major: features [N][B][D] (lg_gcn_fwd_nm), else [B][N][D].  p: dropout prob
+    (0 = eval).  Every activation is returned: the backward reads its ReLU/dropout masks
+    back as [x > 0] and needs x_l for dW, so no mask is ever stored."""
+    lib = load_library()
+    proj, node_bias = _c(proj), _c(node_bias)
+    weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]
+    _req(proj, node_bias, *weights, *biases)
+    B, S, D = proj.shape
+    _check_d(D)
+    N = sensor_slot.shape[0]
+    drop = p > 0.0
+    seed_v, sbit = _seed_args(seed) if drop else (0, 0)
+    dflag = nat.LG_F_DROPOUT if drop else 0
+    st = stream_of(proj)
+    x0 = torch.empty((N, B, D) if node_major else (B, N, D), device=proj.device, dtype=torch.float32)
+    with _timed("node_init", proj.device):
+        check(lib.lg_node_init_fwd(ptr(sensor_slot), ptr(proj), ptr(node_bias), ptr(x0), B, N, S, D,
+                                   dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v, 0 | sbit, st),
+              "lg_node_init_fwd")
+    xs = [x0]
+    for l, (W, b) in enumerate(zip(weights, biases)):
+        y = torch.empty_like(x0)
+        flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag
+        with _timed("gcn_fwd", proj.device):
+            if node_major:
+                check(lib.lg_gcn_fwd_nm(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
+                                        col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v, (l + 1) | sbit, st),
+                      "lg_gcn_fwd_nm")
+            else:
+                check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
+                                     col.numel(), flags, p, seed_v, (l + 1) | sbit, st), "lg_gcn_fwd")
+        xs.append(y)
+    return xs
+
+
+@gnn_trunk.register_fake
+def _(proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab, pairs, rowptr,
+      col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed):
+    B, S, D = proj.shape
+    N = sensor_slot.shape[0]
+    shape = (N, B, D) if node_major else (B, N, D)
+    return [proj.new_empty(shape) for _ in range(len(weights) + 1)]
+
+
+@torch.library.custom_op(f"{NS}::gnn_trunk_backward", mutates_args=(), device_types="cuda")
+def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor], sensor_slot: Tensor,
+                       sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab_t: Tensor,
+                       pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
+                       node_major: bool) -> Tuple[Tensor, Tensor, List[Tensor], List[Tensor]]:
+    """(dproj, dnode_bias, [dW_l], [db_l]): one fused lg_gcn_bwd[_nm] per layer, last
+    first; ReLU/dropout masks of a layer's output and input applied inside the kernel from
+    the saved activations; the node-init bias gradient summed inside layer 0's launch."""
+    lib = load_library()
+    L = len(weights)
+    dev = grad_out.device
+    st = stream_of(grad_out)
+    if node_major:
+        N, B, D = xs[0].shape
+    else:
+        B, N, D = xs[0].shape
+    scale = 1.0 / (1.0 - p) if p > 0.0 else 1.0
+    dy = grad_out.contiguous()
+    wsb = lib.lg_gcn_bwd_nm_workspace_bytes(D) if node_major else lib.lg_gcn_bwd_workspace_bytes(D)
+    ws = torch.empty(int(wsb), device=dev, dtype=torch.uint8)
+    dWs: List[Tensor] = [grad_out] * L
+    dbs: List[Tensor] = [grad_out] * L
+    dbias = torch.empty(D, device=dev, dtype=torch.float32)
+    for l in range(L - 1, -1, -1):
+        flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0)
+        dx = torch.empty_like(dy)
+        dW = torch.empty(D, D, device=dev, dtype=torch.float32)
+        db = torch.empty(D, device=dev, dtype=torch.float32)
+        slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias)) if l == 0 else (None, None)
+        with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dev):
+            if node_major:
+                check(lib.lg_gcn_bwd_nm(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                                        ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D, flags,
+                                        scale, scale, ptr(ws), st), "lg_gcn_bwd_nm")
+            else:
+                check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                                     ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
+                                     col_t.numel(), flags, scale, scale, ptr(ws), st), "lg_gcn_bwd")
+        dWs[l], dbs[l] = dW, db
+        dy = dx  # already masked by the previous op's relu/dropout
+    dproj = dy.index_select(0, sensor_idx).transpose(0, 1) if node_major else dy.index_select(1, sensor_idx)
+    if slot_live is not None:
+        dproj = dproj * slot_live.view(1, -1, 1)
+    if L == 0:
+        dbias = dy.index_select(0 if node_major else 1, nonsensor_idx).sum(dim=(0, 1))
+    return dproj.contiguous(), dbias, dWs, dbs
+
+
+@gnn_trunk_backward.register_fake
+def _(grad_out, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t,
+      w_t, p, node_major):
+    D = xs[0].shape[2]
+    B = xs[0].shape[1] if node_major else xs[0].shape[0]
+    S = sensor_idx.shape[0]
+    return (grad_out.new_empty(B, S, D), grad_out.new_empty(D), [torch.empty_like(t) for t in weights],
+            [grad_out.new_empty(D) for _ in weights])
+
+
+def _trunk_setup(ctx, inputs, output):
+    (proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, _, _, _, _, _, nodetab_t,
+     pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
+    ctx.L = len(weights)
+    ctx.mark_non_differentiable(*output[:-1])  # x_0 .. x_{L-1}: returned for the backward's masks
+    ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
+    ctx.save_for_backward(*output, *weights, sensor_slot, sensor_idx, nonsensor_idx,
+                          slot_live if slot_live is not None else sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t)
+
+
+def _trunk_bwd(ctx, grads):
+    L = ctx.L
+    saved = ctx.saved_tensors
+    xs, weights = list(saved[:L + 1]), list(saved[L + 1:2 * L + 1])
+    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 1:]
+    g = grads[-1] if grads[-1] is not None else torch.zeros_like(xs[-1])
+    dproj, dbias, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
+        g, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None, nodetab_t, pairs_t,
+        rowptr_t, col_t, w_t, ctx.p, ctx.node_major)
+    return (dproj, dbias, dWs, dbs) + (None,) * 17
+
+
+gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)
+
+
+# ============================================================================ detector_heads
+@torch.library.custom_op(f"{NS}::detector_heads", mutates_args=(), device_types="cuda")
+def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw1: Tensor, nb1: Tensor, nw2: Tensor,
+                   nb2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor, p_edge: float, p_noleak: float,
+                   node_major: bool, keep_hidden: bool, seed: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """(logits (B, P+1), EdgeHead hidden, pooled, NoLeakHead hidden).  Columns [0, P) by
+    lg_edge_head_fwd (endpoint gather -> MFMA MLP -> dot, the (B, P, 3D) features never
+    stored), column P by lg_pool_head_fwd (mean pool + NoLeakHead): the torch.cat of
+    detector.py:218 is never a separate copy.  keep_hidden: keep the EdgeHead hidden layer
+    for a recompute-free backward (else it is empty)."""
+    lib = load_library()
+    h, w1, b1, w2, b2, nw1, nb1, nw2, nb2 = (_c(t) for t in (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2))
+    _req(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
+    N, B, D = h.shape if node_major else (h.shape[1], h.shape[0], h.shape[2])
+    _check_d(D)
+    lay = nat.LG_F_NODE_MAJOR if node_major else 0
+    hidden, nhidden = w1.shape[0], nw1.shape[0]
+    P = ends.shape[0]
+    seed_v, sbit = _seed_args(seed) if (p_edge > 0.0 or p_noleak > 0.0) else (0, 0)
+    fe = nat.LG_F_DROPOUT if p_edge > 0.0 else 0
+    fn = nat.LG_F_DROPOUT if p_noleak > 0.0 else 0
+    st = stream_of(h)
+    dev = h.device
+    logits = torch.empty(B, P + 1, device=dev, dtype=torch.float32)
+    pooled = torch.empty(B, D, device=dev, dtype=torch.float32)
+    hid = torch.empty(B, nhidden, device=dev, dtype=torch.float32)
+    ehid = torch.empty(B * P, hidden, device=dev, dtype=torch.float32) if keep_hidden else torch.empty(0, device=dev)
+    with _timed("edge_fwd", dev):
+        check(lib.lg_edge_head_fwd(ptr(ends), ptr(h), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(logits), P + 1,
+                                   ptr(ehid) if keep_hidden else None, B, N, P, D, hidden, fe | lay, p_edge, seed_v,
+                                   EDGE_HEAD_SALT | sbit, st), "lg_edge_head_fwd")
+    with _timed("pool_head", dev):
+        check(lib.lg_pool_head_fwd(ptr(h), ptr(nw1), ptr(nb1), ptr(nw2), ptr(nb2), ptr(pooled), ptr(hid), ptr(logits),
+                                   P + 1, P, B, N, D, nhidden, fn | lay, p_noleak, seed_v, NOLEAK_HEAD_SALT | sbit,
+                                   st), "lg_pool_head_fwd")
+    return logits, ehid, pooled, hid
+
+
+@detector_heads.register_fake
+def _(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, keep_hidden,
+      seed):
+    B = h.shape[1] if node_major else h.shape[0]
+    D = h.shape[2]
+    P = ends.shape[0]
+    ehid = h.new_empty(B * P, w1.shape[0]) if keep_hidden else h.new_empty(0)
+    return h.new_empty(B, P + 1), ehid, h.new_empty(B, D), h.new_empty(B, nw1.shape[0])
+
+
+@torch.library.custom_op(f"{NS}::detector_heads_backward", mutates_args=(), device_types="cuda")
+def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, ehid: Tensor, pooled: Tensor,
+                            hid: Tensor, nw1: Tensor, nw2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor,
+                            p_edge: float, p_noleak: float, node_major: bool
+                            ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """(dh, dW1, db1, dW2, db2, dnW1, dnb1, dnW2, dnb2): lg_edge_head_bwd -> per-pipe
+    endpoint grads; lg_pool_head_bwd -> dpooled and the NoLeakHead grads; ONE deterministic
+    incidence reduce (lg_pipe_scatter_bwd) adds dpooled / N to every node row."""
+    lib = load_library()
+    if ehid.numel() == 0:
+        raise RuntimeError("detector_heads was run with keep_hidden=False; no backward")
+    dl, h = _c(dlogits), _c(h)
+    N, B, D = h.shape if node_major else (h.shape[1], h.shape[0], h.shape[2])
+    lay = nat.LG_F_NODE_MAJOR if node_major else 0
+    P, hidden, nhidden = ends.shape[0], w1.shape[0], nw1.shape[0]
+    fe = nat.LG_F_DROPOUT if p_edge > 0.0 else 0
+    fn = nat.LG_F_DROPOUT if p_noleak > 0.0 else 0
+    dev = h.device
+    st = stream_of(h)
+    dpipe = torch.empty(B, P, 2, D, device=dev)
+    dw1, db1 = torch.empty_like(w1), torch.empty(hidden, device=dev)
+    dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
+    ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
+    with _timed("edge_bwd", dev):
+        check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
+                                   ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe | lay, p_edge,
+                                   ptr(ws), st), "lg_edge_head_bwd")
+    dpooled = torch.empty(B, D, device=dev)
+    ndw1, ndb1 = torch.empty_like(nw1), torch.empty(nhidden, device=dev)
+    ndw2, ndb2 = torch.empty_like(nw2), torch.empty(1, device=dev)
+    wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
+    with _timed("pool_head_bwd", dev):
+        check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
+                                   ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn),
+                                   st), "lg_pool_head_bwd")
+    dh = torch.empty_like(h)
+    with _timed("pipe_scatter", dev):
+        check(lib.lg_pipe_scatter_bwd(ptr(inc_rowptr), ptr(inc_item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P, D,
+                                      lay, st), "lg_pipe_scatter_bwd")
+    return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
+
+
+@detector_heads_backward.register_fake
+def _(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major):
+    H, NH = w1.shape[0], nw1.shape[0]
+    return (torch.empty_like(h), torch.empty_like(w1), w1.new_empty(H), torch.empty_like(w2), w2.new_empty(1),
+            torch.empty_like(nw1), nw1.new_empty(NH), torch.empty_like(nw2), nw2.new_empty(1))
+
+
+def _heads_setup(ctx, inputs, output):
+    (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, _, _) = inputs
+    _, ehid, pooled, hid = output
+    ctx.mark_non_differentiable(ehid, pooled, hid)
+    ctx.cfg = (p_edge, p_noleak, node_major)
+    ctx.save_for_backward(h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item)
+
+
+def _heads_bwd(ctx, dlogits, _dehid, _dpooled, _dhid):
+    h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item = ctx.saved_tensors
+    p_edge, p_noleak, node_major = ctx.cfg
+    g = torch.ops.leakgnn.detector_heads_backward(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr,
+                                                  inc_item, p_edge, p_noleak, node_major)
+    return tuple(g) + (None,) * 8
+
+
+detector_heads.register_autograd(_heads_bwd, setup_context=_heads_setup)
+
+
+# ============================================================================ module-facing helpers
+def seed_tensor(device: torch.device) -> Tensor:
+    """The dropout seed of one call site as a tensor (see ops._new_seed): a CPU int64 value
+    drawn from torch's CPU generator in eager mode; under HIP-graph capture a device word
+    re-drawn on every replay (a SeedSlots slot, or torch's graph-safe CUDA generator)."""
+    from . import ops
+    if ops._SEED_SLOTS is not None:
+        return ops._SEED_SLOTS.take_tensor()
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        return torch.randint(0, 2 ** 62, (1,), dtype=torch.long, device=device)
+    return torch.randint(0, 2 ** 62, (1,), dtype=torch.long)
+
+
+def detector_ops_available() -> bool:
+    return hasattr(torch.ops, NS) and hasattr(torch.ops.leakgnn, "gnn_trunk")

@@ -59,10 +59,11 @@ class LeakDetectorRef(nn.Module):
         B, L, S = residual.shape
         N = len(self.node_names)
         h_s = self.sensor_encoder(residual, tfeat)                                      # :176
-        h0 = torch.zeros(B, N, h_s.shape[-1], dtype=residual.dtype)                     # :179
-        idx = self.sensor_node_idx
+        dev = residual.device
+        h0 = torch.zeros(B, N, h_s.shape[-1], dtype=residual.dtype, device=dev)         # :179
+        idx = self.sensor_node_idx.to(dev)
         h0[:, idx, :] = h_s                                                             # :181
-        mask = torch.zeros(N, 1, dtype=residual.dtype)
+        mask = torch.zeros(N, 1, dtype=residual.dtype, device=dev)
         mask[idx, 0] = 1.0                                                              # :184-186
         h = torch.cat([h0, mask.unsqueeze(0).expand(B, -1, -1)], dim=-1)                # :188
         h = self.dropout(F.relu(self.sensor_to_node(h)))                                 # :189-190
@@ -73,11 +74,11 @@ class LeakDetectorRef(nn.Module):
             x = self.dropout(F.relu(conv(x, ei)))
             self.trace[f"conv{i}"] = x
         h_nodes = x.view(B, N, -1)                                                      # :204
-        u, v = self.pipe_ends[:, 0], self.pipe_ends[:, 1]                               # :206-208
+        u, v = self.pipe_ends[:, 0].to(dev), self.pipe_ends[:, 1].to(dev)               # :206-208
         h_u, h_v = h_nodes[:, u, :], h_nodes[:, v, :]                                   # :209-210
         feat = torch.cat([h_u, h_v, (h_u - h_v).abs()], dim=-1)                          # :87
         pipe_logits = self.edge_head.mlp(feat).squeeze(-1)                               # :88, 211
-        batch = torch.arange(B).repeat_interleave(N)                                    # :214
+        batch = torch.arange(B, device=dev).repeat_interleave(N)                        # :214
         pooled = gcn_ref.global_mean_pool(x, batch, size=B)                              # :215
         noleak = self.noleak_head.mlp(pooled).squeeze(-1).unsqueeze(-1)                  # :216
         return torch.cat([pipe_logits, noleak], dim=-1)                                  # :218

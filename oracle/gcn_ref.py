@@ -12,7 +12,9 @@ reference calls at detector.py:23 / :163 / :199 / :215:
       = scatter_add(edge_weight[:, None] * x[row], col); out += bias
   global_mean_pool: scatter(x, batch, dim=0, reduce='mean') = sum / count
 
-Scatter sums are accumulated in ascending edge order (index_add_ on CPU).
+Scatter sums are accumulated in ascending edge order (index_add_ on CPU).  The functions
+follow the device of their inputs, so the tests can also time the reference arithmetic as
+plain torch on the GPU (as an error yardstick, never as the product).
 """
 from __future__ import annotations
 
@@ -22,14 +24,15 @@ import torch
 def gcn_norm(edge_index: torch.Tensor, num_nodes: int, add_self_loops: bool = True, fill: float = 1.0,
              dtype=torch.float32):
     row, col = edge_index[0], edge_index[1]
-    w = torch.ones(row.numel(), dtype=dtype)
+    dev = edge_index.device
+    w = torch.ones(row.numel(), dtype=dtype, device=dev)
     if add_self_loops:
         keep = row != col
-        loops = torch.arange(num_nodes, dtype=torch.long)
+        loops = torch.arange(num_nodes, dtype=torch.long, device=dev)
         row = torch.cat([row[keep], loops])
         col = torch.cat([col[keep], loops])
-        w = torch.cat([w[keep], torch.full((num_nodes,), fill, dtype=dtype)])
-    deg = torch.zeros(num_nodes, dtype=dtype).index_add_(0, col, w)
+        w = torch.cat([w[keep], torch.full((num_nodes,), fill, dtype=dtype, device=dev)])
+    deg = torch.zeros(num_nodes, dtype=dtype, device=dev).index_add_(0, col, w)
     dis = deg.pow(-0.5)
     dis = dis.masked_fill(torch.isinf(dis), 0.0)
     return row, col, dis[row] * w * dis[col]
@@ -39,13 +42,15 @@ def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor, bi
              add_self_loops: bool = True, normalize: bool = True) -> torch.Tensor:
     """GCNConv.forward: weight is lin.weight [out, in]."""
     N = x.size(0)
+    edge_index = edge_index.to(x.device)
     if normalize:
         row, col, w = gcn_norm(edge_index, N, add_self_loops)
     else:
         row, col = edge_index[0], edge_index[1]
-        w = torch.ones(row.numel(), dtype=x.dtype)
+        w = torch.ones(row.numel(), dtype=x.dtype, device=x.device)
     h = x @ weight.t()
-    out = torch.zeros(N, h.size(1), dtype=h.dtype).index_add_(0, col, w.view(-1, 1) * h.index_select(0, row))
+    out = torch.zeros(N, h.size(1), dtype=h.dtype, device=x.device).index_add_(0, col,
+                                                                             w.view(-1, 1) * h.index_select(0, row))
     if bias is not None:
         out = out + bias
     return out
@@ -53,8 +58,10 @@ def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor, bi
 
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int | None = None) -> torch.Tensor:
     B = int(batch.max()) + 1 if size is None else int(size)
-    s = torch.zeros(B, x.size(1), dtype=x.dtype).index_add_(0, batch, x)
-    cnt = torch.zeros(B, dtype=x.dtype).index_add_(0, batch, torch.ones(batch.numel(), dtype=x.dtype))
+    batch = batch.to(x.device)
+    s = torch.zeros(B, x.size(1), dtype=x.dtype, device=x.device).index_add_(0, batch, x)
+    cnt = torch.zeros(B, dtype=x.dtype, device=x.device).index_add_(
+        0, batch, torch.ones(batch.numel(), dtype=x.dtype, device=x.device))
     return s / cnt.clamp(min=1).view(-1, 1)
 
 

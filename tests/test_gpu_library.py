@@ -1,0 +1,100 @@
+"""The torch.library registration of the hot-path ops (models/library.py, SURVEY §8 b):
+torch.library.opcheck (schema, fake-tensor shapes, autograd registration and the
+AOTAutograd dynamic-shape dispatch of forward + backward) on every differentiable op, and
+one LeakDetector step traced by torch.compile (aot_eager) against the eager step."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import LTA_INP, assert_close, load, lta_ids
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _graph(N=300, E=1500, seed=1):
+    from models.ops import GCNGraph
+    gen = torch.Generator().manual_seed(seed)
+    ei = torch.randint(0, N, (2, E), generator=gen)
+    return GCNGraph.build(ei, N, DEV)
+
+
+def _check(op, args):
+    torch.library.opcheck(op, args, test_utils=("test_schema", "test_autograd_registration", "test_faketensor",
+                                                "test_aot_dispatch_dynamic"))
+
+
+def test_opcheck_gcn_conv_and_mean_pool():
+    g = _graph()
+    x = torch.randn(300, 64, device=DEV, requires_grad=True)
+    W = torch.randn(64, 64, device=DEV, requires_grad=True)
+    b = torch.randn(64, device=DEV, requires_grad=True)
+    _check(torch.ops.leakgnn.gcn_conv.default, (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t))
+    _check(torch.ops.leakgnn.mean_pool.default, (torch.randn(4 * 50, 64, device=DEV, requires_grad=True), 4, 50))
+
+
+def test_opcheck_sensor_proj_and_gru():
+    h = torch.randn(3, 29, 64, device=DEV, requires_grad=True)
+    Wn = torch.randn(64, 65, device=DEV, requires_grad=True)
+    bn = torch.randn(64, device=DEV, requires_grad=True)
+    _check(torch.ops.leakgnn.sensor_proj.default, (h, Wn, bn))
+    r = torch.randn(3, 36, 29, device=DEV, requires_grad=True)
+    tf = torch.randn(3, 36, 9, device=DEV)
+    ws = [torch.randn(*s, device=DEV).div_(8).requires_grad_(True) for s in ((192, 10), (192, 64), (192,), (192,))]
+    _check(torch.ops.leakgnn.gru_encoder.default, (r, tf, *ws, True))
+
+
+@pytest.mark.parametrize("B,p", [(3, 0.0), (16, 0.1)])
+def test_opcheck_trunk_and_heads(B, p):
+    """gnn_trunk (window-major at B = 3, node-major with dropout at B = 16) and
+    detector_heads on L-TOWN-A, with the detector's own graph state."""
+    from models import ops
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV)
+    graph, inc, slot, sidx, live, nons = m._device_state(DEV)
+    nm = ops.use_node_major(B, 661, 64)
+    seed = torch.tensor([12345], dtype=torch.long)
+    proj = torch.randn(B, 29, 64, device=DEV, requires_grad=True)
+    wts = [c.lin.weight.detach().clone().requires_grad_(True) for c in m.convs]
+    bs = [c.bias.detach().clone().normal_(0, 0.1).requires_grad_(True) for c in m.convs]
+    nb = torch.randn(64, device=DEV, requires_grad=True)
+    g = graph
+    _check(torch.ops.leakgnn.gnn_trunk.default,
+           (proj, nb, wts, bs, slot, sidx, nons, live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t,
+            g.pairs_t, g.rowptr_t, g.col_t, g.w_t, p, nm, seed))
+    h = torch.randn((661, B, 64) if nm else (B, 661, 64), device=DEV).relu_().requires_grad_(True)
+    mlp, nmlp = m.edge_head.mlp, m.noleak_head.mlp
+    hw = [t.detach().clone().requires_grad_(True) for t in (mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
+                                                              nmlp[0].weight, nmlp[0].bias, nmlp[3].weight,
+                                                              nmlp[3].bias)]
+    _check(torch.ops.leakgnn.detector_heads.default, (h, *hw, inc.ends, inc.rowptr, inc.item, p, p, nm, True, seed))
+
+
+def test_torch_compile_aot_eager_matches_eager():
+    """The detector forward + backward traced by torch.compile (aot_eager: every
+    leakgnn:: op stays an opaque registered op) equals the eager run."""
+    from models.detector import LeakDetector
+    state = load("detector_b2.npz")
+    sensors, pipes = lta_ids()
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
+    m.load_state_dict({k[len("param."):]: torch.from_numpy(v) for k, v in state.items() if k.startswith("param.")})
+    r = torch.randn(20, 36, 29, device=DEV)
+    tf = torch.randn(20, 36, 9, device=DEV)
+    lab = torch.randint(0, len(pipes) + 1, (20,), device=DEV)
+
+    def step(model):
+        model.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.cross_entropy(model(r, tf), lab)
+        loss.backward()
+        return loss.detach(), [p.grad.clone() for p in model.parameters()]
+
+    l0, g0 = step(m)
+    mc = torch.compile(m, backend="aot_eager", fullgraph=True)
+    l1, g1 = step(mc)
+    assert_close(l1, l0, rtol=1e-6, what="compiled loss")
+    for a, b in zip(g1, g0):
+        assert_close(a, b, rtol=1e-6, what="compiled grad")
+    assert np.isfinite(l1.item())

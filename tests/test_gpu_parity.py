@@ -296,8 +296,8 @@ def test_detector_train_mode_replay_with_oracle_masks():
     grads = {n: p.grad.clone() for n, p in m.named_parameters()}
     m.zero_grad()
     torch.manual_seed(9)
-    seed_t = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # GNNTrunkFn draw
-    seed_h = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # HeadsFn draw
+    seed_t = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # gnn_trunk draw
+    seed_h = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item())   # detector_heads draw
     sc = 1.0 / 0.9
     R = B * N
     from oracle.dropout_ref import row_stream_mask
@@ -440,8 +440,9 @@ def test_detector_node_major_matches_window_major(train, monkeypatch):
 @pytest.mark.parametrize("train", [False, True])
 @pytest.mark.parametrize("D", [64, 32])
 def test_fused_heads_vs_torch(train, D, nm):
-    """HeadsFn (fused EdgeHead, mean pool + NoLeakHead, one (B, P+1) output, incidence-reduced
-    backward) vs float64 torch with the same dropout masks (oracle/dropout_ref.py)."""
+    """leakgnn::detector_heads (fused EdgeHead, mean pool + NoLeakHead, one (B, P+1) output,
+    incidence-reduced backward) vs float64 torch with the same dropout masks
+    (oracle/dropout_ref.py)."""
     _heads_case(train, D, nm, 5)
 
 
@@ -452,23 +453,31 @@ def test_fused_heads_multi_tile(D):
     _heads_case(True, D, True, 70)
 
 
+def _heads(inc, p, nm, params, keep=True):
+    """leakgnn::detector_heads on (h, W1, b1, W2, b2, V1, c1, V2, c2); the seed drawn as the
+    detector draws it (torch's CPU generator), logits only."""
+    from models import library
+    seed = library.seed_tensor(DEV) if p > 0 else torch.zeros(1, dtype=torch.long)
+    return torch.ops.leakgnn.detector_heads(*params, inc.ends, inc.rowptr, inc.item, p, p, nm, keep, seed)[0]
+
+
 def test_edge_head_eval_without_hidden():
     """No-grad forward passes hid = NULL (nothing kept for a backward); logits unchanged."""
-    from models.ops import HeadsConfig, HeadsFn, Incidence
+    from models.ops import Incidence
     g = load("graph_ltown_a.npz")
     inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV)
     gen = torch.Generator().manual_seed(3)
     ps = [torch.randn(*s, generator=gen).to(DEV) / 8 for s in
           ((4, 661, 64), (128, 192), (128,), (1, 128), (1,), (128, 64), (128,), (1, 128), (1,))]
-    a = HeadsFn.apply(HeadsConfig(inc, 0.1, False), *ps)
+    a = _heads(inc, 0.0, False, ps, keep=False)
     ps[1].requires_grad_(True)
-    b = HeadsFn.apply(HeadsConfig(inc, 0.1, False), *ps)
+    b = _heads(inc, 0.0, False, ps, keep=True)
     assert torch.equal(a, b.detach())
 
 
 def _heads_case(train, D, nm, B):
     from models import ops
-    from models.ops import HeadsConfig, HeadsFn, Incidence
+    from models.ops import Incidence
     g = load("graph_ltown_a.npz")
     ends = torch.from_numpy(g["pipe_ends"])
     inc = Incidence.build(ends, 661, DEV)
@@ -489,7 +498,7 @@ def _heads_case(train, D, nm, B):
     if nm:  # node-major input (N, B, D): the grad is compared in the same layout below
         params[0] = h.transpose(0, 1).contiguous().to(DEV).requires_grad_(True)
     torch.manual_seed(77)
-    logits = HeadsFn.apply(HeadsConfig(inc, 0.1, train, node_major=nm), *params)
+    logits = _heads(inc, 0.1 if train else 0.0, nm, params)
     (logits * dl.to(DEV)).sum().backward()
     # float64 reference with the same dropout masks
     ref = [t.double().requires_grad_(True) for t in (h, W1, b1, W2, b2, V1, c1, V2, c2)]

@@ -89,15 +89,16 @@ def test_captured_forward_reads_device_seeds():
         outs.append(out.clone())
         seeds.append([int(v) for v in slots.buf[:slots.i].cpu()])
     assert seeds[0] != seeds[1] and not torch.equal(outs[0], outs[1])  # re-drawn per replay
-    orig = ops._new_seed
+    from models import library
+    orig = library.seed_tensor
     for got, sd in zip(outs, seeds):
         it = iter(sd)
-        ops._new_seed = lambda device=None: (next(it), 0, None)
+        library.seed_tensor = lambda device=None: torch.tensor([next(it)], dtype=torch.long)
         try:
             with torch.no_grad():
                 ref = m(r, tf)
         finally:
-            ops._new_seed = orig
+            library.seed_tensor = orig
         assert torch.equal(got, ref)
 
 

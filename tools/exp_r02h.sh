@@ -1,10 +1,11 @@
 #!/bin/bash
-# r02h: full GPU suite, then the bench (all new legs) and its rocprofv3 kernel stats
+# r02h: full GPU suite (no -x: report every failure), then the bench and its rocprofv3 kernel stats
 set -o pipefail
 OUT=gpurun_out/r02h; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > $OUT/tests.log 2>&1 || { grep -E "FAILED|Error" $OUT/tests.log | head -5; tail -40 $OUT/tests.log; exit 1; }
-grep -E "passed|failed" $OUT/tests.log | tail -2
+timeout -k 10 1200 python -u -m pytest tests -v --timeout 300 --timeout-method thread -m gpu > $OUT/tests.log 2>&1
+grep -E "FAILED|passed|failed" $OUT/tests.log | tail -12
+grep -E "^E  " $OUT/tests.log | head -30
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-pmc --no-c4 --steps 20 --warmup 5 > $OUT/bench_prof.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
