@@ -289,8 +289,11 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     f32x4 dwa[G::KT];
 #pragma unroll
     for (int i = 0; i < G::KT; ++i) dwa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 dw2a = f32x4{0.f, 0.f, 0.f, 0.f}, db1a = dw2a;
-    double db2 = 0.0;  // sum of all dlogits: heavy cancellation, kept in fp64 end to end
+    f32x4 dw2a = f32x4{0.f, 0.f, 0.f, 0.f};
+    // db1 / db2 are sums of dlogit-weighted terms that cancel heavily (the dlogits of one
+    // window sum to ~0 under the CE gradient): kept in fp64 end to end
+    double db1a[4] = {0.0, 0.0, 0.0, 0.0};
+    double db2 = 0.0;
 
     const int64_t step = gridDim.x;
     int64_t tile = blockIdx.x;
@@ -338,7 +341,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             for (int j = 0; j < 4; ++j) {
                 g[j] = hp[i][j] > 0.f ? dl[i] * w2g[j] * dscale : 0.f;
                 dw2a[j] = fmaf(dl[i], hp[i][j], dw2a[j]);
-                db1a[j] += g[j];
+                db1a[j] += static_cast<double>(g[j]);
             }
             if (n4 == 0) db2 += static_cast<double>(dl[i]);
             st_split4(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
@@ -426,27 +429,33 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     }
     db2 += __shfl_xor(db2, 32);
     __syncthreads();  // the last tile's LDS readers are done: reuse the partials area
-    float* fin = reinterpret_cast<float*>(red);
-    double* find = reinterpret_cast<double*>(fin + NW * 32 * 8);
+    float* fin = reinterpret_cast<float*>(red);                  // [NW][32][4] dW2
+    double* find = reinterpret_cast<double*>(fin + NW * 32 * 4);  // [NW][32][4] db1, [NW] db2
     if (lane < 32) {
-        st4(fin + (w * 32 + lane) * 8, db1a);
-        st4(fin + (w * 32 + lane) * 8 + 4, dw2a);
+        st4(fin + (w * 32 + lane) * 4, dw2a);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) find[(w * 32 + lane) * 4 + j] = db1a[j];
     }
-    if (lane == 0) find[w] = db2;
+    if (lane == 0) find[NW * 32 * 4 + w] = db2;
     __syncthreads();
     if (threadIdx.x < 32) {
-        f32x4 a = ld4(fin + threadIdx.x * 8), b = ld4(fin + threadIdx.x * 8 + 4);
+        f32x4 b = ld4(fin + threadIdx.x * 4);
+        double a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = find[threadIdx.x * 4 + j];
 #pragma unroll
         for (int i = 1; i < NW; ++i) {
-            a += ld4(fin + (i * 32 + threadIdx.x) * 8);
-            b += ld4(fin + (i * 32 + threadIdx.x) * 8 + 4);
+            b += ld4(fin + (i * 32 + threadIdx.x) * 4);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] += find[(i * 32 + threadIdx.x) * 4 + j];
         }
-        st4(out + HID * G::K3 + 4 * threadIdx.x, a);
+        st4(out + HID * G::K3 + 4 * threadIdx.x,
+            f32x4{static_cast<float>(a[0]), static_cast<float>(a[1]), static_cast<float>(a[2]), static_cast<float>(a[3])});
         st4(out + HID * G::K3 + HID + 4 * threadIdx.x, b);
     }
     if (threadIdx.x == 0) {
-        double s = find[0];
-        for (int i = 1; i < NW; ++i) s += find[i];
+        double s = find[NW * 32 * 4];
+        for (int i = 1; i < NW; ++i) s += find[NW * 32 * 4 + i];
         db2slab[blockIdx.x] = s;
     }
 }

@@ -121,6 +121,10 @@ class LeakDetector(nn.Module):
         self.edge_head = EdgeHead(node_hidden, hidden_dim=128, dropout=dropout)
         self.noleak_head = NoLeakHead(node_hidden, hidden_dim=128, dropout=dropout)
         self._dev_state: Dict[torch.device, tuple] = {}
+        # Test hook: a dict here receives the step's ReLU outputs as the kernels produced them
+        # ("xs": node init + every GCN layer, "edge_hidden", "noleak_hidden"), so parity tests
+        # can evaluate the fp64 truth on the same side of every ReLU kink.  None: nothing kept.
+        self.capture: Optional[dict] = None
 
     # -- device-resident graph state (built once per device; not part of state_dict)
     def _device_state(self, device: torch.device):
@@ -151,6 +155,11 @@ class LeakDetector(nn.Module):
         # rows with a sensor: [h_s, 1] W^T + b ; rows without: [0, 0] W^T + b = b
         proj = torch.ops.leakgnn.sensor_proj(h_s, Wn, bn)                  # (B, S, D)
         N, D = len(self.node_names), Wn.shape[0]
+        if self.capture is not None and torch.is_grad_enabled():
+            for name, t in (("h_s", h_s), ("proj", proj)):
+                if t.requires_grad:
+                    t.retain_grad()
+                self.capture[name] = t
         nm = ops.use_node_major(B, N, D)
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
@@ -169,8 +178,10 @@ class LeakDetector(nn.Module):
         keep = torch.is_grad_enabled() and (h_nodes.requires_grad or any(t.requires_grad for t in hw))
         seed = library.seed_tensor(residual.device) if (pe > 0.0 or pn > 0.0) else _NO_SEED
         # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-218)
-        return torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep,
-                                                seed)[0]
+        out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed)
+        if self.capture is not None:
+            self.capture.update(xs=xs, node_major=nm, edge_hidden=out[1], noleak_hidden=out[3])
+        return out[0]
 
 
 _NO_SEED = torch.zeros(1, dtype=torch.long)  # seed argument of an op that draws no dropout mask

@@ -54,6 +54,23 @@ class LeakDetectorRef(nn.Module):
         self.edge_head = _MLPHead(3 * node_hidden, 128, dropout)
         self.noleak_head = _MLPHead(node_hidden, 128, dropout)
         self.trace = {}
+        # Test hook: ReLU sites ("init", "conv0", "conv1", "edge", "noleak") -> 0/1 mask used
+        # instead of the sign of this run's own pre-activation; "absdiff" -> the sign pattern
+        # of h_u - h_v for the |h_u - h_v| features (-1 / 0 / 1).  Gradient parity of an fp32
+        # path is checked against the fp64 truth on the SAME branch of every ReLU: a unit whose
+        # pre-activation sits within fp32 rounding of 0 may land on either side.  The
+        # pre-activations of every site are kept in trace["pre_<site>"].
+        self.relu_masks = {}
+
+    def _abs(self, site, d):  # |d|, or d * (the given sign pattern): abs has a kink at 0 too
+        self.trace[f"pre_{site}"] = d
+        sg = self.relu_masks.get(site)
+        return d.abs() if sg is None else d * sg.to(d.dtype).to(d.device).reshape(d.shape)
+
+    def _relu(self, site, z):
+        self.trace[f"pre_{site}"] = z
+        m = self.relu_masks.get(site)
+        return F.relu(z) if m is None else z * m.to(z.dtype).to(z.device).reshape(z.shape)
 
     def forward(self, residual, tfeat=None):
         B, L, S = residual.shape
@@ -66,19 +83,21 @@ class LeakDetectorRef(nn.Module):
         mask = torch.zeros(N, 1, dtype=residual.dtype, device=dev)
         mask[idx, 0] = 1.0                                                              # :184-186
         h = torch.cat([h0, mask.unsqueeze(0).expand(B, -1, -1)], dim=-1)                # :188
-        h = self.dropout(F.relu(self.sensor_to_node(h)))                                 # :189-190
+        h = self.dropout(self._relu("init", self.sensor_to_node(h)))                     # :189-190
         self.trace["node_init"] = h
         x = h.reshape(B * N, -1)                                                        # :193
         ei = torch.from_numpy(graph_ref.batchify(self.edge_index_single.numpy(), N, B))  # :195-196
         for i, conv in enumerate(self.convs):                                            # :198-201
-            x = self.dropout(F.relu(conv(x, ei)))
+            x = self.dropout(self._relu(f"conv{i}", conv(x, ei)))
             self.trace[f"conv{i}"] = x
         h_nodes = x.view(B, N, -1)                                                      # :204
         u, v = self.pipe_ends[:, 0].to(dev), self.pipe_ends[:, 1].to(dev)               # :206-208
         h_u, h_v = h_nodes[:, u, :], h_nodes[:, v, :]                                   # :209-210
-        feat = torch.cat([h_u, h_v, (h_u - h_v).abs()], dim=-1)                          # :87
-        pipe_logits = self.edge_head.mlp(feat).squeeze(-1)                               # :88, 211
+        feat = torch.cat([h_u, h_v, self._abs("absdiff", h_u - h_v)], dim=-1)             # :87
+        mlp = self.edge_head.mlp                                                         # :88, 211
+        pipe_logits = mlp[3](mlp[2](self._relu("edge", mlp[0](feat)))).squeeze(-1)
         batch = torch.arange(B, device=dev).repeat_interleave(N)                        # :214
         pooled = gcn_ref.global_mean_pool(x, batch, size=B)                              # :215
-        noleak = self.noleak_head.mlp(pooled).squeeze(-1).unsqueeze(-1)                  # :216
+        nmlp = self.noleak_head.mlp                                                      # :216
+        noleak = nmlp[3](nmlp[2](self._relu("noleak", nmlp[0](pooled)))).squeeze(-1).unsqueeze(-1)
         return torch.cat([pipe_logits, noleak], dim=-1)                                  # :218

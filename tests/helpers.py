@@ -109,3 +109,48 @@ def assert_grads_match_truth(gpu: dict, cpu32: dict, cpu64: dict, slack: float =
     assert not bad, "; ".join(bad)
     e_gpu2, e_cpu2, n2 = e_gpu2 ** 0.5, e_cpu2 ** 0.5, n2 ** 0.5
     assert e_gpu2 <= max(slack * e_cpu2, rtol * n2), f"grad vector: gpu {e_gpu2:.3e}, cpu32 {e_cpu2:.3e}, |g| {n2:.3e}"
+
+
+def hip_relu_masks(cap: dict, B: int, N: int, P: int, ends) -> dict:
+    """The kink decisions the HIP path took, from LeakDetector.capture, in the shapes of the
+    oracle's sites (oracle/detector_ref.py relu_masks): every ReLU (its stored
+    post-ReLU/dropout activations: x > 0 <=> unit active and kept) and the sign of
+    h_u - h_v behind the EdgeHead's |h_u - h_v| features (pipe ends `ends` (P, 2)), taken
+    from the same fp32 node features the edge kernels read."""
+    xs = cap["xs"]
+    hn = xs[-1].detach()
+    hn = hn.permute(1, 0, 2) if cap["node_major"] else hn  # (B, N, D)
+    ends = ends.to(hn.device).long()
+    sign = torch.sign(hn[:, ends[:, 0]] - hn[:, ends[:, 1]]).cpu()
+
+    def bnd(x):
+        x = x.detach()
+        return (x.permute(1, 0, 2) if cap["node_major"] else x).reshape(B, N, -1).cpu() > 0
+    out = {"init": bnd(xs[0])}
+    for l, x in enumerate(xs[1:]):
+        out[f"conv{l}"] = bnd(x)
+    out["edge"] = cap["edge_hidden"].detach().reshape(B, P, -1).cpu() > 0
+    out["noleak"] = cap["noleak_hidden"].detach().reshape(B, -1).cpu() > 0
+    out["absdiff"] = sign
+    return out
+
+
+def check_relu_ties(pre64: dict, masks: dict, keep: dict | None = None, rel: float = 1e-5) -> int:
+    """Every kink (ReLU, or the sign behind |h_u - h_v|) where the HIP path and the fp64
+    oracle took different sides must be a tie: |fp64 pre-activation| <= rel x the site's
+    largest.  Units dropped by dropout (keep == 0)
+    are not decisions.  Returns the number of such ties (each then enters the fp64 truth
+    through relu_masks, so gradients are compared on the same branch)."""
+    ties = 0
+    for site, m in masks.items():
+        z = pre64[site].detach().double().cpu().reshape(m.shape)
+        flip = m != (z > 0) if m.dtype == torch.bool else m != torch.sign(z)
+        if keep is not None and site in keep:
+            flip &= keep[site].cpu().reshape(m.shape) != 0
+        n = int(flip.sum())
+        if n:
+            worst = z[flip].abs().max().item()
+            lim = rel * z.abs().max().item()
+            assert worst <= lim, f"ReLU site {site}: {n} HIP decisions differ from fp64, |pre| up to {worst:.3e} > {lim:.3e}"
+            ties += n
+    return ties

@@ -18,7 +18,8 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import LTA_INP, RTOL, assert_close, assert_grads_match_truth, load, lta_ids
+from helpers import (LTA_INP, RTOL, assert_close, assert_grads_match_truth, check_relu_ties, hip_relu_masks, load,
+                     lta_ids)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -181,11 +182,37 @@ def _random_ref(seed: int):
     return {k: v.clone() for k, v in ref.state_dict().items()}
 
 
+def _oracle_b256(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None):
+    """The oracle detector in eval mode: (logits, grads, fp64-comparable ReLU
+    pre-activations, upstream gradient) for `up`, or for the CE gradient of `lab` in this
+    run's own precision when up is None.  masks: ReLU decisions to use (relu_masks)."""
+    from oracle.detector_ref import LeakDetectorRef
+    sensors, pipes = lta_ids()
+    mr = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
+    mr.load_state_dict(sd)
+    mr = mr.to(dt).to(dev)
+    mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)
+    mr.relu_masks = masks or {}
+    out = mr(r.to(dt).to(dev), tf.to(dt).to(dev))
+    if up is None:
+        lo = out.detach().requires_grad_(True)
+        torch.nn.functional.cross_entropy(lo, lab).backward()
+        up = lo.grad.clone()
+    out.backward(up.to(dt).to(dev))
+    pre = {k[len("pre_"):]: v.detach() for k, v in mr.trace.items() if k.startswith("pre_")}
+    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in mr.named_parameters()}, pre, up
+
+
 def test_detector_b256_eval_vs_oracle():
     """L-TOWN-A at the bench batch (B = 256, node-major trunk), eval mode, random weights:
-    logits within 1e-5 of the oracle; grads for the oracle's fp64 CE gradient vs fp64 truth."""
+    logits within 1e-5 of the oracle; grads for the oracle's fp64 CE gradient vs fp64 truth
+    on the same side of every kink.  A ReLU pre-activation within fp32 rounding of 0, or an
+    h_u - h_v of two nodes with (near-)identical features behind |h_u - h_v|, may fall
+    either way in ANY fp32 evaluation; one such unit moves a gradient by a whole term
+    (measured: 8 sign ties of h_u - h_v put torch fp32 2e-2 off fp64 in the GRU input
+    gradient).  check_relu_ties proves every differing decision is such a tie, then the
+    fp64 truth and the fp32 yardsticks are all evaluated on the HIP path's side."""
     from models.detector import LeakDetector
-    from oracle.detector_ref import LeakDetectorRef
     sensors, pipes = lta_ids()
     sd = _random_ref(41)
     B = 256
@@ -193,39 +220,34 @@ def test_detector_b256_eval_vs_oracle():
     r = torch.randn(B, 36, 29, generator=gen)
     tf = torch.randn(B, 36, 9, generator=gen)
     lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen)
-    logits, grads = {}, {}
-    for dt, dev in ((torch.float64, "cpu"), (torch.float32, "cpu"), (torch.float32, "cuda")):
-        mr = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
-        mr.load_state_dict(sd)
-        mr = mr.to(dt).to(dev)
-        mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)
-        out = mr(r.to(dt).to(dev), tf.to(dt).to(dev))
-        if dt == torch.float64:
-            l64 = out.detach().requires_grad_(True)
-            torch.nn.functional.cross_entropy(l64, lab).backward()
-            up = l64.grad.clone()
-        out.backward(up.to(dt).to(dev))
-        logits[(dt, dev)] = out.detach().cpu()
-        grads[(dt, dev)] = {n: p.grad.detach().cpu() for n, p in mr.named_parameters()}
+    _, _, pre64, up = _oracle_b256(sd, r, tf, torch.float64, "cpu", lab=lab)
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
     m.load_state_dict(sd)
+    m.capture = {}
     lg = m(r.to(DEV), tf.to(DEV))
     lg.backward(up.float().to(DEV))
-    assert_close(lg, logits[(torch.float32, "cpu")], what="B=256 logits")
+    masks = hip_relu_masks(m.capture, B, len(m.node_names), len(pipes), m.pipe_ends)
+    check_relu_ties(pre64, masks)
+    # truth and fp32 yardsticks all on the HIP path's side of every kink
+    _, g64, _, _ = _oracle_b256(sd, r, tf, torch.float64, "cpu", up=up, masks=masks)
+    o32, g32, _, _ = _oracle_b256(sd, r, tf, torch.float32, "cpu", up=up, masks=masks)
+    _, g32d, _, _ = _oracle_b256(sd, r, tf, torch.float32, DEV, up=up, masks=masks)
+    assert_close(lg, o32, what="B=256 logits")
     # The CE gradient makes dW1 of the EdgeHead and the conv bias grads the difference of two
     # sums over ~2e5 rows that nearly cancel (the label rows against all the others): per
     # tensor 5e-5 of scale, or 4x the error of the reference arithmetic in fp32 (torch on the
     # CPU or on this GPU); the whole-vector 2-norm bar stays at 1e-5
-    assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, grads[(torch.float32, "cpu")],
-                             grads[(torch.float64, "cpu")], ref32=grads[(torch.float32, "cuda")], rtol_tensor=5e-5)
+    assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64, ref32=g32d, rtol_tensor=5e-5)
 
 
-def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu"):
+def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu", masks=None, aux=None):
     """The oracle detector (reference detector.py:170-218 op for op) in train mode on the
     CPU, with every dropout mask the HIP path draws regenerated by oracle/dropout_ref.py
     from the same seeds: node init (per-element hash), GCN layers (row streams), EdgeHead
-    hidden (row streams), NoLeakHead hidden (per-element hash).  Returns logits and grads
-    for the upstream gradient `up`."""
+    hidden (row streams), NoLeakHead hidden (per-element hash).  Returns logits, grads for
+    the upstream gradient `up`, the ReLU pre-activations and the dropout keep masks per
+    site; masks: ReLU decisions to use instead of the pre-activations' signs; aux: a dict
+    that receives h_s and the node-init pre-activation z0 (their .grad kept)."""
     from models import ops
     from oracle import gcn_ref, graph_ref
     from oracle.detector_ref import LeakDetectorRef
@@ -239,6 +261,13 @@ def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu"):
     N, D, P = len(m.node_names), 64, len(pipes)
     R = B * N
     sc = 1.0 / 0.9
+    pre = {}
+
+    def relu(site, z):
+        pre[site] = z.detach()
+        if masks is None or site not in masks:
+            return torch.relu(z)
+        return z * masks[site].to(dt).to(dev).reshape(z.shape)
 
     def t(a):
         return torch.from_numpy(a.astype(np.float64)).to(dt).to(dev)
@@ -252,22 +281,31 @@ def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu"):
     h0[:, si] = h_s
     mask = torch.zeros(N, 1, dtype=dt, device=dev)
     mask[si] = 1
-    x = torch.relu(m.sensor_to_node(torch.cat([h0, mask.expand(B, -1, -1)], -1))).reshape(R, D) * mk0 * sc
+    z0 = m.sensor_to_node(torch.cat([h0, mask.expand(B, -1, -1)], -1))
+    if aux is not None:
+        h_s.retain_grad()
+        z0.retain_grad()
+        aux.update(h_s=h_s, z0=z0)
+    x = relu("init", z0).reshape(R, D) * mk0 * sc
     ei = torch.from_numpy(graph_ref.batchify(m.edge_index_single.numpy(), N, B))
     for l, conv in enumerate(m.convs):
-        x = torch.relu(conv(x, ei)) * mkl[l] * sc
+        x = relu(f"conv{l}", conv(x, ei)) * mkl[l] * sc
     hn = x.view(B, N, D)
     u, v = m.pipe_ends[:, 0].to(dev), m.pipe_ends[:, 1].to(dev)
-    feat = torch.cat([hn[:, u], hn[:, v], (hn[:, u] - hn[:, v]).abs()], -1).reshape(B * P, 3 * D)
+    d = hn[:, u] - hn[:, v]
+    pre["absdiff"] = d.detach()
+    ad = d.abs() if masks is None or "absdiff" not in masks else d * masks["absdiff"].to(dt).to(dev)
+    feat = torch.cat([hn[:, u], hn[:, v], ad], -1).reshape(B * P, 3 * D)
     mlp = m.edge_head.mlp
-    hid = torch.relu(mlp[0](feat)) * me * sc
+    hid = relu("edge", mlp[0](feat).view(B, P, -1)).reshape(B * P, -1) * me * sc
     pl = mlp[3](hid).view(B, P)
     pooled = gcn_ref.global_mean_pool(x, torch.arange(B).repeat_interleave(N), size=B)  # follows x's device
     nmlp = m.noleak_head.mlp
-    nl = nmlp[3](torch.relu(nmlp[0](pooled)) * mn * sc)
+    nl = nmlp[3](relu("noleak", nmlp[0](pooled)) * mn * sc)
     out = torch.cat([pl, nl], -1)
     out.backward(up.to(dt).to(dev))
-    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
+    keep = {"init": mk0, "conv0": mkl[0], "conv1": mkl[1], "edge": me, "noleak": mn}
+    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()}, pre, keep
 
 
 def test_detector_b256_train_vs_oracle_masks():
@@ -285,15 +323,21 @@ def test_detector_b256_train_vs_oracle_masks():
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
     m.load_state_dict(sd)
     torch.manual_seed(53)
+    m.capture = {}
     lg = m(r.to(DEV), tf.to(DEV))
     lg.backward(up.to(DEV))
+    masks = hip_relu_masks(m.capture, B, len(m.node_names), len(pipes), m.pipe_ends)
     torch.manual_seed(53)
     seeds = tuple(int(torch.randint(0, 2 ** 62, (1,), dtype=torch.long).item()) for _ in range(2))
-    o32, g32 = _replay_train_cpu(sd, r, tf, seeds, torch.float32, up)
-    o64, g64 = _replay_train_cpu(sd, r, tf, seeds, torch.float64, up)
-    assert_close(o32, o64, rtol=1e-5, what="replay fp32 vs fp64 (self-check)")
+    m.capture = None
+    o64, _, pre64, keep = _replay_train_cpu(sd, r, tf, seeds, torch.float64, up)
     assert_close(lg, o64, what="B=256 train-mode logits")
-    _, g32d = _replay_train_cpu(sd, r, tf, seeds, torch.float32, up, dev=DEV)
+    check_relu_ties(pre64, masks, keep)
+    # truth and fp32 yardsticks on the HIP path's side of every kink (see the eval test)
+    _, g64, _, _ = _replay_train_cpu(sd, r, tf, seeds, torch.float64, up, masks=masks)
+    o32, g32, _, _ = _replay_train_cpu(sd, r, tf, seeds, torch.float32, up, masks=masks)
+    assert_close(o32, o64, rtol=1e-5, what="replay fp32 vs fp64 (self-check)")
+    _, g32d, _, _ = _replay_train_cpu(sd, r, tf, seeds, torch.float32, up, dev=DEV, masks=masks)
     assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64, ref32=g32d, rtol_tensor=5e-5)
 
 

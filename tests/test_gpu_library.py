@@ -73,9 +73,13 @@ def test_opcheck_trunk_and_heads(B, p):
     _check(torch.ops.leakgnn.detector_heads.default, (h, *hw, inc.ends, inc.rowptr, inc.item, p, p, nm, True, seed))
 
 
-def test_torch_compile_aot_eager_matches_eager():
+@pytest.mark.parametrize("fullgraph", [False, True])
+def test_torch_compile_aot_eager_matches_eager(fullgraph):
     """The detector forward + backward traced by torch.compile (aot_eager: every
-    leakgnn:: op stays an opaque registered op) equals the eager run."""
+    leakgnn:: op stays an opaque registered op) equals the eager run.  Dynamo refuses to
+    wrap an nn.GRU module by default (torch._dynamo.config.allow_rnn), and the encoder
+    reads its weights off the reference's nn.GRU (state-dict compatibility): plain
+    torch.compile graph-breaks there; with allow_rnn the whole step is ONE graph."""
     from models.detector import LeakDetector
     state = load("detector_b2.npz")
     sensors, pipes = lta_ids()
@@ -92,8 +96,10 @@ def test_torch_compile_aot_eager_matches_eager():
         return loss.detach(), [p.grad.clone() for p in model.parameters()]
 
     l0, g0 = step(m)
-    mc = torch.compile(m, backend="aot_eager", fullgraph=True)
-    l1, g1 = step(mc)
+    torch._dynamo.reset()
+    mc = torch.compile(m, backend="aot_eager", fullgraph=fullgraph)
+    with torch._dynamo.config.patch(allow_rnn=fullgraph):
+        l1, g1 = step(mc)
     assert_close(l1, l0, rtol=1e-6, what="compiled loss")
     for a, b in zip(g1, g0):
         assert_close(a, b, rtol=1e-6, what="compiled grad")
