@@ -84,6 +84,20 @@ enum {
 int lg_abi_version(void);
 const char* lg_strerror(int code);
 
+/* Kernel timing (bench.py; no reference counterpart — the reference has no kernels).
+ * lg_timing_arm(slot): the NEXT library kernel launch on this host thread that is the main
+ * kernel of an entry point (lg_gcn_fwd[_nm], lg_gcn_bwd[_nm], lg_edge_head_fwd/bwd,
+ * lg_gru_fwd/bwd, lg_node_init_fwd, lg_pipe_scatter, lg_pool_head_fwd/bwd, lg_linear_dw,
+ * lg_spmm) is launched with hipExtLaunchKernelGGL and the event pair of `slot` (created on
+ * first use, reused after; process-wide, so a call on another thread, e.g. autograd's
+ * worker, is read back on the caller's): their elapsed time is that kernel's own execution, as a
+ * profiler's kernel trace reports it.  lg_timing_disarm returns 1 if the armed pair was
+ * never consumed (and drops it), else 0.  lg_timing_elapsed: milliseconds of `slot` once
+ * its stop event has completed.  Not for use inside stream capture. */
+int lg_timing_arm(int slot);
+int lg_timing_disarm(void);
+int lg_timing_elapsed(int slot, float* ms);
+
 /* ---------------------------------------------------------------------------
  * K4  gcn_norm + CSR build, once per graph.
  * Replaces: PyG GCNConv.forward -> gcn_norm (add_remaining_self_loops, degree,

@@ -1,5 +1,6 @@
 // Shared device helpers for libleakgnn (gfx950 / CDNA4 only).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "leakgnn.h"
@@ -13,6 +14,24 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 static inline hipStream_t lg_stream(lg_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Kernel timing (lg_timing_arm, include/leakgnn.h): the armed event pair of this host
+// thread, or nullptr; taking it disarms.  lg_launch sends a launch through
+// hipExtLaunchKernelGGL with that pair, so the events carry the kernel's own start and end
+// (its dispatch packet), not the enqueue gap around it; unarmed it is a plain launch.
+struct LgTimingPair {
+    hipEvent_t start, stop;
+};
+LgTimingPair* lg_timing_take();
+
+template <typename... P, typename... A>
+inline void lg_launch(void (*kernel)(P...), dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... args) {
+    static_assert(sizeof...(P) == sizeof...(A), "kernel argument count");
+    if (LgTimingPair* t = lg_timing_take())
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t->start, t->stop, 0, static_cast<P>(args)...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, static_cast<P>(args)...);
+}
 
 static inline int lg_num_cus() {
     int dev = 0, cus = 0;

@@ -502,11 +502,11 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 #endif
     if (D == 64) {
         if (!allow_lds(k_edge_fwd<64>, EG<64>::FWD_LDS)) return LG_EHIP;
-        k_edge_fwd<64><<<grid, NT, EG<64>::FWD_LDS, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
+        lg_launch(k_edge_fwd<64>, grid, NT, EG<64>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
                                                          ntiles, dropout_arg, dropout_p, scale, seed, salt);
     } else {
         if (!allow_lds(k_edge_fwd<32>, EG<32>::FWD_LDS)) return LG_EHIP;
-        k_edge_fwd<32><<<grid, NT, EG<32>::FWD_LDS, s>>>(ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
+        lg_launch(k_edge_fwd<32>, grid, NT, EG<32>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
                                                          ntiles, dropout_arg, dropout_p, scale, seed, salt);
     }
     LG_RET_IF_LAUNCH_FAILED();
@@ -548,12 +548,12 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     } else if (D == 64) {
         constexpr int64_t lds = EG<64>::BWD_LDS;
         if (!allow_lds(k_edge_bwd<64>, lds)) return LG_EHIP;
-        k_edge_bwd<64><<<grid, NT, lds, s>>>(ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
+        lg_launch(k_edge_bwd<64>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
                                              ntiles, scale);
     } else {
         constexpr int64_t lds = EG<32>::BWD_LDS;
         if (!allow_lds(k_edge_bwd<32>, lds)) return LG_EHIP;
-        k_edge_bwd<32><<<grid, NT, lds, s>>>(ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
+        lg_launch(k_edge_bwd<32>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
                                              ntiles, scale);
     }
     LG_RET_IF_LAUNCH_FAILED();

@@ -670,7 +670,7 @@ int launch_fwd(const int32_t* rowptr, const int32_t* col, const float* w, const 
     auto kern = k_gcn_fwd<D, kFwdWaves, CL, DROP>;
     if (!allow_lds(kern, dyn)) return LG_EHIP;
     const int grid = resident_grid(kern, 64 * kFwdWaves, dyn, ceil_div(ntiles, kFwdWaves), 2);
-    kern<<<grid, 64 * kFwdWaves, dyn, s>>>(rowptr, col, w, x, W, bias, y, static_cast<uint32_t>(N),
+    lg_launch(kern, grid, 64 * kFwdWaves, dyn, s, rowptr, col, w, x, W, bias, y, static_cast<uint32_t>(N),
                                             lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
                                             ntiles, relu_floor, p, scale, seed, salt, row_offset,
                                             static_cast<int>(csr_words));
@@ -702,7 +702,7 @@ int launch_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, 
     if (!allow_lds(kern, dyn)) return LG_EHIP;
     // every chunk of a split launch uses the first chunk's grid (the slab rows it accumulates into)
     if (*grid_io == 0) *grid_io = resident_grid(kern, 64 * kBwdWaves, dyn, ceil_div(ntiles, kBwdWaves), 2);
-    kern<<<*grid_io, 64 * kBwdWaves, dyn, s>>>(rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab,
+    lg_launch(kern, *grid_io, 64 * kBwdWaves, dyn, s, rowptr_t, col_t, w_t, dy, y, x, W, node_slot, dx, slab,
                                                 static_cast<uint32_t>(N),
                                                 lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
                                                 ntiles, mask_out, scale_in, scale_out, static_cast<int>(csr_words),
@@ -743,7 +743,7 @@ int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* w, const
     const int64_t dyn = CL ? csr_bytes : 0;
     auto kern = k_spmm<D, CL>;
     const int grid = resident_grid(kern, 64 * kSpmmWaves, dyn, ceil_div(ntiles, kSpmmWaves), 8);
-    kern<<<grid, 64 * kSpmmWaves, dyn, s>>>(rowptr, col, w, x, y, static_cast<uint32_t>(N),
+    lg_launch(kern, grid, 64 * kSpmmWaves, dyn, s, rowptr, col, w, x, y, static_cast<uint32_t>(N),
                                              lg_make_fastdiv(static_cast<uint32_t>(N)), static_cast<uint32_t>(R),
                                              ntiles);
     LG_RET_IF_LAUNCH_FAILED();

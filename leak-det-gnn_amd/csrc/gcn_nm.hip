@@ -1438,25 +1438,25 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
             auto kern = k_gcn_fwd_nm<DD, DR>;                                                                      \
             const size_t dyn1 = 4 * static_cast<size_t>(DD * (DD + 4) + DD + kNmFwdWaves * 16 * (DD + 4));        \
             const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn1, ntiles, kNmFwdWaves, 4);                        \
-            kern<<<grid, 64 * kNmFwdWaves, dyn1, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,     \
+            lg_launch(kern, grid, 64 * kNmFwdWaves, dyn1, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,     \
                                                       dropout_p, scale, seed, salt);                               \
         } else if (lab_nm2) {                                                                                      \
             auto kern = nm2_kernel<DD, DR>(flags);                                                                 \
             const size_t dyn2 = split ? Nm2Lds<DD, true>::BYTES : Nm2Lds<DD, false>::BYTES;                        \
             const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
-            kern<<<grid, 64 * kNm2Waves, dyn2, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
+            lg_launch(kern, grid, 64 * kNm2Waves, dyn2, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
                                                     dropout_p, scale, seed, salt);                                 \
         } else if (w8) {                                                                                           \
             auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
-            kern<<<grid, 64 * 8, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
+            lg_launch(kern, grid, 64 * 8, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
                                             salt);                                                                 \
         } else {                                                                                                   \
             auto kern = relu ? nm3_kernel<DD, DR, true, 4>(flags) : nm3_kernel<DD, DR, false, 4>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 4>::BYTES : Nm3Lds<DD, false, 4>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
-            kern<<<grid, 64 * 4, dyn3, s>>>(nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
+            lg_launch(kern, grid, 64 * 4, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
                                             salt);                                                                 \
         }                                                                                                          \
     } while (0)
@@ -1502,7 +1502,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
             auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                 \
             grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),\
                                  2 * lg_num_cus());                                                                \
-            kern<<<grid, 64 * kNmBwdWaves, dyn, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,          \
+            lg_launch(kern, grid, 64 * kNmBwdWaves, dyn, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,          \
                                                      static_cast<uint32_t>(N), static_cast<uint32_t>(B),           \
                                                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
                                                      scale_out);                                                   \
@@ -1512,7 +1512,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
             grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
                                          2),                                                                       \
                                  2 * lg_num_cus());                                                                \
-            kern<<<grid, 64 * kNmBwdWaves3, dyn3, s>>>(nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,        \
+            lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,        \
                                                        static_cast<uint32_t>(N), static_cast<uint32_t>(B),         \
                                                        static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,     \
                                                        scale_out);                                                 \

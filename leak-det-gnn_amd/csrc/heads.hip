@@ -2,6 +2,10 @@
 // All HBM-bound row kernels: D/4 lanes per row, one float4 per lane, rows read
 // and written as whole 4*D-byte lines.
 #include <algorithm>
+#include <deque>
+#include <mutex>
+#include <vector>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -157,11 +161,11 @@ extern "C" int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, c
     hipStream_t s = lg_stream(stream);
     switch (D) {
         case 64:
-            k_node_init<64><<<row_grid(R, 64), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+            lg_launch(k_node_init<64>, row_grid(R, 64), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
                                                             dropout_p, scale, seed, salt);
             break;
         case 32:
-            k_node_init<32><<<row_grid(R, 32), 256, 0, s>>>(sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+            lg_launch(k_node_init<32>, row_grid(R, 32), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
                                                             dropout_p, scale, seed, salt);
             break;
         default:
@@ -181,8 +185,8 @@ extern "C" int lg_pipe_gather_fwd(const int64_t* ends, const float* h, float* fe
     const lg_fastdiv fdP = lg_make_fastdiv(static_cast<uint32_t>(P));
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64: k_pipe_gather<64><<<row_grid(BP, 64), 256, 0, s>>>(ends, h, feat, N, fdP, BP); break;
-        case 32: k_pipe_gather<32><<<row_grid(BP, 32), 256, 0, s>>>(ends, h, feat, N, fdP, BP); break;
+        case 64: lg_launch(k_pipe_gather<64>, row_grid(BP, 64), 256, 0, s, ends, h, feat, N, fdP, BP); break;
+        case 32: lg_launch(k_pipe_gather<32>, row_grid(BP, 32), 256, 0, s, ends, h, feat, N, fdP, BP); break;
         default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();
@@ -202,10 +206,10 @@ extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc
     hipStream_t s = lg_stream(stream);
     switch (D) {
         case 64:
-            k_pipe_scatter<64><<<row_grid(R, 64), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
+            lg_launch(k_pipe_scatter<64>, row_grid(R, 64), 256, 0, s, inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
             break;
         case 32:
-            k_pipe_scatter<32><<<row_grid(R, 32), 256, 0, s>>>(inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
+            lg_launch(k_pipe_scatter<32>, row_grid(R, 32), 256, 0, s, inc_rowptr, inc_item, dpipe, dpool, dh, N, fdM, nm, P, R);
             break;
         default: return LG_EUNSUPPORTED;
     }
@@ -229,7 +233,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     if (K == 0) {
         if (hipMemsetAsync(slab, 0, SL * sizeof(float), s) != hipSuccess) return LG_EHIP;
     } else {
-#define LG_LDW(MM, NN) k_linear_dw<MM, NN><<<G, 64 * (MM / 16), 0, s>>>(dy, x, K, slab)
+#define LG_LDW(MM, NN) lg_launch(k_linear_dw<MM, NN>, G, 64 * (MM / 16), 0, s, dy, x, K, slab)
         if (M == 64) {
             if (N == 64) LG_LDW(64, 64); else LG_LDW(64, 32);
         } else {
@@ -242,7 +246,61 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 8; }
+extern "C" int lg_abi_version(void) { return 9; }
+
+// ------------------------------------------------------------------ kernel timing
+// The event pairs are process-wide (a backward op runs on autograd's worker thread, the
+// timer reads the pairs back on the caller's); only the armed slot is per host thread.
+// std::deque: growing it never moves the pairs already handed out.
+namespace {
+std::mutex g_timing_mu;
+std::deque<LgTimingPair> g_timing_pool;
+thread_local int t_timing_armed = -1;
+}  // namespace
+
+LgTimingPair* lg_timing_take() {
+    if (t_timing_armed < 0) return nullptr;
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    LgTimingPair* t = &g_timing_pool[t_timing_armed];
+    t_timing_armed = -1;
+    return t;
+}
+
+extern "C" int lg_timing_arm(int slot) {
+    if (slot < 0 || slot > (1 << 20)) return LG_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        while (static_cast<int>(g_timing_pool.size()) <= slot) {
+            LgTimingPair t{};
+            if (hipEventCreate(&t.start) != hipSuccess) return LG_EHIP;
+            if (hipEventCreate(&t.stop) != hipSuccess) {
+                (void)hipEventDestroy(t.start);
+                return LG_EHIP;
+            }
+            g_timing_pool.push_back(t);
+        }
+    }
+    t_timing_armed = slot;
+    return LG_OK;
+}
+
+extern "C" int lg_timing_disarm(void) {
+    const int was = t_timing_armed >= 0 ? 1 : 0;
+    t_timing_armed = -1;
+    return was;
+}
+
+extern "C" int lg_timing_elapsed(int slot, float* ms) {
+    if (!ms || slot < 0) return LG_EINVAL;
+    hipEvent_t a, z;
+    {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        if (slot >= static_cast<int>(g_timing_pool.size())) return LG_EINVAL;
+        a = g_timing_pool[slot].start;
+        z = g_timing_pool[slot].stop;
+    }
+    return hipEventElapsedTime(ms, a, z) == hipSuccess ? LG_OK : LG_EHIP;
+}
 
 extern "C" const char* lg_strerror(int code) {
     switch (code) {

@@ -150,8 +150,8 @@ extern "C" int lg_mean_pool_fwd(const float* x, float* out, int64_t B, int64_t N
     if (!x || !out || B > INT32_MAX) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     switch (D) {
-        case 64: k_mean_pool<64><<<static_cast<unsigned>(B), kPoolThreads, 0, s>>>(x, out, N); break;
-        case 32: k_mean_pool<32><<<static_cast<unsigned>(B), kPoolThreads, 0, s>>>(x, out, N); break;
+        case 64: lg_launch(k_mean_pool<64>, static_cast<unsigned>(B), kPoolThreads, 0, s, x, out, N); break;
+        case 32: lg_launch(k_mean_pool<32>, static_cast<unsigned>(B), kPoolThreads, 0, s, x, out, N); break;
         default: return LG_EUNSUPPORTED;
     }
     LG_RET_IF_LAUNCH_FAILED();
@@ -174,7 +174,7 @@ extern "C" int lg_pool_head_fwd(const float* x, const float* w1, const float* b1
     const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // x is [N][B][D] instead of [B][N][D]
     const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
 #define LG_PH(DD, DR)                                                                                             \
-    k_pool_head_fwd<DD, DR><<<grid, kPoolThreads, 0, s>>>(x, w1, b1, w2, b2, pooled, hid, logits, ldo, col, N,    \
+    lg_launch(k_pool_head_fwd<DD, DR>, grid, kPoolThreads, 0, s, x, w1, b1, w2, b2, pooled, hid, logits, ldo, col, N,    \
                                                            sb, sn, dropout_p, scale, seed, salt)
     if (D == 64) {
         if (drop) LG_PH(64, true); else LG_PH(64, false);
@@ -212,9 +212,9 @@ extern "C" int lg_pool_head_bwd(const float* pooled, const float* hid, const flo
         if (hipMemsetAsync(slab, 0, SL * G * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, G * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else if (D == 64) {
-        k_pool_head_bwd<64><<<G, kHid, 0, s>>>(pooled, hid, w1, w2, dlogits, ldo, col, dpooled, slab, dslab, B, scale);
+        lg_launch(k_pool_head_bwd<64>, G, kHid, 0, s, pooled, hid, w1, w2, dlogits, ldo, col, dpooled, slab, dslab, B, scale);
     } else {
-        k_pool_head_bwd<32><<<G, kHid, 0, s>>>(pooled, hid, w1, w2, dlogits, ldo, col, dpooled, slab, dslab, B, scale);
+        lg_launch(k_pool_head_bwd<32>, G, kHid, 0, s, pooled, hid, w1, w2, dlogits, ldo, col, dpooled, slab, dslab, B, scale);
     }
     LG_RET_IF_LAUNCH_FAILED();
     const LgSlabSeg segs[3] = {{0, kHid * D, dw1}, {kHid * D, kHid, db1}, {kHid * D + kHid, kHid, dw2}};

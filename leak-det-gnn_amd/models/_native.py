@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 8  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 9  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -36,6 +36,9 @@ _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint3
 SIGNATURES = {
     "lg_abi_version": (_i32, []),
     "lg_strerror": (ctypes.c_char_p, [_i32]),
+    "lg_timing_arm": (_i32, [_i32]),
+    "lg_timing_disarm": (_i32, []),
+    "lg_timing_elapsed": (_i32, [_i32, _p]),
     "lg_graph_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _p]),
     "lg_nm_table_build": (_i32, [_p, _p, _i64, _p, _p]),

@@ -16,6 +16,7 @@ and the non-differentiable helpers (batchify, pipe_features, spmm).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import time
 from dataclasses import dataclass
@@ -52,44 +53,54 @@ GCN_FWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_NM_FLAGS", "0"), 0)
 
 # ----------------------------------------------------------------------------- timing hook
 class KernelTimer:
-    """Optional HIP-event bracketing of named kernel launches (used by bench.py).
+    """Optional HIP-event timing of named kernel launches (used by bench.py).
 
-    Events are recorded on the stream the kernel is enqueued on (torch's current
-    stream), so elapsed times are the device-side durations of those launches.
+    Each named library call arms one event pair of the library (lg_timing_arm,
+    include/leakgnn.h): its main kernel is then launched with hipExtLaunchKernelGGL and
+    that pair, so the elapsed time is the kernel's own execution on its stream — what a
+    profiler's kernel trace reports — not the enqueue gaps a pair of event commands
+    around the call would add.
     """
 
     def __init__(self, names: Sequence[str]):
         self.names = set(names)
-        self.events: dict = {n: [] for n in names}
+        self.events: dict = {n: [] for n in names}  # name -> [slot]
         self.enabled = False
+        self._next = 0
 
     def wrap(self, name: str, device: torch.device):
         timer = self
 
         class _Ctx:
             def __enter__(self_inner):
+                self_inner.slot = None
                 if timer.enabled and name in timer.names:
-                    s = torch.cuda.current_stream(device)
-                    self_inner.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    self_inner.ev[0].record(s)
-                else:
-                    self_inner.ev = None
+                    slot = timer._next
+                    timer._next += 1
+                    check(load_library().lg_timing_arm(slot), "lg_timing_arm")
+                    self_inner.slot = slot
                 return self_inner
 
             def __exit__(self_inner, *exc):
-                if self_inner.ev is not None:
-                    self_inner.ev[1].record(torch.cuda.current_stream(device))
-                    timer.events[name].append(self_inner.ev)
+                if self_inner.slot is not None:
+                    if load_library().lg_timing_disarm():
+                        raise RuntimeError(f"KernelTimer: {name} launched no timed kernel")
+                    timer.events[name].append(self_inner.slot)
                 return False
 
         return _Ctx()
 
     def mean_ms(self, name: str) -> Optional[float]:
-        evs = self.events.get(name, [])
-        if not evs:
+        slots = self.events.get(name, [])
+        if not slots:
             return None
         torch.cuda.synchronize()
-        return sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        lib, ms = load_library(), ctypes.c_float()
+        tot = 0.0
+        for s in slots:
+            check(lib.lg_timing_elapsed(s, ctypes.byref(ms)), "lg_timing_elapsed")
+            tot += ms.value
+        return tot / len(slots)
 
     def count(self, name: str) -> int:
         return len(self.events.get(name, []))
@@ -97,6 +108,7 @@ class KernelTimer:
     def reset(self) -> None:
         for n in self.events:
             self.events[n] = []
+        self._next = 0
 
 
 _TIMER: Optional[KernelTimer] = None

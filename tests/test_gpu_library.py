@@ -9,6 +9,7 @@ import pytest
 import torch
 
 from helpers import LTA_INP, assert_close, load, lta_ids
+from models import library  # noqa: F401  (registers the torch.ops.leakgnn ops)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -104,3 +105,33 @@ def test_torch_compile_aot_eager_matches_eager(fullgraph):
     for a, b in zip(g1, g0):
         assert_close(a, b, rtol=1e-6, what="compiled grad")
     assert np.isfinite(l1.item())
+
+
+def test_kernel_timer_times_the_kernel():
+    """bench.py's KernelTimer: every named call arms one library event pair
+    (lg_timing_arm) that its main kernel consumes (hipExtLaunchKernelGGL); the mean is a
+    positive kernel duration, no longer than a pair of stream events around the call."""
+    from models import ops
+    g = _graph(N=20000, E=100000)
+    x = torch.randn(20000, 64, device=DEV)
+    W = torch.randn(64, 64, device=DEV)
+    b = torch.randn(64, device=DEV)
+    args = (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t)
+    torch.ops.leakgnn.gcn_conv(*args)
+    timer = ops.KernelTimer(["gcn_fwd"])
+    ops.set_kernel_timer(timer)
+    timer.enabled = True
+    try:
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(5):
+            torch.ops.leakgnn.gcn_conv(*args)
+        z.record()
+    finally:
+        timer.enabled = False
+        ops.set_kernel_timer(None)
+    ms = timer.mean_ms("gcn_fwd")
+    assert timer.count("gcn_fwd") == 5
+    assert 0.0 < ms <= a.elapsed_time(z) / 5
+    from models import _native
+    assert _native.load_library().lg_timing_disarm() == 0  # nothing left armed
