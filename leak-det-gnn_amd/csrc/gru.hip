@@ -25,7 +25,6 @@
 // workgroup writes its partial sums once to a slab reduced in fixed order
 // (deterministic).
 #include <algorithm>
-#include <cstdlib>
 #include "common.h"
 #include "reduce.h"
 
@@ -39,7 +38,23 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int fk(int ks, int q) { return 16 * (ks >> 2) + 4 * q + (ks & 3); }
-__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate nonlinearities on the hardware transcendentals (v_exp_f32, v_rcp_f32, ~1 ulp each)
+// instead of libm's IEEE expf / division / tanhf sequences: the recurrence's per-step
+// critical path runs through them (MI355X, B = 256: GRU training forward 139 -> 116 us).
+// sigma: ~3 ulp.  tanh: e^{-2|x|} form for |x| >= 1/16 (the 1 - t cancellation costs at
+// most a factor 8 there, ~5e-7 relative), odd Taylor polynomial below it (truncation
+// < 1e-9 relative).
+__device__ __forceinline__ float sigm(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float gru_tanh(float x) {
+    const float ax = fabsf(x);
+    const float t = __builtin_amdgcn_exp2f(-2.88539008177792682f * ax);  // e^{-2|x|}
+    const float big = (1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t);
+    const float x2 = x * x;
+    const float small = ax * fmaf(x2, fmaf(x2, 0.133333333333f, -0.333333333333f), 1.0f);
+    return copysignf(ax < 0.0625f ? small : big, x);
+}
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 // xs[tt][seq][0..15] (row stride XR) = [x_0 .. x_{I-1}, 0.., 1 (col 10), 0..] for steps
@@ -90,6 +105,9 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __r
 // v_mfma_f32_16x16x32_bf16 (K permuted so each lane's two lane-major h tiles form its B
 // fragment, no extra exchange) ran 158 -> 165 us and doubled the W_ih gradient error —
 // the step is bound by its barriers / transcendentals / LDS round trip, not MFMA issue.
+// Also dropped: one wave per unit group owning all three gates (one barrier per step, no
+// sigma exchange) — 148 vs 142 us with libm math, 114 vs 116 us with the fast gate math;
+// PMC (profiles/pmc/r02m_pmc_summary.txt): 51% of its wave time in dependency stalls.
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
 template <int H, bool UT, bool SAVE>
 __global__ void __launch_bounds__(12 * H) __attribute__((amdgpu_waves_per_eu(6, 8)))  // 2 workgroups / CU
@@ -156,7 +174,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                 f32x4 n, hn;
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {
-                    n[reg] = tanhf(a0[reg] + r[reg] * hp[reg]);
+                    n[reg] = gru_tanh(a0[reg] + r[reg] * hp[reg]);
                     hn[reg] = (1.f - z[reg]) * n[reg] + z[reg] * hprev[reg];
                 }
                 hb[u][lane] = hn;
@@ -182,114 +200,6 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
         }
     }
     if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hb[u][lane]);
-}
-
-// Forward, one wave per unit group (the default): wave u of H/16 owns units [16u, 16u+16)
-// of ALL three gates for the workgroup's 16 sequences, so r, z, n and h' are formed in the
-// wave that computes them (no sigma exchange) and the only exchange is h' itself: one
-// lane-major LDS tile per wave, double-buffered, ONE barrier per step.  Per step a wave
-// issues 3 (3 + H/4) MFMAs in 7 independent accumulator chains, enough to keep its SIMD's
-// matrix pipe streaming on its own; H/16-wave workgroups leave room for ~2 of them per
-// SIMD, whose VALU / barrier phases interleave with each other's MFMA phases.  (The
-// 12-wave layout above spends two barriers per step and leaves the r / z waves idle
-// while the n waves form tanh and h'.)  Same stores and layouts as k_gru_fwd.
-template <int H, bool UT, bool SAVE>
-__global__ void __launch_bounds__(4 * H)
-k_gru_fwd_u(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Wih,
-            const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
-            float* __restrict__ hs, float* __restrict__ gates, float* __restrict__ hout, uint32_t Nseq, int L, int S,
-            lg_fastdiv fdS) {
-    constexpr int NU = H / 16, KH = H / 4, I = UT ? 10 : 1;
-    __shared__ __attribute__((aligned(16))) float xs[kLC * TS * XR];
-    __shared__ __attribute__((aligned(16))) f32x4 hb[2][NU][64];  // h_t tiles, lane-major, by step parity
-    const int u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const uint32_t seq0 = blockIdx.x * TS, seq = seq0 + j;
-    const bool valid = seq < Nseq;
-
-    float ah[3][KH], ax[3][3];
-    f32x4 bx[3], bhn;  // x-side biases (r, z: both biases folded), h-side bias of n
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-        const int row = g * H + 16 * u + j;  // A-operand row of this lane
-#pragma unroll
-        for (int ks = 0; ks < KH; ++ks) ah[g][ks] = Whh[row * H + fk(ks, q)];
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const int k = 4 * kx + q;
-            ax[g][kx] = k < I ? Wih[row * I + k] : 0.f;
-        }
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-            const int c = g * H + 16 * u + 4 * q + reg;
-            bx[g][reg] = g < 2 ? bih[c] + bhh[c] : bih[c];
-            if (g == 2) bhn[reg] = bhh[c];
-        }
-    }
-    float hf[KH];  // B operand: h_{t-1}[unit fk(ks, q)][seq j]; hf[4u + reg] is this lane's own units
-#pragma unroll
-    for (int i = 0; i < KH; ++i) hf[i] = 0.f;
-    f32x4 hn = zero4();
-
-    for (int t0 = 0; t0 < L; t0 += kLC) {
-        const int nt = min(kLC, L - t0);
-        __syncthreads();
-        stage_x<UT>(xs, resid, tfeat, t0, nt, seq0, Nseq, L, S, fdS);
-        __syncthreads();
-        for (int tt = 0; tt < nt; ++tt) {
-            const int t = t0 + tt;
-            float xv[3];
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) xv[kx] = xs[(tt * TS + j) * XR + 4 * kx + q];
-            f32x4 r0 = bx[0], z0 = bx[1], nx = bx[2], r1 = zero4(), z1 = zero4(), n0 = bhn, n1 = zero4();
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-                r0 = mfma(ax[0][kx], xv[kx], r0);
-                z0 = mfma(ax[1][kx], xv[kx], z0);
-                nx = mfma(ax[2][kx], xv[kx], nx);
-            }
-#pragma unroll
-            for (int ks = 0; ks < KH; ks += 2) {
-                r1 = mfma(ah[0][ks], hf[ks], r1);
-                z1 = mfma(ah[1][ks], hf[ks], z1);
-                n0 = mfma(ah[2][ks], hf[ks], n0);
-                r0 = mfma(ah[0][ks + 1], hf[ks + 1], r0);
-                z0 = mfma(ah[1][ks + 1], hf[ks + 1], z0);
-                n1 = mfma(ah[2][ks + 1], hf[ks + 1], n1);
-            }
-            const f32x4 hp = n0 + n1;  // W_hn h + b_hn
-            f32x4 r, z, n;
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                r[reg] = sigm(r0[reg] + r1[reg]);
-                z[reg] = sigm(z0[reg] + z1[reg]);
-                n[reg] = tanhf(nx[reg] + r[reg] * hp[reg]);
-                hn[reg] = (1.f - z[reg]) * n[reg] + z[reg] * hf[4 * u + reg];
-            }
-            hb[t & 1][u][lane] = hn;
-            if (valid) {
-                const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
-                if (hs) st4(hs + rw * H + 16 * u + 4 * q, hn);
-                if constexpr (SAVE) {
-                    float* gp = gates + rw * 4 * H + 16 * u + 4 * q;
-                    st4(gp, r);
-                    st4(gp + H, z);
-                    st4(gp + 2 * H, n);
-                    st4(gp + 3 * H, hp);
-                }
-            }
-            // h_t posted.  The other parity's tiles were read before this barrier by every
-            // wave, so step t + 1 may overwrite them.
-            __syncthreads();
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                const f32x4 v = hb[t & 1][a][lane];
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
-            }
-        }
-    }
-    if (valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hn);
 }
 
 // ------------------------------------------------------------------ backward
@@ -498,19 +408,9 @@ int launch_fwd(bool ut, bool save, const float* residual, const float* tfeat, co
     const uint32_t Nseq = static_cast<uint32_t>(B * S);
     const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
     const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
-    bool v12 = true;  // the 12-wave kernel; kernel lab: LG_GRU_FWD_UNIT=1 -> k_gru_fwd_u
-#ifdef LG_KERNEL_LAB
-    v12 = getenv("LG_GRU_FWD_UNIT") == nullptr;
-#endif
-#define LG_GRU_FWD(UT, SV)                                                                                         \
-    do {                                                                                                           \
-        if (v12)                                                                                                   \
-            lg_launch(k_gru_fwd<H, UT, SV>, grid, 12 * H, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, \
-                      h_last, Nseq, static_cast<int>(L), static_cast<int>(S), fdS);                                \
-        else                                                                                                       \
-            lg_launch(k_gru_fwd_u<H, UT, SV>, grid, 4 * H, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq,     \
-                      gates, h_last, Nseq, static_cast<int>(L), static_cast<int>(S), fdS);                         \
-    } while (0)
+#define LG_GRU_FWD(UT, SV)                                                                                        \
+    lg_launch(k_gru_fwd<H, UT, SV>, grid, 12 * H, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, h_last, \
+              Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
     if (ut) {
         if (save) LG_GRU_FWD(true, true); else LG_GRU_FWD(true, false);
     } else {

@@ -281,11 +281,14 @@ def _gru_setup(ctx, inputs, output):
     residual, tfeat, w_ih, w_hh, _, _, _ = inputs
     _, h_seq, gates = output
     ctx.mark_non_differentiable(h_seq, gates)
+    ctx.set_materialize_grads(False)  # no zero-filled (L, B*S, 4H) gradients for the saved tensors
     ctx.has_tfeat = tfeat is not None
     ctx.save_for_backward(residual, tfeat, w_ih, w_hh, h_seq, gates)
 
 
 def _gru_bwd(ctx, dh, _dhseq, _dgates):
+    if dh is None:
+        return (None,) * 7
     residual, tfeat, w_ih, w_hh, h_seq, gates = ctx.saved_tensors
     B, L, S = residual.shape
     I = w_ih.shape[1]
@@ -420,6 +423,7 @@ def _trunk_setup(ctx, inputs, output):
      pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
     ctx.L = len(weights)
     ctx.mark_non_differentiable(*output[:-1])  # x_0 .. x_{L-1}: returned for the backward's masks
+    ctx.set_materialize_grads(False)  # their gradients would be zero-filled (B, N, D) tensors
     ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
     ctx.save_for_backward(*output, *weights, sensor_slot, sensor_idx, nonsensor_idx,
                           slot_live if slot_live is not None else sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t)
@@ -430,7 +434,9 @@ def _trunk_bwd(ctx, grads):
     saved = ctx.saved_tensors
     xs, weights = list(saved[:L + 1]), list(saved[L + 1:2 * L + 1])
     sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 1:]
-    g = grads[-1] if grads[-1] is not None else torch.zeros_like(xs[-1])
+    g = grads[-1]
+    if g is None:
+        return (None,) * 21
     dproj, dbias, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
         g, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None, nodetab_t, pairs_t,
         rowptr_t, col_t, w_t, ctx.p, ctx.node_major)
@@ -541,11 +547,14 @@ def _heads_setup(ctx, inputs, output):
     (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, _, _) = inputs
     _, ehid, pooled, hid = output
     ctx.mark_non_differentiable(ehid, pooled, hid)
+    ctx.set_materialize_grads(False)  # else autograd zero-fills a (B*P, 128) gradient for ehid
     ctx.cfg = (p_edge, p_noleak, node_major)
     ctx.save_for_backward(h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item)
 
 
 def _heads_bwd(ctx, dlogits, _dehid, _dpooled, _dhid):
+    if dlogits is None:
+        return (None,) * 17
     h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item = ctx.saved_tensors
     p_edge, p_noleak, node_major = ctx.cfg
     g = torch.ops.leakgnn.detector_heads_backward(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr,

@@ -77,10 +77,13 @@ def derive(c: dict) -> dict:
             if k in c:
                 d[f"{k}/wave"] = round(c[k] / c["SQ_WAVES"], 1)
     if g("GRBM_GUI_ACTIVE"):
+        # GRBM_GUI_ACTIVE comes back summed over the 8 XCDs' instances: per-XCD busy cycles
+        # = the dispatch's duration in GPU cycles
+        gui = c["GRBM_GUI_ACTIVE"] / 8.0
         simds = 1024  # 256 CUs x 4 SIMDs
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
-            d["MFMA_busy_of_SIMD_cycles"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] * simds), 4)
-        d["GRBM_GUI_ACTIVE_us_at_2.4GHz"] = round(c["GRBM_GUI_ACTIVE"] / 2400.0, 2)
+            d["MFMA_busy_of_SIMD_cycles"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * simds), 4)
+        d["duration_us_at_2.4GHz(GRBM_GUI_ACTIVE/8)"] = round(gui / 2400.0, 2)
     if "SQ_LDS_BANK_CONFLICT" in c and g("SQ_LDS_IDX_ACTIVE"):
         d["LDS_bank_conflict/LDS_active"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"], 4)
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
