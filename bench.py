@@ -323,6 +323,60 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
                                  "avg_launch_us": round(fwd_ms * 1e3, 2)}}
 
 
+def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str, batch: int) -> dict:
+    """BASELINE configs[2] as written — "bf16 node-MLP on MFMA" (SURVEY §8 d C3: bf16 for the
+    K5 GCN transforms and the K9 EdgeHead MLP, fp32 accumulate): the same L-TOWN-A training
+    step with LeakDetector(mlp_dtype=...), captured, timed like the main line; plus the
+    in-step durations of the kernels whose products change."""
+    from models import ops
+    from models.detector import LeakDetector
+    from models.graph_step import CapturedTrainStep
+    pipes = all_pipe_ids(LTA_INP)
+    P, B = len(pipes), batch
+    torch.manual_seed(0)
+    m = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
+                     use_time=True, mlp_dtype=mlp_dtype).to(dev).train()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    gen = torch.Generator().manual_seed(1234 + rank)
+    r = torch.randn(B, 36, len(SENSORS), generator=gen).to(dev)
+    tf = time_features(B, 36, gen).to(dev)
+    lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
+    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=1.0, warmup=3)
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    names = ["gcn_fwd", "gcn_bwd", "gcn_bwd_l0", "edge_fwd", "edge_bwd"]
+    timer = ops.KernelTimer(names)
+    ops.set_kernel_timer(timer)
+    timer.enabled = True
+    for _ in range(5):
+        opt.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(m(r, tf), lab).backward()
+    timer.enabled = False
+    ops.set_kernel_timer(None)
+    kms = {k: timer.mean_ms(k) for k in names}
+    return {"metric": "windowed graphs/sec fwd+bwd on L-TOWN-A (BASELINE configs[2]: bf16 node-MLP on MFMA)"
+            if mlp_dtype == "bf16" else "windowed graphs/sec fwd+bwd on L-TOWN-A (fp32 node-MLP)",
+            "value": round(B * world * steps / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / steps, 4),
+            "mlp_dtype": mlp_dtype, "windows_per_rank": B, "scaling": "weak",
+            "parity": "logits within 2e-2 of the fp32 oracle (tests/test_gpu_configs.py::test_bf16_tier_b256)"
+            if mlp_dtype == "bf16" else "fp32 bars",
+            "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()}}
+
+
 def _event_ms(fn, iters: int) -> float:
     fn()
     torch.cuda.synchronize()
@@ -416,6 +470,9 @@ def main() -> None:
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--eager", action="store_true", help="launch the step eagerly instead of replaying its HIP graph")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launch-path check (no GPU, no measurement)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="node-MLP tier of the main line: fp32 (split-bf16 MFMA, fp32 parity) or bf16 (configs[2])")
+    ap.add_argument("--no-tier-leg", action="store_true", help="skip the leg of the other node-MLP tier")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
@@ -445,7 +502,7 @@ def main() -> None:
 
     torch.manual_seed(0)
     model = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
-                         use_time=True).to(dev).train()
+                         use_time=True, mlp_dtype=args.dtype).to(dev).train()
     # fused=True: one multi-tensor launch for the whole update (same AdamW math as the reference's);
     # capturable=True: device-side step counters, so the update can live inside the step graph
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
@@ -508,6 +565,8 @@ def main() -> None:
     kms = {k: timer.mean_ms(k) for k in timer.names}
     # BASELINE configs[3] (C4) at every world size: 64 windows per rank, weak scaling
     c4 = None if args.no_c4 else c4_leg(dev, max(10, args.steps // 2), 3, rank, world)
+    other = "bf16" if args.dtype == "fp32" else "fp32"
+    tier = None if args.no_tier_leg else tier_leg(dev, args.steps, 3, rank, world, other, B)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -536,7 +595,7 @@ def main() -> None:
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
         "n_gpus": world, "ranks_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic residual windows (B,36,29) + time features, random-init weights",
         "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",
                    "nodes": N, "edge_columns": E1 - N, "pipes": P, "windows_per_rank": B,
@@ -568,6 +627,8 @@ def main() -> None:
     }
     if c4 is not None:
         out["c4"] = c4
+    if tier is not None:
+        out["mlp_tier"] = tier
     if world == 1:
         out["e2e_training"] = e2e_training(model, opt, label, B, max(5, args.steps // 2), dev)
     if world == 1 and not args.no_cpu_baseline:

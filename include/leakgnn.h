@@ -59,6 +59,13 @@ enum {
  * node-major [N][B][D] (row n*B + b), the layout of lg_gcn_fwd_nm / lg_gcn_bwd_nm.
  * Dropout masks are indexed by the window-major row in both layouts. */
 #define LG_F_NODE_MAJOR 0x20
+/* The bf16 node-MLP tier (BASELINE configs[2], SURVEY §8 d C3: "bf16 for K2/K5/K9 GEMMs
+ * with fp32 accumulate"): lg_gcn_fwd_nm / lg_gcn_bwd_nm / lg_edge_head_fwd /
+ * lg_edge_head_bwd run their products as ONE bf16 MFMA (operands rounded to bf16, fp32
+ * accumulate, fp32 in HBM) instead of the 3-way split that holds fp32 accuracy.  Not an
+ * fp32-parity mode: its bar is 2e-2 relative on logits against the fp32 oracle (SURVEY
+ * §7).  Ignored by the kernels that have no bf16 form (they compute fp32). */
+#define LG_F_BF16 0x40
 /* Dropout seeds: every forward entry point taking (seed, salt) reads `seed` as the address
  * of a device-resident uint64 when salt has bit 31 set (the salt proper is bits 0..30).  A
  * captured HIP graph of a training step then re-draws its dropout streams on each replay by

@@ -56,8 +56,9 @@ struct EG {
     static constexpr int FPL = TR * FSB, FTPL = TR * FTB, GPL = TR * GSB;  // image plane strides
     static constexpr int NROLE = DT * RG * RBW;  // dfeat output blocks (16 features x 16 rows) = NW
     static constexpr int NRED = 2 * NROLE * 3;   // dfeat partials of both hidden halves (f32x4 x 64 lanes)
-    // forward workgroups resident per CU (VGPR-bound: 144 VGPRs of split W1 at D=64)
-    static constexpr int FWD_WG_PER_CU = 1;
+    // forward workgroups resident per CU (VGPR-bound: 144 VGPRs of split W1 at D=64; the
+    // bf16 tier keeps only the hi part, 48 VGPRs, and fits two)
+    static constexpr int FWD_WG_PER_CU = 1, FWD_WG_PER_CU_BF = 2;
     static constexpr int64_t FWD_LDS = int64_t{2} * 2 * 3 * FPL + 4 * (2 * 4 * TR + 2 * HID);  // images, partials, b1/W2
     static constexpr int64_t BWD_LDS = int64_t{2} * (3 * FTPL + 3 * GPL) + 2 * TR * D + 16 * 64 * NRED;
 };
@@ -95,16 +96,20 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ h, int64_t r
     }
 }
 // three bf16 parts of 4 floats -> 8-byte slots at img[off], img[pl + off], img[2 pl + off]
+// (BF: the hi part only; the other planes are never read)
+template <bool BF = false>
 __device__ __forceinline__ void st_split4(uint16_t* img, int pl, int off, const f32x4& x) {
     lg_u32x2 a, b, c;
     split3_x4(x, a, b, c);
     *reinterpret_cast<lg_u32x2*>(img + off) = a;
+    if (BF) return;
     *reinterpret_cast<lg_u32x2*>(img + pl + off) = b;
     *reinterpret_cast<lg_u32x2*>(img + 2 * pl + off) = c;
 }
 
-template <int D>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EG<D>::FWD_WG_PER_CU * 2, 4)))
+template <int D, bool BF>
+__global__ void __launch_bounds__(NT)
+__attribute__((amdgpu_waves_per_eu((BF ? EG<D>::FWD_WG_PER_CU_BF : EG<D>::FWD_WG_PER_CU) * 2, 4)))
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
            float* __restrict__ logit, int64_t ldo, float* __restrict__ hid_out, uint32_t sb, uint32_t sn,
@@ -154,13 +159,13 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     auto rowof = [&](int64_t t) { return t * G::TR + arow; };
     auto stage = [&](uint16_t* img, int part3, const f32x4& pu, const f32x4& pv) {  // a third of the slot
         if (lab & 4) return;
-        if (part3 == 0) st_split4(img, G::FPL, arow * G::FSB + 4 * af, pu);
-        if (part3 == 1) st_split4(img, G::FPL, arow * G::FSB + D + 4 * af, pv);
+        if (part3 == 0) st_split4<BF>(img, G::FPL, arow * G::FSB + 4 * af, pu);
+        if (part3 == 1) st_split4<BF>(img, G::FPL, arow * G::FSB + D + 4 * af, pv);
         if (part3 == 2) {
             f32x4 a;
 #pragma unroll
             for (int i = 0; i < 4; ++i) a[i] = fabsf(pu[i] - pv[i]);
-            st_split4(img, G::FPL, arow * G::FSB + 2 * D + 4 * af, a);
+            st_split4<BF>(img, G::FPL, arow * G::FSB + 2 * D + 4 * af, a);
         }
     };
     const int64_t t0 = blockIdx.x;
@@ -196,8 +201,8 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                     acc[rb][0][0] += bf[0][0];
                     continue;
                 }
-                acc[rb][0] = mfma_split(wa[0][ks], bf, acc[rb][0]);
-                acc[rb][1] = mfma_split(wa[1][ks], bf, acc[rb][1]);
+                acc[rb][0] = mfma_prec<BF>(wa[0][ks], bf, acc[rb][0]);
+                acc[rb][1] = mfma_prec<BF>(wa[1][ks], bf, acc[rb][1]);
             }
             // the next tile's split, spread over the MFMA stream
             if (ks * 3 / G::KS != (ks + 1) * 3 / G::KS) stage(nxt, ks * 3 / G::KS, pu, pv);
@@ -251,7 +256,7 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 }
 
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
-template <int D>
+template <int D, bool BF>
 __global__ void __launch_bounds__(NT)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ W2, const float* __restrict__ hid, const float* __restrict__ dlogit, int64_t ldo,
@@ -329,9 +334,9 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 a[i] = fabsf(d);
                 sw |= static_cast<uint32_t>(static_cast<uint8_t>(d > 0.f ? 1 : (d < 0.f ? -1 : 0))) << (8 * i);
             }
-            st_split4(fimg, G::FTPL, arow * G::FTB + 4 * af, pu);
-            st_split4(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv);
-            st_split4(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a);
+            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 4 * af, pu);
+            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv);
+            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a);
             *reinterpret_cast<uint32_t*>(sgnb + arow * D + 4 * af) = sw;
         }
 #pragma unroll
@@ -344,7 +349,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 db1a[j] += static_cast<double>(g[j]);
             }
             if (n4 == 0) db2 += static_cast<double>(dl[i]);
-            st_split4(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
+            st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
         }
         __syncthreads();
         load_rows<D>(h, (tile + step) * G::TR + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
@@ -370,7 +375,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                     const uint16_t* src = fimg + pp * G::FTPL + r0 * G::FTB + 16 * t + 4 * tp;
                     fb[pp] = lds_frag_tr16(src, src + 16 * G::FTB);
                 }
-                dwa[t] = mfma_split(ga, fb, dwa[t]);
+                dwa[t] = mfma_prec<BF>(ga, fb, dwa[t]);
             }
         }
         // dfeat^T[k][row] = sum_n W1[n][k] g[row][n] over this wave's hidden half; partial
@@ -384,7 +389,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 const uint16_t* src = gimg + (rowb + c) * G::GSB + 64 * hh + 32 * ks + 8 * q;
                 const lg_bf16x8 gb[3] = {lds_frag_row(src), lds_frag_row(src + G::GPL), lds_frag_row(src + 2 * G::GPL)};
 #pragma unroll
-                for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_split(wt[s3][ks], gb, cacc[s3]);
+                for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_prec<BF>(wt[s3][ks], gb, cacc[s3]);
             }
             const int role = (rg * G::DT + kt) * G::RBW + rbw;
 #pragma unroll
@@ -491,7 +496,9 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
     const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
     const int64_t ntiles = cdiv(BP, tile_rows(D));
     // persistent grid sized to residency (tiles are dealt statically)
-    const int64_t per_cu = D == 64 ? EG<64>::FWD_WG_PER_CU : EG<32>::FWD_WG_PER_CU;
+    const bool bf = (flags & LG_F_BF16) != 0;
+    const int64_t per_cu = bf ? (D == 64 ? EG<64>::FWD_WG_PER_CU_BF : EG<32>::FWD_WG_PER_CU_BF)
+                              : (D == 64 ? EG<64>::FWD_WG_PER_CU : EG<32>::FWD_WG_PER_CU);
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ntiles, per_cu * lg_num_cus()));
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
@@ -500,15 +507,18 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 #else
     const int dropout_arg = dropout;
 #endif
+#define LG_EDGE_FWD(DD, BFB)                                                                                      \
+    do {                                                                                                          \
+        if (!allow_lds(k_edge_fwd<DD, BFB>, EG<DD>::FWD_LDS)) return LG_EHIP;                                     \
+        lg_launch(k_edge_fwd<DD, BFB>, grid, NT, EG<DD>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb,   \
+                  sn, fdP, BP, ntiles, dropout_arg, dropout_p, scale, seed, salt);                                \
+    } while (0)
     if (D == 64) {
-        if (!allow_lds(k_edge_fwd<64>, EG<64>::FWD_LDS)) return LG_EHIP;
-        lg_launch(k_edge_fwd<64>, grid, NT, EG<64>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
-                                                         ntiles, dropout_arg, dropout_p, scale, seed, salt);
+        if (bf) LG_EDGE_FWD(64, true); else LG_EDGE_FWD(64, false);
     } else {
-        if (!allow_lds(k_edge_fwd<32>, EG<32>::FWD_LDS)) return LG_EHIP;
-        lg_launch(k_edge_fwd<32>, grid, NT, EG<32>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb, sn, fdP, BP,
-                                                         ntiles, dropout_arg, dropout_p, scale, seed, salt);
+        if (bf) LG_EDGE_FWD(32, true); else LG_EDGE_FWD(32, false);
     }
+#undef LG_EDGE_FWD
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
@@ -545,16 +555,20 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     if (BP == 0) {
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
-    } else if (D == 64) {
-        constexpr int64_t lds = EG<64>::BWD_LDS;
-        if (!allow_lds(k_edge_bwd<64>, lds)) return LG_EHIP;
-        lg_launch(k_edge_bwd<64>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
-                                             ntiles, scale);
     } else {
-        constexpr int64_t lds = EG<32>::BWD_LDS;
-        if (!allow_lds(k_edge_bwd<32>, lds)) return LG_EHIP;
-        lg_launch(k_edge_bwd<32>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, dslab, sb, sn, fdP, BP,
-                                             ntiles, scale);
+        const bool bf = (flags & LG_F_BF16) != 0;
+#define LG_EDGE_BWD(DD, BFB)                                                                                      \
+    do {                                                                                                          \
+        if (!allow_lds(k_edge_bwd<DD, BFB>, EG<DD>::BWD_LDS)) return LG_EHIP;                                     \
+        lg_launch(k_edge_bwd<DD, BFB>, grid, NT, EG<DD>::BWD_LDS, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, \
+                  dslab, sb, sn, fdP, BP, ntiles, scale);                                                         \
+    } while (0)
+        if (D == 64) {
+            if (bf) LG_EDGE_BWD(64, true); else LG_EDGE_BWD(64, false);
+        } else {
+            if (bf) LG_EDGE_BWD(32, true); else LG_EDGE_BWD(32, false);
+        }
+#undef LG_EDGE_BWD
     }
     LG_RET_IF_LAUNCH_FAILED();
     const int64_t K3 = 3 * D;

@@ -567,7 +567,8 @@ constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
 // 2 = skip the neighbour loads, 4 = skip the y stores (kept behind a runtime-false test so
 // the transform is not dead code).  DST: epilogue stores straight from the MFMA layout
 // (16 rows x 64 B per store) instead of through the LDS tile.
-template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false>
+// BF (LG_F_BF16, the bf16 node-MLP tier): the transform's single hi x hi product.
+template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false, bool BF = false>
 __global__ void __launch_bounds__(64 * WAVES)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
@@ -768,6 +769,10 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 for (int mt = 0; mt < G::CH; ++mt) {
                     const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
                     const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                    if constexpr (BF) {
+                        o[mt] = mfma_bf(a0, b0f, o[mt]);
+                        continue;
+                    }
                     const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
                     const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
                     o[mt] = mfma_bf(a2, b0f, o[mt]);
@@ -1028,7 +1033,7 @@ struct Nb3Lds {
     static constexpr size_t BYTES = 4 * static_cast<size_t>(WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L);
 };
 
-template <int D, bool MASK_IN, bool NB>
+template <int D, bool MASK_IN, bool NB, bool BF = false>  // BF: LG_F_BF16, single-product MFMAs
 __global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
 k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
               const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
@@ -1251,6 +1256,10 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
                 for (int ni = 0; ni < G::CH; ++ni) {
                     f32x4 c = dw[mo][ni];
+                    if constexpr (BF) {
+                        dw[mo][ni] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][0], c, 0, 0, 0);
+                        continue;
+                    }
                     c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, xb[ni][0], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, xb[ni][1], c, 0, 0, 0);
                     c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][2], c, 0, 0, 0);
@@ -1273,6 +1282,10 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int mt = 0; mt < G::CH; ++mt) {
                 const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
                 const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                if constexpr (BF) {
+                    o[mt] = mfma_bf(a0, b0f, o[mt]);
+                    continue;
+                }
                 const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
                 const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
                 o[mt] = mfma_bf(a2, b0f, o[mt]);
@@ -1380,6 +1393,7 @@ auto nm2_kernel(int flags) {
 }
 template <int D, bool DR, bool RL, int WV>
 auto nm3_kernel(int flags) {
+    if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, true>;
     const bool split = (flags & LG_F_F32_MFMA) == 0;
 #ifdef LG_KERNEL_LAB
     const bool dst = (flags & LG_F_LAB_DST) != 0;
@@ -1494,6 +1508,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
+    const bool bf = (flags & LG_F_BF16) != 0;
     int grid = 1;
     // B == 0 still runs one (empty) launch so the slab holds zeros
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
@@ -1507,7 +1522,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
                                                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
                                                      scale_out);                                                   \
         } else {                                                                                                   \
-            auto kern = k_gcn_bwd_nm3<DD, MI, NBB>;                                                                \
+            auto kern = bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>;                 \
             const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                             \
             grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
                                          2),                                                                       \

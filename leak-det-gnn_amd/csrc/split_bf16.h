@@ -59,12 +59,26 @@ __device__ __forceinline__ f32x4 mfma_bf(const lg_bf16x8& a, const lg_bf16x8& b,
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 // acc += a * b on split operands: the six terms with i + j <= 2, smallest first
+// BF (the bf16 node-MLP tier, LG_F_BF16): the single hi x hi product — operands rounded to
+// bf16, fp32 accumulate.  Unused split parts and their LDS reads are dead code then.
+template <bool BF>
+__device__ __forceinline__ f32x4 mfma_prec(const lg_bf16x8 (&a)[3], const lg_bf16x8 (&b)[3], f32x4 c);
+
 __device__ __forceinline__ f32x4 mfma_split(const lg_bf16x8 (&a)[3], const lg_bf16x8 (&b)[3], f32x4 c) {
     c = mfma_bf(a[2], b[0], c);
     c = mfma_bf(a[1], b[1], c);
     c = mfma_bf(a[0], b[2], c);
     c = mfma_bf(a[1], b[0], c);
     c = mfma_bf(a[0], b[1], c);
+    return mfma_bf(a[0], b[0], c);
+}
+
+template <>
+__device__ __forceinline__ f32x4 mfma_prec<false>(const lg_bf16x8 (&a)[3], const lg_bf16x8 (&b)[3], f32x4 c) {
+    return mfma_split(a, b, c);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma_prec<true>(const lg_bf16x8 (&a)[3], const lg_bf16x8 (&b)[3], f32x4 c) {
     return mfma_bf(a[0], b[0], c);
 }
 

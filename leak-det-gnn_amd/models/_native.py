@@ -27,6 +27,7 @@ LG_SALT_SEED_PTR = 0x80000000  # salt bit 31: `seed` is the address of a device-
 LG_F_LAB_V1 = 0x00800000  # kernel-lab schedule bit of lg_gcn_fwd_nm (tools/kbench.py)
 LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 3-way split bf16 MFMA)
 LG_F_LAB_NM2 = 0x00200000  # lg_gcn_fwd_nm schedule: round-1 rowptr-walking pipeline (kernel lab)
+LG_F_BF16 = 0x40  # lg_gcn_fwd_nm / lg_gcn_bwd_nm / lg_edge_head_*: the bf16 node-MLP tier
 LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel lab)
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,

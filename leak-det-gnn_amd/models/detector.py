@@ -98,8 +98,15 @@ class LeakDetector(nn.Module):
 
     def __init__(self, inp_path: str | Path, sensor_node_ids: Sequence[str], pipe_ids_in_order: Sequence[str],
                  sensor_hidden: int = 64, node_hidden: int = 64, gnn_layers: int = 2, dropout: float = 0.1,
-                 use_time: bool = True, include_links: Sequence[str] = ("PIPES", "PUMPS", "VALVES")) -> None:
+                 use_time: bool = True, include_links: Sequence[str] = ("PIPES", "PUMPS", "VALVES"),
+                 mlp_dtype: str = "fp32") -> None:
         super().__init__()
+        if mlp_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"mlp_dtype must be 'fp32' or 'bf16', got {mlp_dtype!r}")
+        # "bf16": BASELINE configs[2]'s tier — the GCN transforms and the EdgeHead MLP as one
+        # bf16 MFMA product with fp32 accumulate (LG_F_BF16); activations stay fp32.  Not an
+        # fp32-parity mode (2e-2 relative on logits).  Not a state-dict entry.
+        self.mlp_dtype = mlp_dtype
         self.graph: WDNGraph = build_wdn_graph_from_inp(inp_path=inp_path, sensor_node_ids=sensor_node_ids,
                                                         pipe_ids_in_order=pipe_ids_in_order,
                                                         include_links=include_links, add_self_loops=False,
@@ -167,7 +174,7 @@ class LeakDetector(nn.Module):
             proj, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
             nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
             g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
-            library.seed_tensor(residual.device) if drop else _NO_SEED)
+            library.seed_tensor(residual.device) if drop else _NO_SEED, bf16=self.mlp_dtype == "bf16")
         h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
         mlp = self.edge_head.mlp     # Linear(3D,128), ReLU, Dropout, Linear(128,1)
         nmlp = self.noleak_head.mlp  # Linear(D,128), ReLU, Dropout, Linear(128,1)
@@ -178,7 +185,8 @@ class LeakDetector(nn.Module):
         keep = torch.is_grad_enabled() and (h_nodes.requires_grad or any(t.requires_grad for t in hw))
         seed = library.seed_tensor(residual.device) if (pe > 0.0 or pn > 0.0) else _NO_SEED
         # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-218)
-        out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed)
+        out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed,
+                                               bf16=self.mlp_dtype == "bf16")
         if self.capture is not None:
             self.capture.update(xs=xs, node_major=nm, edge_hidden=out[1], noleak_hidden=out[3])
         return out[0]

@@ -311,14 +311,16 @@ gru_encoder.register_autograd(_gru_bwd, setup_context=_gru_setup)
 def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor], sensor_slot: Tensor,
               sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab: Tensor, pairs: Tensor,
               rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor,
-              col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor) -> List[Tensor]:
+              col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor, *,
+              bf16: bool = False) -> List[Tensor]:
     """[x_0, ..., x_L]: node init (detector.py:178-190) then L x dropout(relu(GCNConv)).
 
       x_0     = dropout(relu(slot >= 0 ? proj[b, slot] : node_bias))     (lg_node_init_fwd)
       x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                     (lg_gcn_fwd[_nm], fused)
     node_major: features [N][B][D] (lg_gcn_fwd_nm), else [B][N][D].  p: dropout prob
     (0 = eval).  Every activation is returned: the backward reads its ReLU/dropout masks
-    back as [x > 0] and needs x_l for dW, so no mask is ever stored."""
+    back as [x > 0] and needs x_l for dW, so no mask is ever stored.  bf16: the node-major
+    transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier)."""
     lib = load_library()
     proj, node_bias = _c(proj), _c(node_bias)
     weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]
@@ -338,7 +340,7 @@ def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: Li
     xs = [x0]
     for l, (W, b) in enumerate(zip(weights, biases)):
         y = torch.empty_like(x0)
-        flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag
+        flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag | (nat.LG_F_BF16 if bf16 else 0)
         with _timed("gcn_fwd", proj.device):
             if node_major:
                 check(lib.lg_gcn_fwd_nm(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
@@ -353,7 +355,7 @@ def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: Li
 
 @gnn_trunk.register_fake
 def _(proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab, pairs, rowptr,
-      col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed):
+      col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed, *, bf16=False):
     B, S, D = proj.shape
     N = sensor_slot.shape[0]
     shape = (N, B, D) if node_major else (B, N, D)
@@ -364,7 +366,7 @@ def _(proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, 
 def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor], sensor_slot: Tensor,
                        sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab_t: Tensor,
                        pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
-                       node_major: bool) -> Tuple[Tensor, Tensor, List[Tensor], List[Tensor]]:
+                       node_major: bool, *, bf16: bool = False) -> Tuple[Tensor, Tensor, List[Tensor], List[Tensor]]:
     """(dproj, dnode_bias, [dW_l], [db_l]): one fused lg_gcn_bwd[_nm] per layer, last
     first; ReLU/dropout masks of a layer's output and input applied inside the kernel from
     the saved activations; the node-init bias gradient summed inside layer 0's launch."""
@@ -384,7 +386,7 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor]
     dbs: List[Tensor] = [grad_out] * L
     dbias = torch.empty(D, device=dev, dtype=torch.float32)
     for l in range(L - 1, -1, -1):
-        flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0)
+        flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
         dx = torch.empty_like(dy)
         dW = torch.empty(D, D, device=dev, dtype=torch.float32)
         db = torch.empty(D, device=dev, dtype=torch.float32)
@@ -410,7 +412,7 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor]
 
 @gnn_trunk_backward.register_fake
 def _(grad_out, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t,
-      w_t, p, node_major):
+      w_t, p, node_major, *, bf16=False):
     D = xs[0].shape[2]
     B = xs[0].shape[1] if node_major else xs[0].shape[0]
     S = sensor_idx.shape[0]
@@ -418,10 +420,12 @@ def _(grad_out, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, 
             [grad_out.new_empty(D) for _ in weights])
 
 
-def _trunk_setup(ctx, inputs, output):
+def _trunk_setup(ctx, inputs, keyword_only_inputs, output):
     (proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, _, _, _, _, _, nodetab_t,
      pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
+    bf16 = bool(keyword_only_inputs.get("bf16", False))
     ctx.L = len(weights)
+    ctx.bf16 = bf16
     ctx.mark_non_differentiable(*output[:-1])  # x_0 .. x_{L-1}: returned for the backward's masks
     ctx.set_materialize_grads(False)  # their gradients would be zero-filled (B, N, D) tensors
     ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
@@ -439,7 +443,7 @@ def _trunk_bwd(ctx, grads):
         return (None,) * 21
     dproj, dbias, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
         g, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None, nodetab_t, pairs_t,
-        rowptr_t, col_t, w_t, ctx.p, ctx.node_major)
+        rowptr_t, col_t, w_t, ctx.p, ctx.node_major, bf16=ctx.bf16)
     return (dproj, dbias, dWs, dbs) + (None,) * 17
 
 
@@ -450,12 +454,14 @@ gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)
 @torch.library.custom_op(f"{NS}::detector_heads", mutates_args=(), device_types="cuda")
 def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw1: Tensor, nb1: Tensor, nw2: Tensor,
                    nb2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor, p_edge: float, p_noleak: float,
-                   node_major: bool, keep_hidden: bool, seed: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+                   node_major: bool, keep_hidden: bool, seed: Tensor, *,
+                   bf16: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """(logits (B, P+1), EdgeHead hidden, pooled, NoLeakHead hidden).  Columns [0, P) by
     lg_edge_head_fwd (endpoint gather -> MFMA MLP -> dot, the (B, P, 3D) features never
     stored), column P by lg_pool_head_fwd (mean pool + NoLeakHead): the torch.cat of
     detector.py:218 is never a separate copy.  keep_hidden: keep the EdgeHead hidden layer
-    for a recompute-free backward (else it is empty)."""
+    for a recompute-free backward (else it is empty).  bf16: the EdgeHead MLP as one bf16
+    MFMA product (LG_F_BF16, the configs[2] tier); the NoLeakHead stays fp32."""
     lib = load_library()
     h, w1, b1, w2, b2, nw1, nb1, nw2, nb2 = (_c(t) for t in (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2))
     _req(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
@@ -465,7 +471,7 @@ def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw
     hidden, nhidden = w1.shape[0], nw1.shape[0]
     P = ends.shape[0]
     seed_v, sbit = _seed_args(seed) if (p_edge > 0.0 or p_noleak > 0.0) else (0, 0)
-    fe = nat.LG_F_DROPOUT if p_edge > 0.0 else 0
+    fe = (nat.LG_F_DROPOUT if p_edge > 0.0 else 0) | (nat.LG_F_BF16 if bf16 else 0)
     fn = nat.LG_F_DROPOUT if p_noleak > 0.0 else 0
     st = stream_of(h)
     dev = h.device
@@ -497,7 +503,7 @@ def _(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge,
 @torch.library.custom_op(f"{NS}::detector_heads_backward", mutates_args=(), device_types="cuda")
 def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, ehid: Tensor, pooled: Tensor,
                             hid: Tensor, nw1: Tensor, nw2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor,
-                            p_edge: float, p_noleak: float, node_major: bool
+                            p_edge: float, p_noleak: float, node_major: bool, *, bf16: bool = False
                             ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
     """(dh, dW1, db1, dW2, db2, dnW1, dnb1, dnW2, dnb2): lg_edge_head_bwd -> per-pipe
     endpoint grads; lg_pool_head_bwd -> dpooled and the NoLeakHead grads; ONE deterministic
@@ -509,7 +515,7 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     N, B, D = h.shape if node_major else (h.shape[1], h.shape[0], h.shape[2])
     lay = nat.LG_F_NODE_MAJOR if node_major else 0
     P, hidden, nhidden = ends.shape[0], w1.shape[0], nw1.shape[0]
-    fe = nat.LG_F_DROPOUT if p_edge > 0.0 else 0
+    fe = (nat.LG_F_DROPOUT if p_edge > 0.0 else 0) | (nat.LG_F_BF16 if bf16 else 0)
     fn = nat.LG_F_DROPOUT if p_noleak > 0.0 else 0
     dev = h.device
     st = stream_of(h)
@@ -537,18 +543,20 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
 
 
 @detector_heads_backward.register_fake
-def _(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major):
+def _(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, *,
+      bf16=False):
     H, NH = w1.shape[0], nw1.shape[0]
     return (torch.empty_like(h), torch.empty_like(w1), w1.new_empty(H), torch.empty_like(w2), w2.new_empty(1),
             torch.empty_like(nw1), nw1.new_empty(NH), torch.empty_like(nw2), nw2.new_empty(1))
 
 
-def _heads_setup(ctx, inputs, output):
+def _heads_setup(ctx, inputs, keyword_only_inputs, output):
     (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, _, _) = inputs
+    bf16 = bool(keyword_only_inputs.get("bf16", False))
     _, ehid, pooled, hid = output
     ctx.mark_non_differentiable(ehid, pooled, hid)
     ctx.set_materialize_grads(False)  # else autograd zero-fills a (B*P, 128) gradient for ehid
-    ctx.cfg = (p_edge, p_noleak, node_major)
+    ctx.cfg = (p_edge, p_noleak, node_major, bf16)
     ctx.save_for_backward(h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item)
 
 
@@ -556,9 +564,9 @@ def _heads_bwd(ctx, dlogits, _dehid, _dpooled, _dhid):
     if dlogits is None:
         return (None,) * 17
     h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item = ctx.saved_tensors
-    p_edge, p_noleak, node_major = ctx.cfg
+    p_edge, p_noleak, node_major, bf16 = ctx.cfg
     g = torch.ops.leakgnn.detector_heads_backward(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr,
-                                                  inc_item, p_edge, p_noleak, node_major)
+                                                  inc_item, p_edge, p_noleak, node_major, bf16=bf16)
     return tuple(g) + (None,) * 8
 
 

@@ -160,6 +160,9 @@ def main(argv=None) -> None:
     ap.add_argument("--num_workers", type=int, default=0)
     ap.add_argument("--log_every", type=int, default=50)
     ap.add_argument("--loader", type=str, default="device", choices=["device", "torch"])
+    ap.add_argument("--dtype", type=str, default="fp32", choices=["fp32", "bf16"],
+                    help="node-MLP tier: fp32 (fp32 parity) or bf16 (GCN transforms and EdgeHead MLP as one bf16 "
+                         "MFMA product, BASELINE configs[2])")
     ap.add_argument("--dist_backend", type=str, default="auto", choices=["auto", "nccl", "gloo"],
                     help="data parallel under torchrun: nccl (= RCCL on ROCm) for GPUs, gloo for CPU / tests")
     args = ap.parse_args(argv)
@@ -227,7 +230,8 @@ def main(argv=None) -> None:
     _, test_loader = mk(args.test_steps, args.seed + 2, 2048, leak_test, nl_test)
 
     detector = LeakDetector(inp_path=args.inp_path, sensor_node_ids=sensor_ids, pipe_ids_in_order=pipe_ids_in_order,
-                            sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1, use_time=True).to(device)
+                            sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1, use_time=True,
+                            mlp_dtype=args.dtype).to(device)
     opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay,
                             fused=(device.type == "cuda"))
     loss_fn = nn.CrossEntropyLoss()

@@ -49,8 +49,8 @@ def gcn_conv(x: torch.Tensor, edge_index: torch.Tensor, weight: torch.Tensor, bi
         row, col = edge_index[0], edge_index[1]
         w = torch.ones(row.numel(), dtype=x.dtype, device=x.device)
     h = x @ weight.t()
-    out = torch.zeros(N, h.size(1), dtype=h.dtype, device=x.device).index_add_(0, col,
-                                                                             w.view(-1, 1) * h.index_select(0, row))
+    msg = w.view(-1, 1) * h.index_select(0, row)  # PyG message(): edge_weight * x_j (type-promoted)
+    out = torch.zeros(N, h.size(1), dtype=msg.dtype, device=x.device).index_add_(0, col, msg)
     if bias is not None:
         out = out + bias
     return out

@@ -182,7 +182,7 @@ def _random_ref(seed: int):
     return {k: v.clone() for k, v in ref.state_dict().items()}
 
 
-def _oracle_b256(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None):
+def _oracle_b256(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None, autocast=False):
     """The oracle detector in eval mode: (logits, grads, fp64-comparable ReLU
     pre-activations, upstream gradient) for `up`, or for the CE gradient of `lab` in this
     run's own precision when up is None.  masks: ReLU decisions to use (relu_masks)."""
@@ -193,7 +193,15 @@ def _oracle_b256(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None):
     mr = mr.to(dt).to(dev)
     mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)
     mr.relu_masks = masks or {}
-    out = mr(r.to(dt).to(dev), tf.to(dt).to(dev))
+    if autocast:  # the tier keeps the GRU encoder fp32: so does the yardstick
+        enc_fwd = mr.sensor_encoder.forward
+
+        def enc_fp32(*a):
+            with torch.autocast("cuda", enabled=False):
+                return enc_fwd(*a)
+        mr.sensor_encoder.forward = enc_fp32
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        out = mr(r.to(dt).to(dev), tf.to(dt).to(dev)).float() if autocast else mr(r.to(dt).to(dev), tf.to(dt).to(dev))
     if up is None:
         lo = out.detach().requires_grad_(True)
         torch.nn.functional.cross_entropy(lo, lab).backward()
@@ -238,6 +246,61 @@ def test_detector_b256_eval_vs_oracle():
     # tensor 5e-5 of scale, or 4x the error of the reference arithmetic in fp32 (torch on the
     # CPU or on this GPU); the whole-vector 2-norm bar stays at 1e-5
     assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64, ref32=g32d, rtol_tensor=5e-5)
+
+
+def test_bf16_tier_b256():
+    """BASELINE configs[2] as written ("bf16 node-MLP on MFMA"): LeakDetector(mlp_dtype="bf16")
+    at B = 256 against the fp64 oracle.  Its bar is SURVEY §7's: logits within 2e-2 of their
+    scale.  Gradients for a dense random upstream gradient, against the fp64 truth, are held
+    to the reference model's own bf16 arithmetic: torch.autocast(bfloat16) of the oracle on
+    this GPU sets the yardstick (per tensor and whole vector: at most 2x its error, or 1e-2).
+    bf16 rounding of the pre-activations moves ReLU decisions, so ~1e-1 gradient errors are
+    the nature of the tier, not a kernel defect.  (Not the CE gradient of a random-init
+    model: its parameter gradients are differences of sums that cancel to ~1e-3 of their
+    terms, and bf16 rounding moves thousands of ReLU decisions, so no bf16 evaluation is
+    within 1e-1 of them — measured: EdgeHead db1 99 % off while the kernels agree with the
+    fp32 ones to 0.25 % on the same hidden layer, tools/diag_bf16.py.)  A train-mode step
+    with dropout is finite."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    sd = _random_ref(41)
+    B = 256
+    gen = torch.Generator().manual_seed(42)
+    r = torch.randn(B, 36, 29, generator=gen)
+    tf = torch.randn(B, 36, 9, generator=gen)
+    lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen)
+    up = torch.randn(B, len(pipes) + 1, generator=gen, dtype=torch.float64) / B
+    o64, g64, _, _ = _oracle_b256(sd, r, tf, torch.float64, "cpu", up=up)
+    m = LeakDetector(LTA_INP, sensors, pipes, mlp_dtype="bf16").to(DEV).eval()
+    m.load_state_dict(sd)
+    lg = m(r.to(DEV), tf.to(DEV))
+    lg.backward(up.float().to(DEV))
+    err = (lg.detach().double().cpu() - o64.double()).abs().max().item()
+    scale = o64.abs().max().item()
+    print(f"bf16 tier: logits max err {err:.3e} of scale {scale:.3e} ({err / scale:.2e})")
+    assert err <= 2e-2 * scale
+    _, gac, _, _ = _oracle_b256(sd, r, tf, torch.float32, DEV, up=up, autocast=True)
+    num = den = nac = 0.0
+    bad = []
+    for n, p in m.named_parameters():
+        t = g64[n].double()
+        t2 = (t ** 2).sum().item()
+        d = ((p.grad.double().cpu() - t) ** 2).sum().item()
+        da = ((gac[n].double() - t) ** 2).sum().item()
+        rel, rel_ac = (d / max(t2, 1e-300)) ** 0.5, (da / max(t2, 1e-300)) ** 0.5
+        print(f"  {n:40s} rel 2-norm err {rel:.2e}   torch autocast-bf16 {rel_ac:.2e}")
+        if rel > max(2 * rel_ac, 1e-2):
+            bad.append(n)
+        num, den, nac = num + d, den + t2, nac + da
+    print(f"  whole vector rel 2-norm err {(num / den) ** 0.5:.2e}   torch autocast-bf16 {(nac / den) ** 0.5:.2e}")
+    assert num <= max(4 * nac, 1e-4 * den)
+    assert not bad, bad
+    # train mode (dropout) step
+    m.train()
+    m.zero_grad(set_to_none=True)
+    loss = torch.nn.functional.cross_entropy(m(r.to(DEV), tf.to(DEV)), lab.to(DEV))
+    loss.backward()
+    assert np.isfinite(loss.item()) and all(torch.isfinite(p.grad).all() for p in m.parameters())
 
 
 def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu", masks=None, aux=None):
