@@ -165,6 +165,28 @@ int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float*
                      int64_t B, int64_t N, int64_t S, int64_t D,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
 
+/* K1+K2 with the sensor projection folded in: x0 as lg_node_init_fwd with
+ *   proj[b][s] = h_s[b][s] @ W[:, :Ds]^T + W[:, Ds] + bias     (W: fp32 [D][Ds+1], nn.Linear layout)
+ * formed per sensor row inside the launch (no separate GEMM / proj buffer).
+ * sensor_idx: int64 [S], node of sensor s (sensor_slot is its inverse; a duplicated id's
+ * earlier entries are skipped, as h0[:, idx] = h_s keeps the last write, detector.py:181).
+ * Replaces: sensor_to_node (detector.py:160, 184-189) + node init.  Ds == D in {32, 64}. */
+int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx, const float* h_s, const float* W,
+                          const float* bias, float* x0, int64_t B, int64_t N, int64_t S, int64_t Ds, int64_t D,
+                          int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);
+
+/* Backward of the folded projection, from dx0 = the gradient of the node-init
+ * pre-activation (lg_gcn_bwd[_nm] of layer 0 with LG_F_MASK_OUT):
+ *   dproj[b][s] = dx0[row(sensor_idx[s], b)] * (live ? live[s] : 1)   (row per LG_F_NODE_MAJOR)
+ *   dh_s = dproj @ W[:, :Ds];   dW = dproj^T [h_s, 1];   db = sum dproj + dbias_in (may be NULL)
+ * live: fp32 [S] (0 for a duplicated sensor id whose row was overwritten, detector.py:181),
+ * or NULL.  One launch + one fixed-order slab reduce (deterministic). */
+int64_t lg_sensor_proj_bwd_workspace_bytes(int64_t B, int64_t S, int64_t Ds, int64_t D);
+int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, const float* live, const float* h_s,
+                       const float* W, const float* dbias_in, float* dh_s, float* dW, float* db, int64_t B,
+                       int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace,
+                       lg_stream_t stream);
+
 /* K2 backward (node init Linear(Ds+1 -> D), detector.py:160, 184-189), weight side:
  * for sensor rows the Linear input is [h_s, 1], so with dy = d(proj) [K][M] (K = B*S rows)
  * and x = h_s [K][N]:

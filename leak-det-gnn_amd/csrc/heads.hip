@@ -41,6 +41,160 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
     }
 }
 
+// k_node_init with the sensor projection folded in (detector.py:160, 184-190): a sensor
+// row's pre-activation is h_s[b][s] . W[o][:Ds] + (W[o][Ds] + bias[o]) (its Linear input is
+// [h_s, 1]), every other row's is bias (input [0, 0]).  The first GS workgroups stage W^T
+// and the folded bias in LDS and form the S*B sensor rows (a lane group per row, 4 outputs
+// per lane, 4 * Ds fmas in ascending k); then every workgroup writes the non-sensor rows
+// like k_node_init, so no other workgroup pays for W.
+template <int D, int DS>
+__global__ void __launch_bounds__(256)
+k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ sidx, const float* __restrict__ hs,
+                 const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ x0, int64_t B,
+                 int64_t N, lg_fastdiv fdM, int nm, int64_t S, int64_t R, int GS, int dropout, float p, float scale,
+                 uint64_t seed, uint32_t salt) {
+    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    __shared__ __attribute__((aligned(16))) float wt[DS][D];  // W^T[k][o]
+    __shared__ __attribute__((aligned(16))) float bf[D];      // W[o][DS] + bias[o]
+    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
+    auto finish = [&](f32x4 v, int64_t b, int64_t n) {
+        const int64_t rw = b * N + n;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float t = fmaxf(v[i], 0.f);
+            if (dropout) t = lg_dropout(t, p, scale, key, rw * D + 4 * fg + i);
+            v[i] = t;
+        }
+        st4(x0 + (nm ? n * B + b : b * N + n) * D + 4 * fg, v);
+    };
+    if (static_cast<int>(blockIdx.x) < GS) {
+        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {
+            const int o = i / (DS + 1), k = i % (DS + 1);
+            if (k < DS) wt[k][o] = W[i];
+            else bf[o] = W[i] + bias[o];
+        }
+        __syncthreads();
+        const f32x4 bs = ld4(bf + 4 * fg);
+        for (int64_t q = static_cast<int64_t>(blockIdx.x) * RPB + rl; q < S * B; q += static_cast<int64_t>(GS) * RPB) {
+            const int64_t sc = q / B, b = q - sc * B, n = sidx[sc];
+            if (slot[n] != sc) continue;  // a duplicated sensor id: the last one's row wins (detector.py:181)
+            const float* hrow = hs + (b * S + sc) * DS;
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+            for (int k4 = 0; k4 < DS / 4; ++k4) {
+                const f32x4 h4 = ld4(hrow + 4 * k4);
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const f32x4 w = ld4(&wt[4 * k4 + kk][4 * fg]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] = fmaf(h4[kk], w[i], acc[i]);
+                }
+            }
+            finish(acc + bs, b, n);
+        }
+    }
+    const f32x4 b0 = ld4(bias + 4 * fg);
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
+        const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
+        const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
+        if (slot[n] >= 0) continue;
+        finish(b0, b, n);
+    }
+}
+
+// Backward of the sensor projection from the node-init pre-activation gradient dx0 (the
+// layer-0 backward's output, already masked by the node init's ReLU/dropout):
+//   dproj[b][s] = dx0[row(sensor_node[s], b)] * live[s]
+//   dh_s[b][s][k] = sum_o dproj[b][s][o] W[o][k]                          (written)
+//   slab row: dW[o][k] = sum dproj[.][o] [h_s, 1][.][k],  db[o] = sum dproj[.][o] (+ dbias_in
+//   from workgroup 0: the non-sensor rows' sum the layer-0 backward already formed)
+// One workgroup per kSpRows (b, s) rows, staged in LDS; every sum in a fixed order.
+constexpr int kSpRows = 32;
+template <int D, int DS>
+__global__ void __launch_bounds__(256)
+k_sensor_proj_bwd(const float* __restrict__ dx0, const int64_t* __restrict__ sidx, const float* __restrict__ live,
+                  const float* __restrict__ hs, const float* __restrict__ W, const float* __restrict__ dbias_in,
+                  float* __restrict__ dhs, float* __restrict__ slab, int64_t B, int64_t N, int64_t S, int nm) {
+    constexpr int SL = D * (DS + 1) + D;
+    __shared__ __attribute__((aligned(16))) float dp[kSpRows][D + 4];
+    __shared__ __attribute__((aligned(16))) float hx[kSpRows][DS + 4];  // column DS = 1 (the bias input)
+    __shared__ __attribute__((aligned(16))) float wl[D][DS];
+    const int64_t K = B * S, k0 = static_cast<int64_t>(blockIdx.x) * kSpRows;
+    for (int i = threadIdx.x; i < D * DS / 4; i += 256) {
+        const int o = i / (DS / 4), c4 = 4 * (i % (DS / 4));
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = W[o * (DS + 1) + c4 + j];
+        st4(&wl[o][c4], v);
+    }
+    for (int i = threadIdx.x; i < kSpRows * (D / 4); i += 256) {
+        const int rr = i / (D / 4), c4 = 4 * (i % (D / 4));
+        const int64_t kr = k0 + rr;
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kr < K) {
+            const int64_t b = kr / S, sc = kr - b * S, n = sidx[sc];
+            const int64_t row = nm ? n * B + b : b * N + n;
+            v = ld4(dx0 + row * D + c4);
+            if (live) v = v * live[sc];
+        }
+        st4(&dp[rr][c4], v);
+    }
+    for (int i = threadIdx.x; i < kSpRows * (DS / 4); i += 256) {
+        const int rr = i / (DS / 4), c4 = 4 * (i % (DS / 4));
+        const int64_t kr = k0 + rr;
+        st4(&hx[rr][c4], kr < K ? ld4(hs + kr * DS + c4) : f32x4{0.f, 0.f, 0.f, 0.f});
+        if (c4 == 0) hx[rr][DS] = 1.f;
+    }
+    __syncthreads();
+    // dh_s: thread -> (row, 4 consecutive k); the wave's lanes share o, so the W reads broadcast
+    {
+        constexpr int TPR = DS / 4;  // threads per row
+        for (int t = threadIdx.x; t < kSpRows * TPR; t += 256) {
+            const int rr = t / TPR, kc = 4 * (t % TPR);
+            f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int o4 = 0; o4 < D / 4; ++o4) {
+                const f32x4 g = ld4(&dp[rr][4 * o4]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const f32x4 w = ld4(&wl[4 * o4 + j][kc]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] = fmaf(g[j], w[i], acc[i]);
+                }
+            }
+            const int64_t kr = k0 + rr;
+            if (kr < K) st4(dhs + kr * DS + kc, acc);
+        }
+    }
+    // slab: dW[o][k] over this block's rows; thread -> (o, KW consecutive k), KW independent
+    // accumulator chains; the k = DS column (the constant-1 input) is db[o]
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
+    {
+        constexpr int KQ = 256 / D, KW = DS / KQ;
+        const int o = threadIdx.x / KQ, kb = (threadIdx.x % KQ) * KW;
+        float acc[KW];
+#pragma unroll
+        for (int j = 0; j < KW; ++j) acc[j] = 0.f;
+        float a1 = 0.f;
+        for (int rr = 0; rr < kSpRows; ++rr) {
+            const float g = dp[rr][o];
+#pragma unroll
+            for (int j = 0; j < KW; j += 4) {
+                const f32x4 hv = ld4(&hx[rr][kb + j]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[j + i] = fmaf(g, hv[i], acc[j + i]);
+            }
+            a1 += g;
+        }
+#pragma unroll
+        for (int j = 0; j < KW; ++j) out[o * (DS + 1) + kb + j] = acc[j];
+        if (kb == 0) {
+            out[o * (DS + 1) + DS] = a1;
+            out[D * (DS + 1) + o] = a1 + ((blockIdx.x == 0 && dbias_in) ? dbias_in[o] : 0.f);
+        }
+    }
+}
+
 template <int D>
 __global__ void __launch_bounds__(256)
 k_pipe_gather(const int64_t* __restrict__ ends, const float* __restrict__ h, float* __restrict__ feat, int64_t N,
@@ -217,6 +371,63 @@ extern "C" int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc
     return LG_OK;
 }
 
+extern "C" int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx, const float* h_s,
+                                     const float* W, const float* bias, float* x0, int64_t B, int64_t N, int64_t S,
+                                     int64_t Ds, int64_t D, int flags, float dropout_p, uint64_t seed, uint32_t salt,
+                                     lg_stream_t stream) {
+    if (B < 0 || N <= 0 || S < 0) return LG_EINVAL;
+    if (!sensor_slot || !W || !bias || !x0 || (S > 0 && B > 0 && (!h_s || !sensor_idx))) return LG_EINVAL;
+    if (!((D == 64 && Ds == 64) || (D == 32 && Ds == 32))) return LG_EUNSUPPORTED;
+    const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
+    if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    const int64_t R = B * N;
+    if (R == 0) return LG_OK;
+    if (R >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const int nm = (flags & LG_F_NODE_MAJOR) ? 1 : 0;
+    const lg_fastdiv fdM = lg_make_fastdiv(static_cast<uint32_t>(nm ? B : N));
+    const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    hipStream_t s = lg_stream(stream);
+    const int RPBD = 256 / (static_cast<int>(D) / 4);
+    const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * B, RPBD), lg_num_cus())));
+    if (D == 64)
+        lg_launch(k_node_init_proj<64, 64>, std::max<unsigned>(row_grid(R, 64), GS), 256, 0, s, sensor_slot, sensor_idx,
+                  h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
+    else
+        lg_launch(k_node_init_proj<32, 32>, std::max<unsigned>(row_grid(R, 32), GS), 256, 0, s, sensor_slot, sensor_idx,
+                  h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int64_t lg_sensor_proj_bwd_workspace_bytes(int64_t B, int64_t S, int64_t Ds, int64_t D) {
+    if (B < 0 || S < 0 || !((D == 64 && Ds == 64) || (D == 32 && Ds == 32))) return LG_EUNSUPPORTED;
+    const int64_t G = std::max<int64_t>(1, ceil_div(B * S, kSpRows));
+    return G * (D * (Ds + 1) + D) * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, const float* live, const float* h_s,
+                                  const float* W, const float* dbias_in, float* dh_s, float* dW, float* db, int64_t B,
+                                  int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace,
+                                  lg_stream_t stream) {
+    if (B < 0 || N <= 0 || S < 0 || !W || !dW || !db || !workspace) return LG_EINVAL;
+    if (B * S > 0 && (!dx0 || !sensor_idx || !h_s || !dh_s)) return LG_EINVAL;
+    if (!((D == 64 && Ds == 64) || (D == 32 && Ds == 32))) return LG_EUNSUPPORTED;
+    const int nm = (flags & LG_F_NODE_MAJOR) ? 1 : 0;
+    const int G = static_cast<int>(std::max<int64_t>(1, ceil_div(B * S, kSpRows)));
+    const int64_t SL = D * (Ds + 1) + D;
+    float* slab = static_cast<float*>(workspace);
+    hipStream_t s = lg_stream(stream);
+    if (D == 64)
+        lg_launch(k_sensor_proj_bwd<64, 64>, G, 256, 0, s, dx0, sensor_idx, live, h_s, W, dbias_in, dh_s, slab, B, N, S,
+                  nm);
+    else
+        lg_launch(k_sensor_proj_bwd<32, 32>, G, 256, 0, s, dx0, sensor_idx, live, h_s, W, dbias_in, dh_s, slab, B, N, S,
+                  nm);
+    LG_RET_IF_LAUNCH_FAILED();
+    const LgSlabSeg segs[2] = {{0, D * (Ds + 1), dW}, {D * (Ds + 1), D, db}};
+    return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
+}
+
 extern "C" int64_t lg_linear_dw_workspace_bytes(int64_t K, int64_t M, int64_t N) {
     if (K < 0 || (M != 32 && M != 64) || (N != 32 && N != 64)) return LG_EUNSUPPORTED;
     return static_cast<int64_t>(linear_dw_grid(K)) * (M * (N + 1) + M) * static_cast<int64_t>(sizeof(float));
@@ -246,7 +457,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 9; }
+extern "C" int lg_abi_version(void) { return 10; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 9  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 10  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -49,6 +49,10 @@ SIGNATURES = {
     "lg_linear_dw_workspace_bytes": (_i64, [_i64, _i64, _i64]),
     "lg_linear_dw": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
     "lg_node_init_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_node_init_proj_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32,
+                                     _p]),
+    "lg_sensor_proj_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "lg_sensor_proj_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _p, _p]),
     "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_gcn_bwd_workspace_bytes": (_i64, [_i64]),

@@ -159,19 +159,17 @@ class LeakDetector(nn.Module):
         h_s = self.sensor_encoder(residual, tfeat)                        # (B, S, Ds)
         f = ops._f32
         Wn, bn = f(self.sensor_to_node.weight), f(self.sensor_to_node.bias)  # (D, Ds+1), (D,)
-        # rows with a sensor: [h_s, 1] W^T + b ; rows without: [0, 0] W^T + b = b
-        proj = torch.ops.leakgnn.sensor_proj(h_s, Wn, bn)                  # (B, S, D)
         N, D = len(self.node_names), Wn.shape[0]
         if self.capture is not None and torch.is_grad_enabled():
-            for name, t in (("h_s", h_s), ("proj", proj)):
-                if t.requires_grad:
-                    t.retain_grad()
-                self.capture[name] = t
+            if h_s.requires_grad:
+                h_s.retain_grad()
+            self.capture["h_s"] = h_s
         nm = ops.use_node_major(B, N, D)
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
+        # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init
         xs = torch.ops.leakgnn.gnn_trunk(
-            proj, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
+            h_s, Wn, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
             nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
             g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
             library.seed_tensor(residual.device) if drop else _NO_SEED, bf16=self.mlp_dtype == "bf16")

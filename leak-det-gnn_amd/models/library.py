@@ -308,40 +308,46 @@ gru_encoder.register_autograd(_gru_bwd, setup_context=_gru_setup)
 
 # ============================================================================ gnn_trunk
 @torch.library.custom_op(f"{NS}::gnn_trunk", mutates_args=(), device_types="cuda")
-def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor], sensor_slot: Tensor,
-              sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab: Tensor, pairs: Tensor,
-              rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor,
-              col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor, *,
-              bf16: bool = False) -> List[Tensor]:
-    """[x_0, ..., x_L]: node init (detector.py:178-190) then L x dropout(relu(GCNConv)).
+def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor],
+              sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
+              nodetab: Tensor, pairs: Tensor, rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor,
+              pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor,
+              *, bf16: bool = False) -> List[Tensor]:
+    """[x_0, ..., x_L]: sensor_to_node + node init (detector.py:160, 178-190), then
+    L x dropout(relu(GCNConv)).
 
-      x_0     = dropout(relu(slot >= 0 ? proj[b, slot] : node_bias))     (lg_node_init_fwd)
-      x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                     (lg_gcn_fwd[_nm], fused)
-    node_major: features [N][B][D] (lg_gcn_fwd_nm), else [B][N][D].  p: dropout prob
-    (0 = eval).  Every activation is returned: the backward reads its ReLU/dropout masks
-    back as [x > 0] and needs x_l for dW, so no mask is ever stored.  bf16: the node-major
-    transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier)."""
+      x_0     = dropout(relu(slot >= 0 ? [h_s[b, slot], 1] W^T + b : b))   (lg_node_init_proj_fwd)
+      x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                        (lg_gcn_fwd[_nm], fused)
+    h_s: (B, S, Ds) sensor encodings; proj_weight: sensor_to_node.weight (D, Ds + 1);
+    node_bias: its bias.  The projection is formed inside the node-init launch (no GEMM, no
+    proj buffer).  node_major: features [N][B][D] (lg_gcn_fwd_nm), else [B][N][D].  p:
+    dropout prob (0 = eval).  Every activation is returned: the backward reads its
+    ReLU/dropout masks back as [x > 0] and needs x_l for dW, so no mask is ever stored.
+    bf16: the node-major transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier)."""
     lib = load_library()
-    proj, node_bias = _c(proj), _c(node_bias)
+    h_s, proj_weight, node_bias = _c(h_s), _c(proj_weight), _c(node_bias)
     weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]
-    _req(proj, node_bias, *weights, *biases)
-    B, S, D = proj.shape
+    _req(h_s, proj_weight, node_bias, *weights, *biases)
+    B, S, Ds = h_s.shape
+    D = proj_weight.shape[0]
     _check_d(D)
+    if tuple(proj_weight.shape) != (D, Ds + 1):
+        raise ValueError(f"proj_weight must be (D, Ds + 1) = ({D}, {Ds + 1}), got {tuple(proj_weight.shape)}")
     N = sensor_slot.shape[0]
     drop = p > 0.0
     seed_v, sbit = _seed_args(seed) if drop else (0, 0)
     dflag = nat.LG_F_DROPOUT if drop else 0
-    st = stream_of(proj)
-    x0 = torch.empty((N, B, D) if node_major else (B, N, D), device=proj.device, dtype=torch.float32)
-    with _timed("node_init", proj.device):
-        check(lib.lg_node_init_fwd(ptr(sensor_slot), ptr(proj), ptr(node_bias), ptr(x0), B, N, S, D,
-                                   dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v, 0 | sbit, st),
-              "lg_node_init_fwd")
+    st = stream_of(h_s)
+    x0 = torch.empty((N, B, D) if node_major else (B, N, D), device=h_s.device, dtype=torch.float32)
+    with _timed("node_init", h_s.device):
+        check(lib.lg_node_init_proj_fwd(ptr(sensor_slot), ptr(sensor_idx), ptr(h_s), ptr(proj_weight), ptr(node_bias),
+                                        ptr(x0), B, N, S, Ds, D, dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v,
+                                        0 | sbit, st), "lg_node_init_proj_fwd")
     xs = [x0]
     for l, (W, b) in enumerate(zip(weights, biases)):
         y = torch.empty_like(x0)
         flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag | (nat.LG_F_BF16 if bf16 else 0)
-        with _timed("gcn_fwd", proj.device):
+        with _timed("gcn_fwd", h_s.device):
             if node_major:
                 check(lib.lg_gcn_fwd_nm(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
                                         col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v, (l + 1) | sbit, st),
@@ -354,22 +360,26 @@ def gnn_trunk(proj: Tensor, node_bias: Tensor, weights: List[Tensor], biases: Li
 
 
 @gnn_trunk.register_fake
-def _(proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab, pairs, rowptr,
-      col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed, *, bf16=False):
-    B, S, D = proj.shape
+def _(h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab, pairs,
+      rowptr, col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed, *, bf16=False):
+    B = h_s.shape[0]
+    D = proj_weight.shape[0]
     N = sensor_slot.shape[0]
     shape = (N, B, D) if node_major else (B, N, D)
-    return [proj.new_empty(shape) for _ in range(len(weights) + 1)]
+    return [h_s.new_empty(shape) for _ in range(len(weights) + 1)]
 
 
 @torch.library.custom_op(f"{NS}::gnn_trunk_backward", mutates_args=(), device_types="cuda")
-def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor], sensor_slot: Tensor,
-                       sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor], nodetab_t: Tensor,
-                       pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
-                       node_major: bool, *, bf16: bool = False) -> Tuple[Tensor, Tensor, List[Tensor], List[Tensor]]:
-    """(dproj, dnode_bias, [dW_l], [db_l]): one fused lg_gcn_bwd[_nm] per layer, last
-    first; ReLU/dropout masks of a layer's output and input applied inside the kernel from
-    the saved activations; the node-init bias gradient summed inside layer 0's launch."""
+def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], h_s: Tensor, proj_weight: Tensor, weights: List[Tensor],
+                       sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
+                       nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
+                       node_major: bool, *, bf16: bool = False
+                       ) -> Tuple[Tensor, Tensor, Tensor, List[Tensor], List[Tensor]]:
+    """(dh_s, dproj_weight, dnode_bias, [dW_l], [db_l]): one fused lg_gcn_bwd[_nm] per layer,
+    last first (ReLU/dropout masks of a layer's output and input applied inside the kernel
+    from the saved activations; the non-sensor rows' node-bias gradient summed inside layer
+    0's launch), then ONE lg_sensor_proj_bwd for the projection (gather of the sensor rows,
+    dh_s, dW and the full bias gradient)."""
     lib = load_library()
     L = len(weights)
     dev = grad_out.device
@@ -378,19 +388,20 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor]
         N, B, D = xs[0].shape
     else:
         B, N, D = xs[0].shape
+    S, Ds = h_s.shape[1], h_s.shape[2]
     scale = 1.0 / (1.0 - p) if p > 0.0 else 1.0
     dy = grad_out.contiguous()
     wsb = lib.lg_gcn_bwd_nm_workspace_bytes(D) if node_major else lib.lg_gcn_bwd_workspace_bytes(D)
     ws = torch.empty(int(wsb), device=dev, dtype=torch.uint8)
     dWs: List[Tensor] = [grad_out] * L
     dbs: List[Tensor] = [grad_out] * L
-    dbias = torch.empty(D, device=dev, dtype=torch.float32)
+    dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
     for l in range(L - 1, -1, -1):
         flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
         dx = torch.empty_like(dy)
         dW = torch.empty(D, D, device=dev, dtype=torch.float32)
         db = torch.empty(D, device=dev, dtype=torch.float32)
-        slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias)) if l == 0 else (None, None)
+        slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias_ns)) if l == 0 else (None, None)
         with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dev):
             if node_major:
                 check(lib.lg_gcn_bwd_nm(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
@@ -402,49 +413,55 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], weights: List[Tensor]
                                      col_t.numel(), flags, scale, scale, ptr(ws), st), "lg_gcn_bwd")
         dWs[l], dbs[l] = dW, db
         dy = dx  # already masked by the previous op's relu/dropout
-    dproj = dy.index_select(0, sensor_idx).transpose(0, 1) if node_major else dy.index_select(1, sensor_idx)
-    if slot_live is not None:
-        dproj = dproj * slot_live.view(1, -1, 1)
-    if L == 0:
-        dbias = dy.index_select(0 if node_major else 1, nonsensor_idx).sum(dim=(0, 1))
-    return dproj.contiguous(), dbias, dWs, dbs
+    if L == 0:  # no layer-0 launch applied the node init's relu/dropout mask
+        dy = dy * (xs[0] > 0) * scale
+        dbias_ns = dy.index_select(0 if node_major else 1, nonsensor_idx).sum(dim=(0, 1))
+    dh_s = torch.empty(B, S, Ds, device=dev, dtype=torch.float32)
+    dWp = torch.empty(D, Ds + 1, device=dev, dtype=torch.float32)
+    dbp = torch.empty(D, device=dev, dtype=torch.float32)
+    wsp = torch.empty(int(lib.lg_sensor_proj_bwd_workspace_bytes(B, S, Ds, D)), device=dev, dtype=torch.uint8)
+    with _timed("linear_dw", dev):
+        check(lib.lg_sensor_proj_bwd(ptr(dy), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
+                                     ptr(h_s), ptr(proj_weight), ptr(dbias_ns), ptr(dh_s), ptr(dWp), ptr(dbp), B, N,
+                                     S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), st),
+              "lg_sensor_proj_bwd")
+    return dh_s, dWp, dbp, dWs, dbs
 
 
 @gnn_trunk_backward.register_fake
-def _(grad_out, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t,
-      w_t, p, node_major, *, bf16=False):
-    D = xs[0].shape[2]
-    B = xs[0].shape[1] if node_major else xs[0].shape[0]
-    S = sensor_idx.shape[0]
-    return (grad_out.new_empty(B, S, D), grad_out.new_empty(D), [torch.empty_like(t) for t in weights],
-            [grad_out.new_empty(D) for _ in weights])
+def _(grad_out, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t, pairs_t,
+      rowptr_t, col_t, w_t, p, node_major, *, bf16=False):
+    D = proj_weight.shape[0]
+    return (torch.empty_like(h_s), torch.empty_like(proj_weight), grad_out.new_empty(D),
+            [torch.empty_like(t) for t in weights], [grad_out.new_empty(D) for _ in weights])
 
 
 def _trunk_setup(ctx, inputs, keyword_only_inputs, output):
-    (proj, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, _, _, _, _, _, nodetab_t,
-     pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
+    (h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, _, _, _, _, _,
+     nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
     bf16 = bool(keyword_only_inputs.get("bf16", False))
     ctx.L = len(weights)
     ctx.bf16 = bf16
     ctx.mark_non_differentiable(*output[:-1])  # x_0 .. x_{L-1}: returned for the backward's masks
     ctx.set_materialize_grads(False)  # their gradients would be zero-filled (B, N, D) tensors
     ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
-    ctx.save_for_backward(*output, *weights, sensor_slot, sensor_idx, nonsensor_idx,
+    ctx.save_for_backward(*output, h_s, proj_weight, *weights, sensor_slot, sensor_idx, nonsensor_idx,
                           slot_live if slot_live is not None else sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t)
 
 
 def _trunk_bwd(ctx, grads):
     L = ctx.L
     saved = ctx.saved_tensors
-    xs, weights = list(saved[:L + 1]), list(saved[L + 1:2 * L + 1])
-    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 1:]
+    xs, h_s, proj_weight = list(saved[:L + 1]), saved[L + 1], saved[L + 2]
+    weights = list(saved[L + 3:2 * L + 3])
+    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 3:]
     g = grads[-1]
     if g is None:
-        return (None,) * 21
-    dproj, dbias, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
-        g, xs, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None, nodetab_t, pairs_t,
-        rowptr_t, col_t, w_t, ctx.p, ctx.node_major, bf16=ctx.bf16)
-    return (dproj, dbias, dWs, dbs) + (None,) * 17
+        return (None,) * 22
+    dh_s, dWp, dbp, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
+        g, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None,
+        nodetab_t, pairs_t, rowptr_t, col_t, w_t, ctx.p, ctx.node_major, bf16=ctx.bf16)
+    return (dh_s, dWp, dbp, dWs, dbs) + (None,) * 17
 
 
 gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)
@@ -492,7 +509,7 @@ def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw
 
 @detector_heads.register_fake
 def _(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, keep_hidden,
-      seed):
+      seed, *, bf16=False):
     B = h.shape[1] if node_major else h.shape[0]
     D = h.shape[2]
     P = ends.shape[0]

@@ -154,3 +154,32 @@ def check_relu_ties(pre64: dict, masks: dict, keep: dict | None = None, rel: flo
             assert worst <= lim, f"ReLU site {site}: {n} HIP decisions differ from fp64, |pre| up to {worst:.3e} > {lim:.3e}"
             ties += n
     return ties
+
+
+def oracle_run(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None, autocast=False):
+    """The oracle detector (oracle/detector_ref.py) in eval mode: (logits, grads, fp64-comparable ReLU
+    pre-activations, upstream gradient) for `up`, or for the CE gradient of `lab` in this
+    run's own precision when up is None.  masks: ReLU decisions to use (relu_masks)."""
+    from oracle.detector_ref import LeakDetectorRef
+    sensors, pipes = lta_ids()
+    mr = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
+    mr.load_state_dict(sd)
+    mr = mr.to(dt).to(dev)
+    mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)
+    mr.relu_masks = masks or {}
+    if autocast:  # the tier keeps the GRU encoder fp32: so does the yardstick
+        enc_fwd = mr.sensor_encoder.forward
+
+        def enc_fp32(*a):
+            with torch.autocast("cuda", enabled=False):
+                return enc_fwd(*a)
+        mr.sensor_encoder.forward = enc_fp32
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        out = mr(r.to(dt).to(dev), tf.to(dt).to(dev)).float() if autocast else mr(r.to(dt).to(dev), tf.to(dt).to(dev))
+    if up is None:
+        lo = out.detach().requires_grad_(True)
+        torch.nn.functional.cross_entropy(lo, lab).backward()
+        up = lo.grad.clone()
+    out.backward(up.to(dt).to(dev))
+    pre = {k[len("pre_"):]: v.detach() for k, v in mr.trace.items() if k.startswith("pre_")}
+    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in mr.named_parameters()}, pre, up

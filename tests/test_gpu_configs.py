@@ -19,7 +19,7 @@ import pytest
 import torch
 
 from helpers import (LTA_INP, RTOL, assert_close, assert_grads_match_truth, check_relu_ties, hip_relu_masks, load,
-                     lta_ids)
+                     lta_ids, oracle_run)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -182,35 +182,6 @@ def _random_ref(seed: int):
     return {k: v.clone() for k, v in ref.state_dict().items()}
 
 
-def _oracle_b256(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None, autocast=False):
-    """The oracle detector in eval mode: (logits, grads, fp64-comparable ReLU
-    pre-activations, upstream gradient) for `up`, or for the CE gradient of `lab` in this
-    run's own precision when up is None.  masks: ReLU decisions to use (relu_masks)."""
-    from oracle.detector_ref import LeakDetectorRef
-    sensors, pipes = lta_ids()
-    mr = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
-    mr.load_state_dict(sd)
-    mr = mr.to(dt).to(dev)
-    mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)
-    mr.relu_masks = masks or {}
-    if autocast:  # the tier keeps the GRU encoder fp32: so does the yardstick
-        enc_fwd = mr.sensor_encoder.forward
-
-        def enc_fp32(*a):
-            with torch.autocast("cuda", enabled=False):
-                return enc_fwd(*a)
-        mr.sensor_encoder.forward = enc_fp32
-    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
-        out = mr(r.to(dt).to(dev), tf.to(dt).to(dev)).float() if autocast else mr(r.to(dt).to(dev), tf.to(dt).to(dev))
-    if up is None:
-        lo = out.detach().requires_grad_(True)
-        torch.nn.functional.cross_entropy(lo, lab).backward()
-        up = lo.grad.clone()
-    out.backward(up.to(dt).to(dev))
-    pre = {k[len("pre_"):]: v.detach() for k, v in mr.trace.items() if k.startswith("pre_")}
-    return out.detach().cpu(), {n: p.grad.detach().cpu() for n, p in mr.named_parameters()}, pre, up
-
-
 def test_detector_b256_eval_vs_oracle():
     """L-TOWN-A at the bench batch (B = 256, node-major trunk), eval mode, random weights:
     logits within 1e-5 of the oracle; grads for the oracle's fp64 CE gradient vs fp64 truth
@@ -228,7 +199,7 @@ def test_detector_b256_eval_vs_oracle():
     r = torch.randn(B, 36, 29, generator=gen)
     tf = torch.randn(B, 36, 9, generator=gen)
     lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen)
-    _, _, pre64, up = _oracle_b256(sd, r, tf, torch.float64, "cpu", lab=lab)
+    _, _, pre64, up = oracle_run(sd, r, tf, torch.float64, "cpu", lab=lab)
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
     m.load_state_dict(sd)
     m.capture = {}
@@ -237,9 +208,9 @@ def test_detector_b256_eval_vs_oracle():
     masks = hip_relu_masks(m.capture, B, len(m.node_names), len(pipes), m.pipe_ends)
     check_relu_ties(pre64, masks)
     # truth and fp32 yardsticks all on the HIP path's side of every kink
-    _, g64, _, _ = _oracle_b256(sd, r, tf, torch.float64, "cpu", up=up, masks=masks)
-    o32, g32, _, _ = _oracle_b256(sd, r, tf, torch.float32, "cpu", up=up, masks=masks)
-    _, g32d, _, _ = _oracle_b256(sd, r, tf, torch.float32, DEV, up=up, masks=masks)
+    _, g64, _, _ = oracle_run(sd, r, tf, torch.float64, "cpu", up=up, masks=masks)
+    o32, g32, _, _ = oracle_run(sd, r, tf, torch.float32, "cpu", up=up, masks=masks)
+    _, g32d, _, _ = oracle_run(sd, r, tf, torch.float32, DEV, up=up, masks=masks)
     assert_close(lg, o32, what="B=256 logits")
     # The CE gradient makes dW1 of the EdgeHead and the conv bias grads the difference of two
     # sums over ~2e5 rows that nearly cancel (the label rows against all the others): per
@@ -272,7 +243,7 @@ def test_bf16_tier_b256():
     tf = torch.randn(B, 36, 9, generator=gen)
     lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen)
     up = torch.randn(B, len(pipes) + 1, generator=gen, dtype=torch.float64) / B
-    o64, g64, _, _ = _oracle_b256(sd, r, tf, torch.float64, "cpu", up=up)
+    o64, g64, _, _ = oracle_run(sd, r, tf, torch.float64, "cpu", up=up)
     m = LeakDetector(LTA_INP, sensors, pipes, mlp_dtype="bf16").to(DEV).eval()
     m.load_state_dict(sd)
     lg = m(r.to(DEV), tf.to(DEV))
@@ -281,7 +252,7 @@ def test_bf16_tier_b256():
     scale = o64.abs().max().item()
     print(f"bf16 tier: logits max err {err:.3e} of scale {scale:.3e} ({err / scale:.2e})")
     assert err <= 2e-2 * scale
-    _, gac, _, _ = _oracle_b256(sd, r, tf, torch.float32, DEV, up=up, autocast=True)
+    _, gac, _, _ = oracle_run(sd, r, tf, torch.float32, DEV, up=up, autocast=True)
     num = den = nac = 0.0
     bad = []
     for n, p in m.named_parameters():

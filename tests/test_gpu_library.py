@@ -22,9 +22,9 @@ def _graph(N=300, E=1500, seed=1):
     return GCNGraph.build(ei, N, DEV)
 
 
-def _check(op, args):
-    torch.library.opcheck(op, args, test_utils=("test_schema", "test_autograd_registration", "test_faketensor",
-                                                "test_aot_dispatch_dynamic"))
+def _check(op, args, kwargs=None):
+    torch.library.opcheck(op, args, kwargs, test_utils=("test_schema", "test_autograd_registration",
+                                                        "test_faketensor", "test_aot_dispatch_dynamic"))
 
 
 def test_opcheck_gcn_conv_and_mean_pool():
@@ -49,7 +49,7 @@ def test_opcheck_sensor_proj_and_gru():
 
 @pytest.mark.parametrize("B,p", [(3, 0.0), (16, 0.1)])
 def test_opcheck_trunk_and_heads(B, p):
-    """gnn_trunk (window-major at B = 3, node-major with dropout at B = 16) and
+    """gnn_trunk (window-major at B = 3, node-major with dropout and the bf16 tier at B = 16) and
     detector_heads on L-TOWN-A, with the detector's own graph state."""
     from models import ops
     from models.detector import LeakDetector
@@ -58,20 +58,22 @@ def test_opcheck_trunk_and_heads(B, p):
     graph, inc, slot, sidx, live, nons = m._device_state(DEV)
     nm = ops.use_node_major(B, 661, 64)
     seed = torch.tensor([12345], dtype=torch.long)
-    proj = torch.randn(B, 29, 64, device=DEV, requires_grad=True)
+    h_s = torch.randn(B, 29, 64, device=DEV, requires_grad=True)
+    Wn = torch.randn(64, 65, device=DEV).div_(8).requires_grad_(True)
     wts = [c.lin.weight.detach().clone().requires_grad_(True) for c in m.convs]
     bs = [c.bias.detach().clone().normal_(0, 0.1).requires_grad_(True) for c in m.convs]
     nb = torch.randn(64, device=DEV, requires_grad=True)
     g = graph
     _check(torch.ops.leakgnn.gnn_trunk.default,
-           (proj, nb, wts, bs, slot, sidx, nons, live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t,
-            g.pairs_t, g.rowptr_t, g.col_t, g.w_t, p, nm, seed))
+           (h_s, Wn, nb, wts, bs, slot, sidx, nons, live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t,
+            g.pairs_t, g.rowptr_t, g.col_t, g.w_t, p, nm, seed), {"bf16": B == 16})
     h = torch.randn((661, B, 64) if nm else (B, 661, 64), device=DEV).relu_().requires_grad_(True)
     mlp, nmlp = m.edge_head.mlp, m.noleak_head.mlp
     hw = [t.detach().clone().requires_grad_(True) for t in (mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
                                                               nmlp[0].weight, nmlp[0].bias, nmlp[3].weight,
                                                               nmlp[3].bias)]
-    _check(torch.ops.leakgnn.detector_heads.default, (h, *hw, inc.ends, inc.rowptr, inc.item, p, p, nm, True, seed))
+    _check(torch.ops.leakgnn.detector_heads.default, (h, *hw, inc.ends, inc.rowptr, inc.item, p, p, nm, True, seed),
+           {"bf16": B == 16})
 
 
 @pytest.mark.parametrize("fullgraph", [False, True])

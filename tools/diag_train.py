@@ -63,11 +63,6 @@ def main():
     s = t.abs().max().item()
     e = lambda x: (x.double().cpu() - t).abs().max().item() / s  # noqa: E731
     print(f"d h_s   scale {s:.2e}  hip {e(cap['h_s'].grad):.2e}  cpu32 {e(a32['h_s'].grad):.2e}  gpu32 {e(a32d['h_s'].grad):.2e}")
-    t = a64["z0"].grad.double().cpu()[:, sidx]
-    s = t.abs().max().item()
-    e = lambda x: (x.double().cpu() - t).abs().max().item() / s  # noqa: E731
-    print(f"d proj  scale {s:.2e}  hip {e(cap['proj'].grad):.2e}  cpu32 {e(a32['z0'].grad[:, sidx]):.2e}  "
-          f"gpu32 {e(a32d['z0'].grad[:, sidx]):.2e}")
     for n, p in m.named_parameters():
         t = g64[n].double()
         s = t.abs().max().item()
