@@ -233,7 +233,7 @@ def e2e_training(model, opt, label, B: int, steps: int, dev) -> dict:
     seg = torch.randn(B, 72, len(SENSORS), generator=gen).to(dev)
     tseg = time_features(B, 72, gen).to(dev)
     e2e = ResidualDetector(predictor, model).to(dev)
-    step = CapturedTrainStep(e2e, torch.nn.CrossEntropyLoss(), opt, (seg, tseg), label, clip=1.0, warmup=3)
+    step = CapturedTrainStep(e2e, torch.nn.CrossEntropyLoss(), opt, (seg, tseg), label, clip=None, warmup=3)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -280,12 +280,13 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
         sensors = pick_sensors(node_ids, 29, seed=0)
         torch.manual_seed(0)
         m = LeakDetector(inp, sensors, pipe_ids, sensor_hidden=D, node_hidden=D).to(dev).train()
-    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    from models.optim import ClipAdamW
+    opt = ClipAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)  # clip_grad_norm_(1.0) + AdamW
     gen = torch.Generator().manual_seed(99 + rank)
     r = torch.randn(B, 36, 29, generator=gen).to(dev)
     tf = time_features(B, 36, gen).to(dev)
     lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
-    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=1.0, warmup=3)
+    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
     for _ in range(warmup):
         step()
     if world > 1:
@@ -336,12 +337,13 @@ def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str
     torch.manual_seed(0)
     m = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
                      use_time=True, mlp_dtype=mlp_dtype).to(dev).train()
-    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    from models.optim import ClipAdamW
+    opt = ClipAdamW(m.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)  # clip_grad_norm_(1.0) + AdamW
     gen = torch.Generator().manual_seed(1234 + rank)
     r = torch.randn(B, 36, len(SENSORS), generator=gen).to(dev)
     tf = time_features(B, 36, gen).to(dev)
     lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
-    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=1.0, warmup=3)
+    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
     for _ in range(warmup):
         step()
     if world > 1:
@@ -503,9 +505,10 @@ def main() -> None:
     torch.manual_seed(0)
     model = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
                          use_time=True, mlp_dtype=args.dtype).to(dev).train()
-    # fused=True: one multi-tensor launch for the whole update (same AdamW math as the reference's);
-    # capturable=True: device-side step counters, so the update can live inside the step graph
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, fused=True, capturable=True)
+    # clip_grad_norm_(1.0) + AdamW(lr 1e-3, wd 1e-4) as ONE launch (models/optim.py: the same
+    # arithmetic as the reference's pair, device-side step counter so it lives in the step graph)
+    from models.optim import ClipAdamW
+    opt = ClipAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
     allreduce = GradAllReduce(model.parameters())
     N = len(model.node_names)
     E1 = int(model.edge_index_single.shape[1]) + N  # E' = E + N self loops
@@ -522,8 +525,7 @@ def main() -> None:
         opt.zero_grad(set_to_none=True)
         loss.backward()
         allreduce()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-        opt.step()
+        opt.step()  # clip_grad_norm_(1.0) + AdamW
         return loss
 
     for _ in range(args.warmup):
@@ -532,7 +534,7 @@ def main() -> None:
     if not args.eager:
         # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay)
         from models.graph_step import CapturedTrainStep
-        step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=1.0, warmup=3)
+        step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=None, warmup=3)
     timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "gcn_bwd_l0", "node_init", "gru_fwd", "gru_bwd", "edge_fwd",
                              "edge_bwd", "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)
@@ -600,7 +602,8 @@ def main() -> None:
         "config": {"workload": "L-TOWN-A detector training step (BASELINE configs[2])", "graph": "L-TOWN-A",
                    "nodes": N, "edge_columns": E1 - N, "pipes": P, "windows_per_rank": B,
                    "global_batch": B * world, "feat": D, "gnn_layers": 2, "parallelism": f"dp{world}",
-                   "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode",
+                   "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode (clip_grad_norm_ + AdamW in one launch, "
+                           "models/optim.py)",
                    "launch": "eager" if args.eager else "hipgraph (one replay per step, dropout re-drawn on device)"},
         "roofline": {"kernel": "lg_gcn_fwd_nm (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

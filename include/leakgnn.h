@@ -91,6 +91,20 @@ enum {
 int lg_abi_version(void);
 const char* lg_strerror(int code);
 
+/* Training-step tail: torch.nn.utils.clip_grad_norm_(params, max_norm) then
+ * torch.optim.AdamW.step() (reference train_detector.py:313-317), two launches.
+ *   table : int64 [T][4] (HOST array) device addresses of (param, grad, exp_avg, exp_avg_sq), fp32
+ *   sizes : int64 [T] (HOST array) element counts, T <= 48 (passed by value to the launches, so
+ *           captured launches need no host copy)
+ *   step  : device fp32 [2]: step[0] the AdamW step counter (incremented), step[1] scratch
+ *   max_norm <= 0: no clipping.  norm_out (device fp32, may be NULL): the pre-clip total norm.
+ *   workspace: lg_clip_adamw_workspace_bytes(sizes, T) bytes (per-slice fp64 partial norms).
+ * The norm is summed in fp64 in a fixed order (deterministic). */
+int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T);
+int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
+                  float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace,
+                  lg_stream_t stream);
+
 /* Kernel timing (bench.py; no reference counterpart — the reference has no kernels).
  * lg_timing_arm(slot): the NEXT library kernel launch on this host thread that is the main
  * kernel of an entry point (lg_gcn_fwd[_nm], lg_gcn_bwd[_nm], lg_edge_head_fwd/bwd,

@@ -137,3 +137,30 @@ def test_kernel_timer_times_the_kernel():
     assert 0.0 < ms <= a.elapsed_time(z) / 5
     from models import _native
     assert _native.load_library().lg_timing_disarm() == 0  # nothing left armed
+
+
+def test_clip_adamw_matches_torch():
+    """models/optim.py ClipAdamW == torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW
+    (fused) over three steps on the detector's parameter set: clipped gradients, the
+    returned total norm, and the updated parameters, to fp32 rounding (the norm is summed in
+    a different order)."""
+    from models.detector import LeakDetector
+    from models.optim import ClipAdamW
+    sensors, pipes = lta_ids()
+    torch.manual_seed(5)
+    ma = LeakDetector(LTA_INP, sensors, pipes).to(DEV)
+    mb = LeakDetector(LTA_INP, sensors, pipes).to(DEV)
+    mb.load_state_dict(ma.state_dict())
+    oa = torch.optim.AdamW(ma.parameters(), lr=1e-2, weight_decay=1e-2, fused=True)
+    ob = ClipAdamW(mb.parameters(), lr=1e-2, weight_decay=1e-2, max_norm=1.0)
+    for it in range(3):
+        for pa, pb in zip(ma.parameters(), mb.parameters()):
+            g = torch.randn_like(pa) * (0.05 if it == 1 else 1.0)  # step 1: under the clip threshold
+            pa.grad, pb.grad = g.clone(), g.clone()
+        na = torch.nn.utils.clip_grad_norm_(ma.parameters(), 1.0)
+        oa.step()
+        ob.step()
+        assert_close(ob.last_grad_norm[0], na, rtol=1e-6, what="total norm")
+        for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+            assert_close(pb.grad, pa.grad, rtol=1e-6, what=f"clipped grad {n}")
+            assert_close(pb, pa, rtol=1e-6, what=f"param {n} after step {it}")

@@ -150,3 +150,32 @@ def test_captured_step_two_ranks_equals_full_batch(tmp_path):
         step()
     for n, p in m.named_parameters():
         assert_close(got[n], p, rtol=2e-5, what=n)
+
+
+def test_captured_step_with_clip_adamw_matches_eager():
+    """The bench's step: ClipAdamW (clip_grad_norm_ + AdamW in one launch, device step
+    counter) inside the captured graph == the same optimizer stepped eagerly."""
+    from models.graph_step import CapturedTrainStep
+    from models.optim import ClipAdamW
+    r, tf, lab = _batch(6)
+    m1 = _model(0.0)
+    m2 = copy.deepcopy(m1)
+    o1 = ClipAdamW(m1.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
+    o2 = ClipAdamW(m2.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
+    step = CapturedTrainStep(m2, torch.nn.functional.cross_entropy, o2, (r, tf), lab, clip=None, warmup=3)
+
+    def eager():
+        o1.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.cross_entropy(m1(r, tf), lab)
+        loss.backward()
+        o1.step()
+        return loss
+    for _ in range(3):
+        eager()
+    for _ in range(4):
+        l1 = eager()
+        l2 = step()
+    torch.cuda.synchronize()
+    assert_close(l2, l1, rtol=1e-6, what="loss")
+    for (n, a), b in zip(m2.named_parameters(), m1.parameters()):
+        assert_close(a, b, rtol=1e-5, what=n)
