@@ -233,7 +233,7 @@ def e2e_training(model, opt, label, B: int, steps: int, dev) -> dict:
     seg = torch.randn(B, 72, len(SENSORS), generator=gen).to(dev)
     tseg = time_features(B, 72, gen).to(dev)
     e2e = ResidualDetector(predictor, model).to(dev)
-    step = CapturedTrainStep(e2e, torch.nn.CrossEntropyLoss(), opt, (seg, tseg), label, clip=None, warmup=3)
+    step = CapturedTrainStep(e2e, CrossEntropyLoss(), opt, (seg, tseg), label, clip=None, warmup=3)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -286,7 +286,7 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
     r = torch.randn(B, 36, 29, generator=gen).to(dev)
     tf = time_features(B, 36, gen).to(dev)
     lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
-    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
+    step = CapturedTrainStep(m, CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
     for _ in range(warmup):
         step()
     if world > 1:
@@ -324,6 +324,12 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
                                  "avg_launch_us": round(fwd_ms * 1e3, 2)}}
 
 
+def CrossEntropyLoss():
+    """nn.CrossEntropyLoss() on the fused HIP op (models/loss.py; same defaults)."""
+    from models.loss import CrossEntropyLoss as _CE
+    return _CE()
+
+
 def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str, batch: int) -> dict:
     """BASELINE configs[2] as written — "bf16 node-MLP on MFMA" (SURVEY §8 d C3: bf16 for the
     K5 GCN transforms and the K9 EdgeHead MLP, fp32 accumulate): the same L-TOWN-A training
@@ -343,7 +349,7 @@ def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str
     r = torch.randn(B, 36, len(SENSORS), generator=gen).to(dev)
     tf = time_features(B, 36, gen).to(dev)
     lab = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
-    step = CapturedTrainStep(m, torch.nn.CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
+    step = CapturedTrainStep(m, CrossEntropyLoss(), opt, (r, tf), lab, clip=None, warmup=3)
     for _ in range(warmup):
         step()
     if world > 1:
@@ -517,7 +523,7 @@ def main() -> None:
     residual = torch.randn(B, 36, len(SENSORS), generator=gen).to(dev)
     tfeat = time_features(B, 36, gen).to(dev)
     label = torch.randint(0, P + 1, (B,), generator=gen).to(dev)
-    loss_fn = torch.nn.CrossEntropyLoss()
+    loss_fn = CrossEntropyLoss()
 
     def step():
         logits = model(residual, tfeat)

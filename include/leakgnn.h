@@ -91,6 +91,20 @@ enum {
 int lg_abi_version(void);
 const char* lg_strerror(int code);
 
+/* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;
+ * reference train_detector.py:235, 311) over logits [B][C] (row stride ldx).
+ *   fwd: loss (device fp32 scalar), lse [B] (saved for the backward), rowloss [B] scratch;
+ *        counter: a device uint32 that is 0 at entry and left 0 (the last workgroup forms
+ *        the mean over rows in row order and re-arms it) — one per concurrently used stream.
+ *   bwd: dlogits[b][c] = grad_loss[0] / n * (exp(x - lse[b]) - [c == target[b]]), 0 for
+ *        ignored rows (row stride ldd).  Two launches for what torch runs as six. */
+int lg_cross_entropy_fwd(const float* logits, const int64_t* target, int64_t B, int64_t C, int64_t ldx,
+                         int64_t ignore_index, float* loss, float* lse, float* rowloss, unsigned* counter,
+                         lg_stream_t stream);
+int lg_cross_entropy_bwd(const float* logits, const int64_t* target, const float* lse, const float* grad_loss,
+                         int64_t B, int64_t C, int64_t ldx, int64_t ignore_index, float* dlogits, int64_t ldd,
+                         lg_stream_t stream);
+
 /* Training-step tail: torch.nn.utils.clip_grad_norm_(params, max_norm) then
  * torch.optim.AdamW.step() (reference train_detector.py:313-317), two launches.
  *   table : int64 [T][4] (HOST array) device addresses of (param, grad, exp_avg, exp_avg_sq), fp32

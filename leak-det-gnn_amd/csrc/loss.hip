@@ -1,0 +1,159 @@
+// The training loss (reference train_detector.py:235, 311: nn.CrossEntropyLoss(), mean
+// reduction, ignore_index -100) over the (B, P+1) logits, forward and backward.  torch runs
+// it as six launches (log_softmax, nll forward, two fills, nll backward, log_softmax
+// backward); here:
+//   forward : one wave per row: lse = max + log(sum exp(x - max)) (fp32, fixed lane order
+//             then a fixed shuffle tree), row loss = lse - x[target] -> lse[b], rowloss[b]
+//             and, by the LAST workgroup to finish (device-scope counter), the mean over the
+//             counted rows summed in row order (deterministic)
+//   backward: dx[b][c] = g / n * (exp(x - lse[b]) - [c == target[b]])   (0 for ignored rows)
+#include <algorithm>
+#include "common.h"
+
+namespace {
+
+constexpr int kCeWaves = 4;
+constexpr int kCeThreads = 64 * kCeWaves;
+constexpr int kCePer = 16;  // row elements per lane held in registers (C <= 1024)
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__global__ void __launch_bounds__(kCeThreads)
+k_ce_fwd(const float* __restrict__ x, const int64_t* __restrict__ target, int64_t B, int64_t C, int64_t ldx,
+         int64_t ignore, float* __restrict__ lse, float* __restrict__ rowloss, unsigned* __restrict__ done,
+         float* __restrict__ loss) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kCeWaves + w; b < B; b += static_cast<int64_t>(gridDim.x) * kCeWaves) {
+        const float* row = x + b * ldx;
+        float m = -__builtin_huge_valf(), s = 0.f;
+        if (C <= 64 * kCePer) {  // the whole row in registers: every load in flight at once
+            float v[kCePer];
+#pragma unroll
+            for (int k = 0; k < kCePer; ++k) {
+                const int64_t c = lane + 64 * k;
+                v[k] = c < C ? row[c] : -__builtin_huge_valf();
+            }
+#pragma unroll
+            for (int k = 0; k < kCePer; ++k) m = fmaxf(m, v[k]);
+            m = wave_max(m);
+#pragma unroll
+            for (int k = 0; k < kCePer; ++k) s += lane + 64 * k < C ? expf(v[k] - m) : 0.f;
+        } else {
+            for (int64_t c = lane; c < C; c += 64) m = fmaxf(m, row[c]);
+            m = wave_max(m);
+            for (int64_t c = lane; c < C; c += 64) s += expf(row[c] - m);
+        }
+        s = wave_sum(s);
+        const float l = m + logf(s);
+        if (lane == 0) {
+            const int64_t t = target[b];
+            lse[b] = l;
+            // a target outside [0, C) (torch raises) poisons the loss with NaN, never reads out of bounds
+            rowloss[b] = t == ignore ? 0.f : (t >= 0 && t < C ? l - row[t] : __builtin_nanf(""));
+        }
+    }
+    // last workgroup: the mean, rows in order.  Release: every storing lane's device-scope
+    // fence, the barrier, then the counter (a vector atomic at agent scope); acquire: the
+    // last workgroup's device-scope fence before it reads the other workgroups' rows.
+    __shared__ unsigned last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (w == 0) {
+        float acc = 0.f, cnt = 0.f;
+        for (int64_t b0 = 0; b0 < B; b0 += 64) {
+            const int64_t b = b0 + lane;
+            float v = 0.f, c = 0.f;
+            if (b < B) {
+                v = rowloss[b];
+                c = target[b] == ignore ? 0.f : 1.f;
+            }
+            acc += wave_sum(v);
+            cnt += wave_sum(c);
+        }
+        if (lane == 0) {
+            loss[0] = acc / cnt;  // NaN when every row is ignored, as torch
+            done[0] = 0u;         // re-armed for the next call (and the next graph replay)
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kCeThreads)
+k_ce_bwd(const float* __restrict__ x, const int64_t* __restrict__ target, const float* __restrict__ lse,
+         const float* __restrict__ gout, int64_t B, int64_t C, int64_t ldx, int64_t ignore, float* __restrict__ dx,
+         int64_t ldd) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // n = counted rows (every workgroup counts them the same way)
+    float cnt = 0.f;
+    for (int64_t b0 = 0; b0 < B; b0 += 64) {
+        const int64_t b = b0 + lane;
+        cnt += wave_sum((b < B && target[b] != ignore) ? 1.f : 0.f);
+    }
+    const float g = gout[0] / cnt;
+    for (int64_t b = static_cast<int64_t>(blockIdx.x) * kCeWaves + w; b < B; b += static_cast<int64_t>(gridDim.x) * kCeWaves) {
+        const float* row = x + b * ldx;
+        float* drow = dx + b * ldd;
+        const int64_t t = target[b];
+        const float l = lse[b];
+        const float gi = t == ignore ? 0.f : g;
+        if (C <= 64 * kCePer) {
+            float v[kCePer];
+#pragma unroll
+            for (int k = 0; k < kCePer; ++k) {
+                const int64_t c = lane + 64 * k;
+                v[k] = c < C ? row[c] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < kCePer; ++k) {
+                const int64_t c = lane + 64 * k;
+                if (c < C) drow[c] = gi * (expf(v[k] - l) - (c == t ? 1.f : 0.f));
+            }
+        } else {
+            for (int64_t c = lane; c < C; c += 64) drow[c] = gi * (expf(row[c] - l) - (c == t ? 1.f : 0.f));
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int lg_cross_entropy_fwd(const float* logits, const int64_t* target, int64_t B, int64_t C, int64_t ldx,
+                                    int64_t ignore_index, float* loss, float* lse, float* rowloss, unsigned* counter,
+                                    lg_stream_t stream) {
+    if (B < 0 || C <= 0 || ldx < C || !loss || !counter) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    if (B == 0) {
+        const float nan = __builtin_nanf("");
+        return hipMemcpyAsync(loss, &nan, sizeof(float), hipMemcpyHostToDevice, s) == hipSuccess ? LG_OK : LG_EHIP;
+    }
+    if (!logits || !target || !lse || !rowloss) return LG_EINVAL;
+    const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, 4 * lg_num_cus()));
+    lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss, counter, loss);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_cross_entropy_bwd(const float* logits, const int64_t* target, const float* lse,
+                                    const float* grad_loss, int64_t B, int64_t C, int64_t ldx, int64_t ignore_index,
+                                    float* dlogits, int64_t ldd, lg_stream_t stream) {
+    if (B < 0 || C <= 0 || ldx < C || ldd < C || !grad_loss) return LG_EINVAL;
+    if (B == 0) return LG_OK;
+    if (!logits || !target || !lse || !dlogits) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, 4 * lg_num_cus()));
+    lg_launch(k_ce_bwd, grid, kCeThreads, 0, s, logits, target, lse, grad_loss, B, C, ldx, ignore_index, dlogits, ldd);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}

@@ -37,6 +37,8 @@ _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint3
 SIGNATURES = {
     "lg_abi_version": (_i32, []),
     "lg_strerror": (ctypes.c_char_p, [_i32]),
+    "lg_cross_entropy_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
+    "lg_cross_entropy_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_clip_adamw_workspace_bytes": (_i64, [_p, _i32]),
     "lg_clip_adamw": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _p]),
     "lg_timing_arm": (_i32, [_i32]),

@@ -164,3 +164,29 @@ def test_clip_adamw_matches_torch():
         for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
             assert_close(pb.grad, pa.grad, rtol=1e-6, what=f"clipped grad {n}")
             assert_close(pb, pa, rtol=1e-6, what=f"param {n} after step {it}")
+
+
+def test_cross_entropy_matches_torch():
+    """models/loss.py CrossEntropyLoss (two HIP launches) == torch's nn.CrossEntropyLoss:
+    loss and dlogits at the detector's shape, with ignored rows, and the all-ignored NaN;
+    a non-default configuration falls through to torch."""
+    from models.loss import CrossEntropyLoss
+    torch.manual_seed(3)
+    for B, C, n_ign in ((256, 765, 0), (37, 100, 5), (4, 3, 4)):
+        x = torch.randn(B, C, device=DEV) * 3
+        t = torch.randint(0, C, (B,), device=DEV)
+        t[:n_ign] = -100
+        xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        la = torch.nn.CrossEntropyLoss()(xa, t)
+        lb = CrossEntropyLoss()(xb, t)
+        if n_ign == B:
+            assert torch.isnan(la) and torch.isnan(lb)
+            continue
+        la.backward()
+        lb.backward()
+        assert_close(lb, la, rtol=1e-6, what=f"loss B={B}")
+        assert_close(xb.grad, xa.grad, rtol=1e-5, what=f"dlogits B={B}")
+    x = torch.randn(8, 5, device=DEV)
+    t = torch.randint(0, 5, (8,), device=DEV)
+    assert_close(CrossEntropyLoss(label_smoothing=0.1)(x, t), torch.nn.CrossEntropyLoss(label_smoothing=0.1)(x, t),
+                 rtol=1e-6, what="fallback")

@@ -153,8 +153,9 @@ def test_captured_step_two_ranks_equals_full_batch(tmp_path):
 
 
 def test_captured_step_with_clip_adamw_matches_eager():
-    """The bench's step: ClipAdamW (clip_grad_norm_ + AdamW in one launch, device step
-    counter) inside the captured graph == the same optimizer stepped eagerly."""
+    """The bench's step: the fused cross-entropy and ClipAdamW (clip_grad_norm_ + AdamW,
+    device step counter) inside the captured graph == the same loss and optimizer stepped
+    eagerly (each is checked against torch's in test_gpu_library.py)."""
     from models.graph_step import CapturedTrainStep
     from models.optim import ClipAdamW
     r, tf, lab = _batch(6)
@@ -162,11 +163,13 @@ def test_captured_step_with_clip_adamw_matches_eager():
     m2 = copy.deepcopy(m1)
     o1 = ClipAdamW(m1.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
     o2 = ClipAdamW(m2.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
-    step = CapturedTrainStep(m2, torch.nn.functional.cross_entropy, o2, (r, tf), lab, clip=None, warmup=3)
+    from models.loss import CrossEntropyLoss
+    ce = CrossEntropyLoss()  # the bench's loss: the fused HIP op, inside the graph too
+    step = CapturedTrainStep(m2, ce, o2, (r, tf), lab, clip=None, warmup=3)
 
     def eager():
         o1.zero_grad(set_to_none=True)
-        loss = torch.nn.functional.cross_entropy(m1(r, tf), lab)
+        loss = ce(m1(r, tf), lab)
         loss.backward()
         o1.step()
         return loss
