@@ -17,7 +17,7 @@
 namespace {
 
 constexpr int kOptThreads = 256;
-constexpr int kOptChunk = 2048;      // elements per workgroup
+constexpr int kOptChunk = 512;       // elements per workgroup (two per thread: one round trip)
 constexpr int kOptMaxTensors = 48;   // by-value kernel argument: a captured launch needs no host copy
 
 struct AdamTensors {
