@@ -27,6 +27,7 @@
 #include <algorithm>
 #include "common.h"
 #include "reduce.h"
+#include "split_bf16.h"
 
 namespace {
 
@@ -93,21 +94,22 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __r
 }
 
 // ------------------------------------------------------------------ forward
-// One wave per 16-row gate tile: 3 * H/16 waves per 16 sequences (12 at H = 64), so each
-// wave issues only 3 + H/4 MFMAs per step (x part; h part split over two accumulator
-// chains) and ~5 waves share a SIMD to hide the recurrence's latency.  Wave (g, u),
-// g in {r, z, n}, u = unit group: the r and z waves post sigma(.) tiles to LDS; the n
-// wave u keeps W_in x + b_in and W_hn h + b_hn, forms n = tanh(.), h' = (1-z) n + z h
-// for units [16u, 16u+16) and posts h' to LDS, from where every wave reads the next
-// step's B operand.  Exchanges use lane-major slots (the reader lane is the writer
-// lane), so every LDS access is a conflict-free b128.  Two barriers per step.
-// Measured and dropped (MI355X, B = 256): the recurrent product on split-bf16
-// v_mfma_f32_16x16x32_bf16 (K permuted so each lane's two lane-major h tiles form its B
-// fragment, no extra exchange) ran 158 -> 165 us and doubled the W_ih gradient error —
-// the step is bound by its barriers / transcendentals / LDS round trip, not MFMA issue.
-// Also dropped: one wave per unit group owning all three gates (one barrier per step, no
-// sigma exchange) — 148 vs 142 us with libm math, 114 vs 116 us with the fast gate math;
-// PMC (profiles/pmc/r02m_pmc_summary.txt): 51% of its wave time in dependency stalls.
+// One wave per 16-row gate tile: 3 * H/16 waves per 16 sequences (12 at H = 64).  Wave
+// (g, u), g in {r, z, n}, u = unit group: the r and z waves post sigma(.) tiles to LDS; the
+// n wave u keeps W_in x + b_in and W_hn h + b_hn, forms n = tanh(.), h' = (1-z) n + z h for
+// units [16u, 16u+16) (h of its own units stays in registers, fp32) and posts h' to LDS,
+// from where every wave reads the next step's B operand.  Two barriers per step.
+// The recurrent product W_hh h runs on v_mfma_f32_16x16x32_bf16 with 3-way split operands
+// (split_bf16.h: six products, fp32-level accuracy): 12 MFMAs of 16 cycles per wave and
+// step instead of 16 v_mfma_f32_16x16x4_f32 of 32.  W_hh is split once into registers; h'
+// is split ONCE, by the n wave that produces it (4 values per lane), and posted as bf16
+// parts.  The K order of chunk c is permuted, k = 8q + p <-> unit 16(2c + p/4) + 4q + p%4,
+// so a lane's B fragment is exactly the lane's own outputs of n waves 2c and 2c+1: the
+// exchange is lane-major (reader lane == writer lane), one b128 read per chunk and part.
+// The x part (K = I <= 12) stays on v_mfma_f32_16x16x4_f32 (exact, off the critical path).
+// Measured and dropped (MI355X, B = 256): one wave per unit group owning all three gates
+// (one barrier per step, no sigma exchange) — 114 vs 116 us with fp32 MFMA; PMC
+// (profiles/pmc/r02m_pmc_summary.txt): 51% of its wave time in dependency stalls.
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
 template <int H, bool UT, bool SAVE>
 __global__ void __launch_bounds__(12 * H) __attribute__((amdgpu_waves_per_eu(6, 8)))  // 2 workgroups / CU
@@ -115,10 +117,11 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
           const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
           float* __restrict__ hs, float* __restrict__ gates, float* __restrict__ hout, uint32_t Nseq, int L, int S,
           lg_fastdiv fdS) {
-    constexpr int NU = H / 16, KH = H / 4, I = UT ? 10 : 1;
-    __shared__ __attribute__((aligned(16))) float xs[kLC * TS * XR];
-    __shared__ __attribute__((aligned(16))) f32x4 grz[2][NU][64];  // [r|z][unit group][lane]: sigma tiles
-    __shared__ __attribute__((aligned(16))) f32x4 hb[NU][64];      // h_t tiles, lane-major
+    constexpr int NU = H / 16, NC = H / 32, I = UT ? 10 : 1;
+    constexpr int LC = H == 64 ? kLC : 30;  // H = 32: four workgroups per CU fit in LDS
+    __shared__ __attribute__((aligned(16))) float xs[LC * TS * XR];
+    __shared__ __attribute__((aligned(16))) f32x4 grz[2][NU][64];   // [r|z][unit group][lane]: sigma tiles
+    __shared__ __attribute__((aligned(16))) lg_u32x4 hbs[3][NC][64];  // h_t split parts: [part][chunk][lane]
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = w / NU, u = w % NU;  // gate (0 r, 1 z, 2 n), unit group
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
@@ -126,61 +129,73 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     const bool valid = seq < Nseq;
 
     const int row = g * H + 16 * u + j;  // A-operand row of this lane
-    float ah[KH], ax[3];
+    lg_bf16x8 ah[NC][3];
 #pragma unroll
-    for (int ks = 0; ks < KH; ++ks) ah[ks] = Whh[row * H + fk(ks, q)];
+    for (int c = 0; c < NC; ++c) {
+        f32x4 v0, v1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            v0[p] = Whh[row * H + 32 * c + 4 * q + p];
+            v1[p] = Whh[row * H + 32 * c + 16 + 4 * q + p];
+        }
+        split3_x8(v0, v1, ah[c][0], ah[c][1], ah[c][2]);
+    }
+    // x-side A operand; column 10 meets x's constant-1 column: the x-side bias (r, z: both
+    // biases) rides in the x product, exactly (x = 1)
+    float ax[3];
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
         const int k = 4 * kx + q;
-        ax[kx] = k < I ? Wih[row * I + k] : 0.f;
+        ax[kx] = k < I ? Wih[row * I + k] : (k == 10 ? (g < 2 ? bih[row] + bhh[row] : bih[row]) : 0.f);
     }
-    f32x4 bx, bh;  // x-side / h-side biases of rows 4q+reg (r, z: both folded into bx)
+    __shared__ __attribute__((aligned(16))) float bhn[H];  // b_hn (n waves add it to W_hn h)
+    for (int i = threadIdx.x; i < H; i += blockDim.x) bhn[i] = bhh[2 * H + i];
+    f32x4 hcur = zero4();  // n waves: h of units 16u + 4q + reg, fp32
+    if (g == 2) {  // h_{-1} = 0 (published by the first staging barrier)
+        lg_u32x2* dst = reinterpret_cast<lg_u32x2*>(&hbs[0][u >> 1][lane]) + (u & 1);
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        const int c = g * H + 16 * u + 4 * q + reg;
-        bx[reg] = g < 2 ? bih[c] + bhh[c] : bih[c];
-        bh[reg] = g < 2 ? 0.f : bhh[c];
+        for (int p = 0; p < 3; ++p) dst[2 * NC * 64 * p] = lg_u32x2{0u, 0u};
     }
-    float hf[KH];
-#pragma unroll
-    for (int i = 0; i < KH; ++i) hf[i] = 0.f;
-    if (g == 2) hb[u][lane] = zero4();  // h_{-1}; each n wave reads its own slot back as h_{t-1}
 
-    for (int t0 = 0; t0 < L; t0 += kLC) {
-        const int nt = min(kLC, L - t0);
+    for (int t0 = 0; t0 < L; t0 += LC) {
+        const int nt = min(LC, L - t0);
         __syncthreads();
         stage_x<UT, 2>(xs, resid, tfeat, t0, nt, seq0, Nseq, L, S, fdS);
         __syncthreads();
         for (int tt = 0; tt < nt; ++tt) {
             const int t = t0 + tt;
-            f32x4 a0 = bx, a1 = bh, a2 = zero4();  // a0: x part, a1 + a2: h part
+            f32x4 a0 = zero4();  // x part
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) a0 = mfma(ax[kx], xs[(tt * TS + j) * XR + 4 * kx + q], a0);
+            // h part: B fragments read just before their chunk's MFMAs (register budget of
+            // two workgroups per CU)
+            f32x4 hp = zero4();
 #pragma unroll
-            for (int ks = 0; ks < KH; ks += 2) {
-                a1 = mfma(ah[ks], hf[ks], a1);
-                a2 = mfma(ah[ks + 1], hf[ks + 1], a2);
+            for (int c = 0; c < NC; ++c) {
+                lg_bf16x8 hf[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) hf[p] = __builtin_bit_cast(lg_bf16x8, hbs[p][c][lane]);
+                hp = mfma_split(ah[c], hf, hp);
             }
-            const f32x4 hp = a1 + a2;
             if (g < 2) {
                 f32x4 sg;
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) sg[reg] = sigm(a0[reg] + hp[reg]);
                 grz[g][u][lane] = sg;
             }
-            __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hb
+            __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hbs
             if (g == 2) {
-                const f32x4 r = grz[0][u][lane], z = grz[1][u][lane], hprev = hb[u][lane];
-                f32x4 n, hn;
+                hp += *reinterpret_cast<const f32x4*>(&bhn[16 * u + 4 * q]);
+                const f32x4 r = grz[0][u][lane], z = grz[1][u][lane];
+                f32x4 n;
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {
                     n[reg] = gru_tanh(a0[reg] + r[reg] * hp[reg]);
-                    hn[reg] = (1.f - z[reg]) * n[reg] + z[reg] * hprev[reg];
+                    hcur[reg] = (1.f - z[reg]) * n[reg] + z[reg] * hcur[reg];
                 }
-                hb[u][lane] = hn;
                 if (valid) {
                     const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
-                    if (hs) st4(hs + rw * H + 16 * u + 4 * q, hn);
+                    if (hs) st4(hs + rw * H + 16 * u + 4 * q, hcur);
                     if constexpr (SAVE) {
                         float* gp = gates + rw * 4 * H + 16 * u + 4 * q;
                         st4(gp, r);
@@ -189,17 +204,17 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                         st4(gp + 3 * H, hp);
                     }
                 }
+                lg_u32x2 f0, f1, f2;
+                split3_x4(hcur, f0, f1, f2);
+                lg_u32x2* dst = reinterpret_cast<lg_u32x2*>(&hbs[0][u >> 1][lane]) + (u & 1);
+                dst[0] = f0;
+                dst[2 * NC * 64] = f1;
+                dst[4 * NC * 64] = f2;
             }
             __syncthreads();  // (B) h_t posted; sigma slots free again
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                const f32x4 v = hb[a][lane];
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) hf[4 * a + reg] = v[reg];
-            }
         }
     }
-    if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hb[u][lane]);
+    if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hcur);
 }
 
 // ------------------------------------------------------------------ backward
