@@ -414,7 +414,261 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     }
 }
 
+// ------------------------------------------------------------------ backward, split-bf16
+// The training step's backward (no dx: the residual is data).  One workgroup = 32
+// sequences x 2 H/16 waves: wave (w, s) owns hidden units [16w, 16w+16) of sequences
+// [16s, 16s+16).  Per step t (descending), one barrier:
+//   1. elementwise gate backward for the lane's 4 units (gates, h_{t-1} and x_t prefetched
+//      two steps ahead from global); dG = (dG_r, dG_z, dG_hn, dG_in), h_{t-1} and x_t are
+//      split into three bf16 parts (split_bf16.h) and posted row-major [seq][column] to a
+//      double-buffered LDS image
+//   2. dh_{t-1} = d z + W_hh^T dG_h on v_mfma_f32_16x16x32_bf16 (K = the 3H gate rows read
+//      straight from the [seq][rho] rows: one b128 per chunk and part), W_hh^T split once into
+//      registers
+//   3. dW_hh += dG_h^T h_{t-1} and dW_ih += dG_i^T x_t over the 32 sequences (K = 32: one
+//      16x16x32 per tile and product); both operands come from the row-major images through
+//      ds_read_b64_tr_b16 (transposing 4 x 16 blocks), wave (w, s) owning the dW_hh column
+//      tiles of its half
+// Six products per MFMA operand pair keep fp32-level accuracy.  MFMA cycles per wave and step:
+// 36 x 16 (dh) + 36-48 x 16 (dW) against 108 x 32 for the fp32 v_mfma_f32_16x16x4_f32 kernel
+// above, which stays for the dx variant.
+constexpr int TS2 = 32;  // sequences per workgroup
+template <int H>
+struct GB2 {
+    static constexpr int NW = H / 16;         // unit groups
+    static constexpr int NWAVE = 2 * NW;      // x 2 sequence halves
+    static constexpr int NTH = 64 * NWAVE;
+    static constexpr int DGS = 4 * H + 16;    // dG row (bf16): [r | z | hn | in], 8 dwords mod 64: conflict-free
+    static constexpr int HLS = H + 16;        // h row (bf16)
+    static constexpr int XLS = 16;            // x row (bf16): 16 columns (I <= 10, col 10 = 1)
+    static constexpr int NCH = 3 * H / 32;    // dh contraction chunks
+    static constexpr int NTS = NW / 2;        // dW_hh column tiles per wave
+};
+
+__device__ __forceinline__ void split3_1(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+    const uint32_t a = pk_bf16(x, 0.f);
+    const float r = x - bf_lo(a);
+    const uint32_t b = pk_bf16(r, 0.f);
+    const uint32_t c = pk_bf16(r - bf_lo(b), 0.f);
+    p0 = static_cast<uint16_t>(a);
+    p1 = static_cast<uint16_t>(b);
+    p2 = static_cast<uint16_t>(c);
+}
+
+template <int H, bool UT>
+__global__ void __launch_bounds__(GB2<H>::NTH)
+k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Whh,
+           const float* __restrict__ hs, const float* __restrict__ gates, const float* __restrict__ dhL,
+           float* __restrict__ slab, uint32_t Nseq, int L, int S, lg_fastdiv fdS) {
+    using G = GB2<H>;
+    constexpr int I = UT ? 10 : 1, G3 = 3 * H;
+    constexpr int SLAB = G3 * H + G3 * I + 2 * G3;
+    constexpr int XPT = TS2 * 16 / G::NTH;  // x values staged per thread and step
+    __shared__ __attribute__((aligned(16))) uint16_t dgs[2][3][TS2][G::DGS];
+    __shared__ __attribute__((aligned(16))) uint16_t hls[2][3][TS2][G::HLS];
+    __shared__ __attribute__((aligned(16))) uint16_t xls[2][3][TS2][G::XLS];
+    __shared__ __attribute__((aligned(16))) float dbh[H];
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = wid % G::NW, sh = wid / G::NW;
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int sl = 16 * sh + j;  // local sequence of this lane (elementwise, dh)
+    const uint32_t seq0 = blockIdx.x * TS2, seq = seq0 + sl;
+    const bool valid = seq < Nseq;
+    const uint32_t seqc = valid ? seq : 0u;
+    const int u0 = 16 * w + 4 * q;  // this lane's 4 units
+
+    // W_hh^T A fragments: row = unit 16w + j, k = gate row 32c + 8q + p
+    lg_bf16x8 adh[G::NCH][3];
+#pragma unroll
+    for (int c = 0; c < G::NCH; ++c) {
+        f32x4 v0, v1;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            v0[p] = Whh[(32 * c + 8 * q + p) * H + 16 * w + j];
+            v1[p] = Whh[(32 * c + 8 * q + 4 + p) * H + 16 * w + j];
+        }
+        split3_x8(v0, v1, adh[c][0], adh[c][1], adh[c][2]);
+    }
+
+    auto load_g = [&](int t, f32x4 (&g)[4]) {
+        const float* p = gates + (static_cast<int64_t>(t) * Nseq + seqc) * 4 * H + u0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] = (valid && t >= 0) ? ld4(p + k * H) : zero4();
+    };
+    auto load_h = [&](int t) -> f32x4 {  // h_t of this lane's units (zero for t < 0 / padded)
+        return (valid && t >= 0) ? ld4(hs + (static_cast<int64_t>(t) * Nseq + seqc) * H + u0) : zero4();
+    };
+    auto load_x = [&](int t, float (&x)[XPT]) {
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) {
+            const int e = threadIdx.x + i * G::NTH, xs = e >> 4, k = e & 15;
+            const uint32_t sg = seq0 + xs;
+            float v = 0.f;
+            if (sg < Nseq && t >= 0) {
+                const uint32_t b = lg_div(sg, fdS), s = sg - b * fdS.d;
+                const int64_t row = static_cast<int64_t>(b) * L + t;
+                if (k == 0) v = resid[row * S + s];
+                else if (UT && k <= 9) v = tfeat[row * 9 + (k - 1)];
+                else if (k == 10) v = 1.f;
+            }
+            x[i] = v;
+        }
+    };
+
+    f32x4 dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + u0) : zero4();
+    f32x4 dwh[3][G::NTS], dwx[2], dbhn = zero4();
+#pragma unroll
+    for (int gi = 0; gi < 3; ++gi)
+#pragma unroll
+        for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = zero4();
+    dwx[0] = dwx[1] = zero4();
+
+    f32x4 g_cur[4], g_n1[4], h_cur, h_n1;
+    float x_cur[XPT], x_n1[XPT];
+    load_g(L - 1, g_cur);
+    load_g(L - 2, g_n1);
+    h_cur = load_h(L - 2);
+    h_n1 = load_h(L - 3);
+    load_x(L - 1, x_cur);
+    load_x(L - 2, x_n1);
+
+    for (int t = L - 1; t >= 0; --t) {
+        const int bf = t & 1;
+        // (1) elementwise gate backward (h_cur = h_{t-1})
+        {
+            const f32x4 r = g_cur[0], z = g_cur[1], n = g_cur[2], hnp = g_cur[3], hp = h_cur;
+            f32x4 gr, gz, ghn, gin, dhp;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const float d = dh[reg];
+                const float dn = d * (1.f - z[reg]);
+                const float dzv = d * (hp[reg] - n[reg]);
+                dhp[reg] = d * z[reg];
+                const float dnp = dn * (1.f - n[reg] * n[reg]);
+                gin[reg] = dnp;
+                ghn[reg] = dnp * r[reg];
+                gr[reg] = dnp * hnp[reg] * r[reg] * (1.f - r[reg]);
+                gz[reg] = dzv * z[reg] * (1.f - z[reg]);
+            }
+            dbhn += ghn;
+            dh = dhp;
+            const f32x4 blk[4] = {gr, gz, ghn, gin};
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                lg_u32x2 f0, f1, f2;
+                split3_x4(blk[b], f0, f1, f2);
+                *reinterpret_cast<lg_u32x2*>(&dgs[bf][0][sl][b * H + u0]) = f0;
+                *reinterpret_cast<lg_u32x2*>(&dgs[bf][1][sl][b * H + u0]) = f1;
+                *reinterpret_cast<lg_u32x2*>(&dgs[bf][2][sl][b * H + u0]) = f2;
+            }
+            lg_u32x2 f0, f1, f2;
+            split3_x4(hp, f0, f1, f2);
+            *reinterpret_cast<lg_u32x2*>(&hls[bf][0][sl][u0]) = f0;
+            *reinterpret_cast<lg_u32x2*>(&hls[bf][1][sl][u0]) = f1;
+            *reinterpret_cast<lg_u32x2*>(&hls[bf][2][sl][u0]) = f2;
+#pragma unroll
+            for (int i = 0; i < XPT; ++i) {
+                const int e = threadIdx.x + i * G::NTH;
+                uint16_t p0, p1, p2;
+                split3_1(x_cur[i], p0, p1, p2);
+                xls[bf][0][e >> 4][e & 15] = p0;
+                xls[bf][1][e >> 4][e & 15] = p1;
+                xls[bf][2][e >> 4][e & 15] = p2;
+            }
+        }
+        // prefetch: step t-2's gates / x and h_{t-3}
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g_cur[k] = g_n1[k];
+        load_g(t - 2, g_n1);
+        h_cur = h_n1;
+        h_n1 = load_h(t - 3);
+#pragma unroll
+        for (int i = 0; i < XPT; ++i) x_cur[i] = x_n1[i];
+        load_x(t - 2, x_n1);
+        // dgs/hls/xls[bf] complete.  Buffer bf was last read at step t+2, which every wave
+        // finished before arriving at step t+1's barrier: one barrier per step suffices.
+        __syncthreads();
+
+        // (2) dh_{t-1} = d z + W_hh^T dG_h: two accumulator chains
+        {
+            f32x4 acc[2] = {zero4(), zero4()};
+#pragma unroll
+            for (int c = 0; c < G::NCH; ++c) {
+                lg_bf16x8 b[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) b[p] = lds_frag_row(&dgs[bf][p][sl][32 * c + 8 * q]);
+                acc[c & 1] = mfma_split(adh[c], b, acc[c & 1]);
+            }
+            dh += acc[0] + acc[1];
+        }
+        // (3) dW over the 32 sequences: A = dG^T tiles (rows = gate rows 16w.., K = seq),
+        // B = h_{t-1} / x_t (K = seq, columns = units / x columns)
+        {
+            const int tr = 8 * q + (j >> 2), tc = 4 * (j & 3);  // tr16 addressing of this lane
+            lg_bf16x8 bh[G::NTS][3], bx[3];
+#pragma unroll
+            for (int n = 0; n < G::NTS; ++n)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bh[n][p] = lds_frag_tr16(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
+                                             &hls[bf][p][tr + 4][16 * (sh * G::NTS + n) + tc]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bx[p] = lds_frag_tr16(&xls[bf][p][tr][tc], &xls[bf][p][tr + 4][tc]);
+#pragma unroll
+            for (int gi = 0; gi < 3; ++gi) {
+                lg_bf16x8 a[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 4][gi * H + 16 * w + tc]);
+#pragma unroll
+                for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mfma_split(a, bh[n], dwh[gi][n]);
+                if (sh == 0 && gi < 2) dwx[gi] = mfma_split(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
+            }
+            if (sh == 1) {  // n gate's input side: dG_in
+                lg_bf16x8 a[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 4][3 * H + 16 * w + tc]);
+                dwx[0] = mfma_split(a, bx, dwx[0]);
+            }
+        }
+    }
+
+    // per-workgroup slab (the layout of k_gru_bwd): C rows = gate rows 16w + 4q + reg, columns j
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+    float* oWhh = out;
+    float* oWih = out + G3 * H;
+    float* obih = oWih + G3 * I;
+    float* obhh = obih + G3;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi)
+#pragma unroll
+            for (int n = 0; n < G::NTS; ++n)
+                oWhh[(gi * H + u0 + reg) * H + 16 * (sh * G::NTS + n) + j] = dwh[gi][n][reg];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            if (sh == 1 && x == 1) break;
+            const int gi = sh == 0 ? x : 2;
+            const int g = gi * H + u0 + reg;
+            if (j < I) oWih[g * I + j] = dwx[x][reg];
+            if (j == 10) obih[g] = dwx[x][reg];            // constant-1 column: sum of dG_i
+            if (j == 10 && gi < 2) obhh[g] = dwx[x][reg];  // r, z: dG_h == dG_i
+        }
+    }
+    // db_hh(n) = sum over sequences of dG_hn: 16 lanes, then the two sequence halves
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) dbhn[reg] += __shfl_xor(dbhn[reg], off);
+    if (sh == 1 && j == 0) st4(&dbh[u0], dbhn);
+    __syncthreads();
+    if (sh == 0 && j == 0) st4(obhh + 2 * H + u0, dbhn + ld4(&dbh[u0]));
+}
+
 inline int64_t nblocks_seq(int64_t nseq) { return (nseq + TS - 1) / TS; }
+inline int64_t nblocks_seq2(int64_t nseq) { return (nseq + TS2 - 1) / TS2; }
 
 template <int H>
 int launch_fwd(bool ut, bool save, const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
@@ -446,12 +700,16 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
 #define LG_GRU_BWD(UT, DX)                                                                                       \
     lg_launch(k_gru_bwd<H, UT, DX>, grid, 4 * H, 0, s, residual, tfeat, w_ih, w_hh, h_seq, gates, dh_last, dx, slab,   \
                                                  Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+#define LG_GRU_BWD2(UT)                                                                                          \
+    lg_launch(k_gru_bwd2<H, UT>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual, tfeat,  \
+              w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
     if (ut) {
-        if (need_dx) LG_GRU_BWD(true, true); else LG_GRU_BWD(true, false);
+        if (need_dx) LG_GRU_BWD(true, true); else LG_GRU_BWD2(true);
     } else {
-        if (need_dx) LG_GRU_BWD(false, true); else LG_GRU_BWD(false, false);
+        if (need_dx) LG_GRU_BWD(false, true); else LG_GRU_BWD2(false);
     }
 #undef LG_GRU_BWD
+#undef LG_GRU_BWD2
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
@@ -493,7 +751,8 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
         !workspace || (I == 10 && !tfeat))
         return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
-    const int nb = static_cast<int>(std::max<int64_t>(1, nblocks_seq(B * S)));
+    // slabs written: one per workgroup (16 sequences with dx, 32 without)
+    const int nb = static_cast<int>(std::max<int64_t>(1, dx ? nblocks_seq(B * S) : nblocks_seq2(B * S)));
     float* slab = static_cast<float*>(workspace);
     const int64_t G3 = 3 * H, len = G3 * H + G3 * I + 2 * G3;
     if (B == 0) {

@@ -558,33 +558,38 @@ def test_full_size_properties_c5():
     assert torch.equal(k1, k2)
 
 
-@pytest.mark.parametrize("use_time", [True, False])
+@pytest.mark.parametrize("use_time,dx,H", [(True, True, 64), (False, True, 64), (True, False, 64),
+                                             (False, False, 64), (True, False, 32)])
 @pytest.mark.parametrize("B", [5, 64])
-def test_gru_encoder_vs_torch_cpu(use_time, B):
-    """Fused HIP GRU vs nn.GRU on the CPU (the reference's own op), fwd h_L and all grads."""
+def test_gru_encoder_vs_torch_cpu(use_time, dx, H, B):
+    """Fused HIP GRU vs nn.GRU on the CPU (the reference's own op), fwd h_L and all grads.
+    dx=False is the detector's training case (the residual is data): the split-bf16
+    backward k_gru_bwd2 (32 sequences per workgroup; B = 5 leaves a ragged last one);
+    dx=True runs the fp32 kernel that also writes d residual / d tfeat."""
     from models.detector import SharedSensorGRUEncoder
     from oracle.detector_ref import _GRUEncoder
     torch.manual_seed(B)
-    ref = _GRUEncoder(64, use_time=use_time)
+    ref = _GRUEncoder(H, use_time=use_time)
     with torch.no_grad():
         for p in ref.parameters():
             p.uniform_(-0.3, 0.3)
-    enc = SharedSensorGRUEncoder(hidden_size=64, use_time=use_time)
+    enc = SharedSensorGRUEncoder(hidden_size=H, use_time=use_time)
     enc.gru.load_state_dict(ref.gru.state_dict())
     enc = enc.to(DEV)
     gen = torch.Generator().manual_seed(3)
     r = torch.randn(B, 36, 29, generator=gen)
     tf = torch.randn(B, 36, 9, generator=gen)
-    gy = torch.randn(B, 29, 64, generator=gen)
-    rc, tc = r.clone().requires_grad_(True), tf.clone().requires_grad_(use_time)
+    gy = torch.randn(B, 29, H, generator=gen)
+    rc, tc = r.clone().requires_grad_(dx), tf.clone().requires_grad_(use_time and dx)
     yc = ref(rc, tc if use_time else None)
     (yc * gy).sum().backward()
-    rg, tg = r.to(DEV).requires_grad_(True), tf.to(DEV).requires_grad_(use_time)
+    rg, tg = r.to(DEV).requires_grad_(dx), tf.to(DEV).requires_grad_(use_time and dx)
     yg = enc(rg, tg if use_time else None)
     (yg * gy.to(DEV)).sum().backward()
     assert_close(yg, yc, what="GRU h_L")
-    assert_close(rg.grad, rc.grad, what="GRU d residual")
-    if use_time:
+    if dx:
+        assert_close(rg.grad, rc.grad, what="GRU d residual")
+    if use_time and dx:
         assert_close(tg.grad, tc.grad, what="GRU d tfeat")
     assert_grads_close([(n, p.grad) for n, p in enc.gru.named_parameters()],
                        {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
