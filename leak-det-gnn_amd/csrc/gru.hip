@@ -490,29 +490,35 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         split3_x8(v0, v1, adh[c][0], adh[c][1], adh[c][2]);
     }
 
+    // Prefetch loads are unconditional and raw: addresses clamped in range (a padded
+    // sequence reads sequence 0, t < 0 reads step 0) and nothing selected on the loaded
+    // value until it is consumed — a load under a divergent branch, or a select on its
+    // result, makes the compiler wait for it (vmcnt) in the iteration that issued it, which
+    // serialises the two-step prefetch.  A padded sequence needs no masking: its dh is zero,
+    // every dG term is proportional to dh, and its h / x rows only ever multiply its own dG.
     auto load_g = [&](int t, f32x4 (&g)[4]) {
-        const float* p = gates + (static_cast<int64_t>(t) * Nseq + seqc) * 4 * H + u0;
+        const float* p = gates + (static_cast<int64_t>(max(t, 0)) * Nseq + seqc) * 4 * H + u0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[k] = (valid && t >= 0) ? ld4(p + k * H) : zero4();
+        for (int k = 0; k < 4; ++k) g[k] = ld4(p + k * H);
     };
-    auto load_h = [&](int t) -> f32x4 {  // h_t of this lane's units (zero for t < 0 / padded)
-        return (valid && t >= 0) ? ld4(hs + (static_cast<int64_t>(t) * Nseq + seqc) * H + u0) : zero4();
+    auto load_h = [&](int t) -> f32x4 {  // h_t of this lane's units (h_0 for t < 0: masked at use)
+        return ld4(hs + (static_cast<int64_t>(max(t, 0)) * Nseq + seqc) * H + u0);
     };
-    auto load_x = [&](int t, float (&x)[XPT]) {
+    auto load_x = [&](int t, float (&x)[XPT]) {  // raw residual / tfeat value (see x_val)
 #pragma unroll
         for (int i = 0; i < XPT; ++i) {
             const int e = threadIdx.x + i * G::NTH, xs = e >> 4, k = e & 15;
             const uint32_t sg = seq0 + xs;
-            float v = 0.f;
-            if (sg < Nseq && t >= 0) {
-                const uint32_t b = lg_div(sg, fdS), s = sg - b * fdS.d;
-                const int64_t row = static_cast<int64_t>(b) * L + t;
-                if (k == 0) v = resid[row * S + s];
-                else if (UT && k <= 9) v = tfeat[row * 9 + (k - 1)];
-                else if (k == 10) v = 1.f;
-            }
-            x[i] = v;
+            const uint32_t sgc = sg < Nseq ? sg : 0u;
+            const uint32_t b = lg_div(sgc, fdS), s = sgc - b * fdS.d;
+            const int64_t row = static_cast<int64_t>(b) * L + max(t, 0);
+            const bool from_t = UT && k >= 1 && k <= 9;
+            x[i] = *(from_t ? tfeat + row * 9 + (k - 1) : resid + row * S + s);
         }
+    };
+    auto x_val = [&](int i, float raw) {  // x row column k: residual, tfeat, the constant 1, 0
+        const int k = (threadIdx.x + i * G::NTH) & 15;
+        return (k == 0 || (UT && k >= 1 && k <= 9)) ? raw : (k == 10 ? 1.f : 0.f);
     };
 
     f32x4 dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + u0) : zero4();
@@ -523,20 +529,24 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = zero4();
     dwx[0] = dwx[1] = zero4();
 
-    f32x4 g_cur[4], g_n1[4], h_cur, h_n1;
-    float x_cur[XPT], x_n1[XPT];
-    load_g(L - 1, g_cur);
-    load_g(L - 2, g_n1);
-    h_cur = load_h(L - 2);
-    h_n1 = load_h(L - 3);
-    load_x(L - 1, x_cur);
-    load_x(L - 2, x_n1);
+    // Two prefetch slots (steps of one parity each), each consumed and refilled with the
+    // step two earlier by the same unrolled copy of the step: no register rotation, whose
+    // moves would wait for the loads just issued.
+    f32x4 gA[4], gB[4], hA, hB;
+    float xA[XPT], xB[XPT];
+    load_g(L - 1, gA);
+    load_g(L - 2, gB);
+    hA = load_h(L - 2);
+    hB = load_h(L - 3);
+    load_x(L - 1, xA);
+    load_x(L - 2, xB);
 
-    for (int t = L - 1; t >= 0; --t) {
+    auto step = [&](const int t, f32x4 (&g_cur)[4], f32x4& h_cur, float (&x_cur)[XPT]) {
         const int bf = t & 1;
         // (1) elementwise gate backward (h_cur = h_{t-1})
         {
-            const f32x4 r = g_cur[0], z = g_cur[1], n = g_cur[2], hnp = g_cur[3], hp = h_cur;
+            const f32x4 r = g_cur[0], z = g_cur[1], n = g_cur[2], hnp = g_cur[3];
+            const f32x4 hp = t >= 1 ? h_cur : zero4();  // h_{-1} = 0
             f32x4 gr, gz, ghn, gin, dhp;
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
@@ -570,21 +580,16 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             for (int i = 0; i < XPT; ++i) {
                 const int e = threadIdx.x + i * G::NTH;
                 uint16_t p0, p1, p2;
-                split3_1(x_cur[i], p0, p1, p2);
+                split3_1(x_val(i, x_cur[i]), p0, p1, p2);
                 xls[bf][0][e >> 4][e & 15] = p0;
                 xls[bf][1][e >> 4][e & 15] = p1;
                 xls[bf][2][e >> 4][e & 15] = p2;
             }
         }
-        // prefetch: step t-2's gates / x and h_{t-3}
-#pragma unroll
-        for (int k = 0; k < 4; ++k) g_cur[k] = g_n1[k];
-        load_g(t - 2, g_n1);
-        h_cur = h_n1;
-        h_n1 = load_h(t - 3);
-#pragma unroll
-        for (int i = 0; i < XPT; ++i) x_cur[i] = x_n1[i];
-        load_x(t - 2, x_n1);
+        // refill this slot: step t-2's gates / x and h_{t-3}
+        load_g(t - 2, g_cur);
+        h_cur = load_h(t - 3);
+        load_x(t - 2, x_cur);
         // dgs/hls/xls[bf] complete.  Buffer bf was last read at step t+2, which every wave
         // finished before arriving at step t+1's barrier: one barrier per step suffices.
         __syncthreads();
@@ -632,7 +637,13 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
                 dwx[0] = mfma_split(a, bx, dwx[0]);
             }
         }
+    };
+    int t = L - 1;
+    for (; t >= 1; t -= 2) {  // unconditional pairs: a conditional second half would merge
+        step(t, gA, hA, xA);  // the slot registers in a phi, i.e. moves that wait for loads
+        step(t - 1, gB, hB, xB);
     }
+    if (t == 0) step(0, gA, hA, xA);
 
     // per-workgroup slab (the layout of k_gru_bwd): C rows = gate rows 16w + 4q + reg, columns j
     float* out = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
