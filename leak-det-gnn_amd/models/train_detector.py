@@ -8,7 +8,9 @@ checkpoint schema (:346-353).
 
 The detector is this package's LeakDetector (HIP GRU / GCN / heads kernels); batches
 come from datasets.DeviceBatchLoader (--loader torch restores the DataLoader path);
-the optimizer is AdamW(fused=True) on the GPU.  Checkpoints load with
+on the GPU the loss is models.loss.CrossEntropyLoss (two launches) and clip_grad_norm_ +
+AdamW run as models.optim.ClipAdamW (two launches, the same arithmetic as torch's
+clip then AdamW step); on the CPU they are torch's.  Checkpoints load with
 torch.load(weights_only=True).
 
 Data parallel (not in the reference, which is single-device): launched under torchrun
@@ -40,6 +42,8 @@ import torch.nn as nn
 from .datasets import AbruptLeakDetectorDataset, SensorStandardizer
 from .ddp import GradAllReduce, dist_env, init_distributed
 from .detector import LeakDetector
+from .loss import CrossEntropyLoss
+from .optim import ClipAdamW
 from .predictor import NormalPredictorGRU, NormalPredictorTCN
 from .train_predictor import make_loader, pick_device, set_seed
 from .utils import build_residual_sequence_from_segment, now
@@ -232,9 +236,13 @@ def main(argv=None) -> None:
     detector = LeakDetector(inp_path=args.inp_path, sensor_node_ids=sensor_ids, pipe_ids_in_order=pipe_ids_in_order,
                             sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1, use_time=True,
                             mlp_dtype=args.dtype).to(device)
-    opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay,
-                            fused=(device.type == "cuda"))
-    loss_fn = nn.CrossEntropyLoss()
+    clip = args.grad_clip if args.grad_clip and args.grad_clip > 0 else None
+    fused_step = device.type == "cuda"  # clip_grad_norm_ + AdamW.step as one fused op pair
+    if fused_step:
+        opt = ClipAdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay, max_norm=clip)
+    else:
+        opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+    loss_fn = CrossEntropyLoss()  # torch's own path on the CPU
     allreduce = GradAllReduce(detector.parameters())  # no-op at world 1
     evaluator = DetectorEvaluator(predictor=predictor, detector=detector, device=device, l_pred=args.l_pred,
                                   l_det=args.l_det,
@@ -292,8 +300,8 @@ def main(argv=None) -> None:
                 allreduce()
             else:
                 loss.backward()
-            if args.grad_clip and args.grad_clip > 0:
-                torch.nn.utils.clip_grad_norm_(detector.parameters(), args.grad_clip)
+            if clip is not None and not fused_step:
+                torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
             opt.step()
             running += loss.detach().double() * n_local
             seen += n_local

@@ -1,0 +1,8 @@
+#!/bin/bash
+# r02z: round-2 validation: full -m gpu suite, then the default bench line (driver command)
+set -o pipefail
+OUT=gpurun_out/r02z; mkdir -p $OUT
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1; rc=$?
+tail -3 $OUT/gpu_tests.txt; [ $rc = 0 ] || exit 1
+timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/bench.json')); print(d['value'], d['ms_per_step'], d['roofline'], d['cpu_baseline'])"
