@@ -72,28 +72,31 @@ __device__ __forceinline__ int64_t lg_row_index(int64_t r, const lg_fastdiv& fdP
     return static_cast<int64_t>(b) * ldo + (static_cast<uint32_t>(r) - b * fdP.d);
 }
 
-// endpoint node ids of pipe row r (0, 0 past the end)
+// Prefetch loads below are unconditional (a row past the end reads pipe row 0 of window 0,
+// whose values are never stored and meet a zero dlogit in the backward) and land exactly in
+// the registers that are used: a load under a divergent branch, or a 16-byte load of an
+// int64 pair whose unused high words the register allocator recycles as temporaries, makes
+// the compiler wait for every load in flight (vmcnt(0)) right after issuing the prefetch —
+// measured, that exposed a full memory round trip per tile.
+__device__ __forceinline__ uint32_t clamp_row(int64_t r, int64_t BP) { return r < BP ? static_cast<uint32_t>(r) : 0u; }
+// endpoint node ids of pipe row r: the low words of the int64 ids (ids < 2^31)
 __device__ __forceinline__ void load_ends(const int64_t* __restrict__ ends, int64_t r, int64_t BP,
                                           const lg_fastdiv& fdP, uint32_t& nu, uint32_t& nv) {
-    nu = nv = 0;
-    if (r < BP) {
-        const uint32_t p = static_cast<uint32_t>(r) - lg_div(static_cast<uint32_t>(r), fdP) * fdP.d;
-        nu = static_cast<uint32_t>(ends[2 * p]);
-        nv = static_cast<uint32_t>(ends[2 * p + 1]);
-    }
+    const uint32_t rr = clamp_row(r, BP);
+    const uint32_t p = rr - lg_div(rr, fdP) * fdP.d;
+    const uint32_t* e32 = reinterpret_cast<const uint32_t*>(ends);
+    nu = e32[4 * p];
+    nv = e32[4 * p + 2];
 }
-// float4 f of the two endpoint rows of pipe row r (zeros past the end); 32-bit element
-// offsets (the API requires N*B*D < 2^32)
+// float4 f of the two endpoint rows of pipe row r; 32-bit element offsets (the API requires
+// N*B*D < 2^32)
 template <int D>
 __device__ __forceinline__ void load_rows(const float* __restrict__ h, int64_t r, int64_t BP, const lg_fastdiv& fdP,
                                           uint32_t nu, uint32_t nv, uint32_t sb, uint32_t sn, int f, f32x4& u,
                                           f32x4& v) {
-    u = v = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (r < BP) {
-        const uint32_t b = lg_div(static_cast<uint32_t>(r), fdP);
-        u = ld4(h + ((b * sb + nu * sn) * D + 4 * f));
-        v = ld4(h + ((b * sb + nv * sn) * D + 4 * f));
-    }
+    const uint32_t b = lg_div(clamp_row(r, BP), fdP);
+    u = ld4(h + ((b * sb + nu * sn) * D + 4 * f));
+    v = ld4(h + ((b * sb + nv * sn) * D + 4 * f));
 }
 // three bf16 parts of 4 floats -> 8-byte slots at img[off], img[pl + off], img[2 pl + off]
 // (BF: the hi part only; the other planes are never read)
@@ -153,8 +156,10 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     const int64_t step = gridDim.x;
     // Software pipeline, one barrier per tile: while tile i's MFMAs run on feature image
     // i&1, the wave splits tile i+1's endpoint rows into image (i+1)&1.  Rows are loaded
-    // three tiles ahead into two alternating register sets, node ids a tile before their rows.
-    uint32_t nu, nv;
+    // three tiles ahead into two alternating register sets, node ids two tiles before their
+    // rows (one pair per set), so issuing a tile's row loads never waits on the id load
+    // issued just before it.
+    uint32_t nu, nv, nua, nva, nub = 0, nvb = 0;
     f32x4 pu0, pv0, pu1, pv1;
     auto rowof = [&](int64_t t) { return t * G::TR + arow; };
     auto stage = [&](uint16_t* img, int part3, const f32x4& pu, const f32x4& pv) {  // a third of the slot
@@ -178,10 +183,14 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     load_rows<D>(h, rowof(t0 + step), BP, fdP, nu, nv, sb, sn, af, pu0, pv0);
     load_ends(ends, rowof(t0 + 2 * step), BP, fdP, nu, nv);
     load_rows<D>(h, rowof(t0 + 2 * step), BP, fdP, nu, nv, sb, sn, af, pu1, pv1);
-    load_ends(ends, rowof(t0 + 3 * step), BP, fdP, nu, nv);
+    // BF (two workgroups per CU, 128 VGPRs): one shared id pair, a tile ahead of its rows
+    constexpr int IDA = BF ? 4 : 5;  // the id pair refilled in a body is tile + IDA step's
+    load_ends(ends, rowof(t0 + 3 * step), BP, fdP, nua, nva);
+    if constexpr (!BF) load_ends(ends, rowof(t0 + 4 * step), BP, fdP, nub, nvb);
     __syncthreads();
     // tile: this iteration's tile; (pu, pv): tile + step's rows, refilled with tile + 3 step's
-    auto body = [&](int64_t tile, int buf, f32x4& pu, f32x4& pv) {
+    // (ids (eu, ev), refilled with tile + 5 step's)
+    auto body = [&](int64_t tile, int buf, f32x4& pu, f32x4& pv, uint32_t& eu, uint32_t& ev) {
         const int64_t row0 = tile * G::TR;
         const uint16_t* cur = fimg + buf * 3 * G::FPL;
         uint16_t* nxt = fimg + (buf ^ 1) * 3 * G::FPL;
@@ -208,8 +217,8 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             if (ks * 3 / G::KS != (ks + 1) * 3 / G::KS) stage(nxt, ks * 3 / G::KS, pu, pv);
         }
         if (!(lab & 2)) {
-            load_rows<D>(h, rowof(tile + 3 * step), BP, fdP, nu, nv, sb, sn, af, pu, pv);
-            load_ends(ends, rowof(tile + 4 * step), BP, fdP, nu, nv);
+            load_rows<D>(h, rowof(tile + 3 * step), BP, fdP, eu, ev, sb, sn, af, pu, pv);
+            load_ends(ends, rowof(tile + IDA * step), BP, fdP, eu, ev);
         }
 #pragma unroll
         for (int rb = 0; rb < RBF; ++rb) {
@@ -249,10 +258,15 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             if (r < BP) logit[lg_row_index(r, fdP, ldo)] = tot + bias2;
         }
     };
-    for (int64_t tile = t0; tile < ntiles; tile += 2 * step) {
-        body(tile, 0, pu0, pv0);
-        if (tile + step < ntiles) body(tile + step, 1, pu1, pv1);
+    // unconditional pairs (a conditional second body merges both paths' pending loads at the
+    // loop head, and the compiler then waits for all of them), the odd tail after the loop
+    int64_t tile = t0;
+    for (; tile + step < ntiles; tile += 2 * step) {
+        body(tile, 0, pu0, pv0, nua, nva);
+        if constexpr (BF) body(tile + step, 1, pu1, pv1, nua, nva);
+        else body(tile + step, 1, pu1, pv1, nub, nvb);
     }
+    if (tile < ntiles) body(tile, 0, pu0, pv0, nua, nva);
 }
 
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
@@ -305,16 +319,12 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     uint32_t nu, nv;
     f32x4 pu, pv, hp[G::HPT];
     float dl[G::HPT];
-    auto load_hid = [&](int64_t t) {
+    auto load_hid = [&](int64_t t) {  // raw (see load_ends); a row past the end is zeroed at use
 #pragma unroll
         for (int i = 0; i < G::HPT; ++i) {
-            const int64_t r = t * G::TR + hrow + 16 * i;
-            hp[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            dl[i] = 0.f;
-            if (r < BP) {
-                hp[i] = ld4(hid + (static_cast<uint32_t>(r) * HID + 4 * n4));
-                dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
-            }
+            const uint32_t r = clamp_row(t * G::TR + hrow + 16 * i, BP);
+            hp[i] = ld4(hid + (r * HID + 4 * n4));
+            dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
         }
     };
     load_ends(ends, tile * G::TR + arow, BP, fdP, nu, nv);
@@ -342,13 +352,14 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 #pragma unroll
         for (int i = 0; i < G::HPT; ++i) {
             f32x4 g;
+            const float dli = row0 + hrow + 16 * i < BP ? dl[i] : 0.f;  // rows past the end: no gradient
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                g[j] = hp[i][j] > 0.f ? dl[i] * w2g[j] * dscale : 0.f;
-                dw2a[j] = fmaf(dl[i], hp[i][j], dw2a[j]);
+                g[j] = hp[i][j] > 0.f ? dli * w2g[j] * dscale : 0.f;
+                dw2a[j] = fmaf(dli, hp[i][j], dw2a[j]);
                 db1a[j] += static_cast<double>(g[j]);
             }
-            if (n4 == 0) db2 += static_cast<double>(dl[i]);
+            if (n4 == 0) db2 += static_cast<double>(dli);
             st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
         }
         __syncthreads();
