@@ -84,6 +84,7 @@ enum {
  * that walks rowptr per tile (round-1 kernel), LG_F_LAB_W8 = 8-wave workgroups. */
 #define LG_F_LAB_NM2       0x00200000
 #define LG_F_LAB_W8        0x00100000
+#define LG_F_LAB_W5        0x00040000  /* lab: 5-wave workgroups (3 per CU: 15 waves) */
 #define LG_F_LAB_DST       0x00080000  /* lab: epilogue stores straight from the MFMA layout */
 
 #define LG_F_LAB_BPC_SHIFT 24
@@ -188,7 +189,9 @@ int lg_batchify_edge_index(const int64_t* edge_index, int64_t E, int64_t N, int6
  * (a 7,424 x 64 x 64 GEMM at B=256) and bias = bs (rows with h0 = 0, mask = 0).
  *   sensor_slot : int32 [N]  (-1 for non-sensor nodes)
  *   proj : fp32 [B][S][D];  bias : fp32 [D];  x0 : fp32 [B][N][D]
- *   flags: LG_F_DROPOUT (p, seed as lg_gcn_fwd; salt distinguishes the call site) */
+ *   flags: LG_F_DROPOUT (p, seed as lg_gcn_fwd; salt distinguishes the call site).  The
+ *   keep mask is the row stream of lg_gcn_fwd_nm (seeded per window-major row b*N + n and
+ *   lane group), also for lg_node_init_proj_fwd (ABI 11; the per-element hash before). */
 int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float* bias, float* x0,
                      int64_t B, int64_t N, int64_t S, int64_t D,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);

@@ -96,6 +96,17 @@ __host__ __device__ __forceinline__ uint32_t lg_xorshift32(uint32_t s) {
     s ^= s << 5;
     return s;
 }
+// Row-stream keep bits of channels c4 .. c4 + 3 (c4 % 4 == 0) of one global row: the lane
+// group is q = (c4 / 4) % 4, block mt = c4 / 16, and pair k of the group's stream is the
+// state after k + 1 xorshift32 steps (bit i = channel c4 + i).  For a lane that owns only
+// these four channels (the node init's sensor rows).
+__device__ __forceinline__ uint32_t lg_row_stream_keep4(uint32_t key, uint64_t row, int c4, uint32_t thr) {
+    uint32_t s = lg_row_stream_seed(key, row, static_cast<uint32_t>((c4 >> 2) & 3));
+    for (int k = 0; k <= 2 * (c4 >> 4); ++k) s = lg_xorshift32(s);
+    const uint32_t s2 = lg_xorshift32(s);
+    return static_cast<uint32_t>((s & 0xFFFFu) >= thr) | (static_cast<uint32_t>((s >> 16) >= thr) << 1) |
+           (static_cast<uint32_t>((s2 & 0xFFFFu) >= thr) << 2) | (static_cast<uint32_t>((s2 >> 16) >= thr) << 3);
+}
 __device__ __forceinline__ bool lg_keep_u(uint32_t s, float p) {
     return static_cast<float>(s >> 8) * (1.0f / 16777216.0f) >= p;
 }

@@ -571,7 +571,7 @@ constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
 // (16 rows x 64 B per store) instead of through the LDS tile.
 // BF (LG_F_BF16, the bf16 node-MLP tier): the transform's single hi x hi product.
 template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false, bool BF = false>
-__global__ void __launch_bounds__(64 * WAVES)
+__global__ void __launch_bounds__(64 * WAVES, WAVES >= 5 ? 4 : 1)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
@@ -1440,6 +1440,7 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
     // n workgroups per CU
     const bool lab_v1 = (flags & LG_F_LAB_V1) != 0, lab_nm2 = (flags & LG_F_LAB_NM2) != 0;
     const bool w8 = (flags & LG_F_LAB_W8) != 0;
+    const bool w5 = (flags & LG_F_LAB_W5) != 0;
     const bool relu = (flags & LG_F_RELU) != 0;
     const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
     (void)nnz_cap;
@@ -1462,6 +1463,12 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
             const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
             lg_launch(kern, grid, 64 * kNm2Waves, dyn2, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
                                                     dropout_p, scale, seed, salt);                                 \
+        } else if (w5) {                                                                                           \
+            auto kern = relu ? nm3_kernel<DD, DR, true, 5>(flags) : nm3_kernel<DD, DR, false, 5>(flags);           \
+            const size_t dyn3 = split ? Nm3Lds<DD, true, 5>::BYTES : Nm3Lds<DD, false, 5>::BYTES;                  \
+            const int grid = nm_grid(kern, 64 * 5, dyn3, ntiles, 5, bpc);                                          \
+            lg_launch(kern, grid, 64 * 5, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
+                                            salt);                                                                 \
         } else if (w8) {                                                                                           \
             auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \

@@ -13,31 +13,59 @@ namespace {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// One row group of LPR lanes per (b, n) row.
+// Node init dropout: the row-stream rule of the fused GCN forward (common.h
+// lg_row_stream_seed, oracle/dropout_ref.py row_stream_mask) with the window-major row id,
+// so both layouts draw the same mask.  The bulk rows are written by lane groups (row, q):
+// lane q owns channels 16 mt + 4 q .. + 3 of its row, i.e. exactly one stream, so a row
+// costs one seed and D / 8 xorshift32 steps per lane instead of a multiply hash per element.
+constexpr int kNiRowsPerBlock = 64;  // 256 threads, 4 lanes per row
+
+// v[mt] = keep(channel 16 mt + 4 q + reg) ? t[mt] : 0 over the (row, q) stream
+template <int CH>
+__device__ __forceinline__ void ni_stream_select(uint32_t key, uint64_t rw, uint32_t q, uint32_t thr,
+                                                 const f32x4 (&t)[CH], f32x4 (&v)[CH]) {
+    uint32_t st = lg_row_stream_seed(key, rw, q);
+#pragma unroll
+    for (int mt = 0; mt < CH; ++mt) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            if ((reg & 1) == 0) st = lg_xorshift32(st);
+            const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+            v[mt][reg] = u16 >= thr ? t[mt][reg] : 0.0f;
+        }
+    }
+}
+
+// Output row r of x0: window-major r = b N + n, node-major (nm) r = n B + b; fdM divides by
+// the fast index's extent (N, resp. B).  x0 = dropout(relu(sensor row ? proj[b][slot] : bias)).
 template <int D>
 __global__ void __launch_bounds__(256)
-// Output row r of x0: window-major r = b N + n, node-major (nm) r = n B + b; fdM divides by
-// the fast index's extent (N, resp. B).  The dropout index is always the window-major one,
-// so both layouts draw the same mask.
 k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, const float* __restrict__ bias,
             float* __restrict__ x0, int64_t N, lg_fastdiv fdM, int nm, int64_t S, int64_t R, int dropout, float p,
             float scale, uint64_t seed, uint32_t salt) {
-    constexpr int LPR = D / 4, RPB = 256 / LPR;
-    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+    constexpr int CH = D / 16;
+    const int rl = threadIdx.x >> 2, q = threadIdx.x & 3;
     const uint32_t key = lg_dropout_key_dev(seed, salt);
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
+    const uint32_t thr = lg_keep_threshold16(p);
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * kNiRowsPerBlock + rl; r < R;
+         r += static_cast<int64_t>(gridDim.x) * kNiRowsPerBlock) {
         const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
         const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
         const int32_t s = slot[n];
-        f32x4 v = s >= 0 ? ld4(proj + (static_cast<int64_t>(b) * S + s) * D + 4 * fg) : ld4(bias + 4 * fg);
-        const int64_t rw = static_cast<int64_t>(b) * N + n;
+        const float* src = s >= 0 ? proj + (static_cast<int64_t>(b) * S + s) * D : bias;
+        f32x4 t[CH], v[CH];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float t = fmaxf(v[i], 0.f);
-            if (dropout) t = lg_dropout(t, p, scale, key, rw * D + 4 * fg + i);
-            v[i] = t;
+        for (int mt = 0; mt < CH; ++mt) {
+            t[mt] = ld4(src + 16 * mt + 4 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) t[mt][i] = fmaxf(t[mt][i], 0.f) * (dropout ? scale : 1.0f);
         }
-        st4(x0 + r * D + 4 * fg, v);
+        if (dropout) ni_stream_select<CH>(key, static_cast<uint64_t>(b) * N + n, q, thr, t, v);
+        else
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt) v[mt] = t[mt];
+#pragma unroll
+        for (int mt = 0; mt < CH; ++mt) st4(x0 + r * D + 16 * mt + 4 * q, v[mt]);
     }
 }
 
@@ -53,22 +81,13 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
                  const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ x0, int64_t B,
                  int64_t N, lg_fastdiv fdM, int nm, int64_t S, int64_t R, int GS, int dropout, float p, float scale,
                  uint64_t seed, uint32_t salt) {
-    constexpr int LPR = D / 4, RPB = 256 / LPR;
+    constexpr int LPR = D / 4, RPB = 256 / LPR, CH = D / 16;
     __shared__ __attribute__((aligned(16))) float wt[DS][D];  // W^T[k][o]
     __shared__ __attribute__((aligned(16))) float bf[D];      // W[o][DS] + bias[o]
-    const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const uint32_t key = lg_dropout_key_dev(seed, salt);
-    auto finish = [&](f32x4 v, int64_t b, int64_t n) {
-        const int64_t rw = b * N + n;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float t = fmaxf(v[i], 0.f);
-            if (dropout) t = lg_dropout(t, p, scale, key, rw * D + 4 * fg + i);
-            v[i] = t;
-        }
-        st4(x0 + (nm ? n * B + b : b * N + n) * D + 4 * fg, v);
-    };
+    const uint32_t thr = lg_keep_threshold16(p);
     if (static_cast<int>(blockIdx.x) < GS) {
+        const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
         for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {
             const int o = i / (DS + 1), k = i % (DS + 1);
             if (k < DS) wt[k][o] = W[i];
@@ -91,15 +110,34 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
                     for (int i = 0; i < 4; ++i) acc[i] = fmaf(h4[kk], w[i], acc[i]);
                 }
             }
-            finish(acc + bs, b, n);
+            f32x4 v = acc + bs;
+            const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b * N + n), 4 * fg, thr) : 0xFu;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = ((kb >> i) & 1u) ? fmaxf(v[i], 0.f) * (dropout ? scale : 1.0f) : 0.0f;
+            st4(x0 + (nm ? n * B + b : b * N + n) * D + 4 * fg, v);
         }
     }
-    const f32x4 b0 = ld4(bias + 4 * fg);
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * RPB + rl; r < R; r += static_cast<int64_t>(gridDim.x) * RPB) {
+    // every row without a sensor: dropout(relu(bias)), in (row, q) lane groups
+    const int rl = threadIdx.x >> 2, q = threadIdx.x & 3;
+    f32x4 t[CH];
+#pragma unroll
+    for (int mt = 0; mt < CH; ++mt) {
+        t[mt] = ld4(bias + 16 * mt + 4 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[mt][i] = fmaxf(t[mt][i], 0.f) * (dropout ? scale : 1.0f);
+    }
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * kNiRowsPerBlock + rl; r < R;
+         r += static_cast<int64_t>(gridDim.x) * kNiRowsPerBlock) {
         const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
         const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
         if (slot[n] >= 0) continue;
-        finish(b0, b, n);
+        f32x4 v[CH];
+        if (dropout) ni_stream_select<CH>(key, static_cast<uint64_t>(b) * N + n, q, thr, t, v);
+        else
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt) v[mt] = t[mt];
+#pragma unroll
+        for (int mt = 0; mt < CH; ++mt) st4(x0 + r * D + 16 * mt + 4 * q, v[mt]);
     }
 }
 
@@ -235,10 +273,22 @@ k_pipe_scatter(const int32_t* __restrict__ inc_rowptr, const int32_t* __restrict
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[k] = g[k] / fN;
         }
+        // incidences in item order, kScatterBatch items and their rows requested before
+        // the first add (a node has few incidences: one round trip instead of one per item)
+        constexpr int kScatterBatch = 4;
         const int32_t e0 = inc_rowptr[n], e1 = inc_rowptr[n + 1];
-        for (int32_t e = e0; e < e1; ++e) {
-            const int32_t it = inc_item[e];  // 2*p + role
-            acc += ld4(dpipe + ((b * P + (it >> 1)) * 2 + (it & 1)) * D + 4 * fg);
+        for (int32_t e = e0; e < e1; e += kScatterBatch) {
+            int32_t it[kScatterBatch];
+#pragma unroll
+            for (int u = 0; u < kScatterBatch; ++u) it[u] = e + u < e1 ? inc_item[e + u] : -1;  // 2*p + role
+            f32x4 v[kScatterBatch];
+#pragma unroll
+            for (int u = 0; u < kScatterBatch; ++u)
+                v[u] = it[u] >= 0 ? ld4(dpipe + ((b * P + (it[u] >> 1)) * 2 + (it[u] & 1)) * D + 4 * fg)
+                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < kScatterBatch; ++u)
+                if (it[u] >= 0) acc += v[u];
         }
         st4(dh + r * D + 4 * fg, acc);
     }
@@ -292,6 +342,10 @@ k_linear_dw(const float* __restrict__ dy, const float* __restrict__ x, int64_t K
 
 int linear_dw_grid(int64_t K) { return static_cast<int>(std::max<int64_t>(1, ceil_div(K, kLinRows))); }
 
+inline unsigned ni_grid(int64_t rows) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, kNiRowsPerBlock), 16LL * lg_num_cus())));
+}
+
 inline unsigned row_grid(int64_t rows, int D) {
     const int64_t rpb = 256 / (D / 4);
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, rpb), 16LL * lg_num_cus())));
@@ -315,11 +369,11 @@ extern "C" int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, c
     hipStream_t s = lg_stream(stream);
     switch (D) {
         case 64:
-            lg_launch(k_node_init<64>, row_grid(R, 64), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+            lg_launch(k_node_init<64>, ni_grid(R), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
                                                             dropout_p, scale, seed, salt);
             break;
         case 32:
-            lg_launch(k_node_init<32>, row_grid(R, 32), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
+            lg_launch(k_node_init<32>, ni_grid(R), 256, 0, s, sensor_slot, proj, bias, x0, N, fdM, nm, S, R, dropout,
                                                             dropout_p, scale, seed, salt);
             break;
         default:
@@ -390,10 +444,10 @@ extern "C" int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* 
     const int RPBD = 256 / (static_cast<int>(D) / 4);
     const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * B, RPBD), lg_num_cus())));
     if (D == 64)
-        lg_launch(k_node_init_proj<64, 64>, std::max<unsigned>(row_grid(R, 64), GS), 256, 0, s, sensor_slot, sensor_idx,
+        lg_launch(k_node_init_proj<64, 64>, std::max<unsigned>(ni_grid(R), GS), 256, 0, s, sensor_slot, sensor_idx,
                   h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
     else
-        lg_launch(k_node_init_proj<32, 32>, std::max<unsigned>(row_grid(R, 32), GS), 256, 0, s, sensor_slot, sensor_idx,
+        lg_launch(k_node_init_proj<32, 32>, std::max<unsigned>(ni_grid(R), GS), 256, 0, s, sensor_slot, sensor_idx,
                   h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
@@ -457,7 +511,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 10; }
+extern "C" int lg_abi_version(void) { return 11; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

@@ -47,16 +47,16 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ 
     __shared__ double part[16][64];
     double acc = 0.0;
     if (col < len) {
+        // slabs g = w, w + 16, ... added in that order; kRedInflight independent loads per
+        // round trip (a 512-slab reduce is 2 round trips per wave instead of 8)
+        constexpr int kRedInflight = 16;
         int g = w;
-        for (; g + 48 < G; g += 64) {  // four independent loads in flight
-            const float a = src[static_cast<int64_t>(g) * stride + col];
-            const float bb = src[static_cast<int64_t>(g + 16) * stride + col];
-            const float c = src[static_cast<int64_t>(g + 32) * stride + col];
-            const float d = src[static_cast<int64_t>(g + 48) * stride + col];
-            acc += a;
-            acc += bb;
-            acc += c;
-            acc += d;
+        for (; g + 16 * (kRedInflight - 1) < G; g += 16 * kRedInflight) {
+            float v[kRedInflight];
+#pragma unroll
+            for (int u = 0; u < kRedInflight; ++u) v[u] = src[static_cast<int64_t>(g + 16 * u) * stride + col];
+#pragma unroll
+            for (int u = 0; u < kRedInflight; ++u) acc += v[u];
         }
         for (; g < G; g += 16) acc += src[static_cast<int64_t>(g) * stride + col];
     }

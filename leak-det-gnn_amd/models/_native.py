@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 10  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 11  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -29,6 +29,7 @@ LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 
 LG_F_LAB_NM2 = 0x00200000  # lg_gcn_fwd_nm schedule: round-1 rowptr-walking pipeline (kernel lab)
 LG_F_BF16 = 0x40  # lg_gcn_fwd_nm / lg_gcn_bwd_nm / lg_edge_head_*: the bf16 node-MLP tier
 LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel lab)
+LG_F_LAB_W5 = 0x00040000  # lg_gcn_fwd_nm schedule: 5-wave workgroups (kernel lab)
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)

@@ -48,6 +48,7 @@ class CapturedTrainStep:
         dev = label.device
         self.world = _world()
         self.slots = ops.SeedSlots(dev, seed_slots)
+        self._one: Optional[torch.Tensor] = None
 
         # eager warm-up on a side stream (allocator pools, optimizer state, cached graph CSR)
         side = torch.cuda.Stream(dev)
@@ -88,7 +89,11 @@ class CapturedTrainStep:
 
     def _forward_backward(self) -> torch.Tensor:
         loss = self.loss_fn(self.model(*self.inputs), self.label)
-        loss.backward()
+        # the seed gradient is a resident constant: autograd's ones_like would be one more
+        # (fill) launch per step
+        if self._one is None or self._one.shape != loss.shape:
+            self._one = torch.ones_like(loss)
+        loss.backward(self._one)
         return loss
 
     def _update(self) -> None:

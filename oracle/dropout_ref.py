@@ -8,6 +8,8 @@ torch's bitwise (SURVEY §7 "Dropout RNG cannot match bitwise"); the tests pin i
   key       = mix32(lo32(seed) ^ mix32(hi32(seed) ^ salt * 0x9E3779B9))
   h(idx)    = mix32(lo32(idx) * 0x9E3779B9 ^ key ^ hi32(idx) * 0x85EBCA6B)     (uint32 wrap-around)
   keep      <=> (h >> 8) / 2^24 >= p ;  kept values scaled by 1 / (1 - p)
+keep_mask is the NoLeakHead's rule; the node init (salt 0), the GCN layers and the EdgeHead
+draw row streams (row_stream_mask / edge_stream_mask below).
 """
 from __future__ import annotations
 

@@ -307,7 +307,7 @@ def _replay_train_cpu(sd: dict, r, tf, seeds: tuple, dt, up, dev="cpu", masks=No
 
     def t(a):
         return torch.from_numpy(a.astype(np.float64)).to(dt).to(dev)
-    mk0 = t(keep_mask(seed_t, 0, np.arange(R * D, dtype=np.uint64).reshape(R, D), 0.1))
+    mk0 = t(row_stream_mask(seed_t, 0, np.arange(R), D, 0.1))
     mkl = [t(row_stream_mask(seed_t, l, np.arange(R), D, 0.1)) for l in (1, 2)]
     me = t(edge_stream_mask(seed_h, ops.EDGE_HEAD_SALT, np.arange(B * P), 0.1))
     mn = t(keep_mask(seed_h, ops.NOLEAK_HEAD_SALT, np.arange(B * 128, dtype=np.uint64).reshape(B, 128), 0.1))

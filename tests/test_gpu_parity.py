@@ -295,9 +295,9 @@ def test_detector_train_mode_replay_with_oracle_masks():
     sc = 1.0 / 0.9
     R = B * N
     from oracle.dropout_ref import row_stream_mask
-    mk = [_masks(seed_t, 0, (R, D), 0.1)] + [   # node init: per-element hash; GCN layers: row streams
+    mk = [   # node init (salt 0) and the GCN layers (salts 1, 2): row streams
         torch.from_numpy(row_stream_mask(seed_t, l, np.arange(R), D, 0.1).astype(np.float32)).to(DEV)
-        for l in (1, 2)]
+        for l in (0, 1, 2)]
     from oracle.dropout_ref import edge_stream_mask
     me = torch.from_numpy(edge_stream_mask(seed_h, ops.EDGE_HEAD_SALT, np.arange(B * P), 0.1)
                           .astype(np.float32)).to(DEV)   # EdgeHead: row streams

@@ -113,7 +113,7 @@ def main():
     for lab in [v for v in args.nmlab.split(",") if v]:
         bits = 0
         for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
-            bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "nomfma": 1 << 28,
+            bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "w5": nat.LG_F_LAB_W5, "nomfma": 1 << 28,
                      "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA}.get(tok, 0)
             if tok.startswith("bpc"):
                 bits |= int(tok[3:]) << 24
