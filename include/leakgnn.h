@@ -90,6 +90,21 @@ enum {
 #define LG_F_LAB_BPC_SHIFT 24
 
 int lg_abi_version(void);
+
+/* Reduce batch (ABI 12).  The backward entry points end in a deterministic slab reduction
+ * of their weight/bias gradients (lg_gcn_bwd[_nm], lg_sensor_proj_bwd, lg_edge_head_bwd,
+ * lg_pool_head_bwd, lg_gru_bwd, lg_linear_dw).  Between lg_reduce_batch_begin() and
+ * lg_reduce_batch_flush(stream) on the SAME host thread those reductions are recorded
+ * instead of launched, and the flush launches them together (one launch per 16
+ * segments); every gradient column is summed in the same order, so results are unchanged.
+ * Until the flush is enqueued the recorded outputs are undefined and the recorded
+ * workspaces must stay allocated and unwritten.  A lg_sensor_proj_bwd whose dbias_in is
+ * a recorded output folds that output's partials into its own db reduction.  Replaces
+ * nothing in the reference: it merges the per-op launches of one backward pass
+ * (the autograd of detector.py:170-218).  begin: LG_EINVAL when a batch is already open;
+ * flush: LG_EINVAL when none is. */
+int lg_reduce_batch_begin(void);
+int lg_reduce_batch_flush(lg_stream_t stream);
 const char* lg_strerror(int code);
 
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;
@@ -191,7 +206,7 @@ int lg_batchify_edge_index(const int64_t* edge_index, int64_t E, int64_t N, int6
  *   proj : fp32 [B][S][D];  bias : fp32 [D];  x0 : fp32 [B][N][D]
  *   flags: LG_F_DROPOUT (p, seed as lg_gcn_fwd; salt distinguishes the call site).  The
  *   keep mask is the row stream of lg_gcn_fwd_nm (seeded per window-major row b*N + n and
- *   lane group), also for lg_node_init_proj_fwd (ABI 11; the per-element hash before). */
+ *   lane group), also for lg_node_init_proj_fwd (since ABI 11; the per-element hash before). */
 int lg_node_init_fwd(const int32_t* sensor_slot, const float* proj, const float* bias, float* x0,
                      int64_t B, int64_t N, int64_t S, int64_t D,
                      int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream);

@@ -471,6 +471,11 @@ extern "C" int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, c
     const int64_t SL = D * (Ds + 1) + D;
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
+    // inside a reduce batch dbias_in may still be pending (the layer-0 backward's reduction
+    // not yet launched): its partials are then summed into db by the batch instead of being
+    // read by workgroup 0
+    LgSlabSeg dbseg{D * (Ds + 1), D, db};
+    if (lg_reduce_batch_pending(dbias_in, &dbseg.slab2, &dbseg.G2, &dbseg.stride2, &dbseg.off2)) dbias_in = nullptr;
     if (D == 64)
         lg_launch(k_sensor_proj_bwd<64, 64>, G, 256, 0, s, dx0, sensor_idx, live, h_s, W, dbias_in, dh_s, slab, B, N, S,
                   nm);
@@ -478,7 +483,7 @@ extern "C" int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, c
         lg_launch(k_sensor_proj_bwd<32, 32>, G, 256, 0, s, dx0, sensor_idx, live, h_s, W, dbias_in, dh_s, slab, B, N, S,
                   nm);
     LG_RET_IF_LAUNCH_FAILED();
-    const LgSlabSeg segs[2] = {{0, D * (Ds + 1), dW}, {D * (Ds + 1), D, db}};
+    const LgSlabSeg segs[2] = {{0, D * (Ds + 1), dW}, dbseg};
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
@@ -511,7 +516,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 11; }
+extern "C" int lg_abi_version(void) { return 12; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

@@ -8,65 +8,149 @@
 // in wave order through LDS.  An optional fp64 column (sum of G doubles, used for
 // the cancellation-heavy output-bias gradients) is reduced by one extra block as a
 // fixed-shape tree.  Per-column work and the combine order depend only on (G, len),
-// never on scheduling.
+// never on scheduling.  A reduce batch (lg_reduce_batch_begin / _flush, include/leakgnn.h)
+// takes the reductions of several backward calls into ONE launch (up to 16 segments and
+// 4 fp64 columns per launch); each column keeps its own order, so results do not change.
 #include "common.h"
 #include "reduce.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace {
 
+constexpr int kJobSegs = 16;  // segments per launch
+constexpr int kJobD = 4;      // fp64 columns per launch
+
 struct Segs {
-    int64_t off[kLgMaxSlabSegs];
-    int64_t len[kLgMaxSlabSegs];
-    float* out[kLgMaxSlabSegs];
-    int first[kLgMaxSlabSegs + 1];  // first block of each segment; first[n] = total column blocks
+    const float* slab[kJobSegs];
+    const float* slab2[kJobSegs];
+    int64_t stride[kJobSegs], off[kJobSegs], stride2[kJobSegs], off2[kJobSegs], len[kJobSegs];
+    float* out[kJobSegs];
+    int G[kJobSegs], G2[kJobSegs];
+    int first[kJobSegs + 1];  // first block of each segment; first[n] = total column blocks
     int n;
+    const double* dslab[kJobD];
+    float* dout[kJobD];
+    int dG[kJobD];
+    int nd;
 };
 
-__global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ slab, int G, int64_t stride, Segs sg,
-                                                      const double* __restrict__ dslab, float* __restrict__ dout) {
+// fp64 sum over slabs g = w, w + 16, ... < G of src[g * stride + col], in that order,
+// kRedInflight independent loads per round trip
+__device__ __forceinline__ void slab_col_sum(const float* __restrict__ src, int G, int64_t stride, int64_t col, int w,
+                                             double& acc) {
+    constexpr int kRedInflight = 16;
+    int g = w;
+    for (; g + 16 * (kRedInflight - 1) < G; g += 16 * kRedInflight) {
+        float v[kRedInflight];
+#pragma unroll
+        for (int u = 0; u < kRedInflight; ++u) v[u] = src[static_cast<int64_t>(g + 16 * u) * stride + col];
+#pragma unroll
+        for (int u = 0; u < kRedInflight; ++u) acc += v[u];
+    }
+    for (; g < G; g += 16) acc += src[static_cast<int64_t>(g) * stride + col];
+}
+
+__global__ void __launch_bounds__(1024) k_slab_reduce(Segs sg) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.x;
     if (b >= sg.first[sg.n]) {  // fp64 column: 1024 strided partials, then a fixed tree
+        const int d = b - sg.first[sg.n];
         __shared__ double dp[1024];
         double acc = 0.0;
-        for (int g = threadIdx.x; g < G; g += 1024) acc += dslab[g];
+        for (int g = threadIdx.x; g < sg.dG[d]; g += 1024) acc += sg.dslab[d][g];
         dp[threadIdx.x] = acc;
         __syncthreads();
         for (int h = 512; h > 0; h >>= 1) {
             if (threadIdx.x < h) dp[threadIdx.x] += dp[threadIdx.x + h];
             __syncthreads();
         }
-        if (threadIdx.x == 0) dout[0] = static_cast<float>(dp[0]);
+        if (threadIdx.x == 0) sg.dout[d][0] = static_cast<float>(dp[0]);
         return;
     }
     int k = 0;
     while (k + 1 < sg.n && b >= sg.first[k + 1]) ++k;
     const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 64 + lane;
-    const int64_t len = sg.len[k];
-    const float* src = slab + sg.off[k];
     __shared__ double part[16][64];
     double acc = 0.0;
-    if (col < len) {
-        // slabs g = w, w + 16, ... added in that order; kRedInflight independent loads per
-        // round trip (a 512-slab reduce is 2 round trips per wave instead of 8)
-        constexpr int kRedInflight = 16;
-        int g = w;
-        for (; g + 16 * (kRedInflight - 1) < G; g += 16 * kRedInflight) {
-            float v[kRedInflight];
-#pragma unroll
-            for (int u = 0; u < kRedInflight; ++u) v[u] = src[static_cast<int64_t>(g + 16 * u) * stride + col];
-#pragma unroll
-            for (int u = 0; u < kRedInflight; ++u) acc += v[u];
-        }
-        for (; g < G; g += 16) acc += src[static_cast<int64_t>(g) * stride + col];
+    if (col < sg.len[k]) {
+        slab_col_sum(sg.slab[k] + sg.off[k], sg.G[k], sg.stride[k], col, w, acc);
+        if (sg.slab2[k]) slab_col_sum(sg.slab2[k] + sg.off2[k], sg.G2[k], sg.stride2[k], col, w, acc);
     }
     part[w][lane] = acc;
     __syncthreads();
-    if (w == 0 && col < len) {
+    if (w == 0 && col < sg.len[k]) {
         double s = part[0][lane];
         for (int i = 1; i < 16; ++i) s += part[i][lane];
         sg.out[k][col] = static_cast<float>(s);
     }
+}
+
+struct SegJob {
+    const float* slab;
+    int G;
+    int64_t stride;
+    LgSlabSeg seg;
+};
+struct DJob {
+    const double* dslab;
+    int G;
+    float* out;
+};
+
+// The reduce batch of this host thread (lg_reduce_batch_begin / _flush)
+struct Batch {
+    bool active = false;
+    std::vector<SegJob> segs;
+    std::vector<DJob> djobs;
+};
+thread_local Batch t_batch;
+
+int launch_jobs(const SegJob* segs, int nseg, const DJob* dj, int nd, hipStream_t s) {
+    Segs sg{};
+    int blocks = 0;
+    for (int i = 0; i < nseg; ++i) {
+        const SegJob& j = segs[i];
+        sg.slab[i] = j.slab;
+        sg.G[i] = j.G;
+        sg.stride[i] = j.stride;
+        sg.off[i] = j.seg.off;
+        sg.len[i] = j.seg.len;
+        sg.out[i] = j.seg.out;
+        sg.slab2[i] = j.seg.slab2;
+        sg.G2[i] = j.seg.G2;
+        sg.stride2[i] = j.seg.stride2;
+        sg.off2[i] = j.seg.off2;
+        sg.first[i] = blocks;
+        blocks += static_cast<int>((j.seg.len + 63) / 64);
+    }
+    sg.first[nseg] = blocks;
+    sg.n = nseg;
+    for (int d = 0; d < nd; ++d) {
+        sg.dslab[d] = dj[d].dslab;
+        sg.dG[d] = dj[d].G;
+        sg.dout[d] = dj[d].out;
+    }
+    sg.nd = nd;
+    const int total = blocks + nd;
+    if (total == 0) return LG_OK;
+    k_slab_reduce<<<total, 1024, 0, s>>>(sg);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+int launch_all(const std::vector<SegJob>& segs, const std::vector<DJob>& dj, hipStream_t s) {
+    size_t i = 0, d = 0;
+    while (i < segs.size() || d < dj.size()) {
+        const int ns = static_cast<int>(std::min<size_t>(kJobSegs, segs.size() - i));
+        const int nd = static_cast<int>(std::min<size_t>(kJobD, dj.size() - d));
+        const int rc = launch_jobs(segs.data() + i, ns, dj.data() + d, nd, s);
+        if (rc != LG_OK) return rc;
+        i += ns;
+        d += nd;
+    }
+    return LG_OK;
 }
 
 }  // namespace
@@ -74,27 +158,53 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(const float* __restrict__ 
 int lg_launch_slab_reduce_multi(const float* slab, int G, int64_t stride, const LgSlabSeg* segs, int nseg,
                                 const double* dslab, float* dout, hipStream_t s) {
     if (nseg < 0 || nseg > kLgMaxSlabSegs || G < 0 || (dslab && !dout)) return LG_EINVAL;
-    Segs sg{};
-    int blocks = 0, n = 0;
+    std::vector<SegJob> js;
+    std::vector<DJob> dj;
     for (int i = 0; i < nseg; ++i) {
         if (segs[i].out == nullptr || segs[i].len <= 0) continue;
-        sg.off[n] = segs[i].off;
-        sg.len[n] = segs[i].len;
-        sg.out[n] = segs[i].out;
-        sg.first[n] = blocks;
-        blocks += static_cast<int>((segs[i].len + 63) / 64);
-        ++n;
+        js.push_back(SegJob{slab, G, stride, segs[i]});
     }
-    sg.first[n] = blocks;
-    sg.n = n;
-    const int total = blocks + (dslab ? 1 : 0);
-    if (total == 0) return LG_OK;
-    k_slab_reduce<<<total, 1024, 0, s>>>(slab, G, stride, sg, dslab, dout);
-    LG_RET_IF_LAUNCH_FAILED();
-    return LG_OK;
+    if (dslab) dj.push_back(DJob{dslab, G, dout});
+    if (t_batch.active) {
+        t_batch.segs.insert(t_batch.segs.end(), js.begin(), js.end());
+        t_batch.djobs.insert(t_batch.djobs.end(), dj.begin(), dj.end());
+        return LG_OK;
+    }
+    return launch_all(js, dj, s);
 }
 
 int lg_launch_slab_reduce(const float* slab, int G, int64_t stride, int64_t len, float* out, hipStream_t s) {
     const LgSlabSeg seg{0, len, out};
     return lg_launch_slab_reduce_multi(slab, G, stride, &seg, 1, nullptr, nullptr, s);
+}
+
+bool lg_reduce_batch_pending(const float* out, const float** slab, int* G, int64_t* stride, int64_t* off) {
+    if (!t_batch.active || out == nullptr) return false;
+    for (const SegJob& j : t_batch.segs) {
+        if (j.seg.out == out && j.seg.slab2 == nullptr) {
+            *slab = j.slab;
+            *G = j.G;
+            *stride = j.stride;
+            *off = j.seg.off;
+            return true;
+        }
+    }
+    return false;
+}
+
+extern "C" int lg_reduce_batch_begin(void) {
+    if (t_batch.active) return LG_EINVAL;
+    t_batch.segs.clear();
+    t_batch.djobs.clear();
+    t_batch.active = true;
+    return LG_OK;
+}
+
+extern "C" int lg_reduce_batch_flush(lg_stream_t stream) {
+    if (!t_batch.active) return LG_EINVAL;
+    t_batch.active = false;
+    const int rc = launch_all(t_batch.segs, t_batch.djobs, lg_stream(stream));
+    t_batch.segs.clear();
+    t_batch.djobs.clear();
+    return rc;
 }

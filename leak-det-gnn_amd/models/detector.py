@@ -57,7 +57,9 @@ class SharedSensorGRUEncoder(nn.Module):
             raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 32/64, bias")
         f = ops._f32
         ws = [f(t) for t in (g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)]
-        tf = f(tfeat) if self.use_time else None
+        # contiguous once here: a strided tfeat (a slice of a longer segment) would otherwise be
+        # saved as is and copied again in the backward
+        tf = f(tfeat).contiguous() if self.use_time else None
         r = f(r)
         save = torch.is_grad_enabled() and any(t.requires_grad for t in [r, *ws] + ([tf] if tf is not None else []))
         return torch.ops.leakgnn.gru_encoder(r, tf, *ws, save)[0]

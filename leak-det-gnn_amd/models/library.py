@@ -22,6 +22,8 @@ draw fresh masks.
 """
 from __future__ import annotations
 
+import contextlib
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -306,6 +308,24 @@ def _gru_bwd(ctx, dh, _dhseq, _dgates):
 gru_encoder.register_autograd(_gru_bwd, setup_context=_gru_setup)
 
 
+REDUCE_BATCH = True  # tests switch it off to compare with one reduction launch per op
+
+
+@contextlib.contextmanager
+def _reduce_batch(lib, st):
+    """All slab reductions of the enclosed backward launches as one launch at the end
+    (lg_reduce_batch_begin / _flush, include/leakgnn.h).  The enclosed code keeps every
+    workspace it passes alive until the flush (they are locals of the caller)."""
+    if not REDUCE_BATCH:
+        yield
+        return
+    check(lib.lg_reduce_batch_begin(), "lg_reduce_batch_begin")
+    try:
+        yield
+    finally:
+        check(lib.lg_reduce_batch_flush(st), "lg_reduce_batch_flush")
+
+
 # ============================================================================ gnn_trunk
 @torch.library.custom_op(f"{NS}::gnn_trunk", mutates_args=(), device_types="cuda")
 def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor],
@@ -392,11 +412,30 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], h_s: Tensor, proj_wei
     scale = 1.0 / (1.0 - p) if p > 0.0 else 1.0
     dy = grad_out.contiguous()
     wsb = lib.lg_gcn_bwd_nm_workspace_bytes(D) if node_major else lib.lg_gcn_bwd_workspace_bytes(D)
-    ws = torch.empty(int(wsb), device=dev, dtype=torch.uint8)
+    # one workspace per layer: the layers' slab reductions run together at the batch flush
+    wss = [torch.empty(int(wsb), device=dev, dtype=torch.uint8) for _ in range(L)]
     dWs: List[Tensor] = [grad_out] * L
     dbs: List[Tensor] = [grad_out] * L
     dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
+    with _reduce_batch(lib, st):
+        dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx,
+                                                  nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
+                                                  node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st)
+    return dh_s, dWp, dbp, dWs, dbs
+
+
+def _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live,
+                             nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_major, bf16, scale, wss, dWs, dbs, dbias_ns,
+                             st):
+    L = len(weights)
+    dev = dy.device
+    if node_major:
+        N, B, D = xs[0].shape
+    else:
+        B, N, D = xs[0].shape
+    S, Ds = h_s.shape[1], h_s.shape[2]
     for l in range(L - 1, -1, -1):
+        ws = wss[l]
         flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
         dx = torch.empty_like(dy)
         dW = torch.empty(D, D, device=dev, dtype=torch.float32)
@@ -420,12 +459,13 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], h_s: Tensor, proj_wei
     dWp = torch.empty(D, Ds + 1, device=dev, dtype=torch.float32)
     dbp = torch.empty(D, device=dev, dtype=torch.float32)
     wsp = torch.empty(int(lib.lg_sensor_proj_bwd_workspace_bytes(B, S, Ds, D)), device=dev, dtype=torch.uint8)
+    wss.append(wsp)  # held by the caller until the reduce batch is flushed
     with _timed("linear_dw", dev):
         check(lib.lg_sensor_proj_bwd(ptr(dy), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
                                      ptr(h_s), ptr(proj_weight), ptr(dbias_ns), ptr(dh_s), ptr(dWp), ptr(dbp), B, N,
                                      S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), st),
               "lg_sensor_proj_bwd")
-    return dh_s, dWp, dbp, dWs, dbs
+    return dh_s, dWp, dbp
 
 
 @gnn_trunk_backward.register_fake
@@ -539,24 +579,34 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     dpipe = torch.empty(B, P, 2, D, device=dev)
     dw1, db1 = torch.empty_like(w1), torch.empty(hidden, device=dev)
     dw2, db2 = torch.empty_like(w2), torch.empty(1, device=dev)
-    ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
-    with _timed("edge_bwd", dev):
-        check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
-                                   ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe | lay, p_edge,
-                                   ptr(ws), st), "lg_edge_head_bwd")
-    dpooled = torch.empty(B, D, device=dev)
     ndw1, ndb1 = torch.empty_like(nw1), torch.empty(nhidden, device=dev)
     ndw2, ndb2 = torch.empty_like(nw2), torch.empty(1, device=dev)
+    ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
     wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
-    with _timed("pool_head_bwd", dev):
-        check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
-                                   ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn),
-                                   st), "lg_pool_head_bwd")
+    with _reduce_batch(lib, st):  # the EdgeHead's and the NoLeakHead's weight-grad reductions in one launch
+        dpooled = _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, P, B, N, D, hidden,
+                                           nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dw1, db1, dw2, db2, ndw1,
+                                           ndb1, ndw2, ndb2, ws, wsn, st)
     dh = torch.empty_like(h)
     with _timed("pipe_scatter", dev):
         check(lib.lg_pipe_scatter_bwd(ptr(inc_rowptr), ptr(inc_item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P, D,
                                       lay, st), "lg_pipe_scatter_bwd")
     return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
+
+
+def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, P, B, N, D, hidden, nhidden, fe,
+                             fn, p_edge, p_noleak, dpipe, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2, ws, wsn, st):
+    dev = h.device
+    with _timed("edge_bwd", dev):
+        check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
+                                   ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, p_edge,
+                                   ptr(ws), st), "lg_edge_head_bwd")
+    dpooled = torch.empty(B, D, device=dev)
+    with _timed("pool_head_bwd", dev):
+        check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
+                                   ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn),
+                                   st), "lg_pool_head_bwd")
+    return dpooled
 
 
 @detector_heads_backward.register_fake

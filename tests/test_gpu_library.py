@@ -190,3 +190,34 @@ def test_cross_entropy_matches_torch():
     t = torch.randint(0, 5, (8,), device=DEV)
     assert_close(CrossEntropyLoss(label_smoothing=0.1)(x, t), torch.nn.CrossEntropyLoss(label_smoothing=0.1)(x, t),
                  rtol=1e-6, what="fallback")
+
+
+def test_reduce_batch_matches_per_op_reductions():
+    """The backward ops' slab reductions merged into one launch per op group
+    (lg_reduce_batch_begin / _flush; the trunk's layer-0 node-bias partials folded into the
+    sensor projection's bias reduction) give the same gradients as one reduction launch per
+    op: bitwise, except sensor_to_node.bias, whose two partial sets are now summed in one
+    fp64 column instead of through a float intermediate."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    torch.manual_seed(3)
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
+    r = torch.randn(64, 36, 29, device=DEV)
+    tf = torch.randn(64, 36, 9, device=DEV)
+    grads = []
+    for batched in (True, False):
+        library.REDUCE_BATCH = batched
+        try:
+            m.zero_grad(set_to_none=True)
+            torch.manual_seed(11)
+            m(r, tf).square().mean().backward()
+            torch.cuda.synchronize()
+        finally:
+            library.REDUCE_BATCH = True
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    for n, g in grads[0].items():
+        ref = grads[1][n]
+        if n == "sensor_to_node.bias":
+            assert_close(g, ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item(), what=n)
+        else:
+            assert torch.equal(g, ref), f"{n}: batched reduction differs"
