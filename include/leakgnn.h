@@ -175,13 +175,27 @@ int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
                    void* workspace, lg_stream_t stream);
 
 /* Node table of the node-major kernels, once per graph (and once for the transposed CSR):
- * one 64-byte record per node = {e0, e1, (col, float_as_int(w)) x 6, self, 0} so a tile
+ * one 64-byte record per node = {e0, e1, (col, float_as_int(w)) x 6, self, node} so a tile
  * reads its CSR row with ONE scalar load.  self = position (< 6) of the row's entry whose
- * col is the node itself, -1 if none inline.
+ * col is the node itself, -1 if none inline.  Two sections (ABI 13): records 0 .. N-1 in
+ * node order, then records N .. 2N-1 in the SCHEDULE order `order` (node order[i] at
+ * N + i; NULL = node order), the order in which lg_gcn_fwd_nm / lg_gcn_bwd_nm visit
+ * nodes.  The order changes which tiles are in flight together, never a result: with a
+ * bandwidth-reducing order (lg_rcm_order) the neighbour rows a tile gathers were gathered
+ * by tiles just before it and still sit in L2.
  *   rowptr : int32 [N+1];  pairs : int32 [2 * nnz] (col, float_as_int(w));
- *   nodetab : int32 [N][16] (64-byte aligned). */
-int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, int32_t* nodetab,
-                      lg_stream_t stream);
+ *   order : NULL or device int32 [N], a permutation of 0 .. N-1;
+ *   nodetab : int32 [2N][16] (64-byte aligned). */
+int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, const int32_t* order,
+                      int32_t* nodetab, lg_stream_t stream);
+
+/* Reverse Cuthill-McKee order of the undirected graph edge_index (HOST memory, int64
+ * [2][E], self loops and duplicates ignored): order[i] = the node visited i-th.  Each
+ * connected component is a breadth-first sweep from a minimum-degree node, neighbours
+ * by increasing degree (ties by id), the whole sequence reversed.  Deterministic.  Used as
+ * the node-major kernels' schedule order (lg_nm_table_build): on L-TOWN-A it cuts the
+ * largest |u - v| over the pipes from 656 to 27.  Returns LG_EINVAL on bad ids. */
+int lg_rcm_order(const int64_t* edge_index, int64_t E, int64_t N, int32_t* order);
 
 /* Pipe-endpoint incidence CSR, once per model (backward of detector.py:206-210).
  *   ends : int64 [P][2] device (pipe_ends, utils.py:352-358)
@@ -272,8 +286,9 @@ int lg_gcn_fwd(const int32_t* rowptr, const int32_t* col, const float* w,
  * Every window shares the graph, so a 16-row tile is one node and 16 consecutive
  * windows, and each CSR entry (m, w) names one contiguous 16 x D block of x — the
  * entry is wave-uniform and the row loads need no per-lane index arithmetic.
- *   nodetab : int32 [N][16] from lg_nm_table_build (one 64-byte record per node:
- *             e0, e1, the first 6 (col, w) pairs of the row, self position);
+ *   nodetab : int32 [2N][16] from lg_nm_table_build (one 64-byte record per node:
+ *             e0, e1, the first 6 (col, w) pairs of the row, self position, node id;
+ *             tiles are visited in the table's schedule order);
  *   pairs : int32 [2 * nnz] interleaved (col, float_as_int(w)) of the lg_graph_build CSR.
  *   Dropout: row-stream masks indexed by the window-major row b*N + n (the mask of
  *   lg_gcn_fwd for the same seed/salt).

@@ -519,7 +519,7 @@ k_gcn_fwd_nm2(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 constexpr int kNm3Npf = 4;
 
 struct NmRec {  // one node-table record (wave-uniform, SGPRs)
-    int e0, e1, self;
+    int e0, e1, self, node;
     int2 p[kLgNmInline];
 };
 
@@ -536,6 +536,7 @@ __device__ __forceinline__ NmRec nm_rec(const int32_t* __restrict__ tab, uint32_
     r.p[4] = int2{c.z, c.w};
     r.p[5] = int2{d.x, d.y};
     r.self = d.z;
+    r.node = d.w;
     return r;
 }
 static_assert(kLgNmInline == 6, "nm_rec unpacks six inline pairs");
@@ -612,6 +613,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     NmRec cur;
     uint32_t cn, cb0, cnb;
     auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+        n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
@@ -633,7 +635,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     {
         uint32_t n0, b00, nb00;
         tile_coords(t0, n0, b00, nb00);
-        issue(nm_rec(tab, n0), n0, b00, nb00);
+        issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
     }
 
     // W (x dropout scale fold) and bias to LDS, after the first tile's loads are out
@@ -680,7 +682,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         // the next tile's record goes in flight while this tile's rows are waited for
         uint32_t nn, nb0, nnb;
         tile_coords(tile + sc.stride, nn, nb0, nnb);
-        const NmRec nxt = nm_rec(tab, nn);
+        const NmRec nxt = nm_rec(tab, N + nn);
         asm volatile("" ::: "memory");  // keep the request here: the compiler would sink it to its use
         // CSR order from 0: the first term is the product itself (an absent first neighbour
         // loaded zeros, and its weight is taken as 0), the rest fma'd in
@@ -1090,6 +1092,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     NmRec cur;
     uint32_t cn, cb0;
     auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+        n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
@@ -1112,7 +1115,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     {
         uint32_t n0, b00, nb00;
         tile_coords(sc.first, n0, b00, nb00);
-        issue(nm_rec(tab, n0), n0, b00, nb00);
+        issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
     }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
     {
@@ -1160,7 +1163,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
         uint32_t nn, nb0, nnb;
         tile_coords(tile + sc.stride, nn, nb0, nnb);
-        const NmRec nxt = nm_rec(tab, nn);
+        const NmRec nxt = nm_rec(tab, N + nn);
         asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
         f32x4 acc[G::K], xv[G::K];
 #pragma unroll

@@ -5,6 +5,10 @@
 // atomics, then a per-row insertion sort that restores ascending edge order so the
 // CSR is bit-identical from run to run and visits each row's entries in the order
 // PyG's scatter_add does (edges ascending, appended self loop last).
+#include <algorithm>
+#include <utility>
+#include <vector>
+
 #include "common.h"
 
 namespace {
@@ -157,10 +161,12 @@ __global__ void k_batchify(const int64_t* __restrict__ ei, int64_t E, int64_t N,
 // load (s_load_dwordx16) per tile: {e0, e1, (col, w bits) x kLgNmInline, self, 0}.
 // self = position k < kLgNmInline of the entry whose col is the node itself (-1: none
 // inline); the backward reads that entry's block as the tile's own dz rows.
+// thread i writes record i (node i) and record N + i (node order[i], the schedule section)
 __global__ void k_nm_table(const int32_t* __restrict__ rowptr, const int2* __restrict__ pairs, int64_t N,
-                           int32_t* __restrict__ tab) {
-    const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (n >= N) return;
+                           const int32_t* __restrict__ order, int32_t* __restrict__ tab) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= 2 * N) return;
+    const int64_t n = i < N ? i : (order ? order[i - N] : i - N);
     const int e0 = rowptr[n], e1 = rowptr[n + 1];
     int v[16];
     v[0] = e0;
@@ -175,8 +181,8 @@ __global__ void k_nm_table(const int32_t* __restrict__ rowptr, const int2* __res
         if (have && self < 0 && p.x == static_cast<int>(n)) self = k;
     }
     v[2 + 2 * kLgNmInline] = self;
-    v[3 + 2 * kLgNmInline] = 0;
-    int4* o = reinterpret_cast<int4*>(tab + 16 * n);
+    v[3 + 2 * kLgNmInline] = static_cast<int>(n);
+    int4* o = reinterpret_cast<int4*>(tab + 16 * i);
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = int4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
 }
@@ -268,11 +274,59 @@ extern "C" int lg_batchify_edge_index(const int64_t* edge_index, int64_t E, int6
     return LG_OK;
 }
 
-extern "C" int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, int32_t* nodetab,
-                                 lg_stream_t stream) {
-    if (N <= 0 || N > INT32_MAX / 16 || !rowptr || !pairs || !nodetab) return LG_EINVAL;
-    k_nm_table<<<nblocks(N), kThreads, 0, lg_stream(stream)>>>(rowptr, reinterpret_cast<const int2*>(pairs), N,
-                                                               nodetab);
+extern "C" int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, const int32_t* order,
+                                 int32_t* nodetab, lg_stream_t stream) {
+    if (N <= 0 || N > INT32_MAX / 32 || !rowptr || !pairs || !nodetab) return LG_EINVAL;
+    k_nm_table<<<nblocks(2 * N), kThreads, 0, lg_stream(stream)>>>(rowptr, reinterpret_cast<const int2*>(pairs), N,
+                                                                   order, nodetab);
     LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_rcm_order(const int64_t* edge_index, int64_t E, int64_t N, int32_t* order) {
+    if (N <= 0 || N > INT32_MAX / 2 || E < 0 || !order || (E > 0 && !edge_index)) return LG_EINVAL;
+    // undirected adjacency without self loops / duplicates, CSR sorted by neighbour id
+    std::vector<std::pair<int32_t, int32_t>> und;
+    und.reserve(2 * static_cast<size_t>(E));
+    for (int64_t e = 0; e < E; ++e) {
+        const int64_t u = edge_index[e], v = edge_index[E + e];
+        if (u < 0 || u >= N || v < 0 || v >= N) return LG_EINVAL;
+        if (u == v) continue;
+        und.emplace_back(static_cast<int32_t>(u), static_cast<int32_t>(v));
+        und.emplace_back(static_cast<int32_t>(v), static_cast<int32_t>(u));
+    }
+    std::sort(und.begin(), und.end());
+    und.erase(std::unique(und.begin(), und.end()), und.end());
+    std::vector<int64_t> rp(N + 1, 0);
+    for (const auto& uv : und) ++rp[uv.first + 1];
+    for (int64_t n = 0; n < N; ++n) rp[n + 1] += rp[n];
+    std::vector<int32_t> deg(N);
+    for (int64_t n = 0; n < N; ++n) deg[n] = static_cast<int32_t>(rp[n + 1] - rp[n]);
+    // component starts: nodes by (degree, id)
+    std::vector<int32_t> by_deg(N);
+    for (int64_t n = 0; n < N; ++n) by_deg[n] = static_cast<int32_t>(n);
+    std::stable_sort(by_deg.begin(), by_deg.end(), [&](int32_t a, int32_t b) { return deg[a] < deg[b]; });
+    std::vector<char> seen(N, 0);
+    std::vector<int32_t> seq;
+    seq.reserve(N);
+    std::vector<int32_t> nb;
+    for (int32_t s : by_deg) {
+        if (seen[s]) continue;
+        seen[s] = 1;
+        size_t head = seq.size();
+        seq.push_back(s);
+        while (head < seq.size()) {
+            const int32_t u = seq[head++];
+            nb.clear();
+            for (int64_t k = rp[u]; k < rp[u + 1]; ++k)
+                if (!seen[und[k].second]) nb.push_back(und[k].second);
+            std::stable_sort(nb.begin(), nb.end(), [&](int32_t a, int32_t b) { return deg[a] < deg[b]; });
+            for (int32_t v : nb) {
+                seen[v] = 1;
+                seq.push_back(v);
+            }
+        }
+    }
+    for (int64_t i = 0; i < N; ++i) order[i] = seq[N - 1 - i];
     return LG_OK;
 }

@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 12  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 13  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -49,7 +49,8 @@ SIGNATURES = {
     "lg_timing_elapsed": (_i32, [_i32, _p]),
     "lg_graph_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _p]),
-    "lg_nm_table_build": (_i32, [_p, _p, _i64, _p, _p]),
+    "lg_nm_table_build": (_i32, [_p, _p, _i64, _p, _p, _p]),
+    "lg_rcm_order": (_i32, [_p, _i64, _i64, _p]),
     "lg_incidence_workspace_bytes": (_i64, [_i64, _i64]),
     "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
     "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),

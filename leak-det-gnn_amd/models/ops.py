@@ -157,8 +157,9 @@ class GCNGraph:
     w_t: torch.Tensor
     pairs: Optional[torch.Tensor] = None    # int32 (cap, 2): (col, float bits of w), node-major kernels
     pairs_t: Optional[torch.Tensor] = None  # same for the transposed CSR
-    nodetab: Optional[torch.Tensor] = None    # int32 (N, 16): node-major kernels' per-node record
+    nodetab: Optional[torch.Tensor] = None    # int32 (2N, 16): node-major kernels' per-node records
     nodetab_t: Optional[torch.Tensor] = None  # same for the transposed CSR
+    order: Optional[torch.Tensor] = None      # int32 (N,): their schedule order (reverse Cuthill-McKee)
 
 
     @staticmethod
@@ -183,12 +184,26 @@ class GCNGraph:
         g._keepalive = (ei, ws)  # freed after the stream consumes them
         g.pairs = torch.stack([g.col, g.w.view(torch.int32)], dim=1).contiguous()
         g.pairs_t = torch.stack([g.col_t, g.w_t.view(torch.int32)], dim=1).contiguous()
-        g.nodetab = torch.empty(N, 16, **i32)
-        g.nodetab_t = torch.empty(N, 16, **i32)
-        check(lib.lg_nm_table_build(ptr(g.rowptr), ptr(g.pairs), N, ptr(g.nodetab), stream_of(ei)), "lg_nm_table_build")
-        check(lib.lg_nm_table_build(ptr(g.rowptr_t), ptr(g.pairs_t), N, ptr(g.nodetab_t), stream_of(ei)),
+        # node-major schedule order: reverse Cuthill-McKee (host, once per graph), so a tile's
+        # neighbour rows were gathered by the tiles just before it (L2 reuse); results do
+        # not depend on it
+        g.order = schedule_order(edge_index, N).to(device)
+        g.nodetab = torch.empty(2 * N, 16, **i32)
+        g.nodetab_t = torch.empty(2 * N, 16, **i32)
+        check(lib.lg_nm_table_build(ptr(g.rowptr), ptr(g.pairs), N, ptr(g.order), ptr(g.nodetab), stream_of(ei)),
               "lg_nm_table_build")
+        check(lib.lg_nm_table_build(ptr(g.rowptr_t), ptr(g.pairs_t), N, ptr(g.order), ptr(g.nodetab_t),
+                                    stream_of(ei)), "lg_nm_table_build")
         return g
+
+
+def schedule_order(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
+    """int32 (N,) reverse Cuthill-McKee order of the graph (lg_rcm_order, host)."""
+    ei = edge_index.detach().to("cpu", torch.long).contiguous()
+    order = torch.empty(int(num_nodes), dtype=torch.int32)
+    check(load_library().lg_rcm_order(ei.data_ptr() if ei.numel() else None, int(ei.size(1)), int(num_nodes),
+                                      order.data_ptr()), "lg_rcm_order")
+    return order
 
 
 @dataclass

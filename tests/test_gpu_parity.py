@@ -646,3 +646,49 @@ def test_gcn_node_major_high_degree_graph(D):
         ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(W), ops.ptr(b),
                                     ops.ptr(ys), B, N, D, graph.nnz_cap, flags, 0.2, 5, 3, st), "fwd_nm split")
         assert (ys.double() - yn.double()).abs().max().item() <= 1e-6 * yn.abs().amax().item()
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_gcn_node_major_schedule_order_changes_no_result(drop):
+    """The node table's schedule section (reverse Cuthill-McKee order, lg_rcm_order) only
+    reorders tiles: forward y and backward dx are bit-identical to the node-order schedule;
+    dW / db / node bias (other slab groupings) within 1e-6 of scale."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    N, B, D = 661, 48, 64
+    graph = GCNGraph.build(torch.from_numpy(load("graph_ltown_a.npz")["edge_index"]), N, DEV)
+    assert not torch.equal(graph.order.cpu(), torch.arange(N, dtype=torch.int32))
+    st = ops.stream_of(graph.w)
+    tab_id, tab_id_t = torch.empty_like(graph.nodetab), torch.empty_like(graph.nodetab_t)
+    ops.check(lib.lg_nm_table_build(ops.ptr(graph.rowptr), ops.ptr(graph.pairs), N, None, ops.ptr(tab_id), st), "t")
+    ops.check(lib.lg_nm_table_build(ops.ptr(graph.rowptr_t), ops.ptr(graph.pairs_t), N, None, ops.ptr(tab_id_t), st),
+              "t")
+    gen = torch.Generator().manual_seed(5 + drop)
+    x = torch.randn(N, B, D, generator=gen).relu().to(DEV)
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    b = (torch.randn(D, generator=gen) / 4).to(DEV)
+    dy = torch.randn(N, B, D, generator=gen).to(DEV)
+    slot = torch.full((N,), -1, dtype=torch.int32)
+    slot[:29] = torch.arange(29, dtype=torch.int32)
+    slot = slot.to(DEV)
+    flags = ops.nat.LG_F_BIAS | ops.nat.LG_F_RELU | (ops.nat.LG_F_DROPOUT if drop else 0)
+    p = 0.1 if drop else 0.0
+    res = []
+    for tab, tab_t in ((graph.nodetab, graph.nodetab_t), (tab_id, tab_id_t)):
+        y = torch.empty_like(x)
+        ops.check(lib.lg_gcn_fwd_nm(ops.ptr(tab), ops.ptr(graph.pairs), ops.ptr(x), ops.ptr(W), ops.ptr(b), ops.ptr(y),
+                                    B, N, D, graph.nnz_cap, flags, p, 77, 1, st), "fwd")
+        dx = torch.empty_like(x)
+        dW, db, dnb = torch.empty(D, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV)
+        ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+        sc = 1.0 / 0.9 if drop else 1.0
+        ops.check(lib.lg_gcn_bwd_nm(ops.ptr(tab_t), ops.ptr(graph.pairs_t), ops.ptr(dy), ops.ptr(y), ops.ptr(x),
+                                    ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db), ops.ptr(slot), ops.ptr(dnb), B, N,
+                                    D, ops.nat.LG_F_MASK_IN | ops.nat.LG_F_MASK_OUT, sc, sc, ops.ptr(ws), st), "bwd")
+        torch.cuda.synchronize()
+        res.append((y, dx, dW, db, dnb))
+    assert torch.equal(res[0][0], res[1][0]), "schedule order changed the forward"
+    assert torch.equal(res[0][1], res[1][1]), "schedule order changed dx"
+    for k, name in ((2, "dW"), (3, "db"), (4, "node bias")):
+        assert_close(res[0][k], res[1][k], rtol=1e-6, atol=1e-7, what=name)

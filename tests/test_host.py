@@ -105,9 +105,9 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 12
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 13
     assert lib.lg_timing_arm(-1) == -1 and lib.lg_timing_disarm() == 0 and lib.lg_timing_elapsed(0, None) == -1
-    assert lib.lg_nm_table_build(None, None, 661, None, None) == -1
+    assert lib.lg_nm_table_build(None, None, 661, None, None, None) == -1
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
     assert lib.lg_graph_workspace_bytes(1532, 661) >= 4 * (5 * 661 + 2 * (1532 + 661))
     assert lib.lg_graph_workspace_bytes(-1, 5) == -1
@@ -162,3 +162,29 @@ def test_seed_pointer_salt_bit_matches_header():
     hdr = (Path(__file__).resolve().parents[1] / "include" / "leakgnn.h").read_text()
     m = re.search(r"#define LG_SALT_SEED_PTR (0x[0-9a-fA-F]+)u", hdr)
     assert m and int(m.group(1), 16) == _native.LG_SALT_SEED_PTR == 1 << 31
+
+
+def test_rcm_schedule_order():
+    """lg_rcm_order (host): a permutation, deterministic, bandwidth-reducing on L-TOWN-A
+    (largest |u - v| over the pipes 656 -> <= 32), self loops / duplicates / isolated nodes
+    and a second component handled, out-of-range ids refused."""
+    from models import _native, ops
+    with np.load(REPO / "tests" / "golden" / "graph_ltown_a.npz") as g:
+        ei = g["edge_index"]
+    o = ops.schedule_order(torch.from_numpy(ei), 661).numpy()
+    assert sorted(o.tolist()) == list(range(661))
+    assert np.array_equal(o, ops.schedule_order(torch.from_numpy(ei), 661).numpy())
+    inv = np.empty(661, np.int64)
+    inv[o] = np.arange(661)
+    assert np.abs(ei[0] - ei[1]).max() > 600
+    assert np.abs(inv[ei[0]] - inv[ei[1]]).max() <= 32
+    # path 0-2-4 plus self loop and duplicate, a separate edge 1-3, isolated node 5
+    small = torch.tensor([[0, 2, 2, 4, 1, 0], [2, 4, 0, 4, 3, 2]])
+    o = ops.schedule_order(small, 6).numpy()
+    assert sorted(o.tolist()) == list(range(6))
+    pos = {int(n): i for i, n in enumerate(o)}
+    assert abs(pos[0] - pos[2]) == 1 and abs(pos[2] - pos[4]) == 1 and abs(pos[1] - pos[3]) == 1
+    lib = _native.load_library()
+    bad = torch.tensor([[0], [7]], dtype=torch.long)
+    out = torch.empty(6, dtype=torch.int32)
+    assert lib.lg_rcm_order(bad.data_ptr(), 1, 6, out.data_ptr()) == -1
