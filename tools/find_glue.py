@@ -40,13 +40,19 @@ torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
     step()
     torch.cuda.synchronize()
-evs = prof.events()
-for e in evs:
-    ks = [k for k in getattr(e, "kernels", []) if "anonymous namespace" not in k.name]
-    if e.device_type == torch.autograd.DeviceType.CPU and ks:
-        chain, p = [], e.cpu_parent
-        while p is not None and len(chain) < 5:
-            chain.append(p.name)
-            p = p.cpu_parent
-        for k in ks:
-            print(f"{k.name[:60]:60s} | {e.name} <- {' <- '.join(chain)}")
+import json
+import tempfile
+path = tempfile.mktemp(suffix=".json")
+prof.export_chrome_trace(path)
+tr = json.load(open(path))["traceEvents"]
+ops = {}
+for e in tr:
+    if e.get("cat") == "cpu_op" and "External id" in e.get("args", {}):
+        ops.setdefault(e["args"]["External id"], []).append(e)
+for e in sorted((e for e in tr if e.get("cat") == "kernel"), key=lambda e: e["ts"]):
+    if "anonymous namespace" in e["name"]:
+        print(f"   ours {e['name'][:60]}")
+        continue
+    ext = e.get("args", {}).get("External id")
+    names = [o["name"] for o in ops.get(ext, [])]
+    print(f"GLUE {e['name'][:60]:60s} {e.get('dur')} us <- {names}")
