@@ -105,6 +105,11 @@ int lg_abi_version(void);
  * flush: LG_EINVAL when none is. */
 int lg_reduce_batch_begin(void);
 int lg_reduce_batch_flush(lg_stream_t stream);
+
+/* Measurement helper (bench.py's stream_copy, the achievable-HBM reference beside the
+ * 8 TB/s roofline): dst = src over `bytes` (a multiple of 16) with 16-byte non-temporal
+ * loads and stores.  No reference counterpart. */
+int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stream_t stream);
 const char* lg_strerror(int code);
 
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;

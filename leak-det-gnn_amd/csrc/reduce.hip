@@ -208,3 +208,33 @@ extern "C" int lg_reduce_batch_flush(lg_stream_t stream) {
     t_batch.djobs.clear();
     return rc;
 }
+
+// ---------------------------------------------------------------- measured copy peak
+// The box's achievable HBM rate for a read + write stream (bench.py stream_copy): 16-byte
+// non-temporal loads and stores, four in flight per lane, grid-stride over the buffer.
+namespace {
+__global__ void __launch_bounds__(256) k_stream_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                     int64_t n4) {
+    constexpr int U = 4;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+    int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+    }
+    for (; i < n4; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+}  // namespace
+
+extern "C" int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stream_t stream) {
+    if (bytes < 0 || (bytes % 16) != 0 || (bytes > 0 && (!src || !dst))) return LG_EINVAL;
+    if (bytes == 0) return LG_OK;
+    const int64_t n4 = bytes / 16;
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 16LL * lg_num_cus())));
+    k_stream_copy<<<grid, 256, 0, lg_stream(stream)>>>(static_cast<const f32x4*>(src), static_cast<f32x4*>(dst), n4);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
