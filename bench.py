@@ -624,7 +624,8 @@ def main() -> None:
     D = 64
     csr_bytes = 4 * (N + 1) + 8 * E1
     fwd_bytes = 8 * B * N * D + csr_bytes           # read x once, write y once
-    bwd_bytes = 16 * B * N * D + csr_bytes          # layer-L-1 backward: read dy, y (mask), x; write dx
+    # layer-L-1 backward: read dy, x and the forward's [y > 0] bits (B*N*D/8 bytes); write dx
+    bwd_bytes = 12 * B * N * D + N * ((B + 15) // 16) * 128 + csr_bytes
     fwd_ms, bwd_ms = kms["gcn_fwd"], kms["gcn_bwd"]
     achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
@@ -656,8 +657,9 @@ def main() -> None:
                      "traffic_source": src if traffic else None,
                      "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2),
                      "frac_of_measured_copy": round(achieved / copy["GBps"], 4)},
-        "roofline_bwd": {"kernel": "lg_gcn_bwd_nm (layer 2: gather of dy * [y > 0] over the transposed CSR, "
-                                   "dx = t W, dW, db, masked by [x > 0])", "bound": "hbm",
+        "roofline_bwd": {"kernel": "lg_gcn_bwd_nm_bits (layer 2: gather of dy * [y > 0] over the transposed CSR, "
+                                   "[y > 0] from the forward's mask bits; dx = t W, dW, db, masked by [x > 0])",
+                         "bound": "hbm",
                          "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic_bwd["bytes"]) if traffic_bwd else None,

@@ -311,6 +311,23 @@ int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float*
                   const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
                   int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream);
 
+/* The layer's output mask as bits (ABI 15).  lg_gcn_fwd_nm_bits = lg_gcn_fwd_nm that also
+ * writes ymask (when non-NULL): [y > 0] of every output element, one uint16 per lane and
+ * 16-row tile (node n, window group g = b / 16): bit 4k + i of lane l at
+ * ((n * ceil(B/16) + g) * 64 + l) * 2 bytes is row g*16 + (64/(D/4)) k + l / (D/4), channel
+ * 4 (l % (D/4)) + i  ->  N * ceil(B/16) * 128 bytes (1/32 of y).  lg_gcn_bwd_nm_bits =
+ * lg_gcn_bwd_nm that, under LG_F_MASK_IN with ymask non-NULL, reads the mask from those
+ * bits instead of gathering y (y may then be NULL).  Same results as the y path. */
+int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
+                       const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
+                       int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream,
+                       uint16_t* ymask);
+int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
+                       const float* x, const float* W, float* dx_out, float* dW, float* db,
+                       const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
+                       int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream,
+                       const uint16_t* ymask);
+
 /* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
  * weights; no transform).  Used for the HBM-roofline stress case (config C5). */
 int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,

@@ -559,6 +559,18 @@ __device__ __forceinline__ void pk_fma4(f32x4& a, float w, const f32x4& v) {
     a = f32x4{lo[0], lo[1], hi[0], hi[1]};
 }
 
+// Output mask of a layer (ymask, lg_gcn_fwd_nm_bits): per 16-row tile (node n, window
+// group g) one uint16 per lane of the gather layout, bit 4 k + i = [y > 0] of the lane's
+// slot k, element i; 128 bytes per tile at ((n * ngroups + g) * 64 + lane) * 2.  The
+// backward reads it instead of gathering y (1/32 of the bytes).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nm_mask_rsrc(const uint16_t* p, uint32_t N, uint32_t ngroups) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p), static_cast<short>(0),
+                                             static_cast<int>(static_cast<uint64_t>(N) * ngroups * 128u), 0x00020000);
+}
+__device__ __forceinline__ uint32_t nm_mask_off(uint32_t n, uint32_t grp, uint32_t ngroups, int lane) {
+    return (n * ngroups + grp) * 128u + 2u * static_cast<uint32_t>(lane);
+}
+
 // Out-of-range offsets of the nm3 addressing: a lane offset of a masked row is kNm3RowOob
 // and an absent neighbour's block base is kNm3BlkOob, so lane + base lands past
 // num_records (<= kNm3MaxBytes) with ONE v_add per load and no wrap-around.
@@ -576,7 +588,7 @@ __global__ void __launch_bounds__(64 * WAVES, WAVES >= 5 ? 4 : 1)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
-              uint32_t salt) {
+              uint32_t salt, uint16_t* __restrict__ ymask) {
     using G = NmGeo<D>;
     using LY = Nm3Lds<D, SPLIT, WAVES>;
     constexpr int SB = LY::SB;
@@ -593,6 +605,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     float* tl = tiles + wave * G::TILE;
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
@@ -835,13 +848,19 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
             wave_sync_nm();
-            if (do_store)
+            uint32_t bits = 0;  // [y > 0] of this lane's 4 K elements (bit 4 k + i), for ymask
 #pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t,
-                                           ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg)),
-                        yrs, tlo[k] + ob, 0, 0);
+            for (int k = 0; k < G::K; ++k) {
+                const f32x4 v = ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg);
+                if (do_store)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                           yrs, tlo[k] + ob, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
+            }
+            if (ymask)
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs,
+                                                      nm_mask_off(n, b0 >> 4, ngroups, lane), 0, 0);
         }
     }
 }
@@ -1037,16 +1056,21 @@ struct Nb3Lds {
     static constexpr size_t BYTES = 4 * static_cast<size_t>(WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L);
 };
 
-template <int D, bool MASK_IN, bool NB, bool BF = false>  // BF: LG_F_BF16, single-product MFMAs
+// MB (with MASK_IN): the layer's output mask comes as the forward's ymask bits instead of a
+// gather of y, so the prefetch keeps the unmasked depth
+template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false>  // BF: LG_F_BF16, single-product MFMAs
 __global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
 k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
               const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
               const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
-              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out) {
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out,
+              const uint16_t* __restrict__ ymask) {
+    static_assert(!MB || MASK_IN, "mask bits replace the y gather of MASK_IN");
+    constexpr bool MY = MASK_IN && !MB;  // mask from gathered y rows
     using G = NmGeo<D>;
     using LY = Nb3Lds<D, MASK_IN>;
     constexpr int SB = LY::SB;
-    constexpr int NPF = MASK_IN ? 2 : 4;
+    constexpr int NPF = MY ? 2 : 4;
     constexpr int L = LY::L;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // 3 x W^T [in][out] bf16, stride SB
@@ -1058,8 +1082,9 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     float* tl = tiles + wave * LY::TL;  // t tile [row][feature], later dx
     float* xl = tl + G::TILE;           // x tile [row][feature]
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MASK_IN ? yv : dy, bytes),
+    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MY ? yv : dy, bytes),
                                  xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
+    const __amdgpu_buffer_rsrc_t mbs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
@@ -1085,9 +1110,22 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int c = 0; c < 4; ++c) r[c] = m[c] > 0.f ? g[c] * scale_in : 0.f;
         return r;
     };
+    // the same from mask bits (slot k of the lane)
+    auto dzb = [&](const f32x4& g, uint32_t bits, int k) {
+        f32x4 r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) r[c] = (bits >> (4 * k + c)) & 1u ? g[c] * scale_in : 0.f;
+        return r;
+    };
+    // mask bits of the 16-row block of node m in window group grp (0 for an absent block)
+    auto ldb = [&](uint32_t m, uint32_t grp, bool have) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b16(mbs, have ? nm_mask_off(m, grp, ngroups, lane) : kNm3BlkOob + 2u * lane,
+                                                    0, 0);
+    };
 
     // tile in flight: record, coordinates, lane offsets, first NPF neighbour blocks, own x block
-    f32x4 pf[NPF][G::K], pm[MASK_IN ? NPF : 1][G::K], px[G::K];
+    f32x4 pf[NPF][G::K], pm[MY ? NPF : 1][G::K], px[G::K];
+    uint32_t pmb[MB ? NPF : 1];
     uint32_t lo[G::K];
     NmRec cur;
     uint32_t cn, cb0;
@@ -1108,8 +1146,9 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
             for (int k = 0; k < G::K; ++k) {
                 pf[i][k] = ld(dys, lo[k] + base);
-                if constexpr (MASK_IN) pm[i][k] = ld(ms, lo[k] + base);
+                if constexpr (MY) pm[i][k] = ld(ms, lo[k] + base);
             }
+            if constexpr (MB) pmb[i] = ldb(static_cast<uint32_t>(r.p[i].x), b0 >> 4, have);
         }
     };
     {
@@ -1177,7 +1216,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 const float w = __int_as_float(cur.p[i].y);
 #pragma unroll
                 for (int k = 0; k < G::K; ++k) {
-                    const f32x4 z = dzf(pf[i][k], MASK_IN ? pm[i < (MASK_IN ? NPF : 1) ? i : 0][k] : pf[i][k]);
+                    const f32x4 z = MB ? dzb(pf[i][k], pmb[MB ? i : 0], k)
+                                       : dzf(pf[i][k], MY ? pm[i < (MY ? NPF : 1) ? i : 0][k] : pf[i][k]);
                     pk_fma4(acc[k], w, z);
                     if (i == self) dbacc += z;
                 }
@@ -1195,12 +1235,13 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
                     for (int k = 0; k < G::K; ++k) {
                         va[k] = ld(dys, tlo[k] + ba);
-                        vm[k] = MASK_IN ? ld(ms, tlo[k] + ba) : va[k];
+                        vm[k] = MY ? ld(ms, tlo[k] + ba) : va[k];
                     }
+                    const uint32_t bm = MB ? ldb(static_cast<uint32_t>(ip[i].x), b0 >> 4, true) : 0u;
                     const float wa = __int_as_float(ip[i].y);
 #pragma unroll
                     for (int k = 0; k < G::K; ++k) {
-                        const f32x4 z = dzf(va[k], vm[k]);
+                        const f32x4 z = MB ? dzb(va[k], bm, k) : dzf(va[k], vm[k]);
                         pk_fma4(acc[k], wa, z);
                         if (NPF + i == self) dbacc += z;
                     }
@@ -1213,17 +1254,20 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
                 for (int k = 0; k < G::K; ++k) {
                     va[k] = ld(dys, tlo[k] + ba);
-                    vm[k] = MASK_IN ? ld(ms, tlo[k] + ba) : va[k];
+                    vm[k] = MY ? ld(ms, tlo[k] + ba) : va[k];
                 }
+                const uint32_t bm = MB ? ldb(static_cast<uint32_t>(pa.x), b0 >> 4, true) : 0u;
                 const float wa = __int_as_float(pa.y);
 #pragma unroll
-                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, dzf(va[k], vm[k]));
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, MB ? dzb(va[k], bm, k) : dzf(va[k], vm[k]));
             }
         }
         if (self < 0) {  // no self entry among the inline pairs: the own dz rows explicitly
             const uint32_t ob = (n * B + b0) * (4u * D);
+            const uint32_t bo = MB ? ldb(n, b0 >> 4, true) : 0u;
 #pragma unroll
-            for (int k = 0; k < G::K; ++k) dbacc += dzf(ld(dys, tlo[k] + ob), MASK_IN ? ld(ms, tlo[k] + ob) : f32x4{});
+            for (int k = 0; k < G::K; ++k)
+                dbacc += MB ? dzb(ld(dys, tlo[k] + ob), bo, k) : dzf(ld(dys, tlo[k] + ob), MY ? ld(ms, tlo[k] + ob) : f32x4{});
         }
         issue(nxt, nn, nb0, nnb);
         __builtin_amdgcn_sched_barrier(0);
@@ -1424,9 +1468,9 @@ auto nm3_kernel(int flags) {
 
 }  // namespace
 
-extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
+extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                              const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
-                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
+                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream, uint16_t* ymask) {
     if (B < 0 || N <= 0 || !nodetab || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
     if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
@@ -1442,6 +1486,7 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
     // the rowptr-walking pipeline, LG_F_LAB_W8 = 8-wave workgroups, LG_F_LAB_BPC(n) = at most
     // n workgroups per CU
     const bool lab_v1 = (flags & LG_F_LAB_V1) != 0, lab_nm2 = (flags & LG_F_LAB_NM2) != 0;
+    if (ymask && (lab_v1 || lab_nm2 || (flags & LG_F_LAB_DST))) return LG_EUNSUPPORTED;  // lab schedules: no mask
     const bool w8 = (flags & LG_F_LAB_W8) != 0;
     const bool w5 = (flags & LG_F_LAB_W5) != 0;
     const bool relu = (flags & LG_F_RELU) != 0;
@@ -1471,19 +1516,19 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
             const size_t dyn3 = split ? Nm3Lds<DD, true, 5>::BYTES : Nm3Lds<DD, false, 5>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 5, dyn3, ntiles, 5, bpc);                                          \
             lg_launch(kern, grid, 64 * 5, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt);                                                                 \
+                                            salt, ymask);                                                                 \
         } else if (w8) {                                                                                           \
             auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
             lg_launch(kern, grid, 64 * 8, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt);                                                                 \
+                                            salt, ymask);                                                                 \
         } else {                                                                                                   \
             auto kern = relu ? nm3_kernel<DD, DR, true, 4>(flags) : nm3_kernel<DD, DR, false, 4>(flags);           \
             const size_t dyn3 = split ? Nm3Lds<DD, true, 4>::BYTES : Nm3Lds<DD, false, 4>::BYTES;                  \
             const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
             lg_launch(kern, grid, 64 * 4, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt);                                                                 \
+                                            salt, ymask);                                                                 \
         }                                                                                                          \
     } while (0)
     if (D == 64) {
@@ -1498,19 +1543,28 @@ extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const
     return LG_OK;
 }
 
+extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
+                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
+                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    return lg_gcn_fwd_nm_bits(nodetab, pairs, x, W, bias, y, B, N, D, nnz_cap, flags, dropout_p, seed, salt, stream,
+                              nullptr);
+}
+
 extern "C" int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D) {
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     return static_cast<int64_t>(2) * lg_num_cus() * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));
 }
 
-extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
+extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                              const float* x, const float* W, float* dx_out, float* dW, float* db,
                              const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
-                             float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
+                             float scale_in, float scale_out, void* workspace, lg_stream_t stream, const uint16_t* ymask) {
     if (B < 0 || N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
     if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
-    if (mask_in && !y) return LG_EINVAL;
+    if (mask_in && !y && !ymask) return LG_EINVAL;
+    const bool mbits = mask_in && ymask != nullptr;
+    if (mbits && (flags & LG_F_LAB_NM2)) return LG_EUNSUPPORTED;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
     const int64_t ngroups = (B + 15) / 16, ntiles = std::max<int64_t>(ngroups * N, 0);
@@ -1534,7 +1588,8 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
                                                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
                                                      scale_out);                                                   \
         } else {                                                                                                   \
-            auto kern = bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>;                 \
+            auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>) \
+                                      : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>);   \
             const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                             \
             grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
                                          2),                                                                       \
@@ -1542,7 +1597,7 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
             lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,        \
                                                        static_cast<uint32_t>(N), static_cast<uint32_t>(B),         \
                                                        static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,     \
-                                                       scale_out);                                                 \
+                                                       scale_out, ymask);                                          \
         }                                                                                                          \
     } while (0)
 #define LG_NM_BWD_D(DD)                                  \
@@ -1563,4 +1618,12 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
     const int64_t L = D * D + 2 * D;
     const LgSlabSeg segs[3] = {{0, D * D, dW}, {D * D, D, db}, {D * D + D, D, dnode_bias}};
     return lg_launch_slab_reduce_multi(slab, grid, L, segs, 3, nullptr, nullptr, s);
+}
+
+extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
+                             const float* x, const float* W, float* dx_out, float* dW, float* db,
+                             const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
+                             float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
+    return lg_gcn_bwd_nm_bits(nodetab_t, pairs_t, dy, y, x, W, dx_out, dW, db, node_slot, dnode_bias, B, N, D, flags,
+                              scale_in, scale_out, workspace, stream, nullptr);
 }

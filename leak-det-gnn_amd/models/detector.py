@@ -175,6 +175,7 @@ class LeakDetector(nn.Module):
             nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
             g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
             library.seed_tensor(residual.device) if drop else _NO_SEED, bf16=self.mlp_dtype == "bf16")
+        xs = xs[:-1]                                                       # [x_0 .. x_L] (the last item: x_L's mask bits)
         h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
         mlp = self.edge_head.mlp     # Linear(3D,128), ReLU, Dropout, Linear(128,1)
         nmlp = self.noleak_head.mlp  # Linear(D,128), ReLU, Dropout, Linear(128,1)

@@ -333,8 +333,8 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
               nodetab: Tensor, pairs: Tensor, rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor,
               pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor,
               *, bf16: bool = False) -> List[Tensor]:
-    """[x_0, ..., x_L]: sensor_to_node + node init (detector.py:160, 178-190), then
-    L x dropout(relu(GCNConv)).
+    """[x_0, ..., x_L, ymask]: sensor_to_node + node init (detector.py:160, 178-190),
+    then L x dropout(relu(GCNConv)).
 
       x_0     = dropout(relu(slot >= 0 ? [h_s[b, slot], 1] W^T + b : b))   (lg_node_init_proj_fwd)
       x_{l+1} = dropout(relu(Ahat x_l W_l^T + b_l))                        (lg_gcn_fwd[_nm], fused)
@@ -342,7 +342,9 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     node_bias: its bias.  The projection is formed inside the node-init launch (no GEMM, no
     proj buffer).  node_major: features [N][B][D] (lg_gcn_fwd_nm), else [B][N][D].  p:
     dropout prob (0 = eval).  Every activation is returned: the backward reads its
-    ReLU/dropout masks back as [x > 0] and needs x_l for dW, so no mask is ever stored.
+    ReLU/dropout masks back as [x > 0] and needs x_l for dW.  ymask (node-major only, int16
+    (N * ceil(B/16) * 64,), else empty): [x_L > 0] as bits (lg_gcn_fwd_nm_bits), which the
+    last layer's backward reads instead of gathering x_L.
     bf16: the node-major transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier)."""
     lib = load_library()
     h_s, proj_weight, node_bias = _c(h_s), _c(proj_weight), _c(node_bias)
@@ -364,19 +366,23 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
                                         ptr(x0), B, N, S, Ds, D, dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v,
                                         0 | sbit, st), "lg_node_init_proj_fwd")
     xs = [x0]
+    L = len(weights)
+    ymask = torch.empty(N * ((B + 15) // 16) * 64 if (node_major and L > 0) else 0, device=h_s.device,
+                        dtype=torch.int16)
     for l, (W, b) in enumerate(zip(weights, biases)):
         y = torch.empty_like(x0)
         flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag | (nat.LG_F_BF16 if bf16 else 0)
         with _timed("gcn_fwd", h_s.device):
             if node_major:
-                check(lib.lg_gcn_fwd_nm(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
-                                        col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v, (l + 1) | sbit, st),
-                      "lg_gcn_fwd_nm")
+                check(lib.lg_gcn_fwd_nm_bits(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
+                                             D, col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v,
+                                             (l + 1) | sbit, st, ptr(ymask) if l == L - 1 else None),
+                      "lg_gcn_fwd_nm_bits")
             else:
                 check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
                                      col.numel(), flags, p, seed_v, (l + 1) | sbit, st), "lg_gcn_fwd")
         xs.append(y)
-    return xs
+    return xs + [ymask]
 
 
 @gnn_trunk.register_fake
@@ -386,11 +392,14 @@ def _(h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, non
     D = proj_weight.shape[0]
     N = sensor_slot.shape[0]
     shape = (N, B, D) if node_major else (B, N, D)
-    return [h_s.new_empty(shape) for _ in range(len(weights) + 1)]
+    L = len(weights)
+    nmask = N * ((B + 15) // 16) * 64 if (node_major and L > 0) else 0
+    return [h_s.new_empty(shape) for _ in range(L + 1)] + [h_s.new_empty((nmask,), dtype=torch.int16)]
 
 
 @torch.library.custom_op(f"{NS}::gnn_trunk_backward", mutates_args=(), device_types="cuda")
-def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], h_s: Tensor, proj_weight: Tensor, weights: List[Tensor],
+def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: Tensor, proj_weight: Tensor,
+                       weights: List[Tensor],
                        sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
                        nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
                        node_major: bool, *, bf16: bool = False
@@ -418,13 +427,13 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], h_s: Tensor, proj_wei
     dbs: List[Tensor] = [grad_out] * L
     dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
     with _reduce_batch(lib, st):
-        dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx,
+        dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx,
                                                   nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
                                                   node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st)
     return dh_s, dWp, dbp, dWs, dbs
 
 
-def _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live,
+def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live,
                              nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_major, bf16, scale, wss, dWs, dbs, dbias_ns,
                              st):
     L = len(weights)
@@ -443,9 +452,10 @@ def _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot
         slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias_ns)) if l == 0 else (None, None)
         with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dev):
             if node_major:
-                check(lib.lg_gcn_bwd_nm(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
-                                        ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D, flags,
-                                        scale, scale, ptr(ws), st), "lg_gcn_bwd_nm")
+                bits = ptr(ymask) if (l == L - 1 and ymask.numel() > 0) else None  # [x_L > 0] as bits
+                check(lib.lg_gcn_bwd_nm_bits(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
+                                             ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
+                                             flags, scale, scale, ptr(ws), st, bits), "lg_gcn_bwd_nm_bits")
             else:
                 check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                      ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
@@ -469,8 +479,8 @@ def _trunk_backward_launches(lib, dy, xs, h_s, proj_weight, weights, sensor_slot
 
 
 @gnn_trunk_backward.register_fake
-def _(grad_out, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t, pairs_t,
-      rowptr_t, col_t, w_t, p, node_major, *, bf16=False):
+def _(grad_out, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t,
+      pairs_t, rowptr_t, col_t, w_t, p, node_major, *, bf16=False):
     D = proj_weight.shape[0]
     return (torch.empty_like(h_s), torch.empty_like(proj_weight), grad_out.new_empty(D),
             [torch.empty_like(t) for t in weights], [grad_out.new_empty(D) for _ in weights])
@@ -482,7 +492,8 @@ def _trunk_setup(ctx, inputs, keyword_only_inputs, output):
     bf16 = bool(keyword_only_inputs.get("bf16", False))
     ctx.L = len(weights)
     ctx.bf16 = bf16
-    ctx.mark_non_differentiable(*output[:-1])  # x_0 .. x_{L-1}: returned for the backward's masks
+    # x_0 .. x_{L-1} (returned for the backward's masks) and ymask
+    ctx.mark_non_differentiable(*output[:ctx.L], output[ctx.L + 1])
     ctx.set_materialize_grads(False)  # their gradients would be zero-filled (B, N, D) tensors
     ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
     ctx.save_for_backward(*output, h_s, proj_weight, *weights, sensor_slot, sensor_idx, nonsensor_idx,
@@ -492,14 +503,14 @@ def _trunk_setup(ctx, inputs, keyword_only_inputs, output):
 def _trunk_bwd(ctx, grads):
     L = ctx.L
     saved = ctx.saved_tensors
-    xs, h_s, proj_weight = list(saved[:L + 1]), saved[L + 1], saved[L + 2]
-    weights = list(saved[L + 3:2 * L + 3])
-    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 3:]
-    g = grads[-1]
+    xs, ymask, h_s, proj_weight = list(saved[:L + 1]), saved[L + 1], saved[L + 2], saved[L + 3]
+    weights = list(saved[L + 4:2 * L + 4])
+    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 4:]
+    g = grads[L]
     if g is None:
         return (None,) * 22
     dh_s, dWp, dbp, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
-        g, xs, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None,
+        g, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None,
         nodetab_t, pairs_t, rowptr_t, col_t, w_t, ctx.p, ctx.node_major, bf16=ctx.bf16)
     return (dh_s, dWp, dbp, dWs, dbs) + (None,) * 17
 

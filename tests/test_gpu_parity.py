@@ -692,3 +692,64 @@ def test_gcn_node_major_schedule_order_changes_no_result(drop):
     assert torch.equal(res[0][1], res[1][1]), "schedule order changed dx"
     for k, name in ((2, "dW"), (3, "db"), (4, "node bias")):
         assert_close(res[0][k], res[1][k], rtol=1e-6, atol=1e-7, what=name)
+
+
+@pytest.mark.parametrize("D,B", [(64, 48), (32, 37)])
+def test_gcn_node_major_mask_bits_equal_y_gather(D, B):
+    """lg_gcn_fwd_nm_bits writes [y > 0] as bits beside the same y; lg_gcn_bwd_nm_bits with
+    those bits (y passed as NULL) gives dx bit for bit equal to the y-gather backward (dW, db
+    and the node bias within 1e-6).  B = 37 leaves a ragged window group."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    N = 661
+    graph = GCNGraph.build(torch.from_numpy(load("graph_ltown_a.npz")["edge_index"]), N, DEV)
+    st = ops.stream_of(graph.w)
+    gen = torch.Generator().manual_seed(D + B)
+    x = torch.randn(N, B, D, generator=gen).relu().to(DEV)
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    b = (torch.randn(D, generator=gen) / 4).to(DEV)
+    dy = torch.randn(N, B, D, generator=gen).to(DEV)
+    slot = torch.full((N,), -1, dtype=torch.int32)
+    slot[:29] = torch.arange(29, dtype=torch.int32)
+    slot = slot.to(DEV)
+    flags = ops.nat.LG_F_BIAS | ops.nat.LG_F_RELU | ops.nat.LG_F_DROPOUT
+    y, y2 = torch.empty_like(x), torch.empty_like(x)
+    bits = torch.zeros(N * ((B + 15) // 16) * 64, dtype=torch.int16, device=DEV)
+    ops.check(lib.lg_gcn_fwd_nm(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(x), ops.ptr(W), ops.ptr(b),
+                                ops.ptr(y), B, N, D, graph.nnz_cap, flags, 0.1, 99, 2, st), "fwd")
+    ops.check(lib.lg_gcn_fwd_nm_bits(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(x), ops.ptr(W), ops.ptr(b),
+                                     ops.ptr(y2), B, N, D, graph.nnz_cap, flags, 0.1, 99, 2, st, ops.ptr(bits)), "fwd bits")
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    # the bits restate [y > 0] in the gather layout (lane l: row (64/(D/4)) k + l/(D/4), cols 4 (l % (D/4)) + i)
+    lpr = D // 4
+    rpi = 64 // lpr
+    bb = bits.view(N, (B + 15) // 16, 64).to(torch.int32).cpu() & 0xFFFF
+    yc = (y.cpu() > 0)
+    for g in range((B + 15) // 16):
+        for lane in (0, 5, lpr - 1, 63):
+            for k in range(16 // rpi):
+                row = g * 16 + rpi * k + lane // lpr
+                if row >= B:
+                    continue
+                for i in range(4):
+                    want = yc[:, row, 4 * (lane % lpr) + i]
+                    got = ((bb[:, g, lane] >> (4 * k + i)) & 1).bool()
+                    assert torch.equal(got, want), (g, lane, k, i)
+    sc = 1.0 / 0.9
+    outs = []
+    for use_bits in (False, True):
+        dx = torch.empty_like(x)
+        dW, db, dnb = torch.empty(D, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV)
+        ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+        ops.check(lib.lg_gcn_bwd_nm_bits(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t), ops.ptr(dy),
+                                         None if use_bits else ops.ptr(y), ops.ptr(x), ops.ptr(W), ops.ptr(dx),
+                                         ops.ptr(dW), ops.ptr(db), ops.ptr(slot), ops.ptr(dnb), B, N, D,
+                                         ops.nat.LG_F_MASK_IN | ops.nat.LG_F_MASK_OUT, sc, sc, ops.ptr(ws), st,
+                                         ops.ptr(bits) if use_bits else None), "bwd")
+        torch.cuda.synchronize()
+        outs.append((dx, dW, db, dnb))
+    assert torch.equal(outs[0][0], outs[1][0]), "dx: mask bits differ from the y gather"
+    for a, c, name in zip(outs[0][1:], outs[1][1:], ("dW", "db", "node bias")):  # slab grouping may differ
+        assert_close(c, a, rtol=1e-6, atol=1e-7, what=name)

@@ -124,7 +124,10 @@ def main():
                                                                  1, cs()), "nmlab")
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    # gcn_bwd_nm: the training step's layer-2 backward (output mask as the forward's ymask
+    # bits); gcn_bwd_nm_y: the same with the mask gathered from y
     for name, fl, nbias in (("gcn_bwd_nm", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
+                            ("gcn_bwd_nm_y", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
                             ("gcn_bwd_nm_old", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, False),
                             ("gcn_bwd_nm_l0", nat.LG_F_MASK_OUT, True),
                             ("gcn_bwd_nm_l0_old", nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, True)):
@@ -139,12 +142,22 @@ def main():
         slot[:29] = torch.arange(29, dtype=torch.int32, device=dev)
         dnb = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
-        f = lambda fl=fl, nbias=nbias, dy=dy, yy=yy, dx=dx, dW=dW, db=db, slot=slot, dnb=dnb, ws=ws: check(
-            lib.lg_gcn_bwd_nm(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W), ptr(dx),
-                              ptr(dW), ptr(db), ptr(slot) if nbias else None, ptr(dnb) if nbias else None, B, N, D,
-                              fl, 1.0, 1.0, ptr(ws), cs()), name)
+        bits = None
+        if name == "gcn_bwd_nm":  # the mask bits of yy = dropout(relu(layer(x))) from the forward
+            bits = torch.empty(N * ((B + 15) // 16) * 64, device=dev, dtype=torch.int16)
+            check(lib.lg_gcn_fwd_nm_bits(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias), ptr(yy), B,
+                                         N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT, 0.1, 123, 2,
+                                         cs(), ptr(bits)), "fwd bits")
+        f = lambda fl=fl, nbias=nbias, dy=dy, yy=yy, dx=dx, dW=dW, db=db, slot=slot, dnb=dnb, ws=ws, bits=bits: check(
+            lib.lg_gcn_bwd_nm_bits(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
+                                   ptr(dx), ptr(dW), ptr(db), ptr(slot) if nbias else None,
+                                   ptr(dnb) if nbias else None, B, N, D, fl, 1.0, 1.0, ptr(ws), cs(),
+                                   ptr(bits) if bits is not None else None), name)
         t = timeit(f, args.iters)
-        byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
+        if bits is not None:
+            byts = 12 * B * N * D + bits.numel() * 2
+        else:
+            byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
         res[name] = {"us": t, "GBps": byts / t / 1e3}
     if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
         f = lambda: y.copy_(x)
