@@ -110,6 +110,13 @@ int lg_reduce_batch_flush(lg_stream_t stream);
  * 8 TB/s roofline): dst = src over `bytes` (a multiple of 16) with 16-byte non-temporal
  * loads and stores.  No reference counterpart. */
 int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stream_t stream);
+
+/* Device dropout-seed slots (the seeds LG_SALT_SEED_PTR call sites read at launch): *state
+ * += 1, then slots[i] = splitmix64(*state * n + i + 1) & (2^62 - 1), i < n <= 4096, in ONE
+ * single-wave launch on the device, so a captured training step re-draws its dropout
+ * streams at every replay without the host.  No reference counterpart (the reference's
+ * nn.Dropout draws from torch's generator). */
+int lg_seed_slots_advance(uint64_t* slots, int64_t n, uint64_t* state, lg_stream_t stream);
 const char* lg_strerror(int code);
 
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;

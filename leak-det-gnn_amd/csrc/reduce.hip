@@ -238,3 +238,31 @@ extern "C" int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stre
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
+
+// ---------------------------------------------------------------- dropout seed slots
+// Re-draw of a captured step's device seed slots (models/ops.py SeedSlots.refresh): the
+// state word advances by one and slot i becomes splitmix64(state * n + i + 1) & (2^62 - 1).
+// One wave, no host involvement, so a replayed graph draws fresh seeds with ONE launch
+// (torch's generator inside a graph costs a random_ kernel plus two fills per replay).
+namespace {
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(64) k_seed_advance(uint64_t* __restrict__ slots, int n, uint64_t* __restrict__ state) {
+    const uint64_t c = state[0] + 1;  // every lane reads before lane 0 writes (one wave, same address)
+    for (int i = threadIdx.x; i < n; i += 64)
+        slots[i] = splitmix64(c * static_cast<uint64_t>(n) + static_cast<uint64_t>(i) + 1) & ((1ull << 62) - 1);
+    if (threadIdx.x == 0) state[0] = c;
+}
+}  // namespace
+
+extern "C" int lg_seed_slots_advance(uint64_t* slots, int64_t n, uint64_t* state, lg_stream_t stream) {
+    if (n < 0 || n > 4096 || (n > 0 && (!slots || !state))) return LG_EINVAL;
+    if (n == 0) return LG_OK;
+    k_seed_advance<<<1, 64, 0, lg_stream(stream)>>>(slots, static_cast<int>(n), state);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}

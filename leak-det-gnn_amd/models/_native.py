@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 15  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 16  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -41,6 +41,7 @@ SIGNATURES = {
     "lg_reduce_batch_begin": (_i32, []),
     "lg_reduce_batch_flush": (_i32, [_p]),
     "lg_stream_copy": (_i32, [_p, _p, _i64, _p]),
+    "lg_seed_slots_advance": (_i32, [_p, _i64, _p, _p]),
     "lg_cross_entropy_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
     "lg_cross_entropy_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_clip_adamw_workspace_bytes": (_i64, [_p, _i32]),

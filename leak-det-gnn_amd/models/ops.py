@@ -249,14 +249,21 @@ class SeedSlots:
     LG_SALT_SEED_PTR).  While installed (use_device_seeds), every forward that needs a
     dropout seed takes the next slot and passes its ADDRESS with salt bit 31 set; the
     kernels read the seed at launch.  refresh(), captured at the head of the step, re-draws
-    all slots from torch's CUDA generator (graph-safe), so every replay gets new masks."""
+    all slots on the device (lg_seed_slots_advance: a device state word advanced per call,
+    hashed per slot), so every replay gets new masks with one launch.  The state starts from
+    torch's generator (torch.manual_seed reproduces the sequence)."""
 
     def __init__(self, device, n: int = 16):
         self.buf = torch.zeros(n, dtype=torch.int64, device=device)
+        self.state = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(device)
         self.n, self.i = n, 0
 
     def refresh(self) -> None:
-        self.buf.random_(0, 2 ** 62)
+        if self.buf.is_cuda:
+            check(load_library().lg_seed_slots_advance(ptr(self.buf), self.n, ptr(self.state), stream_of(self.buf)),
+                  "lg_seed_slots_advance")
+        else:
+            self.buf.random_(0, 2 ** 62)
         self.i = 0
 
     def take(self) -> int:

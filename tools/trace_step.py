@@ -11,11 +11,21 @@ print("launches", len(rows))
 for n, c in cnt.most_common(12):
     print(f"{c:8d}  {n}")
 idx = [i for i, r in enumerate(rows) if "k_gru_fwd" in r["Kernel_Name"]]
-a, b = idx[-4], idx[-3]
-tot = 0.0
-print("\none step:")
-for r in rows[a:b]:
-    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
-    tot += d
-    print(f"{r['Kernel_Name'][:80]:80s} {d:8.2f}")
-print("sum", round(tot, 1), "span", (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1000, "n", b - a)
+
+
+def show(title, a, b):
+    tot = 0.0
+    print(f"\n{title}:")
+    for r in rows[a:b]:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+        tot += d
+        print(f"{r['Kernel_Name'][:80]:80s} {d:8.2f}")
+    print("sum", round(tot, 1), "span", (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1000,
+          "n", b - a)
+
+
+# the headline step runs first (its timed replays are the longest run of GRU launches), the
+# e2e leg (residual build + step) last
+k = len(idx) // 3
+show("headline step (replay %d of %d)" % (k, len(idx)), idx[k], idx[k + 1])
+show("one step", idx[-4], idx[-3])
