@@ -516,7 +516,10 @@ k_gcn_fwd_nm2(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 // of tile i and lands while tile i's rows are waited for and accumulated, so tile i+1's
 // NPF neighbour blocks issue at once, right before tile i's transform.  (A record carried
 // across the loop back edge in SGPRs is copied there, and the copy waits for the load.)
-constexpr int kNm3Npf = 4;
+#ifndef LG_NM3_NPF
+#define LG_NM3_NPF 3  // lab builds override (-DLG_NM3_NPF=n); 3 measured best of 2-5 (tools/exp_r02an.sh)
+#endif
+constexpr int kNm3Npf = LG_NM3_NPF;
 
 struct NmRec {  // one node-table record (wave-uniform, SGPRs)
     int e0, e1, self, node;
