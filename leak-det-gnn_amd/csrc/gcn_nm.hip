@@ -1059,6 +1059,9 @@ struct Nb3Lds {
     static constexpr size_t BYTES = 4 * static_cast<size_t>(WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L);
 };
 
+#ifndef LG_NB3_NPF
+#define LG_NB3_NPF 4  // neighbour blocks in flight in the backward (lab builds override)
+#endif
 // MB (with MASK_IN): the layer's output mask comes as the forward's ymask bits instead of a
 // gather of y, so the prefetch keeps the unmasked depth
 template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false>  // BF: LG_F_BF16, single-product MFMAs
@@ -1073,7 +1076,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     using G = NmGeo<D>;
     using LY = Nb3Lds<D, MASK_IN>;
     constexpr int SB = LY::SB;
-    constexpr int NPF = MY ? 2 : 4;
+    constexpr int NPF = MY ? 2 : LG_NB3_NPF;
     constexpr int L = LY::L;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // 3 x W^T [in][out] bf16, stride SB
