@@ -88,6 +88,15 @@ enum {
 #define LG_F_LAB_DST       0x00080000  /* lab: epilogue stores straight from the MFMA layout */
 
 #define LG_F_LAB_BPC_SHIFT 24
+/* lg_gcn_fwd_nm schedule: the W-in-registers pipeline (2 waves/SIMD, no workgroup staging);
+ * results identical to the default pipeline */
+#define LG_F_NM5           0x00002000
+/* lg_gcn_fwd_nm schedule: producer / consumer waves (gather waves hand tiles to MFMA waves
+ * through an LDS ring); results identical to the default pipeline */
+#define LG_F_PC            0x00004000
+/* lab builds only: bits 8..11 pick the lg_gcn_fwd_nm (D = 64) kernel's OPT variant */
+#define LG_F_LAB_OPT       0x00001000
+#define LG_F_LAB_OPT_SHIFT 8
 
 int lg_abi_version(void);
 

@@ -24,6 +24,7 @@
 // wave and reduced per block in a fixed order (deterministic), then by the slab reducer.
 // Tiles are ordered window-group-major and dealt XCD-aware.
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 #include "reduce.h"
 #include "split_bf16.h"
@@ -544,13 +545,53 @@ __device__ __forceinline__ NmRec nm_rec(const int32_t* __restrict__ tab, uint32_
 }
 static_assert(kLgNmInline == 6, "nm_rec unpacks six inline pairs");
 
-template <int D, bool SPLIT, int WAVES>
+// OPT bits of k_gcn_fwd_nm3 (results never change):
+//   kNm3WFrag: W's split parts in LDS in MFMA-fragment order — fragment f = (part, mt, s2) is
+//     1 KiB, lane l's 8 bf16 at f * 1024 + 16 l — so every A-operand read is one
+//     conflict-free ds_read_b128 from ONE address register plus an immediate offset (the
+//     row-major image with stride D + 8 put 2 lanes on a bank in every 16-lane group);
+//   kNm3Swz (D = 64): the per-wave tile unpadded, 16-byte chunk c of row r at chunk
+//     c ^ r: the gather-layout stores/loads, the B-operand loads and the MFMA-layout
+//     epilogue stores are all conflict-free (stride D + 4 conflicted on the loads);
+//   kNm3Epi: ReLU as an integer max on the bits (one op, no NaN canonicalisation), the
+//     dropout decision as one compare + select, the [y > 0] mask bits as min + shift-or;
+//   kNm3Soff: neighbour block bases in the buffer load's scalar offset (no per-load
+//     address add), an absent neighbour through a zero-record descriptor.
+//   kNm3WFirst: W's global loads issued before the first tile's neighbour blocks.
+constexpr int kNm3WFrag = 1, kNm3Swz = 2, kNm3Epi = 4, kNm3Soff = 8, kNm3WFirst = 16;
+#ifndef LG_NM3_OPT
+#define LG_NM3_OPT 0
+#endif
+constexpr int kNm3OptDefault = LG_NM3_OPT;
+
+template <int D, bool SPLIT, int WAVES, int OPT = 0>
 struct Nm3Lds {  // dynamic LDS layout (floats)
+    static constexpr bool WFRAG = SPLIT && (OPT & kNm3WFrag);
+    static constexpr bool SWZ = (OPT & kNm3Swz) && D == 64;
     static constexpr int SB = D + 8;
-    static constexpr int WF = SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
+    static constexpr int WF = WFRAG ? (3 * D * D) / 2 : SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
     static constexpr int TILES = WF + D;
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + WAVES * NmGeo<D>::TILE);
+    static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + WAVES * TILE);
+    // float offset of 16-byte chunk c of row r in a wave's tile
+    static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
+
+#ifdef LG_NM3_STAMPS
+// kernel-lab timeline (LG_NM3_STAMPS builds only): per wave, slot 0 realtime at start, 1 clock
+// at start, 2 after the W staging barrier, 3 + 3 t .. 5 + 3 t for tile t < 6 (rows
+// accumulated, transform done, stores issued), 21 clock at end, 22 realtime at end, 23 hw id.
+constexpr int kNm3Stamps = 24;
+__device__ uint64_t g_nm3_stamps[8192 * kNm3Stamps];
+#define LG_NM3_STAMP(slot, v)                                                                      \
+    do {                                                                                           \
+        if (lane == 0) g_nm3_stamps[(static_cast<size_t>(blockIdx.x) * WAVES + wave) * kNm3Stamps + (slot)] = (v); \
+    } while (0)
+#else
+#define LG_NM3_STAMP(slot, v) \
+    do {                      \
+    } while (0)
+#endif
 
 // acc += w * v on packed fp32 (v_pk_fma_f32: two lanes' worth of fma per instruction,
 // each element the same IEEE fma as fmaf)
@@ -586,28 +627,36 @@ constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
 // the transform is not dead code).  DST: epilogue stores straight from the MFMA layout
 // (16 rows x 64 B per store) instead of through the LDS tile.
 // BF (LG_F_BF16, the bf16 node-MLP tier): the transform's single hi x hi product.
-template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false, bool BF = false>
+template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false, bool BF = false,
+          int OPT = kNm3OptDefault>
 __global__ void __launch_bounds__(64 * WAVES, WAVES >= 5 ? 4 : 1)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
               uint32_t salt, uint16_t* __restrict__ ymask) {
     using G = NmGeo<D>;
-    using LY = Nm3Lds<D, SPLIT, WAVES>;
+    using LY = Nm3Lds<D, SPLIT, WAVES, OPT>;
     constexpr int SB = LY::SB;
     constexpr int NPF = kNm3Npf;
+    constexpr bool WFRAG = LY::WFRAG, EPI = (OPT & kNm3Epi) != 0, SOFF = (OPT & kNm3Soff) != 0;
+    constexpr bool WFIRST = (OPT & kNm3WFirst) != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* wl = reinterpret_cast<float*>(smem);         // fp32: W [out][in] * fold, stride S
-    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB
+    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB (WFRAG: fragments)
     float* bl = wl + LY::WF;                            // bias * fold
     float* tiles = wl + LY::TILES;
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* tl = tiles + wave * G::TILE;
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
+    float* tl = tiles + wave * LY::TILE;
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t xrs0 = nm_rsrc(x, 0);  // SOFF: an absent neighbour's loads return zeros
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
 #pragma unroll
@@ -639,6 +688,16 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
             const bool have = r.e0 + i < r.e1;
+            if constexpr (SOFF) {
+                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
+                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
+                                         : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                         rs, lo[k], base, 0));
+                continue;
+            }
             const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : kNm3BlkOob;
 #pragma unroll
             for (int k = 0; k < G::K; ++k)
@@ -647,28 +706,58 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                                                                      xrs, lo[k] + base, 0, 0));
         }
     };
+    // a present neighbour's block (the rows past the prefetched ones)
+    auto ldblk = [&](uint32_t base, uint32_t lk) -> f32x4 {
+        if constexpr (SOFF) return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk, base, 0));
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk + base, 0, 0));
+    };
     const int64_t t0 = sc.first;
+    // W (x dropout scale fold) and bias to LDS.  kNm3WFirst: W's loads go out BEFORE the first
+    // tile's neighbour blocks, so the staging waits for W alone (vector loads complete in
+    // order: staged after them, it waited for the whole first gather, ~2.6 us of the launch
+    // in the kernel-lab timeline)
+    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
+    f32x4 wv[WPER];
+    float bb = 0.f;
+    auto load_w = [&]() {
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
+        bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+    };
+    if constexpr (WFIRST) {
+        load_w();
+        asm volatile("" ::: "memory");
+    }
     {
         uint32_t n0, b00, nb00;
         tile_coords(t0, n0, b00, nb00);
         issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
     }
-
-    // W (x dropout scale fold) and bias to LDS, after the first tile's loads are out
+    if constexpr (!WFIRST) load_w();
     {
-        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
         const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
-        f32x4 wv[WPER];
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
-        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
             const int i = u * 64 * WAVES + threadIdx.x;
             if (i >= W4) continue;
             const int o = i / (D / 4), c4 = 4 * (i % (D / 4));
-            const f32x4 w = wv[u] * fold;
-            if constexpr (SPLIT) {
+            // the product rounded to fp32 before the split, as every other staging path stores it
+            // (the empty asm keeps -ffp-contract from fusing it into the split's residual)
+            f32x4 w = wv[u] * fold;
+            asm volatile("" : "+v"(w));
+            if constexpr (WFRAG) {
+                // element (o, c) -> fragment (part, mt = o / 16, s2 = c / 32), lane (o % 16) + 16 ((c / 8) % 4),
+                // bf16 slot c % 8
+                uint32_t pa[3], pb[3];
+                split3_pair(w[0], w[1], pa[0], pa[1], pa[2]);
+                split3_pair(w[2], w[3], pb[0], pb[1], pb[2]);
+                const int fl = (o & 15) + 16 * ((c4 >> 3) & 3);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const int f = (p * G::CH + (o >> 4)) * (D / 32) + (c4 >> 5);
+                    *reinterpret_cast<uint2*>(wsl + f * 512 + fl * 8 + (c4 & 7)) = uint2{pa[p], pb[p]};
+                }
+            } else if constexpr (SPLIT) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     uint32_t p0, p1, p2;
@@ -689,6 +778,9 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p_drop);
 
+    int tcount = 0;
+    (void)tcount;
+    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
     for (int64_t tile = t0; tile < tend; tile += sc.stride) {
         const uint32_t n = cn, b0 = cb0, nb = cnb;
         const int e0 = cur.e0, e1 = cur.e1;
@@ -727,8 +819,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                     const uint32_t ba = (static_cast<uint32_t>(ip[i].x) * B + b0) * (4u * D);
                     f32x4 va[G::K];
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k)
-                        va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
+                    for (int k = 0; k < G::K; ++k) va[k] = ldblk(ba, tlo[k]);
                     const float wa = __int_as_float(ip[i].y);
 #pragma unroll
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
@@ -742,8 +833,8 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 f32x4 va[G::K], vb[G::K];
 #pragma unroll
                 for (int k = 0; k < G::K; ++k) {
-                    va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
-                    vb[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + bbs, 0, 0));
+                    va[k] = ldblk(ba, tlo[k]);
+                    vb[k] = ldblk(bbs, tlo[k]);
                 }
                 const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
 #pragma unroll
@@ -757,13 +848,15 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
                 f32x4 va[G::K];
 #pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, tlo[k] + ba, 0, 0));
+                for (int k = 0; k < G::K; ++k) va[k] = ldblk(ba, tlo[k]);
                 const float wa = __int_as_float(pa.y);
 #pragma unroll
                 for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
             }
         }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(3 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
         // next tile's blocks go in flight under this tile's transform (its record landed meanwhile)
         issue(nxt, nn, nb0, nnb);
         __builtin_amdgcn_sched_barrier(0);
@@ -771,30 +864,39 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         // gather layout -> LDS -> MFMA B operand
         wave_sync_nm();
 #pragma unroll
-        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
+        for (int k = 0; k < G::K; ++k) st4(tl + LY::tix(G::RPI * k + rl, fg), acc[k]);
         wave_sync_nm();
         f32x4 o[G::CH];
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
         if constexpr ((LAB & 1) != 0) {
 #pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + j * G::S + 16 * mt + 4 * q);
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + LY::tix(j, 4 * mt + q));
         } else if constexpr (SPLIT) {
 #pragma unroll
             for (int s2 = 0; s2 < D / 32; ++s2) {
                 lg_bf16x8 b0f, b1f, b2f;
-                split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f,
+                split3_x8(ld4(tl + LY::tix(j, 8 * s2 + 2 * q)), ld4(tl + LY::tix(j, 8 * s2 + 2 * q + 1)), b0f, b1f,
                           b2f);
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) {
-                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
-                    const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                    lg_bf16x8 a0, a1, a2;
+                    if constexpr (WFRAG) {
+                        const uint16_t* fb = wsl + 8 * lane + 512 * (mt * (D / 32) + s2);
+                        constexpr int PS = 512 * G::CH * (D / 32);  // one part's fragments
+                        a0 = *reinterpret_cast<const lg_bf16x8*>(fb);
+                        a1 = *reinterpret_cast<const lg_bf16x8*>(fb + PS);
+                        a2 = *reinterpret_cast<const lg_bf16x8*>(fb + 2 * PS);
+                    } else {
+                        const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                        a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                        a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
+                        a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
+                    }
                     if constexpr (BF) {
                         o[mt] = mfma_bf(a0, b0f, o[mt]);
                         continue;
                     }
-                    const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
-                    const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
                     o[mt] = mfma_bf(a2, b0f, o[mt]);
                     o[mt] = mfma_bf(a1, b1f, o[mt]);
                     o[mt] = mfma_bf(a0, b2f, o[mt]);
@@ -807,7 +909,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         } else {
 #pragma unroll
             for (int c = 0; c < G::CH; ++c) {
-                const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);
+                const f32x4 bt = ld4(tl + LY::tix(j, 4 * c + q));
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) {
                     const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);
@@ -817,6 +919,9 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(4 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
         // epilogue: ReLU, row-stream dropout seeded with the window-major row id (b0 + j) N + n,
         // both as ONE select per element (no fmaxf: its NaN canonicalisation costs a VALU op)
         uint32_t st = 0;
@@ -825,7 +930,18 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                const float v = o[mt][reg];
+                float v = o[mt][reg];
+                if constexpr (EPI) {
+                    // relu(v) on the bits: negative floats (and -0) are negative integers
+                    if constexpr (RELU) v = __int_as_float(max(__float_as_int(v), 0));
+                    if constexpr (DROP) {
+                        if ((reg & 1) == 0) st = lg_xorshift32(st);
+                        const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                        v = u16 >= thr ? v : 0.0f;
+                    }
+                    o[mt][reg] = v;
+                    continue;
+                }
                 bool keep = true;
                 if constexpr (DROP) {
                     if ((reg & 1) == 0) st = lg_xorshift32(st);
@@ -849,22 +965,704 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         } else {
             wave_sync_nm();
 #pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+            for (int mt = 0; mt < G::CH; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
             wave_sync_nm();
             uint32_t bits = 0;  // [y > 0] of this lane's 4 K elements (bit 4 k + i), for ymask
+            f32x4 vk[EPI ? G::K : 1];
 #pragma unroll
             for (int k = 0; k < G::K; ++k) {
-                const f32x4 v = ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg);
-                if (do_store)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                                           yrs, tlo[k] + ob, 0, 0);
+                const f32x4 v = ld4(tl + LY::tix(G::RPI * k + rl, fg));
+                if (do_store) {
+                    if constexpr (SOFF)
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), yrs, tlo[k], ob, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), yrs, tlo[k] + ob, 0, 0);
+                }
+                if constexpr (EPI) {
+                    vk[k] = v;
+                } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
+                    for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
+                }
+            }
+            if constexpr (EPI) {
+                // [y > 0] = bit 31 of (bits(y) + 0x7FFFFFFF) for y >= +0 (after the ReLU; without it,
+                // negative y first go to 0 by an integer max); alignbit shifts the mask left by one
+                // and takes that bit in, highest element first: two ops per element, no VCC
+#pragma unroll
+                for (int k = G::K - 1; k >= 0; --k)
+#pragma unroll
+                    for (int i = 3; i >= 0; --i) {
+                        const uint32_t u = RELU ? __float_as_uint(vk[k][i])
+                                                : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
+                        bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
+                    }
             }
             if (ymask)
                 __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs,
                                                       nm_mask_off(n, b0 >> 4, ngroups, lane), 0, 0);
         }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
+        ++tcount;
+#endif
+    }
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
+    LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                         static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
+#endif
+}
+
+// ------------------------------------------------------------------ forward, W in registers
+// k_gcn_fwd_nm3's tile pipeline at 2 waves per SIMD with the transform's A operand (W's
+// three bf16 parts, 96 VGPRs at D = 64) held in registers for the whole launch.  A per-wave
+// timeline of nm3 (kernel-lab stamps, profiles/r03a) put 1.4 of ~2.7 us per tile in the
+// transform, most of it waiting on the 24 W-fragment LDS reads that the register budget of
+// 3 waves/SIMD forced just in time, and 2.6 us in the workgroup's W staging before the
+// first tile.  Here every wave splits its own W fragments from global memory once, no wave
+// waits on another (no workgroup barrier: the LDS holds only the wave's own transpose tile,
+// XOR-swizzled and conflict-free at D = 64), and the transform is 48 MFMAs back to back on
+// operands already in registers.  Epilogue, loads and stores as nm3's kNm3Epi | kNm3Soff;
+// results are bit-identical to k_gcn_fwd_nm3 (same products, same order).
+constexpr int kNm5Waves = 4;
+
+template <int D>
+struct Nm5Lds {
+    static constexpr bool SWZ = D == 64;
+    static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
+    static constexpr int WS = D + 4;                     // fp32 W staging row stride (read once per wave)
+    static constexpr int WOFF = kNm5Waves * TILE;        // W [out][in] * fold, then the bias * fold
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(WOFF + D * WS + D);
+    static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
+};
+
+#ifndef LG_NM5_NPF
+#define LG_NM5_NPF 4  // neighbour blocks in flight per wave (L-TOWN-A: 97 % of nodes have degree <= 4 with the self loop)
+#endif
+template <int D, bool DROP, bool RELU, bool BF>
+__global__ void __launch_bounds__(64 * kNm5Waves, 2)
+k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
+              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
+              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
+              uint32_t salt, uint16_t* __restrict__ ymask) {
+    using G = NmGeo<D>;
+    using LY = Nm5Lds<D>;
+    constexpr int WAVES = kNm5Waves;
+    constexpr int NPF = LG_NM5_NPF;
+    constexpr int KS = D / 32;      // MFMA k-steps of 32 channels
+    constexpr int NP = BF ? 1 : 3;  // W parts held
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
+    float* tl = reinterpret_cast<float*>(smem) + wave * LY::TILE;
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t xrs0 = nm_rsrc(x, 0);  // an absent neighbour's loads return zeros
+    const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, WAVES);
+    const int64_t tend = sc.end;
+
+    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+        const bool valid = tile < tend;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        n = t32 - grp * N;
+        b0 = grp * 16;
+        nb = valid ? min(16u, B - b0) : 0u;
+    };
+    f32x4 pf[NPF][G::K];
+    uint32_t lo[G::K];
+    NmRec cur;
+    uint32_t cn, cb0, cnb;
+    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+        n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
+        cur = r;
+        cn = n;
+        cb0 = b0;
+        cnb = nb;
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+#pragma unroll
+        for (int i = 0; i < NPF; ++i) {
+            const bool have = r.e0 + i < r.e1;
+            const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
+            const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+                pf[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[k], base, 0));
+        }
+    };
+    auto ldblk = [&](uint32_t base, uint32_t lk) -> f32x4 {
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk, base, 0));
+    };
+    const int64_t t0 = sc.first;
+    // W (16 KiB at D = 64) is read from global memory once per WORKGROUP, before the first
+    // tile's neighbour blocks (vector loads complete in order), staged in LDS, and each wave
+    // takes its fragments from there: read per wave from global memory, every wave of the
+    // launch hit the same 16 KiB at once (6 us of staging in the kernel-lab timeline)
+    float* wst = reinterpret_cast<float*>(smem) + LY::WOFF;
+    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
+        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+        asm volatile("" ::: "memory");
+        uint32_t n0, b00, nb00;
+        tile_coords(t0, n0, b00, nb00);
+        issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i = u * 64 * WAVES + threadIdx.x;
+            if (i < W4) st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), wv[u] * fold);
+        }
+        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
+    }
+    __syncthreads();
+    // this lane's A fragments for the whole launch: W[16 mt + j][32 s2 + 8 q .. + 7] * fold, split
+    // in three bf16 parts; the bias (x fold) of its output channels 16 mt + 4 q .. + 3
+    lg_bf16x8 wf[NP][G::CH][KS];
+#pragma unroll
+    for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
+            lg_bf16x8 f0, f1, f2;
+            split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
+            wf[0][mt][s2] = f0;
+            if constexpr (!BF) {
+                wf[NP > 1 ? 1 : 0][mt][s2] = f1;
+                wf[NP > 2 ? 2 : 0][mt][s2] = f2;
+            }
+        }
+    }
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p_drop);
+
+    int tcount = 0;
+    (void)tcount;
+    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
+    for (int64_t tile = t0; tile < tend; tile += sc.stride) {
+        const uint32_t n = cn, b0 = cb0;
+        const int e0 = cur.e0, e1 = cur.e1;
+        uint32_t tlo[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
+        uint32_t nn, nb0, nnb;
+        tile_coords(tile + sc.stride, nn, nb0, nnb);
+        const NmRec nxt = nm_rec(tab, N + nn);
+        asm volatile("" ::: "memory");  // keep the record request here: the compiler would sink it to its use
+        f32x4 acc[G::K];
+        {
+            const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) acc[k] = pf[0][k] * w;
+        }
+#pragma unroll
+        for (int i = 1; i < NPF; ++i) {
+            if (e0 + i < e1) {
+                const float w = __int_as_float(cur.p[i].y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[i][k]);
+            }
+        }
+        if (e0 + NPF < e1) {  // the rest of the row: inline pairs, then the pair array
+            int2 ip[kLgNmInline - NPF];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) ip[i] = cur.p[NPF + i];
+            // every inline block in flight at once (zeros past the degree), then the sums in CSR order
+            constexpr int NI = kLgNmInline - NPF > 0 ? kLgNmInline - NPF : 1;
+            f32x4 va[NI][G::K];
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) {
+                const bool have = e0 + NPF + i < e1;
+                const uint32_t ba = have ? (static_cast<uint32_t>(ip[i].x) * B + b0) * (4u * D) : 0u;
+                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, tlo[k], ba, 0));
+            }
+#pragma unroll
+            for (int i = 0; i < kLgNmInline - NPF; ++i) {
+                if (e0 + NPF + i < e1) {
+                    const float wa = __int_as_float(ip[i].y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[i][k]);
+                }
+            }
+            for (int e = e0 + kLgNmInline; e < e1; ++e) {
+                const int2 pa = pairs[e];
+                const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                f32x4 va[G::K];
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) va[k] = ldblk(ba, tlo[k]);
+                const float wa = __int_as_float(pa.y);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+            }
+        }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(3 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
+        issue(nxt, nn, nb0, nnb);
+        __builtin_amdgcn_sched_barrier(0);
+
+        // gather layout -> LDS (own tile) -> MFMA B operand
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) st4(tl + LY::tix(G::RPI * k + rl, fg), acc[k]);
+        wave_sync_nm();
+        f32x4 bq[KS][2];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            bq[s2][0] = ld4(tl + LY::tix(j, 8 * s2 + 2 * q));
+            bq[s2][1] = ld4(tl + LY::tix(j, 8 * s2 + 2 * q + 1));
+        }
+        // the row-stream dropout seed (independent of the transform) while the reads land
+        uint32_t st = 0;
+        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            lg_bf16x8 b0f, b1f, b2f;
+#if defined(LG_KERNEL_LAB) && defined(LG_NM5_NOSPLIT)  // lab: no residual VALU (all parts = the hi part)
+            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+            b1f = b0f;
+            b2f = b0f;
+#else
+            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+#endif
+#if defined(LG_KERNEL_LAB) && defined(LG_NM5_NPROD)  // lab: only the NPROD largest products (results WRONG)
+            asm volatile("" ::"v"(b1f), "v"(b2f));
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                if (LG_NM5_NPROD >= 3) o[mt] = mfma_bf(wf[1][mt][s2], b0f, o[mt]);
+                if (LG_NM5_NPROD >= 2) o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+            }
+            continue;
+#endif
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                if constexpr (BF) {
+                    o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+                    continue;
+                }
+                o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
+                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
+                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+            }
+        }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(4 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
+        // epilogue: ReLU as an integer max, row-stream dropout as one compare + select
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float v = o[mt][reg];
+                if constexpr (RELU) v = __int_as_float(max(__float_as_int(v), 0));
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    v = u16 >= thr ? v : 0.0f;
+                }
+                o[mt][reg] = v;
+            }
+        }
+        const uint32_t ob = (n * B + b0) * (4u * D);
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
+        wave_sync_nm();
+        f32x4 vk[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            vk[k] = ld4(tl + LY::tix(G::RPI * k + rl, fg));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                   yrs, tlo[k], ob, 0);
+        }
+        if (ymask) {
+            // [y > 0] = bit 31 of (bits(y) + 0x7FFFFFFF) for y >= +0; alignbit shifts the mask left
+            // by one and takes that bit in, highest element first
+            uint32_t bits = 0;
+#pragma unroll
+            for (int k = G::K - 1; k >= 0; --k)
+#pragma unroll
+                for (int i = 3; i >= 0; --i) {
+                    const uint32_t u = RELU ? __float_as_uint(vk[k][i])
+                                            : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
+                    bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
+                }
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
+                                                  0, 0);
+        }
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
+        ++tcount;
+#endif
+    }
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
+    LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                         static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
+#endif
+}
+
+// ------------------------------------------------------------------ forward, producer / consumer waves
+// The fused layer split by ROLE inside one 8-wave workgroup per CU.  In nm3/nm5 every wave
+// alternates a memory phase (wait for its gathered blocks, accumulate) with a compute phase
+// (transpose, split, 48 MFMAs, epilogue): with 2-3 waves per SIMD each SIMD spent long
+// stretches with all its waves in the same phase (kernel-lab timeline: ~35 % issue, the rest
+// stalled), so neither the memory system nor the SIMDs were kept busy.  Here, per SIMD:
+//   * a PRODUCER wave gathers and accumulates (Ahat x) tiles — two tiles' neighbour blocks
+//     in flight in registers (NPF each) — and hands each finished tile to its consumer
+//     through an LDS ring of R tile slots (16 x D fp32, XOR-swizzled at D = 64);
+//   * a CONSUMER wave reads the slot in the MFMA B layout, splits it, runs the transform
+//     with W's split fragments held in registers for the whole launch, applies bias / ReLU
+//     / dropout, writes y back through the same slot and frees it.
+// Hand-off: per producer/consumer pair a `ready` and a `done` tile counter in LDS (release
+// stores, acquire polls with s_sleep, workgroup scope); the producer reuses slot t % R only
+// after done >= t + 1 - R.  Every poll is bounded (a broken protocol ends the launch with
+// wrong results instead of a hang).  Results are bit-identical to k_gcn_fwd_nm3 (same
+// accumulation order, same products, same masks).
+constexpr int kPcPairs = 4;
+#ifndef LG_PC_RING
+#define LG_PC_RING 4
+#endif
+#ifndef LG_PC_NPF
+#define LG_PC_NPF 4
+#endif
+constexpr int kPcRing = LG_PC_RING;
+
+template <int D>
+struct PcLds {  // floats
+    static constexpr bool SWZ = D == 64;
+    static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
+    static constexpr int WS = D + 4;
+    static constexpr int WOFF = 0;                       // W [out][in] * fold (fp32), then bias * fold
+    static constexpr int FOFF = D * WS + D;              // ready[kPcPairs], done[kPcPairs]
+    static constexpr int MOFF = FOFF + 16;               // per (pair, slot): n, b0, nb, pad
+    static constexpr int ROFF = MOFF + 4 * kPcPairs * kPcRing;  // the rings
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcPairs * kPcRing * TILE);
+    static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
+};
+
+__device__ __forceinline__ uint32_t pc_load_acq(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void pc_store_rel(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until *p >= v (bounded: ~2^20 polls)
+__device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (pc_load_acq(p) >= v) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <int D, bool DROP, bool RELU, bool BF>
+__global__ void __launch_bounds__(128 * kPcPairs, 2)
+k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
+             const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
+             uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
+             uint32_t salt, uint16_t* __restrict__ ymask) {
+    using G = NmGeo<D>;
+    using LY = PcLds<D>;
+    constexpr int NPF = LG_PC_NPF;
+    constexpr int KS = D / 32;
+    constexpr int NP = BF ? 1 : 3;
+    constexpr int R = kPcRing;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    float* wst = lds + LY::WOFF;
+    uint32_t* ready = reinterpret_cast<uint32_t*>(lds + LY::FOFF);
+    uint32_t* done = ready + kPcPairs;
+    uint32_t* meta = reinterpret_cast<uint32_t*>(lds + LY::MOFF);
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pair = wave & (kPcPairs - 1);
+    const bool producer = wave < kPcPairs;
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* ring = lds + LY::ROFF + pair * R * LY::TILE;
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, pair, kPcPairs);
+    const int64_t tend = sc.end;
+    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
+
+    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+        const bool valid = tile < tend;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        n = t32 - grp * N;
+        b0 = grp * 16;
+        nb = valid ? min(16u, B - b0) : 0u;
+    };
+
+    // W (fp32, x fold) and bias to LDS by the whole workgroup; the producers' first tiles go
+    // in flight right after their share of W's loads
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + 128 * kPcPairs - 1) / (128 * kPcPairs);
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 128 * kPcPairs + threadIdx.x, W4 - 1));
+        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i = u * 128 * kPcPairs + threadIdx.x;
+            if (i < W4)
+                st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)),
+                    f32x4{__fmul_rn(wv[u][0], fold), __fmul_rn(wv[u][1], fold), __fmul_rn(wv[u][2], fold),
+                          __fmul_rn(wv[u][3], fold)});
+        }
+        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = __fmul_rn(bb, fold);
+        if (threadIdx.x < 2 * kPcPairs) ready[threadIdx.x] = 0u;  // ready[] and done[]
+    }
+    __syncthreads();
+
+    if (producer) {
+        // ---------------- producer: gather + accumulate, two tiles in flight
+        const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), xrs0 = nm_rsrc(x, 0);
+        uint32_t loff[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+        f32x4 pf[2][NPF][G::K];
+        uint32_t lo[2][G::K];
+        NmRec rec[2];
+        uint32_t tn[2], tb0[2], tnb[2];
+        // r: the tile's node-table record (schedule section: slot -> record with its node id),
+        // requested by the caller a phase earlier
+        auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
+            constexpr int b = decltype(bc)::value;
+            uint32_t n, b0, nb;
+            tile_coords(tile, n, b0, nb);
+            rec[b] = r;
+            n = static_cast<uint32_t>(r.node);
+            tn[b] = n;
+            tb0[b] = b0;
+            tnb[b] = nb;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) lo[b][k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+                const bool have = r.e0 + i < r.e1;
+                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
+                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    pf[b][i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], base, 0));
+            }
+        };
+        // tile t of this pair from buffer b: accumulate, hand over, refill b with tile t + 2
+        auto step = [&](auto bc, int64_t t) -> bool {
+            constexpr int b = decltype(bc)::value;
+            const int64_t tile = sc.first + t * sc.stride;
+            if (tile >= tend) return false;
+            // the record of tile t + 2 goes in flight while this tile is accumulated
+            uint32_t nn, nb0, nnb;
+            tile_coords(tile + 2 * sc.stride, nn, nb0, nnb);
+            const NmRec nxt = nm_rec(tab, N + nn);
+            asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
+            const NmRec& cur = rec[b];
+            const int e0 = cur.e0, e1 = cur.e1;
+            const uint32_t b0 = tb0[b];
+            f32x4 acc[G::K];
+            {
+                const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k) acc[k] = pf[b][0][k] * w;
+            }
+#pragma unroll
+            for (int i = 1; i < NPF; ++i) {
+                if (e0 + i < e1) {
+                    const float w = __int_as_float(cur.p[i].y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[b][i][k]);
+                }
+            }
+            if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): in place
+#pragma unroll
+                for (int i = NPF; i < kLgNmInline; ++i) {
+                    if (e0 + i < e1) {
+                        const uint32_t ba = (static_cast<uint32_t>(cur.p[i].x) * B + b0) * (4u * D);
+                        f32x4 va[G::K];
+#pragma unroll
+                        for (int k = 0; k < G::K; ++k)
+                            va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
+                        const float wa = __int_as_float(cur.p[i].y);
+#pragma unroll
+                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+                    }
+                }
+                for (int e = e0 + kLgNmInline; e < e1; ++e) {
+                    const int2 pa = pairs[e];
+                    const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                    f32x4 va[G::K];
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k)
+                        va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
+                    const float wa = __int_as_float(pa.y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+                }
+            }
+            const int sl = static_cast<int>(t % R);
+            const uint32_t mn = tn[b], mnb = tnb[b];
+            // buffer b is free again: tile t + 2 goes in flight before the hand-off waits
+            issue(bc, nxt, tile + 2 * sc.stride);
+            if (t >= R) pc_wait(&done[pair], static_cast<uint32_t>(t + 1 - R));
+            float* slot = ring + sl * LY::TILE;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
+            if (lane == 0) {
+                uint32_t* m = meta + 4 * (pair * R + sl);
+                m[0] = mn;
+                m[1] = b0;
+                m[2] = mnb;
+            }
+            pc_store_rel(&ready[pair], static_cast<uint32_t>(t + 1));
+            return true;
+        };
+        {
+            uint32_t n0, b00, nb00, n1, b01, nb01;
+            tile_coords(sc.first, n0, b00, nb00);
+            tile_coords(sc.first + sc.stride, n1, b01, nb01);
+            const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
+            issue(std::integral_constant<int, 0>{}, r0, sc.first);
+            issue(std::integral_constant<int, 1>{}, r1, sc.first + sc.stride);
+        }
+        for (int64_t t = 0;; t += 2) {
+            if (!step(std::integral_constant<int, 0>{}, t)) break;
+            if (!step(std::integral_constant<int, 1>{}, t + 1)) break;
+        }
+        return;
+    }
+
+    // ---------------- consumer: transform + epilogue
+    const __amdgpu_buffer_rsrc_t yrs = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    lg_bf16x8 wf[NP][G::CH][KS];
+#pragma unroll
+    for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
+            lg_bf16x8 f0, f1, f2;
+            split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
+            wf[0][mt][s2] = f0;
+            if constexpr (!BF) {
+                wf[NP > 1 ? 1 : 0][mt][s2] = f1;
+                wf[NP > 2 ? 2 : 0][mt][s2] = f2;
+            }
+        }
+    }
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p_drop);
+    for (int64_t t = 0;; ++t) {
+        const int64_t tile = sc.first + t * sc.stride;
+        if (tile >= tend) break;
+        const int sl = static_cast<int>(t % R);
+        pc_wait(&ready[pair], static_cast<uint32_t>(t + 1));
+        float* slot = ring + sl * LY::TILE;
+        const uint32_t* m = meta + 4 * (pair * R + sl);
+        const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
+                       nb = __builtin_amdgcn_readfirstlane(m[2]);
+        f32x4 bq[KS][2];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            bq[s2][0] = ld4(slot + LY::tix(j, 8 * s2 + 2 * q));
+            bq[s2][1] = ld4(slot + LY::tix(j, 8 * s2 + 2 * q + 1));
+        }
+        uint32_t st = 0;
+        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+        f32x4 o[G::CH];
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            lg_bf16x8 b0f, b1f, b2f;
+            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                if constexpr (BF) {
+                    o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+                    continue;
+                }
+                o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
+                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
+                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
+                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+            }
+        }
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) {
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                float v = o[mt][reg];
+                if constexpr (RELU) v = __int_as_float(max(__float_as_int(v), 0));
+                if constexpr (DROP) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    v = u16 >= thr ? v : 0.0f;
+                }
+                o[mt][reg] = v;
+            }
+        }
+        // y back through the slot (the B-operand reads above are older LDS operations of
+        // this wave, so they complete first)
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) st4(slot + LY::tix(j, 4 * mt + q), o[mt]);
+        const uint32_t ob = (n * B + b0) * (4u * D);
+        f32x4 vk[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) {
+            const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+            vk[k] = ld4(slot + LY::tix(G::RPI * k + rl, fg));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                   yrs, lk, ob, 0);
+        }
+        if (ymask) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int k = G::K - 1; k >= 0; --k)
+#pragma unroll
+                for (int i = 3; i >= 0; --i) {
+                    const uint32_t u = RELU ? __float_as_uint(vk[k][i])
+                                            : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
+                    bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
+                }
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
+                                                  0, 0);
+        }
+        pc_store_rel(&done[pair], static_cast<uint32_t>(t + 1));  // the slot's reads are done (release)
     }
 }
 
@@ -1446,17 +2244,74 @@ auto nm2_kernel(int flags) {
 #endif
     return split ? k_gcn_fwd_nm2<D, DR, 4, true, 0> : k_gcn_fwd_nm2<D, DR, 4, false, 0>;
 }
+// OPT of the pipelined forward: the build default, or (kernel-lab builds) flags bits 8..11
+// when LG_F_LAB_OPT is set.
+int nm3_opt(int flags) {
+#ifdef LG_KERNEL_LAB
+    const bool ovr = (flags & LG_F_LAB_OPT) && !(flags & (LG_F_F32_MFMA | LG_F_BF16 | LG_F_LAB_DST)) &&
+                     ((flags >> 28) & 7) == 0;
+    if (ovr) return (flags >> LG_F_LAB_OPT_SHIFT) & 15;
+#endif
+    (void)flags;
+    return kNm3OptDefault;
+}
+template <int D, int WV>
+size_t nm3_lds_bytes(bool split, int opt) {
+    switch (opt & (kNm3WFrag | kNm3Swz)) {  // the only bits that change the LDS image
+        case kNm3WFrag: return split ? Nm3Lds<D, true, WV, kNm3WFrag>::BYTES : Nm3Lds<D, false, WV, kNm3WFrag>::BYTES;
+        case kNm3Swz: return split ? Nm3Lds<D, true, WV, kNm3Swz>::BYTES : Nm3Lds<D, false, WV, kNm3Swz>::BYTES;
+        case kNm3WFrag | kNm3Swz:
+            return split ? Nm3Lds<D, true, WV, kNm3WFrag | kNm3Swz>::BYTES
+                         : Nm3Lds<D, false, WV, kNm3WFrag | kNm3Swz>::BYTES;
+        default: return split ? Nm3Lds<D, true, WV, 0>::BYTES : Nm3Lds<D, false, WV, 0>::BYTES;
+    }
+}
 template <int D, bool DR, bool RL, int WV>
 auto nm3_kernel(int flags) {
-    if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, true>;
+    constexpr int OD = kNm3OptDefault;
+    if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, true, OD>;
     const bool split = (flags & LG_F_F32_MFMA) == 0;
 #ifdef LG_KERNEL_LAB
     const bool dst = (flags & LG_F_LAB_DST) != 0;
+    const int lab = (flags >> 28) & 7;
+    if constexpr (D == 64 && WV == 4) {
+        if ((flags & LG_F_LAB_OPT) && split && !dst && lab == 0) {  // the same test as nm3_opt
+#define LG_NM3_OPTC(O) \
+    case O:            \
+        return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, false, O>;
+            switch (nm3_opt(flags)) {
+                LG_NM3_OPTC(0)
+                LG_NM3_OPTC(1)
+                LG_NM3_OPTC(2)
+                LG_NM3_OPTC(3)
+                LG_NM3_OPTC(4)
+                LG_NM3_OPTC(5)
+                LG_NM3_OPTC(6)
+                LG_NM3_OPTC(7)
+                LG_NM3_OPTC(8)
+                LG_NM3_OPTC(12)
+                LG_NM3_OPTC(14)
+                LG_NM3_OPTC(15)
+                LG_NM3_OPTC(16)
+                LG_NM3_OPTC(20)
+                LG_NM3_OPTC(22)
+                LG_NM3_OPTC(23)
+                LG_NM3_OPTC(24)
+                LG_NM3_OPTC(28)
+                LG_NM3_OPTC(30)
+                LG_NM3_OPTC(31)
+                default: break;
+            }
+#undef LG_NM3_OPTC
+        }
+    }
 #define LG_NM3_LAB(L)                                                                                              \
     case L:                                                                                                        \
-        return split ? (dst ? k_gcn_fwd_nm3<D, DR, RL, true, WV, L, true> : k_gcn_fwd_nm3<D, DR, RL, true, WV, L>) \
-                     : (dst ? k_gcn_fwd_nm3<D, DR, RL, false, WV, L, true> : k_gcn_fwd_nm3<D, DR, RL, false, WV, L>);
-    switch ((flags >> 28) & 7) {
+        return split ? (dst ? k_gcn_fwd_nm3<D, DR, RL, true, WV, L, true, false, OD>                              \
+                            : k_gcn_fwd_nm3<D, DR, RL, true, WV, L, false, false, OD>)                             \
+                     : (dst ? k_gcn_fwd_nm3<D, DR, RL, false, WV, L, true, false, OD>                             \
+                            : k_gcn_fwd_nm3<D, DR, RL, false, WV, L, false, false, OD>);
+    switch (lab) {
         LG_NM3_LAB(0)
         LG_NM3_LAB(1)
         LG_NM3_LAB(2)
@@ -1469,7 +2324,8 @@ auto nm3_kernel(int flags) {
     }
 #undef LG_NM3_LAB
 #endif
-    return split ? k_gcn_fwd_nm3<D, DR, RL, true, WV, 0> : k_gcn_fwd_nm3<D, DR, RL, false, WV, 0>;
+    return split ? k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, false, OD>
+                 : k_gcn_fwd_nm3<D, DR, RL, false, WV, 0, false, false, OD>;
 }
 
 }  // namespace
@@ -1497,6 +2353,13 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     const bool w5 = (flags & LG_F_LAB_W5) != 0;
     const bool relu = (flags & LG_F_RELU) != 0;
     const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
+    const bool bf16 = (flags & LG_F_BF16) != 0;
+    // the W-in-registers pipeline (k_gcn_fwd_nm5): same results as nm3, split or bf16 transform
+    const bool nm5 = (flags & LG_F_NM5) && !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) &&
+                     ((flags >> 28) & 7) == 0;
+    // the producer / consumer pipeline (k_gcn_fwd_pc): same results
+    const bool pc = (flags & LG_F_PC) && !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) &&
+                    ((flags >> 28) & 7) == 0;
     (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
@@ -1517,21 +2380,36 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
             const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
             lg_launch(kern, grid, 64 * kNm2Waves, dyn2, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
                                                     dropout_p, scale, seed, salt);                                 \
+        } else if (pc) {                                                                                           \
+            auto kern = relu ? (bf16 ? k_gcn_fwd_pc<DD, DR, true, true> : k_gcn_fwd_pc<DD, DR, true, false>)       \
+                             : (bf16 ? k_gcn_fwd_pc<DD, DR, false, true> : k_gcn_fwd_pc<DD, DR, false, false>);    \
+            const size_t dynp = PcLds<DD>::BYTES;                                                                  \
+            const int grid = nm_grid(kern, 128 * kPcPairs, dynp, ntiles, kPcPairs, 1);                             \
+            lg_launch(kern, grid, 128 * kPcPairs, dynp, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale,\
+                      seed, salt, ymask);                                                                          \
+        } else if (nm5) {                                                                                          \
+            auto kern = relu ? (bf16 ? k_gcn_fwd_nm5<DD, DR, true, true> : k_gcn_fwd_nm5<DD, DR, true, false>)     \
+                             : (bf16 ? k_gcn_fwd_nm5<DD, DR, false, true> : k_gcn_fwd_nm5<DD, DR, false, false>);  \
+            const size_t dyn5 = Nm5Lds<DD>::BYTES;                                                                 \
+            const int grid = nm_grid(kern, 64 * kNm5Waves, dyn5, ntiles, kNm5Waves,                               \
+                                     ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? bpc : 2);                             \
+            lg_launch(kern, grid, 64 * kNm5Waves, dyn5, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, \
+                      seed, salt, ymask);                                                                          \
         } else if (w5) {                                                                                           \
             auto kern = relu ? nm3_kernel<DD, DR, true, 5>(flags) : nm3_kernel<DD, DR, false, 5>(flags);           \
-            const size_t dyn3 = split ? Nm3Lds<DD, true, 5>::BYTES : Nm3Lds<DD, false, 5>::BYTES;                  \
+            const size_t dyn3 = nm3_lds_bytes<DD, 5>(split, kNm3OptDefault);                  \
             const int grid = nm_grid(kern, 64 * 5, dyn3, ntiles, 5, bpc);                                          \
             lg_launch(kern, grid, 64 * 5, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
                                             salt, ymask);                                                                 \
         } else if (w8) {                                                                                           \
             auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
-            const size_t dyn3 = split ? Nm3Lds<DD, true, 8>::BYTES : Nm3Lds<DD, false, 8>::BYTES;                  \
+            const size_t dyn3 = nm3_lds_bytes<DD, 8>(split, kNm3OptDefault);                  \
             const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
             lg_launch(kern, grid, 64 * 8, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
                                             salt, ymask);                                                                 \
         } else {                                                                                                   \
             auto kern = relu ? nm3_kernel<DD, DR, true, 4>(flags) : nm3_kernel<DD, DR, false, 4>(flags);           \
-            const size_t dyn3 = split ? Nm3Lds<DD, true, 4>::BYTES : Nm3Lds<DD, false, 4>::BYTES;                  \
+            const size_t dyn3 = nm3_lds_bytes<DD, 4>(split, DD == 64 ? nm3_opt(flags) : kNm3OptDefault);                  \
             const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
             lg_launch(kern, grid, 64 * 4, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
                                             salt, ymask);                                                                 \
@@ -1548,6 +2426,20 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
+
+#ifdef LG_NM3_STAMPS
+// kernel-lab timeline readout (LG_NM3_STAMPS builds only; see g_nm3_stamps)
+extern "C" int lg_lab_nm3_stamps(uint64_t* host, int64_t n) {
+    if (n > static_cast<int64_t>(8192) * kNm3Stamps) return LG_EINVAL;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nm3_stamps), static_cast<size_t>(n) * 8) == hipSuccess ? LG_OK
+                                                                                                         : LG_EHIP;
+}
+extern "C" int lg_lab_nm3_stamps_clear(void) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_nm3_stamps)) != hipSuccess) return LG_EHIP;
+    return hipMemset(p, 0, sizeof(uint64_t) * 8192 * kNm3Stamps) == hipSuccess ? LG_OK : LG_EHIP;
+}
+#endif
 
 extern "C" int lg_gcn_fwd_nm(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                              const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,

@@ -134,9 +134,9 @@ extern "C" int lg_cross_entropy_fwd(const float* logits, const int64_t* target, 
                                     lg_stream_t stream) {
     if (B < 0 || C <= 0 || ldx < C || !loss || !counter) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
-    if (B == 0) {
-        const float nan = __builtin_nanf("");
-        return hipMemcpyAsync(loss, &nan, sizeof(float), hipMemcpyHostToDevice, s) == hipSuccess ? LG_OK : LG_EHIP;
+    if (B == 0) {  // the mean over no rows is NaN (torch); a memset node, so the call stays capturable
+        return hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(loss), 0x7FC00000, 1, s) == hipSuccess ? LG_OK
+                                                                                                          : LG_EHIP;
     }
     if (!logits || !target || !lse || !rowloss) return LG_EINVAL;
     const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, 4 * lg_num_cus()));

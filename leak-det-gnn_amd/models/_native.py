@@ -30,6 +30,8 @@ LG_F_LAB_NM2 = 0x00200000  # lg_gcn_fwd_nm schedule: round-1 rowptr-walking pipe
 LG_F_BF16 = 0x40  # lg_gcn_fwd_nm / lg_gcn_bwd_nm / lg_edge_head_*: the bf16 node-MLP tier
 LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel lab)
 LG_F_LAB_W5 = 0x00040000  # lg_gcn_fwd_nm schedule: 5-wave workgroups (kernel lab)
+LG_F_NM5 = 0x00002000  # lg_gcn_fwd_nm schedule: W-in-registers pipeline (same results)
+LG_F_PC = 0x00004000  # lg_gcn_fwd_nm schedule: producer / consumer waves (same results)
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)

@@ -79,6 +79,17 @@ class GradAllReduce:
             off += n
 
 
+def rank_generator_seed(seed: int, rank: int) -> int:
+    """torch generator seed of `rank` for everything drawn AFTER the model is built.  Every
+    rank builds the model from the same seed (identical initial weights), then reseeds
+    with this: the dropout seeds the library draws per step (library.seed_tensor, the
+    captured step's SeedSlots) come from torch's generator, and dropout masks are indexed
+    by the rank-LOCAL row, so with one seed on every rank local window i would get the
+    same mask on all ranks (a global batch of 512 on 8 ranks: 64 distinct patterns).
+    Callers reseed only at world > 1, so a 1-process run draws what it always drew."""
+    return (int(seed) + 0x9E3779B1 * int(rank)) % (1 << 63)
+
+
 def shard_range(global_batch: int, rank: int, world: int) -> range:
     """Contiguous per-rank slice of the global sample index range (datasets are seeded by
     seed + idx, datasets.py:236,490, so the global batch is the same at any world size)."""

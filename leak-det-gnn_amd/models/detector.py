@@ -166,7 +166,7 @@ class LeakDetector(nn.Module):
             if h_s.requires_grad:
                 h_s.retain_grad()
             self.capture["h_s"] = h_s
-        nm = ops.use_node_major(B, N, D)
+        nm = ops.use_node_major(B, N, D, bf16=self.mlp_dtype == "bf16")
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
         # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init

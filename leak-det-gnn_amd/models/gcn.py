@@ -15,15 +15,17 @@ Here forward runs the registered op leakgnn::gcn_conv (models/library.py: the fu
 HIP kernel lg_gcn_fwd, (Ahat x) W^T + b in one launch) and its autograd formula
 leakgnn::gcn_conv_backward (lg_gcn_bwd).  The gcn_norm'ed CSR is built on the device
 (lg_graph_build) and, unlike PyG with cached=False, re-used while an edge_index
-with the SAME CONTENT is passed again (compared element-wise against a private
-copy, one device-side equality check per call) — the graph is a pure function of
-edge_index, so results are unchanged.  Keying on the storage address alone would
-reuse a stale CSR when the caching allocator hands a freed edge_index's address
-to a different graph of the same shape.
+with the SAME CONTENT is passed again — the graph is a pure function of edge_index,
+so results are unchanged.  The same tensor object at the same version counter is a
+hit with no device work (so a HIP-graph-captured step never syncs); any other tensor
+is compared element-wise with a private copy.  Keying on the storage address alone
+would reuse a stale CSR when the caching allocator hands a freed edge_index's
+address to a different graph of the same shape.
 """
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Optional
 
 import torch
@@ -67,9 +69,22 @@ class GCNConv(nn.Module):
         self._graph_key = None
         self._graph_ei = None
         self._graph = None
+        self._graph_ref = None
+        self._graph_ver = -1
 
     def graph_for(self, edge_index: torch.Tensor, num_nodes: int, device: torch.device) -> GCNGraph:
+        """The cached CSR of `edge_index`.  Fast path (no device sync, capture-safe): the SAME
+        tensor object as last time (a weak reference, so a new tensor at a recycled address
+        never matches) at the same version counter.  Otherwise the content is compared with
+        the cached copy (a sync) and the CSR rebuilt if it differs."""
         key = (tuple(edge_index.shape), edge_index.dtype, int(num_nodes), device)
+        ref = self._graph_ref() if self._graph_ref is not None else None
+        if (self._graph is not None and self._graph_key == key and ref is edge_index
+                and edge_index._version == self._graph_ver):
+            return self._graph
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("GCNConv: a new edge_index inside HIP graph capture; run one eager forward with it "
+                               "first (the CSR is built and cached outside the capture)")
         ei = edge_index.to(device)
         if (self._graph is None or self._graph_key != key or self._graph_ei is None
                 or not torch.equal(self._graph_ei, ei)):
@@ -77,6 +92,8 @@ class GCNConv(nn.Module):
                                          normalize=self.normalize, improved=self.improved)
             self._graph_key = key
             self._graph_ei = ei.clone()
+        self._graph_ref = weakref.ref(edge_index)
+        self._graph_ver = edge_index._version
         return self._graph
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor] = None):

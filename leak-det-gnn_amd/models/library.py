@@ -353,6 +353,8 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     B, S, Ds = h_s.shape
     D = proj_weight.shape[0]
     _check_d(D)
+    if bf16 and not node_major:  # the window-major kernels have no bf16 form (ops.use_node_major)
+        raise ValueError("gnn_trunk: the bf16 tier runs on the node-major layout only")
     if tuple(proj_weight.shape) != (D, Ds + 1):
         raise ValueError(f"proj_weight must be (D, Ds + 1) = ({D}, {Ds + 1}), got {tuple(proj_weight.shape)}")
     N = sensor_slot.shape[0]

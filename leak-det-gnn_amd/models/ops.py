@@ -39,11 +39,20 @@ TRUNK_NODE_MAJOR = os.environ.get("LEAKGNN_LAYOUT", "node") != "window"
 NM_MAX_BYTES = 0x7FFFF000  # lg_gcn_fwd_nm / lg_gcn_bwd_nm: one [N][B][D] activation per launch
 
 
-def use_node_major(B: int, N: int, D: int) -> bool:
+def use_node_major(B: int, N: int, D: int, bf16: bool = False) -> bool:
     """Trunk layout for a batch: node-major when a 16-window tile is mostly full (B >= 16)
     and the activation fits one node-major launch; window-major otherwise (B = 1 graphs
-    such as C5, where a node-major tile would carry 1 window in 16)."""
-    return TRUNK_NODE_MAJOR and B >= 16 and N * B * D * 4 <= NM_MAX_BYTES
+    such as C5, where a node-major tile would carry 1 window in 16).  The bf16 node-MLP
+    tier exists only in the node-major kernels (the window-major ones compute fp32), so
+    bf16 takes the node-major layout at every B: the tier's precision never depends on the
+    batch size (a small per-rank batch, a ragged eval batch)."""
+    fits = N * B * D * 4 <= NM_MAX_BYTES
+    if bf16:
+        if not fits:
+            raise NotImplementedError(f"bf16 tier: a node-major activation of {N * B * D * 4} bytes exceeds "
+                                      f"one launch ({NM_MAX_BYTES}); use a smaller batch or fp32")
+        return True
+    return TRUNK_NODE_MAJOR and B >= 16 and fits
 
 
 # lg_gcn_fwd_nm schedule / transform bits (LG_F_F32_MFMA, LG_F_LAB_*; include/leakgnn.h) for A/B

@@ -47,6 +47,12 @@ class ClipAdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = load_library()
+        live = [g for g in self.param_groups if any(p.grad is not None for p in g["params"])]
+        if len(live) > 1 and any(g["max_norm"] is not None for g in live):
+            # clip_grad_norm_(model.parameters()) takes ONE norm over every parameter; the fused
+            # launch clips per group, which equals it only for a single group
+            raise RuntimeError("ClipAdamW: max_norm with more than one param group is not supported "
+                               "(clip_grad_norm_ takes one norm over all parameters); use one group")
         for gi, group in enumerate(self.param_groups):
             params = [p for p in group["params"] if p.grad is not None]
             if not params:

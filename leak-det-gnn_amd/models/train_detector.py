@@ -40,7 +40,7 @@ import torch
 import torch.nn as nn
 
 from .datasets import AbruptLeakDetectorDataset, SensorStandardizer
-from .ddp import GradAllReduce, dist_env, init_distributed
+from .ddp import GradAllReduce, dist_env, init_distributed, rank_generator_seed
 from .detector import LeakDetector
 from .loss import CrossEntropyLoss
 from .optim import ClipAdamW
@@ -244,6 +244,10 @@ def main(argv=None) -> None:
         opt = torch.optim.AdamW(detector.parameters(), lr=args.lr, weight_decay=args.weight_decay)
     loss_fn = CrossEntropyLoss()  # torch's own path on the CPU
     allreduce = GradAllReduce(detector.parameters())  # no-op at world 1
+    # identical weights on every rank (built above from args.seed); from here on each rank
+    # draws its own dropout seeds
+    if world > 1:
+        torch.manual_seed(rank_generator_seed(args.seed, rank))
     evaluator = DetectorEvaluator(predictor=predictor, detector=detector, device=device, l_pred=args.l_pred,
                                   l_det=args.l_det,
                                   metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
@@ -287,6 +291,17 @@ def main(argv=None) -> None:
             noisy_seg = batch["noisy_seg"].to(device)
             time_seg = batch["time_seg"].to(device)
             label = torch.as_tensor(batch["label"], device=device, dtype=torch.long)
+            if noisy_seg.size(0) == 0:  # a ragged last global batch left this rank no windows
+                # (mean CE over no rows is NaN): contribute zero gradients to the all-reduce and
+                # take the same optimizer step as the other ranks
+                opt.zero_grad(set_to_none=True)
+                for p in detector.parameters():
+                    p.grad = torch.zeros_like(p)
+                allreduce()
+                if clip is not None and not fused_step:
+                    torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
+                opt.step()
+                continue
             with torch.no_grad():
                 residual = build_residual_sequence_from_segment(predictor, noisy_seg, time_seg, l_pred=args.l_pred,
                                                                 l_det=args.l_det, device=device)

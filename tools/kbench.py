@@ -55,17 +55,67 @@ def timeit(fn, iters):
     return a.elapsed_time(b) * 1e3 / iters  # us
 
 
+def stamps_summary(lib, launch):
+    """One eager launch of the LG_NM3_STAMPS lab forward, then its per-wave timeline: start /
+    end skew, tiles per wave and the three phases per tile (rows waited for and accumulated,
+    transform, epilogue + stores), in microseconds at the clock derived from the stamps."""
+    import ctypes
+    lib.lg_lab_nm3_stamps_clear.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    torch.cuda.synchronize()
+    check(lib.lg_lab_nm3_stamps_clear(), "stamps clear")
+    torch.cuda.synchronize()
+    launch()
+    torch.cuda.synchronize()
+    n = 8192 * 24
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib.lg_lab_nm3_stamps(buf.ctypes.data, n), "stamps read")
+    st = buf.reshape(8192, 24).astype(np.int64)
+    st = st[st[:, 0] != 0]
+    rt0, rt1, c0, c1 = st[:, 0], st[:, 22], st[:, 1], st[:, 21]
+    ghz = float(np.median((c1 - c0) / np.maximum(rt1 - rt0, 1))) * 0.1  # memrealtime is 100 MHz
+    us = lambda cyc: cyc / (ghz * 1e3)
+    t0 = rt0.min()
+    start = (rt0 - t0) / 100.0
+    end = (rt1 - t0) / 100.0
+    tiles = np.array([sum(1 for t in range(6) if r[5 + 3 * t] != 0) for r in st])
+    ph = {"wait_acc": [], "transform": [], "epilogue": [], "staging": us(st[:, 2] - st[:, 1]).tolist()}
+    for r in st:
+        prev = r[2]
+        for t in range(6):
+            if r[5 + 3 * t] == 0:
+                break
+            ph["wait_acc"].append(us(r[3 + 3 * t] - prev))
+            ph["transform"].append(us(r[4 + 3 * t] - r[3 + 3 * t]))
+            ph["epilogue"].append(us(r[5 + 3 * t] - r[4 + 3 * t]))
+            prev = r[5 + 3 * t]
+    q = lambda a: [round(float(np.percentile(a, p)), 3) for p in (10, 50, 90, 99)]
+    xcc = (st[:, 23] >> 32) & 0xF
+    return {"waves": int(len(st)), "clock_GHz": round(ghz, 3), "span_us": round(float(end.max()), 3),
+            "start_us_p10_50_90_99": q(start), "end_us_p10_50_90_99": q(end),
+            "life_us_mean": round(float((end - start).mean()), 3),
+            "tiles_hist": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
+            **{f"{k}_us_p10_50_90_99": q(v) for k, v in ph.items() if len(v)},
+            "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,gcn_fwd_nm,gcn_fwd_nm_train,gcn_bwd_nm,spmm,"
                                        "edge_fwd,edge_bwd,gru_fwd,gru_bwd")
     ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--graph", default="ltown", choices=["ltown", "selfonly", "ring"],
+                    help="lab graphs on L-TOWN-A's 661 nodes: selfonly = no edges (one gathered block per "
+                         "tile), ring = a cycle (three blocks per tile, neighbours adjacent)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
     ap.add_argument("--edgelab", default="", help="comma list of lg_edge_head_fwd lab bits (1 nomfma, 2 noload, "
                                                    "4 nosplit; LEAKGNN_LIB=lib/lab build only)")
     ap.add_argument("--nmlab", default="", help="comma list of lg_gcn_fwd_nm schedules: v1 or bpc<n> (train mode)")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of a replayed HIP graph")
+    ap.add_argument("--stamps", action="store_true", help="per-wave timeline of each --nmlab train launch "
+                                                           "(LEAKGNN_LIB=lib/lab_stamps build only)")
     args = ap.parse_args()
     global GRAPH
     GRAPH = not args.eager
@@ -74,6 +124,12 @@ def main():
     g = np.load(REPO / "tests/golden/graph_ltown_a.npz")
     ei = torch.from_numpy(g["edge_index"])
     N, D, B = 661, 64, args.B
+    if args.graph == "selfonly":
+        ei = torch.zeros(2, 0, dtype=torch.long)
+    elif args.graph == "ring":
+        a = torch.arange(N)
+        b = (a + 1) % N
+        ei = torch.stack([torch.cat([a, b]), torch.cat([b, a])])
     graph = GCNGraph.build(ei, N, dev)
     inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), N, dev)
     P = inc.num_pipes
@@ -110,20 +166,26 @@ def main():
                                                       1, cs()), name)
             t = timeit(f, args.iters)
             res[name] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+    ymask = torch.empty(N * ((B + 15) // 16) * 64, device=dev, dtype=torch.int16)
     for lab in [v for v in args.nmlab.split(",") if v]:
-        bits = 0
+        bits, with_mask = 0, False
         for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
             bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "w5": nat.LG_F_LAB_W5, "nomfma": 1 << 28,
-                     "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA}.get(tok, 0)
+                     "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA,
+                     "bf16": nat.LG_F_BF16, "nm5": nat.LG_F_NM5, "pc": nat.LG_F_PC}.get(tok, 0)
             if tok.startswith("bpc"):
                 bits |= int(tok[3:]) << 24
+            if tok.startswith("opt"):  # lab OPT variant of the D = 64 forward (LG_F_LAB_OPT, bits 8..11)
+                bits |= 0x00001000 | (int(tok[3:]) << 8)
+            with_mask |= tok == "mask"  # the last layer's form: [y > 0] bits written beside y
         for mode, fl in (("eval", 0), ("train", nat.LG_F_DROPOUT)):
-            f = lambda fl=fl, bits=bits: check(lib.lg_gcn_fwd_nm(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W),
-                                                                 ptr(bias), ptr(y), B, N, D, E1,
-                                                                 nat.LG_F_BIAS | nat.LG_F_RELU | fl | bits, 0.1, 123,
-                                                                 1, cs()), "nmlab")
+            f = lambda fl=fl, bits=bits, wm=with_mask: check(lib.lg_gcn_fwd_nm_bits(
+                ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias), ptr(y), B, N, D, E1,
+                nat.LG_F_BIAS | nat.LG_F_RELU | fl | bits, 0.1, 123, 1, cs(), ptr(ymask) if wm else None), "nmlab")
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+            if args.stamps and mode == "train" and hasattr(lib, "lg_lab_nm3_stamps"):
+                res[f"stamps_{lab}"] = stamps_summary(lib, f)
     # gcn_bwd_nm: the training step's layer-2 backward (output mask as the forward's ymask
     # bits); gcn_bwd_nm_y: the same with the mask gathered from y
     for name, fl, nbias in (("gcn_bwd_nm", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
@@ -278,7 +340,7 @@ def main():
             res["tcn_residual_stock"] = {"us": t, "segments_per_s": B / t * 1e6}
             mutils.RESIDUAL_FAST_PATH = True
     for k, v in res.items():
-        print(k, json.dumps({a: round(b, 2) for a, b in v.items()}))
+        print(k, json.dumps({a: round(b, 2) if isinstance(b, float) else b for a, b in v.items()}))
 
 
 if __name__ == "__main__":
