@@ -363,6 +363,53 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
                                  "avg_launch_us": round(fwd_ms * 1e3, 2)}}
 
 
+def c5_leg(dev, iters: int = 20) -> dict:
+    """BASELINE configs[4], "the HBM-roofline stress of scatter-aggregate": ONE synthetic pipe
+    graph of 100,000 nodes / 300,000 edge columns (150,000 pipes, models/synth.py, seed 0),
+    D = 64, B = 1: GCNConv(64, 64) forward and backward through the product's module (the
+    B = 1 path: lg_gcn_fwd / lg_gcn_bwd), x ~ N(0, 1) seed 0.  Roofline bytes per forward
+    call from SURVEY §8(d): 8 B N D + 4 (N + 1) + 8 E' = 54.8 MB (E' = E + N); backward:
+    read dy (gathered) and x, write dx: 12 B N D + CSR bytes.  HIP events on the launch
+    stream (the library's kernel timer), mean over `iters` calls after warm-up."""
+    from models import ops
+    from models.gcn import GCNConv
+    from models.synth import synthetic_pipe_graph
+    N, P, D = 100_000, 150_000, 64
+    ei, _ = synthetic_pipe_graph(N, P, seed=0)
+    torch.manual_seed(0)
+    conv = GCNConv(D, D).to(dev)
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(N, D, generator=gen).to(dev).requires_grad_(True)
+    dy = torch.randn(N, D, generator=gen).to(dev)
+    eid = ei.to(dev)
+    for _ in range(3):
+        conv(x, eid).backward(dy)
+    torch.cuda.synchronize()
+    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd"])
+    ops.set_kernel_timer(timer)
+    timer.enabled = True
+    for _ in range(iters):
+        x.grad = None
+        conv(x, eid).backward(dy)
+    torch.cuda.synchronize()
+    timer.enabled = False
+    ops.set_kernel_timer(None)
+    fwd_ms, bwd_ms = timer.mean_ms("gcn_fwd"), timer.mean_ms("gcn_bwd")
+    E1 = int(ei.shape[1]) + N
+    csr = 4 * (N + 1) + 8 * E1
+    fwd_bytes, bwd_bytes = 8 * N * D + csr, 12 * N * D + csr
+    fg, bg = fwd_bytes / (fwd_ms * 1e-3) / 1e9, bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    return {"metric": "GCNConv fwd / bwd on one synthetic 100k-node / 300k-edge-column graph (BASELINE configs[4])",
+            "nodes": N, "edge_columns": int(ei.shape[1]), "feat": D, "windows": 1, "scaling": "replicas only",
+            "path": "models.gcn.GCNConv (lg_gcn_fwd / lg_gcn_bwd, window-major = node order at B = 1)",
+            "roofline": {"kernel": "lg_gcn_fwd (K5+K6+K7 fused)", "bound": "hbm", "achieved": round(fg, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fg / HBM_PEAK_GBS, 4),
+                         "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
+            "roofline_bwd": {"kernel": "lg_gcn_bwd (dx, dW, db)", "bound": "hbm", "achieved": round(bg, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bg / HBM_PEAK_GBS, 4),
+                             "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2)}}
+
+
 def CrossEntropyLoss():
     """nn.CrossEntropyLoss() on the fused HIP op (models/loss.py; same defaults)."""
     from models.loss import CrossEntropyLoss as _CE
@@ -514,6 +561,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=24.0, help="seconds of CPU-baseline sampling")
     ap.add_argument("--no-c4", action="store_true", help="skip the configs[3] (C4) leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the configs[4] (C5) leg")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--eager", action="store_true", help="launch the step eagerly instead of replaying its HIP graph")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo launch-path check (no GPU, no measurement)")
@@ -612,6 +660,7 @@ def main() -> None:
     kms = {k: timer.mean_ms(k) for k in timer.names}
     # BASELINE configs[3] (C4) at every world size: 64 windows per rank, weak scaling
     c4 = None if args.no_c4 else c4_leg(dev, max(10, args.steps // 2), 3, rank, world)
+    c5 = None if (args.no_c5 or rank != 0) else c5_leg(dev)  # replicas only: rank 0 reports it
     other = "bf16" if args.dtype == "fp32" else "fp32"
     tier = None if args.no_tier_leg else tier_leg(dev, args.steps, 3, rank, world, other, B)
 
@@ -634,7 +683,7 @@ def main() -> None:
     prop_gbs = fwd_bytes / (prop_ms * 1e-3) / 1e9
     copy = stream_copy_peak(dev)
     pmc = world == 1 and not args.no_pmc
-    traffic = pmc_traffic("gcn_fwd_nm_train", "k_gcn_fwd_nm", B) if pmc else None
+    traffic = pmc_traffic("gcn_fwd_nm_train", "k_gcn_fwd_pc", B) if pmc else None
     traffic_bwd = pmc_traffic("gcn_bwd_nm", "k_gcn_bwd_nm", B) if pmc else None
     gru_rep = gru_mfma_report(kms, B, len(SENSORS))
     src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, 2*FETCH+WRITE (gfx950)"
@@ -650,7 +699,8 @@ def main() -> None:
                    "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode (clip_grad_norm_ + AdamW in one launch, "
                            "models/optim.py)",
                    "launch": "eager" if args.eager else "hipgraph (one replay per step, dropout re-drawn on device)"},
-        "roofline": {"kernel": "lg_gcn_fwd_nm (fused gather-aggregate + MFMA transform, train mode)", "bound": "hbm",
+        "roofline": {"kernel": "lg_gcn_fwd_nm_bits -> k_gcn_fwd_pc (fused gather-aggregate by producer waves, "
+                               "fp16x2 MFMA transform + bias/ReLU/dropout by consumer waves, train mode)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(traffic["bytes"]) if traffic else None,
@@ -675,6 +725,13 @@ def main() -> None:
     }
     if c4 is not None:
         out["c4"] = c4
+    if c5 is not None:
+        if pmc:
+            tr = pmc_traffic("c5_fwd", "k_gcn_fwd", 1)
+            out_c5 = c5["roofline"]
+            out_c5["traffic"] = round(tr["bytes"]) if tr else None
+            out_c5["traffic_source"] = src if tr else None
+        out["c5"] = c5
     if tier is not None:
         out["mlp_tier"] = tier
     if world == 1:

@@ -94,6 +94,18 @@ enum {
 /* lg_gcn_fwd_nm schedule: producer / consumer waves (gather waves hand tiles to MFMA waves
  * through an LDS ring); results identical to the default pipeline */
 #define LG_F_PC            0x00004000
+/* lg_gcn_fwd_nm with LG_F_NM5 or LG_F_PC: the transform as a 2-way fp16 split with power-of-two block
+ * scaling (3 f16 MFMAs per product instead of 6 bf16 ones; fp32-level accuracy, not bit-
+ * identical to the 3-way bf16 split) */
+#define LG_F_F16X2         0x00008000
+/* with LG_F_PC: one consumer wave per producer (default two) */
+#define LG_F_PC1           0x00010000
+/* lg_gcn_fwd_nm schedule: the per-wave pipeline (k_gcn_fwd_nm3) with the 3-way bf16 split.
+ * Without any schedule bit the fp32 tier runs the producer / consumer pipeline with the
+ * 2-way fp16 split (LG_F_PC | LG_F_F16X2), the bf16 tier nm3's single bf16 product. */
+#define LG_F_NM3           0x00020000
+/* with LG_F_PC: six producer waves with one consumer each (default four with two) */
+#define LG_F_PC6           0x00000080
 /* lab builds only: bits 8..11 pick the lg_gcn_fwd_nm (D = 64) kernel's OPT variant */
 #define LG_F_LAB_OPT       0x00001000
 #define LG_F_LAB_OPT_SHIFT 8
@@ -334,6 +346,10 @@ int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float*
  * 4 (l % (D/4)) + i  ->  N * ceil(B/16) * 128 bytes (1/32 of y).  lg_gcn_bwd_nm_bits =
  * lg_gcn_bwd_nm that, under LG_F_MASK_IN with ymask non-NULL, reads the mask from those
  * bits instead of gathering y (y may then be NULL).  Same results as the y path. */
+/* ABI 17: the default fp32-tier transform of lg_gcn_fwd_nm[_bits] is the 2-way fp16 split
+ * with power-of-two block scaling (LG_F_F16X2; |y - y_exact| ~ 4e-7 of max |y|, against
+ * ~1e-8 for the 3-way bf16 split it replaces, which LG_F_NM3 keeps), run by the producer /
+ * consumer pipeline (LG_F_PC). */
 int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                        const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                        int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream,

@@ -1036,15 +1036,21 @@ struct Nm5Lds {
     static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
     static constexpr int WS = D + 4;                     // fp32 W staging row stride (read once per wave)
     static constexpr int WOFF = kNm5Waves * TILE;        // W [out][in] * fold, then the bias * fold
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(WOFF + D * WS + D);
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(WOFF + D * WS + D + kNm5Waves);  // + per-wave max|W|
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
 
 #ifndef LG_NM5_NPF
 #define LG_NM5_NPF 4  // neighbour blocks in flight per wave (L-TOWN-A: 97 % of nodes have degree <= 4 with the self loop)
 #endif
-template <int D, bool DROP, bool RELU, bool BF>
-__global__ void __launch_bounds__(64 * kNm5Waves, 2)
+// F16: the transform as the 2-way fp16 split (split_bf16.h: 3 f16 MFMAs per product instead of
+// 6 bf16 ones, fp32-level accuracy): W scaled by one power of two per launch, each tile's
+// (Ahat x) by one per tile (its largest |value| to [2^14, 2^15)), y = acc 2^-(sa + sw) + b.
+#ifndef LG_NM5_OCC
+#define LG_NM5_OCC 2  // waves per SIMD the register budget is sized for (2: 256 VGPRs, 3: 168)
+#endif
+template <int D, bool DROP, bool RELU, bool BF, bool F16 = false>
+__global__ void __launch_bounds__(64 * kNm5Waves, LG_NM5_OCC)
 k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
@@ -1054,7 +1060,8 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     constexpr int WAVES = kNm5Waves;
     constexpr int NPF = LG_NM5_NPF;
     constexpr int KS = D / 32;      // MFMA k-steps of 32 channels
-    constexpr int NP = BF ? 1 : 3;  // W parts held
+    constexpr int NP = BF ? 1 : 3;  // W parts held (bf16 split)
+    static_assert(!(BF && F16), "one transform");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1086,13 +1093,12 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     f32x4 pf[NPF][G::K];
     uint32_t lo[G::K];
     NmRec cur;
-    uint32_t cn, cb0, cnb;
+    uint32_t cn, cb0;
     auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
         n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
-        cnb = nb;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
 #pragma unroll
@@ -1125,22 +1131,44 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         uint32_t n0, b00, nb00;
         tile_coords(t0, n0, b00, nb00);
         issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
+        uint32_t wmax = 0;
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
             const int i = u * 64 * WAVES + threadIdx.x;
-            if (i < W4) st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), wv[u] * fold);
+            const f32x4 w = wv[u] * fold;
+            if (i < W4) st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wmax = max(wmax, __float_as_uint(fabsf(w[c])));
         }
         if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
+        if constexpr (F16) {
+            wmax = lg_wave_max_bits(wmax);
+            if (lane == 0) reinterpret_cast<uint32_t*>(wst)[D * LY::WS + D + wave] = wmax;
+        }
     }
     __syncthreads();
+    int sw = 0;  // F16: W's scale exponent
+    if constexpr (F16) {
+        const uint32_t* wm = reinterpret_cast<const uint32_t*>(wst) + D * LY::WS + D;
+        uint32_t m = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) m = max(m, wm[w]);
+        sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
+    }
     // this lane's A fragments for the whole launch: W[16 mt + j][32 s2 + 8 q .. + 7] * fold, split
     // in three bf16 parts; the bias (x fold) of its output channels 16 mt + 4 q .. + 3
     lg_bf16x8 wf[NP][G::CH][KS];
+    lg_f16x8 wh[2][G::CH][KS];
 #pragma unroll
     for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
             const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
+            if constexpr (F16) {
+                const float sc = lg_pow2f(sw);
+                split2_f16_x8(ld4(wp) * sc, ld4(wp + 4) * sc, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
+                continue;
+            }
             lg_bf16x8 f0, f1, f2;
             split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
             wf[0][mt][s2] = f0;
@@ -1220,6 +1248,18 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #endif
         issue(nxt, nn, nb0, nnb);
         __builtin_amdgcn_sched_barrier(0);
+        int sa = 0;  // F16: this tile's scale exponent
+        if constexpr (F16) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(acc[k][c])));
+            sa = lg_f16_scale_exp(lg_wave_max_bits(m));
+            const float sc = lg_pow2f(sa);
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) acc[k] *= sc;
+        }
 
         // gather layout -> LDS (own tile) -> MFMA B operand
         wave_sync_nm();
@@ -1237,39 +1277,47 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
         f32x4 o[G::CH];
 #pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+        for (int mt = 0; mt < G::CH; ++mt)
+            o[mt] = F16 ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+        if constexpr (F16) {
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            lg_bf16x8 b0f, b1f, b2f;
-#if defined(LG_KERNEL_LAB) && defined(LG_NM5_NOSPLIT)  // lab: no residual VALU (all parts = the hi part)
-            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
-            b1f = b0f;
-            b2f = b0f;
-#else
-            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
-#endif
-#if defined(LG_KERNEL_LAB) && defined(LG_NM5_NPROD)  // lab: only the NPROD largest products (results WRONG)
-            asm volatile("" ::"v"(b1f), "v"(b2f));
+            for (int s2 = 0; s2 < KS; ++s2) {
+                lg_f16x8 b0h, b1h;
+                split2_f16_x8(bq[s2][0], bq[s2][1], b0h, b1h);
 #pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                if (LG_NM5_NPROD >= 3) o[mt] = mfma_bf(wf[1][mt][s2], b0f, o[mt]);
-                if (LG_NM5_NPROD >= 2) o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
-            }
-            continue;
-#endif
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                if constexpr (BF) {
-                    o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
-                    continue;
+                for (int mt = 0; mt < G::CH; ++mt) {  // smallest terms first
+                    o[mt] = mfma_h(wh[F16 ? 1 : 0][mt][s2], b0h, o[mt]);
+                    o[mt] = mfma_h(wh[0][mt][s2], b1h, o[mt]);
+                    o[mt] = mfma_h(wh[0][mt][s2], b0h, o[mt]);
                 }
-                o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
-                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
-                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+            }
+            // unscale (exact: a power of two) and the bias in one rounding
+            const float us = lg_pow2f(-(sa + sw));
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const f32x4 bv = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[mt][c] = fmaf(o[mt][c], us, bv[c]);
+            }
+        }
+        if constexpr (!F16) {
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                lg_bf16x8 b0f, b1f, b2f;
+                split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    if constexpr (BF) {
+                        o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+                        continue;
+                    }
+                    o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
+                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
+                    o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
+                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
+                    o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
+                    o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+                }
             }
         }
 #ifdef LG_NM3_STAMPS
@@ -1331,43 +1379,46 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 }
 
 // ------------------------------------------------------------------ forward, producer / consumer waves
-// The fused layer split by ROLE inside one 8-wave workgroup per CU.  In nm3/nm5 every wave
+// The fused layer split by ROLE inside one workgroup per CU.  In nm3/nm5 every wave
 // alternates a memory phase (wait for its gathered blocks, accumulate) with a compute phase
-// (transpose, split, 48 MFMAs, epilogue): with 2-3 waves per SIMD each SIMD spent long
-// stretches with all its waves in the same phase (kernel-lab timeline: ~35 % issue, the rest
-// stalled), so neither the memory system nor the SIMDs were kept busy.  Here, per SIMD:
-//   * a PRODUCER wave gathers and accumulates (Ahat x) tiles — two tiles' neighbour blocks
-//     in flight in registers (NPF each) — and hands each finished tile to its consumer
-//     through an LDS ring of R tile slots (16 x D fp32, XOR-swizzled at D = 64);
-//   * a CONSUMER wave reads the slot in the MFMA B layout, splits it, runs the transform
-//     with W's split fragments held in registers for the whole launch, applies bias / ReLU
-//     / dropout, writes y back through the same slot and frees it.
-// Hand-off: per producer/consumer pair a `ready` and a `done` tile counter in LDS (release
-// stores, acquire polls with s_sleep, workgroup scope); the producer reuses slot t % R only
-// after done >= t + 1 - R.  Every poll is bounded (a broken protocol ends the launch with
-// wrong results instead of a hang).  Results are bit-identical to k_gcn_fwd_nm3 (same
-// accumulation order, same products, same masks).
-constexpr int kPcPairs = 4;
+// (transpose, split, MFMAs, epilogue).  A per-wave timeline (kernel-lab stamps) showed each
+// tile's compute phase as a ~3k-cycle latency chain (LDS round trips, the MFMA chain, VALU
+// dependencies) that 2-3 waves per SIMD could not hide, while each wave's loads for the next
+// tile were in flight only during it.  Here:
+//   * kPcProd PRODUCER waves gather and accumulate (Ahat x) tiles — two tiles' neighbour
+//     blocks in flight in registers — and hand each finished tile to a consumer through an
+//     LDS ring of R tile slots (16 x D fp32, XOR-swizzled at D = 64);
+//   * NC CONSUMER waves per producer (tiles t = c, c + NC, ...) read a slot in the MFMA B
+//     layout, run the transform with W's fragments held in registers for the whole launch,
+//     bias / ReLU / dropout, write y back through the same slot, store it and free the slot.
+// Hand-off: per producer a `ready` tile counter, per consumer a `done` counter, in LDS
+// (release stores, acquire polls with s_sleep, workgroup scope); slot t % R is rewritten only
+// after its previous tile's consumer counted it done.  Every poll is bounded (a broken
+// protocol would end the launch with wrong results instead of a hang).
+// Transform: the 3-way bf16 split (bit-identical to k_gcn_fwd_nm3) or, F16, the 2-way fp16
+// split with power-of-two scaling (split_bf16.h; 3 MFMAs per product instead of 6).
 #ifndef LG_PC_RING
 #define LG_PC_RING 4
 #endif
 #ifndef LG_PC_NPF
-#define LG_PC_NPF 4
+#define LG_PC_NPF 3
 #endif
 constexpr int kPcRing = LG_PC_RING;
 
-template <int D>
+template <int D, int kPcProd, int NC>
 struct PcLds {  // floats
     static constexpr bool SWZ = D == 64;
     static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
     static constexpr int WS = D + 4;
-    static constexpr int WOFF = 0;                       // W [out][in] * fold (fp32), then bias * fold
-    static constexpr int FOFF = D * WS + D;              // ready[kPcPairs], done[kPcPairs]
-    static constexpr int MOFF = FOFF + 16;               // per (pair, slot): n, b0, nb, pad
-    static constexpr int ROFF = MOFF + 4 * kPcPairs * kPcRing;  // the rings
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcPairs * kPcRing * TILE);
+    static constexpr int WOFF = 0;                                  // W [out][in] * fold (fp32), bias * fold
+    static constexpr int XOFF = D * WS + D;                         // per-wave max|W| bits (F16)
+    static constexpr int FOFF = XOFF + 16;                          // ready[kPcProd], done[kPcProd * NC]
+    static constexpr int MOFF = FOFF + 16 + kPcProd * NC;           // per (producer, slot): n, b0, nb, pad
+    static constexpr int ROFF = MOFF + 4 * kPcProd * kPcRing;       // the rings
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
+static_assert(kPcRing % 2 == 0, "ring slots alternate between consumers");
 
 __device__ __forceinline__ uint32_t pc_load_acq(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1383,33 +1434,37 @@ __device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
     }
 }
 
-template <int D, bool DROP, bool RELU, bool BF>
-__global__ void __launch_bounds__(128 * kPcPairs, 2)
+template <int D, bool DROP, bool RELU, bool BF, bool F16, int kPcProd, int NC>
+__global__ void __launch_bounds__(64 * kPcProd * (1 + NC), kPcProd * (1 + NC) / 4)
 k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
              uint32_t salt, uint16_t* __restrict__ ymask) {
     using G = NmGeo<D>;
-    using LY = PcLds<D>;
+    using LY = PcLds<D, kPcProd, NC>;
     constexpr int NPF = LG_PC_NPF;
     constexpr int KS = D / 32;
     constexpr int NP = BF ? 1 : 3;
     constexpr int R = kPcRing;
+    constexpr int NT = 64 * kPcProd * (1 + NC);
+    static_assert(!(BF && F16), "one transform");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* lds = reinterpret_cast<float*>(smem);
     float* wst = lds + LY::WOFF;
+    uint32_t* wmx = reinterpret_cast<uint32_t*>(lds + LY::XOFF);
     uint32_t* ready = reinterpret_cast<uint32_t*>(lds + LY::FOFF);
-    uint32_t* done = ready + kPcPairs;
+    uint32_t* done = ready + 16;
     uint32_t* meta = reinterpret_cast<uint32_t*>(lds + LY::MOFF);
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pair = wave & (kPcPairs - 1);
-    const bool producer = wave < kPcPairs;
+    const bool producer = wave < kPcProd;
+    const int prod = producer ? wave : (wave - kPcProd) % kPcProd;  // the producer this wave is or serves
+    const int cons = producer ? 0 : (wave - kPcProd) / kPcProd;     // consumer index 0 .. NC-1
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* ring = lds + LY::ROFF + pair * R * LY::TILE;
+    float* ring = lds + LY::ROFF + prod * R * LY::TILE;
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, pair, kPcPairs);
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, prod, kPcProd);
     const int64_t tend = sc.end;
     const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
 
@@ -1422,24 +1477,31 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         nb = valid ? min(16u, B - b0) : 0u;
     };
 
-    // W (fp32, x fold) and bias to LDS by the whole workgroup; the producers' first tiles go
-    // in flight right after their share of W's loads
+    // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|)
     {
-        constexpr int W4 = D * D / 4, WPER = (W4 + 128 * kPcPairs - 1) / (128 * kPcPairs);
+        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT;
         f32x4 wv[WPER];
 #pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 128 * kPcPairs + threadIdx.x, W4 - 1));
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * NT + threadIdx.x, W4 - 1));
         const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
+        uint32_t wm = 0;
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
-            const int i = u * 128 * kPcPairs + threadIdx.x;
-            if (i < W4)
-                st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)),
-                    f32x4{__fmul_rn(wv[u][0], fold), __fmul_rn(wv[u][1], fold), __fmul_rn(wv[u][2], fold),
-                          __fmul_rn(wv[u][3], fold)});
+            const int i = u * NT + threadIdx.x;
+            f32x4 w = wv[u] * fold;
+            asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
+            if (i < W4) {
+                st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
+            }
         }
-        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = __fmul_rn(bb, fold);
-        if (threadIdx.x < 2 * kPcPairs) ready[threadIdx.x] = 0u;  // ready[] and done[]
+        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
+        if constexpr (F16) {
+            wm = lg_wave_max_bits(wm);
+            if (lane == 0) wmx[wave] = wm;
+        }
+        if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
     }
     __syncthreads();
 
@@ -1476,7 +1538,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     pf[b][i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], base, 0));
             }
         };
-        // tile t of this pair from buffer b: accumulate, hand over, refill b with tile t + 2
+        // tile t of this producer from buffer b: accumulate, hand over, refill b with tile t + 2
         auto step = [&](auto bc, int64_t t) -> bool {
             constexpr int b = decltype(bc)::value;
             const int64_t tile = sc.first + t * sc.stride;
@@ -1503,47 +1565,54 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[b][i][k]);
                 }
             }
-            if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): in place
+            if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
+                constexpr int NI = kLgNmInline - NPF;
+                f32x4 va[NI][G::K];
 #pragma unroll
-                for (int i = NPF; i < kLgNmInline; ++i) {
-                    if (e0 + i < e1) {
-                        const uint32_t ba = (static_cast<uint32_t>(cur.p[i].x) * B + b0) * (4u * D);
-                        f32x4 va[G::K];
+                for (int i = 0; i < NI; ++i) {
+                    const bool have = e0 + NPF + i < e1;
+                    const uint32_t ba = have ? (static_cast<uint32_t>(cur.p[NPF + i].x) * B + b0) * (4u * D) : 0u;
+                    const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
 #pragma unroll
-                        for (int k = 0; k < G::K; ++k)
-                            va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
-                        const float wa = __int_as_float(cur.p[i].y);
+                    for (int k = 0; k < G::K; ++k)
+                        va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], ba, 0));
+                }
 #pragma unroll
-                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+                for (int i = 0; i < NI; ++i) {
+                    if (e0 + NPF + i < e1) {
+                        const float wa = __int_as_float(cur.p[NPF + i].y);
+#pragma unroll
+                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[i][k]);
                     }
                 }
                 for (int e = e0 + kLgNmInline; e < e1; ++e) {
                     const int2 pa = pairs[e];
                     const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-                    f32x4 va[G::K];
+                    f32x4 vb[G::K];
 #pragma unroll
                     for (int k = 0; k < G::K; ++k)
-                        va[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
+                        vb[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
                     const float wa = __int_as_float(pa.y);
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, vb[k]);
                 }
             }
             const int sl = static_cast<int>(t % R);
             const uint32_t mn = tn[b], mnb = tnb[b];
             // buffer b is free again: tile t + 2 goes in flight before the hand-off waits
             issue(bc, nxt, tile + 2 * sc.stride);
-            if (t >= R) pc_wait(&done[pair], static_cast<uint32_t>(t + 1 - R));
+            // slot sl last held tile t - R, consumed by consumer (t - R) % NC as its ((t - R) / NC)-th
+            if (t >= R) pc_wait(&done[prod * NC + static_cast<int>((t - R) % NC)], static_cast<uint32_t>((t - R) / NC + 1));
             float* slot = ring + sl * LY::TILE;
 #pragma unroll
             for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
             if (lane == 0) {
-                uint32_t* m = meta + 4 * (pair * R + sl);
+                uint32_t* m = meta + 4 * (prod * R + sl);
                 m[0] = mn;
                 m[1] = b0;
                 m[2] = mnb;
             }
-            pc_store_rel(&ready[pair], static_cast<uint32_t>(t + 1));
+            pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
             return true;
         };
         {
@@ -1567,12 +1636,24 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     uint32_t loff[G::K];
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    int sw = 0;  // F16: W's scale exponent
+    if constexpr (F16) {
+        uint32_t m = 0;
+        for (int w = 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
+        sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
+    }
     lg_bf16x8 wf[NP][G::CH][KS];
+    lg_f16x8 wh[2][G::CH][KS];
 #pragma unroll
     for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
             const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
+            if constexpr (F16) {
+                const float sc2 = lg_pow2f(sw);
+                split2_f16_x8(ld4(wp) * sc2, ld4(wp + 4) * sc2, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
+                continue;
+            }
             lg_bf16x8 f0, f1, f2;
             split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
             wf[0][mt][s2] = f0;
@@ -1584,13 +1665,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     }
     const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p_drop);
-    for (int64_t t = 0;; ++t) {
+    for (int64_t u = 0;; ++u) {
+        const int64_t t = u * NC + cons;  // this consumer's u-th tile of its producer
         const int64_t tile = sc.first + t * sc.stride;
         if (tile >= tend) break;
         const int sl = static_cast<int>(t % R);
-        pc_wait(&ready[pair], static_cast<uint32_t>(t + 1));
+        pc_wait(&ready[prod], static_cast<uint32_t>(t + 1));
         float* slot = ring + sl * LY::TILE;
-        const uint32_t* m = meta + 4 * (pair * R + sl);
+        const uint32_t* m = meta + 4 * (prod * R + sl);
         const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
                        nb = __builtin_amdgcn_readfirstlane(m[2]);
         f32x4 bq[KS][2];
@@ -1602,24 +1684,57 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         uint32_t st = 0;
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
         f32x4 o[G::CH];
+        if constexpr (F16) {
+            // the tile's scale from its largest |value| (the B-operand values are the whole tile)
+            uint32_t mx = 0;
 #pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+            for (int s2 = 0; s2 < KS; ++s2)
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            lg_bf16x8 b0f, b1f, b2f;
-            split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) mx = max(mx, __float_as_uint(fabsf(bq[s2][h][c])));
+            const int sa = lg_f16_scale_exp(lg_wave_max_bits(mx));
+            const float sc2 = lg_pow2f(sa);
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                lg_f16x8 b0h, b1h;
+                split2_f16_x8(bq[s2][0] * sc2, bq[s2][1] * sc2, b0h, b1h);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {  // smallest terms first
+                    o[mt] = mfma_h(wh[F16 ? 1 : 0][mt][s2], b0h, o[mt]);
+                    o[mt] = mfma_h(wh[0][mt][s2], b1h, o[mt]);
+                    o[mt] = mfma_h(wh[0][mt][s2], b0h, o[mt]);
+                }
+            }
+            const float us = lg_pow2f(-(sa + sw));  // unscale (exact) and the bias in one rounding
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
-                if constexpr (BF) {
+                const f32x4 bv = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+#pragma unroll
+                for (int c = 0; c < 4; ++c) o[mt][c] = fmaf(o[mt][c], us, bv[c]);
+            }
+        } else {
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                lg_bf16x8 b0f, b1f, b2f;
+                split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    if constexpr (BF) {
+                        o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
+                        continue;
+                    }
+                    o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
+                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
+                    o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
+                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
+                    o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
                     o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
-                    continue;
                 }
-                o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
-                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
-                o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
-                o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
             }
         }
 #pragma unroll
@@ -1655,14 +1770,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             for (int k = G::K - 1; k >= 0; --k)
 #pragma unroll
                 for (int i = 3; i >= 0; --i) {
-                    const uint32_t u = RELU ? __float_as_uint(vk[k][i])
-                                            : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
-                    bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
+                    const uint32_t uu = RELU ? __float_as_uint(vk[k][i])
+                                             : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
+                    bits = __builtin_amdgcn_alignbit(bits, uu + 0x7FFFFFFFu, 31);
                 }
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
                                                   0, 0);
         }
-        pc_store_rel(&done[pair], static_cast<uint32_t>(t + 1));  // the slot's reads are done (release)
+        pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));  // the slot's reads are done (release)
     }
 }
 
@@ -2354,12 +2469,21 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     const bool relu = (flags & LG_F_RELU) != 0;
     const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
     const bool bf16 = (flags & LG_F_BF16) != 0;
+    // Default (no schedule / transform bits): the producer / consumer pipeline with the 2-way
+    // fp16 transform (k_gcn_fwd_pc, F16) for the fp32 tier — the fastest measured
+    // (profiles/r03: 18.2-18.6 us against 19.9 for nm3 at B = 256) — and nm3's single bf16
+    // product for the bf16 tier.  LG_F_NM3 keeps nm3's 3-way bf16 split (bit-identical to pc
+    // and nm5 without LG_F_F16X2).
+    const bool sched_bits = (flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5 | LG_F_LAB_V1 |
+                                      LG_F_LAB_NM2 | LG_F_NM3 | LG_F_NM5 | LG_F_PC)) != 0 ||
+                            ((flags >> 28) & 7) != 0 || (flags & LG_F_LAB_OPT) != 0;
+    const bool dflt = !sched_bits && !bf16;
+    const bool clean = !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) && ((flags >> 28) & 7) == 0;
     // the W-in-registers pipeline (k_gcn_fwd_nm5): same results as nm3, split or bf16 transform
-    const bool nm5 = (flags & LG_F_NM5) && !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) &&
-                     ((flags >> 28) & 7) == 0;
-    // the producer / consumer pipeline (k_gcn_fwd_pc): same results
-    const bool pc = (flags & LG_F_PC) && !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) &&
-                    ((flags >> 28) & 7) == 0;
+    const bool nm5 = (flags & LG_F_NM5) && clean;
+    const bool f16 = ((flags & LG_F_F16X2) != 0 || dflt) && !bf16;  // the 2-way fp16 transform (nm5 / pc)
+    // the producer / consumer pipeline (k_gcn_fwd_pc)
+    const bool pc = ((flags & LG_F_PC) && clean) || dflt;
     (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
@@ -2381,18 +2505,35 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
             lg_launch(kern, grid, 64 * kNm2Waves, dyn2, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
                                                     dropout_p, scale, seed, salt);                                 \
         } else if (pc) {                                                                                           \
-            auto kern = relu ? (bf16 ? k_gcn_fwd_pc<DD, DR, true, true> : k_gcn_fwd_pc<DD, DR, true, false>)       \
-                             : (bf16 ? k_gcn_fwd_pc<DD, DR, false, true> : k_gcn_fwd_pc<DD, DR, false, false>);    \
-            const size_t dynp = PcLds<DD>::BYTES;                                                                  \
-            const int grid = nm_grid(kern, 128 * kPcPairs, dynp, ntiles, kPcPairs, 1);                             \
-            lg_launch(kern, grid, 128 * kPcPairs, dynp, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale,\
-                      seed, salt, ymask);                                                                          \
+            const int np = (flags & LG_F_PC6) ? 6 : 4, nc = (np == 6 || (flags & LG_F_PC1)) ? 1 : 2;                \
+            auto pick = [&](auto pcc, auto ncc) {                                                                  \
+                constexpr int PP = decltype(pcc)::value, NCC = decltype(ncc)::value;                               \
+                return relu ? (bf16 ? k_gcn_fwd_pc<DD, DR, true, true, false, PP, NCC>                             \
+                                    : (f16 ? k_gcn_fwd_pc<DD, DR, true, false, true, PP, NCC>                      \
+                                           : k_gcn_fwd_pc<DD, DR, true, false, false, PP, NCC>))                   \
+                            : (bf16 ? k_gcn_fwd_pc<DD, DR, false, true, false, PP, NCC>                            \
+                                    : (f16 ? k_gcn_fwd_pc<DD, DR, false, false, true, PP, NCC>                     \
+                                           : k_gcn_fwd_pc<DD, DR, false, false, false, PP, NCC>));                 \
+            };                                                                                                     \
+            using I1 = std::integral_constant<int, 1>;                                                             \
+            using I2 = std::integral_constant<int, 2>;                                                             \
+            using I4 = std::integral_constant<int, 4>;                                                             \
+            using I6 = std::integral_constant<int, 6>;                                                             \
+            auto kern = np == 6 ? pick(I6{}, I1{}) : nc == 1 ? pick(I4{}, I1{}) : pick(I4{}, I2{});                \
+            const size_t dynp = np == 6 ? PcLds<DD, 6, 1>::BYTES : nc == 1 ? PcLds<DD, 4, 1>::BYTES                \
+                                                                          : PcLds<DD, 4, 2>::BYTES;                \
+            const int thr = 64 * np * (1 + nc);                                                                    \
+            const int grid = nm_grid(kern, thr, dynp, ntiles, np, 1);                                              \
+            lg_launch(kern, grid, thr, dynp, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,    \
+                      salt, ymask);                                                                                \
         } else if (nm5) {                                                                                          \
-            auto kern = relu ? (bf16 ? k_gcn_fwd_nm5<DD, DR, true, true> : k_gcn_fwd_nm5<DD, DR, true, false>)     \
-                             : (bf16 ? k_gcn_fwd_nm5<DD, DR, false, true> : k_gcn_fwd_nm5<DD, DR, false, false>);  \
+            auto kern = relu ? (bf16 ? k_gcn_fwd_nm5<DD, DR, true, true>                                           \
+                                     : (f16 ? k_gcn_fwd_nm5<DD, DR, true, false, true> : k_gcn_fwd_nm5<DD, DR, true, false>)) \
+                             : (bf16 ? k_gcn_fwd_nm5<DD, DR, false, true>                                          \
+                                     : (f16 ? k_gcn_fwd_nm5<DD, DR, false, false, true> : k_gcn_fwd_nm5<DD, DR, false, false>)); \
             const size_t dyn5 = Nm5Lds<DD>::BYTES;                                                                 \
             const int grid = nm_grid(kern, 64 * kNm5Waves, dyn5, ntiles, kNm5Waves,                               \
-                                     ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? bpc : 2);                             \
+                                     ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? bpc : LG_NM5_OCC);                    \
             lg_launch(kern, grid, 64 * kNm5Waves, dyn5, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, \
                       seed, salt, ymask);                                                                          \
         } else if (w5) {                                                                                           \

@@ -99,3 +99,61 @@ __device__ __forceinline__ lg_bf16x8 lds_frag_tr16(const uint16_t* r0, const uin
 __device__ __forceinline__ lg_bf16x8 lds_frag_row(const uint16_t* p) {
     return *reinterpret_cast<const lg_bf16x8*>(p);
 }
+
+// ---- 2-way fp16 split with power-of-two scaling (the "f16x2" transform) -----------------
+// x * 2^s = x0 + x1 + r with x0 = f16_rne(x 2^s), x1 = f16_rne(x 2^s - x0): |r| <= 2^-22 |x 2^s|
+// while x 2^s stays in fp16's normal range.  A product a w is then a0 w0 + a1 w0 + a0 w1
+// (3 f16 MFMAs, products exact in fp32, fp32 accumulate; the dropped a1 w1 is <= 2^-22 |a w|)
+// — fp32-level accuracy at half the MFMAs of the 3-way bf16 split.  The scale exponent s
+// puts the largest |x| of the block at [2^14, 2^15): everything down to 2^-17 of it keeps
+// both parts normal, smaller values lose only absolute precision below 2^-38 of the block max.
+typedef _Float16 lg_f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 lg_f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split2_f16_pair(float a, float b, uint32_t& p0, uint32_t& p1) {
+    const lg_f32x2 v = {a, b};
+    const lg_f16x2 h0 = __builtin_convertvector(v, lg_f16x2);
+    const lg_f32x2 r = v - __builtin_convertvector(h0, lg_f32x2);
+    p0 = __builtin_bit_cast(uint32_t, h0);
+    p1 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, lg_f16x2));
+}
+// 8 floats (two f32x4) -> two f16x8 fragments (hi, lo)
+__device__ __forceinline__ void split2_f16_x8(const f32x4& u, const f32x4& v, lg_f16x8& f0, lg_f16x8& f1) {
+    lg_u32x4 p0, p1;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const float a = h < 2 ? u[2 * h] : v[2 * h - 4], b = h < 2 ? u[2 * h + 1] : v[2 * h - 3];
+        uint32_t x0, x1;
+        split2_f16_pair(a, b, x0, x1);
+        p0[h] = x0;
+        p1[h] = x1;
+    }
+    f0 = __builtin_bit_cast(lg_f16x8, p0);
+    f1 = __builtin_bit_cast(lg_f16x8, p1);
+}
+__device__ __forceinline__ f32x4 mfma_h(const lg_f16x8& a, const lg_f16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// 2^e as a float for e in [-126, 127] (clamped)
+__device__ __forceinline__ float lg_pow2f(int e) {
+    e = e < -126 ? -126 : (e > 127 ? 127 : e);
+    return __uint_as_float(static_cast<uint32_t>(e + 127) << 23);
+}
+// scale exponent for a block whose largest |value| has the float bits `mbits` (>= 0): puts that
+// value at [2^14, 2^15); a zero block gets 0
+__device__ __forceinline__ int lg_f16_scale_exp(uint32_t mbits) {
+    if (mbits == 0) return 0;
+    const int e = static_cast<int>((mbits >> 23) & 0xFF) - 127;  // floor(log2 max) (subnormals: -127)
+    return 14 - e;
+}
+// max over the wave of a non-negative float's bits (integer order = float order), broadcast
+// (DPP within rows of 16, then the four row results through readlane)
+__device__ __forceinline__ uint32_t lg_wave_max_bits(uint32_t m) {
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0xB1, 0xF, 0xF, false)));  // xor 1
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x4E, 0xF, 0xF, false)));  // xor 2
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x124, 0xF, 0xF, false)));  // row_ror 4
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x128, 0xF, 0xF, false)));  // row_ror 8
+    const uint32_t r0 = __builtin_amdgcn_readlane(m, 0), r1 = __builtin_amdgcn_readlane(m, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(m, 32), r3 = __builtin_amdgcn_readlane(m, 48);
+    return max(max(r0, r1), max(r2, r3));
+}

@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 16  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 17  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -32,6 +32,10 @@ LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel la
 LG_F_LAB_W5 = 0x00040000  # lg_gcn_fwd_nm schedule: 5-wave workgroups (kernel lab)
 LG_F_NM5 = 0x00002000  # lg_gcn_fwd_nm schedule: W-in-registers pipeline (same results)
 LG_F_PC = 0x00004000  # lg_gcn_fwd_nm schedule: producer / consumer waves (same results)
+LG_F_F16X2 = 0x00008000  # lg_gcn_fwd_nm + LG_F_NM5/PC: 2-way fp16 split transform (fp32-level accuracy)
+LG_F_PC1 = 0x00010000  # with LG_F_PC: one consumer wave per producer (default two)
+LG_F_NM3 = 0x00020000  # lg_gcn_fwd_nm schedule: per-wave nm3 pipeline, 3-way bf16 split
+LG_F_PC6 = 0x00000080  # with LG_F_PC: six producers, one consumer each
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)

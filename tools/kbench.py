@@ -172,7 +172,9 @@ def main():
         for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
             bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "w5": nat.LG_F_LAB_W5, "nomfma": 1 << 28,
                      "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA,
-                     "bf16": nat.LG_F_BF16, "nm5": nat.LG_F_NM5, "pc": nat.LG_F_PC}.get(tok, 0)
+                     "bf16": nat.LG_F_BF16, "nm5": nat.LG_F_NM5, "pc": nat.LG_F_PC, "f16": nat.LG_F_F16X2,
+                     "pc1": nat.LG_F_PC | nat.LG_F_PC1, "pc6": nat.LG_F_PC | nat.LG_F_PC6,
+                     "nm3": nat.LG_F_NM3}.get(tok, 0)
             if tok.startswith("bpc"):
                 bits |= int(tok[3:]) << 24
             if tok.startswith("opt"):  # lab OPT variant of the D = 64 forward (LG_F_LAB_OPT, bits 8..11)
@@ -221,6 +223,29 @@ def main():
         else:
             byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
         res[name] = {"us": t, "GBps": byts / t / 1e3}
+    if "c5_fwd" in which or "c5_bwd" in which:  # BASELINE configs[4]: one 100k-node graph, B = 1, GCNConv's launches
+        from models.synth import synthetic_pipe_graph
+        ei5, _ = synthetic_pipe_graph(100_000, 150_000, seed=0)
+        N5 = 100_000
+        g5 = GCNGraph.build(ei5, N5, dev)
+        x5 = torch.randn(N5, D, device=dev)
+        y5 = torch.empty_like(x5)
+        b5 = 8 * N5 * D + 4 * (N5 + 1) + 8 * (int(ei5.shape[1]) + N5)  # 54.8 MB
+        f = lambda: check(lib.lg_gcn_fwd(ptr(g5.rowptr), ptr(g5.col), ptr(g5.w), ptr(x5), ptr(W), ptr(bias), ptr(y5),
+                                         1, N5, D, g5.col.numel(), nat.LG_F_BIAS, 0.0, 0, 0, cs()), "c5 fwd")
+        if "c5_fwd" in which:
+            t = timeit(f, args.iters)
+            res["c5_fwd"] = {"us": t, "GBps": b5 / t / 1e3}
+        if "c5_bwd" in which:
+            dy5 = torch.randn_like(x5)
+            dx5 = torch.empty_like(x5)
+            dW5, db5 = torch.empty(D, D, device=dev), torch.empty(D, device=dev)
+            ws5 = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
+            f = lambda: check(lib.lg_gcn_bwd(ptr(g5.rowptr_t), ptr(g5.col_t), ptr(g5.w_t), ptr(dy5), None, ptr(x5),
+                                             ptr(W), ptr(dx5), ptr(dW5), ptr(db5), None, None, 1, N5, D,
+                                             g5.col_t.numel(), 0, 1.0, 1.0, ptr(ws5), cs()), "c5 bwd")
+            t = timeit(f, args.iters)
+            res["c5_bwd"] = {"us": t, "GBps": (b5 + 4 * N5 * D) / t / 1e3}
     if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
         f = lambda: y.copy_(x)
         t = timeit(f, args.iters)

@@ -48,13 +48,25 @@ def main():
             y0, m0 = run(0)
             if args.nm5:
                 for name, ex in (("nm5", nat.LG_F_NM5), ("nm5-bf16", nat.LG_F_NM5 | nat.LG_F_BF16),
-                                 ("pc", nat.LG_F_PC), ("pc-bf16", nat.LG_F_PC | nat.LG_F_BF16)):
+                                 ("pc", nat.LG_F_PC), ("pc-bf16", nat.LG_F_PC | nat.LG_F_BF16),
+                                 ("pc1", nat.LG_F_PC | nat.LG_F_PC1)):
                     ya, ma = run(None, ex)
                     yb, mb = (y0, m0) if "bf16" not in name else run(None, nat.LG_F_BF16)
                     same_y = torch.equal(ya.view(torch.int32), yb.view(torch.int32))
                     same_m = torch.equal(ma, mb)
                     print(f"B={B} drop={bool(fl)} {name}: y {'==' if same_y else '!='} mask {'==' if same_m else '!='}")
                     bad += (not same_y) + (not same_m)
+            if args.nm5:  # the fp16x2 transform: fp32-level accuracy, not bit-identical
+                ya, ma = run(None, nat.LG_F_NM5 | nat.LG_F_F16X2)
+                scale = y0.abs().max().item()
+                err = (ya.double() - y0.double()).abs().max().item() / scale
+                nbits = int((ma.view(torch.int16) ^ m0.view(torch.int16)).ne(0).sum().item())
+                print(f"B={B} drop={bool(fl)} nm5-f16x2: max|dy|/scale = {err:.2e}, mask words differing {nbits}")
+                bad += err > 1e-6
+                yc, mc = run(None, nat.LG_F_PC | nat.LG_F_F16X2)
+                same = torch.equal(ya.view(torch.int32), yc.view(torch.int32)) and torch.equal(ma, mc)
+                print(f"B={B} drop={bool(fl)} pc-f16x2 {'==' if same else '!='} nm5-f16x2")
+                bad += not same
             for opt in [int(v) for v in args.opts.split(",") if v]:
                 y1, m1 = run(opt)
                 same_y = torch.equal(y0.view(torch.int32), y1.view(torch.int32))

@@ -34,7 +34,7 @@ PASSES = [
     ["WRITE_SIZE"],
     ["TCC_HIT_sum", "TCC_MISS_sum"],
 ]
-DEFAULT_TARGETS = ("gcn_fwd_nm_train:k_gcn_fwd_nm3,gcn_bwd_nm:k_gcn_bwd_nm3,edge_fwd:k_edge_fwd,"
+DEFAULT_TARGETS = ("gcn_fwd_nm_train:k_gcn_fwd_pc,gcn_bwd_nm:k_gcn_bwd_nm3,edge_fwd:k_edge_fwd,"
                    "edge_bwd:k_edge_bwd,gru_fwd:k_gru_fwd,gru_bwd:k_gru_bwd")
 
 
