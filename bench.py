@@ -76,6 +76,28 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_share() -> dict:
+    """The host cores this process may run on: os.cpu_count(), the affinity mask, and the
+    cgroup CPU quota (cpu.max; on the GPU box the pod's share is far below the machine's
+    core count, and threads past the quota only queue behind it).  `threads` = the affinity
+    count, capped by the quota when one is set."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = total
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(np.ceil(quota))))
+    return {"threads": threads, "cpu_count": total, "affinity": aff,
+            "cgroup_quota_cpus": round(quota, 2) if quota is not None else None}
+
+
 def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
     """The oracle's CPU restatement of the same step timed on the host cores (reported only,
     BASELINE.md plan): eval-mode forward and train-mode fwd+CE+bwd, median of >= 10 timed
@@ -112,7 +134,9 @@ def cpu_baseline(batch: int, budget_s: float, threads: int) -> dict:
 
     tr, ntr = timed(train_step, "train")
     ev, nev = timed(eval_fwd, "eval")
+    share = cpu_share()
     return {"value": round(batch / tr, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+            "host_cpus": share,
             "cpu_model": cpu_model(), "eval_forward_windows_per_s": round(batch / ev, 2),
             "train_ms_per_step": round(tr * 1e3, 1), "eval_ms_per_step": round(ev * 1e3, 1),
             "sample": f"median of {ntr} train-mode fwd+CE+bwd steps (value) and {nev} eval-mode forwards, each "
@@ -525,6 +549,40 @@ def launch_ranks(args, argv) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _timed_max(fn, steps: int, sync, world: int) -> float:
+    """Seconds of `steps` calls of fn between barrier + sync fences, max over ranks."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    if world > 1:
+        dist.barrier()
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def exchange_fields(t_full: float, t_nocomm: float, t_ar: float, steps: int, world: int, how: str) -> dict:
+    """The multi-rank step's exchange cost.  allreduce_us: the gradient all-reduce alone, per
+    step; exchange_exposed_us: what the exchange adds to the step (with it minus without,
+    the rest identical); weak_scaling_eff: the step without the exchange over the step with
+    it — per-rank throughput at this world size relative to the same step with nothing to
+    wait for (the driver computes the cross-run efficiency from its own N=1 line)."""
+    if world == 1:
+        return {"allreduce_us": 0.0, "exchange_exposed_us": 0.0, "weak_scaling_eff": 1.0, "exchange": how}
+    return {"allreduce_us": round(t_ar * 1e6 / steps, 2),
+            "exchange_exposed_us": round(max(0.0, t_full - t_nocomm) * 1e6 / steps, 2),
+            "weak_scaling_eff": round(min(1.0, t_nocomm / t_full), 4), "exchange": how}
+
+
 def dry_run(args, rank: int, world: int) -> None:
     """`--dry-run`: the multi-rank launch / barrier / max-over-ranks timing / JSON path on
     CPU (gloo), with the step reduced to the detector's gradient all-reduce (60,418 fp32
@@ -533,22 +591,31 @@ def dry_run(args, rank: int, world: int) -> None:
     from models.ddp import init_distributed
     init_distributed(backend="gloo")
     grad = torch.ones(60418) * (rank + 1)
+    a = torch.randn(192, 192)
+
+    def compute():  # stand-in for the detector step (a fixed CPU workload)
+        for _ in range(4):
+            a.matmul(a)
+
+    def full():
+        compute()
+        dist.all_reduce(grad)
+
     for _ in range(args.warmup):
-        dist.all_reduce(grad)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dist.all_reduce(grad)
-    dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        full()
+    nosync = lambda: None  # noqa: E731
+    t_full = _timed_max(full, args.steps, nosync, world)
+    t_nocomm = _timed_max(compute, args.steps, nosync, world)
+    t_ar = _timed_max(lambda: dist.all_reduce(grad), args.steps, nosync, world)
     if rank == 0:
-        print(json.dumps({"metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": None, "unit": "windows/s",
-                          "n_gpus": world, "ranks_seen": dist.get_world_size(), "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": round(float(t.item()) * 1e3 / max(args.steps, 1), 4),
-                          "dry_run": True, "backend": "gloo",
-                          "config": {"workload": "gradient all-reduce only (no detector step)",
-                                     "parallelism": f"dp{world}"}}), flush=True)
+        out = {"metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": None, "unit": "windows/s",
+               "n_gpus": world, "ranks_seen": dist.get_world_size(), "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(t_full * 1e3 / max(args.steps, 1), 4),
+               "dry_run": True, "backend": "gloo",
+               "config": {"workload": "gradient all-reduce (60,418 fp32) after a fixed CPU matmul stand-in step",
+                          "parallelism": f"dp{world}"}}
+        out.update(exchange_fields(t_full, t_nocomm, t_ar, max(args.steps, 1), world, "one bucket, blocking (gloo)"))
+        print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 
 
@@ -586,7 +653,7 @@ def main() -> None:
         sys.exit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible")
 
     from models import ops
-    from models.ddp import GradAllReduce, init_distributed
+    from models.ddp import GradAllReduce, init_distributed, reseed_rank
     from models.detector import LeakDetector
 
     rank, local_rank, world = init_distributed()
@@ -603,6 +670,7 @@ def main() -> None:
     from models.optim import ClipAdamW
     opt = ClipAdamW(model.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0)
     allreduce = GradAllReduce(model.parameters())
+    reseed_rank(0, rank, world)  # same weights on every rank, per-rank dropout seeds from here on
     N = len(model.node_names)
     E1 = int(model.edge_index_single.shape[1]) + N  # E' = E + N self loops
 
@@ -649,6 +717,23 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item())
+    # the exchange's cost: the same captured step with the collectives skipped, and the
+    # gradient all-reduce alone (two buckets as the step issues them, or one eagerly)
+    if world > 1:
+        cuda_sync = torch.cuda.synchronize
+        if hasattr(step, "comm"):
+            step.comm = False
+            t_nocomm = _timed_max(step, args.steps, cuda_sync, world)
+            step.comm = True
+            bucks = [b for b, _ in step.buckets]
+            how = ("head bucket async under the trunk backward, trunk bucket blocking"
+                   if len(bucks) == 2 else "one bucket, blocking")
+        else:
+            t_nocomm, bucks, how = elapsed, [allreduce.flat], "one bucket, blocking (eager)"
+        t_ar = _timed_max(lambda: [dist.all_reduce(b) for b in bucks], args.steps, cuda_sync, world)
+        xchg = exchange_fields(elapsed, t_nocomm, t_ar, args.steps, world, how)
+    else:
+        xchg = exchange_fields(elapsed, elapsed, 0.0, args.steps, 1, "none (one rank)")
     # pass 2: per-kernel HIP-event durations over the same number of steps (eager launches:
     # the events bracket each library call on its stream)
     timer.enabled = True
@@ -719,6 +804,7 @@ def main() -> None:
                                "achieved": round(prop_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(prop_gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(prop_ms * 1e3, 2)},
         "stream_copy": copy,
+        **xchg,
         "gru_mfma": gru_rep,
         "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
         "final_loss": round(final_loss, 4),
@@ -737,7 +823,7 @@ def main() -> None:
     if world == 1:
         out["e2e_training"] = e2e_training(model, opt, label, B, max(5, args.steps // 2), dev)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(B, args.cpu_budget, threads=min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(B, args.cpu_budget, threads=cpu_share()["threads"])
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

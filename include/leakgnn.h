@@ -17,8 +17,13 @@
  *    No entry point synchronises the device or the host, so every call is
  *    capturable into a hipGraph.
  *  - Return value: LG_OK (0) or a negative LG_E* code; lg_strerror() names it.
- *    A launch failure returns LG_EHIP.  The library keeps no mutable global state
- *    and is reentrant.
+ *    A launch failure returns LG_EHIP.  Compute entry points keep no mutable global
+ *    state and are reentrant.  Two OPTIONAL facilities hold state, both documented
+ *    at their declarations: the reduce batch (per host thread: begin and flush must
+ *    come from the same thread; a flush on another thread returns LG_EINVAL and the
+ *    batch stays open on its own thread) and the kernel-timing slots (one process-wide
+ *    set of event pairs plus a per-thread armed slot; measurement only).  A caller that
+ *    uses neither sees a stateless library.
  *  - Node features are fp32, row-major [B][N][D] (window-major, then node, then
  *    feature; one 4·D-byte row per node).  B identical graphs form the disjoint
  *    union of reference detector.py:105-114; the library keeps ONE single-graph
@@ -123,7 +128,9 @@ int lg_abi_version(void);
  * a recorded output folds that output's partials into its own db reduction.  Replaces
  * nothing in the reference: it merges the per-op launches of one backward pass
  * (the autograd of detector.py:170-218).  begin: LG_EINVAL when a batch is already open;
- * flush: LG_EINVAL when none is. */
+ * flush: LG_EINVAL when none is.  The open batch is THREAD-LOCAL state: a flush from a
+ * thread that did not begin it returns LG_EINVAL (nothing launched, the other thread's
+ * batch untouched), and a thread that exits with an open batch drops its records. */
 int lg_reduce_batch_begin(void);
 int lg_reduce_batch_flush(lg_stream_t stream);
 

@@ -210,22 +210,17 @@ extern "C" int lg_reduce_batch_flush(lg_stream_t stream) {
 }
 
 // ---------------------------------------------------------------- measured copy peak
-// The box's achievable HBM rate for a read + write stream (bench.py stream_copy): 16-byte
-// non-temporal loads and stores, four in flight per lane, grid-stride over the buffer.
+// The box's achievable HBM rate for a read + write stream (bench.py stream_copy): one 16-byte
+// non-temporal load and store per lane, one workgroup per 4 KiB, no grid stride.  Measured
+// (profiles/r03/r03n/copy_lab.txt, 2 GiB): this flat shape 6.52 TB/s; grid-stride loops with
+// 4-64 workgroups per CU and 1-8 vectors in flight per lane 4.3-5.5 TB/s (the round-2 kernel,
+// U=4 at 16/CU, 4.7); hipMemcpyAsync D2D 4.8.  Short-lived workgroups keep every channel fed
+// as the dispatcher refills CUs; long-lived strided ones drift into channel-hot phases.
 namespace {
 __global__ void __launch_bounds__(256) k_stream_copy(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                                      int64_t n4) {
-    constexpr int U = 4;
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-    int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    for (; i + (U - 1) * stride < n4; i += U * stride) {
-        f32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
-    }
-    for (; i < n4; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i < n4) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 }  // namespace
 
@@ -233,7 +228,8 @@ extern "C" int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stre
     if (bytes < 0 || (bytes % 16) != 0 || (bytes > 0 && (!src || !dst))) return LG_EINVAL;
     if (bytes == 0) return LG_OK;
     const int64_t n4 = bytes / 16;
-    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 16LL * lg_num_cus())));
+    if ((n4 + 255) / 256 > 0x7FFFFFFFLL) return LG_EINVAL;
+    const unsigned grid = static_cast<unsigned>((n4 + 255) / 256);
     k_stream_copy<<<grid, 256, 0, lg_stream(stream)>>>(static_cast<const f32x4*>(src), static_cast<f32x4*>(dst), n4);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;

@@ -90,6 +90,13 @@ def rank_generator_seed(seed: int, rank: int) -> int:
     return (int(seed) + 0x9E3779B1 * int(rank)) % (1 << 63)
 
 
+def reseed_rank(seed: int, rank: int, world: int) -> None:
+    """Called once the model is built (identical weights everywhere): from here on every rank
+    draws its own dropout seeds.  No-op at world 1."""
+    if world > 1:
+        torch.manual_seed(rank_generator_seed(seed, rank))
+
+
 def shard_range(global_batch: int, rank: int, world: int) -> range:
     """Contiguous per-rank slice of the global sample index range (datasets are seeded by
     seed + idx, datasets.py:236,490, so the global batch is the same at any world size)."""

@@ -134,6 +134,16 @@ class LeakDetector(nn.Module):
         # ("xs": node init + every GCN layer, "edge_hidden", "noleak_hidden"), so parity tests
         # can evaluate the fp64 truth on the same side of every ReLU kink.  None: nothing kept.
         self.capture: Optional[dict] = None
+        # graph_step.CapturedTrainStep at world > 1: forward keeps the trunk output (the heads'
+        # input) as `boundary` while keep_boundary is set, so the backward can stop there and
+        # the heads' gradient all-reduce overlaps the trunk backward (overlap_split)
+        self.keep_boundary = False
+        self.boundary: Optional[torch.Tensor] = None
+
+    def overlap_split(self):
+        """Parameters whose gradients are final once the backward reaches `boundary` (the
+        heads: EdgeHead + NoLeakHead, detector.py:206-218 of the reference)."""
+        return list(self.edge_head.parameters()) + list(self.noleak_head.parameters())
 
     # -- device-resident graph state (built once per device; not part of state_dict)
     def _device_state(self, device: torch.device):
@@ -177,6 +187,8 @@ class LeakDetector(nn.Module):
             library.seed_tensor(residual.device) if drop else _NO_SEED, bf16=self.mlp_dtype == "bf16")
         xs = xs[:-1]                                                       # [x_0 .. x_L] (the last item: x_L's mask bits)
         h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
+        if self.keep_boundary:
+            self.boundary = h_nodes
         mlp = self.edge_head.mlp     # Linear(3D,128), ReLU, Dropout, Linear(128,1)
         nmlp = self.noleak_head.mlp  # Linear(D,128), ReLU, Dropout, Linear(128,1)
         pe = float(mlp[2].p) if self.training else 0.0

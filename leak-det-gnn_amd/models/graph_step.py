@@ -14,9 +14,17 @@ and replayed: one graph launch per step, the kernels back to back on the device.
     read their seeds from device slots (ops.SeedSlots, include/leakgnn.h
     LG_SALT_SEED_PTR) that a captured torch RNG op re-draws at the head of every replay.
   * The optimizer must be built with capturable=True (device-side step counters).
-  * world > 1: the step is two graphs around ONE eager RCCL all-reduce of a flat
-    gradient bucket (graph A: forward + backward + pack; all-reduce; graph B: unpack +
-    clip + AdamW), so no collective is ever captured.
+  * world > 1: no collective is ever captured.  A model that names a gradient split
+    (`overlap_split()` -> the parameters whose gradients are final at a boundary tensor
+    it keeps as `model.boundary`, LeakDetector: the two heads, 33,282 of 60,418 values)
+    runs THREE graphs around two eager RCCL all-reduces:
+      A1: forward + backward down to the boundary (CE, heads) + pack the head bucket;
+      all-reduce(head bucket, async: RCCL's stream runs it while A2 runs);
+      A2: backward from the boundary (trunk, GRU) + pack the trunk bucket;
+      all-reduce(trunk bucket); wait for both;
+      B:  unpack both + clip + optimizer.
+    Without a split: graph A (forward + backward + pack), one all-reduce, graph B.
+    `comm = False` skips the collectives (bench.py's exposed-exchange measurement only).
 """
 from __future__ import annotations
 
@@ -38,7 +46,11 @@ class CapturedTrainStep:
 
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, opt: torch.optim.Optimizer,
                  inputs: Sequence[torch.Tensor], label: torch.Tensor, clip: Optional[float] = 1.0,
-                 warmup: int = 3, seed_slots: int = 16):
+                 warmup: int = 3, seed_slots: int = 16, preserve_state: bool = False):
+        """preserve_state: the eager warm-up steps (allocator pools, optimizer state) leave the
+        parameters, the optimizer state and torch's CPU generator as they found them, so the
+        first replay is the caller's next step (the training CLI switching to the graph
+        mid-run).  Optimizer state created by the warm-up is zeroed (AdamW's initial value)."""
         for group in opt.param_groups:
             if not group.get("capturable", False):
                 raise ValueError("CapturedTrainStep needs an optimizer built with capturable=True")
@@ -50,6 +62,7 @@ class CapturedTrainStep:
         self.slots = ops.SeedSlots(dev, seed_slots)
         self._one: Optional[torch.Tensor] = None
 
+        snap = self._snapshot() if preserve_state else None
         # eager warm-up on a side stream (allocator pools, optimizer state, cached graph CSR)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -60,32 +73,94 @@ class CapturedTrainStep:
         torch.cuda.synchronize(dev)
 
         self.opt.zero_grad(set_to_none=True)
+        self.comm = True
         self.graph_a = torch.cuda.CUDAGraph()
+        self.graph_a2 = None
         self.graph_b = None
+        split = getattr(model, "overlap_split", None)
+        self.heads = [p for p in split() if p.requires_grad] if (self.world > 1 and split is not None) else []
+        hid = {id(p) for p in self.heads}
+        self.trunk = [p for p in self.params if id(p) not in hid]
         ops.use_device_seeds(self.slots)
         try:
-            with torch.cuda.graph(self.graph_a):
-                self.slots.refresh()
-                # detached: the static loss must not keep the capture-time autograd graph
-                # (and its AccumulateGrad nodes, bound to the capture stream) alive, or a
-                # later eager backward on another stream would sync on them
-                self.loss = self._forward_backward().detach()
-                if self.world == 1:
+            if self.world == 1:
+                with torch.cuda.graph(self.graph_a):
+                    self.slots.refresh()
+                    # detached: the static loss must not keep the capture-time autograd graph
+                    # (and its AccumulateGrad nodes, bound to the capture stream) alive, or a
+                    # later eager backward on another stream would sync on them
+                    self.loss = self._forward_backward().detach()
                     self._update()
-                else:
-                    self.grads = [p.grad for p in self.params]
-                    self.flat = torch.cat([g.reshape(-1) for g in self.grads])
+            elif self.heads:
+                model.keep_boundary = True
+                try:
+                    with torch.cuda.graph(self.graph_a):
+                        self.slots.refresh()
+                        loss = self.loss_fn(self.model(*self.inputs), self.label)
+                        bnd = model.boundary
+                        self._one = torch.ones_like(loss)
+                        # retain_graph: A2 walks the trunk half of this autograd graph
+                        torch.autograd.backward(loss, self._one, retain_graph=True, inputs=self.heads + [bnd])
+                        self.loss = loss.detach()
+                        self.flat_h = torch.cat([p.grad.reshape(-1) for p in self.heads])
+                    self.graph_a2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self.graph_a2, pool=self.graph_a.pool()):
+                        torch.autograd.backward(bnd, bnd.grad, inputs=self.trunk)
+                        self.flat_t = torch.cat([p.grad.reshape(-1) for p in self.trunk])
+                finally:
+                    model.keep_boundary = False
+                    model.boundary = None
+                del loss, bnd
+                self.buckets = [(self.flat_h, self.heads), (self.flat_t, self.trunk)]
+            else:
+                with torch.cuda.graph(self.graph_a):
+                    self.slots.refresh()
+                    self.loss = self._forward_backward().detach()
+                    self.flat = torch.cat([p.grad.reshape(-1) for p in self.params])
+                self.buckets = [(self.flat, self.params)]
         finally:
             ops.use_device_seeds(None)
+        if snap is not None:
+            self._restore(snap)
         if self.world > 1:
-            views, off = [], 0
-            for g in self.grads:
-                views.append(self.flat[off:off + g.numel()].view_as(g))
-                off += g.numel()
+            grads, views = [], []
+            for flat, ps in self.buckets:
+                off = 0
+                for p in ps:
+                    grads.append(p.grad)
+                    views.append(flat[off:off + p.numel()].view_as(p))
+                    off += p.numel()
             self.graph_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_b):
-                torch._foreach_copy_(self.grads, views)
+                torch._foreach_copy_(grads, views)
                 self._update()
+
+    def _opt_tensors(self) -> list:
+        out = []
+        for st in self.opt.state.values():
+            out += [v for v in st.values() if torch.is_tensor(v)]
+        for g in self.opt.param_groups:
+            out += [v for v in g.values() if torch.is_tensor(v)]
+        return out
+
+    def _snapshot(self) -> tuple:
+        with torch.no_grad():
+            params = [(p, p.detach().clone()) for p in self.model.parameters()]
+            opt = {id(t): (t, t.detach().clone()) for t in self._opt_tensors()}
+        return params, opt, torch.get_rng_state()
+
+    def _restore(self, snap: tuple) -> None:
+        params, opt, rng = snap
+        with torch.no_grad():
+            for p, v in params:
+                p.copy_(v)
+            for t in self._opt_tensors():
+                if id(t) in opt:
+                    t.copy_(opt[id(t)][1])
+                else:
+                    t.zero_()
+        torch.set_rng_state(rng)
+        torch.cuda.synchronize()
 
     def _forward_backward(self) -> torch.Tensor:
         loss = self.loss_fn(self.model(*self.inputs), self.label)
@@ -114,13 +189,28 @@ class CapturedTrainStep:
                 off += p.numel()
         self._update()
 
+    def _all_reduce(self, flat: torch.Tensor, async_op: bool = False):
+        if dist.get_backend() == "nccl":
+            return dist.all_reduce(flat, op=dist.ReduceOp.AVG, async_op=async_op)
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=async_op)  # gloo has no AVG
+        if work is not None:
+            work.wait()
+        flat.div_(self.world)
+        return None
+
     def __call__(self) -> torch.Tensor:
         self.graph_a.replay()
         if self.graph_b is not None:
-            if dist.get_backend() == "nccl":
-                dist.all_reduce(self.flat, op=dist.ReduceOp.AVG)
-            else:  # gloo has no AVG
-                dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-                self.flat.div_(self.world)
+            if self.graph_a2 is not None:
+                # the head bucket's exchange overlaps the trunk backward (RCCL's own stream
+                # waits for A1, the current stream runs A2 meanwhile)
+                work = self._all_reduce(self.flat_h, async_op=True) if self.comm else None
+                self.graph_a2.replay()
+                if self.comm:
+                    self._all_reduce(self.flat_t)
+                    if work is not None:
+                        work.wait()
+            elif self.comm:
+                self._all_reduce(self.flat)
             self.graph_b.replay()
         return self.loss

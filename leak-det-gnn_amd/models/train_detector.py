@@ -22,6 +22,11 @@ single-process batch at any world size), scales its mean loss by its share of th
 and one gradient all-reduce (models/ddp.py: RCCL over xGMI, gloo on CPU) averages the
 gradients before clipping, so every rank takes the single-process step.  Rank 0
 evaluates, logs and writes the checkpoints.
+
+On the GPU every full-size batch's step is one captured HIP graph (--capture, default
+auto: models/graph_step.CapturedTrainStep, the batch copied into its static inputs; at
+world > 1 the heads' gradient all-reduce overlaps the trunk backward); a short tail
+batch runs eagerly.  --perf_log writes windows/s per log interval as JSONL.
 """
 from __future__ import annotations
 
@@ -40,7 +45,7 @@ import torch
 import torch.nn as nn
 
 from .datasets import AbruptLeakDetectorDataset, SensorStandardizer
-from .ddp import GradAllReduce, dist_env, init_distributed, rank_generator_seed
+from .ddp import GradAllReduce, dist_env, init_distributed, reseed_rank
 from .detector import LeakDetector
 from .loss import CrossEntropyLoss
 from .optim import ClipAdamW
@@ -48,6 +53,32 @@ from .predictor import NormalPredictorGRU, NormalPredictorTCN
 from .train_predictor import make_loader, pick_device, set_seed
 from .utils import build_residual_sequence_from_segment, now
 from .window_evaluator import DetectorEvaluator
+
+
+class PerfLog:
+    """JSONL perf log of the training loop: one line per --log_every interval with
+    the global windows trained, wall seconds and windows/s since the previous line.  Written
+    at the loss-logging points, which already synchronise (the loss is read back)."""
+
+    def __init__(self, path, world: int):
+        import time
+        self.path, self.world, self._time = path, world, time.perf_counter
+        self.t0, self.n = self._time(), 0
+        if path is not None:
+            Path(path).write_text("", encoding="utf-8")
+
+    def add(self, n_local: int) -> None:
+        self.n += n_local * self.world
+
+    def flush(self, epoch: int, step: int, loss: float, mode: str) -> None:
+        t = self._time()
+        if self.path is not None:
+            dt = max(t - self.t0, 1e-9)
+            rec = {"epoch": epoch, "step": step, "windows": self.n, "seconds": round(dt, 6),
+                   "windows_per_s": round(self.n / dt, 2), "loss": loss, "mode": mode, "world": self.world}
+            with open(self.path, "a", encoding="utf-8") as f:
+                f.write(json.dumps(rec) + "\n")
+        self.t0, self.n = t, 0
 
 
 def scenario_to_pipe_id(sid: str) -> str:
@@ -169,6 +200,11 @@ def main(argv=None) -> None:
                          "MFMA product, BASELINE configs[2])")
     ap.add_argument("--dist_backend", type=str, default="auto", choices=["auto", "nccl", "gloo"],
                     help="data parallel under torchrun: nccl (= RCCL on ROCm) for GPUs, gloo for CPU / tests")
+    ap.add_argument("--capture", type=str, default="auto", choices=["auto", "on", "off"],
+                    help="replay each full-size training batch's step as one captured HIP graph "
+                         "(models/graph_step.py; auto = on for the GPU path); the tail batch runs eagerly")
+    ap.add_argument("--perf_log", type=str, default="detector_perf.jsonl",
+                    help="JSONL perf log (windows/s per log interval), relative to --out_dir; '' disables")
     args = ap.parse_args(argv)
 
     rank, local_rank, world = dist_env()
@@ -246,8 +282,7 @@ def main(argv=None) -> None:
     allreduce = GradAllReduce(detector.parameters())  # no-op at world 1
     # identical weights on every rank (built above from args.seed); from here on each rank
     # draws its own dropout seeds
-    if world > 1:
-        torch.manual_seed(rank_generator_seed(args.seed, rank))
+    reseed_rank(args.seed, rank, world)
     evaluator = DetectorEvaluator(predictor=predictor, detector=detector, device=device, l_pred=args.l_pred,
                                   l_det=args.l_det,
                                   metric_groups=("basic", "binary", "bucket", "atd", "success", "accuracy_i"),
@@ -283,6 +318,13 @@ def main(argv=None) -> None:
             torch.distributed.all_reduce(v)
         return v
 
+    use_graph = args.capture == "on" or (args.capture == "auto" and fused_step)
+    if use_graph and not fused_step:
+        raise ValueError("--capture on needs the GPU path (--device cuda)")
+    per_rank_full = args.batch_size // world if args.batch_size % world == 0 else -1
+    cstep = None  # graph_step.CapturedTrainStep, built at the first full-size batch
+    perf = PerfLog(out_dir / args.perf_log if (lead and args.perf_log) else None, world)
+
     for epoch in range(1, args.epochs + 1):
         detector.train()
         running = torch.zeros((), dtype=torch.float64, device=device)
@@ -305,25 +347,42 @@ def main(argv=None) -> None:
             with torch.no_grad():
                 residual = build_residual_sequence_from_segment(predictor, noisy_seg, time_seg, l_pred=args.l_pred,
                                                                 l_det=args.l_det, device=device)
-            logits = detector(residual, time_seg[:, args.l_pred:, :])
-            loss = loss_fn(logits, label)
-            opt.zero_grad(set_to_none=True)
+            tfeat = time_seg[:, args.l_pred:, :]
             n_local = noisy_seg.size(0)
-            if world > 1:  # mean over the GLOBAL batch after the all-reduce's average over ranks
-                n_glob = min(args.batch_size, len(train_ds) - (it - 1) * args.batch_size)
-                (loss * (n_local * world / n_glob)).backward()
-                allreduce()
+            n_glob = min(args.batch_size, len(train_ds) - (it - 1) * args.batch_size)
+            # decided on the GLOBAL batch, so every rank takes the same branch (same collectives)
+            if use_graph and n_glob == args.batch_size and n_local == per_rank_full:
+                # full-size batch: the whole step (fwd, CE, bwd, all-reduce, clip + AdamW) as graph
+                # replays on static inputs; the same arithmetic as the eager branch below
+                if cstep is None:
+                    from .graph_step import CapturedTrainStep
+                    cstep = CapturedTrainStep(detector, loss_fn, opt, (residual.clone(), tfeat.contiguous().clone()),
+                                              label.clone(), clip=None, warmup=2, preserve_state=True)
+                else:
+                    cstep.inputs[0].copy_(residual)
+                    cstep.inputs[1].copy_(tfeat)
+                    cstep.label.copy_(label)
+                loss = cstep()
             else:
-                loss.backward()
-            if clip is not None and not fused_step:
-                torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
-            opt.step()
+                logits = detector(residual, tfeat)
+                loss = loss_fn(logits, label)
+                opt.zero_grad(set_to_none=True)
+                if world > 1:  # mean over the GLOBAL batch after the all-reduce's average over ranks
+                    (loss * (n_local * world / n_glob)).backward()
+                    allreduce()
+                else:
+                    loss.backward()
+                if clip is not None and not fused_step:
+                    torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
+                opt.step()
             running += loss.detach().double() * n_local
             seen += n_local
+            perf.add(n_local)
             if (it % args.log_every) == 0:
                 r_, s_ = global_sum(running), global_sum(seen)
                 print(f"{now()} [detector][epoch {epoch:02d}] step {it:05d}/{len(train_loader):05d} "
                       f"loss={r_.item() / max(s_.item(), 1):.6f}")
+                perf.flush(epoch, it, r_.item() / max(s_.item(), 1), "graph" if cstep is not None else "eager")
         r_, s_ = global_sum(running), global_sum(seen)
         if lead:
             val_metrics = evaluator.evaluate(val_loader)

@@ -156,13 +156,16 @@ def check_relu_ties(pre64: dict, masks: dict, keep: dict | None = None, rel: flo
     return ties
 
 
-def oracle_run(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None, autocast=False):
+def oracle_run(sd: dict, r, tf, dt, dev, up=None, lab=None, masks=None, autocast=False, net=None):
     """The oracle detector (oracle/detector_ref.py) in eval mode: (logits, grads, fp64-comparable ReLU
     pre-activations, upstream gradient) for `up`, or for the CE gradient of `lab` in this
-    run's own precision when up is None.  masks: ReLU decisions to use (relu_masks)."""
+    run's own precision when up is None.  masks: ReLU decisions to use (relu_masks).
+    net: (inp_path, sensors, pipes, constructor kwargs); default L-TOWN-A."""
     from oracle.detector_ref import LeakDetectorRef
-    sensors, pipes = lta_ids()
-    mr = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
+    if net is None:
+        sensors, pipes = lta_ids()
+        net = (LTA_INP, sensors, pipes, {})
+    mr = LeakDetectorRef(net[0], net[1], net[2], **net[3]).eval()
     mr.load_state_dict(sd)
     mr = mr.to(dt).to(dev)
     mr.sensor_encoder.gru.train()  # MIOpen's RNN backward needs training mode (1 layer: no dropout)

@@ -23,6 +23,19 @@ def test_bench_gpus2_self_launch_dry_run():
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["dry_run"] is True
     assert d["steps"] == 3 and d["config"]["parallelism"] == "dp2"
+    # the exchange fields the driver's multi-GPU line carries (bench.py exchange_fields)
+    assert d["allreduce_us"] > 0 and d["exchange_exposed_us"] >= 0
+    assert 0 < d["weak_scaling_eff"] <= 1 and isinstance(d["exchange"], str)
+
+
+def test_exchange_fields_single_rank_and_arithmetic():
+    sys.path.insert(0, str(REPO))
+    import bench
+    one = bench.exchange_fields(1.0, 1.0, 0.0, 10, 1, "none")
+    assert one["allreduce_us"] == 0.0 and one["weak_scaling_eff"] == 1.0
+    two = bench.exchange_fields(1.2, 1.0, 0.3, 100, 2, "x")
+    assert two["allreduce_us"] == 3000.0 and two["exchange_exposed_us"] == 2000.0
+    assert abs(two["weak_scaling_eff"] - 1.0 / 1.2) < 1e-4
 
 
 def test_bench_refuses_world_mismatch():

@@ -154,3 +154,48 @@ def test_shard_slices_cover_global_batch():
         assert [i for p in parts for i in p] == list(range(100, 100 + n))
     s = list(ShardBatchSampler(20, 8, 1, 2))
     assert s == [[4, 5, 6, 7], [12, 13, 14, 15], [18, 19]]
+
+
+def _seed_worker(rank, world, port, q):
+    """train_detector's seeding order: set_seed(seed), build the model, reseed_rank, then the
+    step's dropout seeds are drawn (library.seed_tensor eagerly, SeedSlots' state word for a
+    captured step)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path[:0] = [str(REPO), str(PKG), str(REPO / "tests")]
+    from models import library, ops
+    from models.ddp import init_distributed, reseed_rank
+    from models.train_predictor import set_seed
+    init_distributed("gloo")
+    set_seed(42)
+    lin = torch.nn.Linear(16, 16)
+    reseed_rank(42, rank, world)
+    seeds = [int(library.seed_tensor(torch.device("cpu"))) for _ in range(3)]
+    slot_state = int(ops.SeedSlots(torch.device("cpu"), 4).state)
+    mask = torch.nn.functional.dropout(torch.ones(256), 0.5) != 0
+    q.put((rank, lin.weight.detach().numpy(), seeds, slot_state, mask.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ranks_draw_distinct_dropout_seeds():
+    """with one generator seed on every rank, local window i got the same dropout
+    mask on all ranks.  After reseed_rank the weights are still identical but every seed
+    draw (and so every mask) differs across ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(k, 2, port, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        k, *v = q.get(timeout=300)
+        res[k] = v
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (w0, s0, st0, m0), (w1, s1, st1, m1) = res[0], res[1]
+    assert (w0 == w1).all()
+    assert all(a != b for a, b in zip(s0, s1)) and st0 != st1
+    assert (m0 != m1).any()

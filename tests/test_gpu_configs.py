@@ -123,6 +123,77 @@ def test_c5_node_major_trunk_kernels(c5_graph, drop):
         assert_close(outs[True][i], outs[False][i], what=f"C5 node-major bwd {what}")
 
 
+@pytest.mark.parametrize("drop", [False, True])
+def test_c5_node_major_trunk_vs_fp64_oracle(c5_graph, drop):
+    """The node-major trunk kernels the product runs at B >= 16 (lg_gcn_fwd_nm_bits default:
+    producer / consumer waves, 2-way fp16 split transform; lg_gcn_bwd_nm_bits) at C5 size
+    (N = 100,000, 300,000 edge columns + self loops, B = 16, D = 64) against the oracle's
+    GCNConv arithmetic (oracle/gcn_ref.py gcn_norm / gcn_conv) in fp64 DIRECTLY, with the
+    dropout keep mask regenerated by oracle/dropout_ref.py.  Forward within 1e-5 of scale,
+    mask bits == [y64 > 0] away from ties; backward (ReLU/dropout of this layer and of the
+    previous op, from the forward's mask bits) dx, dW, db within 1e-5 of scale."""
+    from models import ops
+    from models.ops import GCNGraph
+    from oracle.dropout_ref import row_stream_mask
+    from oracle.gcn_ref import gcn_norm
+    lib = ops.load_library()
+    nat = ops.nat
+    N, D, B, p, seed, salt = 100_000, 64, 16, 0.1, 91, 2
+    graph = GCNGraph.build(c5_graph, N, DEV)
+    gen = torch.Generator().manual_seed(17)
+    xw = torch.relu(torch.randn(B, N, D, generator=gen))               # window-major truth layout
+    W = torch.randn(D, D, generator=gen) / 8
+    b = torch.randn(D, generator=gen) / 4
+    dy = torch.randn(B, N, D, generator=gen)
+    sc = 1.0 / (1.0 - p) if drop else 1.0
+    # fp64 truth (gcn_conv: h = x W^T; out[col] += w h[row]; + b), batched over windows
+    row, col, w = gcn_norm(c5_graph, N, dtype=torch.float64)
+    h = (xw.double() @ W.double().t()).transpose(0, 1).reshape(N, B * D)
+    z64 = torch.zeros(N, B * D, dtype=torch.float64).index_add_(0, col, w.view(-1, 1) * h.index_select(0, row))
+    z64 = z64.view(N, B, D) + b.double()
+    keep = torch.ones(N, B, D, dtype=torch.float64)
+    if drop:  # row b * N + n of the disjoint union (the kernels' dropout row index)
+        rows = (np.arange(B)[None, :] * N + np.arange(N)[:, None]).reshape(-1)
+        keep = torch.from_numpy(row_stream_mask(seed, salt, rows, D, p).reshape(N, B, D)).double()
+    y64 = torch.relu(z64) * keep * sc
+    del h
+    # the product kernels, node-major [N][B][D]
+    xn = xw.transpose(0, 1).contiguous().to(DEV)
+    Wd, bd = W.to(DEV), b.to(DEV)
+    st = ops.stream_of(xn)
+    flags = nat.LG_F_BIAS | nat.LG_F_RELU | (nat.LG_F_DROPOUT if drop else 0)
+    ng = (B + 15) // 16
+    yn = torch.empty_like(xn)
+    ybits = torch.zeros(N * ng * 64, dtype=torch.int16, device=DEV)
+    ops.check(lib.lg_gcn_fwd_nm_bits(ops.ptr(graph.nodetab), ops.ptr(graph.pairs), ops.ptr(xn), ops.ptr(Wd),
+                                     ops.ptr(bd), ops.ptr(yn), B, N, D, graph.nnz_cap, flags, p, seed, salt, st,
+                                     ops.ptr(ybits)), "fwd_nm_bits")
+    y = yn.cpu()
+    assert_close(y, y64, what="C5 node-major forward vs fp64 oracle")
+    pos = y > 0
+    tie = (z64.abs() <= 1e-5 * z64.abs().max()).logical_and(keep > 0)
+    assert torch.equal(pos[~tie], (y64 > 0)[~tie]), "ReLU/dropout decisions differ away from ties"
+    # backward, masks on the HIP run's side of every kink
+    dz64 = dy.double().transpose(0, 1) * pos.double() * sc                                   # [N, B, D]
+    t64 = torch.zeros(N, B * D, dtype=torch.float64).index_add_(
+        0, row, w.view(-1, 1) * dz64.reshape(N, B * D).index_select(0, col)).view(N, B, D)   # Ahat^T dz
+    xin = xw.double().transpose(0, 1)
+    dx64 = (t64 @ W.double()) * (xin > 0).double() * sc
+    dW64 = t64.reshape(-1, D).t() @ xin.reshape(-1, D)
+    db64 = dz64.reshape(-1, D).sum(0)
+    dyn = dy.transpose(0, 1).contiguous().to(DEV)
+    dx = torch.empty_like(xn)
+    dW, db = torch.empty(D, D, device=DEV), torch.empty(D, device=DEV)
+    ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+    ops.check(lib.lg_gcn_bwd_nm_bits(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t), ops.ptr(dyn), None,
+                                     ops.ptr(xn), ops.ptr(Wd), ops.ptr(dx), ops.ptr(dW), ops.ptr(db), None, None, B,
+                                     N, D, nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, sc, sc, ops.ptr(ws), st,
+                                     ops.ptr(ybits)), "bwd_nm_bits")
+    assert_close(dx, dx64, what="C5 node-major dx vs fp64 oracle")
+    assert_close(dW, dW64, what="C5 node-major dW vs fp64 oracle")
+    assert_close(db, db64, what="C5 node-major db vs fp64 oracle")
+
+
 def test_c5_detector_vs_oracle(tmp_path):
     """One full LeakDetector on the C5 network written as an EPANET .inp (100,000 nodes,
     150,000 pipes, S = 29 sensors, P = 150,000 pipe classes), B = 1, eval mode, random

@@ -182,3 +182,49 @@ def test_train_detector_data_parallel_equals_single_process(data, tmp_path):
     for k in b:
         d = (a[k].double() - b[k].double()).abs().max().item()
         assert d <= 2e-5 * max(b[k].abs().max().item(), 1e-3), f"{k}: {d:.3e}"
+
+
+def test_train_detector_captured_cli_equals_eager_cli(data, tmp_path):
+    """--capture on (every full-size batch's step one replayed HIP graph, the tail batch
+    eager) writes the checkpoint the eager CLI (--capture off) writes, dropout off on both
+    sides (the graph draws its masks from device seed slots); the JSONL perf log has one
+    line per log interval with windows/s."""
+    from models import train_detector, train_predictor
+    from models.detector import LeakDetector
+    from models.synth import write_synthetic_leak_set
+    write_synthetic_leak_set(tmp_path / "leak", INFO["sensors"], INFO["pipes"], scenes_per_pipe=4, n_noleak=12,
+                             T=300, seed=1)
+    out = tmp_path / "pred"
+    train_predictor.main(["--normal_root", str(data / "normal"), "--out_dir", str(out), "--epochs", "1",
+                          "--steps_per_epoch", "16", "--val_steps", "8", "--test_steps", "8", "--batch_size", "8",
+                          "--device", "cuda"])
+
+    class NoDropout(LeakDetector):
+        def __init__(self, *a, **k):
+            k["dropout"] = 0.0
+            super().__init__(*a, **k)
+
+    def run(o, mode):
+        train_detector.main(["--leak_root", str(tmp_path / "leak"), "--inp_path", str(LTA_INP), "--predictor_ckpt",
+                             str(out / "predictor_best.ckpt"), "--out_dir", str(o), "--epochs", "2",
+                             "--steps_per_epoch", "20", "--val_steps", "8", "--test_steps", "8", "--batch_size", "8",
+                             "--device", "cuda", "--log_every", "1", "--capture", mode])
+    orig = train_detector.LeakDetector
+    train_detector.LeakDetector = NoDropout
+    try:
+        run(tmp_path / "g", "on")
+        run(tmp_path / "e", "off")
+    finally:
+        train_detector.LeakDetector = orig
+    a = torch.load(tmp_path / "g" / "detector_last.ckpt", weights_only=True)["detector_state"]
+    b = torch.load(tmp_path / "e" / "detector_last.ckpt", weights_only=True)["detector_state"]
+    assert set(a) == set(b)
+    for k in b:
+        d = (a[k].double() - b[k].double()).abs().max().item()
+        assert d <= 1e-6 * max(b[k].abs().max().item(), 1e-3), f"{k}: {d:.3e}"
+    recs = [json.loads(ln) for ln in (tmp_path / "g" / "detector_perf.jsonl").read_text().splitlines()]
+    assert len(recs) == 6  # 2 epochs x 3 batches (8, 8, tail 4)
+    assert [r["mode"] for r in recs[:3]] == ["graph"] * 3  # the graph exists from the first full batch on
+    assert [r["windows"] for r in recs[:3]] == [8, 8, 4] and all(r["windows_per_s"] > 0 for r in recs)
+    eager = [json.loads(ln) for ln in (tmp_path / "e" / "detector_perf.jsonl").read_text().splitlines()]
+    assert {r["mode"] for r in eager} == {"eager"}

@@ -239,6 +239,51 @@ def test_detector_c4_graph_vs_oracle(tmp_path):
                              grads[torch.float64], slack=8.0)
 
 
+def test_detector_c4_graph_b64_vs_oracle(tmp_path):
+    """C4 at the bench's per-rank batch (BASELINE configs[3]: B = 64 windows per rank, D = 32,
+    10k nodes / 15k pipes), eval mode: B >= 16 runs the NODE-MAJOR trunk kernels at D = 32
+    (the B = 3 test above covers the window-major ones).  Logits within 1e-5 of the fp32
+    oracle; gradients vs the fp64 oracle evaluated on the HIP run's own ReLU decisions
+    (hip_relu_masks, as the L-TOWN-A B = 64 test), bounded by 4x the fp32 oracle's error
+    (CPU or GPU torch) or 5e-5 of the tensor's scale."""
+    from models.synth import pick_sensors, write_synthetic_inp
+    from oracle.detector_ref import LeakDetectorRef
+    from models.detector import LeakDetector
+    from models import ops
+    inp = tmp_path / "c4.inp"
+    node_ids, pipe_ids = write_synthetic_inp(inp, 10_000, 15_000, seed=0)
+    sensors = pick_sensors(node_ids, 29, seed=0)
+    kw = dict(sensor_hidden=32, node_hidden=32)
+    net = (inp, sensors, pipe_ids, kw)
+    torch.manual_seed(23)
+    ref = LeakDetectorRef(inp, sensors, pipe_ids, **kw).eval()
+    with torch.no_grad():
+        for c in ref.convs:
+            c.bias.normal_(0, 0.1)
+    sd = {k: v.clone() for k, v in ref.state_dict().items()}
+    m = LeakDetector(inp, sensors, pipe_ids, **kw).to(DEV).eval()
+    m.load_state_dict(sd)
+    B = 64
+    assert ops.use_node_major(B, len(m.node_names), 32)
+    gen = torch.Generator().manual_seed(24)
+    r = torch.randn(B, 36, 29, generator=gen)
+    tf = torch.randn(B, 36, 9, generator=gen)
+    lab = torch.randint(0, len(pipe_ids) + 1, (B,), generator=gen)
+    _, _, pre64, upstream = oracle_run(sd, r, tf, torch.float64, "cpu", lab=lab, net=net)
+    m.capture = {}
+    lg = m(r.to(DEV), tf.to(DEV))
+    lg.backward(upstream.float().to(DEV))
+    masks = hip_relu_masks(m.capture, B, len(m.node_names), len(pipe_ids), m.pipe_ends)
+    check_relu_ties(pre64, masks)
+    _, g64, _, _ = oracle_run(sd, r, tf, torch.float64, "cpu", up=upstream, masks=masks, net=net)
+    o32, g32, _, _ = oracle_run(sd, r, tf, torch.float32, "cpu", up=upstream, masks=masks, net=net)
+    assert_close(lg, o32, what="logits C4 B=64")
+    # EdgeHead dW sums B * P = 960k rows: yardstick also torch fp32 on the GPU, tensor bar 5e-5
+    # (as the B = 256 train-mode test, test_gpu_configs.py)
+    _, g32d, _, _ = oracle_run(sd, r, tf, torch.float32, DEV, up=upstream, masks=masks, net=net)
+    assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64, ref32=g32d, rtol_tensor=5e-5)
+
+
 def test_detector_train_mode_dropout():
     state = load("detector_b2.npz")
     m = _product_model(state).train()
