@@ -361,6 +361,10 @@ int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float
                        const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                        int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream,
                        uint16_t* ymask);
+/* lg_gcn_bwd_nm[_bits] lab variants (default: the 3-way bf16 split in the per-wave pipeline,
+ * the fastest measured): LG_F_F16X2 the 2-way fp16 split (block-scaled, |err| ~3e-7 of
+ * scale); LG_F_F16X2 | LG_F_PC at D = 64 the producer / consumer kernel.  Same results
+ * within that tolerance. */
 int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                        const float* x, const float* W, float* dx_out, float* dW, float* db,
                        const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,

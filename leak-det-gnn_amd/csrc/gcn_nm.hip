@@ -75,6 +75,18 @@ __device__ __forceinline__ void nm_st(__amdgpu_buffer_rsrc_t rs, uint32_t lane_o
                                            ok ? lane_off + base : kNmOob, 0, AUX);
 }
 
+// 16-byte buffer stores read their data VGPRs after issue: keep those registers unwritten for a
+// few wait states.  Measured on k_gcn_bwd_pc (tools/bpc_check.py; profiles/r03/r03q-r03t): the
+// compiler reused a store's data registers for VALU results 0-1 instructions after the
+// buffer_store_dwordx4 and dwords 0-1 of some lanes went out overwritten (~1 % of dx rows).
+// Call after the last store of a tile with all of its data values.
+template <int K>
+__device__ __forceinline__ void lg_store_guard(const f32x4 (&v)[K]) {
+    if constexpr (K == 4) asm volatile("s_nop 7" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]));
+    else if constexpr (K == 2) asm volatile("s_nop 7" ::"v"(v[0]), "v"(v[1]));
+    else asm volatile("s_nop 7" ::"v"(v[0]));
+}
+
 // Tile -> (node, window group) and the XCD-aware persistent schedule over groups * N tiles.
 struct NmSched {
     int64_t first, end, stride;
@@ -1003,6 +1015,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             if (ymask)
                 __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs,
                                                       nm_mask_off(n, b0 >> 4, ngroups, lane), 0, 0);
+            if constexpr (EPI) lg_store_guard(vk);
         }
 #ifdef LG_NM3_STAMPS
         if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
@@ -1365,6 +1378,7 @@ k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
                                                   0, 0);
         }
+        lg_store_guard(vk);
 #ifdef LG_NM3_STAMPS
         if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
         ++tcount;
@@ -1777,6 +1791,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
                                                   0, 0);
         }
+        lg_store_guard(vk);
         pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));  // the slot's reads are done (release)
     }
 }
@@ -1969,7 +1984,8 @@ struct Nb3Lds {
     static constexpr int WF = (3 * D * SB) / 2;          // W^T split parts (bf16), in floats
     static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
     static constexpr int L = D * D + 2 * D;               // slab row: dW, db, d(node bias)
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L);
+    static constexpr int MX = WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L;
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(MX + kNmBwdWaves3);  // + per-wave max |W| (F16)
 };
 
 #ifndef LG_NB3_NPF
@@ -1977,7 +1993,9 @@ struct Nb3Lds {
 #endif
 // MB (with MASK_IN): the layer's output mask comes as the forward's ymask bits instead of a
 // gather of y, so the prefetch keeps the unmasked depth
-template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false>  // BF: LG_F_BF16, single-product MFMAs
+// F16 (fp32 tier): both GEMMs on the 2-way fp16 split with power-of-two block scales (W per
+// launch, t and x per tile): 3 f16 MFMAs per product instead of 6 bf16 ones
+template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false, bool F16 = false>
 __global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
 k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
               const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
@@ -2076,11 +2094,28 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
     }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
+    int wexp = 0;  // F16: W's scale exponent (WG-wide max |W| at [2^14, 2^15))
     {
         constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
         f32x4 wv[WPER];
 #pragma unroll
         for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
+        float wsc = 1.f;
+        if constexpr (F16) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int u = 0; u < WPER; ++u)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(wv[u][c])));
+            m = lg_wave_max_bits(m);
+            uint32_t* wmx = reinterpret_cast<uint32_t*>(smem) + LY::MX;
+            if (lane == 0) wmx[wave] = m;
+            __syncthreads();
+#pragma unroll
+            for (int w2 = 0; w2 < kNmBwdWaves3; ++w2) m = max(m, wmx[w2]);
+            wexp = lg_f16_scale_exp_c(m);
+            wsc = lg_pow2f(wexp);
+        }
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
             const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
@@ -2088,13 +2123,21 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             const int o = i4 / (D / 4), c4 = 4 * (i4 % (D / 4));
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
+                const int e = (c4 + c) * SB + o;
+                if constexpr (F16) {
+                    const float w = wv[u][c] * wsc;
+                    const _Float16 h0 = static_cast<_Float16>(w);
+                    const _Float16 h1 = static_cast<_Float16>(w - static_cast<float>(h0));
+                    wsl[e] = __builtin_bit_cast(uint16_t, h0);
+                    wsl[D * SB + e] = __builtin_bit_cast(uint16_t, h1);
+                    continue;
+                }
                 const float w = wv[u][c];
                 const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
                 const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
                 const uint16_t h1 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r1));
                 const float r2 = r1 - __uint_as_float(static_cast<uint32_t>(h1) << 16);
                 const uint16_t h2 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r2));
-                const int e = (c4 + c) * SB + o;
                 wsl[e] = h0;
                 wsl[D * SB + e] = h1;
                 wsl[2 * D * SB + e] = h2;
@@ -2190,6 +2233,21 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         issue(nxt, nn, nb0, nnb);
         __builtin_amdgcn_sched_barrier(0);
+        // F16: the tile's t and x scale exponents (max over the wave's registers)
+        int texp = 0, xexp = 0;
+        if constexpr (F16) {
+            uint32_t mt = 0, mx = 0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    mt = max(mt, __float_as_uint(fabsf(acc[k][c])));
+                    mx = max(mx, __float_as_uint(fabsf(xv[k][c])));
+                }
+            texp = lg_f16_scale_exp_c(lg_wave_max_bits(mt));
+            xexp = lg_f16_scale_exp_c(lg_wave_max_bits(mx));
+        }
+        const float tsc = lg_pow2f(texp), xsc = lg_pow2f(xexp);
 
         wave_sync_nm();
 #pragma unroll
@@ -2199,7 +2257,39 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         wave_sync_nm();
         // dW += t^T x over the tile's 16 rows: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
-        {
+        if constexpr (F16) {
+            lg_f16x4 xb[G::CH][2];
+#pragma unroll
+            for (int ni = 0; ni < G::CH; ++ni) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j] * xsc;
+                split2_f16_x4(v, xb[ni][0], xb[ni][1]);
+            }
+            const float us = lg_pow2f(-(texp + xexp));
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j] * tsc;
+                lg_f16x4 a0, a1;
+                split2_f16_x4(v, a0, a1);
+                f32x4 c[G::CH];
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni) {
+                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, xb[ni][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][1], c[ni], 0, 0, 0);
+                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][0], c[ni], 0, 0, 0);
+                }
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) dw[mo][ni][reg] = fmaf(c[ni][reg], us, dw[mo][ni][reg]);
+                // one output row block at a time: interleaving all 16 unscaled partials would hold
+                // 64 more VGPRs
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
             lg_i16x4 xb[G::CH][3];
 #pragma unroll
             for (int ni = 0; ni < G::CH; ++ni) {
@@ -2242,8 +2332,33 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         f32x4 o[G::CH];
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // the W fragments are loop-invariant LDS reads: an opaque zero offset keeps the compiler
+        // from hoisting all of them (64 VGPRs) out of the tile loop
+        int wz = 0;
+        asm volatile("" : "+s"(wz));
 #pragma unroll
-        for (int s2 = 0; s2 < D / 32; ++s2) {
+        for (int s2 = 0; s2 < D / 32 && F16; ++s2) {
+            lg_f16x8 b0f, b1f;
+            split2_f16_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q) * tsc, ld4(tl + j * G::S + 32 * s2 + 8 * q + 4) * tsc, b0f,
+                          b1f);
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) {
+                const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q + wz;
+                const lg_f16x8 a0 = *reinterpret_cast<const lg_f16x8*>(wsl + ew);
+                const lg_f16x8 a1 = *reinterpret_cast<const lg_f16x8*>(wsl + D * SB + ew);
+                o[mt] = mfma_h(a1, b0f, o[mt]);
+                o[mt] = mfma_h(a0, b1f, o[mt]);
+                o[mt] = mfma_h(a0, b0f, o[mt]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (F16) {
+            const float ux = lg_pow2f(-(wexp + texp));
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] *= ux;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < D / 32 && !F16; ++s2) {
             lg_bf16x8 b0f, b1f, b2f;
             split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f, b2f);
 #pragma unroll
@@ -2283,11 +2398,14 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
         wave_sync_nm();
         const uint32_t ob = (n * B + b0) * (4u * D);
+        f32x4 vk[G::K];
+#pragma unroll
+        for (int k = 0; k < G::K; ++k) vk[k] = ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg);
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg)),
-                dxs, tlo[k] + ob, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                   dxs, tlo[k] + ob, 0, 0);
+        lg_store_guard(vk);
     }
     if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
 #pragma unroll
@@ -2323,6 +2441,477 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 for (int mt = 0; mt < G::CH; ++mt)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
+        }
+    }
+    __syncthreads();
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
+}
+
+// ------------------------------------------------------------------ backward, producer / consumer waves
+// lg_gcn_bwd_nm[_bits] at D = 64 split by ROLE, as k_gcn_fwd_pc does the forward.  nm3 held a
+// tile's gather prefetch (64 VGPRs), the dW accumulators (64) and both GEMMs' operands in one
+// wave: 243-256 VGPRs, two waves per SIMD, each alternating a load-latency phase with a
+// ~1.5k-cycle MFMA/LDS phase.  Here:
+//   * kBpcProd PRODUCER waves gather t = Ahat^T dz (dz = dy * scale_in * [y > 0] from the
+//     forward's mask bits) with two tiles' neighbour blocks in flight, keep db (the rows' own
+//     dz, from the self entry), and hand each t tile to a consumer through an LDS ring
+//     (XOR-swizzled 16 x 64 fp32 slots) with the tile's f16 scale exponent;
+//   * NC CONSUMER waves per producer load the tile's own x block one tile ahead, run
+//     dW += t^T x and dx = t W on the 2-way fp16 split (W^T's parts in LDS in MFMA-fragment
+//     order: one conflict-free ds_read_b128 per fragment), apply [x > 0] * scale_out, and
+//     store dx through the slot in the coalesced gather layout.
+// Hand-off as k_gcn_fwd_pc (ready / done counters, bounded acquire polls).  dW, db and the
+// node-bias sums are reduced over the workgroup's waves in a fixed order into the slab row
+// (deterministic), exactly as k_gcn_bwd_nm3.
+#ifndef LG_BPC_RING
+#define LG_BPC_RING 4
+#endif
+#ifndef LG_BPC_NPF
+#define LG_BPC_NPF 3
+#endif
+#ifndef LG_BPC_CONS
+#define LG_BPC_CONS 1  // consumers per producer: 1 -> 8 waves, 256 VGPRs each (2 -> 12 waves at 168 spills)
+#endif
+constexpr int kBpcRing = LG_BPC_RING;
+constexpr int kBpcProd = 4, kBpcCons = LG_BPC_CONS;
+
+struct BpcLds {  // floats, D = 64
+    static constexpr int D = 64, CH = 4, KS = 2;
+    static constexpr int TILE = 16 * D;
+    static constexpr int WFR = 2 * CH * KS * 64 * 4;                   // W^T f16 parts, fragment order (16 B / lane)
+    static constexpr int WMX = WFR;                                     // per-wave max |W| bits
+    static constexpr int FOFF = WMX + 16;                               // ready[16], done[kBpcProd * NC]
+    static constexpr int MOFF = FOFF + 16 + kBpcProd * kBpcCons;        // per (producer, slot): n, b0, nb, texp
+    static constexpr int ROFF = MOFF + 4 * kBpcProd * kBpcRing;         // the rings
+    static constexpr int XOFF = ROFF + kBpcProd * kBpcRing * TILE;      // per consumer: x tile
+    static constexpr int END = XOFF + kBpcProd * kBpcCons * TILE;
+    static constexpr int L = D * D + 2 * D;                             // slab row: dW, db, d(node bias)
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(END > L ? END : L);
+    static __device__ __forceinline__ int tix(int r, int c) { return r * D + 4 * (c ^ r); }
+};
+
+template <bool MI, bool NB>
+__global__ void __launch_bounds__(64 * kBpcProd * (1 + kBpcCons), kBpcProd * (1 + kBpcCons) / 4)
+k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
+             const float* __restrict__ x, const float* __restrict__ W, const int32_t* __restrict__ node_slot,
+             float* __restrict__ dxo, float* __restrict__ slab, uint32_t N, uint32_t B, uint32_t ngroups,
+             lg_fastdiv fdN, int mask_out, float scale_in, float scale_out, const uint16_t* __restrict__ ymask) {
+    constexpr int D = 64;
+    using G = NmGeo<D>;
+    using LY = BpcLds;
+    constexpr int NC = kBpcCons, R = kBpcRing, NPF = LG_BPC_NPF, CH = LY::CH, KS = LY::KS;
+    constexpr int NW = kBpcProd * (1 + NC), NT = 64 * NW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    uint32_t* wmx = reinterpret_cast<uint32_t*>(lds + LY::WMX);
+    uint32_t* ready = reinterpret_cast<uint32_t*>(lds + LY::FOFF);
+    uint32_t* done = ready + 16;
+    uint32_t* meta = reinterpret_cast<uint32_t*>(lds + LY::MOFF);
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool producer = wave < kBpcProd;
+    const int prod = producer ? wave : (wave - kBpcProd) % kBpcProd;
+    const int cons = producer ? 0 : (wave - kBpcProd) / kBpcProd;
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+    const int rl = lane / G::LPR, fg = lane % G::LPR;
+    float* ring = lds + LY::ROFF + prod * R * LY::TILE;
+    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, prod, kBpcProd);
+    const int64_t tend = sc.end;
+    uint32_t loff[G::K];
+#pragma unroll
+    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
+    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+        const bool valid = tile < tend;
+        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+        const uint32_t grp = lg_div(t32, fdN);
+        n = t32 - grp * N;
+        b0 = grp * 16;
+        nb = valid ? min(16u, B - b0) : 0u;
+    };
+
+    // max |W| over the workgroup (the f16 scale of W), counters cleared
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT;
+        uint32_t wm = 0;
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const f32x4 w = ld4(W + 4 * min<int>(u * NT + threadIdx.x, W4 - 1));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
+        }
+        wm = lg_wave_max_bits(wm);
+        if (lane == 0) wmx[wave] = wm;
+        if (threadIdx.x < 16 + kBpcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
+    }
+    __syncthreads();
+    int wexp;
+    {
+        uint32_t m = 0;
+        for (int w2 = 0; w2 < NW; ++w2) m = max(m, wmx[w2]);
+        wexp = lg_f16_scale_exp_c(__builtin_amdgcn_readfirstlane(m));
+    }
+    // W^T's f16 parts in fragment order: fragment (part, mt, s2), lane (j, q) holds
+    // A[i = 16 mt + j][o = 32 s2 + 8 q + e] = W[o][i] * 2^wexp, e = 0..7
+    {
+        const float wsc = lg_pow2f(wexp);
+        uint32_t* wfr = reinterpret_cast<uint32_t*>(lds);
+        for (int f = threadIdx.x; f < CH * KS * 64; f += NT) {
+            const int l = f & 63, ms = f >> 6, mt = ms / KS, s2 = ms % KS;
+            const int i = 16 * mt + (l & 15), o0 = 32 * s2 + 8 * (l >> 4);
+            lg_u32x4 h0, h1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                uint32_t a0, a1;
+                split2_f16_pair(W[(o0 + 2 * e) * D + i] * wsc, W[(o0 + 2 * e + 1) * D + i] * wsc, a0, a1);
+                h0[e] = a0;
+                h1[e] = a1;
+            }
+            *reinterpret_cast<lg_u32x4*>(wfr + 4 * ((0 * CH * KS + ms) * 64 + l)) = h0;
+            *reinterpret_cast<lg_u32x4*>(wfr + 4 * ((1 * CH * KS + ms) * 64 + l)) = h1;
+        }
+    }
+    __syncthreads();
+
+    // initialised only in the role that uses them (a zero held across the other role's loop
+    // would cost its registers)
+    f32x4 dbacc;               // producers: channels 4fg..4fg+3 over the lane's rows
+    f32x4 dw[CH][CH];          // consumers: dW tile (mo, ni)
+    f32x4 nbacc[NB ? CH : 1];  // consumers, NB: channels 16mt + 4q + reg over rows j
+
+    if (producer) {
+        dbacc = f32x4{0.f, 0.f, 0.f, 0.f};
+        // ---------------- producer: t = Ahat^T dz, two tiles in flight
+        const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), dys0 = nm_rsrc(dy, 0);
+        const __amdgpu_buffer_rsrc_t mbs = nm_mask_rsrc(ymask, N, ngroups);
+        auto ldb = [&](uint32_t m, uint32_t grp, bool have) -> uint32_t {
+            if constexpr (!MI) return 0u;
+            return __builtin_amdgcn_raw_buffer_load_b16(mbs, have ? nm_mask_off(m, grp, ngroups, lane) : kNm3BlkOob + 2u * lane,
+                                                        0, 0);
+        };
+        auto dzb = [&](const f32x4& g, uint32_t bits, int k) {
+            if constexpr (!MI) return g;
+            f32x4 r;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) r[c] = (bits >> (4 * k + c)) & 1u ? g[c] * scale_in : 0.f;
+            return r;
+        };
+        f32x4 pf[2][NPF][G::K];
+        uint32_t pmb[2][NPF];
+        uint32_t lo[2][G::K];
+        NmRec rec[2];
+        uint32_t tn[2], tb0[2], tnb[2];
+        auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
+            constexpr int b = decltype(bc)::value;
+            uint32_t n, b0, nb;
+            tile_coords(tile, n, b0, nb);
+            rec[b] = r;
+            tn[b] = static_cast<uint32_t>(r.node);
+            tb0[b] = b0;
+            tnb[b] = nb;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) lo[b][k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+                const bool have = r.e0 + i < r.e1;
+                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
+                const __amdgpu_buffer_rsrc_t rs = have ? dys : dys0;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    pf[b][i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], base, 0));
+                pmb[b][i] = ldb(static_cast<uint32_t>(r.p[i].x), b0 >> 4, have);
+            }
+        };
+        auto step = [&](auto bc, int64_t t) -> bool {
+            constexpr int b = decltype(bc)::value;
+            const int64_t tile = sc.first + t * sc.stride;
+            if (tile >= tend) return false;
+            uint32_t nn, nb0, nnb;
+            tile_coords(tile + 2 * sc.stride, nn, nb0, nnb);
+            const NmRec nxt = nm_rec(tab, N + nn);
+            asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
+            const NmRec& cur = rec[b];
+            const int e0 = cur.e0, e1 = cur.e1, self = cur.self;
+            const uint32_t b0 = tb0[b], n = tn[b];
+            f32x4 acc[G::K];
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+                if (e0 + i < e1) {
+                    const float w = __int_as_float(cur.p[i].y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) {
+                        const f32x4 z = dzb(pf[b][i][k], pmb[b][i], k);
+                        pk_fma4(acc[k], w, z);
+                        if (i == self) dbacc += z;
+                    }
+                }
+            }
+            if (e0 + NPF < e1) {  // the rest of the row: the inline blocks in flight at once, then the pair array
+                constexpr int NI = kLgNmInline - NPF;
+                f32x4 va[NI][G::K];
+                uint32_t vb[NI];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const bool have = e0 + NPF + i < e1;
+                    const uint32_t ba = have ? (static_cast<uint32_t>(cur.p[NPF + i].x) * B + b0) * (4u * D) : 0u;
+                    const __amdgpu_buffer_rsrc_t rs = have ? dys : dys0;
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k)
+                        va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], ba, 0));
+                    vb[i] = ldb(static_cast<uint32_t>(cur.p[NPF + i].x), b0 >> 4, have);
+                }
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    if (e0 + NPF + i < e1) {
+                        const float wa = __int_as_float(cur.p[NPF + i].y);
+#pragma unroll
+                        for (int k = 0; k < G::K; ++k) {
+                            const f32x4 z = dzb(va[i][k], vb[i], k);
+                            pk_fma4(acc[k], wa, z);
+                            if (NPF + i == self) dbacc += z;
+                        }
+                    }
+                }
+                for (int e = e0 + kLgNmInline; e < e1; ++e) {
+                    const int2 pa = pairs[e];
+                    const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
+                    f32x4 vv[G::K];
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k)
+                        vv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dys, lo[b][k], ba, 0));
+                    const uint32_t bm = ldb(static_cast<uint32_t>(pa.x), b0 >> 4, true);
+                    const float wa = __int_as_float(pa.y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, dzb(vv[k], bm, k));
+                }
+            }
+            if (self < 0) {  // no self entry among the inline pairs: the own dz rows for db
+                const uint32_t ob = (n * B + b0) * (4u * D);
+                const uint32_t bo = ldb(n, b0 >> 4, true);
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+                    dbacc += dzb(__builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dys, lo[b][k], ob, 0)), bo, k);
+            }
+            // the tile's f16 scale exponent
+            uint32_t mt = 0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) mt = max(mt, __float_as_uint(fabsf(acc[k][c])));
+            const int texp = lg_f16_scale_exp_c(lg_wave_max_bits(mt));
+            const int sl = static_cast<int>(t % R);
+            const uint32_t mnb = tnb[b];
+            issue(bc, nxt, tile + 2 * sc.stride);
+            if (t >= R) pc_wait(&done[prod * NC + static_cast<int>((t - R) % NC)], static_cast<uint32_t>((t - R) / NC + 1));
+            float* slot = ring + sl * LY::TILE;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
+            if (lane == 0) {
+                uint32_t* m = meta + 4 * (prod * R + sl);
+                m[0] = n;
+                m[1] = b0;
+                m[2] = mnb;
+                m[3] = static_cast<uint32_t>(texp);
+            }
+            pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
+            return true;
+        };
+        {
+            uint32_t n0, b00, nb00, n1, b01, nb01;
+            tile_coords(sc.first, n0, b00, nb00);
+            tile_coords(sc.first + sc.stride, n1, b01, nb01);
+            const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
+            issue(std::integral_constant<int, 0>{}, r0, sc.first);
+            issue(std::integral_constant<int, 1>{}, r1, sc.first + sc.stride);
+        }
+        for (int64_t t = 0;; t += 2) {
+            if (!step(std::integral_constant<int, 0>{}, t)) break;
+            if (!step(std::integral_constant<int, 1>{}, t + 1)) break;
+        }
+    } else {
+        // ---------------- consumer: dW += t^T x, dx = t W, masks, store
+        const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
+        float* xt = lds + LY::XOFF + (wave - kBpcProd) * LY::TILE;  // this consumer's x tile
+        const uint32_t* wfr = reinterpret_cast<const uint32_t*>(lds);
+        // x block of this consumer's u-th tile (zeros past the end: a masked-off block)
+        auto xload = [&](int64_t u, f32x4 (&px)[G::K]) {
+            const int64_t tile = sc.first + (u * NC + cons) * sc.stride;
+            uint32_t n, b0, nb;
+            tile_coords(tile, n, b0, nb);
+            n = tile < tend ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(tab[16 * (N + n) + 15])) : 0u;
+            const uint32_t ob = nb ? (n * B + b0) * (4u * D) : kNm3BlkOob;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) {
+                const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+                px[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, lk, ob, 0));
+            }
+        };
+#pragma unroll
+        for (int a = 0; a < CH; ++a)
+#pragma unroll
+            for (int b = 0; b < CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < (NB ? CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 px[G::K];
+        xload(0, px);
+        for (int64_t u = 0;; ++u) {
+            const int64_t t = u * NC + cons;
+            const int64_t tile = sc.first + t * sc.stride;
+            if (tile >= tend) break;
+            // x to this consumer's LDS tile; its scale from the lane values
+            uint32_t mx = 0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) {
+                st4(xt + LY::tix(G::RPI * k + rl, fg), px[k]);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) mx = max(mx, __float_as_uint(fabsf(px[k][c])));
+            }
+            const int xexp = lg_f16_scale_exp_c(lg_wave_max_bits(mx));
+            xload(u + 1, px);  // the next tile's x block in flight under this tile's work
+            const int sl = static_cast<int>(t % R);
+            pc_wait(&ready[prod], static_cast<uint32_t>(t + 1));
+            float* slot = ring + sl * LY::TILE;
+            const uint32_t* m = meta + 4 * (prod * R + sl);
+            const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
+                           nb = __builtin_amdgcn_readfirstlane(m[2]);
+            const int texp = static_cast<int>(__builtin_amdgcn_readfirstlane(m[3]));
+            const float tsc = lg_pow2f(texp), xsc = lg_pow2f(xexp);
+            wave_sync_nm();
+            // dW += t^T x: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
+            {
+                lg_f16x4 xb[CH][2];
+#pragma unroll
+                for (int ni = 0; ni < CH; ++ni) {
+                    f32x4 v;
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const int r = 4 * q + kk, c = 16 * ni + j;
+                        v[kk] = xt[LY::tix(r, c >> 2) + (c & 3)] * xsc;
+                    }
+                    split2_f16_x4(v, xb[ni][0], xb[ni][1]);
+                }
+                const float us = lg_pow2f(-(texp + xexp));
+#pragma unroll
+                for (int mo = 0; mo < CH; ++mo) {
+                    f32x4 v;
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const int r = 4 * q + kk, c = 16 * mo + j;
+                        v[kk] = slot[LY::tix(r, c >> 2) + (c & 3)] * tsc;
+                    }
+                    lg_f16x4 a0, a1;
+                    split2_f16_x4(v, a0, a1);
+                    f32x4 c[CH];
+#pragma unroll
+                    for (int ni = 0; ni < CH; ++ni) {
+                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, xb[ni][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][1], c[ni], 0, 0, 0);
+                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][0], c[ni], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int ni = 0; ni < CH; ++ni)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg) dw[mo][ni][reg] = fmaf(c[ni][reg], us, dw[mo][ni][reg]);
+                }
+            }
+            // dx^T[i][row] = sum_o W^T[i][o] t[row][o]: B fragment = t row j, columns 32 s2 + 8 q ..
+            f32x4 o[CH];
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // W's fragments are loop-invariant LDS reads: an opaque zero offset keeps the compiler
+            // from hoisting all 16 of them (64 VGPRs) out of the tile loop
+            int wz = 0;
+            asm volatile("" : "+v"(wz));
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                lg_f16x8 b0f, b1f;
+                split2_f16_x8(ld4(slot + LY::tix(j, 8 * s2 + 2 * q)) * tsc, ld4(slot + LY::tix(j, 8 * s2 + 2 * q + 1)) * tsc,
+                              b0f, b1f);
+#pragma unroll
+                for (int mt = 0; mt < CH; ++mt) {
+                    const lg_f16x8 a0 = *reinterpret_cast<const lg_f16x8*>(wfr + 4 * ((0 * CH * KS + mt * KS + s2) * 64 + lane) + wz);
+                    const lg_f16x8 a1 = *reinterpret_cast<const lg_f16x8*>(wfr + 4 * ((1 * CH * KS + mt * KS + s2) * 64 + lane) + wz);
+                    o[mt] = mfma_h(a1, b0f, o[mt]);
+                    o[mt] = mfma_h(a0, b1f, o[mt]);
+                    o[mt] = mfma_h(a0, b0f, o[mt]);
+                }
+            }
+            const float ux = lg_pow2f(-(wexp + texp));
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt) {
+                o[mt] *= ux;
+                if (mask_out) {
+                    const f32x4 xm = ld4(xt + LY::tix(j, 4 * mt + q));
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
+                }
+            }
+            if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
+                if (node_slot[n] < 0)
+#pragma unroll
+                    for (int mt = 0; mt < CH; ++mt) nbacc[mt] += o[mt];
+            }
+            // dx back through the slot (this wave's slot reads above are older LDS operations)
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt) st4(slot + LY::tix(j, 4 * mt + q), o[mt]);
+            wave_sync_nm();
+            const uint32_t ob = (n * B + b0) * (4u * D);
+            f32x4 vk[G::K];
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) vk[k] = ld4(slot + LY::tix(G::RPI * k + rl, fg));
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) {
+                const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                       dxs, lk, ob, 0);
+            }
+            lg_store_guard(vk);
+            wave_sync_nm();
+            pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));
+        }
+    }
+    // ---- per-block reduction of dW / db / node bias (fixed wave order -> deterministic)
+    if (!producer && NB) {
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+            for (int mt = 0; mt < CH; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
+    }
+    if (producer) {
+#pragma unroll
+        for (int off = G::LPR; off < 64; off <<= 1)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
+    }
+    __syncthreads();
+    constexpr int L = LY::L;
+    float* red = lds;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
+    for (int wv2 = 0; wv2 < NW; ++wv2) {
+        __syncthreads();
+        if (wave == wv2) {
+            if (producer) {
+                if (lane < G::LPR)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
+            } else {
+#pragma unroll
+                for (int mo = 0; mo < CH; ++mo)
+#pragma unroll
+                    for (int ni = 0; ni < CH; ++ni)
+#pragma unroll
+                        for (int reg = 0; reg < 4; ++reg) red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
+                if (NB && j == 0)
+#pragma unroll
+                    for (int mt = 0; mt < CH; ++mt)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
+            }
         }
     }
     __syncthreads();
@@ -2614,6 +3203,11 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
     const bool bf = (flags & LG_F_BF16) != 0;
+    // fp32 tier, default: k_gcn_bwd_nm3 on the 3-way bf16 split (fastest measured,
+    // profiles/r03/r03u).  Lab variants: LG_F_F16X2 the 2-way fp16 split in nm3 (spills at
+    // 256 VGPRs), LG_F_PC | LG_F_F16X2 the producer / consumer kernel k_gcn_bwd_pc (D = 64)
+    const bool f16 = !bf && (flags & LG_F_F16X2);
+    const bool pcb = f16 && (flags & LG_F_PC);
     int grid = 1;
     // B == 0 still runs one (empty) launch so the slab holds zeros
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
@@ -2626,9 +3220,22 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
                                                      static_cast<uint32_t>(N), static_cast<uint32_t>(B),           \
                                                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
                                                      scale_out);                                                   \
+        } else if (DD == 64 && pcb && (!MI || mbits)) {                                                          \
+            auto kern = k_gcn_bwd_pc<MI, NBB>;                                                                     \
+            const size_t dynp = BpcLds::BYTES;                                                                     \
+            grid = std::min<int>(nm_grid(kern, 64 * kBpcProd * (1 + kBpcCons), dynp, std::max<int64_t>(ntiles, 1),  \
+                                         kBpcProd, 1),                                                             \
+                                 2 * lg_num_cus());                                                                \
+            lg_launch(kern, grid, 64 * kBpcProd * (1 + kBpcCons), dynp, s, nodetab_t, pr, dy, x, W, node_slot,     \
+                      dx_out, slab, static_cast<uint32_t>(N), static_cast<uint32_t>(B),                            \
+                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in, scale_out, ymask);                   \
         } else {                                                                                                   \
-            auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>) \
-                                      : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>);   \
+            auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI>                                   \
+                                            : (f16 ? k_gcn_bwd_nm3<DD, MI, NBB, false, MI, true>                     \
+                                                   : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>))                          \
+                                      : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true>                                       \
+                                            : (f16 ? k_gcn_bwd_nm3<DD, MI, NBB, false, false, true>                  \
+                                                   : k_gcn_bwd_nm3<DD, MI, NBB, false>));                             \
             const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                             \
             grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
                                          2),                                                                       \

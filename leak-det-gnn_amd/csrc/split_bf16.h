@@ -157,3 +157,21 @@ __device__ __forceinline__ uint32_t lg_wave_max_bits(uint32_t m) {
     const uint32_t r2 = __builtin_amdgcn_readlane(m, 32), r3 = __builtin_amdgcn_readlane(m, 48);
     return max(max(r0, r1), max(r2, r3));
 }
+
+typedef _Float16 lg_f16x4 __attribute__((ext_vector_type(4)));
+// 4 floats -> two f16x4 parts (hi, lo) of the f16x2 split
+__device__ __forceinline__ void split2_f16_x4(const f32x4& u, lg_f16x4& f0, lg_f16x4& f1) {
+    uint32_t a0, a1, b0, b1;
+    split2_f16_pair(u[0], u[1], a0, a1);
+    split2_f16_pair(u[2], u[3], b0, b1);
+    f0 = __builtin_bit_cast(lg_f16x4, lg_u32x2{a0, b0});
+    f1 = __builtin_bit_cast(lg_f16x4, lg_u32x2{a1, b1});
+}
+// the f16x2 scale exponent of a block clamped to [-63, 63], so that the sum of two block
+// exponents (a product's unscale) stays a normal power of two.  Blocks with max |v| < 2^-49
+// keep less relative precision, blocks above 2^79 would overflow f16: neither occurs in the
+// GCN's activations or gradients.
+__device__ __forceinline__ int lg_f16_scale_exp_c(uint32_t mbits) {
+    const int e = lg_f16_scale_exp(mbits);
+    return e < -63 ? -63 : (e > 63 ? 63 : e);
+}

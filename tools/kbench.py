@@ -193,7 +193,12 @@ def main():
     for name, fl, nbias in (("gcn_bwd_nm", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
                             ("gcn_bwd_nm_y", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
                             ("gcn_bwd_nm_old", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, False),
+                            ("gcn_bwd_nm_nm3f16", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_F16X2, False),
+                            ("gcn_bwd_nm_pc", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC,
+                             False),
                             ("gcn_bwd_nm_l0", nat.LG_F_MASK_OUT, True),
+                            ("gcn_bwd_nm_l0_nm3f16", nat.LG_F_MASK_OUT | nat.LG_F_F16X2, True),
+                            ("gcn_bwd_nm_l0_pc", nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC, True),
                             ("gcn_bwd_nm_l0_old", nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, True)):
         if name not in which:
             continue
@@ -207,7 +212,7 @@ def main():
         dnb = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
         bits = None
-        if name == "gcn_bwd_nm":  # the mask bits of yy = dropout(relu(layer(x))) from the forward
+        if name in ("gcn_bwd_nm", "gcn_bwd_nm_nm3f16", "gcn_bwd_nm_pc"):  # the mask bits of yy = dropout(relu(layer(x))) from the forward
             bits = torch.empty(N * ((B + 15) // 16) * 64, device=dev, dtype=torch.int16)
             check(lib.lg_gcn_fwd_nm_bits(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias), ptr(yy), B,
                                          N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT, 0.1, 123, 2,
