@@ -426,10 +426,12 @@ def c5_leg(dev, iters: int = 20) -> dict:
     return {"metric": "GCNConv fwd / bwd on one synthetic 100k-node / 300k-edge-column graph (BASELINE configs[4])",
             "nodes": N, "edge_columns": int(ei.shape[1]), "feat": D, "windows": 1, "scaling": "replicas only",
             "path": "models.gcn.GCNConv (lg_gcn_fwd / lg_gcn_bwd, window-major = node order at B = 1)",
-            "roofline": {"kernel": "lg_gcn_fwd (K5+K6+K7 fused)", "bound": "hbm", "achieved": round(fg, 1),
+            "roofline": {"kernel": "lg_gcn_fwd -> k_gcn_fwd (K5+K6+K7 fused)", "bound": "hbm",
+                         "achieved": round(fg, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fg / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
-            "roofline_bwd": {"kernel": "lg_gcn_bwd (dx, dW, db)", "bound": "hbm", "achieved": round(bg, 1),
+            "roofline_bwd": {"kernel": "lg_gcn_bwd -> k_gcn_bwd (dx, dW, db)", "bound": "hbm",
+                             "achieved": round(bg, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bg / HBM_PEAK_GBS, 4),
                              "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2)}}
 
@@ -813,7 +815,7 @@ def main() -> None:
         out["c4"] = c4
     if c5 is not None:
         if pmc:
-            tr = pmc_traffic("c5_fwd", "k_gcn_fwd", 1)
+            tr = pmc_traffic("c5_fwd_wm", "k_gcn_fwd<", 1)
             out_c5 = c5["roofline"]
             out_c5["traffic"] = round(tr["bytes"]) if tr else None
             out_c5["traffic_source"] = src if tr else None

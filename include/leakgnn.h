@@ -371,6 +371,21 @@ int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const f
                        int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream,
                        const uint16_t* ymask);
 
+/* Single graph (B = 1) on the node tables (ABI 18): the GCNConv module's own call shape,
+ * x [N][D] (BASELINE configs[4], one 100k-node graph).  Replaces: PyG GCNConv.forward
+ * (detector.py:163,199 — lin, propagate, bias) and its autograd backward for ONE graph.
+ * Tiles of 16 nodes in the table's schedule order; transform and dx on the 3-way bf16
+ * split (fp32-level, ~1e-7 of scale), not bit-identical to lg_gcn_fwd / lg_gcn_bwd.
+ *   lg_gcn_fwd_rows: y = Ahat x W^T (+ b with LG_F_BIAS; no other flags).
+ *   lg_gcn_bwd_rows: t = Ahat^T dy; dx = t W; dW = t^T x; db = sum_rows dy (db may be NULL);
+ *     workspace lg_gcn_bwd_nm_workspace_bytes(D).
+ * D = 64 only (LG_EUNSUPPORTED otherwise: use lg_gcn_fwd / lg_gcn_bwd). */
+int lg_gcn_fwd_rows(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W, const float* bias,
+                    float* y, int64_t N, int64_t D, int flags, lg_stream_t stream);
+int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* x,
+                    const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace,
+                    lg_stream_t stream);
+
 /* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
  * weights; no transform).  Used for the HBM-roofline stress case (config C5). */
 int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,

@@ -2919,6 +2919,378 @@ k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
 }
 
+// ------------------------------------------------------------------ single graph (B = 1), row tiles
+// GCNConv on ONE graph (the reference module's own call shape, x [N][D]; BASELINE configs[4]:
+// 100k nodes, 300k edge columns).  The node-major kernels tile one node x 16 windows and
+// share the node's neighbour list across the tile; at B = 1 a tile is 16 NODES (16
+// consecutive slots of the node table's schedule section, RCM order), each with its own
+// neighbour list.  Lane (rl, fg) owns features 4 fg.. of tile rows 4 k + rl (D = 64: the 16
+// lanes of a DPP row cover one node row).  Per tile:
+//   * the 16 records are ONE coalesced vector load (lane fg of a row holds word fg of its
+//     node's 64-byte record), requested a tile ahead; e0, e1, the six inline (col, w) pairs,
+//     self and node are broadcast inside each 16-lane row by DPP row_newbcast (VALU, no
+//     LDS, no scalar round trip per row);
+//   * all inline neighbour rows of the 16 nodes are in flight at once (buffer loads, an
+//     absent neighbour through a zero-record descriptor), entries beyond six from the pair
+//     array afterwards;
+//   * the tile goes through LDS (XOR swizzle) to the MFMA transform on the 3-way bf16 split
+//     (W's parts in LDS in fragment order: one conflict-free ds_read_b128 per fragment), and
+//     rows go back out whole through the same LDS tile.
+// The window-major kernel (k_gcn_fwd) it replaces at B = 1 walked rowptr -> col -> row as
+// three dependent global round trips per round of two neighbours (profiles/r03: 0.25 of
+// HBM peak at C5).
+constexpr int kRowWaves = 4;
+#ifndef LG_ROWS_FWD_NB
+#define LG_ROWS_FWD_NB 3  // inline neighbours per gather batch (x 4 rows per lane)
+#endif
+#ifndef LG_ROWS_BWD_NB
+#define LG_ROWS_BWD_NB 3
+#endif
+
+template <int n>
+__device__ __forceinline__ int row_bcast(int v) {  // lane n of each 16-lane row, to the row
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + n, 0xF, 0xF, false);
+}
+
+struct RowsLds {  // floats
+    static constexpr int D = 64, CH = 4, KS = 2;
+    static constexpr int WFR = 3 * CH * KS * 64 * 4;   // W (fwd) or W^T (bwd) bf16 split parts, fragment order
+    static constexpr int BOFF = WFR;                    // bias [D]
+    static constexpr int TOFF = BOFF + D;               // per wave: tile (fwd) / t tile + x tile (bwd)
+    static constexpr int TILE = 16 * D;
+    static constexpr int L = D * D + 2 * D;
+    static constexpr size_t fwd_bytes() { return 4 * static_cast<size_t>(TOFF + kRowWaves * TILE); }
+    static constexpr size_t bwd_bytes() {
+        return 4 * static_cast<size_t>(TOFF + 2 * kRowWaves * TILE > L ? TOFF + 2 * kRowWaves * TILE : L);
+    }
+    static __device__ __forceinline__ int tix(int r, int c) { return r * D + 4 * (c ^ r); }
+};
+
+// The 3-way bf16 split of M (TRANS: of M^T) into fragment order: fragment (part, mt, s2),
+// lane (j, q) holds A[i = 16 mt + j][k = 32 s2 + 8 q + e], A = M or M^T, M [D][D] row-major.
+template <bool TRANS>
+__device__ __forceinline__ void stage_frag3(uint32_t* wfr, const float* __restrict__ M, int nthreads) {
+    constexpr int D = 64, CH = 4, KS = 2;
+    for (int f = threadIdx.x; f < CH * KS * 64; f += nthreads) {
+        const int l = f & 63, ms = f >> 6, mt = ms / KS, s2 = ms % KS;
+        const int i = 16 * mt + (l & 15), k0 = 32 * s2 + 8 * (l >> 4);
+        f32x4 u, v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            u[e] = TRANS ? M[(k0 + e) * D + i] : M[i * D + k0 + e];
+            v[e] = TRANS ? M[(k0 + 4 + e) * D + i] : M[i * D + k0 + 4 + e];
+        }
+        lg_bf16x8 f0, f1, f2;
+        split3_x8(u, v, f0, f1, f2);
+        *reinterpret_cast<lg_bf16x8*>(wfr + 4 * ((0 * CH * KS + ms) * 64 + l)) = f0;
+        *reinterpret_cast<lg_bf16x8*>(wfr + 4 * ((1 * CH * KS + ms) * 64 + l)) = f1;
+        *reinterpret_cast<lg_bf16x8*>(wfr + 4 * ((2 * CH * KS + ms) * 64 + l)) = f2;
+    }
+}
+
+// dst^T (16 rows x 64) = A (from the fragments) x tile^T, tile rows j: o[mt] = rows j,
+// columns 16 mt + 4 q .. (the fwd transform with A = W, the bwd dx with A = W^T)
+__device__ __forceinline__ void rows_transform(const uint32_t* wfr, const float* tl, int lane, f32x4 (&o)[4]) {
+    using LY = RowsLds;
+    constexpr int CH = 4, KS = 2;
+    const int j = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+        lg_bf16x8 b[3];
+        split3_x8(ld4(tl + LY::tix(j, 8 * s2 + 2 * q)), ld4(tl + LY::tix(j, 8 * s2 + 2 * q + 1)), b[0], b[1], b[2]);
+#pragma unroll
+        for (int mt = 0; mt < CH; ++mt) {
+            lg_bf16x8 a[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const lg_bf16x8*>(wfr + 4 * ((p * CH * KS + mt * KS + s2) * 64 + lane));
+            o[mt] = mfma_split(a, b, o[mt]);
+        }
+    }
+}
+
+// One tile's records (lane fg: word fg of row 4 k + rl's record) and their decoding
+struct RowsRec {
+    int e0[4], e1[4], self[4], node[4];
+    int col[4][kLgNmInline];
+    float w[4][kLgNmInline];
+};
+__device__ __forceinline__ void rows_decode(const int (&rw)[4], RowsRec& r) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        r.e0[k] = row_bcast<0>(rw[k]);
+        r.e1[k] = row_bcast<1>(rw[k]);
+        r.col[k][0] = row_bcast<2>(rw[k]);
+        r.w[k][0] = __int_as_float(row_bcast<3>(rw[k]));
+        r.col[k][1] = row_bcast<4>(rw[k]);
+        r.w[k][1] = __int_as_float(row_bcast<5>(rw[k]));
+        r.col[k][2] = row_bcast<6>(rw[k]);
+        r.w[k][2] = __int_as_float(row_bcast<7>(rw[k]));
+        r.col[k][3] = row_bcast<8>(rw[k]);
+        r.w[k][3] = __int_as_float(row_bcast<9>(rw[k]));
+        r.col[k][4] = row_bcast<10>(rw[k]);
+        r.w[k][4] = __int_as_float(row_bcast<11>(rw[k]));
+        r.col[k][5] = row_bcast<12>(rw[k]);
+        r.w[k][5] = __int_as_float(row_bcast<13>(rw[k]));
+        r.self[k] = row_bcast<14>(rw[k]);
+        r.node[k] = row_bcast<15>(rw[k]);
+    }
+}
+// record words of tile `tile` (slots 16 tile + 4 k + rl; past N: an empty row)
+__device__ __forceinline__ void rows_load_rec(const int32_t* __restrict__ tab, uint32_t N, int64_t tile, int lane,
+                                              int (&rw)[4]) {
+    const int rl = lane >> 4, fg = lane & 15;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t slot = 16 * tile + 4 * k + rl;
+        rw[k] = slot < N ? tab[16 * (static_cast<int64_t>(N) + slot) + fg] : 0;
+    }
+}
+// acc[k] = sum over row 4k + rl's entries (CSR order) of w * src[col] (features 4 fg..); own[k]
+// = the row's own src row (from its self entry, else loaded) when OWN
+template <bool OWN, int NBATCH>
+__device__ __forceinline__ void rows_gather(const RowsRec& r, const int2* __restrict__ pairs, __amdgpu_buffer_rsrc_t src,
+                                            __amdgpu_buffer_rsrc_t src0, int lane, f32x4 (&acc)[4], f32x4 (&own)[4]) {
+    constexpr int D = 64;
+    const uint32_t lo = 16u * static_cast<uint32_t>(lane & 15);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (OWN) own[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    int maxd = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) maxd = max(maxd, r.e1[k] - r.e0[k]);
+    // inline entries in batches of NBATCH x 4 rows in flight; a batch no row reaches is skipped
+#pragma unroll
+    for (int i0 = 0; i0 < kLgNmInline; i0 += NBATCH) {
+        if (__builtin_amdgcn_ballot_w64(maxd > i0) == 0) break;
+        f32x4 v[4][NBATCH];
+#pragma unroll
+        for (int i = 0; i < NBATCH; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool have = i0 + i < kLgNmInline && r.e0[k] + i0 + i < r.e1[k];
+                const uint32_t base = have ? static_cast<uint32_t>(r.col[k][i0 + i < kLgNmInline ? i0 + i : 0]) * (4u * D) : 0u;
+                v[k][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(have ? src : src0, lo, base, 0));
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int i = 0; i < NBATCH; ++i) {
+                if (i0 + i >= kLgNmInline) continue;
+                pk_fma4(acc[k], r.e0[k] + i0 + i < r.e1[k] ? r.w[k][i0 + i] : 0.f, v[k][i]);  // absent: 0 x 0
+                if (OWN && i0 + i == r.self[k]) own[k] = v[k][i];
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        for (int e = r.e0[k] + kLgNmInline; e < r.e1[k]; ++e) {  // per-row tail (degree > 6)
+            const int2 pa = pairs[e];
+            const f32x4 t = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo, static_cast<uint32_t>(pa.x) * (4u * D), 0));
+            pk_fma4(acc[k], __int_as_float(pa.y), t);
+        }
+        if (OWN && (r.self[k] < 0) && r.e0[k] < r.e1[k])  // self entry past the inline six
+            own[k] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo, static_cast<uint32_t>(r.node[k]) * (4u * D), 0));
+    }
+}
+
+template <bool BIAS>
+__global__ void __launch_bounds__(64 * kRowWaves)
+k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
+               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N) {
+    constexpr int D = 64;
+    using LY = RowsLds;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    uint32_t* wfr = reinterpret_cast<uint32_t*>(lds);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4, rl = lane >> 4, fg = lane & 15;
+    float* tl = lds + LY::TOFF + wave * LY::TILE;
+    const int64_t ntiles = (static_cast<int64_t>(N) + 15) / 16;
+    const NmSched sc = nm_sched(ntiles, wave, kRowWaves);
+    const uint64_t bytes = static_cast<uint64_t>(N) * (4u * D);
+    const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), xs0 = nm_rsrc(x, 0), ys = nm_rsrc(y, bytes);
+    int rw[4];
+    rows_load_rec(tab, N, sc.first < sc.end ? sc.first : 0, lane, rw);
+    stage_frag3<false>(wfr, W, 64 * kRowWaves);
+    if (threadIdx.x < D) lds[LY::BOFF + threadIdx.x] = BIAS ? bias[threadIdx.x] : 0.f;
+    __syncthreads();
+    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
+        RowsRec r;
+        rows_decode(rw, r);
+        rows_load_rec(tab, N, tile + sc.stride < sc.end ? tile + sc.stride : tile, lane, rw);  // next tile's records
+        f32x4 acc[4], own[4];
+        rows_gather<false, LG_ROWS_FWD_NB>(r, pairs, xs, xs0, lane, acc, own);
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st4(tl + LY::tix(4 * k + rl, fg), acc[k]);
+        wave_sync_nm();
+        f32x4 o[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) o[mt] = ld4(lds + LY::BOFF + 16 * mt + 4 * q);
+        rows_transform(wfr, tl, lane, o);
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
+        wave_sync_nm();
+        f32x4 vk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vk[k] = ld4(tl + LY::tix(4 * k + rl, fg));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool valid = 16 * tile + 4 * k + rl < N;
+            const uint32_t off = valid ? static_cast<uint32_t>(r.node[k]) * (4u * D) + 16u * fg : kNm3RowOob;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                   ys, off, 0, 0);
+        }
+        lg_store_guard(vk);
+    }
+}
+
+// Backward on one graph: t = Ahat^T dy (transposed table), dx = t W, dW += t^T x, db += the
+// rows' own dy; dW / db per workgroup in a fixed wave order into the slab row.
+__global__ void __launch_bounds__(64 * kRowWaves, 2)
+k_gcn_bwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
+               const float* __restrict__ x, const float* __restrict__ W, float* __restrict__ dxo,
+               float* __restrict__ slab, uint32_t N) {
+    constexpr int D = 64;
+    using LY = RowsLds;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    uint32_t* wfr = reinterpret_cast<uint32_t*>(lds);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4, rl = lane >> 4, fg = lane & 15;
+    float* tl = lds + LY::TOFF + 2 * wave * LY::TILE;
+    float* xl = tl + LY::TILE;
+    const int64_t ntiles = (static_cast<int64_t>(N) + 15) / 16;
+    const NmSched sc = nm_sched(ntiles, wave, kRowWaves);
+    const uint64_t bytes = static_cast<uint64_t>(N) * (4u * D);
+    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), dys0 = nm_rsrc(dy, 0), xs = nm_rsrc(x, bytes),
+                                 dxs = nm_rsrc(dxo, bytes);
+    int rw[4];
+    rows_load_rec(tab, N, sc.first < sc.end ? sc.first : 0, lane, rw);
+    stage_frag3<true>(wfr, W, 64 * kRowWaves);
+    __syncthreads();
+    f32x4 dw[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
+        RowsRec r;
+        rows_decode(rw, r);
+        rows_load_rec(tab, N, tile + sc.stride < sc.end ? tile + sc.stride : tile, lane, rw);
+        f32x4 xv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool valid = 16 * tile + 4 * k + rl < N;
+            xv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xs, valid ? static_cast<uint32_t>(r.node[k]) * (4u * D) + 16u * fg : kNm3RowOob,
+                                                  0, 0));
+        }
+        f32x4 acc[4], own[4];
+        rows_gather<true, LG_ROWS_BWD_NB>(r, pairs, dys, dys0, lane, acc, own);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dbacc += own[k];
+        wave_sync_nm();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            st4(tl + LY::tix(4 * k + rl, fg), acc[k]);
+            st4(xl + LY::tix(4 * k + rl, fg), xv[k]);
+        }
+        wave_sync_nm();
+        // dW += t^T x over the tile's 16 rows (K = rows 4q..4q+3), bf16 split, in place
+        {
+            lg_i16x4 xb[4][3];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int rr = 4 * q + kk, c = 16 * ni + j;
+                    v[kk] = xl[LY::tix(rr, c >> 2) + (c & 3)];
+                }
+                lg_u32x2 f0, f1, f2;
+                split3_x4(v, f0, f1, f2);
+                xb[ni][0] = __builtin_bit_cast(lg_i16x4, f0);
+                xb[ni][1] = __builtin_bit_cast(lg_i16x4, f1);
+                xb[ni][2] = __builtin_bit_cast(lg_i16x4, f2);
+            }
+#pragma unroll
+            for (int mo = 0; mo < 4; ++mo) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int rr = 4 * q + kk, c = 16 * mo + j;
+                    v[kk] = tl[LY::tix(rr, c >> 2) + (c & 3)];
+                }
+                lg_u32x2 f0, f1, f2;
+                split3_x4(v, f0, f1, f2);
+                const lg_i16x4 a0 = __builtin_bit_cast(lg_i16x4, f0), a1 = __builtin_bit_cast(lg_i16x4, f1),
+                                a2 = __builtin_bit_cast(lg_i16x4, f2);
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    f32x4 c = dw[mo][ni];
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, xb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, xb[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, xb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][1], c, 0, 0, 0);
+                    dw[mo][ni] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a0, xb[ni][0], c, 0, 0, 0);
+                }
+            }
+        }
+        f32x4 o[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        rows_transform(wfr, tl, lane, o);  // dx^T = W^T t^T
+        wave_sync_nm();
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
+        wave_sync_nm();
+        f32x4 vk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) vk[k] = ld4(tl + LY::tix(4 * k + rl, fg));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const bool valid = 16 * tile + 4 * k + rl < N;
+            const uint32_t off = valid ? static_cast<uint32_t>(r.node[k]) * (4u * D) + 16u * fg : kNm3RowOob;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
+                                                   dxs, off, 0, 0);
+        }
+        lg_store_guard(vk);
+    }
+    // db: fold the 4 row groups (lanes fg, fg + 16, ..), then waves in a fixed order
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
+    __syncthreads();
+    constexpr int L = LY::L;
+    float* red = lds;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
+    for (int wv2 = 0; wv2 < kRowWaves; ++wv2) {
+        __syncthreads();
+        if (wave == wv2) {
+#pragma unroll
+            for (int mo = 0; mo < 4; ++mo)
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
+            if (lane < 16)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
+        }
+    }
+    __syncthreads();
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
+}
+
 template <typename Kern>
 int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int cap_per_cu) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3272,4 +3644,47 @@ extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, c
                              float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
     return lg_gcn_bwd_nm_bits(nodetab_t, pairs_t, dy, y, x, W, dx_out, dW, db, node_slot, dnode_bias, B, N, D, flags,
                               scale_in, scale_out, workspace, stream, nullptr);
+}
+
+extern "C" int lg_gcn_fwd_rows(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
+                               const float* bias, float* y, int64_t N, int64_t D, int flags, lg_stream_t stream) {
+    if (N <= 0 || !nodetab || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
+    if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
+    if (flags & ~LG_F_BIAS) return LG_EUNSUPPORTED;
+    if (D != 64 || !nm_fits(1, N, D)) return LG_EUNSUPPORTED;
+    const int64_t ntiles = (N + 15) / 16;
+    hipStream_t s = lg_stream(stream);
+    const size_t dyn = RowsLds::fwd_bytes();
+    const int2* pr = reinterpret_cast<const int2*>(pairs);
+    if (flags & LG_F_BIAS) {
+        auto kern = k_gcn_fwd_rows<true>;
+        const int grid = nm_grid(kern, 64 * kRowWaves, dyn, ntiles, kRowWaves, 4);
+        lg_launch(kern, grid, 64 * kRowWaves, dyn, s, nodetab, pr, x, W, bias, y, static_cast<uint32_t>(N));
+    } else {
+        auto kern = k_gcn_fwd_rows<false>;
+        const int grid = nm_grid(kern, 64 * kRowWaves, dyn, ntiles, kRowWaves, 4);
+        lg_launch(kern, grid, 64 * kRowWaves, dyn, s, nodetab, pr, x, W, bias, y, static_cast<uint32_t>(N));
+    }
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* x,
+                               const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace,
+                               lg_stream_t stream) {
+    if (N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx || !dW || !workspace) return LG_EINVAL;
+    if (D != 64 || !nm_fits(1, N, D)) return LG_EUNSUPPORTED;
+    const int64_t ntiles = (N + 15) / 16;
+    hipStream_t s = lg_stream(stream);
+    const size_t dyn = RowsLds::bwd_bytes();
+    auto kern = k_gcn_bwd_rows;
+    // the slab holds lg_gcn_bwd_nm_workspace_bytes(D) / (4 L) = 2 x CUs rows
+    const int grid = std::min<int>(nm_grid(kern, 64 * kRowWaves, dyn, ntiles, kRowWaves, 2), 2 * lg_num_cus());
+    float* slab = static_cast<float*>(workspace);
+    lg_launch(kern, grid, 64 * kRowWaves, dyn, s, nodetab_t, reinterpret_cast<const int2*>(pairs_t), dy, x, W, dx, slab,
+              static_cast<uint32_t>(N));
+    LG_RET_IF_LAUNCH_FAILED();
+    const int64_t L = D * D + 2 * D;
+    const LgSlabSeg segs[2] = {{0, D * D, dW}, {D * D, D, db}};
+    return lg_launch_slab_reduce_multi(slab, grid, L, segs, 2, nullptr, nullptr, s);
 }

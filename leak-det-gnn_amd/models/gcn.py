@@ -11,9 +11,10 @@ reference; the semantics restated here are PyG 2.x's published ones:
      forward(x, edge_index) = propagate(gcn_norm(edge_index), lin(x)) + bias
   global_mean_pool(x, batch, size=None) = scatter(x, batch, reduce='mean')
 
-Here forward runs the registered op leakgnn::gcn_conv (models/library.py: the fused
-HIP kernel lg_gcn_fwd, (Ahat x) W^T + b in one launch) and its autograd formula
-leakgnn::gcn_conv_backward (lg_gcn_bwd).  The gcn_norm'ed CSR is built on the device
+Here forward runs the registered op leakgnn::gcn_conv (models/library.py: one fused HIP
+launch of (Ahat x) W^T + b — lg_gcn_fwd_rows, 16-node tiles off the node table, at D = 64;
+lg_gcn_fwd at D = 32) and its autograd formula leakgnn::gcn_conv_backward
+(lg_gcn_bwd_rows / lg_gcn_bwd).  The gcn_norm'ed CSR is built on the device
 (lg_graph_build) and, unlike PyG with cached=False, re-used while an edge_index
 with the SAME CONTENT is passed again — the graph is a pure function of edge_index,
 so results are unchanged.  The same tensor object at the same version counter is a
@@ -101,7 +102,7 @@ class GCNConv(nn.Module):
             raise NotImplementedError("edge_weight is not used on the Leak-det-gnn path")
         g = self.graph_for(edge_index, x.size(0), x.device)
         return torch.ops.leakgnn.gcn_conv(_f32(x), _f32(self.lin.weight), _f32(self.bias), g.rowptr, g.col, g.w,
-                                          g.rowptr_t, g.col_t, g.w_t)
+                                          g.rowptr_t, g.col_t, g.w_t, g.nodetab, g.pairs, g.nodetab_t, g.pairs_t)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"

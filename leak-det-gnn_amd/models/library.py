@@ -58,11 +58,18 @@ def _c(t: Optional[Tensor]) -> Optional[Tensor]:
 
 
 # ============================================================================ gcn_conv
+# GCNConv's single-graph kernels: False = window-major lg_gcn_fwd / lg_gcn_bwd (exact fp32,
+# the default), True = the node-table row tiles lg_gcn_{fwd,bwd}_rows (D = 64; same speed at C5)
+_ROWS = False
+
 @torch.library.custom_op(f"{NS}::gcn_conv", mutates_args=(), device_types="cuda")
 def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, col: Tensor, w: Tensor,
-             rowptr_t: Tensor, col_t: Tensor, w_t: Tensor) -> Tensor:
-    """y = Ahat (x W^T) + b on one graph (lg_gcn_fwd, B = 1).  (rowptr, col, w): the
-    gcn_norm'ed CSR of lg_graph_build; the transposed CSR is the backward's."""
+             rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, nodetab: Tensor, pairs: Tensor, nodetab_t: Tensor,
+             pairs_t: Tensor) -> Tensor:
+    """y = Ahat (x W^T) + b on one graph: lg_gcn_fwd (B = 1, exact fp32 MFMA).  (rowptr, col,
+    w): the gcn_norm'ed CSR of lg_graph_build; nodetab / pairs: its node table (GCNGraph),
+    for the row-tile kernels (lg_gcn_fwd_rows, `rows=True`; measured no faster at C5:
+    27.7 vs 26.8 us forward, 48.5 vs 50.0 us backward, profiles/r03/r03x)."""
     lib = load_library()
     x, weight, bias = _c(x), _c(weight), _c(bias)
     _req(x, weight, bias)
@@ -73,20 +80,25 @@ def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, 
     y = torch.empty_like(x)
     flags = nat.LG_F_BIAS if bias is not None else 0
     with _timed("gcn_fwd", x.device):
-        check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(x), ptr(weight), ptr(bias), ptr(y), 1, Ntot, D,
-                             col.numel(), flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
+        if D == 64 and _ROWS:
+            check(lib.lg_gcn_fwd_rows(ptr(nodetab), ptr(pairs), ptr(x), ptr(weight), ptr(bias), ptr(y), Ntot, D, flags,
+                                      stream_of(x)), "lg_gcn_fwd_rows")
+        else:
+            check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(x), ptr(weight), ptr(bias), ptr(y), 1, Ntot, D,
+                                 col.numel(), flags, 0.0, 0, 0, stream_of(x)), "lg_gcn_fwd")
     return y
 
 
 @gcn_conv.register_fake
-def _(x, weight, bias, rowptr, col, w, rowptr_t, col_t, w_t):
+def _(x, weight, bias, rowptr, col, w, rowptr_t, col_t, w_t, nodetab, pairs, nodetab_t, pairs_t):
     return torch.empty_like(x)
 
 
 @torch.library.custom_op(f"{NS}::gcn_conv_backward", mutates_args=(), device_types="cuda")
 def gcn_conv_backward(dy: Tensor, x: Tensor, weight: Tensor, rowptr_t: Tensor, col_t: Tensor,
-                      w_t: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
-    """(dx, dW, db) of gcn_conv (lg_gcn_bwd over the transposed CSR)."""
+                      w_t: Tensor, nodetab_t: Tensor, pairs_t: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """(dx, dW, db) of gcn_conv (lg_gcn_bwd over the transposed CSR; lg_gcn_bwd_rows over the
+    transposed node table when the row-tile kernels are selected)."""
     lib = load_library()
     dy, x, weight = _c(dy), _c(x), _c(weight)
     _req(dy, x, weight)
@@ -94,29 +106,34 @@ def gcn_conv_backward(dy: Tensor, x: Tensor, weight: Tensor, rowptr_t: Tensor, c
     dx = torch.empty_like(x)
     dW = torch.empty_like(weight)
     db = torch.empty(D, device=x.device, dtype=x.dtype)
-    ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
     with _timed("gcn_bwd", x.device):
-        check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), None, ptr(x), ptr(weight), ptr(dx),
-                             ptr(dW), ptr(db), None, None, 1, Ntot, D, col_t.numel(), 0, 1.0, 1.0, ptr(ws),
-                             stream_of(x)), "lg_gcn_bwd")
+        if D == 64 and _ROWS:
+            ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
+            check(lib.lg_gcn_bwd_rows(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(x), ptr(weight), ptr(dx), ptr(dW),
+                                      ptr(db), Ntot, D, ptr(ws), stream_of(x)), "lg_gcn_bwd_rows")
+        else:
+            ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
+            check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), None, ptr(x), ptr(weight), ptr(dx),
+                                 ptr(dW), ptr(db), None, None, 1, Ntot, D, col_t.numel(), 0, 1.0, 1.0, ptr(ws),
+                                 stream_of(x)), "lg_gcn_bwd")
     return dx, dW, db
 
 
 @gcn_conv_backward.register_fake
-def _(dy, x, weight, rowptr_t, col_t, w_t):
+def _(dy, x, weight, rowptr_t, col_t, w_t, nodetab_t, pairs_t):
     return torch.empty_like(x), torch.empty_like(weight), x.new_empty(x.shape[1])
 
 
 def _gcn_conv_setup(ctx, inputs, output):
-    x, weight, bias, _, _, _, rowptr_t, col_t, w_t = inputs
+    x, weight, bias, _, _, _, rowptr_t, col_t, w_t, _, _, nodetab_t, pairs_t = inputs
     ctx.has_bias = bias is not None
-    ctx.save_for_backward(x, weight, rowptr_t, col_t, w_t)
+    ctx.save_for_backward(x, weight, rowptr_t, col_t, w_t, nodetab_t, pairs_t)
 
 
 def _gcn_conv_bwd(ctx, dy):
-    x, weight, rowptr_t, col_t, w_t = ctx.saved_tensors
-    dx, dW, db = torch.ops.leakgnn.gcn_conv_backward(dy, x, weight, rowptr_t, col_t, w_t)
-    return dx, dW, (db if ctx.has_bias else None), None, None, None, None, None, None
+    x, weight, rowptr_t, col_t, w_t, nodetab_t, pairs_t = ctx.saved_tensors
+    dx, dW, db = torch.ops.leakgnn.gcn_conv_backward(dy, x, weight, rowptr_t, col_t, w_t, nodetab_t, pairs_t)
+    return (dx, dW, (db if ctx.has_bias else None)) + (None,) * 10
 
 
 gcn_conv.register_autograd(_gcn_conv_bwd, setup_context=_gcn_conv_setup)

@@ -32,8 +32,58 @@ def test_opcheck_gcn_conv_and_mean_pool():
     x = torch.randn(300, 64, device=DEV, requires_grad=True)
     W = torch.randn(64, 64, device=DEV, requires_grad=True)
     b = torch.randn(64, device=DEV, requires_grad=True)
-    _check(torch.ops.leakgnn.gcn_conv.default, (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t))
+    _check(torch.ops.leakgnn.gcn_conv.default, (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t, g.nodetab,
+                                                g.pairs, g.nodetab_t, g.pairs_t))
     _check(torch.ops.leakgnn.mean_pool.default, (torch.randn(4 * 50, 64, device=DEV, requires_grad=True), 4, 50))
+
+
+@pytest.mark.parametrize("N,E,seed", [(661, 1532, 3), (300, 1500, 1), (1000, 400, 2), (17, 0, 4)])
+def test_rows_kernels_match_window_major(N, E, seed):
+    """lg_gcn_fwd_rows / lg_gcn_bwd_rows (the B = 1 GCNConv path at D = 64: 16-node tiles off
+    the node table, 3-way bf16 split) against lg_gcn_fwd / lg_gcn_bwd (exact fp32 MFMA) on
+    the same graph: y, dx, dW, db within 1e-6 of scale.  Random graphs up to degree ~20
+    (entries past the six inline pairs), isolated nodes (E = 400 on 1000 nodes), an edgeless
+    17-node graph (a ragged last tile of one row, self loops only)."""
+    from models import _native as nat
+    from models.ops import GCNGraph, check, ptr, stream_of
+    lib = nat.load_library()
+    gen = torch.Generator().manual_seed(seed)
+    ei = torch.randint(0, N, (2, E), generator=gen)
+    g = GCNGraph.build(ei, N, DEV)
+    D = 64
+    x = torch.randn(N, D, generator=gen).to(DEV)
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    b = torch.randn(D, generator=gen).to(DEV)
+    dy = torch.randn(N, D, generator=gen).to(DEV)
+    st = stream_of(x)
+    for flags in (0, nat.LG_F_BIAS):
+        y0, y1 = torch.empty_like(x), torch.full_like(x, float("nan"))
+        check(lib.lg_gcn_fwd(ptr(g.rowptr), ptr(g.col), ptr(g.w), ptr(x), ptr(W), ptr(b), ptr(y0), 1, N, D,
+                             g.col.numel(), flags, 0.0, 0, 0, st), "fwd")
+        check(lib.lg_gcn_fwd_rows(ptr(g.nodetab), ptr(g.pairs), ptr(x), ptr(W), ptr(b), ptr(y1), N, D, flags, st),
+              "fwd rows")
+        assert_close(y1, y0, rtol=1e-6, atol=0.0, what=f"fwd rows flags={flags}")
+    outs = []
+    for rows in (False, True):
+        dx, dW, db = torch.full_like(x, float("nan")), torch.empty(D, D, device=DEV), torch.empty(D, device=DEV)
+        if rows:
+            ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+            check(lib.lg_gcn_bwd_rows(ptr(g.nodetab_t), ptr(g.pairs_t), ptr(dy), ptr(x), ptr(W), ptr(dx), ptr(dW),
+                                      ptr(db), N, D, ptr(ws), st), "bwd rows")
+        else:
+            ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+            check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), None, ptr(x), ptr(W), ptr(dx),
+                                 ptr(dW), ptr(db), None, None, 1, N, D, g.col_t.numel(), 0, 1.0, 1.0, ptr(ws), st),
+                  "bwd")
+        outs.append((dx, dW, db))
+    for i, what in enumerate(("dx", "dW", "db")):
+        assert_close(outs[1][i], outs[0][i], rtol=1e-6, atol=0.0, what=f"bwd rows {what}")
+    # D = 32 and extra flags are refused (the caller falls back to lg_gcn_fwd)
+    LG_EUNSUPPORTED = -2  # include/leakgnn.h
+    assert lib.lg_gcn_fwd_rows(ptr(g.nodetab), ptr(g.pairs), ptr(x), ptr(W), ptr(b), ptr(y0), N, 32, 0, st) == \
+        LG_EUNSUPPORTED
+    assert lib.lg_gcn_fwd_rows(ptr(g.nodetab), ptr(g.pairs), ptr(x), ptr(W), ptr(b), ptr(y0), N, D,
+                               nat.LG_F_RELU, st) == LG_EUNSUPPORTED
 
 
 def test_opcheck_sensor_proj_and_gru():
@@ -118,7 +168,7 @@ def test_kernel_timer_times_the_kernel():
     x = torch.randn(20000, 64, device=DEV)
     W = torch.randn(64, 64, device=DEV)
     b = torch.randn(64, device=DEV)
-    args = (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t)
+    args = (x, W, b, g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t, g.nodetab, g.pairs, g.nodetab_t, g.pairs_t)
     torch.ops.leakgnn.gcn_conv(*args)
     timer = ops.KernelTimer(["gcn_fwd"])
     ops.set_kernel_timer(timer)

@@ -228,7 +228,7 @@ def main():
         else:
             byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
         res[name] = {"us": t, "GBps": byts / t / 1e3}
-    if "c5_fwd" in which or "c5_bwd" in which:  # BASELINE configs[4]: one 100k-node graph, B = 1, GCNConv's launches
+    if "c5_fwd" in which or "c5_bwd" in which or "c5_fwd_wm" in which:  # BASELINE configs[4]: one 100k-node graph, B = 1, GCNConv's launches
         from models.synth import synthetic_pipe_graph
         ei5, _ = synthetic_pipe_graph(100_000, 150_000, seed=0)
         N5 = 100_000
@@ -236,21 +236,32 @@ def main():
         x5 = torch.randn(N5, D, device=dev)
         y5 = torch.empty_like(x5)
         b5 = 8 * N5 * D + 4 * (N5 + 1) + 8 * (int(ei5.shape[1]) + N5)  # 54.8 MB
-        f = lambda: check(lib.lg_gcn_fwd(ptr(g5.rowptr), ptr(g5.col), ptr(g5.w), ptr(x5), ptr(W), ptr(bias), ptr(y5),
-                                         1, N5, D, g5.col.numel(), nat.LG_F_BIAS, 0.0, 0, 0, cs()), "c5 fwd")
+        # c5_fwd / c5_bwd: the row-tile kernels (lg_gcn_{fwd,bwd}_rows); *_wm: window-major (the product's)
+        f = lambda: check(lib.lg_gcn_fwd_rows(ptr(g5.nodetab), ptr(g5.pairs), ptr(x5), ptr(W), ptr(bias), ptr(y5), N5,
+                                              D, nat.LG_F_BIAS, cs()), "c5 fwd")
+        fwm = lambda: check(lib.lg_gcn_fwd(ptr(g5.rowptr), ptr(g5.col), ptr(g5.w), ptr(x5), ptr(W), ptr(bias), ptr(y5),
+                                           1, N5, D, g5.col.numel(), nat.LG_F_BIAS, 0.0, 0, 0, cs()), "c5 fwd wm")
         if "c5_fwd" in which:
             t = timeit(f, args.iters)
             res["c5_fwd"] = {"us": t, "GBps": b5 / t / 1e3}
+        if "c5_fwd" in which or "c5_fwd_wm" in which:
+            t = timeit(fwm, args.iters)
+            res["c5_fwd_wm"] = {"us": t, "GBps": b5 / t / 1e3}
         if "c5_bwd" in which:
             dy5 = torch.randn_like(x5)
             dx5 = torch.empty_like(x5)
             dW5, db5 = torch.empty(D, D, device=dev), torch.empty(D, device=dev)
             ws5 = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
-            f = lambda: check(lib.lg_gcn_bwd(ptr(g5.rowptr_t), ptr(g5.col_t), ptr(g5.w_t), ptr(dy5), None, ptr(x5),
-                                             ptr(W), ptr(dx5), ptr(dW5), ptr(db5), None, None, 1, N5, D,
-                                             g5.col_t.numel(), 0, 1.0, 1.0, ptr(ws5), cs()), "c5 bwd")
+            wsr = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
+            f = lambda: check(lib.lg_gcn_bwd_rows(ptr(g5.nodetab_t), ptr(g5.pairs_t), ptr(dy5), ptr(x5), ptr(W),
+                                                  ptr(dx5), ptr(dW5), ptr(db5), N5, D, ptr(wsr), cs()), "c5 bwd")
             t = timeit(f, args.iters)
             res["c5_bwd"] = {"us": t, "GBps": (b5 + 4 * N5 * D) / t / 1e3}
+            fwm = lambda: check(lib.lg_gcn_bwd(ptr(g5.rowptr_t), ptr(g5.col_t), ptr(g5.w_t), ptr(dy5), None, ptr(x5),
+                                               ptr(W), ptr(dx5), ptr(dW5), ptr(db5), None, None, 1, N5, D,
+                                               g5.col_t.numel(), 0, 1.0, 1.0, ptr(ws5), cs()), "c5 bwd wm")
+            t = timeit(fwm, args.iters)
+            res["c5_bwd_wm"] = {"us": t, "GBps": (b5 + 4 * N5 * D) / t / 1e3}
     if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
         f = lambda: y.copy_(x)
         t = timeit(f, args.iters)
