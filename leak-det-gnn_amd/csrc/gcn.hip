@@ -163,15 +163,6 @@ __device__ __forceinline__ Csr stage_csr(uint32_t* s, const int32_t* __restrict_
     return Csr{reinterpret_cast<const int32_t*>(s), reinterpret_cast<const int32_t*>(s + n1p), nullptr};
 }
 
-#ifdef GCN_PROF
-// lab build only (tools/gcn_prof.cpp): per wave s_memtime cycles
-// [0 -, 1 csr+issue, 2 hook, 3 wait+fma, 4 tail MFMA, 5 epilogue+stores, 6 tiles, 7 rounds]
-__device__ unsigned long long g_gcn_prof[65536][8];
-__device__ unsigned long long* gcn_prof_slot() {
-    return g_gcn_prof[blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)];
-}
-#define GCN_T() __builtin_amdgcn_s_memtime()
-#endif
 
 struct NoHook {
     __device__ __forceinline__ void operator()(int, int) const {}
@@ -234,9 +225,6 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
     };
     if (rounds > 0) read_entries(0);
     for (int rd = 0; rd < rounds; ++rd) {
-#ifdef GCN_PROF
-        const unsigned long long pt0 = GCN_T();
-#endif
         f32x4 v[G::K][U], m[G::K][U];
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
@@ -251,13 +239,7 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
 #pragma unroll
             for (int u = 0; u < U; ++u) wv[k][u] = ok[k][u] ? ww[k][u] : 0.f;
         if (rd + 1 < rounds) read_entries(rd + 1);
-#ifdef GCN_PROF
-        const unsigned long long pt1 = GCN_T();
-#endif
         hook(rd, rounds);
-#ifdef GCN_PROF
-        const unsigned long long pt2 = GCN_T();
-#endif
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
 #pragma unroll
@@ -270,17 +252,6 @@ __device__ __forceinline__ void gather16(const Csr& g, const Rows<D>& src, const
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc[k][i] = fmaf(wv[k][u], t[i], acc[k][i]);
             }
-#ifdef GCN_PROF
-        asm volatile("" ::"v"(acc[0][0]), "v"(acc[G::K - 1][3]));
-        const unsigned long long pt3 = GCN_T();
-        if ((threadIdx.x & 63) == 0) {
-            unsigned long long* ps = gcn_prof_slot();
-            ps[1] += pt1 - pt0;
-            ps[2] += pt2 - pt1;
-            ps[3] += pt3 - pt2;
-            ps[7] += 1;
-        }
-#endif
     }
 }
 
@@ -347,9 +318,6 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
 
     const TileRange tr = xcd_tiles(ntiles, wave, NW);
     f32x4 acc[G::K];
-#ifdef GCN_PROF
-    unsigned long long tm = GCN_T();
-#endif
     if (tr.first < tr.end) {
         gather16<D, false, 2, CSR_LDS>(g, xs, xs, 1.f, static_cast<uint32_t>(tr.first * kTileRows), R, fdN, lane, acc);
         put_tile<D>(tl, acc, lane);
@@ -380,18 +348,7 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
         if (more)
             gather16<D, false, 2, CSR_LDS>(g, xs, xs, 1.f, static_cast<uint32_t>(next * kTileRows), R, fdN, lane, acc,
                                            hook);
-#ifdef GCN_PROF
-        tm = GCN_T();
-#endif
         while (chunk < G::CH) mfma_chunk();
-#ifdef GCN_PROF
-        {
-            asm volatile("" ::"v"(o[0][0]), "v"(o[G::MT - 1][3]));
-            const unsigned long long t = GCN_T();
-            if (lane == 0) gcn_prof_slot()[4] += t - tm;
-            tm = t;
-        }
-#endif
 
         const uint32_t r0 = static_cast<uint32_t>(tile * kTileRows);
         // row-stream dropout (common.h): seeded by the global row (launch splits do not
@@ -422,15 +379,6 @@ k_gcn_fwd(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, c
             wave_lds_sync();
             put_tile<D>(tl, acc, lane);
         }
-#ifdef GCN_PROF
-        {
-            const unsigned long long t = GCN_T();
-            if (lane == 0) {
-                gcn_prof_slot()[5] += t - tm;
-                gcn_prof_slot()[6] += 1;
-            }
-        }
-#endif
     }
 }
 

@@ -3112,17 +3112,30 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
     const NmSched sc = nm_sched(ntiles, wave, kRowWaves);
     const uint64_t bytes = static_cast<uint64_t>(N) * (4u * D);
     const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), xs0 = nm_rsrc(x, 0), ys = nm_rsrc(y, bytes);
+#ifdef LG_NM3_STAMPS
+    constexpr int WAVES = kRowWaves;
+    int tcount = 0;
+    LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
     int rw[4];
     rows_load_rec(tab, N, sc.first < sc.end ? sc.first : 0, lane, rw);
     stage_frag3<false>(wfr, W, 64 * kRowWaves);
     if (threadIdx.x < D) lds[LY::BOFF + threadIdx.x] = BIAS ? bias[threadIdx.x] : 0.f;
     __syncthreads();
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
+#endif
     for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
         RowsRec r;
         rows_decode(rw, r);
         rows_load_rec(tab, N, tile + sc.stride < sc.end ? tile + sc.stride : tile, lane, rw);  // next tile's records
         f32x4 acc[4], own[4];
         rows_gather<false, LG_ROWS_FWD_NB>(r, pairs, xs, xs0, lane, acc, own);
+#ifdef LG_NM3_STAMPS
+        asm volatile("" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
+        if (tcount < 6) LG_NM3_STAMP(3 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
         wave_sync_nm();
 #pragma unroll
         for (int k = 0; k < 4; ++k) st4(tl + LY::tix(4 * k + rl, fg), acc[k]);
@@ -3131,6 +3144,10 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) o[mt] = ld4(lds + LY::BOFF + 16 * mt + 4 * q);
         rows_transform(wfr, tl, lane, o);
+#ifdef LG_NM3_STAMPS
+        asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]));
+        if (tcount < 6) LG_NM3_STAMP(4 + 3 * tcount, __builtin_amdgcn_s_memtime());
+#endif
         wave_sync_nm();
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
@@ -3146,7 +3163,17 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
                                                    ys, off, 0, 0);
         }
         lg_store_guard(vk);
+#ifdef LG_NM3_STAMPS
+        if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
+        ++tcount;
+#endif
     }
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
+    LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                         static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
+#endif
 }
 
 // Backward on one graph: t = Ahat^T dy (transposed table), dx = t W, dW += t^T x, db += the

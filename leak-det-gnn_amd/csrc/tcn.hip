@@ -173,15 +173,8 @@ struct Pending {
     bool live;
 };
 
-#ifdef TCN_PROF
-__device__ unsigned long long g_tcn_prof[4096][8];  // per workgroup: K-loop, between, prologue, tiles, partials, barrier
-#endif
 
 __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
-#ifdef TCN_PROF
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long t_k = 0, t_b = 0, t_mark = 0, n_t = 0, t_p = 0, t_w = 0;
-#endif
     // tiles[b]: pieces 0..23 = the gathered tap rows (A fragments), pieces 24..31 = the
     // tile's 16 residual rows (block input) in the same fragment layout
     __shared__ __attribute__((aligned(16))) float tiles[2][kTileFloats];
@@ -322,10 +315,6 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
     };
 
     int buf = 0;
-#ifdef TCN_PROF
-    const unsigned long long t_pro = __builtin_amdgcn_s_memtime() - t_start;
-    t_mark = __builtin_amdgcn_s_memtime();
-#endif
     for (uint32_t tile = tr.first; tile < tr.end; tile += tr.stride, buf ^= 1) {
         float res[4][2];
         i32x4 dplan;
@@ -395,14 +384,6 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
 #endif
             },
             std::make_integer_sequence<int, kQ>{});
-#ifdef TCN_PROF
-        {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            t_k += t - t_mark;
-            t_mark = t;
-            ++n_t;
-        }
-#endif
         // LayerNorm partials of this tile: each wave reduces its 32 channels exactly
         // (two-pass mean / M2 inside the wave, DPP only); the four waves' (mean, M2)
         // are merged by ln_stats with Chan's parallel formula.
@@ -431,23 +412,8 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
         pd.tile = tile;
         pd.par = buf;
         pd.live = true;
-#ifdef TCN_PROF
-        const unsigned long long t_p0 = __builtin_amdgcn_s_memtime();
-#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile j+1
         __syncthreads();
-#ifdef TCN_PROF
-        const unsigned long long t_p1 = __builtin_amdgcn_s_memtime();
-        t_p += t_p0 - t_mark;
-        t_w += t_p1 - t_p0;
-#endif
-#ifdef TCN_PROF
-        {
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            t_b += t - t_mark;
-            t_mark = t;
-        }
-#endif
     }
     if (pd.live) {
         read_stats();
@@ -460,16 +426,6 @@ __global__ __launch_bounds__(kThreads) void k_tcn_conv(ConvArgs a) {
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
-#ifdef TCN_PROF
-    if (threadIdx.x == 0 && blockIdx.x < 4096) {
-        g_tcn_prof[blockIdx.x][0] = t_k;
-        g_tcn_prof[blockIdx.x][1] = t_b;
-        g_tcn_prof[blockIdx.x][2] = t_pro;
-        g_tcn_prof[blockIdx.x][3] = n_t;
-        g_tcn_prof[blockIdx.x][4] = t_p;
-        g_tcn_prof[blockIdx.x][5] = t_w;
-    }
-#endif
 }
 
 // Packed weight: wpk[w][q][c][lane][j] = W[co][ci][2 - tap] with co = 32w + 16c + lane % 16,

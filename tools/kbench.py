@@ -244,9 +244,20 @@ def main():
         if "c5_fwd" in which:
             t = timeit(f, args.iters)
             res["c5_fwd"] = {"us": t, "GBps": b5 / t / 1e3}
+            if args.stamps and hasattr(lib, "lg_lab_nm3_stamps"):
+                res["stamps_c5_fwd"] = stamps_summary(lib, f)
         if "c5_fwd" in which or "c5_fwd_wm" in which:
             t = timeit(fwm, args.iters)
             res["c5_fwd_wm"] = {"us": t, "GBps": b5 / t / 1e3}
+        if "c5_copy" in which:  # the floor: x -> y of the same bytes (torch copy_ and the library's copy)
+            t = timeit(lambda: y5.copy_(x5), args.iters)
+            res["c5_copy_torch"] = {"us": t, "GBps": 8 * N5 * D / t / 1e3}
+            t = timeit(lambda: check(lib.lg_stream_copy(ptr(x5), ptr(y5), 4 * N5 * D, cs()), "copy"), args.iters)
+            res["c5_copy_lg"] = {"us": t, "GBps": 8 * N5 * D / t / 1e3}
+        if "c5_spmm" in which:
+            t = timeit(lambda: check(lib.lg_spmm(ptr(g5.rowptr), ptr(g5.col), ptr(g5.w), ptr(x5), ptr(y5), 1, N5, D,
+                                                 g5.col.numel(), cs()), "c5 spmm"), args.iters)
+            res["c5_spmm"] = {"us": t, "GBps": b5 / t / 1e3}
         if "c5_bwd" in which:
             dy5 = torch.randn_like(x5)
             dx5 = torch.empty_like(x5)

@@ -8,7 +8,7 @@ differs (rows / columns).
 import sys
 from pathlib import Path
 
-REPO = Path(__file__).resolve().parents[1]
+REPO = Path(__file__).resolve().parents[3]
 sys.path[:0] = [str(REPO), str(REPO / "leak-det-gnn_amd")]
 import numpy as np
 import torch

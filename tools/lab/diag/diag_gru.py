@@ -9,7 +9,7 @@ from pathlib import Path
 
 import torch
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[3]
 for p in (ROOT, ROOT / "leak-det-gnn_amd", ROOT / "tests"):
     sys.path.insert(0, str(p))
 

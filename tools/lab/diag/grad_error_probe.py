@@ -2,7 +2,7 @@
 both against the CPU oracle run in float64 (the closest thing to ground truth)."""
 import sys
 from pathlib import Path
-REPO = Path(__file__).resolve().parents[1]
+REPO = Path(__file__).resolve().parents[3]
 sys.path[:0] = [str(REPO), str(REPO / "leak-det-gnn_amd"), str(REPO / "tests")]
 import torch
 from helpers import LTA_INP, load, lta_ids

@@ -1,7 +1,7 @@
 """Time single TCN conv layers (lg_tcn_conv_fwd) across batch sizes: python tools/tcn_lab.py 256,1024 [0]."""
 import os, sys
 from pathlib import Path
-REPO = Path(__file__).resolve().parents[1]
+REPO = Path(__file__).resolve().parents[3]
 sys.path[:0] = [str(REPO), str(REPO / "leak-det-gnn_amd")]
 import torch
 from models import _native as nat, tcn_plan

@@ -3,7 +3,7 @@
 set -o pipefail
 OUT=gpurun_out/r03d; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u tools/nm3_opt_check.py --nm5 --opts "" > $OUT/check.txt 2>&1; tail -2 $OUT/check.txt
+timeout -k 10 300 python -u tools/lab/diag/nm3_opt_check.py --nm5 --opts "" > $OUT/check.txt 2>&1; tail -2 $OUT/check.txt
 L="opt0+mask,nm5+mask,nm5,opt0,nm5+mask+bf16,opt0+mask+bf16"
 for v in lab lab_n3 lab_n5 lab; do
   echo "== $v"

@@ -3,7 +3,7 @@
 set -o pipefail
 OUT=gpurun_out/r03m; mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 120 python -u tools/nm3_opt_check.py --nm5 --opts "" > $OUT/check.txt 2>&1; tail -3 $OUT/check.txt
+timeout -k 10 120 python -u tools/lab/diag/nm3_opt_check.py --nm5 --opts "" > $OUT/check.txt 2>&1; tail -3 $OUT/check.txt
 L="mask,nm3+mask,x,mask"
 for v in libleakgnn v_nox4 v_x4n2 v_x4n4 libleakgnn v_nox4; do
   lib=leak-det-gnn_amd/lib/libleakgnn.so; [ $v = libleakgnn ] || lib=leak-det-gnn_amd/lib/$v/libleakgnn.so
