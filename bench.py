@@ -390,8 +390,8 @@ def c4_leg(dev, steps: int, warmup: int, rank: int, world: int) -> dict:
 def c5_leg(dev, iters: int = 20) -> dict:
     """BASELINE configs[4], "the HBM-roofline stress of scatter-aggregate": ONE synthetic pipe
     graph of 100,000 nodes / 300,000 edge columns (150,000 pipes, models/synth.py, seed 0),
-    D = 64, B = 1: GCNConv(64, 64) forward and backward through the product's module (the
-    B = 1 path: lg_gcn_fwd / lg_gcn_bwd), x ~ N(0, 1) seed 0.  Roofline bytes per forward
+    D = 64, B = 1: GCNConv(64, 64) forward and backward through the product's module (its
+    D = 64 path: the node-table row tiles lg_gcn_fwd_rows / lg_gcn_bwd_rows), x ~ N(0, 1) seed 0.  Roofline bytes per forward
     call from SURVEY §8(d): 8 B N D + 4 (N + 1) + 8 E' = 54.8 MB (E' = E + N); backward:
     read dy (gathered) and x, write dx: 12 B N D + CSR bytes.  HIP events on the launch
     stream (the library's kernel timer), mean over `iters` calls after warm-up."""
@@ -425,12 +425,12 @@ def c5_leg(dev, iters: int = 20) -> dict:
     fg, bg = fwd_bytes / (fwd_ms * 1e-3) / 1e9, bwd_bytes / (bwd_ms * 1e-3) / 1e9
     return {"metric": "GCNConv fwd / bwd on one synthetic 100k-node / 300k-edge-column graph (BASELINE configs[4])",
             "nodes": N, "edge_columns": int(ei.shape[1]), "feat": D, "windows": 1, "scaling": "replicas only",
-            "path": "models.gcn.GCNConv (lg_gcn_fwd / lg_gcn_bwd, window-major = node order at B = 1)",
-            "roofline": {"kernel": "lg_gcn_fwd -> k_gcn_fwd (K5+K6+K7 fused)", "bound": "hbm",
+            "path": "models.gcn.GCNConv (lg_gcn_fwd_rows / lg_gcn_bwd_rows: 16-node tiles off the node table)",
+            "roofline": {"kernel": "lg_gcn_fwd_rows -> k_gcn_fwd_rows (K5+K6+K7 fused)", "bound": "hbm",
                          "achieved": round(fg, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fg / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2)},
-            "roofline_bwd": {"kernel": "lg_gcn_bwd -> k_gcn_bwd (dx, dW, db)", "bound": "hbm",
+            "roofline_bwd": {"kernel": "lg_gcn_bwd_rows -> k_gcn_bwd_rows (dx, dW, db)", "bound": "hbm",
                              "achieved": round(bg, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bg / HBM_PEAK_GBS, 4),
                              "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2)}}
@@ -815,7 +815,7 @@ def main() -> None:
         out["c4"] = c4
     if c5 is not None:
         if pmc:
-            tr = pmc_traffic("c5_fwd_wm", "k_gcn_fwd<", 1)
+            tr = pmc_traffic("c5_fwd", "k_gcn_fwd_rows", 1)
             out_c5 = c5["roofline"]
             out_c5["traffic"] = round(tr["bytes"]) if tr else None
             out_c5["traffic_source"] = src if tr else None

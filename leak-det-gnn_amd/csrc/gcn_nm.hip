@@ -2930,9 +2930,9 @@ k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 //     node's 64-byte record), requested a tile ahead; e0, e1, the six inline (col, w) pairs,
 //     self and node are broadcast inside each 16-lane row by DPP row_newbcast (VALU, no
 //     LDS, no scalar round trip per row);
-//   * all inline neighbour rows of the 16 nodes are in flight at once (buffer loads, an
-//     absent neighbour through a zero-record descriptor), entries beyond six from the pair
-//     array afterwards;
+//   * the inline neighbour rows of the 16 nodes in batches of 4 slots (buffer loads with the
+//     per-lane row address in the VGPR offset, an absent neighbour out of range), entries
+//     beyond six from the pair array afterwards;
 //   * the tile goes through LDS (XOR swizzle) to the MFMA transform on the 3-way bf16 split
 //     (W's parts in LDS in fragment order: one conflict-free ds_read_b128 per fragment), and
 //     rows go back out whole through the same LDS tile.
@@ -2941,10 +2941,10 @@ k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 // HBM peak at C5).
 constexpr int kRowWaves = 4;
 #ifndef LG_ROWS_FWD_NB
-#define LG_ROWS_FWD_NB 3  // inline neighbours per gather batch (x 4 rows per lane)
+#define LG_ROWS_FWD_NB 4  // inline neighbours per gather batch (x 4 rows per lane; 2 / 3 / 4 / 6 measured, profiles/r03/r03ad)
 #endif
 #ifndef LG_ROWS_BWD_NB
-#define LG_ROWS_BWD_NB 3
+#define LG_ROWS_BWD_NB 4
 #endif
 
 template <int n>
@@ -3049,7 +3049,7 @@ __device__ __forceinline__ void rows_load_rec(const int32_t* __restrict__ tab, u
 // = the row's own src row (from its self entry, else loaded) when OWN
 template <bool OWN, int NBATCH>
 __device__ __forceinline__ void rows_gather(const RowsRec& r, const int2* __restrict__ pairs, __amdgpu_buffer_rsrc_t src,
-                                            __amdgpu_buffer_rsrc_t src0, int lane, f32x4 (&acc)[4], f32x4 (&own)[4]) {
+                                            int lane, f32x4 (&acc)[4], f32x4 (&own)[4]) {
     constexpr int D = 64;
     const uint32_t lo = 16u * static_cast<uint32_t>(lane & 15);
 #pragma unroll
@@ -3069,9 +3069,13 @@ __device__ __forceinline__ void rows_gather(const RowsRec& r, const int2* __rest
         for (int i = 0; i < NBATCH; ++i)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const bool have = i0 + i < kLgNmInline && r.e0[k] + i0 + i < r.e1[k];
-                const uint32_t base = have ? static_cast<uint32_t>(r.col[k][i0 + i < kLgNmInline ? i0 + i : 0]) * (4u * D) : 0u;
-                v[k][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(have ? src : src0, lo, base, 0));
+                if (i0 + i >= kLgNmInline) continue;  // past the inline six: never read
+                const bool have = r.e0[k] + i0 + i < r.e1[k];
+                // per-lane row: the whole address in the VGPR offset (a per-lane descriptor or soffset
+                // is a waterfall loop: measured 27.5 -> 17 us at C5); an absent slot reads out of
+                // range (0, no memory request)
+                const uint32_t off = lo + static_cast<uint32_t>(r.col[k][i0 + i < kLgNmInline ? i0 + i : 0]) * (4u * D);
+                v[k][i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, have ? off : kNm3RowOob, 0, 0));
             }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -3087,12 +3091,12 @@ __device__ __forceinline__ void rows_gather(const RowsRec& r, const int2* __rest
         for (int e = r.e0[k] + kLgNmInline; e < r.e1[k]; ++e) {  // per-row tail (degree > 6)
             const int2 pa = pairs[e];
             const f32x4 t = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo, static_cast<uint32_t>(pa.x) * (4u * D), 0));
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo + static_cast<uint32_t>(pa.x) * (4u * D), 0, 0));
             pk_fma4(acc[k], __int_as_float(pa.y), t);
         }
         if (OWN && (r.self[k] < 0) && r.e0[k] < r.e1[k])  // self entry past the inline six
             own[k] = __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo, static_cast<uint32_t>(r.node[k]) * (4u * D), 0));
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(src, lo + static_cast<uint32_t>(r.node[k]) * (4u * D), 0, 0));
     }
 }
 
@@ -3111,7 +3115,7 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
     const int64_t ntiles = (static_cast<int64_t>(N) + 15) / 16;
     const NmSched sc = nm_sched(ntiles, wave, kRowWaves);
     const uint64_t bytes = static_cast<uint64_t>(N) * (4u * D);
-    const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), xs0 = nm_rsrc(x, 0), ys = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), ys = nm_rsrc(y, bytes);
 #ifdef LG_NM3_STAMPS
     constexpr int WAVES = kRowWaves;
     int tcount = 0;
@@ -3131,7 +3135,7 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
         rows_decode(rw, r);
         rows_load_rec(tab, N, tile + sc.stride < sc.end ? tile + sc.stride : tile, lane, rw);  // next tile's records
         f32x4 acc[4], own[4];
-        rows_gather<false, LG_ROWS_FWD_NB>(r, pairs, xs, xs0, lane, acc, own);
+        rows_gather<false, LG_ROWS_FWD_NB>(r, pairs, xs, lane, acc, own);
 #ifdef LG_NM3_STAMPS
         asm volatile("" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
         if (tcount < 6) LG_NM3_STAMP(3 + 3 * tcount, __builtin_amdgcn_s_memtime());
@@ -3194,7 +3198,7 @@ k_gcn_bwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
     const int64_t ntiles = (static_cast<int64_t>(N) + 15) / 16;
     const NmSched sc = nm_sched(ntiles, wave, kRowWaves);
     const uint64_t bytes = static_cast<uint64_t>(N) * (4u * D);
-    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), dys0 = nm_rsrc(dy, 0), xs = nm_rsrc(x, bytes),
+    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), xs = nm_rsrc(x, bytes),
                                  dxs = nm_rsrc(dxo, bytes);
     int rw[4];
     rows_load_rec(tab, N, sc.first < sc.end ? sc.first : 0, lane, rw);
@@ -3219,7 +3223,7 @@ k_gcn_bwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
                                                   0, 0));
         }
         f32x4 acc[4], own[4];
-        rows_gather<true, LG_ROWS_BWD_NB>(r, pairs, dys, dys0, lane, acc, own);
+        rows_gather<true, LG_ROWS_BWD_NB>(r, pairs, dys, lane, acc, own);
 #pragma unroll
         for (int k = 0; k < 4; ++k) dbacc += own[k];
         wave_sync_nm();

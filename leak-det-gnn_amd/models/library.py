@@ -58,18 +58,19 @@ def _c(t: Optional[Tensor]) -> Optional[Tensor]:
 
 
 # ============================================================================ gcn_conv
-# GCNConv's single-graph kernels: False = window-major lg_gcn_fwd / lg_gcn_bwd (exact fp32,
-# the default), True = the node-table row tiles lg_gcn_{fwd,bwd}_rows (D = 64; same speed at C5)
-_ROWS = False
+# GCNConv's single-graph kernels at D = 64: True (default) = the node-table row tiles
+# lg_gcn_{fwd,bwd}_rows (split-bf16 MFMA, fp32-level accuracy; at C5 17.7 / 40.4 us against
+# 26.7 / 50.5 us, profiles/r03/r03ac), False = window-major lg_gcn_fwd / lg_gcn_bwd (exact
+# fp32 MFMA, and the D = 32 path)
+_ROWS = True
 
 @torch.library.custom_op(f"{NS}::gcn_conv", mutates_args=(), device_types="cuda")
 def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, col: Tensor, w: Tensor,
              rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, nodetab: Tensor, pairs: Tensor, nodetab_t: Tensor,
              pairs_t: Tensor) -> Tensor:
-    """y = Ahat (x W^T) + b on one graph: lg_gcn_fwd (B = 1, exact fp32 MFMA).  (rowptr, col,
-    w): the gcn_norm'ed CSR of lg_graph_build; nodetab / pairs: its node table (GCNGraph),
-    for the row-tile kernels (lg_gcn_fwd_rows, `rows=True`; measured no faster at C5:
-    27.7 vs 26.8 us forward, 48.5 vs 50.0 us backward, profiles/r03/r03x)."""
+    """y = Ahat (x W^T) + b on one graph: lg_gcn_fwd_rows (D = 64: 16-node tiles off the node
+    table nodetab / pairs of GCNGraph) or lg_gcn_fwd (D = 32, or `_ROWS = False`: exact fp32
+    MFMA over the gcn_norm'ed CSR rowptr / col / w of lg_graph_build)."""
     lib = load_library()
     x, weight, bias = _c(x), _c(weight), _c(bias)
     _req(x, weight, bias)
