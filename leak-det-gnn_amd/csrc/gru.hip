@@ -609,22 +609,27 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         // (3) dW over the 32 sequences: A = dG^T tiles (rows = gate rows 16w.., K = seq),
         // B = h_{t-1} / x_t (K = seq, columns = units / x columns)
         {
-            const int tr = 8 * q + (j >> 2), tc = 4 * (j & 3);  // tr16 addressing of this lane
+            // tr16 addressing of this lane.  K = the 32 sequences, lane group q taking rows
+            // 4q..4q+3 (elements 0-3) and 16+4q..16+4q+3 (elements 4-7), the same in both
+            // operands: a 32-lane half then reads 8 consecutive rows, whose 8-dword windows meet
+            // distinct banks at these row strides (rows 8q.. and 8q+4.. did 2-way:
+            // MI355X_MICROARCH.md §LDS, 54 % of LDS-active cycles were conflicts)
+            const int tr = 4 * q + (j >> 2), tc = 4 * (j & 3);
             lg_bf16x8 bh[G::NTS][3], bx[3];
 #pragma unroll
             for (int n = 0; n < G::NTS; ++n)
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     bh[n][p] = lds_frag_tr16(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
-                                             &hls[bf][p][tr + 4][16 * (sh * G::NTS + n) + tc]);
+                                             &hls[bf][p][tr + 16][16 * (sh * G::NTS + n) + tc]);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bx[p] = lds_frag_tr16(&xls[bf][p][tr][tc], &xls[bf][p][tr + 4][tc]);
+            for (int p = 0; p < 3; ++p) bx[p] = lds_frag_tr16(&xls[bf][p][tr][tc], &xls[bf][p][tr + 16][tc]);
 #pragma unroll
             for (int gi = 0; gi < 3; ++gi) {
                 lg_bf16x8 a[3];
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
-                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 4][gi * H + 16 * w + tc]);
+                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 16][gi * H + 16 * w + tc]);
 #pragma unroll
                 for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mfma_split(a, bh[n], dwh[gi][n]);
                 if (sh == 0 && gi < 2) dwx[gi] = mfma_split(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
@@ -633,7 +638,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
                 lg_bf16x8 a[3];
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
-                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 4][3 * H + 16 * w + tc]);
+                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 16][3 * H + 16 * w + tc]);
                 dwx[0] = mfma_split(a, bx, dwx[0]);
             }
         }
