@@ -150,10 +150,11 @@ const char* lg_strerror(int code);
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;
  * reference train_detector.py:235, 311) over logits [B][C] (row stride ldx).
  *   fwd: loss (device fp32 scalar), lse [B] (saved for the backward), rowloss [B] scratch;
- *        counter: a device uint32 that is 0 at entry and left 0 (the last workgroup forms
- *        the mean over rows in row order and re-arms it) — one per concurrently used stream.
+ *        two launches: the rows, then one wave forms the mean over rows in row order.
+ *        counter: kept for ABI stability (must be non-NULL; unused since ABI 19 — the
+ *        last-workgroup mean behind it needed a device-scope fence, an L2 writeback on gfx950).
  *   bwd: dlogits[b][c] = grad_loss[0] / n * (exp(x - lse[b]) - [c == target[b]]), 0 for
- *        ignored rows (row stride ldd).  Two launches for what torch runs as six. */
+ *        ignored rows (row stride ldd).  Three launches for what torch runs as six. */
 int lg_cross_entropy_fwd(const float* logits, const int64_t* target, int64_t B, int64_t C, int64_t ldx,
                          int64_t ignore_index, float* loss, float* lse, float* rowloss, unsigned* counter,
                          lg_stream_t stream);
@@ -456,6 +457,21 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
                      float* dw1, float* db1, float* dw2, float* db2,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                      int flags, float dropout_p, void* workspace, lg_stream_t stream);
+/* lg_edge_head_bwd followed by lg_pipe_scatter_bwd (dh = dpool / N + the incidence sums of
+ * dpipe; reference detector.py:206-211 and the backward of its gather), with the scatter
+ * FUSED into the backward kernel: each workgroup owns whole windows and sums a window's node
+ * rows right after its pipe rows (read back from L2 / the Infinity Cache instead of a second
+ * launch over HBM), the incidence CSR staged in LDS.  Same results as the two calls (the same
+ * sums in the same order); when the CSR does not fit in LDS (N + 1 + 2P words beside the
+ * kernel's images) it runs the two calls.  dpipe is still written (scratch, [B][P][2][D]);
+ * dpool: NULL or [B][D] (lg_pool_head_bwd's dpooled, computed before this call); the workspace
+ * is lg_edge_head_bwd_workspace_bytes.  ABI 19. */
+int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                             const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
+                             float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
+                             const int32_t* inc_item, const float* dpool, float* dh,
+                             int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
+                             int flags, float dropout_p, void* workspace, lg_stream_t stream);
 
 /* K10 forward: per-window mean over the N node rows.
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)

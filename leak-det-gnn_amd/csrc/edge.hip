@@ -269,13 +269,75 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     if (tile < ntiles) body(tile, 0, pu0, pv0, nua, nva);
 }
 
+// The pipe scatter fused into the backward (SCAT): each workgroup owns whole windows (its tiles
+// are the window's pipe rows, 32 at a time from the window start) and, after a window's last
+// tile, sums that window's node gradients dh[n] = dpool / N + sum over the incidences of n (item
+// order) of dpipe[window][p][role] — the arithmetic of k_pipe_scatter — from the per-pipe rows
+// it has just written (L2 / Infinity Cache, not HBM); the incidence CSR is staged in LDS.
+struct EdgeScatter {
+    const int32_t* inc_rowptr;
+    const int32_t* inc_item;
+    const float* dpool;  // [B][D] or null
+    float* dh;
+    uint32_t N, P, B;
+    int nm;   // dh node-major ([N][B][D]) or window-major
+    int tpw;  // tiles per window
+};
+
+// dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
+// group in flight, the first four incidences of each in one batch; the same sums, in the same
+// order, as k_pipe_scatter (heads.hip).
+constexpr int kScatNodes = 2;
+template <int D>
+__device__ __forceinline__ void edge_scatter_window(const EdgeScatter& sc, const int32_t* icsr, const float* dpipe,
+                                                    uint32_t win) {
+    constexpr int LPR = D / 4, SLOTS = NT / LPR;
+    const int sr = threadIdx.x / LPR, sf = threadIdx.x % LPR;
+    const float fN = static_cast<float>(sc.N);
+    const int32_t* item = icsr + sc.N + 1;
+    f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (sc.dpool) {
+        const f32x4 g = ld4(sc.dpool + static_cast<int64_t>(win) * D + 4 * sf);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g0[c] = g[c] / fN;
+    }
+    const float* dp = dpipe + static_cast<int64_t>(win) * sc.P * 2 * D + 4 * sf;
+    for (uint32_t n0 = 0; n0 < sc.N; n0 += SLOTS * kScatNodes) {
+        int e0[kScatNodes], e1[kScatNodes];
+        f32x4 v[kScatNodes][4];
+#pragma unroll
+        for (int j = 0; j < kScatNodes; ++j) {
+            const uint32_t n = n0 + SLOTS * j + sr;
+            e0[j] = n < sc.N ? icsr[n] : 0;
+            e1[j] = n < sc.N ? icsr[n + 1] : 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int it = e0[j] + u < e1[j] ? item[e0[j] + u] : 0;  // 2 p + role
+                v[j][u] = e0[j] + u < e1[j] ? ld4(dp + static_cast<int64_t>(it) * D) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kScatNodes; ++j) {
+            const uint32_t n = n0 + SLOTS * j + sr;
+            if (n >= sc.N) continue;
+            f32x4 acc = g0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (e0[j] + u < e1[j]) acc += v[j][u];
+            for (int e = e0[j] + 4; e < e1[j]; ++e) acc += ld4(dp + static_cast<int64_t>(item[e]) * D);
+            const int64_t row = sc.nm ? static_cast<int64_t>(n) * sc.B + win : static_cast<int64_t>(win) * sc.N + n;
+            st4(sc.dh + row * D + 4 * sf, acc);
+        }
+    }
+}
+
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
-template <int D, bool BF>
+template <int D, bool BF, bool SCAT = false>
 __global__ void __launch_bounds__(NT)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ W2, const float* __restrict__ hid, const float* __restrict__ dlogit, int64_t ldo,
            float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, uint32_t sb,
-           uint32_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, float dscale) {
+           uint32_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, float dscale, EdgeScatter sc) {
     using G = EG<D>;
     constexpr int SL = HID * G::K3 + 2 * HID + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -314,26 +376,43 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     double db1a[4] = {0.0, 0.0, 0.0, 0.0};
     double db2 = 0.0;
 
-    const int64_t step = gridDim.x;
-    int64_t tile = blockIdx.x;
+    // this workgroup's k-th tile: tile blockIdx.x + k gridDim.x of the (B, P) row space, or
+    // (SCAT) tile k % tpw of window blockIdx.x + (k / tpw) gridDim.x; rows [rbase, rlim) count
+    const int64_t gstep = gridDim.x;
+    auto rbase = [&](int64_t k) -> int64_t {
+        if constexpr (SCAT) return (blockIdx.x + (k / sc.tpw) * gstep) * sc.P + (k % sc.tpw) * G::TR;
+        return (blockIdx.x + k * gstep) * G::TR;
+    };
+    auto rlim = [&](int64_t k) -> int64_t {
+        if constexpr (SCAT) return std::min<int64_t>(BP, (blockIdx.x + (k / sc.tpw) * gstep + 1) * sc.P);
+        return BP;
+    };
+    const int64_t nk = SCAT ? (blockIdx.x < sc.B ? sc.tpw * ((sc.B - blockIdx.x + gstep - 1) / gstep) : 0)
+                            : (blockIdx.x < ntiles ? (ntiles - blockIdx.x + gstep - 1) / gstep : 0);
     uint32_t nu, nv;
     f32x4 pu, pv, hp[G::HPT];
     float dl[G::HPT];
-    auto load_hid = [&](int64_t t) {  // raw (see load_ends); a row past the end is zeroed at use
+    auto load_hid = [&](int64_t rb) {  // raw (see load_ends); a row past the end is zeroed at use
 #pragma unroll
         for (int i = 0; i < G::HPT; ++i) {
-            const uint32_t r = clamp_row(t * G::TR + hrow + 16 * i, BP);
+            const uint32_t r = clamp_row(rb + hrow + 16 * i, BP);
             hp[i] = ld4(hid + (r * HID + 4 * n4));
             dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
         }
     };
-    load_ends(ends, tile * G::TR + arow, BP, fdP, nu, nv);
-    load_rows<D>(h, tile * G::TR + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
-    load_hid(tile);
-    load_ends(ends, (tile + step) * G::TR + arow, BP, fdP, nu, nv);
+    // SCAT: the incidence CSR in LDS (after the kernel's images), staged before the first barrier
+    int32_t* icsr = reinterpret_cast<int32_t*>(smem + G::BWD_LDS);
+    if constexpr (SCAT) {
+        for (uint32_t i = threadIdx.x; i <= sc.N; i += NT) icsr[i] = sc.inc_rowptr[i];
+        for (uint32_t i = threadIdx.x; i < 2 * sc.P; i += NT) icsr[sc.N + 1 + i] = sc.inc_item[i];
+    }
+    load_ends(ends, rbase(0) + arow, BP, fdP, nu, nv);
+    load_rows<D>(h, rbase(0) + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
+    load_hid(rbase(0));
+    load_ends(ends, rbase(1) + arow, BP, fdP, nu, nv);
     int buf = 0;
-    for (; tile < ntiles; tile += step, buf ^= 1) {
-        const int64_t row0 = tile * G::TR;
+    for (int64_t k = 0; k < nk; ++k, buf ^= 1) {
+        const int64_t row0 = rbase(k), rend = rlim(k);
         int8_t* sgnb = sgn + buf * G::TR * D;
         {
             f32x4 a;
@@ -352,7 +431,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 #pragma unroll
         for (int i = 0; i < G::HPT; ++i) {
             f32x4 g;
-            const float dli = row0 + hrow + 16 * i < BP ? dl[i] : 0.f;  // rows past the end: no gradient
+            const float dli = row0 + hrow + 16 * i < rend ? dl[i] : 0.f;  // rows past the end: no gradient
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 g[j] = hp[i][j] > 0.f ? dli * w2g[j] * dscale : 0.f;
@@ -363,9 +442,9 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
         }
         __syncthreads();
-        load_rows<D>(h, (tile + step) * G::TR + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
-        load_hid(tile + step);
-        load_ends(ends, (tile + 2 * step) * G::TR + arow, BP, fdP, nu, nv);
+        load_rows<D>(h, rbase(k + 1) + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
+        load_hid(rbase(k + 1));
+        load_ends(ends, rbase(k + 2) + arow, BP, fdP, nu, nv);
 
         // dW1[n][k] += sum_rows g[row][n] feat[row][k]: n-tile w, every k-tile; the k (= row)
         // order inside a step is 4q + (j & 3) + 16 (j >> 2) in both operands
@@ -428,6 +507,12 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 float* o = dpipe + (static_cast<uint32_t>(r) * 2 * D + ku);
                 st4(o, du);
                 st4(o + D, dv);
+            }
+        }
+        if constexpr (SCAT) {
+            if (k % sc.tpw == sc.tpw - 1) {  // the window's last tile: its node gradients
+                __syncthreads();             // every wave's dpipe rows of the window are stored
+                edge_scatter_window<D>(sc, icsr, dpipe, static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep));
             }
         }
     }
@@ -541,10 +626,12 @@ extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_
     return ((G * SL * 4 + 255) & ~int64_t(255)) + G * 8;
 }
 
-extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
-                                const float* hid, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
-                                float* db1, float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D,
-                                int64_t hidden, int flags, float dropout_p, void* workspace, lg_stream_t stream) {
+namespace {
+
+int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const float* w2, const float* hid,
+                  const float* dlogits, int64_t ldo, float* dpipe, float* dw1, float* db1, float* dw2, float* db2,
+                  int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
+                  void* workspace, lg_stream_t stream, const EdgeScatter* scat) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
@@ -557,22 +644,32 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     const bool nm = (flags & LG_F_NODE_MAJOR) != 0;  // h is [N][B][D] instead of [B][N][D]
     const int64_t sb = nm ? 1 : N, sn = nm ? B : 1;
     const int64_t ntiles = cdiv(std::max<int64_t>(BP, 1), tile_rows(D));
-    const int grid = bwd_grid(ntiles);
+    // SCAT: one workgroup per window (at most one per CU, as the strided schedule); the slab
+    // of lg_edge_head_bwd_workspace_bytes has a row for every one of them
+    const int grid = scat ? static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(B, lg_num_cus()))) : bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const int64_t SL = HID * 3 * D + 2 * HID + 1;
     float* slab = static_cast<float*>(workspace);
     double* dslab = reinterpret_cast<double*>(static_cast<char*>(workspace) + ((grid * SL * 4 + 255) & ~int64_t(255)));
     hipStream_t s = lg_stream(stream);
+    const EdgeScatter none{};
     if (BP == 0) {
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else {
         const bool bf = (flags & LG_F_BF16) != 0;
+        const int64_t lds = scat ? EG<64>::BWD_LDS * (D == 64) + EG<32>::BWD_LDS * (D == 32) + 4 * (N + 1 + 2 * P) : 0;
 #define LG_EDGE_BWD(DD, BFB)                                                                                      \
     do {                                                                                                          \
-        if (!allow_lds(k_edge_bwd<DD, BFB>, EG<DD>::BWD_LDS)) return LG_EHIP;                                     \
-        lg_launch(k_edge_bwd<DD, BFB>, grid, NT, EG<DD>::BWD_LDS, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, \
-                  dslab, sb, sn, fdP, BP, ntiles, scale);                                                         \
+        if (scat) {                                                                                               \
+            if (!allow_lds(k_edge_bwd<DD, BFB, true>, lds)) return LG_EHIP;                                        \
+            lg_launch(k_edge_bwd<DD, BFB, true>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, \
+                      dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                               \
+        } else {                                                                                                  \
+            if (!allow_lds(k_edge_bwd<DD, BFB>, EG<DD>::BWD_LDS)) return LG_EHIP;                                 \
+            lg_launch(k_edge_bwd<DD, BFB>, grid, NT, EG<DD>::BWD_LDS, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, \
+                      slab, dslab, sb, sn, fdP, BP, ntiles, scale, none);                                          \
+        }                                                                                                         \
     } while (0)
         if (D == 64) {
             if (bf) LG_EDGE_BWD(64, true); else LG_EDGE_BWD(64, false);
@@ -585,4 +682,39 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
     const int64_t K3 = 3 * D;
     const LgSlabSeg segs[3] = {{0, HID * K3, dw1}, {HID * K3, HID, db1}, {HID * K3 + HID, HID, dw2}};
     return lg_launch_slab_reduce_multi(slab, grid, SL, segs, 3, dslab, db2, s);
+}
+
+}  // namespace
+
+extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                                const float* hid, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
+                                float* db1, float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D,
+                                int64_t hidden, int flags, float dropout_p, void* workspace, lg_stream_t stream) {
+    return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
+                         dropout_p, workspace, stream, nullptr);
+}
+
+extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                                        const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
+                                        float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
+                                        const int32_t* inc_item, const float* dpool, float* dh, int64_t B, int64_t N,
+                                        int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
+                                        void* workspace, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
+    if (!dh || !inc_rowptr || (P > 0 && !inc_item)) return LG_EINVAL;
+    if (B == 0) return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D,
+                                     hidden, flags, dropout_p, workspace, stream, nullptr);
+    const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS;
+    if (P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
+        // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
+        const int rc = edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
+                                     flags, dropout_p, workspace, stream, nullptr);
+        if (rc != LG_OK) return rc;
+        return lg_pipe_scatter_bwd(inc_rowptr, inc_item, dpipe, dpool, dh, B, N, P, D, flags & LG_F_NODE_MAJOR, stream);
+    }
+    EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
+                   static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0,
+                   static_cast<int>(cdiv(P, tile_rows(D)))};
+    return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
+                         dropout_p, workspace, stream, &sc);
 }

@@ -3,9 +3,12 @@
 // it as six launches (log_softmax, nll forward, two fills, nll backward, log_softmax
 // backward); here:
 //   forward : one wave per row: lse = max + log(sum exp(x - max)) (fp32, fixed lane order
-//             then a fixed shuffle tree), row loss = lse - x[target] -> lse[b], rowloss[b]
-//             and, by the LAST workgroup to finish (device-scope counter), the mean over the
-//             counted rows summed in row order (deterministic)
+//             then a fixed shuffle tree), row loss = lse - x[target] -> lse[b], rowloss[b];
+//             then one single-wave launch sums the counted rows in row order (deterministic).
+//             (The mean used to be taken by the last workgroup behind a device-scope counter:
+//             on gfx950 that release / acquire is an L2 writeback + invalidate in every
+//             workgroup — buffer_wbl2 / buffer_inv — which, right after the EdgeHead forward's
+//             100 MB of stores, made the launch 12 us for 0.8 MB of logits.)
 //   backward: dx[b][c] = g / n * (exp(x - lse[b]) - [c == target[b]])   (0 for ignored rows)
 #include <algorithm>
 #include "common.h"
@@ -29,8 +32,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 __global__ void __launch_bounds__(kCeThreads)
 k_ce_fwd(const float* __restrict__ x, const int64_t* __restrict__ target, int64_t B, int64_t C, int64_t ldx,
-         int64_t ignore, float* __restrict__ lse, float* __restrict__ rowloss, unsigned* __restrict__ done,
-         float* __restrict__ loss) {
+         int64_t ignore, float* __restrict__ lse, float* __restrict__ rowloss) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t b = static_cast<int64_t>(blockIdx.x) * kCeWaves + w; b < B; b += static_cast<int64_t>(gridDim.x) * kCeWaves) {
         const float* row = x + b * ldx;
@@ -61,34 +63,25 @@ k_ce_fwd(const float* __restrict__ x, const int64_t* __restrict__ target, int64_
             rowloss[b] = t == ignore ? 0.f : (t >= 0 && t < C ? l - row[t] : __builtin_nanf(""));
         }
     }
-    // last workgroup: the mean, rows in order.  Release: every storing lane's device-scope
-    // fence, the barrier, then the counter (a vector atomic at agent scope); acquire: the
-    // last workgroup's device-scope fence before it reads the other workgroups' rows.
-    __shared__ unsigned last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    if (w == 0) {
-        float acc = 0.f, cnt = 0.f;
-        for (int64_t b0 = 0; b0 < B; b0 += 64) {
-            const int64_t b = b0 + lane;
-            float v = 0.f, c = 0.f;
-            if (b < B) {
-                v = rowloss[b];
-                c = target[b] == ignore ? 0.f : 1.f;
-            }
-            acc += wave_sum(v);
-            cnt += wave_sum(c);
+}
+
+// the mean over the counted rows, in row order (one wave)
+__global__ void __launch_bounds__(64)
+k_ce_mean(const float* __restrict__ rowloss, const int64_t* __restrict__ target, int64_t B, int64_t ignore,
+          float* __restrict__ loss) {
+    const int lane = threadIdx.x & 63;
+    float acc = 0.f, cnt = 0.f;
+    for (int64_t b0 = 0; b0 < B; b0 += 64) {
+        const int64_t b = b0 + lane;
+        float v = 0.f, c = 0.f;
+        if (b < B) {
+            v = rowloss[b];
+            c = target[b] == ignore ? 0.f : 1.f;
         }
-        if (lane == 0) {
-            loss[0] = acc / cnt;  // NaN when every row is ignored, as torch
-            done[0] = 0u;         // re-armed for the next call (and the next graph replay)
-        }
+        acc += wave_sum(v);
+        cnt += wave_sum(c);
     }
+    if (lane == 0) loss[0] = acc / cnt;  // NaN when every row is ignored, as torch
 }
 
 __global__ void __launch_bounds__(kCeThreads)
@@ -140,7 +133,8 @@ extern "C" int lg_cross_entropy_fwd(const float* logits, const int64_t* target, 
     }
     if (!logits || !target || !lse || !rowloss) return LG_EINVAL;
     const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, 4 * lg_num_cus()));
-    lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss, counter, loss);
+    lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss);
+    lg_launch(k_ce_mean, 1, 64, 0, s, rowloss, target, B, ignore_index, loss);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

@@ -593,9 +593,9 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
                             hid: Tensor, nw1: Tensor, nw2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor,
                             p_edge: float, p_noleak: float, node_major: bool, *, bf16: bool = False
                             ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
-    """(dh, dW1, db1, dW2, db2, dnW1, dnb1, dnW2, dnb2): lg_edge_head_bwd -> per-pipe
-    endpoint grads; lg_pool_head_bwd -> dpooled and the NoLeakHead grads; ONE deterministic
-    incidence reduce (lg_pipe_scatter_bwd) adds dpooled / N to every node row."""
+    """(dh, dW1, db1, dW2, db2, dnW1, dnb1, dnW2, dnb2): lg_pool_head_bwd -> dpooled and the
+    NoLeakHead grads; lg_edge_head_bwd_scatter -> the per-pipe endpoint grads and, fused, their
+    deterministic incidence reduce plus dpooled / N into every node row."""
     lib = load_library()
     if ehid.numel() == 0:
         raise RuntimeError("detector_heads was run with keep_hidden=False; no backward")
@@ -614,30 +614,45 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     ndw2, ndb2 = torch.empty_like(nw2), torch.empty(1, device=dev)
     ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
     wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
-    with _reduce_batch(lib, st):  # the EdgeHead's and the NoLeakHead's weight-grad reductions in one launch
-        dpooled = _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, P, B, N, D, hidden,
-                                           nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dw1, db1, dw2, db2, ndw1,
-                                           ndb1, ndw2, ndb2, ws, wsn, st)
     dh = torch.empty_like(h)
-    with _timed("pipe_scatter", dev):
-        check(lib.lg_pipe_scatter_bwd(ptr(inc_rowptr), ptr(inc_item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P, D,
-                                      lay, st), "lg_pipe_scatter_bwd")
+    with _reduce_batch(lib, st):  # the EdgeHead's and the NoLeakHead's weight-grad reductions in one launch
+        _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N,
+                                 D, hidden, nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2, db2, ndw1,
+                                 ndb1, ndw2, ndb2, ws, wsn, st)
     return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 
-def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, P, B, N, D, hidden, nhidden, fe,
-                             fn, p_edge, p_noleak, dpipe, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2, ws, wsn, st):
+# False: the EdgeHead backward and the pipe scatter as two launches (lg_edge_head_bwd +
+# lg_pipe_scatter_bwd; same results)
+_FUSED_SCATTER = True
+
+
+def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N, D,
+                             hidden, nhidden, fe, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2,
+                             ndb2, ws, wsn, st):
+    """NoLeakHead backward first (its dpooled feeds the node rows), then the EdgeHead backward
+    with the incidence scatter fused in (lg_edge_head_bwd_scatter): dh complete."""
     dev = h.device
-    with _timed("edge_bwd", dev):
-        check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
-                                   ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, p_edge,
-                                   ptr(ws), st), "lg_edge_head_bwd")
     dpooled = torch.empty(B, D, device=dev)
     with _timed("pool_head_bwd", dev):
         check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
                                    ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn),
                                    st), "lg_pool_head_bwd")
-    return dpooled
+    lay = fe & nat.LG_F_NODE_MAJOR
+    if _FUSED_SCATTER:
+        with _timed("edge_bwd", dev):
+            check(lib.lg_edge_head_bwd_scatter(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1,
+                                               ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(inc_rowptr),
+                                               ptr(inc_item), ptr(dpooled), ptr(dh), B, N, P, D, hidden, fe, p_edge,
+                                               ptr(ws), st), "lg_edge_head_bwd_scatter")
+        return
+    with _timed("edge_bwd", dev):
+        check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
+                                   ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, p_edge,
+                                   ptr(ws), st), "lg_edge_head_bwd")
+    with _timed("pipe_scatter", dev):
+        check(lib.lg_pipe_scatter_bwd(ptr(inc_rowptr), ptr(inc_item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P, D,
+                                      lay, st), "lg_pipe_scatter_bwd")
 
 
 @detector_heads_backward.register_fake

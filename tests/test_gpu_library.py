@@ -271,3 +271,36 @@ def test_reduce_batch_matches_per_op_reductions():
             assert_close(g, ref, rtol=1e-6, atol=1e-6 * ref.abs().max().item(), what=n)
         else:
             assert torch.equal(g, ref), f"{n}: batched reduction differs"
+
+
+@pytest.mark.parametrize("B", [3, 64, 300])
+def test_fused_pipe_scatter_matches_two_launches(B):
+    """lg_edge_head_bwd_scatter (the incidence scatter fused into the EdgeHead backward, one
+    workgroup per window) against lg_edge_head_bwd + lg_pipe_scatter_bwd: the node gradient
+    is the same sums in the same order, so every gradient upstream of it (trunk, GRU, sensor
+    projection, NoLeakHead) is bitwise equal; the EdgeHead's weight gradients change only by
+    the slab grouping of the fixed-order reduction (window-owned tiles).  B = 3: window-major
+    trunk; 64: node-major; 300: more windows than CUs (several windows per workgroup)."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    torch.manual_seed(5)
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
+    r = torch.randn(B, 36, 29, device=DEV)
+    tf = torch.randn(B, 36, 9, device=DEV)
+    grads = []
+    for fused in (True, False):
+        library._FUSED_SCATTER = fused
+        try:
+            m.zero_grad(set_to_none=True)
+            torch.manual_seed(17)
+            m(r, tf).square().mean().backward()
+            torch.cuda.synchronize()
+        finally:
+            library._FUSED_SCATTER = True
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    for n, g in grads[0].items():
+        ref = grads[1][n]
+        if n.startswith("edge_head."):
+            assert_close(g, ref, rtol=1e-5, atol=1e-6 * ref.abs().max().item(), what=n)
+        else:
+            assert torch.equal(g, ref), f"{n}: fused scatter differs"
