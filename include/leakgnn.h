@@ -58,6 +58,13 @@ enum {
 #define LG_F_DROPOUT   0x04  /* fwd: inverted dropout after ReLU (nn.Dropout, detector.py:201) */
 #define LG_F_MASK_IN   0x08  /* bwd: dz = dy * scale_in * [y > 0]  (ReLU/dropout backward of THIS layer's output) */
 #define LG_F_MASK_OUT  0x10  /* bwd: dx_out = dx * scale_out * [x > 0] (ReLU/dropout backward of the PREVIOUS op) */
+/* bwd with node_slot / dnode_bias (ABI 20): rows of dx_out whose node has no sensor
+ * (node_slot[n] < 0) MAY be left unwritten; their masked sums are in dnode_bias.  The node
+ * init's backward (lg_sensor_proj_bwd) reads only the sensor rows (detector.py:181-186), so
+ * layer 0's backward then writes 29 of L-TOWN-A's 661 rows per window instead of all of
+ * them.  Honoured by the default node-major schedule of lg_gcn_bwd_nm[_bits]; the other
+ * schedules and lg_gcn_bwd write every row. */
+#define LG_F_DX_SENSOR_ROWS 0x10000000
 /* Node-feature layout for lg_node_init_fwd / lg_pipe_scatter_bwd / lg_edge_head_* /
  * lg_pool_head_fwd: without it node rows are window-major [B][N][D] (row b*N + n, the
  * reference's disjoint-union order, detector.py:105-114, 192-196); with it they are

@@ -496,7 +496,9 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             const f32x4 cu = r0p[0] + r1p[0], cv = r0p[64] + r1p[64], ca = r0p[128] + r1p[128];
             const int ku = 16 * kt2 + 4 * q;
             const uint32_t sw = *reinterpret_cast<const uint32_t*>(sgnb + row * D + ku);
-            if (r < BP) {
+            // rend, not BP: (SCAT) a window's last tile runs past its P rows into the next window's,
+            // which another workgroup owns and may already have written (with the real gradient)
+            if (r < rend) {
                 f32x4 du, dv;
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) {

@@ -1904,7 +1904,7 @@ k_gcn_bwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 for (int mt = 0; mt < G::CH; ++mt) o[mt] = mfma_nm(wl[ko * SW + 16 * mt + j], bt[i], o[mt]);
             }
         }
-        if (mask_out) {
+        if (mask_out & 1) {
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
                 const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
@@ -2380,7 +2380,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (mask_out) {
+        if (mask_out & 1) {
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
                 const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
@@ -2389,9 +2389,12 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             }
         }
         if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
-            if (node_slot[n] < 0)
+            if (node_slot[n] < 0) {
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) nbacc[mt] += o[mt];
+                // LG_F_DX_SENSOR_ROWS: the node init's backward reads only the sensor rows of dx
+                if (mask_out & 2) continue;
+            }
         }
         wave_sync_nm();
 #pragma unroll
@@ -2843,7 +2846,7 @@ k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
             for (int mt = 0; mt < CH; ++mt) {
                 o[mt] *= ux;
-                if (mask_out) {
+                if (mask_out & 1) {
                     const f32x4 xm = ld4(xt + LY::tix(j, 4 * mt + q));
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
@@ -3599,7 +3602,8 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
     const int64_t ngroups = (B + 15) / 16, ntiles = std::max<int64_t>(ngroups * N, 0);
-    const int mask_out = (flags & LG_F_MASK_OUT) ? 1 : 0;
+    // bit 0: MASK_OUT; bit 1: LG_F_DX_SENSOR_ROWS (nm3 only; other schedules write every row)
+    const int mask_out = ((flags & LG_F_MASK_OUT) ? 1 : 0) | ((node_slot && (flags & LG_F_DX_SENSOR_ROWS)) ? 2 : 0);
     const size_t dyn = 4 * static_cast<size_t>(kNmBwdWaves * 2 * 16 * (D + 4) + D * (D + 4));
     const int2* pr = reinterpret_cast<const int2*>(pairs_t);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));

@@ -73,8 +73,8 @@ k_node_init(const int32_t* __restrict__ slot, const float* __restrict__ proj, co
 // row's pre-activation is h_s[b][s] . W[o][:Ds] + (W[o][Ds] + bias[o]) (its Linear input is
 // [h_s, 1]), every other row's is bias (input [0, 0]).  The first GS workgroups stage W^T
 // and the folded bias in LDS and form the S*B sensor rows (a lane group per row, 4 outputs
-// per lane, 4 * Ds fmas in ascending k); then every workgroup writes the non-sensor rows
-// like k_node_init, so no other workgroup pays for W.
+// per lane, 4 * Ds fmas in ascending k); the workgroups after them write the non-sensor rows
+// (kNiRowsPerBlock each), so no other workgroup pays for W.
 template <int D, int DS>
 __global__ void __launch_bounds__(256)
 k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ sidx, const float* __restrict__ hs,
@@ -88,10 +88,10 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
     const uint32_t thr = lg_keep_threshold16(p);
     if (static_cast<int>(blockIdx.x) < GS) {
         const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {
-            const int o = i / (DS + 1), k = i % (DS + 1);
-            if (k < DS) wt[k][o] = W[i];
-            else bf[o] = W[i] + bias[o];
+        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {  // o fastest: conflict-free LDS writes
+            const int k = i / D, o = i % D;
+            if (k < DS) wt[k][o] = W[o * (DS + 1) + k];
+            else bf[o] = W[o * (DS + 1) + DS] + bias[o];
         }
         __syncthreads();
         const f32x4 bs = ld4(bf + 4 * fg);
@@ -117,27 +117,53 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
             st4(x0 + (nm ? n * B + b : b * N + n) * D + 4 * fg, v);
         }
     }
-    // every row without a sensor: dropout(relu(bias)), in (row, q) lane groups
-    const int rl = threadIdx.x >> 2, q = threadIdx.x & 3;
-    f32x4 t[CH];
+    // every row without a sensor: dropout(relu(bias)).  Flat grid: the workgroups after the
+    // first GS own kNiRowsPerBlock rows each.  The keep bits are drawn in (row, q) lane groups
+    // (one stream per group, as above) and posted to LDS; the rows are then stored as whole
+    // lines (at D = 64 a wave's store covers 4 whole rows, 1 KiB contiguous, instead of 64-byte
+    // pieces of 16 rows).
+    if (static_cast<int>(blockIdx.x) < GS) return;
+    __shared__ uint32_t kbits[kNiRowsPerBlock][4];  // keep bits of (row, q): bit 4 mt + reg
+    const int64_t r0 = static_cast<int64_t>(static_cast<int>(blockIdx.x) - GS) * kNiRowsPerBlock;
+    {
+        const int rl = threadIdx.x >> 2, q = threadIdx.x & 3;
+        const int64_t r = r0 + rl;
+        uint32_t kb = 0xFFFFFFFFu;
+        if (dropout && r < R) {
+            const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
+            const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
+            uint32_t st = lg_row_stream_seed(key, static_cast<uint64_t>(b) * N + n, q);
+            kb = 0;
 #pragma unroll
-    for (int mt = 0; mt < CH; ++mt) {
-        t[mt] = ld4(bias + 16 * mt + 4 * q);
+            for (int mt = 0; mt < CH; ++mt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) t[mt][i] = fmaxf(t[mt][i], 0.f) * (dropout ? scale : 1.0f);
+                for (int reg = 0; reg < 4; ++reg) {
+                    if ((reg & 1) == 0) st = lg_xorshift32(st);
+                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
+                    kb |= static_cast<uint32_t>(u16 >= thr) << (4 * mt + reg);
+                }
+        }
+        kbits[rl][q] = kb;
     }
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * kNiRowsPerBlock + rl; r < R;
-         r += static_cast<int64_t>(gridDim.x) * kNiRowsPerBlock) {
+    __syncthreads();
+    // store phase: lane -> (row, float4 group fg), LPR lanes per row
+    const int fg = threadIdx.x % LPR, mt = fg >> 2, q = fg & 3;
+    f32x4 t = ld4(bias + 4 * fg);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[i] = fmaxf(t[i], 0.f) * (dropout ? scale : 1.0f);
+#pragma unroll
+    for (int it = 0; it < kNiRowsPerBlock / RPB; ++it) {
+        const int rl = it * RPB + static_cast<int>(threadIdx.x) / LPR;
+        const int64_t r = r0 + rl;
+        if (r >= R) break;
         const uint32_t hi = lg_div(static_cast<uint32_t>(r), fdM), lo = static_cast<uint32_t>(r) - hi * fdM.d;
-        const uint32_t b = nm ? lo : hi, n = nm ? hi : lo;
+        const uint32_t n = nm ? hi : lo;
         if (slot[n] >= 0) continue;
-        f32x4 v[CH];
-        if (dropout) ni_stream_select<CH>(key, static_cast<uint64_t>(b) * N + n, q, thr, t, v);
-        else
+        const uint32_t kb = kbits[rl][q] >> (4 * mt);
+        f32x4 v;
 #pragma unroll
-            for (int mt = 0; mt < CH; ++mt) v[mt] = t[mt];
-#pragma unroll
-        for (int mt = 0; mt < CH; ++mt) st4(x0 + r * D + 16 * mt + 4 * q, v[mt]);
+        for (int i = 0; i < 4; ++i) v[i] = ((kb >> i) & 1u) ? t[i] : 0.0f;
+        st4(x0 + r * D + 4 * fg, v);
     }
 }
 
@@ -443,12 +469,14 @@ extern "C" int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* 
     hipStream_t s = lg_stream(stream);
     const int RPBD = 256 / (static_cast<int>(D) / 4);
     const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * B, RPBD), lg_num_cus())));
+    // the first GS workgroups form the sensor rows, one workgroup per kNiRowsPerBlock rows after
+    const unsigned grid = static_cast<unsigned>(GS + ceil_div(R, kNiRowsPerBlock));
     if (D == 64)
-        lg_launch(k_node_init_proj<64, 64>, std::max<unsigned>(ni_grid(R), GS), 256, 0, s, sensor_slot, sensor_idx,
-                  h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
+        lg_launch(k_node_init_proj<64, 64>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, x0, B, N, fdM, nm,
+                  S, R, GS, dropout, dropout_p, scale, seed, salt);
     else
-        lg_launch(k_node_init_proj<32, 32>, std::max<unsigned>(ni_grid(R), GS), 256, 0, s, sensor_slot, sensor_idx,
-                  h_s, W, bias, x0, B, N, fdM, nm, S, R, GS, dropout, dropout_p, scale, seed, salt);
+        lg_launch(k_node_init_proj<32, 32>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, x0, B, N, fdM, nm,
+                  S, R, GS, dropout, dropout_p, scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
@@ -516,7 +544,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 19; }
+extern "C" int lg_abi_version(void) { return 20; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

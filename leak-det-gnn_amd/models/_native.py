@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 19  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 20  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -23,6 +23,7 @@ LG_F_DROPOUT = 0x04
 LG_F_MASK_IN = 0x08
 LG_F_MASK_OUT = 0x10
 LG_F_NODE_MAJOR = 0x20
+LG_F_DX_SENSOR_ROWS = 0x10000000  # lg_gcn_bwd_nm[_bits] with node_slot: non-sensor dx rows may stay unwritten
 LG_SALT_SEED_PTR = 0x80000000  # salt bit 31: `seed` is the address of a device-resident uint64
 LG_F_LAB_V1 = 0x00800000  # kernel-lab schedule bit of lg_gcn_fwd_nm (tools/kbench.py)
 LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 3-way split bf16 MFMA)

@@ -466,6 +466,8 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
     for l in range(L - 1, -1, -1):
         ws = wss[l]
         flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
+        if l == 0:  # lg_sensor_proj_bwd reads only the sensor rows of layer 0's dx
+            flags |= nat.LG_F_DX_SENSOR_ROWS
         dx = torch.empty_like(dy)
         dW = torch.empty(D, D, device=dev, dtype=torch.float32)
         db = torch.empty(D, device=dev, dtype=torch.float32)

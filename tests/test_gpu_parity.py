@@ -798,3 +798,44 @@ def test_gcn_node_major_mask_bits_equal_y_gather(D, B):
     assert torch.equal(outs[0][0], outs[1][0]), "dx: mask bits differ from the y gather"
     for a, c, name in zip(outs[0][1:], outs[1][1:], ("dW", "db", "node bias")):  # slab grouping may differ
         assert_close(c, a, rtol=1e-6, atol=1e-7, what=name)
+
+
+@pytest.mark.parametrize("D,B", [(64, 256), (64, 37), (32, 40)])
+def test_gcn_bwd_dx_sensor_rows_only(D, B):
+    """LG_F_DX_SENSOR_ROWS (ABI 20, layer 0's backward in the detector): the sensor rows of dx
+    are bit for bit those of the full backward, the non-sensor rows are left as they were
+    (sentinel), and dW / db / node-bias sums are bitwise unchanged (same tiles, same order)."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    N = 661
+    graph = GCNGraph.build(torch.from_numpy(load("graph_ltown_a.npz")["edge_index"]), N, DEV)
+    st = ops.stream_of(graph.w)
+    gen = torch.Generator().manual_seed(7 * D + B)
+    x = torch.randn(N, B, D, generator=gen).relu().to(DEV)
+    W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
+    dy = torch.randn(N, B, D, generator=gen).to(DEV)
+    slot = torch.full((N,), -1, dtype=torch.int32)
+    sens = torch.randperm(N, generator=gen)[:29]
+    slot[sens] = torch.arange(29, dtype=torch.int32)
+    slot = slot.to(DEV)
+    sc = 1.0 / 0.9
+    outs = []
+    for only in (False, True):
+        dx = torch.full_like(x, 12345.0)
+        dW, db, dnb = torch.empty(D, D, device=DEV), torch.empty(D, device=DEV), torch.empty(D, device=DEV)
+        ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
+        flags = ops.nat.LG_F_MASK_OUT | (ops.nat.LG_F_DX_SENSOR_ROWS if only else 0)
+        ops.check(lib.lg_gcn_bwd_nm_bits(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t), ops.ptr(dy), None,
+                                         ops.ptr(x), ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db), ops.ptr(slot),
+                                         ops.ptr(dnb), B, N, D, flags, sc, sc, ops.ptr(ws), st, None), "bwd")
+        torch.cuda.synchronize()
+        outs.append((dx, dW, db, dnb))
+    full, part = outs
+    sens_d = sens.to(DEV)
+    assert torch.equal(part[0][sens_d], full[0][sens_d]), "sensor rows of dx changed"
+    keep = torch.ones(N, dtype=torch.bool, device=DEV)
+    keep[sens_d] = False
+    assert bool((part[0][keep] == 12345.0).all()), "non-sensor rows of dx were written"
+    for a, c, name in zip(full[1:], part[1:], ("dW", "db", "node bias")):
+        assert torch.equal(a, c), name

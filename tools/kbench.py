@@ -197,6 +197,7 @@ def main():
                             ("gcn_bwd_nm_pc", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC,
                              False),
                             ("gcn_bwd_nm_l0", nat.LG_F_MASK_OUT, True),
+                            ("gcn_bwd_nm_l0s", nat.LG_F_MASK_OUT | nat.LG_F_DX_SENSOR_ROWS, True),
                             ("gcn_bwd_nm_l0_nm3f16", nat.LG_F_MASK_OUT | nat.LG_F_F16X2, True),
                             ("gcn_bwd_nm_l0_pc", nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC, True),
                             ("gcn_bwd_nm_l0_old", nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, True)):
@@ -228,6 +229,19 @@ def main():
         else:
             byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
         res[name] = {"us": t, "GBps": byts / t / 1e3}
+    if "node_init" in which:  # sensor projection + node init (x0 = B*N*D fp32 written, node-major)
+        S5 = 29
+        slot = torch.full((N,), -1, dtype=torch.int32, device=dev)
+        slot[:S5] = torch.arange(S5, dtype=torch.int32, device=dev)
+        sidx = torch.arange(S5, dtype=torch.int64, device=dev)
+        hs = torch.randn(B, S5, D, device=dev)
+        Wp = torch.randn(D, D + 1, device=dev) / 8
+        x0 = torch.empty(N, B, D, device=dev)
+        f = lambda: check(lib.lg_node_init_proj_fwd(ptr(slot), ptr(sidx), ptr(hs), ptr(Wp), ptr(bias), ptr(x0), B, N,
+                                                    S5, D, D, nat.LG_F_DROPOUT | nat.LG_F_NODE_MAJOR, 0.1, 123, 0,
+                                                    cs()), "node_init")
+        t = timeit(f, args.iters)
+        res["node_init"] = {"us": t, "GBps": 4 * B * N * D / t / 1e3}
     if "c5_fwd" in which or "c5_bwd" in which or "c5_fwd_wm" in which:  # BASELINE configs[4]: one 100k-node graph, B = 1, GCNConv's launches
         from models.synth import synthetic_pipe_graph
         ei5, _ = synthetic_pipe_graph(100_000, 150_000, seed=0)
