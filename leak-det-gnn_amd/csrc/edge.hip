@@ -624,7 +624,10 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden) {
     if (B < 0 || P < 0 || hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int64_t SL = HID * 3 * D + 2 * HID + 1;
-    const int64_t G = bwd_grid(cdiv(std::max<int64_t>(B * P, 1), tile_rows(D)));
+    // rows for the larger of the two grids: tile-strided (lg_edge_head_bwd) and one workgroup per
+    // window (lg_edge_head_bwd_scatter), which is the larger when P < 2048 / D pipes
+    const int64_t G = std::max<int64_t>(bwd_grid(cdiv(std::max<int64_t>(B * P, 1), tile_rows(D))),
+                                        std::max<int64_t>(1, std::min<int64_t>(B, lg_num_cus())));
     return ((G * SL * 4 + 255) & ~int64_t(255)) + G * 8;
 }
 

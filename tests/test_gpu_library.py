@@ -273,16 +273,20 @@ def test_reduce_batch_matches_per_op_reductions():
             assert torch.equal(g, ref), f"{n}: batched reduction differs"
 
 
-@pytest.mark.parametrize("B", [3, 64, 300])
-def test_fused_pipe_scatter_matches_two_launches(B):
+@pytest.mark.parametrize("B,npipes", [(3, None), (64, None), (300, None), (37, 6)])
+def test_fused_pipe_scatter_matches_two_launches(B, npipes):
     """lg_edge_head_bwd_scatter (the incidence scatter fused into the EdgeHead backward, one
     workgroup per window) against lg_edge_head_bwd + lg_pipe_scatter_bwd: the node gradient
     is the same sums in the same order, so every gradient upstream of it (trunk, GRU, sensor
     projection, NoLeakHead) is bitwise equal; the EdgeHead's weight gradients change only by
     the slab grouping of the fixed-order reduction (window-owned tiles).  B = 3: window-major
-    trunk; 64: node-major; 300: more windows than CUs (several windows per workgroup)."""
+    trunk; 64: node-major; 300: more windows than CUs (several windows per workgroup); 6 pipes
+    (the synthetic training sets): fewer pipe rows than a tile, so the per-window grid is larger
+    than the tile grid the workspace used to be sized for."""
     from models.detector import LeakDetector
     sensors, pipes = lta_ids()
+    if npipes is not None:
+        pipes = pipes[:npipes]
     torch.manual_seed(5)
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
     r = torch.randn(B, 36, 29, device=DEV)
