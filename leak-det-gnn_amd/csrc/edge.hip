@@ -287,8 +287,17 @@ struct EdgeScatter {
 // dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
 // group in flight, the first four incidences of each in one batch; the same sums, in the same
 // order, as k_pipe_scatter (heads.hip).
-constexpr int kScatNodes = 2;
-template <int D>
+// The scatter is latency-bound (each round: CSR from LDS, rows from L2, sum, store), so the
+// number of nodes in flight sets its time; it is limited by the registers live beside it.
+// Inside the tile loop (a window that is not the workgroup's last) the split W1 and the dW1
+// accumulators are live: kScatNodesLoop.  The last window is scattered after the loop, once the
+// weight-gradient slab is written and those registers are dead: kScatNodesTail.
+constexpr int kScatNodesLoop = 2;  // 11 dependent rounds per window at L-TOWN-A
+#ifndef LG_SCAT_NODES_TAIL
+#define LG_SCAT_NODES_TAIL 8
+#endif
+constexpr int kScatNodesTail = LG_SCAT_NODES_TAIL;  // 3 rounds
+template <int D, int kScatNodes>
 __device__ __forceinline__ void edge_scatter_window(const EdgeScatter& sc, const int32_t* icsr, const float* dpipe,
                                                     uint32_t win) {
     constexpr int LPR = D / 4, SLOTS = NT / LPR;
@@ -512,9 +521,10 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             }
         }
         if constexpr (SCAT) {
-            if (k % sc.tpw == sc.tpw - 1) {  // the window's last tile: its node gradients
-                __syncthreads();             // every wave's dpipe rows of the window are stored
-                edge_scatter_window<D>(sc, icsr, dpipe, static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep));
+            if (k % sc.tpw == sc.tpw - 1 && k + 1 < nk) {  // a window's last tile (not the workgroup's last window)
+                __syncthreads();                            // every wave's dpipe rows of the window are stored
+                edge_scatter_window<D, kScatNodesLoop>(sc, icsr, dpipe,
+                                                       static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep));
             }
         }
     }
@@ -560,6 +570,13 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         double s = find[NW * 32 * 4];
         for (int i = 1; i < NW; ++i) s += find[NW * 32 * 4 + i];
         db2slab[blockIdx.x] = s;
+    }
+    if constexpr (SCAT) {
+        if (nk > 0) {  // the last window's node gradients (its dpipe rows were stored before the barriers above)
+            __syncthreads();
+            edge_scatter_window<D, kScatNodesTail>(sc, icsr, dpipe,
+                                                   static_cast<uint32_t>(blockIdx.x + ((nk - 1) / sc.tpw) * gstep));
+        }
     }
 }
 
