@@ -624,9 +624,13 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 
-# False: the EdgeHead backward and the pipe scatter as two launches (lg_edge_head_bwd +
-# lg_pipe_scatter_bwd; same results)
-_FUSED_SCATTER = True
+# True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter); False:
+# two launches (lg_edge_head_bwd + lg_pipe_scatter_bwd).  Same node gradient bit for bit.
+# Measured at B = 256 (profiles/r03/r03ak-am): the fused kernel takes 152.6 us where the two
+# launches take 112 + 34 us.  With one window per workgroup every workgroup reaches its scatter
+# at the same time, after its MFMA work, so the scatter's 143 MB (the pipe rows have already
+# left the XCD's L2) overlap nothing; the separate launch runs it over the whole chip.
+_FUSED_SCATTER = False
 
 
 def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N, D,

@@ -292,6 +292,7 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
     r = torch.randn(B, 36, 29, device=DEV)
     tf = torch.randn(B, 36, 9, device=DEV)
     grads = []
+    saved = library._FUSED_SCATTER
     for fused in (True, False):
         library._FUSED_SCATTER = fused
         try:
@@ -300,7 +301,7 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
             m(r, tf).square().mean().backward()
             torch.cuda.synchronize()
         finally:
-            library._FUSED_SCATTER = True
+            library._FUSED_SCATTER = saved
         grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
     for n, g in grads[0].items():
         ref = grads[1][n]
