@@ -626,11 +626,11 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
 
 # True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter); False:
 # two launches (lg_edge_head_bwd + lg_pipe_scatter_bwd).  Same node gradient bit for bit.
-# Measured at B = 256 (profiles/r03/r03ak-am): the fused kernel takes 152.6 us where the two
-# launches take 112 + 34 us.  With one window per workgroup every workgroup reaches its scatter
-# at the same time, after its MFMA work, so the scatter's 143 MB (the pipe rows have already
-# left the XCD's L2) overlap nothing; the separate launch runs it over the whole chip.
-_FUSED_SCATTER = False
+# Measured at B = 256: fused 152.6 us, step 0.659 ms (profiles/r03/r03al); two launches
+# 114.6 + 35.3 us, step 0.662 ms (r03am) -- equal within box-to-box noise.  With one window
+# per workgroup every workgroup reaches its scatter at the same time, after its MFMA work, so
+# the scatter's traffic overlaps nothing; the fused form saves the launch.
+_FUSED_SCATTER = True
 
 
 def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N, D,
