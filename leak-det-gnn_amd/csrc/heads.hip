@@ -88,21 +88,10 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
     const uint32_t thr = lg_keep_threshold16(p);
     if (static_cast<int>(blockIdx.x) < GS) {
         const int rl = threadIdx.x / LPR, fg = threadIdx.x % LPR;
-        // o fastest: conflict-free LDS writes; every load issued before the first store
-        constexpr int WIT = (D * (DS + 1) + 255) / 256;
-        float wv[WIT];
-#pragma unroll
-        for (int u = 0; u < WIT; ++u) {
-            const int i = u * 256 + threadIdx.x, k = i / D, o = i % D;
-            wv[u] = i < D * (DS + 1) ? W[o * (DS + 1) + k] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < WIT; ++u) {
-            const int i = u * 256 + threadIdx.x, k = i / D, o = i % D;
-            if (i < D * (DS + 1)) {
-                if (k < DS) wt[k][o] = wv[u];
-                else bf[o] = wv[u] + bias[o];
-            }
+        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {  // o fastest: conflict-free LDS writes
+            const int k = i / D, o = i % D;
+            if (k < DS) wt[k][o] = W[o * (DS + 1) + k];
+            else bf[o] = W[o * (DS + 1) + DS] + bias[o];
         }
         __syncthreads();
         const f32x4 bs = ld4(bf + 4 * fg);
@@ -111,19 +100,12 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
             if (slot[n] != sc) continue;  // a duplicated sensor id: the last one's row wins (detector.py:181)
             const float* hrow = hs + (b * S + sc) * DS;
             f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 hv[DS / 4];  // the whole h_s row in flight at once
-#pragma unroll
-            for (int k4 = 0; k4 < DS / 4; ++k4) hv[k4] = ld4(hrow + 4 * k4);
-            // W^T reads are loop-invariant: an opaque zero offset keeps the compiler from hoisting
-            // all of them (256 VGPRs) out of the row loop
-            int wz = 0;
-            asm volatile("" : "+s"(wz));
-#pragma unroll 2
+#pragma unroll 4
             for (int k4 = 0; k4 < DS / 4; ++k4) {
-                const f32x4 h4 = hv[k4];
+                const f32x4 h4 = ld4(hrow + 4 * k4);
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) {
-                    const f32x4 w = ld4(&wt[4 * k4 + kk][4 * fg] + wz);
+                    const f32x4 w = ld4(&wt[4 * k4 + kk][4 * fg]);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) acc[i] = fmaf(h4[kk], w[i], acc[i]);
                 }
@@ -486,9 +468,7 @@ extern "C" int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* 
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     hipStream_t s = lg_stream(stream);
     const int RPBD = 256 / (static_cast<int>(D) / 4);
-    // sensor workgroups: one pass each up to 2 per CU (their W staging and row loads are latency
-    // chains; with one per CU they outlasted the bulk rows)
-    const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * B, RPBD), 2 * lg_num_cus())));
+    const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * B, RPBD), lg_num_cus())));
     // the first GS workgroups form the sensor rows, one workgroup per kNiRowsPerBlock rows after
     const unsigned grid = static_cast<unsigned>(GS + ceil_div(R, kNiRowsPerBlock));
     if (D == 64)

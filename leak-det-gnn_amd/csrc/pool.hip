@@ -29,24 +29,14 @@ __device__ __forceinline__ void pool_window(const float* __restrict__ x, int64_t
     const int g = threadIdx.x / LPR, fg = threadIdx.x % LPR;
     const float* xb = x + b * sb * D + 4 * fg;
     const int64_t step = sn * D;
-    // U independent loads in flight per lane (a window's rows are 256-byte pieces B * D * 4
-    // bytes apart in the node-major layout: the pass is load-latency-bound, not HBM-bound);
-    // accumulator u takes rows g + (U k + u) G, folded in a fixed tree
-    constexpr int U = 8;
-    f32x4 a[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int64_t n0 = g; n0 < N; n0 += U * G) {
-        f32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t n = n0 + u * G;
-            v[u] = n < N ? ld4(xb + n * step) : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) a[u] += v[u];
+    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    int64_t n = g;
+    for (; n + G < N; n += 2 * G) {  // two independent loads in flight per lane
+        a0 += ld4(xb + n * step);
+        a1 += ld4(xb + (n + G) * step);
     }
-    part[threadIdx.x] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    if (n < N) a0 += ld4(xb + n * step);
+    part[threadIdx.x] = a0 + a1;
     __syncthreads();
     if (threadIdx.x < D) {
         const int d = threadIdx.x, f = d / 4, i = d % 4;
