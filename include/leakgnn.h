@@ -83,44 +83,21 @@ enum {
  * captured HIP graph of a training step then re-draws its dropout streams on each replay by
  * refreshing that word on the device, with no host involvement. */
 #define LG_SALT_SEED_PTR 0x80000000u
-/* Tuning bits of lg_gcn_fwd_nm (kernel lab, tools/kbench.py): they pick a schedule and never
- * change results.  LG_F_LAB_V1: the one-tile-per-wave kernel; bits 24..27: workgroups of
- * 4 waves per CU for the software-pipelined kernel (0 = default). */
-#define LG_F_LAB_V1        0x00800000
-/* lg_gcn_fwd_nm transform: by default on bf16 MFMA with 3-way split fp32 operands
- * (|error| <= ~2^-23 relative per product, fp32 accumulate: fp32-level accuracy, not
- * bit-identical to lg_gcn_fwd); LG_F_F32_MFMA = exact v_mfma_f32_16x16x4_f32, bit-identical
- * to lg_gcn_fwd on the transposed layout. */
+/* lg_gcn_fwd_nm[_bits] kernel and transform.  No bit: the fp32 tier runs the producer /
+ * consumer pipeline (k_gcn_fwd_pc: gather waves hand (A x) tiles to MFMA waves through an LDS
+ * ring) with the transform as a 2-way fp16 split with power-of-two block scaling (3 f16 MFMAs
+ * per product; fp32-level accuracy, ~4e-7 of max |y|); the bf16 tier (LG_F_BF16) the per-wave
+ * pipeline k_gcn_fwd_nm3 with ONE bf16 product.
+ *   LG_F_BF16X3: the pc pipeline with the 3-way bf16 split (6 bf16 MFMAs per product, ~1e-8 of
+ *                max |y|; bit-identical to LG_F_NM3);
+ *   LG_F_NM3:    the per-wave pipeline with the 3-way bf16 split;
+ *   LG_F_F32_MFMA: the per-wave pipeline on exact v_mfma_f32_16x16x4_f32 (bit-identical to
+ *                lg_gcn_fwd on the transposed layout);
+ *   LG_F_PC:     with LG_F_BF16: the pc pipeline's single bf16 product. */
 #define LG_F_F32_MFMA      0x00400000
-/* lg_gcn_fwd_nm schedule bits (kernel lab; results unchanged): LG_F_LAB_NM2 = the pipeline
- * that walks rowptr per tile (round-1 kernel), LG_F_LAB_W8 = 8-wave workgroups. */
-#define LG_F_LAB_NM2       0x00200000
-#define LG_F_LAB_W8        0x00100000
-#define LG_F_LAB_W5        0x00040000  /* lab: 5-wave workgroups (3 per CU: 15 waves) */
-#define LG_F_LAB_DST       0x00080000  /* lab: epilogue stores straight from the MFMA layout */
-
-#define LG_F_LAB_BPC_SHIFT 24
-/* lg_gcn_fwd_nm schedule: the W-in-registers pipeline (2 waves/SIMD, no workgroup staging);
- * results identical to the default pipeline */
-#define LG_F_NM5           0x00002000
-/* lg_gcn_fwd_nm schedule: producer / consumer waves (gather waves hand tiles to MFMA waves
- * through an LDS ring); results identical to the default pipeline */
 #define LG_F_PC            0x00004000
-/* lg_gcn_fwd_nm with LG_F_NM5 or LG_F_PC: the transform as a 2-way fp16 split with power-of-two block
- * scaling (3 f16 MFMAs per product instead of 6 bf16 ones; fp32-level accuracy, not bit-
- * identical to the 3-way bf16 split) */
-#define LG_F_F16X2         0x00008000
-/* with LG_F_PC: one consumer wave per producer (default two) */
-#define LG_F_PC1           0x00010000
-/* lg_gcn_fwd_nm schedule: the per-wave pipeline (k_gcn_fwd_nm3) with the 3-way bf16 split.
- * Without any schedule bit the fp32 tier runs the producer / consumer pipeline with the
- * 2-way fp16 split (LG_F_PC | LG_F_F16X2), the bf16 tier nm3's single bf16 product. */
+#define LG_F_BF16X3        0x00008000
 #define LG_F_NM3           0x00020000
-/* with LG_F_PC: six producer waves with one consumer each (default four with two) */
-#define LG_F_PC6           0x00000080
-/* lab builds only: bits 8..11 pick the lg_gcn_fwd_nm (D = 64) kernel's OPT variant */
-#define LG_F_LAB_OPT       0x00001000
-#define LG_F_LAB_OPT_SHIFT 8
 
 int lg_abi_version(void);
 
@@ -180,7 +157,7 @@ int lg_cross_entropy_bwd(const float* logits, const int64_t* target, const float
  * The norm is summed in fp64 in a fixed order (deterministic). */
 int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T);
 int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
-                  float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace,
+                  float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace, int64_t ws_bytes,
                   lg_stream_t stream);
 
 /* Kernel timing (bench.py; no reference counterpart — the reference has no kernels).
@@ -220,7 +197,7 @@ int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
                    int add_self_loops, int normalize, float fill_value,
                    int32_t* rowptr, int32_t* col, float* w,
                    int32_t* rowptr_t, int32_t* col_t, float* w_t,
-                   void* workspace, lg_stream_t stream);
+                   void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* Node table of the node-major kernels, once per graph (and once for the transposed CSR):
  * one 64-byte record per node = {e0, e1, (col, float_as_int(w)) x 6, self, node} so a tile
@@ -252,7 +229,7 @@ int lg_rcm_order(const int64_t* edge_index, int64_t E, int64_t N, int32_t* order
 int64_t lg_incidence_workspace_bytes(int64_t P, int64_t N);
 int lg_incidence_build(const int64_t* ends, int64_t P, int64_t N,
                        int32_t* inc_rowptr, int32_t* inc_item,
-                       void* workspace, lg_stream_t stream);
+                       void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* K3  disjoint-union edge index (bit-exact).
  * Replaces: detector.py:105-114 `_batchify_edge_index`:  out[:, b*E + e] = ei[:, e] + b*N.
@@ -292,7 +269,7 @@ int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx,
 int64_t lg_sensor_proj_bwd_workspace_bytes(int64_t B, int64_t S, int64_t Ds, int64_t D);
 int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, const float* live, const float* h_s,
                        const float* W, const float* dbias_in, float* dh_s, float* dW, float* db, int64_t B,
-                       int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace,
+                       int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace, int64_t ws_bytes,
                        lg_stream_t stream);
 
 /* K2 backward (node init Linear(Ds+1 -> D), detector.py:160, 184-189), weight side:
@@ -305,7 +282,7 @@ int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, const float*
  * (K = 7,424) torch.mm of the autograd of torch.addmm. */
 int64_t lg_linear_dw_workspace_bytes(int64_t K, int64_t M, int64_t N);
 int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t M, int64_t N,
-                 float* dw, float* db, void* workspace, lg_stream_t stream);
+                 float* dw, float* db, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* nnz_cap (lg_gcn_fwd / lg_spmm / lg_gcn_bwd): capacity of col/w as allocated for
  * lg_graph_build (E + N).  It sizes the on-chip copy of the CSR: when
@@ -352,7 +329,7 @@ int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D);
 int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                   const float* x, const float* W, float* dx_out, float* dW, float* db,
                   const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
-                  int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream);
+                  int flags, float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* The layer's output mask as bits (ABI 15).  lg_gcn_fwd_nm_bits = lg_gcn_fwd_nm that also
  * writes ymask (when non-NULL): [y > 0] of every output element, one uint16 per lane and
@@ -376,7 +353,7 @@ int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float
 int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                        const float* x, const float* W, float* dx_out, float* dW, float* db,
                        const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
-                       int flags, float scale_in, float scale_out, void* workspace, lg_stream_t stream,
+                       int flags, float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream,
                        const uint16_t* ymask);
 
 /* Single graph (B = 1) on the node tables (ABI 18): the GCNConv module's own call shape,
@@ -391,7 +368,7 @@ int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const f
 int lg_gcn_fwd_rows(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W, const float* bias,
                     float* y, int64_t N, int64_t D, int flags, lg_stream_t stream);
 int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* x,
-                    const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace,
+                    const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace, int64_t ws_bytes,
                     lg_stream_t stream);
 
 /* Plain propagate y = Ahat x (PyG MessagePassing.propagate with the gcn_norm
@@ -421,7 +398,7 @@ int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t,
                const int32_t* node_slot, float* dnode_bias,
                int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                int flags, float scale_in, float scale_out,
-               void* workspace, lg_stream_t stream);
+               void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* K8 forward: per-pipe endpoint gather + EdgeHead feature build.
  * Replaces: detector.py:206-210 and :87  feat = cat[h_u, h_v, |h_u - h_v|].
@@ -463,7 +440,7 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
                      const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
                      float* dw1, float* db1, float* dw2, float* db2,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
-                     int flags, float dropout_p, void* workspace, lg_stream_t stream);
+                     int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 /* lg_edge_head_bwd followed by lg_pipe_scatter_bwd (dh = dpool / N + the incidence sums of
  * dpipe; reference detector.py:206-211 and the backward of its gather), with the scatter
  * FUSED into the backward kernel: each workgroup owns whole windows and sums a window's node
@@ -478,7 +455,7 @@ int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w
                              float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
                              const int32_t* inc_item, const float* dpool, float* dh,
                              int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
-                             int flags, float dropout_p, void* workspace, lg_stream_t stream);
+                             int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* K10 forward: per-window mean over the N node rows.
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)
@@ -505,7 +482,7 @@ int lg_pool_head_bwd(const float* pooled, const float* hid, const float* w1, con
                      const float* dlogits, int64_t ldo, int64_t col, float* dpooled,
                      float* dw1, float* db1, float* dw2, float* db2,
                      int64_t B, int64_t D, int64_t hidden, int flags, float dropout_p,
-                     void* workspace, lg_stream_t stream);
+                     void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* ---------------------------------------------------------------------------
  * SharedSensorGRUEncoder (detector.py:28-73): one nn.GRU(1 [+9], H) over the
@@ -530,7 +507,7 @@ int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, con
                const float* h_seq, const float* gates, const float* dh_last,
                float* dx, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H,
-               void* workspace, lg_stream_t stream);
+               void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
 /* ---- Frozen-predictor residual builder (SURVEY 8 f rank 1) ----------------------
  * Replaces the per-window NormalPredictorTCN passes of

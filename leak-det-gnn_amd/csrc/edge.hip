@@ -653,7 +653,7 @@ namespace {
 int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const float* w2, const float* hid,
                   const float* dlogits, int64_t ldo, float* dpipe, float* dw1, float* db1, float* dw2, float* db2,
                   int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
-                  void* workspace, lg_stream_t stream, const EdgeScatter* scat) {
+                  void* workspace, int64_t ws_bytes, lg_stream_t stream, const EdgeScatter* scat) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
@@ -671,6 +671,8 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
     const int grid = scat ? static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(B, lg_num_cus()))) : bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const int64_t SL = HID * 3 * D + 2 * HID + 1;
+    // the slab the launch grid writes: a row per workgroup + one fp64 per workgroup
+    if (ws_bytes < ((grid * SL * 4 + 255) & ~int64_t(255)) + grid * 8) return LG_EINVAL;
     float* slab = static_cast<float*>(workspace);
     double* dslab = reinterpret_cast<double*>(static_cast<char*>(workspace) + ((grid * SL * 4 + 255) & ~int64_t(255)));
     hipStream_t s = lg_stream(stream);
@@ -711,9 +713,9 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
 extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
                                 const float* hid, const float* dlogits, int64_t ldo, float* dpipe, float* dw1,
                                 float* db1, float* dw2, float* db2, int64_t B, int64_t N, int64_t P, int64_t D,
-                                int64_t hidden, int flags, float dropout_p, void* workspace, lg_stream_t stream) {
+                                int64_t hidden, int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
-                         dropout_p, workspace, stream, nullptr);
+                         dropout_p, workspace, ws_bytes, stream, nullptr);
 }
 
 extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
@@ -721,16 +723,16 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                                         float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
                                         const int32_t* inc_item, const float* dpool, float* dh, int64_t B, int64_t N,
                                         int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
-                                        void* workspace, lg_stream_t stream) {
+                                        void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (!dh || !inc_rowptr || (P > 0 && !inc_item)) return LG_EINVAL;
     if (B == 0) return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D,
-                                     hidden, flags, dropout_p, workspace, stream, nullptr);
+                                     hidden, flags, dropout_p, workspace, ws_bytes, stream, nullptr);
     const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS;
     if (P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
         // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
         const int rc = edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
-                                     flags, dropout_p, workspace, stream, nullptr);
+                                     flags, dropout_p, workspace, ws_bytes, stream, nullptr);
         if (rc != LG_OK) return rc;
         return lg_pipe_scatter_bwd(inc_rowptr, inc_item, dpipe, dpool, dh, B, N, P, D, flags & LG_F_NODE_MAJOR, stream);
     }
@@ -738,5 +740,5 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                    static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0,
                    static_cast<int>(cdiv(P, tile_rows(D)))};
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
-                         dropout_p, workspace, stream, &sc);
+                         dropout_p, workspace, ws_bytes, stream, &sc);
 }

@@ -763,7 +763,7 @@ extern "C" int64_t lg_gcn_bwd_workspace_bytes(int64_t D) {
 extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const float* w_t, const float* dy,
                           const float* y, const float* x, const float* W, float* dx_out, float* dW, float* db,
                           const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
-                          int64_t nnz_cap, int flags, float scale_in, float scale_out, void* workspace,
+                          int64_t nnz_cap, int flags, float scale_in, float scale_out, void* workspace, int64_t ws_bytes,
                           lg_stream_t stream) {
     if (B < 0 || N <= 0 || nnz_cap < 0) return LG_EINVAL;
     if (!rowptr_t || !col_t || !w_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
@@ -773,6 +773,8 @@ extern "C" int lg_gcn_bwd(const int32_t* rowptr_t, const int32_t* col_t, const f
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     const int64_t wpl = windows_per_launch(N, D);
     if (wpl < 1) return LG_EUNSUPPORTED;
+    // the launch grid is at most bwd_grid_max() workgroups, one slab row each
+    if (ws_bytes < lg_gcn_bwd_workspace_bytes(D)) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     float* slab = static_cast<float*>(workspace);
     const int mask_out = (flags & LG_F_MASK_OUT) ? 1 : 0;

@@ -31,10 +31,7 @@
 
 namespace {
 
-constexpr int kNmFwdWaves = 8;
-constexpr int kNmBwdWaves = 8;
 constexpr int kNmBwdWaves3 = 4;
-constexpr uint32_t kNmOob = 0xFFFFFFF0u;
 
 __device__ __forceinline__ f32x4 mfma_nm(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -62,19 +59,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t nm_rsrc(const float* p, uint64
                                              0x00020000);
 }
 
-// The block base goes into the VGPR offset, not soffset: a masked lane's offset must stay
-// beyond num_records after the whole address sum, so nothing may be added to kNmOob.
-template <int D>
-__device__ __forceinline__ f32x4 nm_ld(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, bool ok, uint32_t base) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? lane_off + base : kNmOob, 0, 0));
-}
-
-template <int AUX>
-__device__ __forceinline__ void nm_st(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, bool ok, uint32_t base, f32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rs,
-                                           ok ? lane_off + base : kNmOob, 0, AUX);
-}
-
 // 16-byte buffer stores read their data VGPRs after issue: keep those registers unwritten for a
 // few wait states.  Measured on k_gcn_bwd_pc (tools/bpc_check.py; profiles/r03/r03q-r03t): the
 // compiler reused a store's data registers for VALU results 0-1 instructions after the
@@ -97,428 +81,6 @@ __device__ __forceinline__ NmSched nm_sched(int64_t ntiles, int wave, int waves)
     const int64_t x = b % 8, k = b / 8, nbx = (G - x + 7) / 8, chunk = (ntiles + 7) / 8;
     return NmSched{x * chunk + k * waves + wave, std::min<int64_t>(ntiles, x * chunk + chunk), nbx * waves};
 }
-
-// acc[k] (gather layout: row RPI k + rl of the block, channels 4 fg..) =
-//   sum over CSR row n of w * src[m][b0..b0+15]   (MASK: src * mscale * [msk > 0]),
-// entries in CSR order, fp32 fma.  Two neighbours' blocks are in flight at a time.
-template <int D, bool MASK>
-__device__ __forceinline__ void gather_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs,
-                                          __amdgpu_buffer_rsrc_t src, __amdgpu_buffer_rsrc_t msk, float mscale,
-                                          uint32_t n, uint32_t B, uint32_t b0, const uint32_t (&loff)[NmGeo<D>::K],
-                                          const bool (&rv)[NmGeo<D>::K], f32x4 (&acc)[NmGeo<D>::K]) {
-    using G = NmGeo<D>;
-    const int e0 = __builtin_amdgcn_readfirstlane(tab[16 * n]);
-    const int e1 = __builtin_amdgcn_readfirstlane(tab[16 * n + 1]);
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto contrib = [&](float w, const f32x4& v, const f32x4& m, f32x4& a) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float t = v[i];
-            if constexpr (MASK) t = m[i] > 0.f ? t * mscale : 0.f;
-            a[i] = fmaf(w, t, a[i]);
-        }
-    };
-    int e = e0;
-    for (; e + 1 < e1; e += 2) {
-        const int2 pa = pairs[e], pb = pairs[e + 1];  // wave-uniform: scalar loads
-        const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-        const uint32_t bbase = (static_cast<uint32_t>(pb.x) * B + b0) * (4u * D);
-        f32x4 va[G::K], vb[G::K], ma[G::K], mb[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) {
-            va[k] = nm_ld<D>(src, loff[k], rv[k], ba);
-            vb[k] = nm_ld<D>(src, loff[k], rv[k], bbase);
-            if constexpr (MASK) {
-                ma[k] = nm_ld<D>(msk, loff[k], rv[k], ba);
-                mb[k] = nm_ld<D>(msk, loff[k], rv[k], bbase);
-            }
-        }
-        const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) {
-            contrib(wa, va[k], ma[k], acc[k]);
-            contrib(wb, vb[k], mb[k], acc[k]);
-        }
-    }
-    if (e < e1) {
-        const int2 pa = pairs[e];
-        const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-        f32x4 va[G::K], ma[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) {
-            va[k] = nm_ld<D>(src, loff[k], rv[k], ba);
-            if constexpr (MASK) ma[k] = nm_ld<D>(msk, loff[k], rv[k], ba);
-        }
-        const float wa = __int_as_float(pa.y);
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) contrib(wa, va[k], ma[k], acc[k]);
-    }
-}
-
-// ------------------------------------------------------------------ forward
-template <int D, bool DROP>
-__global__ void __launch_bounds__(64 * kNmFwdWaves)
-k_gcn_fwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
-             const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
-             uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
-             uint64_t seed, uint32_t salt) {
-    using G = NmGeo<D>;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* wl = reinterpret_cast<float*>(smem);  // W [out][in] * fold, stride S
-    float* bl = wl + D * G::S;                   // bias * fold
-    float* tiles = bl + D;
-
-    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmFwdWaves - 1) / (64 * kNmFwdWaves);
-    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
-    f32x4 wv[WPER];
-#pragma unroll
-    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmFwdWaves + threadIdx.x, W4 - 1));
-    const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
-#pragma unroll
-    for (int u = 0; u < WPER; ++u) {
-        const int i = u * 64 * kNmFwdWaves + threadIdx.x;
-        if (i < W4) st4(wl + (i / (D / 4)) * G::S + 4 * (i % (D / 4)), wv[u] * fold);
-    }
-    if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
-    __syncthreads();
-
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* tl = tiles + wave * G::TILE;
-    const uint32_t key = lg_dropout_key_dev(seed, salt);
-    const uint32_t thr = lg_keep_threshold16(p_drop);
-    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
-    uint32_t loff[G::K];
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
-
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmFwdWaves);
-    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
-        const uint32_t t32 = static_cast<uint32_t>(tile);
-        const uint32_t grp = lg_div(t32, fdN), n = t32 - grp * N, b0 = grp * 16;
-        const uint32_t nb = min(16u, B - b0);  // windows in this group (the last may be ragged)
-        bool rv[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
-        f32x4 acc[G::K];
-        gather_nm<D, false>(tab, pairs, xrs, xrs, 1.f, n, B, b0, loff, rv, acc);
-
-        // gather layout -> LDS -> MFMA B operand
-        wave_sync_nm();
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
-        wave_sync_nm();
-        f32x4 o[G::CH];
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
-#pragma unroll
-        for (int c = 0; c < G::CH; ++c) {
-            const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);  // W[16mt + j][16c + 4q + i]
-#pragma unroll
-                for (int i = 0; i < 4; ++i) o[mt] = mfma_nm(wa[i], bt[i], o[mt]);
-            }
-        }
-        // epilogue: ReLU, row-stream dropout (two channels per step) seeded with the window-major
-        // row id (b0 + j) N + n, so both layouts draw the same mask
-        uint32_t st = 0;
-        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) {
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                float t = fmaxf(o[mt][reg], relu_floor);
-                if constexpr (DROP) {
-                    if ((reg & 1) == 0) st = lg_xorshift32(st);
-                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
-                    t = u16 >= thr ? t : 0.0f;
-                }
-                o[mt][reg] = t;
-            }
-        }
-        wave_sync_nm();
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
-        wave_sync_nm();
-        const uint32_t ob = (n * B + b0) * (4u * D);
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) nm_st<2>(yrs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
-    }
-}
-
-// ------------------------------------------------------------------ forward, software-pipelined
-// Same math and bit-identical results as k_gcn_fwd_nm, reorganised so the HBM stream and
-// the MFMA transform overlap inside every wave: while tile i is transformed (64 MFMAs at
-// D = 64), the blocks of tile i+1's first NPF neighbours are already in flight in
-// registers (NPF x 16 rows x D floats = 16 KiB per wave at D = 64, NPF = 4).  Fewer waves
-// per CU (2-3 per SIMD) each walk ~5-8 tiles, so the pipeline reaches a steady state; the
-// one-tile-per-wave schedule of k_gcn_fwd_nm instead ran every wave's gather, then every
-// wave's MFMA burst, in lock step.  Neighbours past the NPF prefetched ones (degree > NPF)
-// are loaded in place, two at a time.  Accumulation order = CSR order in both kernels.
-constexpr int kNm2Waves = 4;
-
-// ---- 3-way bf16 split of fp32 operands (SPLIT transform): split_bf16.h ----------------
-
-// LAB (kernel-lab builds only, -DLG_KERNEL_LAB; results are WRONG when set): 1 = skip the
-// MFMA transform, 2 = skip the neighbour loads — the memory-only and compute-only floors.
-// SPLIT: the transform on bf16 MFMA with 3-way split operands (above) instead of
-//   v_mfma_f32_16x16x4_f32; W's three parts are staged once per workgroup in LDS.
-// Measured and dropped (B = 256, L-TOWN-A): two tiles in flight per wave at 2 waves/SIMD
-// (+15-25 %, occupancy), the CSR staged in LDS per workgroup (+3.5 us of prologue), the
-// MFMA-operand gather layout without the LDS transposes (16 rows x 64 B per instruction:
-// the load stream alone 15 -> 25 us).
-template <int D, bool SPLIT>
-struct Nm2Lds {  // dynamic LDS layout (floats)
-    static constexpr int SB = D + 8;  // bf16 row stride of the split W parts
-    static constexpr int WF = SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
-    static constexpr int TILES = WF + D;                                // after W and bias
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + kNm2Waves * NmGeo<D>::TILE);
-};
-
-template <int D, int NPF>
-struct NmSlot {  // one tile in flight: its CSR range, weights and first NPF neighbour blocks
-    f32x4 pf[NPF][NmGeo<D>::K];
-    float pw[NPF];
-    int e0, e1;
-    uint32_t n, b0, nb;
-};
-
-template <int D, bool DROP, int NPF, bool SPLIT, int LAB = 0>
-__global__ void __launch_bounds__(64 * kNm2Waves)
-k_gcn_fwd_nm2(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
-              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
-              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float relu_floor, float p_drop, float dscale,
-              uint64_t seed, uint32_t salt) {
-    using G = NmGeo<D>;
-    using LY = Nm2Lds<D, SPLIT>;
-    constexpr int SB = LY::SB;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* wl = reinterpret_cast<float*>(smem);         // fp32: W [out][in] * fold, stride S
-    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB
-    float* bl = wl + LY::WF;                            // bias * fold
-    float* tiles = wl + LY::TILES;
-
-    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNm2Waves - 1) / (64 * kNm2Waves);
-    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
-    {
-        f32x4 wv[WPER];
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNm2Waves + threadIdx.x, W4 - 1));
-        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) {
-            const int i = u * 64 * kNm2Waves + threadIdx.x;
-            if (i >= W4) continue;
-            const int o = i / (D / 4), c4 = 4 * (i % (D / 4));
-            const f32x4 w = wv[u] * fold;
-            if constexpr (SPLIT) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t p0 = pk_bf16(w[2 * h], w[2 * h + 1]);
-                    const float ra = w[2 * h] - bf_lo(p0), rb = w[2 * h + 1] - bf_hi(p0);
-                    const uint32_t p1 = pk_bf16(ra, rb);
-                    const uint32_t p2 = pk_bf16(ra - bf_lo(p1), rb - bf_hi(p1));
-                    const int e = o * SB + c4 + 2 * h;
-                    *reinterpret_cast<uint32_t*>(wsl + e) = p0;
-                    *reinterpret_cast<uint32_t*>(wsl + D * SB + e) = p1;
-                    *reinterpret_cast<uint32_t*>(wsl + 2 * D * SB + e) = p2;
-                }
-            } else {
-                st4(wl + o * G::S + c4, w);
-            }
-        }
-        if (threadIdx.x < D) bl[threadIdx.x] = bb * fold;
-    }
-
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* tl = tiles + wave * G::TILE;
-    const uint32_t key = lg_dropout_key_dev(seed, salt);
-    const uint32_t thr = lg_keep_threshold16(p_drop);
-    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
-    uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
-
-    auto csr_row = [&](uint32_t n, int& e0, int& e1) {  // wave-uniform: scalar loads
-        e0 = __builtin_amdgcn_readfirstlane(tab[16 * n]);
-        e1 = __builtin_amdgcn_readfirstlane(tab[16 * n + 1]);
-    };
-    auto csr_pair = [&](int e) -> int2 { return pairs[e]; };
-
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNm2Waves);
-
-    // Straight-line issue (no branch around the vector loads, so the compiler counts them
-    // statically and waits per neighbour with vmcnt(n)): slots past the degree, and every
-    // slot past the wave's last tile, load with an out-of-range offset (0, no request).
-    NmSlot<D, NPF> sl;
-    auto issue = [&](NmSlot<D, NPF>& S, int64_t tile) {
-        const bool valid = tile < sc.end;
-        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
-        const uint32_t grp = lg_div(t32, fdN);
-        S.n = t32 - grp * N;
-        S.b0 = grp * 16;
-        S.nb = valid ? min(16u, B - S.b0) : 0u;
-        int e0 = 0, e1 = 0;
-        if (valid) csr_row(S.n, e0, e1);
-        S.e0 = e0;
-        S.e1 = e1;
-#pragma unroll
-        for (int i = 0; i < NPF; ++i) {
-            const bool have = e0 + i < e1;
-            const int2 pa = have ? csr_pair(e0 + i) : int2{0, 0};
-            S.pw[i] = __int_as_float(pa.y);
-            const uint32_t base = (static_cast<uint32_t>(pa.x) * B + S.b0) * (4u * D);
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-                S.pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
-                                       : nm_ld<D>(xrs, loff[k], have && (G::RPI * k + rl) < static_cast<int>(S.nb),
-                                                  base);
-        }
-    };
-    issue(sl, sc.first);
-    __syncthreads();  // W / bias staged (after the first tile's loads are in flight)
-
-    auto process = [&](NmSlot<D, NPF>& S, int64_t tile) {
-        const uint32_t n = S.n, b0 = S.b0, nb = S.nb;
-        const int e0 = S.e0, e1 = S.e1;
-        bool rv[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
-        f32x4 acc[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < NPF; ++i) {
-            if (e0 + i < e1) {
-#pragma unroll
-                for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[k][c] = fmaf(S.pw[i], S.pf[i][k][c], acc[k][c]);
-            }
-        }
-        // neighbours beyond the prefetched ones: in place, two blocks in flight
-        int e = e0 + NPF;
-        for (; e + 1 < e1; e += 2) {
-            const int2 pa = csr_pair(e), pb = csr_pair(e + 1);
-            const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-            const uint32_t bbs = (static_cast<uint32_t>(pb.x) * B + b0) * (4u * D);
-            f32x4 va[G::K], vb[G::K];
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) {
-                va[k] = nm_ld<D>(xrs, loff[k], rv[k], ba);
-                vb[k] = nm_ld<D>(xrs, loff[k], rv[k], bbs);
-            }
-            const float wa = __int_as_float(pa.y), wb = __int_as_float(pb.y);
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    acc[k][c] = fmaf(wa, va[k][c], acc[k][c]);
-                    acc[k][c] = fmaf(wb, vb[k][c], acc[k][c]);
-                }
-        }
-        if (e < e1) {
-            const int2 pa = csr_pair(e);
-            const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-            f32x4 va[G::K];
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) va[k] = nm_ld<D>(xrs, loff[k], rv[k], ba);
-            const float wa = __int_as_float(pa.y);
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[k][c] = fmaf(wa, va[k][c], acc[k][c]);
-        }
-        // this slot's next tile goes in flight under this tile's transform
-        issue(S, tile + sc.stride);
-        __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from hoisting the W reads above the issue
-
-        // gather layout -> LDS -> MFMA B operand
-        wave_sync_nm();
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
-        wave_sync_nm();
-        f32x4 o[G::CH];
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
-        if constexpr ((LAB & 1) != 0) {
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + j * G::S + 16 * mt + 4 * q);
-        } else if constexpr (SPLIT) {
-            // yT[out][row] += sum_k W[out][k] (Ahat x)[row][k], k-step s covers k = 32 s + 8 q + (0..7)
-            // (W fragments read per group: software-pipelining them costs registers, hence occupancy,
-            // and measured slower)
-#pragma unroll
-            for (int s2 = 0; s2 < D / 32; ++s2) {
-                lg_bf16x8 b0f, b1f, b2f;
-                split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f,
-                          b2f);
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) {
-                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
-                    const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
-                    const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
-                    const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
-                    // smallest terms first
-                    o[mt] = mfma_bf(a2, b0f, o[mt]);
-                    o[mt] = mfma_bf(a1, b1f, o[mt]);
-                    o[mt] = mfma_bf(a0, b2f, o[mt]);
-                    o[mt] = mfma_bf(a1, b0f, o[mt]);
-                    o[mt] = mfma_bf(a0, b1f, o[mt]);
-                    o[mt] = mfma_bf(a0, b0f, o[mt]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-#pragma unroll
-            for (int c = 0; c < G::CH; ++c) {
-                const f32x4 bt = ld4(tl + j * G::S + 16 * c + 4 * q);  // (Ahat x)[row j][16c + 4q + i]
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) {
-                    const f32x4 wa = ld4(wl + (16 * mt + j) * G::S + 16 * c + 4 * q);  // W[16mt + j][16c + 4q + i]
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) o[mt] = mfma_nm(wa[i], bt[i], o[mt]);
-                }
-                __builtin_amdgcn_sched_barrier(0);  // W reads per k chunk: bounded register footprint
-            }
-        }
-        // epilogue: ReLU, row-stream dropout (two channels per step) seeded with the window-major
-        // row id (b0 + j) N + n, so both layouts draw the same mask
-        uint32_t st = 0;
-        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) {
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                float t = fmaxf(o[mt][reg], relu_floor);
-                if constexpr (DROP) {
-                    if ((reg & 1) == 0) st = lg_xorshift32(st);
-                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
-                    t = u16 >= thr ? t : 0.0f;
-                }
-                o[mt][reg] = t;
-            }
-        }
-        wave_sync_nm();
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
-        wave_sync_nm();
-        const uint32_t ob = (n * B + b0) * (4u * D);
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) nm_st<2>(yrs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
-    };
-
-    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) process(sl, tile);
-}
-
 
 // ------------------------------------------------------------------ forward, node-table pipeline
 // k_gcn_fwd_nm2's math with the CSR read from the node table (graph.hip k_nm_table): one
@@ -557,36 +119,15 @@ __device__ __forceinline__ NmRec nm_rec(const int32_t* __restrict__ tab, uint32_
 }
 static_assert(kLgNmInline == 6, "nm_rec unpacks six inline pairs");
 
-// OPT bits of k_gcn_fwd_nm3 (results never change):
-//   kNm3WFrag: W's split parts in LDS in MFMA-fragment order — fragment f = (part, mt, s2) is
-//     1 KiB, lane l's 8 bf16 at f * 1024 + 16 l — so every A-operand read is one
-//     conflict-free ds_read_b128 from ONE address register plus an immediate offset (the
-//     row-major image with stride D + 8 put 2 lanes on a bank in every 16-lane group);
-//   kNm3Swz (D = 64): the per-wave tile unpadded, 16-byte chunk c of row r at chunk
-//     c ^ r: the gather-layout stores/loads, the B-operand loads and the MFMA-layout
-//     epilogue stores are all conflict-free (stride D + 4 conflicted on the loads);
-//   kNm3Epi: ReLU as an integer max on the bits (one op, no NaN canonicalisation), the
-//     dropout decision as one compare + select, the [y > 0] mask bits as min + shift-or;
-//   kNm3Soff: neighbour block bases in the buffer load's scalar offset (no per-load
-//     address add), an absent neighbour through a zero-record descriptor.
-//   kNm3WFirst: W's global loads issued before the first tile's neighbour blocks.
-constexpr int kNm3WFrag = 1, kNm3Swz = 2, kNm3Epi = 4, kNm3Soff = 8, kNm3WFirst = 16;
-#ifndef LG_NM3_OPT
-#define LG_NM3_OPT 0
-#endif
-constexpr int kNm3OptDefault = LG_NM3_OPT;
-
-template <int D, bool SPLIT, int WAVES, int OPT = 0>
+template <int D, bool SPLIT, int WAVES>
 struct Nm3Lds {  // dynamic LDS layout (floats)
-    static constexpr bool WFRAG = SPLIT && (OPT & kNm3WFrag);
-    static constexpr bool SWZ = (OPT & kNm3Swz) && D == 64;
     static constexpr int SB = D + 8;
-    static constexpr int WF = WFRAG ? (3 * D * D) / 2 : SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
+    static constexpr int WF = SPLIT ? (3 * D * SB) / 2 : D * NmGeo<D>::S;
     static constexpr int TILES = WF + D;
-    static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
+    static constexpr int TILE = NmGeo<D>::TILE;
     static constexpr size_t BYTES = 4 * static_cast<size_t>(TILES + WAVES * TILE);
     // float offset of 16-byte chunk c of row r in a wave's tile
-    static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
+    static __device__ __forceinline__ int tix(int r, int c) { return r * NmGeo<D>::S + 4 * c; }
 };
 
 #ifdef LG_NM3_STAMPS
@@ -634,27 +175,20 @@ constexpr uint32_t kNm3RowOob = 0x80000000u;
 constexpr uint32_t kNm3BlkOob = 0x7FFFF000u;
 constexpr uint64_t kNm3MaxBytes = 0x7FFFF000u;
 
-// LAB (kernel-lab builds only; results are WRONG when set): 1 = skip the MFMA transform,
-// 2 = skip the neighbour loads, 4 = skip the y stores (kept behind a runtime-false test so
-// the transform is not dead code).  DST: epilogue stores straight from the MFMA layout
-// (16 rows x 64 B per store) instead of through the LDS tile.
 // BF (LG_F_BF16, the bf16 node-MLP tier): the transform's single hi x hi product.
-template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, int LAB = 0, bool DST = false, bool BF = false,
-          int OPT = kNm3OptDefault>
+template <int D, bool DROP, bool RELU, bool SPLIT, int WAVES, bool BF = false>
 __global__ void __launch_bounds__(64 * WAVES, WAVES >= 5 ? 4 : 1)
 k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
               const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
               uint32_t salt, uint16_t* __restrict__ ymask) {
     using G = NmGeo<D>;
-    using LY = Nm3Lds<D, SPLIT, WAVES, OPT>;
+    using LY = Nm3Lds<D, SPLIT, WAVES>;
     constexpr int SB = LY::SB;
     constexpr int NPF = kNm3Npf;
-    constexpr bool WFRAG = LY::WFRAG, EPI = (OPT & kNm3Epi) != 0, SOFF = (OPT & kNm3Soff) != 0;
-    constexpr bool WFIRST = (OPT & kNm3WFirst) != 0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* wl = reinterpret_cast<float*>(smem);         // fp32: W [out][in] * fold, stride S
-    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB (WFRAG: fragments)
+    uint16_t* wsl = reinterpret_cast<uint16_t*>(smem);  // SPLIT: 3 x [out][in] bf16, stride SB
     float* bl = wl + LY::WF;                            // bias * fold
     float* tiles = wl + LY::TILES;
 
@@ -668,7 +202,6 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     float* tl = tiles + wave * LY::TILE;
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
-    const __amdgpu_buffer_rsrc_t xrs0 = nm_rsrc(x, 0);  // SOFF: an absent neighbour's loads return zeros
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];  // byte offset in a 16-row block of this lane's slot k (row RPI k + rl)
 #pragma unroll
@@ -688,46 +221,29 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     f32x4 pf[NPF][G::K];
     uint32_t lo[G::K];  // loff, or kNm3RowOob for rows past the tile's window count
     NmRec cur;
-    uint32_t cn, cb0, cnb;
+    uint32_t cn, cb0;
     auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
         n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
-        cnb = nb;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
             const bool have = r.e0 + i < r.e1;
-            if constexpr (SOFF) {
-                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
-                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
-#pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
-                                         : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                         rs, lo[k], base, 0));
-                continue;
-            }
             const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : kNm3BlkOob;
 #pragma unroll
             for (int k = 0; k < G::K; ++k)
-                pf[i][k] = (LAB & 2) ? f32x4{1.f, 2.f, 3.f, 4.f} * static_cast<float>(base & 7)
-                                     : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                     xrs, lo[k] + base, 0, 0));
+                pf[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[k] + base, 0, 0));
         }
     };
     // a present neighbour's block (the rows past the prefetched ones)
     auto ldblk = [&](uint32_t base, uint32_t lk) -> f32x4 {
-        if constexpr (SOFF) return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk, base, 0));
         return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk + base, 0, 0));
     };
     const int64_t t0 = sc.first;
-    // W (x dropout scale fold) and bias to LDS.  kNm3WFirst: W's loads go out BEFORE the first
-    // tile's neighbour blocks, so the staging waits for W alone (vector loads complete in
-    // order: staged after them, it waited for the whole first gather, ~2.6 us of the launch
-    // in the kernel-lab timeline)
+    // W (x dropout scale fold) and bias to LDS
     constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
     f32x4 wv[WPER];
     float bb = 0.f;
@@ -736,16 +252,12 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
         bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
     };
-    if constexpr (WFIRST) {
-        load_w();
-        asm volatile("" ::: "memory");
-    }
     {
         uint32_t n0, b00, nb00;
         tile_coords(t0, n0, b00, nb00);
         issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
     }
-    if constexpr (!WFIRST) load_w();
+    load_w();
     {
         const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
 #pragma unroll
@@ -757,19 +269,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             // (the empty asm keeps -ffp-contract from fusing it into the split's residual)
             f32x4 w = wv[u] * fold;
             asm volatile("" : "+v"(w));
-            if constexpr (WFRAG) {
-                // element (o, c) -> fragment (part, mt = o / 16, s2 = c / 32), lane (o % 16) + 16 ((c / 8) % 4),
-                // bf16 slot c % 8
-                uint32_t pa[3], pb[3];
-                split3_pair(w[0], w[1], pa[0], pa[1], pa[2]);
-                split3_pair(w[2], w[3], pb[0], pb[1], pb[2]);
-                const int fl = (o & 15) + 16 * ((c4 >> 3) & 3);
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const int f = (p * G::CH + (o >> 4)) * (D / 32) + (c4 >> 5);
-                    *reinterpret_cast<uint2*>(wsl + f * 512 + fl * 8 + (c4 & 7)) = uint2{pa[p], pb[p]};
-                }
-            } else if constexpr (SPLIT) {
+            if constexpr (SPLIT) {
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     uint32_t p0, p1, p2;
@@ -794,7 +294,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     (void)tcount;
     LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
     for (int64_t tile = t0; tile < tend; tile += sc.stride) {
-        const uint32_t n = cn, b0 = cb0, nb = cnb;
+        const uint32_t n = cn, b0 = cb0;
         const int e0 = cur.e0, e1 = cur.e1;
         uint32_t tlo[G::K];
 #pragma unroll
@@ -881,10 +381,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         f32x4 o[G::CH];
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) o[mt] = ld4(bl + 16 * mt + 4 * q);
-        if constexpr ((LAB & 1) != 0) {
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) o[mt] += ld4(tl + LY::tix(j, 4 * mt + q));
-        } else if constexpr (SPLIT) {
+        if constexpr (SPLIT) {
 #pragma unroll
             for (int s2 = 0; s2 < D / 32; ++s2) {
                 lg_bf16x8 b0f, b1f, b2f;
@@ -892,19 +389,10 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                           b2f);
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) {
-                    lg_bf16x8 a0, a1, a2;
-                    if constexpr (WFRAG) {
-                        const uint16_t* fb = wsl + 8 * lane + 512 * (mt * (D / 32) + s2);
-                        constexpr int PS = 512 * G::CH * (D / 32);  // one part's fragments
-                        a0 = *reinterpret_cast<const lg_bf16x8*>(fb);
-                        a1 = *reinterpret_cast<const lg_bf16x8*>(fb + PS);
-                        a2 = *reinterpret_cast<const lg_bf16x8*>(fb + 2 * PS);
-                    } else {
-                        const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
-                        a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
-                        a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
-                        a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
-                    }
+                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                    const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
+                    const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
+                    const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
                     if constexpr (BF) {
                         o[mt] = mfma_bf(a0, b0f, o[mt]);
                         continue;
@@ -942,18 +430,7 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                float v = o[mt][reg];
-                if constexpr (EPI) {
-                    // relu(v) on the bits: negative floats (and -0) are negative integers
-                    if constexpr (RELU) v = __int_as_float(max(__float_as_int(v), 0));
-                    if constexpr (DROP) {
-                        if ((reg & 1) == 0) st = lg_xorshift32(st);
-                        const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
-                        v = u16 >= thr ? v : 0.0f;
-                    }
-                    o[mt][reg] = v;
-                    continue;
-                }
+                const float v = o[mt][reg];
                 bool keep = true;
                 if constexpr (DROP) {
                     if ((reg & 1) == 0) st = lg_xorshift32(st);
@@ -965,420 +442,22 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             }
         }
         const uint32_t ob = (n * B + b0) * (4u * D);
-        const bool do_store = (LAB & 4) == 0 || dscale == 1234.5f;
-        if constexpr (DST) {
-            // lane (j, q) holds row j, channels 16 mt + 4 q .. + 3
-            const uint32_t so = j < static_cast<int>(nb) ? static_cast<uint32_t>(j) * (4u * D) + 16u * q : kNm3RowOob;
-            if (do_store)
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt)
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, o[mt]),
-                                                           yrs, so + ob + 64u * mt, 0, 0);
-        } else {
-            wave_sync_nm();
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
-            wave_sync_nm();
-            uint32_t bits = 0;  // [y > 0] of this lane's 4 K elements (bit 4 k + i), for ymask
-            f32x4 vk[EPI ? G::K : 1];
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) {
-                const f32x4 v = ld4(tl + LY::tix(G::RPI * k + rl, fg));
-                if (do_store) {
-                    if constexpr (SOFF)
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), yrs, tlo[k], ob, 0);
-                    else
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            __builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), yrs, tlo[k] + ob, 0, 0);
-                }
-                if constexpr (EPI) {
-                    vk[k] = v;
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
-                }
-            }
-            if constexpr (EPI) {
-                // [y > 0] = bit 31 of (bits(y) + 0x7FFFFFFF) for y >= +0 (after the ReLU; without it,
-                // negative y first go to 0 by an integer max); alignbit shifts the mask left by one
-                // and takes that bit in, highest element first: two ops per element, no VCC
-#pragma unroll
-                for (int k = G::K - 1; k >= 0; --k)
-#pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        const uint32_t u = RELU ? __float_as_uint(vk[k][i])
-                                                : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
-                        bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
-                    }
-            }
-            if (ymask)
-                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs,
-                                                      nm_mask_off(n, b0 >> 4, ngroups, lane), 0, 0);
-            if constexpr (EPI) lg_store_guard(vk);
-        }
-#ifdef LG_NM3_STAMPS
-        if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
-        ++tcount;
-#endif
-    }
-#ifdef LG_NM3_STAMPS
-    LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
-    LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
-    LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
-                         static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
-#endif
-}
-
-// ------------------------------------------------------------------ forward, W in registers
-// k_gcn_fwd_nm3's tile pipeline at 2 waves per SIMD with the transform's A operand (W's
-// three bf16 parts, 96 VGPRs at D = 64) held in registers for the whole launch.  A per-wave
-// timeline of nm3 (kernel-lab stamps, profiles/r03a) put 1.4 of ~2.7 us per tile in the
-// transform, most of it waiting on the 24 W-fragment LDS reads that the register budget of
-// 3 waves/SIMD forced just in time, and 2.6 us in the workgroup's W staging before the
-// first tile.  Here every wave splits its own W fragments from global memory once, no wave
-// waits on another (no workgroup barrier: the LDS holds only the wave's own transpose tile,
-// XOR-swizzled and conflict-free at D = 64), and the transform is 48 MFMAs back to back on
-// operands already in registers.  Epilogue, loads and stores as nm3's kNm3Epi | kNm3Soff;
-// results are bit-identical to k_gcn_fwd_nm3 (same products, same order).
-constexpr int kNm5Waves = 4;
-
-template <int D>
-struct Nm5Lds {
-    static constexpr bool SWZ = D == 64;
-    static constexpr int TILE = SWZ ? 16 * D : NmGeo<D>::TILE;
-    static constexpr int WS = D + 4;                     // fp32 W staging row stride (read once per wave)
-    static constexpr int WOFF = kNm5Waves * TILE;        // W [out][in] * fold, then the bias * fold
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(WOFF + D * WS + D + kNm5Waves);  // + per-wave max|W|
-    static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
-};
-
-#ifndef LG_NM5_NPF
-#define LG_NM5_NPF 4  // neighbour blocks in flight per wave (L-TOWN-A: 97 % of nodes have degree <= 4 with the self loop)
-#endif
-// F16: the transform as the 2-way fp16 split (split_bf16.h: 3 f16 MFMAs per product instead of
-// 6 bf16 ones, fp32-level accuracy): W scaled by one power of two per launch, each tile's
-// (Ahat x) by one per tile (its largest |value| to [2^14, 2^15)), y = acc 2^-(sa + sw) + b.
-#ifndef LG_NM5_OCC
-#define LG_NM5_OCC 2  // waves per SIMD the register budget is sized for (2: 256 VGPRs, 3: 168)
-#endif
-template <int D, bool DROP, bool RELU, bool BF, bool F16 = false>
-__global__ void __launch_bounds__(64 * kNm5Waves, LG_NM5_OCC)
-k_gcn_fwd_nm5(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
-              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
-              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
-              uint32_t salt, uint16_t* __restrict__ ymask) {
-    using G = NmGeo<D>;
-    using LY = Nm5Lds<D>;
-    constexpr int WAVES = kNm5Waves;
-    constexpr int NPF = LG_NM5_NPF;
-    constexpr int KS = D / 32;      // MFMA k-steps of 32 channels
-    constexpr int NP = BF ? 1 : 3;  // W parts held (bf16 split)
-    static_assert(!(BF && F16), "one transform");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / G::LPR, fg = lane % G::LPR;
-#ifdef LG_NM3_STAMPS
-    LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
-    LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
-#endif
-    float* tl = reinterpret_cast<float*>(smem) + wave * LY::TILE;
-    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), yrs = nm_rsrc(y, bytes);
-    const __amdgpu_buffer_rsrc_t xrs0 = nm_rsrc(x, 0);  // an absent neighbour's loads return zeros
-    const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
-    uint32_t loff[G::K];
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, WAVES);
-    const int64_t tend = sc.end;
-
-    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
-        const bool valid = tile < tend;
-        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
-        const uint32_t grp = lg_div(t32, fdN);
-        n = t32 - grp * N;
-        b0 = grp * 16;
-        nb = valid ? min(16u, B - b0) : 0u;
-    };
-    f32x4 pf[NPF][G::K];
-    uint32_t lo[G::K];
-    NmRec cur;
-    uint32_t cn, cb0;
-    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
-        n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
-        cur = r;
-        cn = n;
-        cb0 = b0;
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-#pragma unroll
-        for (int i = 0; i < NPF; ++i) {
-            const bool have = r.e0 + i < r.e1;
-            const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
-            const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-                pf[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[k], base, 0));
-        }
-    };
-    auto ldblk = [&](uint32_t base, uint32_t lk) -> f32x4 {
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lk, base, 0));
-    };
-    const int64_t t0 = sc.first;
-    // W (16 KiB at D = 64) is read from global memory once per WORKGROUP, before the first
-    // tile's neighbour blocks (vector loads complete in order), staged in LDS, and each wave
-    // takes its fragments from there: read per wave from global memory, every wave of the
-    // launch hit the same 16 KiB at once (6 us of staging in the kernel-lab timeline)
-    float* wst = reinterpret_cast<float*>(smem) + LY::WOFF;
-    const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
-    {
-        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * WAVES - 1) / (64 * WAVES);
-        f32x4 wv[WPER];
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * WAVES + threadIdx.x, W4 - 1));
-        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
-        asm volatile("" ::: "memory");
-        uint32_t n0, b00, nb00;
-        tile_coords(t0, n0, b00, nb00);
-        issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
-        uint32_t wmax = 0;
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) {
-            const int i = u * 64 * WAVES + threadIdx.x;
-            const f32x4 w = wv[u] * fold;
-            if (i < W4) st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) wmax = max(wmax, __float_as_uint(fabsf(w[c])));
-        }
-        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
-        if constexpr (F16) {
-            wmax = lg_wave_max_bits(wmax);
-            if (lane == 0) reinterpret_cast<uint32_t*>(wst)[D * LY::WS + D + wave] = wmax;
-        }
-    }
-    __syncthreads();
-    int sw = 0;  // F16: W's scale exponent
-    if constexpr (F16) {
-        const uint32_t* wm = reinterpret_cast<const uint32_t*>(wst) + D * LY::WS + D;
-        uint32_t m = 0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) m = max(m, wm[w]);
-        sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
-    }
-    // this lane's A fragments for the whole launch: W[16 mt + j][32 s2 + 8 q .. + 7] * fold, split
-    // in three bf16 parts; the bias (x fold) of its output channels 16 mt + 4 q .. + 3
-    lg_bf16x8 wf[NP][G::CH][KS];
-    lg_f16x8 wh[2][G::CH][KS];
-#pragma unroll
-    for (int mt = 0; mt < G::CH; ++mt) {
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
-            if constexpr (F16) {
-                const float sc = lg_pow2f(sw);
-                split2_f16_x8(ld4(wp) * sc, ld4(wp + 4) * sc, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
-                continue;
-            }
-            lg_bf16x8 f0, f1, f2;
-            split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
-            wf[0][mt][s2] = f0;
-            if constexpr (!BF) {
-                wf[NP > 1 ? 1 : 0][mt][s2] = f1;
-                wf[NP > 2 ? 2 : 0][mt][s2] = f2;
-            }
-        }
-    }
-    const uint32_t key = lg_dropout_key_dev(seed, salt);
-    const uint32_t thr = lg_keep_threshold16(p_drop);
-
-    int tcount = 0;
-    (void)tcount;
-    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
-    for (int64_t tile = t0; tile < tend; tile += sc.stride) {
-        const uint32_t n = cn, b0 = cb0;
-        const int e0 = cur.e0, e1 = cur.e1;
-        uint32_t tlo[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
-        uint32_t nn, nb0, nnb;
-        tile_coords(tile + sc.stride, nn, nb0, nnb);
-        const NmRec nxt = nm_rec(tab, N + nn);
-        asm volatile("" ::: "memory");  // keep the record request here: the compiler would sink it to its use
-        f32x4 acc[G::K];
-        {
-            const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) acc[k] = pf[0][k] * w;
-        }
-#pragma unroll
-        for (int i = 1; i < NPF; ++i) {
-            if (e0 + i < e1) {
-                const float w = __int_as_float(cur.p[i].y);
-#pragma unroll
-                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[i][k]);
-            }
-        }
-        if (e0 + NPF < e1) {  // the rest of the row: inline pairs, then the pair array
-            int2 ip[kLgNmInline - NPF];
-#pragma unroll
-            for (int i = 0; i < kLgNmInline - NPF; ++i) ip[i] = cur.p[NPF + i];
-            // every inline block in flight at once (zeros past the degree), then the sums in CSR order
-            constexpr int NI = kLgNmInline - NPF > 0 ? kLgNmInline - NPF : 1;
-            f32x4 va[NI][G::K];
-#pragma unroll
-            for (int i = 0; i < kLgNmInline - NPF; ++i) {
-                const bool have = e0 + NPF + i < e1;
-                const uint32_t ba = have ? (static_cast<uint32_t>(ip[i].x) * B + b0) * (4u * D) : 0u;
-                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
-#pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, tlo[k], ba, 0));
-            }
-#pragma unroll
-            for (int i = 0; i < kLgNmInline - NPF; ++i) {
-                if (e0 + NPF + i < e1) {
-                    const float wa = __int_as_float(ip[i].y);
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[i][k]);
-                }
-            }
-            for (int e = e0 + kLgNmInline; e < e1; ++e) {
-                const int2 pa = pairs[e];
-                const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-                f32x4 va[G::K];
-#pragma unroll
-                for (int k = 0; k < G::K; ++k) va[k] = ldblk(ba, tlo[k]);
-                const float wa = __int_as_float(pa.y);
-#pragma unroll
-                for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[k]);
-            }
-        }
-#ifdef LG_NM3_STAMPS
-        if (tcount < 6) LG_NM3_STAMP(3 + 3 * tcount, __builtin_amdgcn_s_memtime());
-#endif
-        issue(nxt, nn, nb0, nnb);
-        __builtin_amdgcn_sched_barrier(0);
-        int sa = 0;  // F16: this tile's scale exponent
-        if constexpr (F16) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(acc[k][c])));
-            sa = lg_f16_scale_exp(lg_wave_max_bits(m));
-            const float sc = lg_pow2f(sa);
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) acc[k] *= sc;
-        }
-
-        // gather layout -> LDS (own tile) -> MFMA B operand
-        wave_sync_nm();
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) st4(tl + LY::tix(G::RPI * k + rl, fg), acc[k]);
-        wave_sync_nm();
-        f32x4 bq[KS][2];
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            bq[s2][0] = ld4(tl + LY::tix(j, 8 * s2 + 2 * q));
-            bq[s2][1] = ld4(tl + LY::tix(j, 8 * s2 + 2 * q + 1));
-        }
-        // the row-stream dropout seed (independent of the transform) while the reads land
-        uint32_t st = 0;
-        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
-        f32x4 o[G::CH];
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt)
-            o[mt] = F16 ? f32x4{0.f, 0.f, 0.f, 0.f} : ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
-        if constexpr (F16) {
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2) {
-                lg_f16x8 b0h, b1h;
-                split2_f16_x8(bq[s2][0], bq[s2][1], b0h, b1h);
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) {  // smallest terms first
-                    o[mt] = mfma_h(wh[F16 ? 1 : 0][mt][s2], b0h, o[mt]);
-                    o[mt] = mfma_h(wh[0][mt][s2], b1h, o[mt]);
-                    o[mt] = mfma_h(wh[0][mt][s2], b0h, o[mt]);
-                }
-            }
-            // unscale (exact: a power of two) and the bias in one rounding
-            const float us = lg_pow2f(-(sa + sw));
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                const f32x4 bv = ld4(wst + D * LY::WS + 16 * mt + 4 * q);  // bias * fold
-#pragma unroll
-                for (int c = 0; c < 4; ++c) o[mt][c] = fmaf(o[mt][c], us, bv[c]);
-            }
-        }
-        if constexpr (!F16) {
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2) {
-                lg_bf16x8 b0f, b1f, b2f;
-                split3_x8(bq[s2][0], bq[s2][1], b0f, b1f, b2f);
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) {
-                    if constexpr (BF) {
-                        o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
-                        continue;
-                    }
-                    o[mt] = mfma_bf(wf[NP > 2 ? 2 : 0][mt][s2], b0f, o[mt]);
-                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b1f, o[mt]);
-                    o[mt] = mfma_bf(wf[0][mt][s2], b2f, o[mt]);
-                    o[mt] = mfma_bf(wf[NP > 1 ? 1 : 0][mt][s2], b0f, o[mt]);
-                    o[mt] = mfma_bf(wf[0][mt][s2], b1f, o[mt]);
-                    o[mt] = mfma_bf(wf[0][mt][s2], b0f, o[mt]);
-                }
-            }
-        }
-#ifdef LG_NM3_STAMPS
-        if (tcount < 6) LG_NM3_STAMP(4 + 3 * tcount, __builtin_amdgcn_s_memtime());
-#endif
-        // epilogue: ReLU as an integer max, row-stream dropout as one compare + select
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) {
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                float v = o[mt][reg];
-                if constexpr (RELU) v = __int_as_float(max(__float_as_int(v), 0));
-                if constexpr (DROP) {
-                    if ((reg & 1) == 0) st = lg_xorshift32(st);
-                    const uint32_t u16 = (reg & 1) ? (st >> 16) : (st & 0xFFFFu);
-                    v = u16 >= thr ? v : 0.0f;
-                }
-                o[mt][reg] = v;
-            }
-        }
-        const uint32_t ob = (n * B + b0) * (4u * D);
         wave_sync_nm();
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) st4(tl + LY::tix(j, 4 * mt + q), o[mt]);
         wave_sync_nm();
-        f32x4 vk[G::K];
+        uint32_t bits = 0;  // [y > 0] of this lane's 4 K elements (bit 4 k + i), for ymask
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
-            vk[k] = ld4(tl + LY::tix(G::RPI * k + rl, fg));
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                   yrs, tlo[k], ob, 0);
+            const f32x4 v = ld4(tl + LY::tix(G::RPI * k + rl, fg));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                                   yrs, tlo[k] + ob, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
         }
-        if (ymask) {
-            // [y > 0] = bit 31 of (bits(y) + 0x7FFFFFFF) for y >= +0; alignbit shifts the mask left
-            // by one and takes that bit in, highest element first
-            uint32_t bits = 0;
-#pragma unroll
-            for (int k = G::K - 1; k >= 0; --k)
-#pragma unroll
-                for (int i = 3; i >= 0; --i) {
-                    const uint32_t u = RELU ? __float_as_uint(vk[k][i])
-                                            : static_cast<uint32_t>(max(__float_as_int(vk[k][i]), 0));
-                    bits = __builtin_amdgcn_alignbit(bits, u + 0x7FFFFFFFu, 31);
-                }
+        if (ymask)
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
                                                   0, 0);
-        }
-        lg_store_guard(vk);
 #ifdef LG_NM3_STAMPS
         if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
         ++tcount;
@@ -1472,6 +551,16 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool producer = wave < kPcProd;
+#ifdef LG_NM3_STAMPS
+    // pc timeline (lab builds): 0 realtime, 1 clock at start, 2 after the W staging barrier,
+    // 3 + t: tile t (< 16) handed over (producer) / stored (consumer), 21 clock, 22 realtime at end
+    constexpr int WAVES = kPcProd * (1 + NC);
+    {
+        const int lane = threadIdx.x & 63;
+        LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
+        LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
+    }
+#endif
     const int prod = producer ? wave : (wave - kPcProd) % kPcProd;  // the producer this wave is or serves
     const int cons = producer ? 0 : (wave - kPcProd) / kPcProd;     // consumer index 0 .. NC-1
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
@@ -1518,6 +607,15 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
     }
     __syncthreads();
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
+    auto pc_stamp_end = [&]() {
+        LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
+        LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
+        LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                             static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
+    };
+#endif
 
     if (producer) {
         // ---------------- producer: gather + accumulate, two tiles in flight
@@ -1627,6 +725,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 m[2] = mnb;
             }
             pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
+#ifdef LG_NM3_STAMPS
+            if (t < 16) LG_NM3_STAMP(3 + t, __builtin_amdgcn_s_memtime());
+#endif
             return true;
         };
         {
@@ -1641,6 +742,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             if (!step(std::integral_constant<int, 0>{}, t)) break;
             if (!step(std::integral_constant<int, 1>{}, t + 1)) break;
         }
+#ifdef LG_NM3_STAMPS
+        pc_stamp_end();
+#endif
         return;
     }
 
@@ -1793,179 +897,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         }
         lg_store_guard(vk);
         pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));  // the slot's reads are done (release)
+#ifdef LG_NM3_STAMPS
+        if (u < 16) LG_NM3_STAMP(3 + u, __builtin_amdgcn_s_memtime());
+#endif
     }
+#ifdef LG_NM3_STAMPS
+    pc_stamp_end();
+#endif
 }
-
-// ------------------------------------------------------------------ backward
-template <int D, bool MASK_IN, bool NB>
-__global__ void __launch_bounds__(64 * kNmBwdWaves, 2)
-k_gcn_bwd_nm(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
-             const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
-             const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
-             uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out) {
-    using G = NmGeo<D>;
-    constexpr int SW = D + 4;
-    constexpr int WBUF = 2 * G::TILE;
-    constexpr int L = D * D + 2 * D;  // slab row: dW, db, d(node bias)
-    static_assert(kNmBwdWaves * WBUF >= L, "reduction buffer must fit in the tile buffers");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* lds = reinterpret_cast<float*>(smem);
-    float* wl = lds + kNmBwdWaves * WBUF;
-    constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves - 1) / (64 * kNmBwdWaves);
-    f32x4 wv[WPER];
-#pragma unroll
-    for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves + threadIdx.x, W4 - 1));
-#pragma unroll
-    for (int u = 0; u < WPER; ++u) {
-        const int i = u * 64 * kNmBwdWaves + threadIdx.x;
-        if (i < W4) st4(wl + (i / (D / 4)) * SW + 4 * (i % (D / 4)), wv[u]);
-    }
-    __syncthreads();
-
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* tl = lds + wave * WBUF;  // t tile [row][feature], later dx
-    float* xl = tl + G::TILE;       // x tile [row][feature]
-    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MASK_IN ? yv : dy, bytes),
-                                 xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
-    uint32_t loff[G::K];
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
-
-    f32x4 dw[G::CH][G::CH];  // dW tile (mo, ni): rows o = 16mo + 4q + reg, cols i = 16ni + j
-#pragma unroll
-    for (int a = 0; a < G::CH; ++a)
-#pragma unroll
-        for (int b = 0; b < G::CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // channels 4fg..4fg+3, summed over this lane's rows
-    f32x4 nbacc[NB ? G::CH : 1];              // NB: channels 16mt + 4q + reg over this lane's rows j
-#pragma unroll
-    for (int mt = 0; mt < (NB ? G::CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmBwdWaves);
-    for (int64_t tile = sc.first; tile < sc.end; tile += sc.stride) {
-        const uint32_t t32 = static_cast<uint32_t>(tile);
-        const uint32_t grp = lg_div(t32, fdN), n = t32 - grp * N, b0 = grp * 16;
-        const uint32_t nb = min(16u, B - b0);
-        bool rv[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) rv[k] = static_cast<uint32_t>(G::RPI * k + rl) < nb;
-        const uint32_t ob = (n * B + b0) * (4u * D);
-        // own rows (one contiguous block): dz for db, x for dW and the output mask
-        f32x4 dz[G::K], mz[G::K], xv[G::K];
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) {
-            dz[k] = nm_ld<D>(dys, loff[k], rv[k], ob);
-            if constexpr (MASK_IN) mz[k] = nm_ld<D>(ms, loff[k], rv[k], ob);
-            xv[k] = nm_ld<D>(xs, loff[k], rv[k], ob);
-        }
-        f32x4 acc[G::K];
-        gather_nm<D, MASK_IN>(tab, pairs, dys, ms, scale_in, n, B, b0, loff, rv, acc);
-        wave_sync_nm();
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) {
-            st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
-            if constexpr (MASK_IN) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) dz[k][i] = mz[k][i] > 0.f ? dz[k][i] * scale_in : 0.f;
-            }
-            dbacc += dz[k];
-            st4(xl + (G::RPI * k + rl) * G::S + 4 * fg, xv[k]);
-        }
-        wave_sync_nm();
-        // dW[o][i] += sum_rows t[row][o] x[row][i]   (rows = 4q + kk on the K index)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int row = 4 * q + kk;
-            float ta[G::CH], xb[G::CH];
-#pragma unroll
-            for (int m = 0; m < G::CH; ++m) {
-                ta[m] = tl[row * G::S + 16 * m + j];
-                xb[m] = xl[row * G::S + 16 * m + j];
-            }
-#pragma unroll
-            for (int mo = 0; mo < G::CH; ++mo)
-#pragma unroll
-                for (int ni = 0; ni < G::CH; ++ni) dw[mo][ni] = mfma_nm(ta[mo], xb[ni], dw[mo][ni]);
-        }
-        // dx^T[i][row] = sum_o W[o][i] t[row][o] : A = W^T (LDS), B = t tile (LDS)
-        f32x4 o[G::CH];
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int a = 0; a < G::CH; ++a) {
-            const f32x4 bt = ld4(tl + j * G::S + 16 * a + 4 * q);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int ko = 16 * a + 4 * q + i;
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) o[mt] = mfma_nm(wl[ko * SW + 16 * mt + j], bt[i], o[mt]);
-            }
-        }
-        if (mask_out & 1) {
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
-#pragma unroll
-                for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
-            }
-        }
-        if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
-            if (node_slot[n] < 0)
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt) nbacc[mt] += o[mt];
-        }
-        wave_sync_nm();
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
-        wave_sync_nm();
-#pragma unroll
-        for (int k = 0; k < G::K; ++k) nm_st<0>(dxs, loff[k], rv[k], ob, ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg));
-        wave_sync_nm();
-    }
-    if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
-    }
-    // ---- per-block reduction of dW / db / node bias (fixed wave order -> deterministic)
-#pragma unroll
-    for (int off = G::LPR; off < 64; off <<= 1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
-    __syncthreads();
-    float* red = lds;  // reuse the tile buffers
-    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
-    for (int wv2 = 0; wv2 < kNmBwdWaves; ++wv2) {
-        __syncthreads();
-        if (wave == wv2) {
-#pragma unroll
-            for (int mo = 0; mo < G::CH; ++mo)
-#pragma unroll
-                for (int ni = 0; ni < G::CH; ++ni)
-#pragma unroll
-                    for (int reg = 0; reg < 4; ++reg)
-                        red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
-            if (lane < G::LPR)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
-            if (NB && j == 0)
-#pragma unroll
-                for (int mt = 0; mt < G::CH; ++mt)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
-        }
-    }
-    __syncthreads();
-    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
-    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
-}
-
 
 // ------------------------------------------------------------------ backward, node-table pipeline
 // lg_gcn_bwd_nm on k_gcn_fwd_nm3's pipeline: the tile's CSR record (transposed CSR) is one
@@ -2451,477 +1390,6 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
 }
 
-// ------------------------------------------------------------------ backward, producer / consumer waves
-// lg_gcn_bwd_nm[_bits] at D = 64 split by ROLE, as k_gcn_fwd_pc does the forward.  nm3 held a
-// tile's gather prefetch (64 VGPRs), the dW accumulators (64) and both GEMMs' operands in one
-// wave: 243-256 VGPRs, two waves per SIMD, each alternating a load-latency phase with a
-// ~1.5k-cycle MFMA/LDS phase.  Here:
-//   * kBpcProd PRODUCER waves gather t = Ahat^T dz (dz = dy * scale_in * [y > 0] from the
-//     forward's mask bits) with two tiles' neighbour blocks in flight, keep db (the rows' own
-//     dz, from the self entry), and hand each t tile to a consumer through an LDS ring
-//     (XOR-swizzled 16 x 64 fp32 slots) with the tile's f16 scale exponent;
-//   * NC CONSUMER waves per producer load the tile's own x block one tile ahead, run
-//     dW += t^T x and dx = t W on the 2-way fp16 split (W^T's parts in LDS in MFMA-fragment
-//     order: one conflict-free ds_read_b128 per fragment), apply [x > 0] * scale_out, and
-//     store dx through the slot in the coalesced gather layout.
-// Hand-off as k_gcn_fwd_pc (ready / done counters, bounded acquire polls).  dW, db and the
-// node-bias sums are reduced over the workgroup's waves in a fixed order into the slab row
-// (deterministic), exactly as k_gcn_bwd_nm3.
-#ifndef LG_BPC_RING
-#define LG_BPC_RING 4
-#endif
-#ifndef LG_BPC_NPF
-#define LG_BPC_NPF 3
-#endif
-#ifndef LG_BPC_CONS
-#define LG_BPC_CONS 1  // consumers per producer: 1 -> 8 waves, 256 VGPRs each (2 -> 12 waves at 168 spills)
-#endif
-constexpr int kBpcRing = LG_BPC_RING;
-constexpr int kBpcProd = 4, kBpcCons = LG_BPC_CONS;
-
-struct BpcLds {  // floats, D = 64
-    static constexpr int D = 64, CH = 4, KS = 2;
-    static constexpr int TILE = 16 * D;
-    static constexpr int WFR = 2 * CH * KS * 64 * 4;                   // W^T f16 parts, fragment order (16 B / lane)
-    static constexpr int WMX = WFR;                                     // per-wave max |W| bits
-    static constexpr int FOFF = WMX + 16;                               // ready[16], done[kBpcProd * NC]
-    static constexpr int MOFF = FOFF + 16 + kBpcProd * kBpcCons;        // per (producer, slot): n, b0, nb, texp
-    static constexpr int ROFF = MOFF + 4 * kBpcProd * kBpcRing;         // the rings
-    static constexpr int XOFF = ROFF + kBpcProd * kBpcRing * TILE;      // per consumer: x tile
-    static constexpr int END = XOFF + kBpcProd * kBpcCons * TILE;
-    static constexpr int L = D * D + 2 * D;                             // slab row: dW, db, d(node bias)
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(END > L ? END : L);
-    static __device__ __forceinline__ int tix(int r, int c) { return r * D + 4 * (c ^ r); }
-};
-
-template <bool MI, bool NB>
-__global__ void __launch_bounds__(64 * kBpcProd * (1 + kBpcCons), kBpcProd * (1 + kBpcCons) / 4)
-k_gcn_bwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
-             const float* __restrict__ x, const float* __restrict__ W, const int32_t* __restrict__ node_slot,
-             float* __restrict__ dxo, float* __restrict__ slab, uint32_t N, uint32_t B, uint32_t ngroups,
-             lg_fastdiv fdN, int mask_out, float scale_in, float scale_out, const uint16_t* __restrict__ ymask) {
-    constexpr int D = 64;
-    using G = NmGeo<D>;
-    using LY = BpcLds;
-    constexpr int NC = kBpcCons, R = kBpcRing, NPF = LG_BPC_NPF, CH = LY::CH, KS = LY::KS;
-    constexpr int NW = kBpcProd * (1 + NC), NT = 64 * NW;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* lds = reinterpret_cast<float*>(smem);
-    uint32_t* wmx = reinterpret_cast<uint32_t*>(lds + LY::WMX);
-    uint32_t* ready = reinterpret_cast<uint32_t*>(lds + LY::FOFF);
-    uint32_t* done = ready + 16;
-    uint32_t* meta = reinterpret_cast<uint32_t*>(lds + LY::MOFF);
-
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool producer = wave < kBpcProd;
-    const int prod = producer ? wave : (wave - kBpcProd) % kBpcProd;
-    const int cons = producer ? 0 : (wave - kBpcProd) / kBpcProd;
-    const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-    const int rl = lane / G::LPR, fg = lane % G::LPR;
-    float* ring = lds + LY::ROFF + prod * R * LY::TILE;
-    const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, prod, kBpcProd);
-    const int64_t tend = sc.end;
-    uint32_t loff[G::K];
-#pragma unroll
-    for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
-    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
-        const bool valid = tile < tend;
-        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
-        const uint32_t grp = lg_div(t32, fdN);
-        n = t32 - grp * N;
-        b0 = grp * 16;
-        nb = valid ? min(16u, B - b0) : 0u;
-    };
-
-    // max |W| over the workgroup (the f16 scale of W), counters cleared
-    {
-        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT;
-        uint32_t wm = 0;
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) {
-            const f32x4 w = ld4(W + 4 * min<int>(u * NT + threadIdx.x, W4 - 1));
-#pragma unroll
-            for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
-        }
-        wm = lg_wave_max_bits(wm);
-        if (lane == 0) wmx[wave] = wm;
-        if (threadIdx.x < 16 + kBpcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
-    }
-    __syncthreads();
-    int wexp;
-    {
-        uint32_t m = 0;
-        for (int w2 = 0; w2 < NW; ++w2) m = max(m, wmx[w2]);
-        wexp = lg_f16_scale_exp_c(__builtin_amdgcn_readfirstlane(m));
-    }
-    // W^T's f16 parts in fragment order: fragment (part, mt, s2), lane (j, q) holds
-    // A[i = 16 mt + j][o = 32 s2 + 8 q + e] = W[o][i] * 2^wexp, e = 0..7
-    {
-        const float wsc = lg_pow2f(wexp);
-        uint32_t* wfr = reinterpret_cast<uint32_t*>(lds);
-        for (int f = threadIdx.x; f < CH * KS * 64; f += NT) {
-            const int l = f & 63, ms = f >> 6, mt = ms / KS, s2 = ms % KS;
-            const int i = 16 * mt + (l & 15), o0 = 32 * s2 + 8 * (l >> 4);
-            lg_u32x4 h0, h1;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                uint32_t a0, a1;
-                split2_f16_pair(W[(o0 + 2 * e) * D + i] * wsc, W[(o0 + 2 * e + 1) * D + i] * wsc, a0, a1);
-                h0[e] = a0;
-                h1[e] = a1;
-            }
-            *reinterpret_cast<lg_u32x4*>(wfr + 4 * ((0 * CH * KS + ms) * 64 + l)) = h0;
-            *reinterpret_cast<lg_u32x4*>(wfr + 4 * ((1 * CH * KS + ms) * 64 + l)) = h1;
-        }
-    }
-    __syncthreads();
-
-    // initialised only in the role that uses them (a zero held across the other role's loop
-    // would cost its registers)
-    f32x4 dbacc;               // producers: channels 4fg..4fg+3 over the lane's rows
-    f32x4 dw[CH][CH];          // consumers: dW tile (mo, ni)
-    f32x4 nbacc[NB ? CH : 1];  // consumers, NB: channels 16mt + 4q + reg over rows j
-
-    if (producer) {
-        dbacc = f32x4{0.f, 0.f, 0.f, 0.f};
-        // ---------------- producer: t = Ahat^T dz, two tiles in flight
-        const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), dys0 = nm_rsrc(dy, 0);
-        const __amdgpu_buffer_rsrc_t mbs = nm_mask_rsrc(ymask, N, ngroups);
-        auto ldb = [&](uint32_t m, uint32_t grp, bool have) -> uint32_t {
-            if constexpr (!MI) return 0u;
-            return __builtin_amdgcn_raw_buffer_load_b16(mbs, have ? nm_mask_off(m, grp, ngroups, lane) : kNm3BlkOob + 2u * lane,
-                                                        0, 0);
-        };
-        auto dzb = [&](const f32x4& g, uint32_t bits, int k) {
-            if constexpr (!MI) return g;
-            f32x4 r;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) r[c] = (bits >> (4 * k + c)) & 1u ? g[c] * scale_in : 0.f;
-            return r;
-        };
-        f32x4 pf[2][NPF][G::K];
-        uint32_t pmb[2][NPF];
-        uint32_t lo[2][G::K];
-        NmRec rec[2];
-        uint32_t tn[2], tb0[2], tnb[2];
-        auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
-            constexpr int b = decltype(bc)::value;
-            uint32_t n, b0, nb;
-            tile_coords(tile, n, b0, nb);
-            rec[b] = r;
-            tn[b] = static_cast<uint32_t>(r.node);
-            tb0[b] = b0;
-            tnb[b] = nb;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) lo[b][k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-#pragma unroll
-            for (int i = 0; i < NPF; ++i) {
-                const bool have = r.e0 + i < r.e1;
-                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
-                const __amdgpu_buffer_rsrc_t rs = have ? dys : dys0;
-#pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    pf[b][i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], base, 0));
-                pmb[b][i] = ldb(static_cast<uint32_t>(r.p[i].x), b0 >> 4, have);
-            }
-        };
-        auto step = [&](auto bc, int64_t t) -> bool {
-            constexpr int b = decltype(bc)::value;
-            const int64_t tile = sc.first + t * sc.stride;
-            if (tile >= tend) return false;
-            uint32_t nn, nb0, nnb;
-            tile_coords(tile + 2 * sc.stride, nn, nb0, nnb);
-            const NmRec nxt = nm_rec(tab, N + nn);
-            asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
-            const NmRec& cur = rec[b];
-            const int e0 = cur.e0, e1 = cur.e1, self = cur.self;
-            const uint32_t b0 = tb0[b], n = tn[b];
-            f32x4 acc[G::K];
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < NPF; ++i) {
-                if (e0 + i < e1) {
-                    const float w = __int_as_float(cur.p[i].y);
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k) {
-                        const f32x4 z = dzb(pf[b][i][k], pmb[b][i], k);
-                        pk_fma4(acc[k], w, z);
-                        if (i == self) dbacc += z;
-                    }
-                }
-            }
-            if (e0 + NPF < e1) {  // the rest of the row: the inline blocks in flight at once, then the pair array
-                constexpr int NI = kLgNmInline - NPF;
-                f32x4 va[NI][G::K];
-                uint32_t vb[NI];
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    const bool have = e0 + NPF + i < e1;
-                    const uint32_t ba = have ? (static_cast<uint32_t>(cur.p[NPF + i].x) * B + b0) * (4u * D) : 0u;
-                    const __amdgpu_buffer_rsrc_t rs = have ? dys : dys0;
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k)
-                        va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], ba, 0));
-                    vb[i] = ldb(static_cast<uint32_t>(cur.p[NPF + i].x), b0 >> 4, have);
-                }
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    if (e0 + NPF + i < e1) {
-                        const float wa = __int_as_float(cur.p[NPF + i].y);
-#pragma unroll
-                        for (int k = 0; k < G::K; ++k) {
-                            const f32x4 z = dzb(va[i][k], vb[i], k);
-                            pk_fma4(acc[k], wa, z);
-                            if (NPF + i == self) dbacc += z;
-                        }
-                    }
-                }
-                for (int e = e0 + kLgNmInline; e < e1; ++e) {
-                    const int2 pa = pairs[e];
-                    const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
-                    f32x4 vv[G::K];
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k)
-                        vv[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dys, lo[b][k], ba, 0));
-                    const uint32_t bm = ldb(static_cast<uint32_t>(pa.x), b0 >> 4, true);
-                    const float wa = __int_as_float(pa.y);
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, dzb(vv[k], bm, k));
-                }
-            }
-            if (self < 0) {  // no self entry among the inline pairs: the own dz rows for db
-                const uint32_t ob = (n * B + b0) * (4u * D);
-                const uint32_t bo = ldb(n, b0 >> 4, true);
-#pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    dbacc += dzb(__builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(dys, lo[b][k], ob, 0)), bo, k);
-            }
-            // the tile's f16 scale exponent
-            uint32_t mt = 0;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) mt = max(mt, __float_as_uint(fabsf(acc[k][c])));
-            const int texp = lg_f16_scale_exp_c(lg_wave_max_bits(mt));
-            const int sl = static_cast<int>(t % R);
-            const uint32_t mnb = tnb[b];
-            issue(bc, nxt, tile + 2 * sc.stride);
-            if (t >= R) pc_wait(&done[prod * NC + static_cast<int>((t - R) % NC)], static_cast<uint32_t>((t - R) / NC + 1));
-            float* slot = ring + sl * LY::TILE;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
-            if (lane == 0) {
-                uint32_t* m = meta + 4 * (prod * R + sl);
-                m[0] = n;
-                m[1] = b0;
-                m[2] = mnb;
-                m[3] = static_cast<uint32_t>(texp);
-            }
-            pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
-            return true;
-        };
-        {
-            uint32_t n0, b00, nb00, n1, b01, nb01;
-            tile_coords(sc.first, n0, b00, nb00);
-            tile_coords(sc.first + sc.stride, n1, b01, nb01);
-            const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
-            issue(std::integral_constant<int, 0>{}, r0, sc.first);
-            issue(std::integral_constant<int, 1>{}, r1, sc.first + sc.stride);
-        }
-        for (int64_t t = 0;; t += 2) {
-            if (!step(std::integral_constant<int, 0>{}, t)) break;
-            if (!step(std::integral_constant<int, 1>{}, t + 1)) break;
-        }
-    } else {
-        // ---------------- consumer: dW += t^T x, dx = t W, masks, store
-        const __amdgpu_buffer_rsrc_t xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
-        float* xt = lds + LY::XOFF + (wave - kBpcProd) * LY::TILE;  // this consumer's x tile
-        const uint32_t* wfr = reinterpret_cast<const uint32_t*>(lds);
-        // x block of this consumer's u-th tile (zeros past the end: a masked-off block)
-        auto xload = [&](int64_t u, f32x4 (&px)[G::K]) {
-            const int64_t tile = sc.first + (u * NC + cons) * sc.stride;
-            uint32_t n, b0, nb;
-            tile_coords(tile, n, b0, nb);
-            n = tile < tend ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(tab[16 * (N + n) + 15])) : 0u;
-            const uint32_t ob = nb ? (n * B + b0) * (4u * D) : kNm3BlkOob;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) {
-                const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-                px[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xs, lk, ob, 0));
-            }
-        };
-#pragma unroll
-        for (int a = 0; a < CH; ++a)
-#pragma unroll
-            for (int b = 0; b < CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int mt = 0; mt < (NB ? CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 px[G::K];
-        xload(0, px);
-        for (int64_t u = 0;; ++u) {
-            const int64_t t = u * NC + cons;
-            const int64_t tile = sc.first + t * sc.stride;
-            if (tile >= tend) break;
-            // x to this consumer's LDS tile; its scale from the lane values
-            uint32_t mx = 0;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) {
-                st4(xt + LY::tix(G::RPI * k + rl, fg), px[k]);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) mx = max(mx, __float_as_uint(fabsf(px[k][c])));
-            }
-            const int xexp = lg_f16_scale_exp_c(lg_wave_max_bits(mx));
-            xload(u + 1, px);  // the next tile's x block in flight under this tile's work
-            const int sl = static_cast<int>(t % R);
-            pc_wait(&ready[prod], static_cast<uint32_t>(t + 1));
-            float* slot = ring + sl * LY::TILE;
-            const uint32_t* m = meta + 4 * (prod * R + sl);
-            const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
-                           nb = __builtin_amdgcn_readfirstlane(m[2]);
-            const int texp = static_cast<int>(__builtin_amdgcn_readfirstlane(m[3]));
-            const float tsc = lg_pow2f(texp), xsc = lg_pow2f(xexp);
-            wave_sync_nm();
-            // dW += t^T x: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
-            {
-                lg_f16x4 xb[CH][2];
-#pragma unroll
-                for (int ni = 0; ni < CH; ++ni) {
-                    f32x4 v;
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const int r = 4 * q + kk, c = 16 * ni + j;
-                        v[kk] = xt[LY::tix(r, c >> 2) + (c & 3)] * xsc;
-                    }
-                    split2_f16_x4(v, xb[ni][0], xb[ni][1]);
-                }
-                const float us = lg_pow2f(-(texp + xexp));
-#pragma unroll
-                for (int mo = 0; mo < CH; ++mo) {
-                    f32x4 v;
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const int r = 4 * q + kk, c = 16 * mo + j;
-                        v[kk] = slot[LY::tix(r, c >> 2) + (c & 3)] * tsc;
-                    }
-                    lg_f16x4 a0, a1;
-                    split2_f16_x4(v, a0, a1);
-                    f32x4 c[CH];
-#pragma unroll
-                    for (int ni = 0; ni < CH; ++ni) {
-                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, xb[ni][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][1], c[ni], 0, 0, 0);
-                        c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][0], c[ni], 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int ni = 0; ni < CH; ++ni)
-#pragma unroll
-                        for (int reg = 0; reg < 4; ++reg) dw[mo][ni][reg] = fmaf(c[ni][reg], us, dw[mo][ni][reg]);
-                }
-            }
-            // dx^T[i][row] = sum_o W^T[i][o] t[row][o]: B fragment = t row j, columns 32 s2 + 8 q ..
-            f32x4 o[CH];
-#pragma unroll
-            for (int mt = 0; mt < CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // W's fragments are loop-invariant LDS reads: an opaque zero offset keeps the compiler
-            // from hoisting all 16 of them (64 VGPRs) out of the tile loop
-            int wz = 0;
-            asm volatile("" : "+v"(wz));
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2) {
-                lg_f16x8 b0f, b1f;
-                split2_f16_x8(ld4(slot + LY::tix(j, 8 * s2 + 2 * q)) * tsc, ld4(slot + LY::tix(j, 8 * s2 + 2 * q + 1)) * tsc,
-                              b0f, b1f);
-#pragma unroll
-                for (int mt = 0; mt < CH; ++mt) {
-                    const lg_f16x8 a0 = *reinterpret_cast<const lg_f16x8*>(wfr + 4 * ((0 * CH * KS + mt * KS + s2) * 64 + lane) + wz);
-                    const lg_f16x8 a1 = *reinterpret_cast<const lg_f16x8*>(wfr + 4 * ((1 * CH * KS + mt * KS + s2) * 64 + lane) + wz);
-                    o[mt] = mfma_h(a1, b0f, o[mt]);
-                    o[mt] = mfma_h(a0, b1f, o[mt]);
-                    o[mt] = mfma_h(a0, b0f, o[mt]);
-                }
-            }
-            const float ux = lg_pow2f(-(wexp + texp));
-#pragma unroll
-            for (int mt = 0; mt < CH; ++mt) {
-                o[mt] *= ux;
-                if (mask_out & 1) {
-                    const f32x4 xm = ld4(xt + LY::tix(j, 4 * mt + q));
-#pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
-                }
-            }
-            if constexpr (NB) {  // node-bias rows: the tile's node has no sensor (uniform test)
-                if (node_slot[n] < 0)
-#pragma unroll
-                    for (int mt = 0; mt < CH; ++mt) nbacc[mt] += o[mt];
-            }
-            // dx back through the slot (this wave's slot reads above are older LDS operations)
-#pragma unroll
-            for (int mt = 0; mt < CH; ++mt) st4(slot + LY::tix(j, 4 * mt + q), o[mt]);
-            wave_sync_nm();
-            const uint32_t ob = (n * B + b0) * (4u * D);
-            f32x4 vk[G::K];
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) vk[k] = ld4(slot + LY::tix(G::RPI * k + rl, fg));
-#pragma unroll
-            for (int k = 0; k < G::K; ++k) {
-                const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                       dxs, lk, ob, 0);
-            }
-            lg_store_guard(vk);
-            wave_sync_nm();
-            pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));
-        }
-    }
-    // ---- per-block reduction of dW / db / node bias (fixed wave order -> deterministic)
-    if (!producer && NB) {
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-            for (int mt = 0; mt < CH; ++mt)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nbacc[mt][i] += __shfl_xor(nbacc[mt][i], off);
-    }
-    if (producer) {
-#pragma unroll
-        for (int off = G::LPR; off < 64; off <<= 1)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) dbacc[i] += __shfl_xor(dbacc[i], off);
-    }
-    __syncthreads();
-    constexpr int L = LY::L;
-    float* red = lds;
-    for (int i = threadIdx.x; i < L; i += blockDim.x) red[i] = 0.f;
-    for (int wv2 = 0; wv2 < NW; ++wv2) {
-        __syncthreads();
-        if (wave == wv2) {
-            if (producer) {
-                if (lane < G::LPR)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) red[D * D + 4 * lane + i] += dbacc[i];
-            } else {
-#pragma unroll
-                for (int mo = 0; mo < CH; ++mo)
-#pragma unroll
-                    for (int ni = 0; ni < CH; ++ni)
-#pragma unroll
-                        for (int reg = 0; reg < 4; ++reg) red[(16 * mo + 4 * q + reg) * D + 16 * ni + j] += dw[mo][ni][reg];
-                if (NB && j == 0)
-#pragma unroll
-                    for (int mt = 0; mt < CH; ++mt)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) red[D * D + D + 16 * mt + 4 * q + i] += nbacc[mt][i];
-            }
-        }
-    }
-    __syncthreads();
-    float* out = slab + static_cast<int64_t>(blockIdx.x) * L;
-    for (int i = threadIdx.x; i < L; i += blockDim.x) out[i] = red[i];
-}
-
 // ------------------------------------------------------------------ single graph (B = 1), row tiles
 // GCNConv on ONE graph (the reference module's own call shape, x [N][D]; BASELINE configs[4]:
 // 100k nodes, 300k edge columns).  The node-major kernels tile one node x 16 windows and
@@ -3339,103 +1807,15 @@ int nm_grid(Kern kernel, int threads, size_t dyn, int64_t ntiles, int waves, int
 
 bool nm_fits(int64_t B, int64_t N, int64_t D) { return N * B * D * 4 <= static_cast<int64_t>(kNm3MaxBytes); }
 
-// Transform selection of the pipelined forward: split-bf16 MFMA by default, exact f32 MFMA
-// under LG_F_F32_MFMA (bit-identical to lg_gcn_fwd).  Lab builds add the LAB floors (bits 28-29).
-template <int D, bool DR>
-auto nm2_kernel(int flags) {
-    const bool split = (flags & LG_F_F32_MFMA) == 0;
-#ifdef LG_KERNEL_LAB
-    switch ((flags >> 28) & 3) {
-        case 1: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 1> : k_gcn_fwd_nm2<D, DR, 4, false, 1>;
-        case 2: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 2> : k_gcn_fwd_nm2<D, DR, 4, false, 2>;
-        case 3: return split ? k_gcn_fwd_nm2<D, DR, 4, true, 3> : k_gcn_fwd_nm2<D, DR, 4, false, 3>;
-        default: break;
-    }
-#endif
-    return split ? k_gcn_fwd_nm2<D, DR, 4, true, 0> : k_gcn_fwd_nm2<D, DR, 4, false, 0>;
-}
-// OPT of the pipelined forward: the build default, or (kernel-lab builds) flags bits 8..11
-// when LG_F_LAB_OPT is set.
-int nm3_opt(int flags) {
-#ifdef LG_KERNEL_LAB
-    const bool ovr = (flags & LG_F_LAB_OPT) && !(flags & (LG_F_F32_MFMA | LG_F_BF16 | LG_F_LAB_DST)) &&
-                     ((flags >> 28) & 7) == 0;
-    if (ovr) return (flags >> LG_F_LAB_OPT_SHIFT) & 15;
-#endif
-    (void)flags;
-    return kNm3OptDefault;
-}
-template <int D, int WV>
-size_t nm3_lds_bytes(bool split, int opt) {
-    switch (opt & (kNm3WFrag | kNm3Swz)) {  // the only bits that change the LDS image
-        case kNm3WFrag: return split ? Nm3Lds<D, true, WV, kNm3WFrag>::BYTES : Nm3Lds<D, false, WV, kNm3WFrag>::BYTES;
-        case kNm3Swz: return split ? Nm3Lds<D, true, WV, kNm3Swz>::BYTES : Nm3Lds<D, false, WV, kNm3Swz>::BYTES;
-        case kNm3WFrag | kNm3Swz:
-            return split ? Nm3Lds<D, true, WV, kNm3WFrag | kNm3Swz>::BYTES
-                         : Nm3Lds<D, false, WV, kNm3WFrag | kNm3Swz>::BYTES;
-        default: return split ? Nm3Lds<D, true, WV, 0>::BYTES : Nm3Lds<D, false, WV, 0>::BYTES;
-    }
-}
-template <int D, bool DR, bool RL, int WV>
+template <int D, bool DR, bool RL>
 auto nm3_kernel(int flags) {
-    constexpr int OD = kNm3OptDefault;
-    if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, true, OD>;
-    const bool split = (flags & LG_F_F32_MFMA) == 0;
-#ifdef LG_KERNEL_LAB
-    const bool dst = (flags & LG_F_LAB_DST) != 0;
-    const int lab = (flags >> 28) & 7;
-    if constexpr (D == 64 && WV == 4) {
-        if ((flags & LG_F_LAB_OPT) && split && !dst && lab == 0) {  // the same test as nm3_opt
-#define LG_NM3_OPTC(O) \
-    case O:            \
-        return k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, false, O>;
-            switch (nm3_opt(flags)) {
-                LG_NM3_OPTC(0)
-                LG_NM3_OPTC(1)
-                LG_NM3_OPTC(2)
-                LG_NM3_OPTC(3)
-                LG_NM3_OPTC(4)
-                LG_NM3_OPTC(5)
-                LG_NM3_OPTC(6)
-                LG_NM3_OPTC(7)
-                LG_NM3_OPTC(8)
-                LG_NM3_OPTC(12)
-                LG_NM3_OPTC(14)
-                LG_NM3_OPTC(15)
-                LG_NM3_OPTC(16)
-                LG_NM3_OPTC(20)
-                LG_NM3_OPTC(22)
-                LG_NM3_OPTC(23)
-                LG_NM3_OPTC(24)
-                LG_NM3_OPTC(28)
-                LG_NM3_OPTC(30)
-                LG_NM3_OPTC(31)
-                default: break;
-            }
-#undef LG_NM3_OPTC
-        }
-    }
-#define LG_NM3_LAB(L)                                                                                              \
-    case L:                                                                                                        \
-        return split ? (dst ? k_gcn_fwd_nm3<D, DR, RL, true, WV, L, true, false, OD>                              \
-                            : k_gcn_fwd_nm3<D, DR, RL, true, WV, L, false, false, OD>)                             \
-                     : (dst ? k_gcn_fwd_nm3<D, DR, RL, false, WV, L, true, false, OD>                             \
-                            : k_gcn_fwd_nm3<D, DR, RL, false, WV, L, false, false, OD>);
-    switch (lab) {
-        LG_NM3_LAB(0)
-        LG_NM3_LAB(1)
-        LG_NM3_LAB(2)
-        LG_NM3_LAB(3)
-        LG_NM3_LAB(4)
-        LG_NM3_LAB(5)
-        LG_NM3_LAB(6)
-        LG_NM3_LAB(7)
-        default: break;
-    }
-#undef LG_NM3_LAB
-#endif
-    return split ? k_gcn_fwd_nm3<D, DR, RL, true, WV, 0, false, false, OD>
-                 : k_gcn_fwd_nm3<D, DR, RL, false, WV, 0, false, false, OD>;
+    if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, 4, true>;
+    return (flags & LG_F_F32_MFMA) ? k_gcn_fwd_nm3<D, DR, RL, false, 4> : k_gcn_fwd_nm3<D, DR, RL, true, 4>;
+}
+template <int D, bool DR, bool RL>
+auto pc_kernel(bool bf16, bool f16) {
+    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, 2>
+                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, 2> : k_gcn_fwd_pc<D, DR, RL, false, false, 4, 2>);
 }
 
 }  // namespace
@@ -3451,114 +1831,52 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     if (B == 0) return LG_OK;
     if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
     const int64_t ngroups = (B + 15) / 16, ntiles = ngroups * N;
-    const float relu_floor = (flags & LG_F_RELU) ? 0.f : -__builtin_huge_valf();
     const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const float* bp = (flags & LG_F_BIAS) ? bias : nullptr;
-    // schedule bits (never change results): LG_F_LAB_V1 = one tile per wave, LG_F_LAB_NM2 =
-    // the rowptr-walking pipeline, LG_F_LAB_W8 = 8-wave workgroups, LG_F_LAB_BPC(n) = at most
-    // n workgroups per CU
-    const bool lab_v1 = (flags & LG_F_LAB_V1) != 0, lab_nm2 = (flags & LG_F_LAB_NM2) != 0;
-    if (ymask && (lab_v1 || lab_nm2 || (flags & LG_F_LAB_DST))) return LG_EUNSUPPORTED;  // lab schedules: no mask
-    const bool w8 = (flags & LG_F_LAB_W8) != 0;
-    const bool w5 = (flags & LG_F_LAB_W5) != 0;
     const bool relu = (flags & LG_F_RELU) != 0;
-    const int bpc = ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) : 3;
     const bool bf16 = (flags & LG_F_BF16) != 0;
-    // Default (no schedule / transform bits): the producer / consumer pipeline with the 2-way
-    // fp16 transform (k_gcn_fwd_pc, F16) for the fp32 tier — the fastest measured
-    // (profiles/r03: 18.2-18.6 us against 19.9 for nm3 at B = 256) — and nm3's single bf16
-    // product for the bf16 tier.  LG_F_NM3 keeps nm3's 3-way bf16 split (bit-identical to pc
-    // and nm5 without LG_F_F16X2).
-    const bool sched_bits = (flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5 | LG_F_LAB_V1 |
-                                      LG_F_LAB_NM2 | LG_F_NM3 | LG_F_NM5 | LG_F_PC)) != 0 ||
-                            ((flags >> 28) & 7) != 0 || (flags & LG_F_LAB_OPT) != 0;
-    const bool dflt = !sched_bits && !bf16;
-    const bool clean = !(flags & (LG_F_F32_MFMA | LG_F_LAB_DST | LG_F_LAB_W8 | LG_F_LAB_W5)) && ((flags >> 28) & 7) == 0;
-    // the W-in-registers pipeline (k_gcn_fwd_nm5): same results as nm3, split or bf16 transform
-    const bool nm5 = (flags & LG_F_NM5) && clean;
-    const bool f16 = ((flags & LG_F_F16X2) != 0 || dflt) && !bf16;  // the 2-way fp16 transform (nm5 / pc)
-    // the producer / consumer pipeline (k_gcn_fwd_pc)
-    const bool pc = ((flags & LG_F_PC) && clean) || dflt;
+    // Kernel and transform (results: see include/leakgnn.h):
+    //   fp32 tier, default: the producer / consumer pipeline k_gcn_fwd_pc with the 2-way fp16
+    //     transform; LG_F_BF16X3: the same pipeline on the 3-way bf16 split;
+    //   LG_F_NM3: the per-wave pipeline k_gcn_fwd_nm3 (3-way bf16 split; LG_F_F32_MFMA: exact
+    //     fp32 MFMA, bit-identical to lg_gcn_fwd);
+    //   bf16 tier (LG_F_BF16): nm3's single bf16 product, or pc's with LG_F_PC.
+    const bool nm3 = (flags & (LG_F_NM3 | LG_F_F32_MFMA)) != 0 || (bf16 && !(flags & LG_F_PC));
+    const bool f16 = !bf16 && !(flags & LG_F_BF16X3);
     (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
-    const bool split = (flags & LG_F_F32_MFMA) == 0;
     hipStream_t s = lg_stream(stream);
     const uint32_t N32 = static_cast<uint32_t>(N), B32 = static_cast<uint32_t>(B), G32 = static_cast<uint32_t>(ngroups);
-#define LG_NM_FWD(DD, DR)                                                                                          \
-    do {                                                                                                           \
-        if (lab_v1) {                                                                                              \
-            auto kern = k_gcn_fwd_nm<DD, DR>;                                                                      \
-            const size_t dyn1 = 4 * static_cast<size_t>(DD * (DD + 4) + DD + kNmFwdWaves * 16 * (DD + 4));        \
-            const int grid = nm_grid(kern, 64 * kNmFwdWaves, dyn1, ntiles, kNmFwdWaves, 4);                        \
-            lg_launch(kern, grid, 64 * kNmFwdWaves, dyn1, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,     \
-                                                      dropout_p, scale, seed, salt);                               \
-        } else if (lab_nm2) {                                                                                      \
-            auto kern = nm2_kernel<DD, DR>(flags);                                                                 \
-            const size_t dyn2 = split ? Nm2Lds<DD, true>::BYTES : Nm2Lds<DD, false>::BYTES;                        \
-            const int grid = nm_grid(kern, 64 * kNm2Waves, dyn2, ntiles, kNm2Waves, bpc);                          \
-            lg_launch(kern, grid, 64 * kNm2Waves, dyn2, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, relu_floor,       \
-                                                    dropout_p, scale, seed, salt);                                 \
-        } else if (pc) {                                                                                           \
-            const int np = (flags & LG_F_PC6) ? 6 : 4, nc = (np == 6 || (flags & LG_F_PC1)) ? 1 : 2;                \
-            auto pick = [&](auto pcc, auto ncc) {                                                                  \
-                constexpr int PP = decltype(pcc)::value, NCC = decltype(ncc)::value;                               \
-                return relu ? (bf16 ? k_gcn_fwd_pc<DD, DR, true, true, false, PP, NCC>                             \
-                                    : (f16 ? k_gcn_fwd_pc<DD, DR, true, false, true, PP, NCC>                      \
-                                           : k_gcn_fwd_pc<DD, DR, true, false, false, PP, NCC>))                   \
-                            : (bf16 ? k_gcn_fwd_pc<DD, DR, false, true, false, PP, NCC>                            \
-                                    : (f16 ? k_gcn_fwd_pc<DD, DR, false, false, true, PP, NCC>                     \
-                                           : k_gcn_fwd_pc<DD, DR, false, false, false, PP, NCC>));                 \
-            };                                                                                                     \
-            using I1 = std::integral_constant<int, 1>;                                                             \
-            using I2 = std::integral_constant<int, 2>;                                                             \
-            using I4 = std::integral_constant<int, 4>;                                                             \
-            using I6 = std::integral_constant<int, 6>;                                                             \
-            auto kern = np == 6 ? pick(I6{}, I1{}) : nc == 1 ? pick(I4{}, I1{}) : pick(I4{}, I2{});                \
-            const size_t dynp = np == 6 ? PcLds<DD, 6, 1>::BYTES : nc == 1 ? PcLds<DD, 4, 1>::BYTES                \
-                                                                          : PcLds<DD, 4, 2>::BYTES;                \
-            const int thr = 64 * np * (1 + nc);                                                                    \
-            const int grid = nm_grid(kern, thr, dynp, ntiles, np, 1);                                              \
-            lg_launch(kern, grid, thr, dynp, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,    \
-                      salt, ymask);                                                                                \
-        } else if (nm5) {                                                                                          \
-            auto kern = relu ? (bf16 ? k_gcn_fwd_nm5<DD, DR, true, true>                                           \
-                                     : (f16 ? k_gcn_fwd_nm5<DD, DR, true, false, true> : k_gcn_fwd_nm5<DD, DR, true, false>)) \
-                             : (bf16 ? k_gcn_fwd_nm5<DD, DR, false, true>                                          \
-                                     : (f16 ? k_gcn_fwd_nm5<DD, DR, false, false, true> : k_gcn_fwd_nm5<DD, DR, false, false>)); \
-            const size_t dyn5 = Nm5Lds<DD>::BYTES;                                                                 \
-            const int grid = nm_grid(kern, 64 * kNm5Waves, dyn5, ntiles, kNm5Waves,                               \
-                                     ((flags >> LG_F_LAB_BPC_SHIFT) & 0xF) ? bpc : LG_NM5_OCC);                    \
-            lg_launch(kern, grid, 64 * kNm5Waves, dyn5, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, \
-                      seed, salt, ymask);                                                                          \
-        } else if (w5) {                                                                                           \
-            auto kern = relu ? nm3_kernel<DD, DR, true, 5>(flags) : nm3_kernel<DD, DR, false, 5>(flags);           \
-            const size_t dyn3 = nm3_lds_bytes<DD, 5>(split, kNm3OptDefault);                  \
-            const int grid = nm_grid(kern, 64 * 5, dyn3, ntiles, 5, bpc);                                          \
-            lg_launch(kern, grid, 64 * 5, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt, ymask);                                                                 \
-        } else if (w8) {                                                                                           \
-            auto kern = relu ? nm3_kernel<DD, DR, true, 8>(flags) : nm3_kernel<DD, DR, false, 8>(flags);           \
-            const size_t dyn3 = nm3_lds_bytes<DD, 8>(split, kNm3OptDefault);                  \
-            const int grid = nm_grid(kern, 64 * 8, dyn3, ntiles, 8, bpc);                                          \
-            lg_launch(kern, grid, 64 * 8, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt, ymask);                                                                 \
-        } else {                                                                                                   \
-            auto kern = relu ? nm3_kernel<DD, DR, true, 4>(flags) : nm3_kernel<DD, DR, false, 4>(flags);           \
-            const size_t dyn3 = nm3_lds_bytes<DD, 4>(split, DD == 64 ? nm3_opt(flags) : kNm3OptDefault);                  \
-            const int grid = nm_grid(kern, 64 * 4, dyn3, ntiles, 4, bpc);                                          \
-            lg_launch(kern, grid, 64 * 4, dyn3, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,   \
-                                            salt, ymask);                                                                 \
-        }                                                                                                          \
-    } while (0)
+    auto launch = [&](auto dc, auto drc) {
+        constexpr int DD = decltype(dc)::value;
+        constexpr bool DR = decltype(drc)::value;
+        if (nm3) {
+            auto kern = relu ? nm3_kernel<DD, DR, true>(flags) : nm3_kernel<DD, DR, false>(flags);
+            const size_t dyn = (flags & LG_F_F32_MFMA) && !bf16 ? Nm3Lds<DD, false, 4>::BYTES : Nm3Lds<DD, true, 4>::BYTES;
+            const int grid = nm_grid(kern, 64 * 4, dyn, ntiles, 4, 3);
+            lg_launch(kern, grid, 64 * 4, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
+                      salt, ymask);
+        } else {
+            auto kern = relu ? pc_kernel<DD, DR, true>(bf16, f16) : pc_kernel<DD, DR, false>(bf16, f16);
+            const size_t dyn = PcLds<DD, 4, 2>::BYTES;
+            const int thr = 64 * 4 * 3;
+            const int grid = nm_grid(kern, thr, dyn, ntiles, 4, 1);
+            lg_launch(kern, grid, thr, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
+                      salt, ymask);
+        }
+    };
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    using T = std::true_type;
+    using F = std::false_type;
     if (D == 64) {
-        if (drop) LG_NM_FWD(64, true);
-        else LG_NM_FWD(64, false);
+        if (drop) launch(I64{}, T{});
+        else launch(I64{}, F{});
     } else {
-        if (drop) LG_NM_FWD(32, true);
-        else LG_NM_FWD(32, false);
+        if (drop) launch(I32{}, T{});
+        else launch(I32{}, F{});
     }
-#undef LG_NM_FWD
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
@@ -3592,66 +1910,37 @@ extern "C" int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D) {
 extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                              const float* x, const float* W, float* dx_out, float* dW, float* db,
                              const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
-                             float scale_in, float scale_out, void* workspace, lg_stream_t stream, const uint16_t* ymask) {
+                             float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream, const uint16_t* ymask) {
     if (B < 0 || N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
     if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     if (mask_in && !y && !ymask) return LG_EINVAL;
     const bool mbits = mask_in && ymask != nullptr;
-    if (mbits && (flags & LG_F_LAB_NM2)) return LG_EUNSUPPORTED;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
     const int64_t ngroups = (B + 15) / 16, ntiles = std::max<int64_t>(ngroups * N, 0);
-    // bit 0: MASK_OUT; bit 1: LG_F_DX_SENSOR_ROWS (nm3 only; other schedules write every row)
+    // bit 0: MASK_OUT; bit 1: LG_F_DX_SENSOR_ROWS
     const int mask_out = ((flags & LG_F_MASK_OUT) ? 1 : 0) | ((node_slot && (flags & LG_F_DX_SENSOR_ROWS)) ? 2 : 0);
-    const size_t dyn = 4 * static_cast<size_t>(kNmBwdWaves * 2 * 16 * (D + 4) + D * (D + 4));
     const int2* pr = reinterpret_cast<const int2*>(pairs_t);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
+    // the launch grid is at most 2 x CUs workgroups, one slab row each
+    if (ws_bytes < lg_gcn_bwd_nm_workspace_bytes(D)) return LG_EINVAL;
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
     const bool bf = (flags & LG_F_BF16) != 0;
-    // fp32 tier, default: k_gcn_bwd_nm3 on the 3-way bf16 split (fastest measured,
-    // profiles/r03/r03u).  Lab variants: LG_F_F16X2 the 2-way fp16 split in nm3 (spills at
-    // 256 VGPRs), LG_F_PC | LG_F_F16X2 the producer / consumer kernel k_gcn_bwd_pc (D = 64)
-    const bool f16 = !bf && (flags & LG_F_F16X2);
-    const bool pcb = f16 && (flags & LG_F_PC);
+    // k_gcn_bwd_nm3: the 3-way bf16 split (fp32 tier) or the single bf16 product (LG_F_BF16)
     int grid = 1;
     // B == 0 still runs one (empty) launch so the slab holds zeros
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
     do {                                                                                                           \
-        if (flags & LG_F_LAB_NM2) {                                                                                \
-            auto kern = k_gcn_bwd_nm<DD, MI, NBB>;                                                                 \
-            grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves, dyn, std::max<int64_t>(ntiles, 1), kNmBwdWaves, 2),\
-                                 2 * lg_num_cus());                                                                \
-            lg_launch(kern, grid, 64 * kNmBwdWaves, dyn, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,          \
-                                                     static_cast<uint32_t>(N), static_cast<uint32_t>(B),           \
-                                                     static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,       \
-                                                     scale_out);                                                   \
-        } else if (DD == 64 && pcb && (!MI || mbits)) {                                                          \
-            auto kern = k_gcn_bwd_pc<MI, NBB>;                                                                     \
-            const size_t dynp = BpcLds::BYTES;                                                                     \
-            grid = std::min<int>(nm_grid(kern, 64 * kBpcProd * (1 + kBpcCons), dynp, std::max<int64_t>(ntiles, 1),  \
-                                         kBpcProd, 1),                                                             \
-                                 2 * lg_num_cus());                                                                \
-            lg_launch(kern, grid, 64 * kBpcProd * (1 + kBpcCons), dynp, s, nodetab_t, pr, dy, x, W, node_slot,     \
-                      dx_out, slab, static_cast<uint32_t>(N), static_cast<uint32_t>(B),                            \
-                      static_cast<uint32_t>(ngroups), fd, mask_out, scale_in, scale_out, ymask);                   \
-        } else {                                                                                                   \
-            auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI>                                   \
-                                            : (f16 ? k_gcn_bwd_nm3<DD, MI, NBB, false, MI, true>                     \
-                                                   : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>))                          \
-                                      : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true>                                       \
-                                            : (f16 ? k_gcn_bwd_nm3<DD, MI, NBB, false, false, true>                  \
-                                                   : k_gcn_bwd_nm3<DD, MI, NBB, false>));                             \
-            const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                             \
-            grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, \
-                                         2),                                                                       \
-                                 2 * lg_num_cus());                                                                \
-            lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,        \
-                                                       static_cast<uint32_t>(N), static_cast<uint32_t>(B),         \
-                                                       static_cast<uint32_t>(ngroups), fd, mask_out, scale_in,     \
-                                                       scale_out, ymask);                                          \
-        }                                                                                                          \
+        auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>)  \
+                                  : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>);        \
+        const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                                 \
+        grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, 2), \
+                             2 * lg_num_cus());                                                                    \
+        lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,      \
+                  static_cast<uint32_t>(N), static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd, mask_out, \
+                  scale_in, scale_out, ymask);                                                                     \
     } while (0)
 #define LG_NM_BWD_D(DD)                                  \
     do {                                                 \
@@ -3676,9 +1965,9 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
 extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                              const float* x, const float* W, float* dx_out, float* dW, float* db,
                              const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
-                             float scale_in, float scale_out, void* workspace, lg_stream_t stream) {
+                             float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     return lg_gcn_bwd_nm_bits(nodetab_t, pairs_t, dy, y, x, W, dx_out, dW, db, node_slot, dnode_bias, B, N, D, flags,
-                              scale_in, scale_out, workspace, stream, nullptr);
+                              scale_in, scale_out, workspace, ws_bytes, stream, nullptr);
 }
 
 extern "C" int lg_gcn_fwd_rows(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
@@ -3705,10 +1994,11 @@ extern "C" int lg_gcn_fwd_rows(const int32_t* nodetab, const int32_t* pairs, con
 }
 
 extern "C" int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* x,
-                               const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace,
+                               const float* W, float* dx, float* dW, float* db, int64_t N, int64_t D, void* workspace, int64_t ws_bytes,
                                lg_stream_t stream) {
     if (N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx || !dW || !workspace) return LG_EINVAL;
     if (D != 64 || !nm_fits(1, N, D)) return LG_EUNSUPPORTED;
+    if (ws_bytes < lg_gcn_bwd_nm_workspace_bytes(D)) return LG_EINVAL;  // <= 2 x CUs slab rows
     const int64_t ntiles = (N + 15) / 16;
     hipStream_t s = lg_stream(stream);
     const size_t dyn = RowsLds::bwd_bytes();

@@ -201,10 +201,11 @@ extern "C" int64_t lg_graph_workspace_bytes(int64_t E, int64_t N) {
 
 extern "C" int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N, int add_self_loops, int normalize,
                               float fill_value, int32_t* rowptr, int32_t* col, float* w, int32_t* rowptr_t,
-                              int32_t* col_t, float* w_t, void* workspace, lg_stream_t stream) {
+                              int32_t* col_t, float* w_t, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (E < 0 || N <= 0 || N > INT32_MAX / 2 || E > INT32_MAX / 2) return LG_EINVAL;
     if ((E > 0 && !edge_index) || !rowptr || !col || !w || !rowptr_t || !col_t || !w_t || !workspace)
         return LG_EINVAL;
+    if (ws_bytes < lg_graph_workspace_bytes(E, N)) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     int32_t* cnt = static_cast<int32_t*>(workspace);
     int32_t* cnt_t = cnt + N;
@@ -242,9 +243,10 @@ extern "C" int64_t lg_incidence_workspace_bytes(int64_t P, int64_t N) {
 }
 
 extern "C" int lg_incidence_build(const int64_t* ends, int64_t P, int64_t N, int32_t* inc_rowptr,
-                                  int32_t* inc_item, void* workspace, lg_stream_t stream) {
+                                  int32_t* inc_item, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (P < 0 || N <= 0 || 2 * P > INT32_MAX / 2 || N > INT32_MAX / 2) return LG_EINVAL;
     if ((P > 0 && (!ends || !inc_item)) || !inc_rowptr || !workspace) return LG_EINVAL;
+    if (ws_bytes < lg_incidence_workspace_bytes(P, N)) return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
     int32_t* cnt = static_cast<int32_t*>(workspace);
     int32_t* cur = cnt + N;

@@ -760,7 +760,7 @@ extern "C" int lg_gru_fwd(const float* residual, const float* tfeat, const float
 extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
                           const float* h_seq, const float* gates, const float* dh_last, float* dx, float* dw_ih,
                           float* dw_hh, float* db_ih, float* db_hh, int64_t B, int64_t L, int64_t S, int64_t I,
-                          int64_t H, void* workspace, lg_stream_t stream) {
+                          int64_t H, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (!dims_ok(B, L, S)) return LG_EINVAL;
     if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
     if (!residual || !w_ih || !w_hh || !h_seq || !gates || !dh_last || !dw_ih || !dw_hh || !db_ih || !db_hh ||
@@ -771,6 +771,7 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
     const int nb = static_cast<int>(std::max<int64_t>(1, dx ? nblocks_seq(B * S) : nblocks_seq2(B * S)));
     float* slab = static_cast<float*>(workspace);
     const int64_t G3 = 3 * H, len = G3 * H + G3 * I + 2 * G3;
+    if (ws_bytes < nb * len * static_cast<int64_t>(sizeof(float))) return LG_EINVAL;
     if (B == 0) {
         if (hipMemsetAsync(slab, 0, sizeof(float) * len, s) != hipSuccess) return LG_EHIP;
     } else {

@@ -489,7 +489,7 @@ extern "C" int64_t lg_sensor_proj_bwd_workspace_bytes(int64_t B, int64_t S, int6
 
 extern "C" int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, const float* live, const float* h_s,
                                   const float* W, const float* dbias_in, float* dh_s, float* dW, float* db, int64_t B,
-                                  int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace,
+                                  int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, void* workspace, int64_t ws_bytes,
                                   lg_stream_t stream) {
     if (B < 0 || N <= 0 || S < 0 || !W || !dW || !db || !workspace) return LG_EINVAL;
     if (B * S > 0 && (!dx0 || !sensor_idx || !h_s || !dh_s)) return LG_EINVAL;
@@ -497,6 +497,7 @@ extern "C" int lg_sensor_proj_bwd(const float* dx0, const int64_t* sensor_idx, c
     const int nm = (flags & LG_F_NODE_MAJOR) ? 1 : 0;
     const int G = static_cast<int>(std::max<int64_t>(1, ceil_div(B * S, kSpRows)));
     const int64_t SL = D * (Ds + 1) + D;
+    if (ws_bytes < G * SL * static_cast<int64_t>(sizeof(float))) return LG_EINVAL;
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
     // inside a reduce batch dbias_in may still be pending (the layer-0 backward's reduction
@@ -521,13 +522,14 @@ extern "C" int64_t lg_linear_dw_workspace_bytes(int64_t K, int64_t M, int64_t N)
 }
 
 extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t M, int64_t N, float* dw, float* db,
-                            void* workspace, lg_stream_t stream) {
+                            void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (K < 0 || !dw || !workspace || (K > 0 && (!dy || !x))) return LG_EINVAL;
     if ((M != 32 && M != 64) || (N != 32 && N != 64)) return LG_EUNSUPPORTED;
     hipStream_t s = lg_stream(stream);
     const int G = linear_dw_grid(K);
     float* slab = static_cast<float*>(workspace);
     const int64_t SL = M * (N + 1) + M;
+    if (ws_bytes < G * SL * static_cast<int64_t>(sizeof(float))) return LG_EINVAL;
     if (K == 0) {
         if (hipMemsetAsync(slab, 0, SL * sizeof(float), s) != hipSuccess) return LG_EHIP;
     } else {
@@ -544,7 +546,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 20; }
+extern "C" int lg_abi_version(void) { return 21; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

@@ -109,7 +109,7 @@ extern "C" int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T) {
 
 extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
                              float beta2, float eps, float weight_decay, float max_norm, float* norm_out,
-                             void* workspace, lg_stream_t stream) {
+                             void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (T > kOptMaxTensors) return LG_EUNSUPPORTED;
     if (T < 0 || (T > 0 && (!table || !sizes)) || !step || !workspace) return LG_EINVAL;
     if (!(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(eps >= 0.f)) return LG_EINVAL;
@@ -125,6 +125,7 @@ extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, 
     }
     a.T = T;
     const int G = static_cast<int>(std::max<int64_t>(1, (a.off[T] + kOptChunk - 1) / kOptChunk));
+    if (ws_bytes < G * static_cast<int64_t>(sizeof(double))) return LG_EINVAL;  // one fp64 partial per slice
     double* partial = static_cast<double*>(workspace);
     hipStream_t s = lg_stream(stream);
     lg_launch(k_adam_norm, G, kOptThreads, 0, s, a, partial, step);

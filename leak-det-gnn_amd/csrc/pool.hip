@@ -195,7 +195,7 @@ extern "C" int64_t lg_pool_head_bwd_workspace_bytes(int64_t B, int64_t D, int64_
 extern "C" int lg_pool_head_bwd(const float* pooled, const float* hid, const float* w1, const float* w2,
                                 const float* dlogits, int64_t ldo, int64_t col, float* dpooled, float* dw1,
                                 float* db1, float* dw2, float* db2, int64_t B, int64_t D, int64_t hidden, int flags,
-                                float dropout_p, void* workspace, lg_stream_t stream) {
+                                float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (B < 0 || col < 0 || ldo <= col) return LG_EINVAL;
     if (hidden != kHid || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
@@ -205,6 +205,7 @@ extern "C" int lg_pool_head_bwd(const float* pooled, const float* hid, const flo
     const float scale = drop ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const int G = pool_bwd_grid(B);
     const int64_t SL = kHid * D + 2 * kHid;
+    if (ws_bytes < ((G * SL * 4 + 255) & ~int64_t(255)) + G * 8) return LG_EINVAL;
     float* slab = static_cast<float*>(workspace);
     double* dslab = reinterpret_cast<double*>(static_cast<char*>(workspace) + ((G * SL * 4 + 255) & ~int64_t(255)));
     hipStream_t s = lg_stream(stream);

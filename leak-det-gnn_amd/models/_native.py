@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 20  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 21  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -25,18 +25,11 @@ LG_F_MASK_OUT = 0x10
 LG_F_NODE_MAJOR = 0x20
 LG_F_DX_SENSOR_ROWS = 0x10000000  # lg_gcn_bwd_nm[_bits] with node_slot: non-sensor dx rows may stay unwritten
 LG_SALT_SEED_PTR = 0x80000000  # salt bit 31: `seed` is the address of a device-resident uint64
-LG_F_LAB_V1 = 0x00800000  # kernel-lab schedule bit of lg_gcn_fwd_nm (tools/kbench.py)
-LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: exact f32 MFMA transform (default: 3-way split bf16 MFMA)
-LG_F_LAB_NM2 = 0x00200000  # lg_gcn_fwd_nm schedule: round-1 rowptr-walking pipeline (kernel lab)
+LG_F_F32_MFMA = 0x00400000  # lg_gcn_fwd_nm: the per-wave pipeline on exact f32 MFMA (bit-identical to lg_gcn_fwd)
 LG_F_BF16 = 0x40  # lg_gcn_fwd_nm / lg_gcn_bwd_nm / lg_edge_head_*: the bf16 node-MLP tier
-LG_F_LAB_W8 = 0x00100000  # lg_gcn_fwd_nm schedule: 8-wave workgroups (kernel lab)
-LG_F_LAB_W5 = 0x00040000  # lg_gcn_fwd_nm schedule: 5-wave workgroups (kernel lab)
-LG_F_NM5 = 0x00002000  # lg_gcn_fwd_nm schedule: W-in-registers pipeline (same results)
-LG_F_PC = 0x00004000  # lg_gcn_fwd_nm schedule: producer / consumer waves (same results)
-LG_F_F16X2 = 0x00008000  # lg_gcn_fwd_nm + LG_F_NM5/PC: 2-way fp16 split transform (fp32-level accuracy)
-LG_F_PC1 = 0x00010000  # with LG_F_PC: one consumer wave per producer (default two)
-LG_F_NM3 = 0x00020000  # lg_gcn_fwd_nm schedule: per-wave nm3 pipeline, 3-way bf16 split
-LG_F_PC6 = 0x00000080  # with LG_F_PC: six producers, one consumer each
+LG_F_PC = 0x00004000  # with LG_F_BF16: the producer / consumer forward (default: nm3)
+LG_F_BF16X3 = 0x00008000  # lg_gcn_fwd_nm fp32 tier: pc with the 3-way bf16 split (default: 2-way fp16 split)
+LG_F_NM3 = 0x00020000  # lg_gcn_fwd_nm: the per-wave nm3 pipeline, 3-way bf16 split
 
 _i32, _i64, _u32, _u64, _f32, _p = (ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64,
                                     ctypes.c_float, ctypes.c_void_p)
@@ -52,56 +45,50 @@ SIGNATURES = {
     "lg_cross_entropy_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
     "lg_cross_entropy_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_clip_adamw_workspace_bytes": (_i64, [_p, _i32]),
-    "lg_clip_adamw": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _p]),
+    "lg_clip_adamw": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _i64, _p]),
     "lg_timing_arm": (_i32, [_i32]),
     "lg_timing_disarm": (_i32, []),
     "lg_timing_elapsed": (_i32, [_i32, _p]),
     "lg_graph_workspace_bytes": (_i64, [_i64, _i64]),
-    "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "lg_graph_build": (_i32, [_p, _i64, _i64, _i32, _i32, _f32, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "lg_nm_table_build": (_i32, [_p, _p, _i64, _p, _p, _p]),
     "lg_rcm_order": (_i32, [_p, _i64, _i64, _p]),
     "lg_incidence_workspace_bytes": (_i64, [_i64, _i64]),
-    "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _p]),
+    "lg_incidence_build": (_i32, [_p, _i64, _i64, _p, _p, _p, _i64, _p]),
     "lg_batchify_edge_index": (_i32, [_p, _i64, _i64, _i64, _p, _p]),
     "lg_linear_dw_workspace_bytes": (_i64, [_i64, _i64, _i64]),
-    "lg_linear_dw": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _p]),
+    "lg_linear_dw": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, _p, _i64, _p]),
     "lg_node_init_fwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_node_init_proj_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32,
                                      _p]),
     "lg_sensor_proj_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
-    "lg_sensor_proj_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _p, _p]),
+    "lg_sensor_proj_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _p, _i64, _p]),
     "lg_gcn_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_spmm": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_gcn_bwd_workspace_bytes": (_i64, [_i64]),
-    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32,
-                          _p, _p]),
+    "lg_gcn_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _f32, _p, _i64, _p]),
     "lg_pipe_gather_fwd": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),
     "lg_gcn_fwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_gcn_fwd_nm_bits": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p, _p]),
     "lg_gcn_fwd_rows": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p]),
-    "lg_gcn_bwd_rows": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p, _p]),
-    "lg_gcn_bwd_nm_bits": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p,
-                                  _p, _p]),
+    "lg_gcn_bwd_rows": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p]),
+    "lg_gcn_bwd_nm_bits": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p, _i64, _p, _p]),
     "lg_gcn_bwd_nm_workspace_bytes": (_i64, [_i64]),
-    "lg_gcn_bwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p,
-                             _p]),
+    "lg_gcn_bwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p, _i64, _p]),
     "lg_edge_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32,
                                 _u64, _u32, _p]),
     "lg_edge_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
-    "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32,
-                                _f32, _p, _p]),
-    "lg_edge_head_bwd_scatter": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
-                                        _i64, _i64, _i64, _i32, _f32, _p, _p]),
+    "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
+    "lg_edge_head_bwd_scatter": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
     "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
     "lg_pool_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64,
                                 _u32, _p]),
     "lg_pool_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64]),
-    "lg_pool_head_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p,
-                                _p]),
+    "lg_pool_head_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
     "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
-    "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _p]),
+    "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_tcn_packed_weight_floats": (_i64, [_i64]),
     "lg_tcn_pack_weight": (_i32, [_p, _p, _i64, _p]),
     "lg_tcn_conv_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _f32, _p, _i64, _i64, _i64, _i64, _i64, _p]),

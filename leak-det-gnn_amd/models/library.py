@@ -31,7 +31,7 @@ from torch import Tensor
 
 from . import _native as nat
 from ._native import check, load_library, ptr, stream_of
-from .ops import EDGE_HEAD_SALT, GCN_FWD_NM_EXTRA_FLAGS, NOLEAK_HEAD_SALT, _check_d, _timed
+from .ops import EDGE_HEAD_SALT, GCN_FWD_NM_EXTRA_FLAGS, NM_MAX_BYTES, NOLEAK_HEAD_SALT, _check_d, _timed
 
 NS = "leakgnn"
 
@@ -64,6 +64,13 @@ def _c(t: Optional[Tensor]) -> Optional[Tensor]:
 # fp32 MFMA, and the D = 32 path)
 _ROWS = True
 
+
+def _use_rows(Ntot: int, D: int) -> bool:
+    """The row-tile kernels take the graph only when its node-major activation fits one launch's
+    32-bit buffer offsets (N * D * 4 <= ops.NM_MAX_BYTES, ~8.4M nodes at D = 64); larger graphs
+    go to lg_gcn_fwd / lg_gcn_bwd (window-major, up to kLgMaxRows rows)."""
+    return D == 64 and _ROWS and Ntot * D * 4 <= NM_MAX_BYTES
+
 @torch.library.custom_op(f"{NS}::gcn_conv", mutates_args=(), device_types="cuda")
 def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, col: Tensor, w: Tensor,
              rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, nodetab: Tensor, pairs: Tensor, nodetab_t: Tensor,
@@ -81,7 +88,7 @@ def gcn_conv(x: Tensor, weight: Tensor, bias: Optional[Tensor], rowptr: Tensor, 
     y = torch.empty_like(x)
     flags = nat.LG_F_BIAS if bias is not None else 0
     with _timed("gcn_fwd", x.device):
-        if D == 64 and _ROWS:
+        if _use_rows(Ntot, D):
             check(lib.lg_gcn_fwd_rows(ptr(nodetab), ptr(pairs), ptr(x), ptr(weight), ptr(bias), ptr(y), Ntot, D, flags,
                                       stream_of(x)), "lg_gcn_fwd_rows")
         else:
@@ -108,14 +115,14 @@ def gcn_conv_backward(dy: Tensor, x: Tensor, weight: Tensor, rowptr_t: Tensor, c
     dW = torch.empty_like(weight)
     db = torch.empty(D, device=x.device, dtype=x.dtype)
     with _timed("gcn_bwd", x.device):
-        if D == 64 and _ROWS:
+        if _use_rows(Ntot, D):
             ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
             check(lib.lg_gcn_bwd_rows(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(x), ptr(weight), ptr(dx), ptr(dW),
-                                      ptr(db), Ntot, D, ptr(ws), stream_of(x)), "lg_gcn_bwd_rows")
+                                      ptr(db), Ntot, D, ptr(ws), ws.numel(), stream_of(x)), "lg_gcn_bwd_rows")
         else:
             ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=x.device, dtype=torch.uint8)
             check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), None, ptr(x), ptr(weight), ptr(dx),
-                                 ptr(dW), ptr(db), None, None, 1, Ntot, D, col_t.numel(), 0, 1.0, 1.0, ptr(ws),
+                                 ptr(dW), ptr(db), None, None, 1, Ntot, D, col_t.numel(), 0, 1.0, 1.0, ptr(ws), ws.numel(),
                                  stream_of(x)), "lg_gcn_bwd")
     return dx, dW, db
 
@@ -205,7 +212,7 @@ def sensor_proj_backward(dproj: Tensor, h_s: Tensor, weight: Tensor) -> Tuple[Te
     db = torch.empty(D, device=d2.device, dtype=torch.float32)
     ws = torch.empty(int(lib.lg_linear_dw_workspace_bytes(K, D, Ds)), device=d2.device, dtype=torch.uint8)
     with _timed("linear_dw", d2.device):
-        check(lib.lg_linear_dw(ptr(d2), ptr(h2), K, D, Ds, ptr(dW), ptr(db), ptr(ws), stream_of(d2)), "lg_linear_dw")
+        check(lib.lg_linear_dw(ptr(d2), ptr(h2), K, D, Ds, ptr(dW), ptr(db), ptr(ws), ws.numel(), stream_of(d2)), "lg_linear_dw")
     return dh, dW, db
 
 
@@ -285,7 +292,7 @@ def gru_encoder_backward(dh: Tensor, residual: Tensor, tfeat: Optional[Tensor], 
     with _timed("gru_bwd", dev):
         check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates), ptr(dh),
                              ptr(dx) if need_dx else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L, S, I,
-                             H, ptr(ws), stream_of(residual)), "lg_gru_bwd")
+                             H, ptr(ws), ws.numel(), stream_of(residual)), "lg_gru_bwd")
     return dx, dw_ih, dw_hh, db_ih, db_hh
 
 
@@ -477,11 +484,11 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
                 bits = ptr(ymask) if (l == L - 1 and ymask.numel() > 0) else None  # [x_L > 0] as bits
                 check(lib.lg_gcn_bwd_nm_bits(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                              ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
-                                             flags, scale, scale, ptr(ws), st, bits), "lg_gcn_bwd_nm_bits")
+                                             flags, scale, scale, ptr(ws), ws.numel(), st, bits), "lg_gcn_bwd_nm_bits")
             else:
                 check(lib.lg_gcn_bwd(ptr(rowptr_t), ptr(col_t), ptr(w_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                      ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
-                                     col_t.numel(), flags, scale, scale, ptr(ws), st), "lg_gcn_bwd")
+                                     col_t.numel(), flags, scale, scale, ptr(ws), ws.numel(), st), "lg_gcn_bwd")
         dWs[l], dbs[l] = dW, db
         dy = dx  # already masked by the previous op's relu/dropout
     if L == 0:  # no layer-0 launch applied the node init's relu/dropout mask
@@ -495,7 +502,7 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
     with _timed("linear_dw", dev):
         check(lib.lg_sensor_proj_bwd(ptr(dy), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
                                      ptr(h_s), ptr(proj_weight), ptr(dbias_ns), ptr(dh_s), ptr(dWp), ptr(dbp), B, N,
-                                     S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), st),
+                                     S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), wsp.numel(), st),
               "lg_sensor_proj_bwd")
     return dh_s, dWp, dbp
 
@@ -642,7 +649,7 @@ def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, en
     dpooled = torch.empty(B, D, device=dev)
     with _timed("pool_head_bwd", dev):
         check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
-                                   ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn),
+                                   ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn), wsn.numel(),
                                    st), "lg_pool_head_bwd")
     lay = fe & nat.LG_F_NODE_MAJOR
     if _FUSED_SCATTER:
@@ -650,12 +657,12 @@ def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, en
             check(lib.lg_edge_head_bwd_scatter(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1,
                                                ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(inc_rowptr),
                                                ptr(inc_item), ptr(dpooled), ptr(dh), B, N, P, D, hidden, fe, p_edge,
-                                               ptr(ws), st), "lg_edge_head_bwd_scatter")
+                                               ptr(ws), ws.numel(), st), "lg_edge_head_bwd_scatter")
         return
     with _timed("edge_bwd", dev):
         check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
                                    ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), B, N, P, D, hidden, fe, p_edge,
-                                   ptr(ws), st), "lg_edge_head_bwd")
+                                   ptr(ws), ws.numel(), st), "lg_edge_head_bwd")
     with _timed("pipe_scatter", dev):
         check(lib.lg_pipe_scatter_bwd(ptr(inc_rowptr), ptr(inc_item), ptr(dpipe), ptr(dpooled), ptr(dh), B, N, P, D,
                                       lay, st), "lg_pipe_scatter_bwd")

@@ -55,8 +55,8 @@ def use_node_major(B: int, N: int, D: int, bf16: bool = False) -> bool:
     return TRUNK_NODE_MAJOR and B >= 16 and fits
 
 
-# lg_gcn_fwd_nm schedule / transform bits (LG_F_F32_MFMA, LG_F_LAB_*; include/leakgnn.h) for A/B
-# timing of the trunk; the schedule bits never change results.
+# lg_gcn_fwd_nm kernel / transform bits (LG_F_NM3, LG_F_BF16X3, LG_F_F32_MFMA; include/leakgnn.h) for
+# A/B timing of the trunk forward inside the training step (bench.py --trunk-fwd-flags).
 GCN_FWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_NM_FLAGS", "0"), 0)
 
 
@@ -188,7 +188,7 @@ class GCNGraph:
         ws = torch.empty(int(lib.lg_graph_workspace_bytes(E, N)), device=device, dtype=torch.uint8)
         fill = 2.0 if improved else 1.0
         check(lib.lg_graph_build(ptr(ei), E, N, int(add_self_loops), int(normalize), fill, ptr(g.rowptr),
-                                 ptr(g.col), ptr(g.w), ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(ws),
+                                 ptr(g.col), ptr(g.w), ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(ws), ws.numel(),
                                  stream_of(ei)), "lg_graph_build")
         g._keepalive = (ei, ws)  # freed after the stream consumes them
         g.pairs = torch.stack([g.col, g.w.view(torch.int32)], dim=1).contiguous()
@@ -235,7 +235,7 @@ class Incidence:
         inc = Incidence(N, P, ends, torch.empty(N + 1, device=device, dtype=torch.int32),
                         torch.empty(max(2 * P, 1), device=device, dtype=torch.int32))
         ws = torch.empty(int(lib.lg_incidence_workspace_bytes(P, N)), device=device, dtype=torch.uint8)
-        check(lib.lg_incidence_build(ptr(ends), P, N, ptr(inc.rowptr), ptr(inc.item), ptr(ws), stream_of(ends)),
+        check(lib.lg_incidence_build(ptr(ends), P, N, ptr(inc.rowptr), ptr(inc.item), ptr(ws), ws.numel(), stream_of(ends)),
               "lg_incidence_build")
         inc._keepalive = ws
         return inc

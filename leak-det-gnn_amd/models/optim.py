@@ -86,6 +86,6 @@ class ClipAdamW(torch.optim.Optimizer):
                                     group["step_t"].data_ptr(),
                                     float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                                     float(group["weight_decay"]), float(mn) if mn is not None else 0.0,
-                                    self.last_grad_norm.data_ptr(), ws.data_ptr(), stream_of(params[0])),
+                                    self.last_grad_norm.data_ptr(), ws.data_ptr(), ws.numel(), stream_of(params[0])),
                   "lg_clip_adamw")
         return loss

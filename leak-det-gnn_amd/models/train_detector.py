@@ -333,9 +333,11 @@ def main(argv=None) -> None:
             noisy_seg = batch["noisy_seg"].to(device)
             time_seg = batch["time_seg"].to(device)
             label = torch.as_tensor(batch["label"], device=device, dtype=torch.long)
-            if noisy_seg.size(0) == 0:  # a ragged last global batch left this rank no windows
-                # (mean CE over no rows is NaN): contribute zero gradients to the all-reduce and
-                # take the same optimizer step as the other ranks
+            n_local = noisy_seg.size(0)
+            if n_local == 0:  # a ragged last global batch left this rank no windows
+                # (mean CE over no rows is NaN): contribute zero gradients to the all-reduce, take
+                # the same optimizer step as the other ranks, and fall through to the shared
+                # bookkeeping below (its logging all-reduces are collectives every rank makes)
                 opt.zero_grad(set_to_none=True)
                 for p in detector.parameters():
                     p.grad = torch.zeros_like(p)
@@ -343,38 +345,38 @@ def main(argv=None) -> None:
                 if clip is not None and not fused_step:
                     torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
                 opt.step()
-                continue
-            with torch.no_grad():
-                residual = build_residual_sequence_from_segment(predictor, noisy_seg, time_seg, l_pred=args.l_pred,
-                                                                l_det=args.l_det, device=device)
-            tfeat = time_seg[:, args.l_pred:, :]
-            n_local = noisy_seg.size(0)
-            n_glob = min(args.batch_size, len(train_ds) - (it - 1) * args.batch_size)
-            # decided on the GLOBAL batch, so every rank takes the same branch (same collectives)
-            if use_graph and n_glob == args.batch_size and n_local == per_rank_full:
-                # full-size batch: the whole step (fwd, CE, bwd, all-reduce, clip + AdamW) as graph
-                # replays on static inputs; the same arithmetic as the eager branch below
-                if cstep is None:
-                    from .graph_step import CapturedTrainStep
-                    cstep = CapturedTrainStep(detector, loss_fn, opt, (residual.clone(), tfeat.contiguous().clone()),
-                                              label.clone(), clip=None, warmup=2, preserve_state=True)
-                else:
-                    cstep.inputs[0].copy_(residual)
-                    cstep.inputs[1].copy_(tfeat)
-                    cstep.label.copy_(label)
-                loss = cstep()
+                loss = torch.zeros((), device=device)
             else:
-                logits = detector(residual, tfeat)
-                loss = loss_fn(logits, label)
-                opt.zero_grad(set_to_none=True)
-                if world > 1:  # mean over the GLOBAL batch after the all-reduce's average over ranks
-                    (loss * (n_local * world / n_glob)).backward()
-                    allreduce()
+                with torch.no_grad():
+                    residual = build_residual_sequence_from_segment(predictor, noisy_seg, time_seg, l_pred=args.l_pred,
+                                                                    l_det=args.l_det, device=device)
+                tfeat = time_seg[:, args.l_pred:, :]
+                n_glob = min(args.batch_size, len(train_ds) - (it - 1) * args.batch_size)
+                # decided on the GLOBAL batch, so every rank takes the same branch (same collectives)
+                if use_graph and n_glob == args.batch_size and n_local == per_rank_full:
+                    # full-size batch: the whole step (fwd, CE, bwd, all-reduce, clip + AdamW) as graph
+                    # replays on static inputs; the same arithmetic as the eager branch below
+                    if cstep is None:
+                        from .graph_step import CapturedTrainStep
+                        cstep = CapturedTrainStep(detector, loss_fn, opt, (residual.clone(), tfeat.contiguous().clone()),
+                                                  label.clone(), clip=None, warmup=2, preserve_state=True)
+                    else:
+                        cstep.inputs[0].copy_(residual)
+                        cstep.inputs[1].copy_(tfeat)
+                        cstep.label.copy_(label)
+                    loss = cstep()
                 else:
-                    loss.backward()
-                if clip is not None and not fused_step:
-                    torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
-                opt.step()
+                    logits = detector(residual, tfeat)
+                    loss = loss_fn(logits, label)
+                    opt.zero_grad(set_to_none=True)
+                    if world > 1:  # mean over the GLOBAL batch after the all-reduce's average over ranks
+                        (loss * (n_local * world / n_glob)).backward()
+                        allreduce()
+                    else:
+                        loss.backward()
+                    if clip is not None and not fused_step:
+                        torch.nn.utils.clip_grad_norm_(detector.parameters(), clip)
+                    opt.step()
             running += loss.detach().double() * n_local
             seen += n_local
             perf.add(n_local)

@@ -111,13 +111,13 @@ def test_c5_node_major_trunk_kernels(c5_graph, drop):
             ops.check(lib.lg_gcn_bwd_nm(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t),
                                         ops.ptr(dy.transpose(0, 1).contiguous()), ops.ptr(yn), ops.ptr(xn), ops.ptr(W),
                                         ops.ptr(dx), ops.ptr(dW), ops.ptr(db), None, None, B, N, D, bflags, sc, sc,
-                                        ops.ptr(ws), st), "bwd_nm")
+                                        ops.ptr(ws), ws.numel(), st), "bwd_nm")
             dx = dx.transpose(0, 1)
         else:
             ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
             ops.check(lib.lg_gcn_bwd(ops.ptr(graph.rowptr_t), ops.ptr(graph.col_t), ops.ptr(graph.w_t), ops.ptr(dy),
                                      ops.ptr(y), ops.ptr(x), ops.ptr(W), ops.ptr(dx), ops.ptr(dW), ops.ptr(db), None,
-                                     None, B, N, D, graph.nnz_cap, bflags, sc, sc, ops.ptr(ws), st), "bwd")
+                                     None, B, N, D, graph.nnz_cap, bflags, sc, sc, ops.ptr(ws), ws.numel(), st), "bwd")
         outs[nm] = (dx, dW, db)
     for i, what in enumerate(("dx", "dW", "db")):
         assert_close(outs[True][i], outs[False][i], what=f"C5 node-major bwd {what}")
@@ -187,7 +187,7 @@ def test_c5_node_major_trunk_vs_fp64_oracle(c5_graph, drop):
     ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
     ops.check(lib.lg_gcn_bwd_nm_bits(ops.ptr(graph.nodetab_t), ops.ptr(graph.pairs_t), ops.ptr(dyn), None,
                                      ops.ptr(xn), ops.ptr(Wd), ops.ptr(dx), ops.ptr(dW), ops.ptr(db), None, None, B,
-                                     N, D, nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, sc, sc, ops.ptr(ws), st,
+                                     N, D, nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, sc, sc, ops.ptr(ws), ws.numel(), st,
                                      ops.ptr(ybits)), "bwd_nm_bits")
     assert_close(dx, dx64, what="C5 node-major dx vs fp64 oracle")
     assert_close(dW, dW64, what="C5 node-major dW vs fp64 oracle")

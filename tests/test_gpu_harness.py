@@ -139,11 +139,14 @@ def _dp_trainer_worker(rank, world, port, argv):
     train_detector.main(argv)
 
 
-def test_train_detector_data_parallel_equals_single_process(data, tmp_path):
+@pytest.mark.parametrize("steps,log_every", [(24, 10), (25, 1)])
+def test_train_detector_data_parallel_equals_single_process(data, tmp_path, steps, log_every):
     """train_detector under a 2-rank launch (torchrun environment, gloo, both ranks on this
     GPU): each rank trains on its half of every global batch of --batch_size samples and the
     gradients are all-reduced; rank 0's checkpoint equals a single-process run's on the same
-    global batches (dropout off on both sides)."""
+    global batches (dropout off on both sides).  steps 25: the last global batch is ONE window,
+    so rank 1 gets none and must still join every collective (the step's all-reduce and, at
+    --log_every 1, the logging all-reduces)."""
     import socket
     import torch.multiprocessing as mp
     from models import train_detector, train_predictor
@@ -158,9 +161,9 @@ def test_train_detector_data_parallel_equals_single_process(data, tmp_path):
 
     def argv(o):
         return ["--leak_root", str(tmp_path / "leak"), "--inp_path", str(LTA_INP), "--predictor_ckpt",
-                str(out / "predictor_best.ckpt"), "--out_dir", str(o), "--epochs", "1", "--steps_per_epoch", "24",
+                str(out / "predictor_best.ckpt"), "--out_dir", str(o), "--epochs", "1", "--steps_per_epoch", str(steps),
                 "--val_steps", "8", "--test_steps", "8", "--batch_size", "8", "--device", "cuda",
-                "--dist_backend", "gloo"]
+                "--dist_backend", "gloo", "--log_every", str(log_every)]
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]

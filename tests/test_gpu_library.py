@@ -69,11 +69,11 @@ def test_rows_kernels_match_window_major(N, E, seed):
         if rows:
             ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
             check(lib.lg_gcn_bwd_rows(ptr(g.nodetab_t), ptr(g.pairs_t), ptr(dy), ptr(x), ptr(W), ptr(dx), ptr(dW),
-                                      ptr(db), N, D, ptr(ws), st), "bwd rows")
+                                      ptr(db), N, D, ptr(ws), ws.numel(), st), "bwd rows")
         else:
             ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=DEV, dtype=torch.uint8)
             check(lib.lg_gcn_bwd(ptr(g.rowptr_t), ptr(g.col_t), ptr(g.w_t), ptr(dy), None, ptr(x), ptr(W), ptr(dx),
-                                 ptr(dW), ptr(db), None, None, 1, N, D, g.col_t.numel(), 0, 1.0, 1.0, ptr(ws), st),
+                                 ptr(dW), ptr(db), None, None, 1, N, D, g.col_t.numel(), 0, 1.0, 1.0, ptr(ws), ws.numel(), st),
                   "bwd")
         outs.append((dx, dW, db))
     for i, what in enumerate(("dx", "dW", "db")):

@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 20
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 21
     assert lib.lg_timing_arm(-1) == -1 and lib.lg_timing_disarm() == 0 and lib.lg_timing_elapsed(0, None) == -1
     assert lib.lg_nm_table_build(None, None, 661, None, None, None) == -1
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
@@ -116,29 +116,70 @@ def test_c_abi_host_only_calls():
     assert lib.lg_gcn_fwd(None, None, None, None, None, None, None, 1, 661, 64, 2193, 0, 0.0, 0, 0, None) == -1
     assert lib.lg_gcn_bwd(None, None, None, None, None, None, None, None, None, None, None, None, 1, 661, 64, 2193, 0,
                           1.0, 1.0,
-                          None, None) == -1
+                          None, 0, None) == -1
     assert lib.lg_gcn_bwd_nm_workspace_bytes(48) == -2
     assert lib.lg_gcn_fwd_nm(None, None, None, None, None, None, 16, 661, 64, 2193, 0, 0.0, 0, 0, None) == -1
     assert lib.lg_gcn_bwd_nm(None, None, None, None, None, None, None, None, None, None, None, 16, 661, 64, 0, 1.0,
-                             1.0, None, None) == -1
-    assert lib.lg_graph_build(None, 5, 0, 1, 1, 1.0, None, None, None, None, None, None, None, None) == -1
+                             1.0, None, 0, None) == -1
+    assert lib.lg_graph_build(None, 5, 0, 1, 1, 1.0, None, None, None, None, None, None, None, 0, None) == -1
     assert lib.lg_pipe_gather_fwd(None, None, None, 1, 10, 5, 64, None) == -1
     assert lib.lg_mean_pool_fwd(None, None, 2, 10, 64, None) == -1
     assert lib.lg_pool_head_bwd_workspace_bytes(256, 64, 64) == -2   # hidden must be 128
     assert lib.lg_linear_dw_workspace_bytes(7424, 64, 48) == -2
-    assert lib.lg_linear_dw(None, None, 7424, 64, 64, None, None, None, None) == -1
+    assert lib.lg_linear_dw(None, None, 7424, 64, 64, None, None, None, 0, None) == -1
     assert lib.lg_pool_head_fwd(None, None, None, None, None, None, None, None, 765, 764, 2, 661, 64, 128, 0, 0.0, 0,
                                 102, None) == -1
     assert lib.lg_edge_head_fwd(None, None, None, None, None, None, None, 764, None, 2, 661, 764, 64, 128, 0, 0.0, 0,
                                 101, None) == -1
     assert lib.lg_edge_head_bwd(None, None, None, None, None, None, 764, None, None, None, None, None, 2, 661, 764, 64,
-                                128, 0, 0.0, None, None) == -1
+                                128, 0, 0.0, None, 0, None) == -1
     # GRU: H in {32, 64}; the backward needs the saved gates; gates need h_seq
     assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 48) == -1
     assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 32) > 0
     assert lib.lg_gru_fwd(None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 48, None) == -2
     assert lib.lg_gru_bwd(None, None, None, None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 64,
-                          None, None) == -1
+                          None, 0, None) == -1
+
+
+def test_undersized_workspace_returns_einval():
+    """Every workspace-taking entry point checks the caller's ws_bytes against the slab its own
+    launch grid writes and returns LG_EINVAL (-1) before launching anything when it is short
+    (ABI 21; round 3's trainer hang was a silent overrun of a grid-sized slab).  No GPU is
+    needed: the checks run on the host before any HIP call, with stand-in device pointers."""
+    from models import _native
+    lib = _native.load_library()
+    F = 16  # a non-NULL stand-in device pointer (never dereferenced on these paths)
+    B, N, D, P, S = 256, 661, 64, 764, 29
+    need = lib.lg_gcn_bwd_nm_workspace_bytes(D)
+    assert need > 0
+    args = (F, F, F, F, F, F, F, F, F, None, None, B, N, D, 0x10, 1.0, 1.0, F)
+    assert lib.lg_gcn_bwd_nm_bits(*args, need - 1, None, None) == -1
+    assert lib.lg_gcn_bwd_nm(*args, 0, None) == -1
+    assert lib.lg_gcn_bwd_rows(F, F, F, F, F, F, F, F, 100_000, 64, F, need - 1, None) == -1
+    assert lib.lg_gcn_bwd(F, F, F, F, None, F, F, F, F, F, None, None, B, N, D, 2193, 0, 1.0, 1.0, F,
+                          lib.lg_gcn_bwd_workspace_bytes(D) - 1, None) == -1
+    wse = lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)
+    assert wse > 0
+    eargs = (F, F, F, F, F, F, P, F, F, F, F, F)
+    assert lib.lg_edge_head_bwd(*eargs, B, N, P, D, 128, 0, 0.0, F, wse - 1, None) == -1
+    assert lib.lg_edge_head_bwd_scatter(*eargs, F, F, None, F, B, N, P, D, 128, 0x20, 0.0, F, wse - 1, None) == -1
+    wsp = lib.lg_pool_head_bwd_workspace_bytes(B, D, 128)
+    assert lib.lg_pool_head_bwd(F, F, F, F, F, P + 1, P, F, F, F, F, F, B, D, 128, 0, 0.0, F, wsp - 1, None) == -1
+    wsg = lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)
+    assert lib.lg_gru_bwd(F, F, F, F, F, F, F, None, F, F, F, F, B, 36, S, 10, 64, F, wsg // 2 - 1, None) == -1
+    wss = lib.lg_sensor_proj_bwd_workspace_bytes(B, S, D, D)
+    assert lib.lg_sensor_proj_bwd(F, F, F, F, F, None, F, F, F, B, N, S, D, D, 0x20, F, wss - 1, None) == -1
+    wsl = lib.lg_linear_dw_workspace_bytes(B * S, D, D)
+    assert lib.lg_linear_dw(F, F, B * S, D, D, F, F, F, wsl - 1, None) == -1
+    assert lib.lg_graph_build(F, 1532, N, 1, 1, 1.0, F, F, F, F, F, F, F,
+                              lib.lg_graph_workspace_bytes(1532, N) - 1, None) == -1
+    assert lib.lg_incidence_build(F, P, N, F, F, F, lib.lg_incidence_workspace_bytes(P, N) - 1, None) == -1
+    sizes = (ctypes.c_int64 * 1)(1000)
+    table = (ctypes.c_int64 * 4)(F, F, F, F)
+    wsa = lib.lg_clip_adamw_workspace_bytes(ctypes.addressof(sizes), 1)
+    assert wsa == 16  # two 512-element slices, one fp64 partial each
+    assert lib.lg_clip_adamw(ctypes.addressof(table), ctypes.addressof(sizes), 1, F, 1e-3, 0.9, 0.999, 1e-8, 0.0,
+                             1.0, None, F, wsa - 1, None) == -1
 
 
 def test_library_built_for_gfx950_only():
@@ -188,3 +229,14 @@ def test_rcm_schedule_order():
     bad = torch.tensor([[0], [7]], dtype=torch.long)
     out = torch.empty(6, dtype=torch.int32)
     assert lib.lg_rcm_order(bad.data_ptr(), 1, 6, out.data_ptr()) == -1
+
+
+def test_gcn_conv_row_tiles_only_within_one_launch():
+    """GCNConv at D = 64 takes the row-tile kernels only while N * D * 4 fits one launch's 32-bit
+    buffer offsets; past it (and at D = 32) it falls back to lg_gcn_fwd / lg_gcn_bwd."""
+    from models import library, ops
+    limit = ops.NM_MAX_BYTES // (64 * 4)
+    assert library._use_rows(100_000, 64)
+    assert library._use_rows(limit, 64)
+    assert not library._use_rows(limit + 1, 64)
+    assert not library._use_rows(100_000, 32)

@@ -100,6 +100,57 @@ def stamps_summary(lib, launch):
             "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
 
 
+def pc_stamps_summary(lib, launch, waves_per_wg=12, prod=4):
+    """Per-wave timeline of one eager k_gcn_fwd_pc launch (LG_NM3_STAMPS build): producers and
+    consumers separately — start / end, tiles handed over / stored, the per-tile interval, and
+    the tail (last end minus the median end), the end by tile count and by XCC."""
+    import ctypes
+    lib.lg_lab_nm3_stamps_clear.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    torch.cuda.synchronize()
+    check(lib.lg_lab_nm3_stamps_clear(), "stamps clear")
+    torch.cuda.synchronize()
+    launch()
+    torch.cuda.synchronize()
+    n = 8192 * 24
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib.lg_lab_nm3_stamps(buf.ctypes.data, n), "stamps read")
+    st = buf.reshape(8192, 24).astype(np.int64)
+    rows = np.nonzero(st[:, 0] != 0)[0]
+    st = st[rows]
+    role = np.where((rows % waves_per_wg) < prod, "prod", "cons")
+    rt0, rt1, c0, c1 = st[:, 0], st[:, 22], st[:, 1], st[:, 21]
+    ghz = float(np.median((c1 - c0) / np.maximum(rt1 - rt0, 1))) * 0.1
+    us = lambda cyc: cyc / (ghz * 1e3)
+    t0 = rt0.min()
+    start = (rt0 - t0) / 100.0
+    end = (rt1 - t0) / 100.0
+    q = lambda a: [round(float(np.percentile(a, p)), 3) for p in (10, 50, 90, 99, 100)] if len(a) else []
+    xcc = (st[:, 23] >> 32) & 0xF
+    out = {"waves": int(len(st)), "clock_GHz": round(ghz, 3), "span_us": round(float(end.max()), 3)}
+    for r in ("prod", "cons"):
+        m = role == r
+        sr = st[m]
+        tiles = (sr[:, 3:19] != 0).sum(1)
+        gaps = []
+        for row, nt in zip(sr, tiles):
+            prev = row[2]
+            for t in range(min(nt, 16)):
+                gaps.append(us(row[3 + t] - prev))
+                prev = row[3 + t]
+        e = end[m]
+        out[r] = {"start_us_p10_50_90_99_max": q(start[m]), "end_us_p10_50_90_99_max": q(e),
+                  "tail_us": round(float(e.max() - np.median(e)), 3),
+                  "staging_us_p50": round(float(np.median(us(sr[:, 2] - sr[:, 1]))), 3),
+                  "tiles_hist": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
+                  "tile_us_p10_50_90_99_max": q(gaps),
+                  "end_by_tiles_p50": {int(k): round(float(np.median(e[tiles == k])), 3) for k in np.unique(tiles)},
+                  "end_by_xcc_max": [round(float(e[xcc[m] == i].max()), 3) if (xcc[m] == i).any() else None
+                                     for i in range(8)]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,gcn_fwd_nm,gcn_fwd_nm_train,gcn_bwd_nm,spmm,"
@@ -169,16 +220,9 @@ def main():
     ymask = torch.empty(N * ((B + 15) // 16) * 64, device=dev, dtype=torch.int16)
     for lab in [v for v in args.nmlab.split(",") if v]:
         bits, with_mask = 0, False
-        for tok in lab.split("+"):  # v1 | bpc<n> | nomfma | noload (the last two: LEAKGNN_LIB=lib/lab build only)
-            bits |= {"v1": nat.LG_F_LAB_V1, "nm2": nat.LG_F_LAB_NM2, "w8": nat.LG_F_LAB_W8, "w5": nat.LG_F_LAB_W5, "nomfma": 1 << 28,
-                     "noload": 2 << 28, "nostore": 4 << 28, "dst": 0x00080000, "f32": nat.LG_F_F32_MFMA,
-                     "bf16": nat.LG_F_BF16, "nm5": nat.LG_F_NM5, "pc": nat.LG_F_PC, "f16": nat.LG_F_F16X2,
-                     "pc1": nat.LG_F_PC | nat.LG_F_PC1, "pc6": nat.LG_F_PC | nat.LG_F_PC6,
-                     "nm3": nat.LG_F_NM3}.get(tok, 0)
-            if tok.startswith("bpc"):
-                bits |= int(tok[3:]) << 24
-            if tok.startswith("opt"):  # lab OPT variant of the D = 64 forward (LG_F_LAB_OPT, bits 8..11)
-                bits |= 0x00001000 | (int(tok[3:]) << 8)
+        for tok in lab.split("+"):  # dflt | x3 | nm3 | f32 | bf16 | pc | mask
+            bits |= {"f32": nat.LG_F_F32_MFMA, "bf16": nat.LG_F_BF16, "pc": nat.LG_F_PC, "x3": nat.LG_F_BF16X3,
+                     "nm3": nat.LG_F_NM3, "dflt": 0}.get(tok, 0)
             with_mask |= tok == "mask"  # the last layer's form: [y > 0] bits written beside y
         for mode, fl in (("eval", 0), ("train", nat.LG_F_DROPOUT)):
             f = lambda fl=fl, bits=bits, wm=with_mask: check(lib.lg_gcn_fwd_nm_bits(
@@ -187,20 +231,15 @@ def main():
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
             if args.stamps and mode == "train" and hasattr(lib, "lg_lab_nm3_stamps"):
-                res[f"stamps_{lab}"] = stamps_summary(lib, f)
+                pcs = not (bits & (nat.LG_F_NM3 | nat.LG_F_F32_MFMA)) and not (bits & nat.LG_F_BF16 and not bits & nat.LG_F_PC)
+                res[f"stamps_{lab}"] = pc_stamps_summary(lib, f) if pcs else stamps_summary(lib, f)
     # gcn_bwd_nm: the training step's layer-2 backward (output mask as the forward's ymask
     # bits); gcn_bwd_nm_y: the same with the mask gathered from y
     for name, fl, nbias in (("gcn_bwd_nm", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
                             ("gcn_bwd_nm_y", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, False),
-                            ("gcn_bwd_nm_old", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, False),
-                            ("gcn_bwd_nm_nm3f16", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_F16X2, False),
-                            ("gcn_bwd_nm_pc", nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC,
-                             False),
                             ("gcn_bwd_nm_l0", nat.LG_F_MASK_OUT, True),
                             ("gcn_bwd_nm_l0s", nat.LG_F_MASK_OUT | nat.LG_F_DX_SENSOR_ROWS, True),
-                            ("gcn_bwd_nm_l0_nm3f16", nat.LG_F_MASK_OUT | nat.LG_F_F16X2, True),
-                            ("gcn_bwd_nm_l0_pc", nat.LG_F_MASK_OUT | nat.LG_F_F16X2 | nat.LG_F_PC, True),
-                            ("gcn_bwd_nm_l0_old", nat.LG_F_MASK_OUT | nat.LG_F_LAB_NM2, True)):
+                            ):
         if name not in which:
             continue
         dy = torch.randn_like(x)
@@ -213,7 +252,7 @@ def main():
         dnb = torch.empty(D, device=dev)
         ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
         bits = None
-        if name in ("gcn_bwd_nm", "gcn_bwd_nm_nm3f16", "gcn_bwd_nm_pc"):  # the mask bits of yy = dropout(relu(layer(x))) from the forward
+        if name == "gcn_bwd_nm":  # the mask bits of yy = dropout(relu(layer(x))) from the forward
             bits = torch.empty(N * ((B + 15) // 16) * 64, device=dev, dtype=torch.int16)
             check(lib.lg_gcn_fwd_nm_bits(ptr(graph.nodetab), ptr(graph.pairs), ptr(x), ptr(W), ptr(bias), ptr(yy), B,
                                          N, D, E1, nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT, 0.1, 123, 2,
@@ -221,7 +260,7 @@ def main():
         f = lambda fl=fl, nbias=nbias, dy=dy, yy=yy, dx=dx, dW=dW, db=db, slot=slot, dnb=dnb, ws=ws, bits=bits: check(
             lib.lg_gcn_bwd_nm_bits(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(dy), ptr(yy), ptr(x), ptr(W),
                                    ptr(dx), ptr(dW), ptr(db), ptr(slot) if nbias else None,
-                                   ptr(dnb) if nbias else None, B, N, D, fl, 1.0, 1.0, ptr(ws), cs(),
+                                   ptr(dnb) if nbias else None, B, N, D, fl, 1.0, 1.0, ptr(ws), ws.numel(), cs(),
                                    ptr(bits) if bits is not None else None), name)
         t = timeit(f, args.iters)
         if bits is not None:
@@ -279,12 +318,12 @@ def main():
             ws5 = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
             wsr = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
             f = lambda: check(lib.lg_gcn_bwd_rows(ptr(g5.nodetab_t), ptr(g5.pairs_t), ptr(dy5), ptr(x5), ptr(W),
-                                                  ptr(dx5), ptr(dW5), ptr(db5), N5, D, ptr(wsr), cs()), "c5 bwd")
+                                                  ptr(dx5), ptr(dW5), ptr(db5), N5, D, ptr(wsr), wsr.numel(), cs()), "c5 bwd")
             t = timeit(f, args.iters)
             res["c5_bwd"] = {"us": t, "GBps": (b5 + 4 * N5 * D) / t / 1e3}
             fwm = lambda: check(lib.lg_gcn_bwd(ptr(g5.rowptr_t), ptr(g5.col_t), ptr(g5.w_t), ptr(dy5), None, ptr(x5),
                                                ptr(W), ptr(dx5), ptr(dW5), ptr(db5), None, None, 1, N5, D,
-                                               g5.col_t.numel(), 0, 1.0, 1.0, ptr(ws5), cs()), "c5 bwd wm")
+                                               g5.col_t.numel(), 0, 1.0, 1.0, ptr(ws5), ws5.numel(), cs()), "c5 bwd wm")
             t = timeit(fwm, args.iters)
             res["c5_bwd_wm"] = {"us": t, "GBps": (b5 + 4 * N5 * D) / t / 1e3}
     if "copy" in which:  # torch device copy of the same bytes: x (B*N*D fp32) -> y
@@ -305,7 +344,7 @@ def main():
         ws = torch.empty(int(lib.lg_gcn_bwd_workspace_bytes(D)), device=dev, dtype=torch.uint8)
         f = lambda: check(lib.lg_gcn_bwd(ptr(graph.rowptr_t), ptr(graph.col_t), ptr(graph.w_t), ptr(dy), ptr(yy),
                                          ptr(x), ptr(W), ptr(dx), ptr(dW), ptr(db), None, None, B, N, D, E1,
-                                         nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), cs()), "bwd")
+                                         nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), ws.numel(), cs()), "bwd")
         t = timeit(f, args.iters)
         res["gcn_bwd"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
     if "edge_fwd" in which or "edge_bwd" in which:
@@ -336,7 +375,7 @@ def main():
             ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=dev, dtype=torch.uint8)
             f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(W2), ptr(hid), ptr(dl), P,
                                                    ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
-                                                   nat.LG_F_DROPOUT, 0.1, ptr(ws), cs()), "edge bwd")
+                                                   nat.LG_F_DROPOUT, 0.1, ptr(ws), ws.numel(), cs()), "edge bwd")
             t = timeit(f, args.iters)
             res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
     if "gru_fwd" in which or "gru_bwd" in which:
@@ -366,7 +405,7 @@ def main():
             ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)), device=dev, dtype=torch.uint8)
             f = lambda: check(lib.lg_gru_bwd(ptr(r), ptr(tf), ptr(wih), ptr(whh), ptr(hs), ptr(gt), ptr(dh), None,
                                              ptr(dws[0]), ptr(dws[1]), ptr(dws[2]), ptr(dws[3]), B, L, S, 10, 64,
-                                             ptr(ws), cs()), "gru bwd")
+                                             ptr(ws), ws.numel(), cs()), "gru bwd")
             t = timeit(f, args.iters)
             res["gru_bwd"] = {"us": t, "TFLOPs": 2 * flops / t / 1e6}
     if "tcn" in which:
