@@ -698,8 +698,8 @@ def main() -> None:
         # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay)
         from models.graph_step import CapturedTrainStep
         step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=None, warmup=3)
-    timer = ops.KernelTimer(["gcn_fwd", "gcn_bwd", "gcn_bwd_l0", "node_init", "gru_fwd", "gru_bwd", "edge_fwd",
-                             "edge_bwd", "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
+    timer = ops.KernelTimer(["gcn_fwd", "gcn_fwd_l0", "gcn_bwd", "gcn_bwd_l0", "node_init", "gru_fwd", "gru_bwd",
+                             "edge_fwd", "edge_bwd", "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)
 
     def barrier():
@@ -786,8 +786,9 @@ def main() -> None:
                    "step": "fwd+CE+bwd+allreduce+clip+AdamW, train mode (clip_grad_norm_ + AdamW in one launch, "
                            "models/optim.py)",
                    "launch": "eager" if args.eager else "hipgraph (one replay per step, dropout re-drawn on device)"},
-        "roofline": {"kernel": "lg_gcn_fwd_nm_bits -> k_gcn_fwd_pc (fused gather-aggregate by producer waves, "
-                               "fp16x2 MFMA transform + bias/ReLU/dropout by consumer waves, train mode)", "bound": "hbm",
+        "roofline": {"kernel": "lg_gcn_fwd_nm_bits -> k_gcn_fwd_pc, layer 1 (fused gather-aggregate by producer "
+                               "waves, fp16x2 MFMA transform + bias/ReLU/dropout by consumer waves, train mode; layer 0 "
+                               "reads the compressed node init: kernels_us.gcn_fwd_l0)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(traffic["bytes"]) if traffic else None,

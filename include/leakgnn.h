@@ -214,6 +214,17 @@ int lg_graph_build(const int64_t* edge_index, int64_t E, int64_t N,
 int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, int64_t N, const int32_t* order,
                       int32_t* nodetab, lg_stream_t stream);
 
+/* Sensor marks for the compressed layer-0 input (ABI 21; lg_node_init_bits_fwd /
+ * lg_gcn_fwd_nm_x0 / lg_gcn_bwd_nm_x0).  Copies a node table (lg_nm_table_build) and its pair
+ * array with every CSR entry whose col n has a sensor slot (node_slot[n] >= 0) rewritten to
+ * col = 0x40000000 | node_slot[n], so a tile learns from its record alone which neighbours
+ * are stored as sensor rows; pos_slot[i] = node_slot of the schedule section's record N + i.
+ *   node_slot : int32 [N] (-1 = no sensor);  nodetab_out : int32 [2N][16];
+ *   pairs_out : int32 [2 * nnz];  pos_slot : int32 [N]. */
+int lg_nm_table_sensor_mark(const int32_t* nodetab, const int32_t* pairs, int64_t N, int64_t nnz,
+                            const int32_t* node_slot, int32_t* nodetab_out, int32_t* pairs_out, int32_t* pos_slot,
+                            lg_stream_t stream);
+
 /* Reverse Cuthill-McKee order of the undirected graph edge_index (HOST memory, int64
  * [2][E], self loops and duplicates ignored): order[i] = the node visited i-th.  Each
  * connected component is a breadth-first sweep from a minimum-degree node, neighbours
@@ -355,6 +366,38 @@ int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const f
                        const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
                        int flags, float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream,
                        const uint16_t* ymask);
+
+/* Compressed layer-0 input (ABI 21).  The node init's non-sensor rows are dropout(relu(b)):
+ * 632 of L-TOWN-A's 661 rows carry no information beyond their keep bits, yet materialising
+ * x0 costs a 43 MB write and layer 0's forward and backward read it back (86 MB).
+ * lg_node_init_bits_fwd replaces lg_node_init_proj_fwd (LG_F_NODE_MAJOR layout) with
+ *   xs0    : fp32 [S][B][D], x0's rows of the live sensor slots (node_slot[n] = s), bit-identical
+ *            to lg_node_init_proj_fwd's rows;
+ *   x0bits : uint16 [N * ceil(B/16) * 64], [x0 > 0] of EVERY row in the mask layout of
+ *            lg_gcn_fwd_nm_bits (ABI 15),
+ * from which a non-sensor element is x0 = bit ? relu(bias) * scale : 0 exactly.
+ * lg_gcn_fwd_nm_x0 is lg_gcn_fwd_nm_bits of layer 0 reading (xs0, x0bits, node_bias) through a
+ * sensor-marked node table (lg_nm_table_sensor_mark): the same sums in the same order, so y is
+ * bit-identical to the dense forward.  lg_gcn_bwd_nm_x0 is lg_gcn_bwd_nm_bits of layer 0 (no
+ * MASK_IN) with the tile's own x block from (xs0, x0bits); pos_slot_t = the transposed table's
+ * schedule-section slots.  The node init and the layer share one Dropout (detector.py:190,
+ * 201): flags' LG_F_DROPOUT and dropout_p describe both.  lg_node_init_expand materialises x0
+ * (diagnostics, tests). */
+int lg_node_init_bits_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx, const float* h_s, const float* W,
+                          const float* bias, float* xs0, uint16_t* x0bits, int64_t B, int64_t N, int64_t S,
+                          int64_t Ds, int64_t D, int flags, float dropout_p, uint64_t seed, uint32_t salt,
+                          lg_stream_t stream);
+int lg_node_init_expand(const int32_t* sensor_slot, const float* xs0, const uint16_t* x0bits, const float* bias,
+                        float* x0, int64_t B, int64_t N, int64_t D, int flags, float dropout_p, lg_stream_t stream);
+int lg_gcn_fwd_nm_x0(const int32_t* nodetab_s, const int32_t* pairs_s, const float* xs0, const uint16_t* x0bits,
+                     const float* node_bias, const float* W, const float* bias, float* y, int64_t B, int64_t N,
+                     int64_t S, int64_t D, int flags, float dropout_p, uint64_t seed, uint32_t salt,
+                     lg_stream_t stream);
+int lg_gcn_bwd_nm_x0(const int32_t* nodetab_t, const int32_t* pairs_t, const int32_t* pos_slot_t, const float* dy,
+                     const float* xs0, const uint16_t* x0bits, const float* node_bias, const float* W, float* dx_out,
+                     float* dW, float* db, const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N,
+                     int64_t S, int64_t D, int flags, float dropout_p, float scale_out, void* workspace,
+                     int64_t ws_bytes, lg_stream_t stream);
 
 /* Single graph (B = 1) on the node tables (ABI 18): the GCNConv module's own call shape,
  * x [N][D] (BASELINE configs[4], one 100k-node graph).  Replaces: PyG GCNConv.forward

@@ -138,6 +138,7 @@ __device__ __forceinline__ uint32_t lg_div(uint32_t n, const lg_fastdiv& f) {
 }
 
 constexpr int kLgNmInline = 6;  // CSR entries held inline in a node-table record (graph.hip k_nm_table)
+constexpr int32_t kLgSensorCol = 0x40000000;  // sensor-marked node-table col: kLgSensorCol | sensor slot
 
 constexpr int64_t kLgMaxRows = int64_t{1} << 31;  // row-index space of the fast-division kernels
 

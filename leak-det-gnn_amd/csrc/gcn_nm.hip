@@ -527,12 +527,21 @@ __device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
     }
 }
 
-template <int D, bool DROP, bool RELU, bool BF, bool F16, int kPcProd, int NC>
+// X0: layer 0 reading the compressed node init (lg_node_init_bits_fwd): x = the sensor rows
+// [S][B][D], bits = [x0 > 0] of every row, a non-sensor element = bit ? relu(bias) * scale : 0
+struct PcX0 {
+    const uint16_t* bits;
+    const float* bias;
+    float scale;
+    uint32_t S;
+};
+
+template <int D, bool DROP, bool RELU, bool BF, bool F16, int kPcProd, int NC, bool X0 = false>
 __global__ void __launch_bounds__(64 * kPcProd * (1 + NC), kPcProd * (1 + NC) / 4)
 k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ x,
              const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ y, uint32_t N,
              uint32_t B, uint32_t ngroups, lg_fastdiv fdN, float p_drop, float dscale, uint64_t seed,
-             uint32_t salt, uint16_t* __restrict__ ymask) {
+             uint32_t salt, uint16_t* __restrict__ ymask, PcX0 x0) {
     using G = NmGeo<D>;
     using LY = PcLds<D, kPcProd, NC>;
     constexpr int NPF = LG_PC_NPF;
@@ -619,7 +628,18 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     if (producer) {
         // ---------------- producer: gather + accumulate, two tiles in flight
-        const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, bytes), xrs0 = nm_rsrc(x, 0);
+        // X0 (layer 0 on the compressed node init): a neighbour whose record col carries
+        // kLgSensorCol is a sensor row of x (= xs0 [S][B][D]) at its slot; any other
+        // neighbour's block is its [x0 > 0] mask word (one uint16 per lane), x0 = bit ? v0 : 0
+        const __amdgpu_buffer_rsrc_t xrs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : bytes),
+                                     xrs0 = nm_rsrc(x, 0);
+        const __amdgpu_buffer_rsrc_t brs = nm_mask_rsrc(x0.bits, N, ngroups);
+        f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (X0) {
+            const f32x4 bv = ld4(x0.bias + 4 * fg);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v0[i] = fmaxf(bv[i], 0.f) * x0.scale;
+        }
         uint32_t loff[G::K];
 #pragma unroll
         for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
@@ -627,6 +647,36 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         uint32_t lo[2][G::K];
         NmRec rec[2];
         uint32_t tn[2], tb0[2], tnb[2];
+        // one neighbour's block into blk: its rows (a sensor row under X0), or X0's mask word in
+        // blk[0][0]; an absent neighbour (have == false) reads zeros
+        auto load_nb = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K]) {
+            if constexpr (X0) {
+                if (have && !(c & kLgSensorCol)) {
+                    blk[0][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b16(
+                        brs, nm_mask_off(static_cast<uint32_t>(c), b0 >> 4, ngroups, lane), 0, 0));
+                    return;
+                }
+                c &= ~kLgSensorCol;
+            }
+            const uint32_t base = have ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
+            const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+                blk[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lk[k], base, 0));
+        };
+        // slot k of a loaded neighbour block as values
+        auto nbv = [&](int c, const f32x4 (&blk)[G::K], int k) -> f32x4 {
+            if constexpr (X0) {
+                if (!(c & kLgSensorCol)) {
+                    const uint32_t w = __float_as_uint(blk[0][0]) >> (4 * k);
+                    f32x4 r;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) r[i] = (w >> i) & 1u ? v0[i] : 0.f;
+                    return r;
+                }
+            }
+            return blk[k];
+        };
         // r: the tile's node-table record (schedule section: slot -> record with its node id),
         // requested by the caller a phase earlier
         auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
@@ -642,12 +692,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             for (int k = 0; k < G::K; ++k) lo[b][k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
 #pragma unroll
             for (int i = 0; i < NPF; ++i) {
-                const bool have = r.e0 + i < r.e1;
-                const uint32_t base = have ? (static_cast<uint32_t>(r.p[i].x) * B + b0) * (4u * D) : 0u;
-                const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+                if constexpr (X0) {
+                    if (!(r.e0 + i < r.e1)) {  // absent: no load (the first product takes weight 0)
 #pragma unroll
-                for (int k = 0; k < G::K; ++k)
-                    pf[b][i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], base, 0));
+                        for (int k = 0; k < G::K; ++k) pf[b][i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                        continue;
+                    }
+                }
+                load_nb(r.p[i].x, r.e0 + i < r.e1, b0, lo[b], pf[b][i]);
             }
         };
         // tile t of this producer from buffer b: accumulate, hand over, refill b with tile t + 2
@@ -666,47 +718,38 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             f32x4 acc[G::K];
             {
                 const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
+                const int c = e0 < e1 ? cur.p[0].x : kLgSensorCol;
 #pragma unroll
-                for (int k = 0; k < G::K; ++k) acc[k] = pf[b][0][k] * w;
+                for (int k = 0; k < G::K; ++k) acc[k] = nbv(c, pf[b][0], k) * w;
             }
 #pragma unroll
             for (int i = 1; i < NPF; ++i) {
                 if (e0 + i < e1) {
                     const float w = __int_as_float(cur.p[i].y);
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, pf[b][i][k]);
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, nbv(cur.p[i].x, pf[b][i], k));
                 }
             }
             if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
                 constexpr int NI = kLgNmInline - NPF;
                 f32x4 va[NI][G::K];
 #pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    const bool have = e0 + NPF + i < e1;
-                    const uint32_t ba = have ? (static_cast<uint32_t>(cur.p[NPF + i].x) * B + b0) * (4u * D) : 0u;
-                    const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k)
-                        va[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo[b][k], ba, 0));
-                }
+                for (int i = 0; i < NI; ++i) load_nb(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i]);
 #pragma unroll
                 for (int i = 0; i < NI; ++i) {
                     if (e0 + NPF + i < e1) {
                         const float wa = __int_as_float(cur.p[NPF + i].y);
 #pragma unroll
-                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, va[i][k]);
+                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], k));
                     }
                 }
                 for (int e = e0 + kLgNmInline; e < e1; ++e) {
                     const int2 pa = pairs[e];
-                    const uint32_t ba = (static_cast<uint32_t>(pa.x) * B + b0) * (4u * D);
                     f32x4 vb[G::K];
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k)
-                        vb[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, lo[b][k], ba, 0));
+                    load_nb(pa.x, true, b0, lo[b], vb);
                     const float wa = __int_as_float(pa.y);
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, vb[k]);
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vb, k));
                 }
             }
             const int sl = static_cast<int>(t % R);
@@ -924,23 +967,31 @@ struct Nb3Lds {
     static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
     static constexpr int L = D * D + 2 * D;               // slab row: dW, db, d(node bias)
     static constexpr int MX = WF + kNmBwdWaves3 * TL > L ? WF + kNmBwdWaves3 * TL : L;
-    static constexpr size_t BYTES = 4 * static_cast<size_t>(MX + kNmBwdWaves3);  // + per-wave max |W| (F16)
+    static constexpr size_t BYTES = 4 * static_cast<size_t>(MX);
 };
 
 #ifndef LG_NB3_NPF
 #define LG_NB3_NPF 4  // neighbour blocks in flight in the backward (lab builds override)
 #endif
 // MB (with MASK_IN): the layer's output mask comes as the forward's ymask bits instead of a
-// gather of y, so the prefetch keeps the unmasked depth
-// F16 (fp32 tier): both GEMMs on the 2-way fp16 split with power-of-two block scales (W per
-// launch, t and x per tile): 3 f16 MFMAs per product instead of 6 bf16 ones
-template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false, bool F16 = false>
+// gather of y, so the prefetch keeps the unmasked depth.
+// X0 (layer 0 on the compressed node init, lg_gcn_bwd_nm_x0): the tile's own x block is a
+// sensor row block of x = xs0 [S][B][D] (pos_slot of the schedule position >= 0) or, for any
+// other node, its [x0 > 0] mask word: x0 = bit ? relu(bias) * scale : 0.
+struct NbX0 {
+    const uint16_t* bits;
+    const float* bias;
+    float scale;
+    uint32_t S;
+    const int32_t* pos_slot;
+};
+template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false, bool X0 = false>
 __global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
 k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
               const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
               const int32_t* __restrict__ node_slot, float* __restrict__ dxo, float* __restrict__ slab, uint32_t N,
               uint32_t B, uint32_t ngroups, lg_fastdiv fdN, int mask_out, float scale_in, float scale_out,
-              const uint16_t* __restrict__ ymask) {
+              const uint16_t* __restrict__ ymask, NbX0 x0) {
     static_assert(!MB || MASK_IN, "mask bits replace the y gather of MASK_IN");
     constexpr bool MY = MASK_IN && !MB;  // mask from gathered y rows
     using G = NmGeo<D>;
@@ -959,8 +1010,16 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     float* xl = tl + G::TILE;           // x tile [row][feature]
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MY ? yv : dy, bytes),
-                                 xs = nm_rsrc(x, bytes), dxs = nm_rsrc(dxo, bytes);
+                                 xs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : bytes),
+                                 dxs = nm_rsrc(dxo, bytes);
     const __amdgpu_buffer_rsrc_t mbs = nm_mask_rsrc(ymask, N, ngroups);
+    const __amdgpu_buffer_rsrc_t x0bs = nm_mask_rsrc(x0.bits, N, ngroups);
+    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f};  // X0: a kept non-sensor element of the lane's slots
+    if constexpr (X0) {
+        const f32x4 bv = ld4(x0.bias + 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v0[i] = fmaxf(bv[i], 0.f) * x0.scale;
+    }
     uint32_t loff[G::K];
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
@@ -1005,16 +1064,23 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     uint32_t lo[G::K];
     NmRec cur;
     uint32_t cn, cb0;
-    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb) {
+    int cslot = -1;  // X0: the tile's sensor slot (-1: its x block is a mask word in px[0][0])
+    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb, int pslot) {
         n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
+        cslot = pslot;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-        const uint32_t ob = nb ? (n * B + b0) * (4u * D) : kNm3BlkOob;
+        if (X0 && pslot < 0) {
+            px[0][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b16(
+                x0bs, nb ? nm_mask_off(n, b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane, 0, 0));
+        } else {
+            const uint32_t ob = nb ? ((X0 ? static_cast<uint32_t>(pslot) : n) * B + b0) * (4u * D) : kNm3BlkOob;
 #pragma unroll
-        for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
+            for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
+        }
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
             const bool have = r.e0 + i < r.e1;
@@ -1027,34 +1093,20 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             if constexpr (MB) pmb[i] = ldb(static_cast<uint32_t>(r.p[i].x), b0 >> 4, have);
         }
     };
+    // X0: the sensor slot of schedule position i (wave-uniform scalar load, no dependence on
+    // the record)
+    auto pslot_of = [&](uint32_t i) -> int { return X0 ? __builtin_amdgcn_readfirstlane(x0.pos_slot[i]) : -1; };
     {
         uint32_t n0, b00, nb00;
         tile_coords(sc.first, n0, b00, nb00);
-        issue(nm_rec(tab, N + n0), n0, b00, nb00);  // schedule section
+        issue(nm_rec(tab, N + n0), n0, b00, nb00, pslot_of(n0));  // schedule section
     }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
-    int wexp = 0;  // F16: W's scale exponent (WG-wide max |W| at [2^14, 2^15))
     {
         constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
         f32x4 wv[WPER];
 #pragma unroll
         for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
-        float wsc = 1.f;
-        if constexpr (F16) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int u = 0; u < WPER; ++u)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(wv[u][c])));
-            m = lg_wave_max_bits(m);
-            uint32_t* wmx = reinterpret_cast<uint32_t*>(smem) + LY::MX;
-            if (lane == 0) wmx[wave] = m;
-            __syncthreads();
-#pragma unroll
-            for (int w2 = 0; w2 < kNmBwdWaves3; ++w2) m = max(m, wmx[w2]);
-            wexp = lg_f16_scale_exp_c(m);
-            wsc = lg_pow2f(wexp);
-        }
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
             const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
@@ -1063,14 +1115,6 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int e = (c4 + c) * SB + o;
-                if constexpr (F16) {
-                    const float w = wv[u][c] * wsc;
-                    const _Float16 h0 = static_cast<_Float16>(w);
-                    const _Float16 h1 = static_cast<_Float16>(w - static_cast<float>(h0));
-                    wsl[e] = __builtin_bit_cast(uint16_t, h0);
-                    wsl[D * SB + e] = __builtin_bit_cast(uint16_t, h1);
-                    continue;
-                }
                 const float w = wv[u][c];
                 const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
                 const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
@@ -1104,12 +1148,19 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         uint32_t nn, nb0, nnb;
         tile_coords(tile + sc.stride, nn, nb0, nnb);
         const NmRec nxt = nm_rec(tab, N + nn);
+        const int nslot = pslot_of(nn);
         asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
         f32x4 acc[G::K], xv[G::K];
+        const uint32_t xw = __float_as_uint(px[0][0]);
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
             acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-            xv[k] = px[k];
+            if (X0 && cslot < 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xv[k][i] = (xw >> (4 * k + i)) & 1u ? v0[i] : 0.f;
+            } else {
+                xv[k] = px[k];
+            }
         }
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
@@ -1170,23 +1221,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int k = 0; k < G::K; ++k)
                 dbacc += MB ? dzb(ld(dys, tlo[k] + ob), bo, k) : dzf(ld(dys, tlo[k] + ob), MY ? ld(ms, tlo[k] + ob) : f32x4{});
         }
-        issue(nxt, nn, nb0, nnb);
+        issue(nxt, nn, nb0, nnb, nslot);
         __builtin_amdgcn_sched_barrier(0);
-        // F16: the tile's t and x scale exponents (max over the wave's registers)
-        int texp = 0, xexp = 0;
-        if constexpr (F16) {
-            uint32_t mt = 0, mx = 0;
-#pragma unroll
-            for (int k = 0; k < G::K; ++k)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    mt = max(mt, __float_as_uint(fabsf(acc[k][c])));
-                    mx = max(mx, __float_as_uint(fabsf(xv[k][c])));
-                }
-            texp = lg_f16_scale_exp_c(lg_wave_max_bits(mt));
-            xexp = lg_f16_scale_exp_c(lg_wave_max_bits(mx));
-        }
-        const float tsc = lg_pow2f(texp), xsc = lg_pow2f(xexp);
 
         wave_sync_nm();
 #pragma unroll
@@ -1196,39 +1232,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         wave_sync_nm();
         // dW += t^T x over the tile's 16 rows: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
-        if constexpr (F16) {
-            lg_f16x4 xb[G::CH][2];
-#pragma unroll
-            for (int ni = 0; ni < G::CH; ++ni) {
-                f32x4 v;
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j] * xsc;
-                split2_f16_x4(v, xb[ni][0], xb[ni][1]);
-            }
-            const float us = lg_pow2f(-(texp + xexp));
-#pragma unroll
-            for (int mo = 0; mo < G::CH; ++mo) {
-                f32x4 v;
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j] * tsc;
-                lg_f16x4 a0, a1;
-                split2_f16_x4(v, a0, a1);
-                f32x4 c[G::CH];
-#pragma unroll
-                for (int ni = 0; ni < G::CH; ++ni) {
-                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, xb[ni][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][1], c[ni], 0, 0, 0);
-                    c[ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][0], c[ni], 0, 0, 0);
-                }
-#pragma unroll
-                for (int ni = 0; ni < G::CH; ++ni)
-#pragma unroll
-                    for (int reg = 0; reg < 4; ++reg) dw[mo][ni][reg] = fmaf(c[ni][reg], us, dw[mo][ni][reg]);
-                // one output row block at a time: interleaving all 16 unscaled partials would hold
-                // 64 more VGPRs
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
+        {
             lg_i16x4 xb[G::CH][3];
 #pragma unroll
             for (int ni = 0; ni < G::CH; ++ni) {
@@ -1271,33 +1275,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         f32x4 o[G::CH];
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // the W fragments are loop-invariant LDS reads: an opaque zero offset keeps the compiler
-        // from hoisting all of them (64 VGPRs) out of the tile loop
-        int wz = 0;
-        asm volatile("" : "+s"(wz));
 #pragma unroll
-        for (int s2 = 0; s2 < D / 32 && F16; ++s2) {
-            lg_f16x8 b0f, b1f;
-            split2_f16_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q) * tsc, ld4(tl + j * G::S + 32 * s2 + 8 * q + 4) * tsc, b0f,
-                          b1f);
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) {
-                const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q + wz;
-                const lg_f16x8 a0 = *reinterpret_cast<const lg_f16x8*>(wsl + ew);
-                const lg_f16x8 a1 = *reinterpret_cast<const lg_f16x8*>(wsl + D * SB + ew);
-                o[mt] = mfma_h(a1, b0f, o[mt]);
-                o[mt] = mfma_h(a0, b1f, o[mt]);
-                o[mt] = mfma_h(a0, b0f, o[mt]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (F16) {
-            const float ux = lg_pow2f(-(wexp + texp));
-#pragma unroll
-            for (int mt = 0; mt < G::CH; ++mt) o[mt] *= ux;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < D / 32 && !F16; ++s2) {
+        for (int s2 = 0; s2 < D / 32; ++s2) {
             lg_bf16x8 b0f, b1f, b2f;
             split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f, b2f);
 #pragma unroll
@@ -1812,17 +1791,16 @@ auto nm3_kernel(int flags) {
     if (flags & LG_F_BF16) return k_gcn_fwd_nm3<D, DR, RL, true, 4, true>;
     return (flags & LG_F_F32_MFMA) ? k_gcn_fwd_nm3<D, DR, RL, false, 4> : k_gcn_fwd_nm3<D, DR, RL, true, 4>;
 }
-template <int D, bool DR, bool RL>
+template <int D, bool DR, bool RL, bool X0>
 auto pc_kernel(bool bf16, bool f16) {
-    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, 2>
-                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, 2> : k_gcn_fwd_pc<D, DR, RL, false, false, 4, 2>);
+    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, 2, X0>
+                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, 2, X0> : k_gcn_fwd_pc<D, DR, RL, false, false, 4, 2, X0>);
 }
 
-}  // namespace
-
-extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
-                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
-                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream, uint16_t* ymask) {
+// lg_gcn_fwd_nm_bits (x0 == NULL) and lg_gcn_fwd_nm_x0 (x the sensor rows, *x0 the rest)
+int nm_fwd(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W, const float* bias, float* y,
+           int64_t B, int64_t N, int64_t D, int flags, float dropout_p, uint64_t seed, uint32_t salt,
+           lg_stream_t stream, uint16_t* ymask, const PcX0* x0) {
     if (B < 0 || N <= 0 || !nodetab || !pairs || !x || !W || !y || x == y) return LG_EINVAL;
     if ((flags & LG_F_BIAS) && !bias) return LG_EINVAL;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
@@ -1841,13 +1819,14 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     //   LG_F_NM3: the per-wave pipeline k_gcn_fwd_nm3 (3-way bf16 split; LG_F_F32_MFMA: exact
     //     fp32 MFMA, bit-identical to lg_gcn_fwd);
     //   bf16 tier (LG_F_BF16): nm3's single bf16 product, or pc's with LG_F_PC.
-    const bool nm3 = (flags & (LG_F_NM3 | LG_F_F32_MFMA)) != 0 || (bf16 && !(flags & LG_F_PC));
+    // The compressed layer-0 input runs on pc only.
+    const bool nm3 = !x0 && ((flags & (LG_F_NM3 | LG_F_F32_MFMA)) != 0 || (bf16 && !(flags & LG_F_PC)));
     const bool f16 = !bf16 && !(flags & LG_F_BF16X3);
-    (void)nnz_cap;
     const int2* pr = reinterpret_cast<const int2*>(pairs);
     const lg_fastdiv fd = lg_make_fastdiv(static_cast<uint32_t>(N));
     hipStream_t s = lg_stream(stream);
     const uint32_t N32 = static_cast<uint32_t>(N), B32 = static_cast<uint32_t>(B), G32 = static_cast<uint32_t>(ngroups);
+    const PcX0 xz = x0 ? *x0 : PcX0{nullptr, nullptr, 1.f, 0u};
     auto launch = [&](auto dc, auto drc) {
         constexpr int DD = decltype(dc)::value;
         constexpr bool DR = decltype(drc)::value;
@@ -1858,12 +1837,13 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
             lg_launch(kern, grid, 64 * 4, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
                       salt, ymask);
         } else {
-            auto kern = relu ? pc_kernel<DD, DR, true>(bf16, f16) : pc_kernel<DD, DR, false>(bf16, f16);
+            auto kern = x0 ? (relu ? pc_kernel<DD, DR, true, true>(bf16, f16) : pc_kernel<DD, DR, false, true>(bf16, f16))
+                           : (relu ? pc_kernel<DD, DR, true, false>(bf16, f16) : pc_kernel<DD, DR, false, false>(bf16, f16));
             const size_t dyn = PcLds<DD, 4, 2>::BYTES;
             const int thr = 64 * 4 * 3;
             const int grid = nm_grid(kern, thr, dyn, ntiles, 4, 1);
             lg_launch(kern, grid, thr, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
-                      salt, ymask);
+                      salt, ymask, xz);
         }
     };
     using I32 = std::integral_constant<int, 32>;
@@ -1879,6 +1859,27 @@ extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, 
     }
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
+}
+
+}  // namespace
+
+extern "C" int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
+                             const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, int flags,
+                             float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream, uint16_t* ymask) {
+    (void)nnz_cap;
+    return nm_fwd(nodetab, pairs, x, W, bias, y, B, N, D, flags, dropout_p, seed, salt, stream, ymask, nullptr);
+}
+
+extern "C" int lg_gcn_fwd_nm_x0(const int32_t* nodetab_s, const int32_t* pairs_s, const float* xs0,
+                                const uint16_t* x0bits, const float* node_bias, const float* W, const float* bias,
+                                float* y, int64_t B, int64_t N, int64_t S, int64_t D, int flags, float dropout_p,
+                                uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    if (S < 0 || S > 0xFFFF || !x0bits || !node_bias || !xs0) return LG_EINVAL;
+    if (S * B * D * 4 > static_cast<int64_t>(kNm3MaxBytes)) return LG_EUNSUPPORTED;
+    const bool drop = (flags & LG_F_DROPOUT) != 0;
+    const float scale = drop && dropout_p >= 0.f && dropout_p < 1.f ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    const PcX0 x0{x0bits, node_bias, scale, static_cast<uint32_t>(S)};
+    return nm_fwd(nodetab_s, pairs_s, xs0, W, bias, y, B, N, D, flags, dropout_p, seed, salt, stream, nullptr, &x0);
 }
 
 #ifdef LG_NM3_STAMPS
@@ -1907,14 +1908,17 @@ extern "C" int64_t lg_gcn_bwd_nm_workspace_bytes(int64_t D) {
     return static_cast<int64_t>(2) * lg_num_cus() * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));
 }
 
-extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
-                             const float* x, const float* W, float* dx_out, float* dW, float* db,
-                             const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
-                             float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream, const uint16_t* ymask) {
+namespace {
+// lg_gcn_bwd_nm_bits (x0 == NULL) and lg_gcn_bwd_nm_x0 (x the sensor rows, *x0 the rest)
+int nm_bwd(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y, const float* x,
+           const float* W, float* dx_out, float* dW, float* db, const int32_t* node_slot, float* dnode_bias, int64_t B,
+           int64_t N, int64_t D, int flags, float scale_in, float scale_out, void* workspace, int64_t ws_bytes,
+           lg_stream_t stream, const uint16_t* ymask, const NbX0* x0) {
     if (B < 0 || N <= 0 || !nodetab_t || !pairs_t || !dy || !x || !W || !dx_out || !dW || !workspace) return LG_EINVAL;
     if ((node_slot == nullptr) != (dnode_bias == nullptr)) return LG_EINVAL;
     const bool mask_in = (flags & LG_F_MASK_IN) != 0;
     if (mask_in && !y && !ymask) return LG_EINVAL;
+    if (x0 && mask_in) return LG_EUNSUPPORTED;  // layer 0: its output mask is the next layer's input mask
     const bool mbits = mask_in && ymask != nullptr;
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     if (!nm_fits(B, N, D) || N * ((B + 15) / 16) >= kLgMaxRows) return LG_EUNSUPPORTED;
@@ -1928,19 +1932,29 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
     const bool bf = (flags & LG_F_BF16) != 0;
+    const NbX0 xz = x0 ? *x0 : NbX0{nullptr, nullptr, 1.f, 0u, nullptr};
     // k_gcn_bwd_nm3: the 3-way bf16 split (fp32 tier) or the single bf16 product (LG_F_BF16)
     int grid = 1;
     // B == 0 still runs one (empty) launch so the slab holds zeros
+    auto launch = [&](auto kern, size_t dyn3) {
+        grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, 2),
+                             2 * lg_num_cus());
+        lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,
+                  static_cast<uint32_t>(N), static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd, mask_out,
+                  scale_in, scale_out, ymask, xz);
+    };
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
     do {                                                                                                           \
-        auto kern = (MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>)  \
-                                  : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>);        \
-        const size_t dyn3 = Nb3Lds<DD, MI>::BYTES;                                                                 \
-        grid = std::min<int>(nm_grid(kern, 64 * kNmBwdWaves3, dyn3, std::max<int64_t>(ntiles, 1), kNmBwdWaves3, 2), \
-                             2 * lg_num_cus());                                                                    \
-        lg_launch(kern, grid, 64 * kNmBwdWaves3, dyn3, s, nodetab_t, pr, dy, y, x, W, node_slot, dx_out, slab,      \
-                  static_cast<uint32_t>(N), static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd, mask_out, \
-                  scale_in, scale_out, ymask);                                                                     \
+        if constexpr (!MI) {                                                                                       \
+            if (x0) {                                                                                              \
+                launch(bf ? k_gcn_bwd_nm3<DD, false, NBB, true, false, true>                                       \
+                          : k_gcn_bwd_nm3<DD, false, NBB, false, false, true>, Nb3Lds<DD, false>::BYTES);          \
+                break;                                                                                             \
+            }                                                                                                      \
+        }                                                                                                          \
+        launch((MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>)  \
+                             : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>),         \
+               Nb3Lds<DD, MI>::BYTES);                                                                             \
     } while (0)
 #define LG_NM_BWD_D(DD)                                  \
     do {                                                 \
@@ -1960,6 +1974,31 @@ extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs
     const int64_t L = D * D + 2 * D;
     const LgSlabSeg segs[3] = {{0, D * D, dW}, {D * D, D, db}, {D * D + D, D, dnode_bias}};
     return lg_launch_slab_reduce_multi(slab, grid, L, segs, 3, nullptr, nullptr, s);
+}
+}  // namespace
+
+extern "C" int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
+                             const float* x, const float* W, float* dx_out, float* dW, float* db,
+                             const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D, int flags,
+                             float scale_in, float scale_out, void* workspace, int64_t ws_bytes, lg_stream_t stream,
+                             const uint16_t* ymask) {
+    return nm_bwd(nodetab_t, pairs_t, dy, y, x, W, dx_out, dW, db, node_slot, dnode_bias, B, N, D, flags, scale_in,
+                  scale_out, workspace, ws_bytes, stream, ymask, nullptr);
+}
+
+extern "C" int lg_gcn_bwd_nm_x0(const int32_t* nodetab_t, const int32_t* pairs_t, const int32_t* pos_slot_t,
+                                const float* dy, const float* xs0, const uint16_t* x0bits, const float* node_bias,
+                                const float* W, float* dx_out, float* dW, float* db, const int32_t* node_slot,
+                                float* dnode_bias, int64_t B, int64_t N, int64_t S, int64_t D, int flags,
+                                float dropout_p, float scale_out, void* workspace, int64_t ws_bytes,
+                                lg_stream_t stream) {
+    if (S < 0 || S > 0xFFFF || !x0bits || !node_bias || !xs0 || !pos_slot_t) return LG_EINVAL;
+    if (S * B * D * 4 > static_cast<int64_t>(kNm3MaxBytes)) return LG_EUNSUPPORTED;
+    const bool drop = (flags & LG_F_DROPOUT) != 0;
+    if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    const NbX0 x0{x0bits, node_bias, drop ? 1.0f / (1.0f - dropout_p) : 1.0f, static_cast<uint32_t>(S), pos_slot_t};
+    return nm_bwd(nodetab_t, pairs_t, dy, nullptr, xs0, W, dx_out, dW, db, node_slot, dnode_bias, B, N, D,
+                  flags & ~LG_F_DROPOUT, 1.0f, scale_out, workspace, ws_bytes, stream, nullptr, &x0);
 }
 
 extern "C" int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,

@@ -187,6 +187,39 @@ __global__ void k_nm_table(const int32_t* __restrict__ rowptr, const int2* __res
     for (int i = 0; i < 4; ++i) o[i] = int4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
 }
 
+// Sensor marks of a node table for the compressed layer-0 input (lg_gcn_fwd_nm_x0): every
+// (col, w) entry whose col has a sensor slot gets col = kLgSensorCol | slot; pos_slot[i] =
+// node_slot of the schedule section's record N + i.
+__global__ void k_nm_mark(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, int64_t N, int64_t nnz,
+                          const int32_t* __restrict__ node_slot, int32_t* __restrict__ tab_out,
+                          int2* __restrict__ pairs_out, int32_t* __restrict__ pos_slot) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    auto mark = [&](int32_t c) { return (c >= 0 && c < N && node_slot[c] >= 0) ? (kLgSensorCol | node_slot[c]) : c; };
+    if (i < 2 * N) {
+        const int4* t = reinterpret_cast<const int4*>(tab + 16 * i);
+        int v[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int4 q = t[k];
+            v[4 * k] = q.x;
+            v[4 * k + 1] = q.y;
+            v[4 * k + 2] = q.z;
+            v[4 * k + 3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < kLgNmInline; ++k)
+            if (v[0] + k < v[1]) v[2 + 2 * k] = mark(v[2 + 2 * k]);
+        int4* o = reinterpret_cast<int4*>(tab_out + 16 * i);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = int4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+        if (i >= N) pos_slot[i - N] = node_slot[v[15]];
+    }
+    if (i < nnz) {
+        const int2 p = pairs[i];
+        pairs_out[i] = int2{mark(p.x), p.y};
+    }
+}
+
 inline unsigned nblocks(int64_t n) { return static_cast<unsigned>((n + kThreads - 1) / kThreads); }
 inline int64_t align256(int64_t b) { return (b + 255) & ~int64_t(255); }
 
@@ -281,6 +314,20 @@ extern "C" int lg_nm_table_build(const int32_t* rowptr, const int32_t* pairs, in
     if (N <= 0 || N > INT32_MAX / 32 || !rowptr || !pairs || !nodetab) return LG_EINVAL;
     k_nm_table<<<nblocks(2 * N), kThreads, 0, lg_stream(stream)>>>(rowptr, reinterpret_cast<const int2*>(pairs), N,
                                                                    order, nodetab);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_nm_table_sensor_mark(const int32_t* nodetab, const int32_t* pairs, int64_t N, int64_t nnz,
+                                       const int32_t* node_slot, int32_t* nodetab_out, int32_t* pairs_out,
+                                       int32_t* pos_slot, lg_stream_t stream) {
+    if (N <= 0 || N > INT32_MAX / 32 || nnz < 0 || nnz > INT32_MAX / 2 || !nodetab || !node_slot || !nodetab_out ||
+        !pos_slot || (nnz > 0 && (!pairs || !pairs_out)))
+        return LG_EINVAL;
+    const int64_t n = std::max<int64_t>(2 * N, nnz);
+    k_nm_mark<<<nblocks(n), kThreads, 0, lg_stream(stream)>>>(nodetab, reinterpret_cast<const int2*>(pairs), N, nnz,
+                                                              node_slot, nodetab_out, reinterpret_cast<int2*>(pairs_out),
+                                                              pos_slot);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

@@ -167,6 +167,137 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
     }
 }
 
+// Compressed node init (lg_node_init_bits_fwd): x0 never materialised.  Output:
+//   xs0   [S][B][D]: the sensor rows dropout(relu([h_s, 1] W^T + b)) of every LIVE slot s
+//                    (the node's last slot, detector.py:181), node-major per slot;
+//   x0bits          : [x0 > 0] of EVERY row in the node-major mask layout of lg_gcn_fwd_nm_bits
+//                    (per 16-row tile (node n, window group g) one uint16 per lane l of the
+//                    gather layout: bit 4 k + i = row 16 g + RPI k + l / LPR, channel
+//                    4 (l % LPR) + i);
+// a non-sensor element is then x0 = bit ? relu(b) * scale : 0 exactly (relu(b) * scale > 0
+// <=> b > 0 kept).  The first GS workgroups stage W^T and form the sensor tiles (16 rows
+// each: the same per-row arithmetic as k_node_init_proj, so the rows are bit-identical),
+// posting each row's nibbles to LDS and storing the tile's mask words; the workgroups after
+// them write the non-sensor tiles' mask words, one lane of one tile per thread.
+template <int D, int DS>
+__global__ void __launch_bounds__(256)
+k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ sidx, const float* __restrict__ hs,
+                 const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ xs0,
+                 uint16_t* __restrict__ bits, int64_t B, int64_t N, int64_t S, int64_t ngroups, int GS, int dropout,
+                 float p, float scale, uint64_t seed, uint32_t salt) {
+    constexpr int LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI, TPI = 256 / (16 * LPR);
+    const uint32_t key = lg_dropout_key_dev(seed, salt);
+    const uint32_t thr = lg_keep_threshold16(p);
+    if (static_cast<int>(blockIdx.x) < GS) {
+        __shared__ __attribute__((aligned(16))) float wt[DS][D];  // W^T[k][o]
+        __shared__ __attribute__((aligned(16))) float bf[D];      // W[o][DS] + bias[o]
+        __shared__ uint8_t nib[TPI][16][LPR];                     // [x0 > 0] nibbles of the sensor rows
+        const int rr = threadIdx.x / LPR, fg = threadIdx.x % LPR, ti = rr / 16, r = rr % 16;
+        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {
+            const int k = i / D, o = i % D;
+            if (k < DS) wt[k][o] = W[o * (DS + 1) + k];
+            else bf[o] = W[o * (DS + 1) + DS] + bias[o];
+        }
+        __syncthreads();
+        const f32x4 bs = ld4(bf + 4 * fg);
+        const int64_t T = S * ngroups;
+        for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * TPI; t0 < T; t0 += static_cast<int64_t>(GS) * TPI) {
+            const int64_t t = t0 + ti;
+            const int64_t sc = t < T ? t / ngroups : 0, grp = t < T ? t - sc * ngroups : 0;
+            const int64_t n = sidx[sc];
+            const bool live = t < T && slot[n] == sc;
+            const int64_t b = 16 * grp + r;
+            uint32_t nb = 0;
+            if (live && b < B) {
+                const float* hrow = hs + (b * S + sc) * DS;
+                f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+                for (int k4 = 0; k4 < DS / 4; ++k4) {
+                    const f32x4 h4 = ld4(hrow + 4 * k4);
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const f32x4 w = ld4(&wt[4 * k4 + kk][4 * fg]);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[i] = fmaf(h4[kk], w[i], acc[i]);
+                    }
+                }
+                f32x4 v = acc + bs;
+                const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b * N + n), 4 * fg, thr) : 0xFu;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[i] = ((kb >> i) & 1u) ? fmaxf(v[i], 0.f) * (dropout ? scale : 1.0f) : 0.0f;
+                    nb |= static_cast<uint32_t>(v[i] > 0.f) << i;
+                }
+                st4(xs0 + (sc * B + b) * D + 4 * fg, v);
+            }
+            nib[ti][r][fg] = static_cast<uint8_t>(nb);
+            __syncthreads();
+            if (threadIdx.x < 64 * TPI) {
+                const int tj = threadIdx.x / 64, l = threadIdx.x % 64, rl = l / LPR, fl = l % LPR;
+                const int64_t tt = t0 + tj;
+                const int64_t sc2 = tt < T ? tt / ngroups : 0, g2 = tt < T ? tt - sc2 * ngroups : 0;
+                const int64_t n2 = sidx[sc2];
+                if (tt < T && slot[n2] == sc2) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) w |= static_cast<uint32_t>(nib[tj][RPI * k + rl][fl]) << (4 * k);
+                    bits[(n2 * ngroups + g2) * 64 + l] = static_cast<uint16_t>(w);
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+    // non-sensor tiles: one lane of one tile per thread
+    const int64_t t = static_cast<int64_t>(static_cast<int>(blockIdx.x) - GS) * 4 + threadIdx.x / 64;
+    if (t >= N * ngroups) return;
+    const int64_t n = t / ngroups, grp = t - n * ngroups;
+    if (slot[n] >= 0) return;
+    const int l = threadIdx.x % 64, rl = l / LPR, fg = l % LPR;
+    uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
+    {
+        const f32x4 bv = ld4(bias + 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * (dropout ? scale : 1.0f) > 0.f) << i;
+    }
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int64_t b = 16 * grp + RPI * k + rl;
+        if (b < B) {
+            const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b * N + n), 4 * fg, thr) : 0xFu;
+            w |= (kb & pos) << (4 * k);
+        }
+    }
+    bits[t * 64 + l] = static_cast<uint16_t>(w);
+}
+
+// x0 materialised from its compressed form (lg_node_init_expand; diagnostics and tests):
+// node-major [N][B][D], a row per LPR lanes.
+template <int D>
+__global__ void __launch_bounds__(256)
+k_node_init_expand(const int32_t* __restrict__ slot, const float* __restrict__ xs0, const uint16_t* __restrict__ bits,
+                   const float* __restrict__ bias, float* __restrict__ x0, int64_t B, int64_t N, int64_t ngroups,
+                   float vscale) {
+    constexpr int LPR = D / 4, RPI = 64 / LPR;
+    const int64_t r = static_cast<int64_t>(blockIdx.x) * (256 / LPR) + threadIdx.x / LPR;
+    const int fg = threadIdx.x % LPR;
+    if (r >= N * B) return;
+    const int64_t n = r / B, b = r - n * B;
+    f32x4 v;
+    if (slot[n] >= 0) {
+        v = ld4(xs0 + (static_cast<int64_t>(slot[n]) * B + b) * D + 4 * fg);
+    } else {
+        const int64_t grp = b / 16, rb = b % 16;
+        const int k = static_cast<int>(rb) / RPI, rl = static_cast<int>(rb) % RPI;
+        const uint32_t w = bits[(n * ngroups + grp) * 64 + rl * LPR + fg] >> (4 * k);
+        const f32x4 bv = ld4(bias + 4 * fg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = ((w >> i) & 1u) ? fmaxf(bv[i], 0.f) * vscale : 0.0f;
+    }
+    st4(x0 + r * D + 4 * fg, v);
+}
+
 // Backward of the sensor projection from the node-init pre-activation gradient dx0 (the
 // layer-0 backward's output, already masked by the node init's ReLU/dropout):
 //   dproj[b][s] = dx0[row(sensor_node[s], b)] * live[s]
@@ -477,6 +608,53 @@ extern "C" int lg_node_init_proj_fwd(const int32_t* sensor_slot, const int64_t* 
     else
         lg_launch(k_node_init_proj<32, 32>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, x0, B, N, fdM, nm,
                   S, R, GS, dropout, dropout_p, scale, seed, salt);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_node_init_bits_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx, const float* h_s,
+                                     const float* W, const float* bias, float* xs0, uint16_t* x0bits, int64_t B,
+                                     int64_t N, int64_t S, int64_t Ds, int64_t D, int flags, float dropout_p,
+                                     uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || S < 0) return LG_EINVAL;
+    if (!sensor_slot || !W || !bias || !x0bits || (S > 0 && B > 0 && (!h_s || !sensor_idx || !xs0))) return LG_EINVAL;
+    if (!((D == 64 && Ds == 64) || (D == 32 && Ds == 32))) return LG_EUNSUPPORTED;
+    const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
+    if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    if (B == 0) return LG_OK;
+    const int64_t ngroups = (B + 15) / 16;
+    if (B * N >= kLgMaxRows || N * ngroups * 64 >= kLgMaxRows) return LG_EUNSUPPORTED;
+    const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    hipStream_t s = lg_stream(stream);
+    const int64_t tpi = 256 / (16 * (D / 4));
+    const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * ngroups, tpi), 2 * lg_num_cus())));
+    const unsigned grid = static_cast<unsigned>(GS + ceil_div(N * ngroups, 4));
+    if (D == 64)
+        lg_launch(k_node_init_bits<64, 64>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B, N, S,
+                  ngroups, GS, dropout, dropout_p, scale, seed, salt);
+    else
+        lg_launch(k_node_init_bits<32, 32>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B, N, S,
+                  ngroups, GS, dropout, dropout_p, scale, seed, salt);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int lg_node_init_expand(const int32_t* sensor_slot, const float* xs0, const uint16_t* x0bits,
+                                   const float* bias, float* x0, int64_t B, int64_t N, int64_t D, int flags,
+                                   float dropout_p, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || !sensor_slot || !x0bits || !bias || !x0) return LG_EINVAL;
+    if (D != 32 && D != 64) return LG_EUNSUPPORTED;
+    const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
+    if (dropout && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    if (B == 0) return LG_OK;
+    const int64_t ngroups = (B + 15) / 16, R = B * N, rpb = 256 / (D / 4);
+    const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    hipStream_t s = lg_stream(stream);
+    const unsigned grid = static_cast<unsigned>(ceil_div(R, rpb));
+    if (D == 64)
+        lg_launch(k_node_init_expand<64>, grid, 256, 0, s, sensor_slot, xs0, x0bits, bias, x0, B, N, ngroups, scale);
+    else
+        lg_launch(k_node_init_expand<32>, grid, 256, 0, s, sensor_slot, xs0, x0bits, bias, x0, B, N, ngroups, scale);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

@@ -71,6 +71,13 @@ SIGNATURES = {
     "lg_pipe_scatter_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _p]),
     "lg_gcn_fwd_nm": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
     "lg_gcn_fwd_nm_bits": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p, _p]),
+    "lg_nm_table_sensor_mark": (_i32, [_p, _p, _i64, _i64, _p, _p, _p, _p, _p]),
+    "lg_node_init_bits_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32,
+                                     _p]),
+    "lg_node_init_expand": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p]),
+    "lg_gcn_fwd_nm_x0": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_gcn_bwd_nm_x0": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i32,
+                                _f32, _f32, _p, _i64, _p]),
     "lg_gcn_fwd_rows": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i32, _p]),
     "lg_gcn_bwd_rows": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p]),
     "lg_gcn_bwd_nm_bits": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _f32, _p, _i64, _p, _p]),

@@ -138,6 +138,9 @@ class LeakDetector(nn.Module):
         # input) as `boundary` while keep_boundary is set, so the backward can stop there and
         # the heads' gradient all-reduce overlaps the trunk backward (overlap_split)
         self.keep_boundary = False
+        # node-major trunk: keep the node init compressed (sensor rows + [x0 > 0] bits,
+        # lg_node_init_bits_fwd) instead of materialising x_0 (43 MB at B = 256)
+        self.compress_x0 = True
         self.boundary: Optional[torch.Tensor] = None
 
     def overlap_split(self):
@@ -157,6 +160,8 @@ class LeakDetector(nn.Module):
                 slot[n] = s  # duplicate sensor ids: last write wins, as h0[:, idx] = h_s does
             live = torch.tensor([float(slot[n] == s) for s, n in enumerate(self.sensor_node_idx.tolist())])
             nonsensor = torch.nonzero(slot < 0).flatten()
+            # the compressed layer-0 input's sensor-marked node tables (lg_nm_table_sensor_mark)
+            graph.x0marks = ops.SensorMarks.build(graph, slot.to(device))
             st = (graph, inc, slot.to(device), self.sensor_node_idx.to(device),
                   None if bool(live.all()) else live.to(device), nonsensor.to(device))
             self._dev_state[device] = st
@@ -180,12 +185,16 @@ class LeakDetector(nn.Module):
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
         # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init
-        xs = torch.ops.leakgnn.gnn_trunk(
+        mk = g.x0marks if (nm and self.compress_x0) else None
+        out = torch.ops.leakgnn.gnn_trunk(
             h_s, Wn, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
             nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
             g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
-            library.seed_tensor(residual.device) if drop else _NO_SEED, bf16=self.mlp_dtype == "bf16")
-        xs = xs[:-1]                                                       # [x_0 .. x_L] (the last item: x_L's mask bits)
+            library.seed_tensor(residual.device) if drop else _NO_SEED,
+            mk.nodetab_s if mk is not None else None, mk.pairs_s if mk is not None else None,
+            mk.pos_slot_t if mk is not None else None, bf16=self.mlp_dtype == "bf16")
+        out_t = out
+        xs = out[:-2]                       # [x_0 .. x_L] (then x_L's mask bits and x_0's, when compressed)
         h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
         if self.keep_boundary:
             self.boundary = h_nodes
@@ -201,6 +210,8 @@ class LeakDetector(nn.Module):
         out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed,
                                                bf16=self.mlp_dtype == "bf16")
         if self.capture is not None:
+            if out_t[-1].numel() > 0:  # x_0 compressed: materialise it for the diagnostics
+                xs = [library.expand_x0(xs[0], out_t[-1], slot, bn, N, float(self.dropout.p) if drop else 0.0)] + xs[1:]
             self.capture.update(xs=xs, node_major=nm, edge_hidden=out[1], noleak_hidden=out[3])
         return out[0]
 

@@ -351,14 +351,26 @@ def _reduce_batch(lib, st):
         check(lib.lg_reduce_batch_flush(st), "lg_reduce_batch_flush")
 
 
+def expand_x0(xs0: Tensor, x0bits: Tensor, sensor_slot: Tensor, node_bias: Tensor, N: int, p: float) -> Tensor:
+    """x_0 (N, B, D) materialised from the compressed node init (lg_node_init_expand):
+    diagnostics and tests only (LeakDetector.capture)."""
+    lib = load_library()
+    S, B, D = xs0.shape
+    x0 = torch.empty(N, B, D, device=xs0.device, dtype=torch.float32)
+    check(lib.lg_node_init_expand(ptr(sensor_slot), ptr(xs0), ptr(x0bits), ptr(node_bias), ptr(x0), B, N, D,
+                                  nat.LG_F_DROPOUT if p > 0.0 else 0, p, stream_of(xs0)), "lg_node_init_expand")
+    return x0
+
+
 # ============================================================================ gnn_trunk
 @torch.library.custom_op(f"{NS}::gnn_trunk", mutates_args=(), device_types="cuda")
 def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor],
               sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
               nodetab: Tensor, pairs: Tensor, rowptr: Tensor, col: Tensor, w: Tensor, nodetab_t: Tensor,
               pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float, node_major: bool, seed: Tensor,
+              nodetab_s: Optional[Tensor], pairs_s: Optional[Tensor], pos_slot_t: Optional[Tensor],
               *, bf16: bool = False) -> List[Tensor]:
-    """[x_0, ..., x_L, ymask]: sensor_to_node + node init (detector.py:160, 178-190),
+    """[x_0, ..., x_L, ymask, x0bits]: sensor_to_node + node init (detector.py:160, 178-190),
     then L x dropout(relu(GCNConv)).
 
       x_0     = dropout(relu(slot >= 0 ? [h_s[b, slot], 1] W^T + b : b))   (lg_node_init_proj_fwd)
@@ -370,7 +382,11 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     ReLU/dropout masks back as [x > 0] and needs x_l for dW.  ymask (node-major only, int16
     (N * ceil(B/16) * 64,), else empty): [x_L > 0] as bits (lg_gcn_fwd_nm_bits), which the
     last layer's backward reads instead of gathering x_L.
-    bf16: the node-major transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier)."""
+    bf16: the node-major transform as one bf16 MFMA product (LG_F_BF16, the configs[2] tier).
+    nodetab_s, pairs_s, pos_slot_t (ops.SensorMarks; node-major, L >= 1): x_0 stays
+    compressed (lg_node_init_bits_fwd): the returned x_0 is its sensor rows (S, B, D), x0bits
+    [x_0 > 0] of every row (int16, ymask's layout), and layer 0 reads them through the marked
+    table (lg_gcn_fwd_nm_x0, bit-identical to the dense forward).  Otherwise x0bits is empty."""
     lib = load_library()
     h_s, proj_weight, node_bias = _c(h_s), _c(proj_weight), _c(node_bias)
     weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]
@@ -387,20 +403,35 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     seed_v, sbit = _seed_args(seed) if drop else (0, 0)
     dflag = nat.LG_F_DROPOUT if drop else 0
     st = stream_of(h_s)
-    x0 = torch.empty((N, B, D) if node_major else (B, N, D), device=h_s.device, dtype=torch.float32)
-    with _timed("node_init", h_s.device):
-        check(lib.lg_node_init_proj_fwd(ptr(sensor_slot), ptr(sensor_idx), ptr(h_s), ptr(proj_weight), ptr(node_bias),
-                                        ptr(x0), B, N, S, Ds, D, dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v,
-                                        0 | sbit, st), "lg_node_init_proj_fwd")
-    xs = [x0]
     L = len(weights)
-    ymask = torch.empty(N * ((B + 15) // 16) * 64 if (node_major and L > 0) else 0, device=h_s.device,
-                        dtype=torch.int16)
+    nmask = N * ((B + 15) // 16) * 64
+    x0c = nodetab_s is not None and node_major and L > 0
+    if x0c:
+        x0 = torch.empty((S, B, D), device=h_s.device, dtype=torch.float32)
+        x0bits = torch.empty(nmask, device=h_s.device, dtype=torch.int16)
+        with _timed("node_init", h_s.device):
+            check(lib.lg_node_init_bits_fwd(ptr(sensor_slot), ptr(sensor_idx), ptr(h_s), ptr(proj_weight),
+                                            ptr(node_bias), ptr(x0), ptr(x0bits), B, N, S, Ds, D, dflag, p, seed_v,
+                                            0 | sbit, st), "lg_node_init_bits_fwd")
+    else:
+        x0 = torch.empty((N, B, D) if node_major else (B, N, D), device=h_s.device, dtype=torch.float32)
+        x0bits = torch.empty(0, device=h_s.device, dtype=torch.int16)
+        with _timed("node_init", h_s.device):
+            check(lib.lg_node_init_proj_fwd(ptr(sensor_slot), ptr(sensor_idx), ptr(h_s), ptr(proj_weight),
+                                            ptr(node_bias), ptr(x0), B, N, S, Ds, D,
+                                            dflag | (nat.LG_F_NODE_MAJOR if node_major else 0), p, seed_v, 0 | sbit, st),
+                  "lg_node_init_proj_fwd")
+    xs = [x0]
+    ymask = torch.empty(nmask if (node_major and L > 0) else 0, device=h_s.device, dtype=torch.int16)
     for l, (W, b) in enumerate(zip(weights, biases)):
-        y = torch.empty_like(x0)
+        y = torch.empty((N, B, D), device=h_s.device, dtype=torch.float32) if node_major else torch.empty_like(x0)
         flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag | (nat.LG_F_BF16 if bf16 else 0)
-        with _timed("gcn_fwd", h_s.device):
-            if node_major:
+        with _timed("gcn_fwd" if not (x0c and l == 0) else "gcn_fwd_l0", h_s.device):
+            if x0c and l == 0:
+                check(lib.lg_gcn_fwd_nm_x0(ptr(nodetab_s), ptr(pairs_s), ptr(x0), ptr(x0bits), ptr(node_bias),
+                                           ptr(W), ptr(b), ptr(y), B, N, S, D, flags | GCN_FWD_NM_EXTRA_FLAGS, p,
+                                           seed_v, (l + 1) | sbit, st), "lg_gcn_fwd_nm_x0")
+            elif node_major:
                 check(lib.lg_gcn_fwd_nm_bits(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
                                              D, col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v,
                                              (l + 1) | sbit, st, ptr(ymask) if l == L - 1 else None),
@@ -409,19 +440,23 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
                 check(lib.lg_gcn_fwd(ptr(rowptr), ptr(col), ptr(w), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
                                      col.numel(), flags, p, seed_v, (l + 1) | sbit, st), "lg_gcn_fwd")
         xs.append(y)
-    return xs + [ymask]
+    return xs + [ymask, x0bits]
 
 
 @gnn_trunk.register_fake
 def _(h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab, pairs,
-      rowptr, col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed, *, bf16=False):
-    B = h_s.shape[0]
+      rowptr, col, w, nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, seed, nodetab_s, pairs_s, pos_slot_t, *,
+      bf16=False):
+    B, S = h_s.shape[0], h_s.shape[1]
     D = proj_weight.shape[0]
     N = sensor_slot.shape[0]
     shape = (N, B, D) if node_major else (B, N, D)
     L = len(weights)
     nmask = N * ((B + 15) // 16) * 64 if (node_major and L > 0) else 0
-    return [h_s.new_empty(shape) for _ in range(L + 1)] + [h_s.new_empty((nmask,), dtype=torch.int16)]
+    x0c = nodetab_s is not None and node_major and L > 0
+    x0 = h_s.new_empty((S, B, D)) if x0c else h_s.new_empty(shape)
+    return ([x0] + [h_s.new_empty(shape) for _ in range(L)] + [h_s.new_empty((nmask,), dtype=torch.int16)]
+            + [h_s.new_empty((nmask if x0c else 0,), dtype=torch.int16)])
 
 
 @torch.library.custom_op(f"{NS}::gnn_trunk_backward", mutates_args=(), device_types="cuda")
@@ -429,19 +464,22 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: T
                        weights: List[Tensor],
                        sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
                        nodetab_t: Tensor, pairs_t: Tensor, rowptr_t: Tensor, col_t: Tensor, w_t: Tensor, p: float,
-                       node_major: bool, *, bf16: bool = False
+                       node_major: bool, x0bits: Optional[Tensor], x0_bias: Optional[Tensor],
+                       pos_slot_t: Optional[Tensor], *, bf16: bool = False
                        ) -> Tuple[Tensor, Tensor, Tensor, List[Tensor], List[Tensor]]:
     """(dh_s, dproj_weight, dnode_bias, [dW_l], [db_l]): one fused lg_gcn_bwd[_nm] per layer,
     last first (ReLU/dropout masks of a layer's output and input applied inside the kernel
     from the saved activations; the non-sensor rows' node-bias gradient summed inside layer
     0's launch), then ONE lg_sensor_proj_bwd for the projection (gather of the sensor rows,
-    dh_s, dW and the full bias gradient)."""
+    dh_s, dW and the full bias gradient).  x0bits, x0_bias (the node init's bias), pos_slot_t: x_0 is
+    compressed (gnn_trunk's x0marks path; xs[0] its sensor rows) and layer 0's backward reads
+    it through lg_gcn_bwd_nm_x0."""
     lib = load_library()
     L = len(weights)
     dev = grad_out.device
     st = stream_of(grad_out)
     if node_major:
-        N, B, D = xs[0].shape
+        N, B, D = xs[-1].shape
     else:
         B, N, D = xs[0].shape
     S, Ds = h_s.shape[1], h_s.shape[2]
@@ -456,17 +494,18 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: T
     with _reduce_batch(lib, st):
         dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx,
                                                   nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
-                                                  node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st)
+                                                  node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st,
+                                                  (x0bits, x0_bias, pos_slot_t) if x0bits is not None else None, p)
     return dh_s, dWp, dbp, dWs, dbs
 
 
 def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live,
                              nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_major, bf16, scale, wss, dWs, dbs, dbias_ns,
-                             st):
+                             st, x0c=None, p=0.0):
     L = len(weights)
     dev = dy.device
     if node_major:
-        N, B, D = xs[0].shape
+        N, B, D = xs[-1].shape
     else:
         B, N, D = xs[0].shape
     S, Ds = h_s.shape[1], h_s.shape[2]
@@ -480,7 +519,13 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
         db = torch.empty(D, device=dev, dtype=torch.float32)
         slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias_ns)) if l == 0 else (None, None)
         with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dev):
-            if node_major:
+            if x0c is not None and l == 0:  # the compressed node init (xs[0]: its sensor rows)
+                x0bits, node_bias, pos_slot_t = x0c
+                check(lib.lg_gcn_bwd_nm_x0(ptr(nodetab_t), ptr(pairs_t), ptr(pos_slot_t), ptr(dy), ptr(xs[0]),
+                                           ptr(x0bits), ptr(node_bias), ptr(weights[0]), ptr(dx), ptr(dW), ptr(db),
+                                           slot_p, dbias_p, B, N, S, D, flags | (nat.LG_F_DROPOUT if p > 0.0 else 0),
+                                           p, scale, ptr(ws), ws.numel(), st), "lg_gcn_bwd_nm_x0")
+            elif node_major:
                 bits = ptr(ymask) if (l == L - 1 and ymask.numel() > 0) else None  # [x_L > 0] as bits
                 check(lib.lg_gcn_bwd_nm_bits(ptr(nodetab_t), ptr(pairs_t), ptr(dy), ptr(xs[l + 1]), ptr(xs[l]),
                                              ptr(weights[l]), ptr(dx), ptr(dW), ptr(db), slot_p, dbias_p, B, N, D,
@@ -509,7 +554,7 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
 
 @gnn_trunk_backward.register_fake
 def _(grad_out, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live, nodetab_t,
-      pairs_t, rowptr_t, col_t, w_t, p, node_major, *, bf16=False):
+      pairs_t, rowptr_t, col_t, w_t, p, node_major, x0bits, x0_bias, pos_slot_t, *, bf16=False):
     D = proj_weight.shape[0]
     return (torch.empty_like(h_s), torch.empty_like(proj_weight), grad_out.new_empty(D),
             [torch.empty_like(t) for t in weights], [grad_out.new_empty(D) for _ in weights])
@@ -517,31 +562,36 @@ def _(grad_out, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, n
 
 def _trunk_setup(ctx, inputs, keyword_only_inputs, output):
     (h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, nonsensor_idx, slot_live, _, _, _, _, _,
-     nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, _) = inputs
+     nodetab_t, pairs_t, rowptr_t, col_t, w_t, p, node_major, _, _, _, pos_slot_in) = inputs
     bf16 = bool(keyword_only_inputs.get("bf16", False))
     ctx.L = len(weights)
     ctx.bf16 = bf16
-    # x_0 .. x_{L-1} (returned for the backward's masks) and ymask
-    ctx.mark_non_differentiable(*output[:ctx.L], output[ctx.L + 1])
+    ctx.x0c = output[ctx.L + 2].numel() > 0  # x_0 compressed (x0bits non-empty)
+    # x_0 .. x_{L-1} (returned for the backward's masks), ymask and x0bits
+    ctx.mark_non_differentiable(*output[:ctx.L], output[ctx.L + 1], output[ctx.L + 2])
     ctx.set_materialize_grads(False)  # their gradients would be zero-filled (B, N, D) tensors
     ctx.p, ctx.node_major, ctx.has_live = p, node_major, slot_live is not None
+    pos_slot_t = pos_slot_in if ctx.x0c else sensor_slot
     ctx.save_for_backward(*output, h_s, proj_weight, *weights, sensor_slot, sensor_idx, nonsensor_idx,
-                          slot_live if slot_live is not None else sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t)
+                          slot_live if slot_live is not None else sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
+                          node_bias, pos_slot_t)
 
 
 def _trunk_bwd(ctx, grads):
     L = ctx.L
     saved = ctx.saved_tensors
-    xs, ymask, h_s, proj_weight = list(saved[:L + 1]), saved[L + 1], saved[L + 2], saved[L + 3]
-    weights = list(saved[L + 4:2 * L + 4])
-    sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t = saved[2 * L + 4:]
+    xs, ymask, x0bits, h_s, proj_weight = list(saved[:L + 1]), saved[L + 1], saved[L + 2], saved[L + 3], saved[L + 4]
+    weights = list(saved[L + 5:2 * L + 5])
+    (sensor_slot, sensor_idx, nonsensor_idx, live, nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_bias,
+     pos_slot_t) = saved[2 * L + 5:]
     g = grads[L]
     if g is None:
-        return (None,) * 22
+        return (None,) * 25
     dh_s, dWp, dbp, dWs, dbs = torch.ops.leakgnn.gnn_trunk_backward(
         g, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, live if ctx.has_live else None,
-        nodetab_t, pairs_t, rowptr_t, col_t, w_t, ctx.p, ctx.node_major, bf16=ctx.bf16)
-    return (dh_s, dWp, dbp, dWs, dbs) + (None,) * 17
+        nodetab_t, pairs_t, rowptr_t, col_t, w_t, ctx.p, ctx.node_major, x0bits if ctx.x0c else None,
+        node_bias if ctx.x0c else None, pos_slot_t if ctx.x0c else None, bf16=ctx.bf16)
+    return (dh_s, dWp, dbp, dWs, dbs) + (None,) * 20
 
 
 gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)

@@ -206,6 +206,32 @@ class GCNGraph:
         return g
 
 
+@dataclass
+class SensorMarks:
+    """The compressed layer-0 input's view of a graph (lg_nm_table_sensor_mark): the forward
+    node table and pair array with every sensor column rewritten to 0x40000000 | slot, and the
+    transposed table's schedule-section slots (pos_slot_t) for the backward's own rows."""
+    nodetab_s: torch.Tensor
+    pairs_s: torch.Tensor
+    pos_slot_t: torch.Tensor
+
+    @staticmethod
+    def build(g: GCNGraph, node_slot: torch.Tensor) -> "SensorMarks":
+        lib = load_library()
+        N = g.num_nodes
+        slot = node_slot.to(device=g.nodetab.device, dtype=torch.int32).contiguous()
+        tab_s, pairs_s = torch.empty_like(g.nodetab), torch.empty_like(g.pairs)
+        pos, pos_t = torch.empty(N, dtype=torch.int32, device=slot.device), torch.empty_like(slot)
+        scratch_t, scratch_p = torch.empty_like(g.nodetab_t), torch.empty_like(g.pairs_t)
+        st = stream_of(slot)
+        check(lib.lg_nm_table_sensor_mark(ptr(g.nodetab), ptr(g.pairs), N, g.pairs.shape[0], ptr(slot), ptr(tab_s),
+                                          ptr(pairs_s), ptr(pos), st), "lg_nm_table_sensor_mark")
+        check(lib.lg_nm_table_sensor_mark(ptr(g.nodetab_t), ptr(g.pairs_t), N, g.pairs_t.shape[0], ptr(slot),
+                                          ptr(scratch_t), ptr(scratch_p), ptr(pos_t), st), "lg_nm_table_sensor_mark")
+        torch.cuda.current_stream(slot.device).synchronize()  # the scratch copies go out of scope here
+        return SensorMarks(tab_s, pairs_s, pos_t)
+
+
 def schedule_order(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:
     """int32 (N,) reverse Cuthill-McKee order of the graph (lg_rcm_order, host)."""
     ei = edge_index.detach().to("cpu", torch.long).contiguous()

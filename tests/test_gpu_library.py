@@ -114,9 +114,11 @@ def test_opcheck_trunk_and_heads(B, p):
     bs = [c.bias.detach().clone().normal_(0, 0.1).requires_grad_(True) for c in m.convs]
     nb = torch.randn(64, device=DEV, requires_grad=True)
     g = graph
+    mk = g.x0marks  # node-major: the compressed node init (lg_node_init_bits_fwd, lg_gcn_*_nm_x0)
+    marks = (mk.nodetab_s, mk.pairs_s, mk.pos_slot_t) if nm else (None, None, None)
     _check(torch.ops.leakgnn.gnn_trunk.default,
            (h_s, Wn, nb, wts, bs, slot, sidx, nons, live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t,
-            g.pairs_t, g.rowptr_t, g.col_t, g.w_t, p, nm, seed), {"bf16": B == 16})
+            g.pairs_t, g.rowptr_t, g.col_t, g.w_t, p, nm, seed, *marks), {"bf16": B == 16})
     h = torch.randn((661, B, 64) if nm else (B, 661, 64), device=DEV).relu_().requires_grad_(True)
     mlp, nmlp = m.edge_head.mlp, m.noleak_head.mlp
     hw = [t.detach().clone().requires_grad_(True) for t in (mlp[0].weight, mlp[0].bias, mlp[3].weight, mlp[3].bias,
