@@ -177,6 +177,66 @@ def pmc_traffic(which: str, kname: str, batch: int) -> dict | None:
             "WRITE_SIZE_KiB": vals["WRITE_SIZE"]}
 
 
+def short_kernel_name(name: str) -> str:
+    """k_gcn_fwd_pc<64, true, ...>(...) -> k_gcn_fwd_pc; (anonymous namespace)::k_ce_fwd(...) -> k_ce_fwd"""
+    n = name.split("(anonymous namespace)::")[-1]
+    return n.split("<")[0].split("(")[0].strip().split(" ")[-1]
+
+
+def small_kernels_us(breakdown: dict | None) -> dict:
+    """kernels_us entries of the step's small launches, from the step trace (per step, us)."""
+    if not breakdown:
+        return {}
+    by = breakdown["by_name_us"]
+    pick = {"ce_fwd": ["k_ce_fwd", "k_ce_mean"], "ce_bwd": ["k_ce_bwd"], "adam": ["k_adam_norm", "k_adam_update"],
+            "seed": ["k_seed_advance"], "slab_reduce": ["k_slab_reduce"], "sensor_proj_bwd": ["k_sensor_proj_bwd"]}
+    return {k: round(sum(by.get(n, 0.0) for n in v), 2) for k, v in pick.items()}
+
+
+def step_breakdown(batch: int, ms_per_step: float, steps: int = 20) -> dict | None:
+    """Every kernel of one replay of the captured step (tools/step_trace.py under a child
+    `rocprofv3 --kernel-trace`): per-kernel device time, their sum, the replay's span, and
+    `step_gap_us` = ms_per_step (the bench's own, unprofiled clock) minus the sum.  The
+    replays between two k_gru_fwd launches are one step each; the median replay is reported."""
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    env = dict(os.environ, TMPDIR="/tmp")
+    with tempfile.TemporaryDirectory(dir="/tmp") as d:
+        cmd = [prof, "--kernel-trace", "-d", d, "-o", "trace", "--output-format", "csv", "--", sys.executable,
+               str(REPO / "tools" / "step_trace.py"), "--B", str(batch), "--steps", str(steps)]
+        try:
+            subprocess.run(cmd, env=env, cwd=str(REPO), timeout=300, check=True, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+        except (subprocess.SubprocessError, OSError):
+            return None
+        rows = []
+        for f in Path(d).rglob("*kernel_trace.csv"):
+            rows += list(csv.DictReader(open(f)))
+    if not rows:
+        return None
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "k_gru_fwd" in r["Kernel_Name"]]
+    if len(marks) < 4:
+        return None
+    reps = []
+    for a, b in zip(marks[len(marks) // 2:-1], marks[len(marks) // 2 + 1:]):  # the later half: steady state
+        ks = [(short_kernel_name(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+              for r in rows[a:b]]
+        span = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+        reps.append((sum(t for _, t in ks), span, ks))
+    reps.sort(key=lambda x: x[0])
+    tot, span, ks = reps[len(reps) // 2]
+    agg: dict = {}
+    for n, t in ks:
+        agg[n] = round(agg.get(n, 0.0) + t, 2)
+    return {"source": "rocprofv3 --kernel-trace over tools/step_trace.py (the same captured step), median replay",
+            "kernels": [[n, round(t, 2)] for n, t in ks], "by_name_us": agg, "launches": len(ks),
+            "sum_us": round(tot, 1), "replay_span_us": round(span, 1), "step_us": round(ms_per_step * 1e3, 1),
+            "step_gap_us": round(ms_per_step * 1e3 - tot, 1),
+            "accounted_frac": round(tot / (ms_per_step * 1e3), 4)}
+
+
 def stream_copy_peak(dev, nbytes: int = 2 << 30, iters: int = 10) -> dict:
     """Measured copy bandwidth on this box: device copy of an nbytes fp32 buffer (past the
     256 MiB Infinity Cache), read + write bytes over HIP-event time."""
@@ -773,6 +833,7 @@ def main() -> None:
     traffic = pmc_traffic("gcn_fwd_nm_train", "k_gcn_fwd_pc", B) if pmc else None
     traffic_bwd = pmc_traffic("gcn_bwd_nm", "k_gcn_bwd_nm", B) if pmc else None
     gru_rep = gru_mfma_report(kms, B, len(SENSORS))
+    breakdown = step_breakdown(B, elapsed * 1e3 / args.steps) if (pmc and not args.eager) else None
     src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, 2*FETCH+WRITE (gfx950)"
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
@@ -809,7 +870,10 @@ def main() -> None:
         "stream_copy": copy,
         **xchg,
         "gru_mfma": gru_rep,
-        "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
+        "kernels_us": {**{k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
+                       **small_kernels_us(breakdown)},
+        "step_gap_us": breakdown["step_gap_us"] if breakdown else None,
+        "step_kernels": breakdown,
         "final_loss": round(final_loss, 4),
     }
     if c4 is not None:

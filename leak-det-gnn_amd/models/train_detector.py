@@ -203,6 +203,9 @@ def main(argv=None) -> None:
     ap.add_argument("--capture", type=str, default="auto", choices=["auto", "on", "off"],
                     help="replay each full-size training batch's step as one captured HIP graph "
                          "(models/graph_step.py; auto = on for the GPU path); the tail batch runs eagerly")
+    ap.add_argument("--profile", type=int, default=0,
+                    help="torch.profiler over this many training steps (after one warm-up step): "
+                         "<out_dir>/detector_trace.json + detector_ops.txt on rank 0 (models/profiling.py)")
     ap.add_argument("--perf_log", type=str, default="detector_perf.jsonl",
                     help="JSONL perf log (windows/s per log interval), relative to --out_dir; '' disables")
     args = ap.parse_args(argv)
@@ -325,6 +328,8 @@ def main(argv=None) -> None:
     cstep = None  # graph_step.CapturedTrainStep, built at the first full-size batch
     perf = PerfLog(out_dir / args.perf_log if (lead and args.perf_log) else None, world)
 
+    from .profiling import StepProfiler
+    prof = StepProfiler(out_dir, "detector", args.profile if lead else 0, device)
     for epoch in range(1, args.epochs + 1):
         detector.train()
         running = torch.zeros((), dtype=torch.float64, device=device)
@@ -380,6 +385,7 @@ def main(argv=None) -> None:
             running += loss.detach().double() * n_local
             seen += n_local
             perf.add(n_local)
+            prof.step()
             if (it % args.log_every) == 0:
                 r_, s_ = global_sum(running), global_sum(seen)
                 print(f"{now()} [detector][epoch {epoch:02d}] step {it:05d}/{len(train_loader):05d} "
@@ -400,6 +406,7 @@ def main(argv=None) -> None:
         if world > 1:
             torch.distributed.barrier()
 
+    prof.close()
     if lead:
         best_ckpt = torch.load(best_path, map_location=device, weights_only=True)
         detector.load_state_dict(best_ckpt["detector_state"])

@@ -103,6 +103,9 @@ def main(argv=None) -> None:
     ap.add_argument("--num_workers", type=int, default=0)
     ap.add_argument("--log_every", type=int, default=50)
     ap.add_argument("--loader", type=str, default="device", choices=["device", "torch"])
+    ap.add_argument("--profile", type=int, default=0,
+                    help="torch.profiler over this many training steps (after one warm-up step): "
+                         "<out_dir>/predictor_trace.json + predictor_ops.txt (models/profiling.py)")
     args = ap.parse_args(argv)
 
     out_dir = Path(args.out_dir)
@@ -148,6 +151,8 @@ def main(argv=None) -> None:
 
     print(f"{now()} [predictor] start training: epochs={args.epochs}, steps/epoch={args.steps_per_epoch}, "
           f"batch={args.batch_size}")
+    from .profiling import StepProfiler
+    prof = StepProfiler(out_dir, "predictor", args.profile, device)
     for epoch in range(1, args.epochs + 1):
         model.train()
         running = torch.zeros((), dtype=torch.float64, device=device)
@@ -163,6 +168,7 @@ def main(argv=None) -> None:
             opt.step()
             running += loss.detach().double() * x.size(0)
             seen += x.size(0)
+            prof.step()
             if (it % args.log_every) == 0:
                 print(f"{now()} [predictor][epoch {epoch:02d}] step {it:05d}/{len(train_loader):05d} "
                       f"loss={running.item() / max(seen, 1):.6f}")
@@ -180,6 +186,7 @@ def main(argv=None) -> None:
             torch.save(ckpt, best_path)
             print(f"{now()} [predictor] new best: rmse={best_rmse:.4f} -> {best_path.name}")
 
+    prof.close()
     best_ckpt = torch.load(best_path, map_location=device, weights_only=True)
     model.load_state_dict(best_ckpt["model_state"])
     test_metrics = evaluate_predictor(model, test_loader, device, mean, std)

@@ -69,7 +69,9 @@ def test_train_predictor_and_detector_cli(data, tmp_path, capsys):
     train_detector.main(["--leak_root", str(tmp_path / "leak"), "--inp_path", str(LTA_INP), "--predictor_ckpt",
                          str(out / "predictor_best.ckpt"), "--out_dir", str(out), "--epochs", "2",
                          "--steps_per_epoch", "16", "--val_steps", "16", "--test_steps", "16", "--batch_size", "8",
-                         "--device", "cuda", "--log_every", "1"])
+                         "--device", "cuda", "--log_every", "1", "--profile", "2"])
+    trace = json.loads((out / "detector_trace.json").read_text())  # --profile 2: torch.profiler, GPU activity
+    assert len({str(e.get("name", "")) for e in trace["traceEvents"]} & {f"ProfilerStep#{i}" for i in range(8)}) == 2
     ck = torch.load(out / "detector_best.ckpt", weights_only=True)
     assert ck["pipe_ids_in_order"] == INFO["pipe_ids_in_order"] and ck["num_classes"] == len(INFO["pipes"]) + 1
     assert set(ck) == {"epoch", "detector_state", "sensor_ids", "pipe_ids_in_order", "num_classes",

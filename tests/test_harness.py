@@ -207,3 +207,20 @@ def test_train_predictor_cpu_plumbing(data, tmp_path):
     std = np.asarray(ck["standardizer_std"], dtype=np.float32)
     assert mean.shape == std.shape == (len(ck["sensor_ids"]),) and (std > 0).all()
     assert (out / "predictor_last.ckpt").is_file() and (out / "predictor_meta.json").is_file()
+
+
+def test_train_predictor_profile_switch(data, tmp_path):
+    """--profile N (SURVEY §5 tracing): torch.profiler over N training steps after one warm-up
+    step writes a chrome trace and a per-op table next to the checkpoints (CPU run here; the
+    detector CLI has the same switch, exercised on the GPU in test_gpu_harness)."""
+    import json as _json
+    from models import train_predictor
+    out = tmp_path / "out"
+    train_predictor.main(["--normal_root", str(data / "normal"), "--out_dir", str(out), "--epochs", "1",
+                          "--steps_per_epoch", "6", "--val_steps", "2", "--test_steps", "2", "--batch_size", "1",
+                          "--device", "cpu", "--log_every", "100", "--profile", "3"])
+    trace = _json.loads((out / "predictor_trace.json").read_text())
+    names = {e.get("name", "") for e in trace["traceEvents"]}
+    assert any("ProfilerStep" in n for n in names), "no profiler steps in the trace"
+    assert sum(1 for n in names if n.startswith("ProfilerStep#")) == 3
+    assert "aten::" in (out / "predictor_ops.txt").read_text()
