@@ -9,7 +9,7 @@
 // the cancellation-heavy output-bias gradients) is reduced by one extra block as a
 // fixed-shape tree.  Per-column work and the combine order depend only on (G, len),
 // never on scheduling.  A reduce batch (lg_reduce_batch_begin / _flush, include/leakgnn.h)
-// takes the reductions of several backward calls into ONE launch (up to 16 segments and
+// takes the reductions of several backward calls into ONE launch (up to 24 segments and
 // 4 fp64 columns per launch); each column keeps its own order, so results do not change.
 #include "common.h"
 #include "reduce.h"
@@ -19,7 +19,7 @@
 
 namespace {
 
-constexpr int kJobSegs = 16;  // segments per launch
+constexpr int kJobSegs = 24;  // segments per launch (a whole detector backward: trunk 8, heads 6, GRU 4)
 constexpr int kJobD = 4;      // fp64 columns per launch
 
 struct Segs {

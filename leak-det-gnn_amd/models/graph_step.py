@@ -62,6 +62,17 @@ class CapturedTrainStep:
         self.slots = ops.SeedSlots(dev, seed_slots)
         self._one: Optional[torch.Tensor] = None
 
+        # every backward below reads its gradients only after backward() returns (set_to_none
+        # before each): its slab reductions run as ONE launch at the end of the pass
+        from . import library
+        defer0, library.DEFER_REDUCE = library.DEFER_REDUCE, True
+        try:
+            self._build(model, warmup, preserve_state)
+        finally:
+            library.DEFER_REDUCE = defer0
+
+    def _build(self, model, warmup: int, preserve_state: bool) -> None:
+        dev = self.label.device
         snap = self._snapshot() if preserve_state else None
         # eager warm-up on a side stream (allocator pools, optimizer state, cached graph CSR)
         side = torch.cuda.Stream(dev)
