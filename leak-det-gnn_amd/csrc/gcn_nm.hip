@@ -505,8 +505,8 @@ struct PcLds {  // floats
     static constexpr int WS = D + 4;
     static constexpr int WOFF = 0;                                  // W [out][in] * fold (fp32), bias * fold
     static constexpr int XOFF = D * WS + D;                         // per-wave max|W| bits (F16)
-    static constexpr int FOFF = XOFF + 16;                          // ready[kPcProd], done[kPcProd * NC]
-    static constexpr int MOFF = FOFF + 16 + kPcProd * NC;           // per (producer, slot): n, b0, nb, pad
+    static constexpr int FOFF = XOFF + 16;                          // ready[16], done[kPcProd * NC], fin[4], ctr
+    static constexpr int MOFF = FOFF + 16 + kPcProd * NC + 8;       // per (producer, slot): n, b0, nb, pad
     static constexpr int ROFF = MOFF + 4 * kPcProd * kPcRing;       // the rings
     static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
@@ -525,6 +525,15 @@ __device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
         if (pc_load_acq(p) >= v) return;
         __builtin_amdgcn_s_sleep(1);
     }
+}
+// wait until *p >= v (true) or the producer has finished with *fin < v tiles (false); bounded
+__device__ __forceinline__ bool pc_wait_or_fin(const uint32_t* p, const uint32_t* fin, uint32_t v) {
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (pc_load_acq(p) >= v) return true;
+        if (pc_load_acq(fin) < v) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
 }
 
 // X0: layer 0 reading the compressed node init (lg_node_init_bits_fwd): x = the sensor rows
@@ -556,6 +565,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     uint32_t* wmx = reinterpret_cast<uint32_t*>(lds + LY::XOFF);
     uint32_t* ready = reinterpret_cast<uint32_t*>(lds + LY::FOFF);
     uint32_t* done = ready + 16;
+    uint32_t* fin = done + kPcProd * NC;  // tiles a producer handed over in all (~0u while it runs)
+    uint32_t* ctr = fin + kPcProd;        // the workgroup's next tile (LDS atomic)
     uint32_t* meta = reinterpret_cast<uint32_t*>(lds + LY::MOFF);
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -576,7 +587,12 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     const int rl = lane / G::LPR, fg = lane % G::LPR;
     float* ring = lds + LY::ROFF + prod * R * LY::TILE;
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
-    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, prod, kPcProd);
+    // Tiles are dealt to WORKGROUPS statically (XCD-aware, nm_sched at one "wave" per workgroup:
+    // workgroup-strided tiles of its XCD's chunk) and to the workgroup's producers dynamically
+    // through an LDS counter: a producer that draws cheap tiles takes more of them, so the
+    // workgroup's tiles finish together (with 4 producers per workgroup the static per-producer
+    // split left 1/3 of them a whole tile behind the rest: 10 vs 11 tiles at B = 256).
+    const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, 0, 1);
     const int64_t tend = sc.end;
     const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
 
@@ -614,6 +630,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             if (lane == 0) wmx[wave] = wm;
         }
         if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
+        if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
+        if (threadIdx.x == 0) *ctr = 0u;
     }
     __syncthreads();
 #ifdef LG_NM3_STAMPS
@@ -644,31 +662,35 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
         for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
         f32x4 pf[2][NPF][G::K];
+        uint32_t pb[2][X0 ? NPF : 1];  // X0: the neighbours' mask words
         uint32_t lo[2][G::K];
         NmRec rec[2];
         uint32_t tn[2], tb0[2], tnb[2];
-        // one neighbour's block into blk: its rows (a sensor row under X0), or X0's mask word in
-        // blk[0][0]; an absent neighbour (have == false) reads zeros
-        auto load_nb = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K]) {
+        // one neighbour's block: its rows into blk (under X0 a sensor row of xs0) and, X0, its mask
+        // word into bw.  Both loads are always issued, the one that does not apply (and both for
+        // an absent neighbour, have == false) out of range (zeros, no memory access): a load
+        // under a branch would make the compiler wait for it where the branch merges.
+        auto load_nb = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K], uint32_t& bw) {
+            bool rows = have;
             if constexpr (X0) {
-                if (have && !(c & kLgSensorCol)) {
-                    blk[0][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b16(
-                        brs, nm_mask_off(static_cast<uint32_t>(c), b0 >> 4, ngroups, lane), 0, 0));
-                    return;
-                }
+                const bool sens = (c & kLgSensorCol) != 0;
+                bw = __builtin_amdgcn_raw_buffer_load_b16(
+                    brs, have && !sens ? nm_mask_off(static_cast<uint32_t>(c), b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane,
+                    0, 0);
+                rows = have && sens;
                 c &= ~kLgSensorCol;
             }
-            const uint32_t base = have ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
-            const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
+            const uint32_t base = rows ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
+            const __amdgpu_buffer_rsrc_t rs = rows ? xrs : xrs0;
 #pragma unroll
             for (int k = 0; k < G::K; ++k)
                 blk[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lk[k], base, 0));
         };
         // slot k of a loaded neighbour block as values
-        auto nbv = [&](int c, const f32x4 (&blk)[G::K], int k) -> f32x4 {
+        auto nbv = [&](int c, const f32x4 (&blk)[G::K], uint32_t bw, int k) -> f32x4 {
             if constexpr (X0) {
                 if (!(c & kLgSensorCol)) {
-                    const uint32_t w = __float_as_uint(blk[0][0]) >> (4 * k);
+                    const uint32_t w = bw >> (4 * k);
                     f32x4 r;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) r[i] = (w >> i) & 1u ? v0[i] : 0.f;
@@ -677,12 +699,21 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             }
             return blk[k];
         };
+        // the workgroup's next tile (an LDS atomic; past tend once its tiles are all dealt)
+        auto grab = [&]() -> int64_t {
+            uint32_t i = 0;
+            if (lane == 0) i = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            i = __builtin_amdgcn_readfirstlane(i);
+            return sc.first + static_cast<int64_t>(i) * sc.stride;
+        };
+        int64_t tl[2];  // the tile whose blocks are in flight in buffer b
         // r: the tile's node-table record (schedule section: slot -> record with its node id),
         // requested by the caller a phase earlier
         auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
             constexpr int b = decltype(bc)::value;
             uint32_t n, b0, nb;
             tile_coords(tile, n, b0, nb);
+            tl[b] = tile;
             rec[b] = r;
             n = static_cast<uint32_t>(r.node);
             tn[b] = n;
@@ -691,25 +722,18 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
             for (int k = 0; k < G::K; ++k) lo[b][k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
 #pragma unroll
-            for (int i = 0; i < NPF; ++i) {
-                if constexpr (X0) {
-                    if (!(r.e0 + i < r.e1)) {  // absent: no load (the first product takes weight 0)
-#pragma unroll
-                        for (int k = 0; k < G::K; ++k) pf[b][i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-                        continue;
-                    }
-                }
-                load_nb(r.p[i].x, r.e0 + i < r.e1, b0, lo[b], pf[b][i]);
-            }
+            for (int i = 0; i < NPF; ++i) load_nb(r.p[i].x, r.e0 + i < r.e1, b0, lo[b], pf[b][i], pb[b][X0 ? i : 0]);
         };
         // tile t of this producer from buffer b: accumulate, hand over, refill b with tile t + 2
         auto step = [&](auto bc, int64_t t) -> bool {
             constexpr int b = decltype(bc)::value;
-            const int64_t tile = sc.first + t * sc.stride;
+            const int64_t tile = tl[b];
             if (tile >= tend) return false;
-            // the record of tile t + 2 goes in flight while this tile is accumulated
+            // the producer's tile t + 2 is drawn, and its record goes in flight while this tile is
+            // accumulated
+            const int64_t tnext = grab();
             uint32_t nn, nb0, nnb;
-            tile_coords(tile + 2 * sc.stride, nn, nb0, nnb);
+            tile_coords(tnext, nn, nb0, nnb);
             const NmRec nxt = nm_rec(tab, N + nn);
             asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
             const NmRec& cur = rec[b];
@@ -718,44 +742,46 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             f32x4 acc[G::K];
             {
                 const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
-                const int c = e0 < e1 ? cur.p[0].x : kLgSensorCol;
+                const int c = e0 < e1 ? cur.p[0].x : kLgSensorCol;  // absent: the zero rows, weight 0
 #pragma unroll
-                for (int k = 0; k < G::K; ++k) acc[k] = nbv(c, pf[b][0], k) * w;
+                for (int k = 0; k < G::K; ++k) acc[k] = nbv(c, pf[b][0], pb[b][0], k) * w;
             }
 #pragma unroll
             for (int i = 1; i < NPF; ++i) {
                 if (e0 + i < e1) {
                     const float w = __int_as_float(cur.p[i].y);
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, nbv(cur.p[i].x, pf[b][i], k));
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, nbv(cur.p[i].x, pf[b][i], pb[b][X0 ? i : 0], k));
                 }
             }
             if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
                 constexpr int NI = kLgNmInline - NPF;
                 f32x4 va[NI][G::K];
+                uint32_t vb[NI];
 #pragma unroll
-                for (int i = 0; i < NI; ++i) load_nb(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i]);
+                for (int i = 0; i < NI; ++i) load_nb(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
 #pragma unroll
                 for (int i = 0; i < NI; ++i) {
                     if (e0 + NPF + i < e1) {
                         const float wa = __int_as_float(cur.p[NPF + i].y);
 #pragma unroll
-                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], k));
+                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], vb[i], k));
                     }
                 }
                 for (int e = e0 + kLgNmInline; e < e1; ++e) {
                     const int2 pa = pairs[e];
-                    f32x4 vb[G::K];
-                    load_nb(pa.x, true, b0, lo[b], vb);
+                    f32x4 vr[G::K];
+                    uint32_t vw;
+                    load_nb(pa.x, true, b0, lo[b], vr, vw);
                     const float wa = __int_as_float(pa.y);
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vb, k));
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vr, vw, k));
                 }
             }
             const int sl = static_cast<int>(t % R);
             const uint32_t mn = tn[b], mnb = tnb[b];
             // buffer b is free again: tile t + 2 goes in flight before the hand-off waits
-            issue(bc, nxt, tile + 2 * sc.stride);
+            issue(bc, nxt, tnext);
             // slot sl last held tile t - R, consumed by consumer (t - R) % NC as its ((t - R) / NC)-th
             if (t >= R) pc_wait(&done[prod * NC + static_cast<int>((t - R) % NC)], static_cast<uint32_t>((t - R) / NC + 1));
             float* slot = ring + sl * LY::TILE;
@@ -774,17 +800,24 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             return true;
         };
         {
+            const int64_t f0 = grab(), f1 = grab();
             uint32_t n0, b00, nb00, n1, b01, nb01;
-            tile_coords(sc.first, n0, b00, nb00);
-            tile_coords(sc.first + sc.stride, n1, b01, nb01);
+            tile_coords(f0, n0, b00, nb00);
+            tile_coords(f1, n1, b01, nb01);
             const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
-            issue(std::integral_constant<int, 0>{}, r0, sc.first);
-            issue(std::integral_constant<int, 1>{}, r1, sc.first + sc.stride);
+            issue(std::integral_constant<int, 0>{}, r0, f0);
+            issue(std::integral_constant<int, 1>{}, r1, f1);
         }
-        for (int64_t t = 0;; t += 2) {
+        int64_t t = 0;
+        for (;; t += 2) {
             if (!step(std::integral_constant<int, 0>{}, t)) break;
-            if (!step(std::integral_constant<int, 1>{}, t + 1)) break;
+            if (!step(std::integral_constant<int, 1>{}, t + 1)) {
+                ++t;
+                break;
+            }
         }
+        // tiles are drawn in increasing order, so the first one past tend ends the producer
+        if (lane == 0) pc_store_rel(&fin[prod], static_cast<uint32_t>(t));
 #ifdef LG_NM3_STAMPS
         pc_stamp_end();
 #endif
@@ -828,10 +861,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     const uint32_t thr = lg_keep_threshold16(p_drop);
     for (int64_t u = 0;; ++u) {
         const int64_t t = u * NC + cons;  // this consumer's u-th tile of its producer
-        const int64_t tile = sc.first + t * sc.stride;
-        if (tile >= tend) break;
+        // wait for tile t, or for the producer's end (it handed over fin[prod] tiles in all)
+        if (!pc_wait_or_fin(&ready[prod], &fin[prod], static_cast<uint32_t>(t + 1))) break;
         const int sl = static_cast<int>(t % R);
-        pc_wait(&ready[prod], static_cast<uint32_t>(t + 1));
         float* slot = ring + sl * LY::TILE;
         const uint32_t* m = meta + 4 * (prod * R + sl);
         const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
@@ -1060,6 +1092,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 
     // tile in flight: record, coordinates, lane offsets, first NPF neighbour blocks, own x block
     f32x4 pf[NPF][G::K], pm[MY ? NPF : 1][G::K], px[G::K];
+    uint32_t pxb = 0;  // X0: the tile's own mask word
     uint32_t pmb[MB ? NPF : 1];
     uint32_t lo[G::K];
     NmRec cur;
@@ -1073,14 +1106,15 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         cslot = pslot;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
-        if (X0 && pslot < 0) {
-            px[0][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b16(
-                x0bs, nb ? nm_mask_off(n, b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane, 0, 0));
-        } else {
-            const uint32_t ob = nb ? ((X0 ? static_cast<uint32_t>(pslot) : n) * B + b0) * (4u * D) : kNm3BlkOob;
+        // X0: both the sensor-row and the mask-word loads are always issued, the one that does
+        // not apply out of range (a load under a branch is waited for where the branch merges)
+        if constexpr (X0)
+            pxb = __builtin_amdgcn_raw_buffer_load_b16(
+                x0bs, nb && pslot < 0 ? nm_mask_off(n, b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane, 0, 0);
+        const bool rows = nb && (!X0 || pslot >= 0);
+        const uint32_t ob = rows ? ((X0 ? static_cast<uint32_t>(pslot) : n) * B + b0) * (4u * D) : kNm3BlkOob;
 #pragma unroll
-            for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
-        }
+        for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
 #pragma unroll
         for (int i = 0; i < NPF; ++i) {
             const bool have = r.e0 + i < r.e1;
@@ -1151,7 +1185,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         const int nslot = pslot_of(nn);
         asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
         f32x4 acc[G::K], xv[G::K];
-        const uint32_t xw = __float_as_uint(px[0][0]);
+        const uint32_t xw = pxb;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
             acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};

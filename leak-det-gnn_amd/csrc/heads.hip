@@ -183,65 +183,97 @@ template <int D, int DS>
 __global__ void __launch_bounds__(256)
 k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ sidx, const float* __restrict__ hs,
                  const float* __restrict__ W, const float* __restrict__ bias, float* __restrict__ xs0,
-                 uint16_t* __restrict__ bits, int64_t B, int64_t N, int64_t S, int64_t ngroups, int GS, int dropout,
-                 float p, float scale, uint64_t seed, uint32_t salt) {
+                 uint16_t* __restrict__ bits, uint32_t B, uint32_t N, uint32_t S, uint32_t ngroups, lg_fastdiv fdG,
+                 int GS, int dropout, float p, float scale, uint64_t seed, uint32_t salt) {
     constexpr int LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI, TPI = 256 / (16 * LPR);
     const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p);
     if (static_cast<int>(blockIdx.x) < GS) {
-        __shared__ __attribute__((aligned(16))) float wt[DS][D];  // W^T[k][o]
-        __shared__ __attribute__((aligned(16))) float bf[D];      // W[o][DS] + bias[o]
-        __shared__ uint8_t nib[TPI][16][LPR];                     // [x0 > 0] nibbles of the sensor rows
+        // one tile (16 rows) of TPI sensor tiles per iteration.  Latency first: W's rows and the
+        // tiles' h_s rows are requested together, coalesced (a float4 per thread), and meet in LDS
+        // behind one barrier; each lane then forms 4 outputs of one row from LDS (the h_s element
+        // is a broadcast read), the same ascending-k fmaf chain as k_node_init_proj.
+        __shared__ __attribute__((aligned(16))) float wt[DS][D];        // W^T[k][o]
+        __shared__ __attribute__((aligned(16))) float bf[D];            // W[o][DS] + bias[o]
+        __shared__ __attribute__((aligned(16))) float hl[TPI][16][DS];  // the tiles' h_s rows
+        __shared__ uint8_t nib[TPI][16][LPR];
         const int rr = threadIdx.x / LPR, fg = threadIdx.x % LPR, ti = rr / 16, r = rr % 16;
-        for (int i = threadIdx.x; i < D * (DS + 1); i += 256) {
-            const int k = i / D, o = i % D;
-            if (k < DS) wt[k][o] = W[o * (DS + 1) + k];
-            else bf[o] = W[o * (DS + 1) + DS] + bias[o];
+        constexpr int WF4 = D * (DS + 1) / 4;  // W is [D][DS + 1] row-major: float4 i = elements 4i..4i+3
+        constexpr int WPT = (WF4 + 255) / 256;
+        f32x4 wv[WPT];
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) wv[u] = ld4(W + 4 * min(u * 256 + static_cast<int>(threadIdx.x), WF4 - 1));
+        const uint32_t T = S * ngroups;
+        constexpr int HF4 = TPI * 16 * DS / 4, HPT = (HF4 + 255) / 256;  // h_s float4 per iteration
+        auto load_h = [&](uint32_t t0, f32x4 (&hv)[HPT]) {
+#pragma unroll
+            for (int u = 0; u < HPT; ++u) {
+                const int e = u * 256 + static_cast<int>(threadIdx.x);  // (tile j, row rj, float4 kk)
+                const int j = e / (16 * DS / 4), rj = (e / (DS / 4)) % 16, kk = e % (DS / 4);
+                const uint32_t t = t0 + j;
+                const uint32_t sc = t < T ? lg_div(t, fdG) : 0u, g = t < T ? t - sc * ngroups : 0u;
+                const uint32_t b = min(16 * g + rj, B - 1);
+                hv[u] = e < HF4 ? ld4(hs + (static_cast<size_t>(b) * S + sc) * DS + 4 * kk) : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        };
+        f32x4 hv[HPT];
+        load_h(blockIdx.x * TPI, hv);
+#pragma unroll
+        for (int u = 0; u < WPT; ++u) {
+            const int i4 = u * 256 + static_cast<int>(threadIdx.x);
+            if (i4 >= WF4) continue;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int e = 4 * i4 + c, o = e / (DS + 1), k = e % (DS + 1);
+                if (k < DS) wt[k][o] = wv[u][c];
+                else bf[o] = wv[u][c] + bias[o];  // the constant-1 column's weight + the bias
+            }
         }
-        __syncthreads();
-        const f32x4 bs = ld4(bf + 4 * fg);
-        const int64_t T = S * ngroups;
-        for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * TPI; t0 < T; t0 += static_cast<int64_t>(GS) * TPI) {
-            const int64_t t = t0 + ti;
-            const int64_t sc = t < T ? t / ngroups : 0, grp = t < T ? t - sc * ngroups : 0;
-            const int64_t n = sidx[sc];
-            const bool live = t < T && slot[n] == sc;
-            const int64_t b = 16 * grp + r;
+        for (uint32_t t0 = blockIdx.x * TPI; t0 < T; t0 += static_cast<uint32_t>(GS) * TPI) {
+#pragma unroll
+            for (int u = 0; u < HPT; ++u) {
+                const int e = u * 256 + static_cast<int>(threadIdx.x);
+                if (e < HF4) st4(&hl[0][0][0] + 4 * e, hv[u]);
+            }
+            __syncthreads();
+            if (t0 + static_cast<uint32_t>(GS) * TPI < T) load_h(t0 + static_cast<uint32_t>(GS) * TPI, hv);  // next iteration's rows
+            const uint32_t t = t0 + ti;
+            const uint32_t sc = t < T ? lg_div(t, fdG) : 0u, grp = t < T ? t - sc * ngroups : 0u;
+            const uint32_t n = static_cast<uint32_t>(sidx[sc]);
+            const bool live = t < T && slot[n] == static_cast<int32_t>(sc);
+            const uint32_t b = 16 * grp + r;
             uint32_t nb = 0;
             if (live && b < B) {
-                const float* hrow = hs + (b * S + sc) * DS;
                 f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-                for (int k4 = 0; k4 < DS / 4; ++k4) {
-                    const f32x4 h4 = ld4(hrow + 4 * k4);
+#pragma unroll 8
+                for (int k = 0; k < DS; ++k) {
+                    const float hk = hl[ti][r][k];
+                    const f32x4 w = ld4(&wt[k][4 * fg]);
 #pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const f32x4 w = ld4(&wt[4 * k4 + kk][4 * fg]);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) acc[i] = fmaf(h4[kk], w[i], acc[i]);
-                    }
+                    for (int i = 0; i < 4; ++i) acc[i] = fmaf(hk, w[i], acc[i]);
                 }
-                f32x4 v = acc + bs;
-                const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b * N + n), 4 * fg, thr) : 0xFu;
+                f32x4 v = acc + ld4(bf + 4 * fg);
+                const uint32_t kb =
+                    dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * N + n, 4 * fg, thr) : 0xFu;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     v[i] = ((kb >> i) & 1u) ? fmaxf(v[i], 0.f) * (dropout ? scale : 1.0f) : 0.0f;
                     nb |= static_cast<uint32_t>(v[i] > 0.f) << i;
                 }
-                st4(xs0 + (sc * B + b) * D + 4 * fg, v);
+                st4(xs0 + (static_cast<size_t>(sc) * B + b) * D + 4 * fg, v);
             }
             nib[ti][r][fg] = static_cast<uint8_t>(nb);
             __syncthreads();
             if (threadIdx.x < 64 * TPI) {
                 const int tj = threadIdx.x / 64, l = threadIdx.x % 64, rl = l / LPR, fl = l % LPR;
-                const int64_t tt = t0 + tj;
-                const int64_t sc2 = tt < T ? tt / ngroups : 0, g2 = tt < T ? tt - sc2 * ngroups : 0;
-                const int64_t n2 = sidx[sc2];
-                if (tt < T && slot[n2] == sc2) {
+                const uint32_t tt = t0 + tj;
+                const uint32_t sc2 = tt < T ? lg_div(tt, fdG) : 0u, g2 = tt < T ? tt - sc2 * ngroups : 0u;
+                const uint32_t n2 = static_cast<uint32_t>(sidx[sc2]);
+                if (tt < T && slot[n2] == static_cast<int32_t>(sc2)) {
                     uint32_t w = 0;
 #pragma unroll
                     for (int k = 0; k < K; ++k) w |= static_cast<uint32_t>(nib[tj][RPI * k + rl][fl]) << (4 * k);
-                    bits[(n2 * ngroups + g2) * 64 + l] = static_cast<uint16_t>(w);
+                    bits[(static_cast<size_t>(n2) * ngroups + g2) * 64 + l] = static_cast<uint16_t>(w);
                 }
             }
             __syncthreads();
@@ -249,9 +281,9 @@ k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
         return;
     }
     // non-sensor tiles: one lane of one tile per thread
-    const int64_t t = static_cast<int64_t>(static_cast<int>(blockIdx.x) - GS) * 4 + threadIdx.x / 64;
+    const uint32_t t = (blockIdx.x - static_cast<uint32_t>(GS)) * 4 + threadIdx.x / 64;
     if (t >= N * ngroups) return;
-    const int64_t n = t / ngroups, grp = t - n * ngroups;
+    const uint32_t n = lg_div(t, fdG), grp = t - n * ngroups;
     if (slot[n] >= 0) return;
     const int l = threadIdx.x % 64, rl = l / LPR, fg = l % LPR;
     uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
@@ -263,13 +295,13 @@ k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
     uint32_t w = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const int64_t b = 16 * grp + RPI * k + rl;
+        const uint32_t b = 16 * grp + RPI * k + rl;
         if (b < B) {
-            const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b * N + n), 4 * fg, thr) : 0xFu;
+            const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * N + n, 4 * fg, thr) : 0xFu;
             w |= (kb & pos) << (4 * k);
         }
     }
-    bits[t * 64 + l] = static_cast<uint16_t>(w);
+    bits[static_cast<size_t>(t) * 64 + l] = static_cast<uint16_t>(w);
 }
 
 // x0 materialised from its compressed form (lg_node_init_expand; diagnostics and tests):
@@ -629,12 +661,15 @@ extern "C" int lg_node_init_bits_fwd(const int32_t* sensor_slot, const int64_t* 
     const int64_t tpi = 256 / (16 * (D / 4));
     const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * ngroups, tpi), 2 * lg_num_cus())));
     const unsigned grid = static_cast<unsigned>(GS + ceil_div(N * ngroups, 4));
+    const lg_fastdiv fdG = lg_make_fastdiv(static_cast<uint32_t>(ngroups));
+    const uint32_t B32 = static_cast<uint32_t>(B), N32 = static_cast<uint32_t>(N), S32 = static_cast<uint32_t>(S),
+                   G32 = static_cast<uint32_t>(ngroups);
     if (D == 64)
-        lg_launch(k_node_init_bits<64, 64>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B, N, S,
-                  ngroups, GS, dropout, dropout_p, scale, seed, salt);
+        lg_launch(k_node_init_bits<64, 64>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B32, N32,
+                  S32, G32, fdG, GS, dropout, dropout_p, scale, seed, salt);
     else
-        lg_launch(k_node_init_bits<32, 32>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B, N, S,
-                  ngroups, GS, dropout, dropout_p, scale, seed, salt);
+        lg_launch(k_node_init_bits<32, 32>, grid, 256, 0, s, sensor_slot, sensor_idx, h_s, W, bias, xs0, x0bits, B32, N32,
+                  S32, G32, fdG, GS, dropout, dropout_p, scale, seed, salt);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

@@ -3,9 +3,12 @@ across ranks, one gradient all-reduce per step (RCCL over xGMI with backend
 "nccl"; gloo on CPU for tests).
 
 The reference is single-device; this is the one collective the
-multi-GPU path adds.  The gradient of the 60,418-parameter detector is 241.7 KB:
-a single flat bucket, all-reduced once after backward — at xGMI link rates this
-is a few tens of microseconds, so no bucketing/overlap machinery is warranted.
+multi-GPU path adds.  The gradient of the 60,418-parameter detector is 241.7 KB.
+GradAllReduce here is the EAGER form: one flat bucket, all-reduced once after backward
+(the trainer's eager steps, the bench's kernel-timing pass).  The captured training step
+(models/graph_step.py) splits it in two buckets and overlaps the heads' bucket (33,282
+values, final at the trunk boundary) with the trunk and GRU backward; at ~242 KB the
+exchange is latency-bound, so two buckets beat finer splits.
 Mean-reduction semantics: each rank's loss is the mean over its local windows,
 the all-reduce averages over ranks, so with equal shards the gradient equals the
 single-process gradient of the global batch.

@@ -28,6 +28,7 @@ and replayed: one graph launch per step, the kernels back to back on the device.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -65,7 +66,8 @@ class CapturedTrainStep:
         # every backward below reads its gradients only after backward() returns (set_to_none
         # before each): its slab reductions run as ONE launch at the end of the pass
         from . import library
-        defer0, library.DEFER_REDUCE = library.DEFER_REDUCE, True
+        defer0 = library.DEFER_REDUCE
+        library.DEFER_REDUCE = os.environ.get("LEAKGNN_DEFER_REDUCE", "0") == "1"
         try:
             self._build(model, warmup, preserve_state)
         finally:

@@ -290,7 +290,9 @@ def gru_encoder_backward(dh: Tensor, residual: Tensor, tfeat: Optional[Tensor], 
     dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
     db_ih, db_hh = torch.empty(3 * H, device=dev), torch.empty(3 * H, device=dev)
     ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I, H)), device=dev, dtype=torch.uint8)
-    with _reduce_batch(lib, stream_of(residual), keep=[ws]), _timed("gru_bwd", dev):
+    # keep: the slab and every reduction target (a target autograd drops must not be freed
+    # before a deferred flush writes it)
+    with _reduce_batch(lib, stream_of(residual), keep=[ws, dw_ih, dw_hh, db_ih, db_hh]), _timed("gru_bwd", dev):
         check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates), ptr(dh),
                              ptr(dx) if need_dx else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L, S, I,
                              H, ptr(ws), ws.numel(), stream_of(residual)), "lg_gru_bwd")
@@ -528,11 +530,13 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: T
     dWs: List[Tensor] = [grad_out] * L
     dbs: List[Tensor] = [grad_out] * L
     dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
-    with _reduce_batch(lib, st, keep=wss):
+    keep: List[Tensor] = []  # slabs and reduction targets, alive until a deferred flush
+    with _reduce_batch(lib, st, keep=keep):
         dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx,
                                                   nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
                                                   node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st,
                                                   (x0bits, x0_bias, pos_slot_t) if x0bits is not None else None, p)
+        keep += wss + dWs + dbs + [dbias_ns, dWp, dbp]
     return dh_s, dWp, dbp, dWs, dbs
 
 
@@ -711,7 +715,9 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
     wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
     dh = torch.empty_like(h)
-    with _reduce_batch(lib, st, keep=[ws, wsn]):  # the EdgeHead's and the NoLeakHead's weight-grad reductions in one launch
+    # one launch for the EdgeHead's and the NoLeakHead's weight-grad reductions; keep: the slabs
+    # and every reduction target (alive until a deferred flush)
+    with _reduce_batch(lib, st, keep=[ws, wsn, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2]):
         _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N,
                                  D, hidden, nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2, db2, ndw1,
                                  ndb1, ndw2, ndb2, ws, wsn, st)

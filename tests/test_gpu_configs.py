@@ -1,9 +1,10 @@
 """GPU parity at the BASELINE.json configs the round-1 suite did not cover (SURVEY §8 d):
 
   configs[4] / C5  synthetic 100k nodes / 300k edge columns, D = 64, one graph, fwd + bwd:
-                   GCNConv (window-major kernels) vs the CPU oracle, the node-major trunk
-                   kernels vs the window-major ones at the same size, and one full
-                   LeakDetector (S = 29, P = 150,000) forward + backward vs the oracle;
+                   GCNConv (the single-graph row-tile kernels lg_gcn_{fwd,bwd}_rows, and the
+                   window-major ones at D = 32) vs the fp64 oracle, the node-major trunk
+                   kernels vs the oracle directly, and one full LeakDetector (S = 29,
+                   P = 150,000) forward + backward vs the oracle;
   configs[2]       L-TOWN-A detector at its own batch, B = 256, vs the CPU oracle in eval
                    mode, and in train mode with every dropout mask regenerated on the host
                    by oracle/dropout_ref.py and fed to a CPU replay of the oracle;

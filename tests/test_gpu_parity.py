@@ -418,11 +418,12 @@ def test_gcn_node_major_matches_window_major(B, D, drop):
     ys = run(0)
     err = (ys.double() - yn.double()).abs().max().item()
     assert err <= 1e-6 * scale, f"default transform off by {err:.3e} (scale {scale:.3e})"
-    # the 3-way bf16 split: the same bits in both pipelines, within 1e-7 of the scale of exact fp32
+    # the 3-way bf16 split: the same bits in both pipelines, fp32-level accuracy (1e-6 of the scale:
+    # the MFMA's K order differs from the exact-fp32 reference's)
     y3 = run(ops.nat.LG_F_BF16X3)
     assert torch.equal(run(ops.nat.LG_F_NM3), y3), "pc and nm3 3-way split transforms must agree bit for bit"
     err3 = (y3.double() - yn.double()).abs().max().item()
-    assert err3 <= 1e-7 * scale, f"3-way split off by {err3:.3e} (scale {scale:.3e})"
+    assert err3 <= 1e-6 * scale, f"3-way split off by {err3:.3e} (scale {scale:.3e})"
     # backward with both masks and the node-bias sum
     slot = torch.full((N,), -1, dtype=torch.int32)
     slot[torch.randperm(N, generator=gen)[:29]] = torch.arange(29, dtype=torch.int32)

@@ -281,6 +281,40 @@ def main():
                                                     cs()), "node_init")
         t = timeit(f, args.iters)
         res["node_init"] = {"us": t, "GBps": 4 * B * N * D / t / 1e3}
+    if any(k in which for k in ("node_init_bits", "gcn_fwd_x0", "gcn_bwd_x0")):  # the compressed node init path
+        S5 = 29
+        slot = torch.full((N,), -1, dtype=torch.int32, device=dev)
+        slot[:S5] = torch.arange(S5, dtype=torch.int32, device=dev)
+        sidx = torch.arange(S5, dtype=torch.int64, device=dev)
+        hs = torch.randn(B, S5, D, device=dev)
+        Wp = torch.randn(D, D + 1, device=dev) / 8
+        xs0 = torch.empty(S5, B, D, device=dev)
+        nbits = N * ((B + 15) // 16) * 64
+        x0b = torch.empty(nbits, device=dev, dtype=torch.int16)
+        for nm_, S_, sl_ in (("node_init_bits", S5, slot), ("node_init_bits_s0", 0, torch.full_like(slot, -1))):
+            f = lambda S_=S_, sl_=sl_: check(lib.lg_node_init_bits_fwd(ptr(sl_), ptr(sidx), ptr(hs), ptr(Wp), ptr(bias),
+                                                                       ptr(xs0), ptr(x0b), B, N, S_, D, D, nat.LG_F_DROPOUT,
+                                                                       0.1, 123, 0, cs()), nm_)
+            t = timeit(f, args.iters)
+            res[nm_] = {"us": t, "GBps": (nbits * 2 + 4 * S_ * B * D) / t / 1e3}
+        f()
+        mk = ops.SensorMarks.build(graph, slot)
+        fx = lambda: check(lib.lg_gcn_fwd_nm_x0(ptr(mk.nodetab_s), ptr(mk.pairs_s), ptr(xs0), ptr(x0b), ptr(bias), ptr(W),
+                                                ptr(bias), ptr(y), B, N, S5, D, nat.LG_F_BIAS | nat.LG_F_RELU |
+                                                nat.LG_F_DROPOUT, 0.1, 123, 1, cs()), "fwd x0")
+        t = timeit(fx, args.iters)
+        res["gcn_fwd_x0"] = {"us": t, "GBps": (4 * B * N * D + nbits * 2 + 4 * S5 * B * D) / t / 1e3}
+        dy = torch.randn_like(x)
+        dx = torch.empty_like(x)
+        dW, db, dnb = torch.empty(D, D, device=dev), torch.empty(D, device=dev), torch.empty(D, device=dev)
+        ws = torch.empty(int(lib.lg_gcn_bwd_nm_workspace_bytes(D)), device=dev, dtype=torch.uint8)
+        fb = lambda: check(lib.lg_gcn_bwd_nm_x0(ptr(graph.nodetab_t), ptr(graph.pairs_t), ptr(mk.pos_slot_t), ptr(dy),
+                                                ptr(xs0), ptr(x0b), ptr(bias), ptr(W), ptr(dx), ptr(dW), ptr(db),
+                                                ptr(slot), ptr(dnb), B, N, S5, D,
+                                                nat.LG_F_MASK_OUT | nat.LG_F_DX_SENSOR_ROWS | nat.LG_F_DROPOUT, 0.1,
+                                                1.0 / 0.9, ptr(ws), ws.numel(), cs()), "bwd x0")
+        t = timeit(fb, args.iters)
+        res["gcn_bwd_x0"] = {"us": t, "GBps": (4 * B * N * D) / t / 1e3}
     if "c5_fwd" in which or "c5_bwd" in which or "c5_fwd_wm" in which:  # BASELINE configs[4]: one 100k-node graph, B = 1, GCNConv's launches
         from models.synth import synthetic_pipe_graph
         ei5, _ = synthetic_pipe_graph(100_000, 150_000, seed=0)
