@@ -179,7 +179,7 @@ def pmc_traffic(which: str, kname: str, batch: int) -> dict | None:
 
 def short_kernel_name(name: str) -> str:
     """k_gcn_fwd_pc<64, true, ...>(...) -> k_gcn_fwd_pc; (anonymous namespace)::k_ce_fwd(...) -> k_ce_fwd"""
-    n = name.split("(anonymous namespace)::")[-1]
+    n = name.replace("(anonymous namespace)::", "")  # also inside the argument list
     return n.split("<")[0].split("(")[0].strip().split(" ")[-1]
 
 

@@ -468,8 +468,11 @@ int lg_pipe_scatter_bwd(const int32_t* inc_rowptr, const int32_t* inc_item, cons
  * pipe columns of detector.py:216's (B, P+1) output in place).  hidden must be 128;
  * D in {32, 64}.  Dropout as lg_gcn_fwd, index (b*P + p)*hidden + unit.
  * hid: NULL, or fp32 [B*P][hidden] receiving the post-dropout hidden layer (what
- * lg_edge_head_bwd needs; pass it in training).  The products run on bf16 MFMA with
- * 3-way split fp32 operands (fp32-level accuracy, not bit-identical to an fp32 GEMM). */
+ * lg_edge_head_bwd needs; pass it in training).  The products run on f16 MFMA with
+ * 2-way split, power-of-two-scaled fp32 operands (D = 64, fp32 tier; W1 scaled per wave,
+ * the features per pipe row, dropped term <= 2^-22 of each product) or, with
+ * LG_F_BF16X3 and at D = 32, on bf16 MFMA with 3-way split operands: fp32-level
+ * accuracy either way, not bit-identical to an fp32 GEMM.  LG_F_BF16: bf16 hi parts only. */
 int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const float* b1,
                      const float* w2, const float* b2, float* logits, int64_t ldo, float* hid,
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
@@ -485,20 +488,43 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
                      int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                      int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 /* lg_edge_head_bwd followed by lg_pipe_scatter_bwd (dh = dpool / N + the incidence sums of
- * dpipe; reference detector.py:206-211 and the backward of its gather), with the scatter
- * FUSED into the backward kernel: each workgroup owns whole windows and sums a window's node
- * rows right after its pipe rows (read back from L2 / the Infinity Cache instead of a second
- * launch over HBM), the incidence CSR staged in LDS.  Same results as the two calls (the same
- * sums in the same order); when the CSR does not fit in LDS (N + 1 + 2P words beside the
- * kernel's images) it runs the two calls.  dpipe is still written (scratch, [B][P][2][D]);
- * dpool: NULL or [B][D] (lg_pool_head_bwd's dpooled, computed before this call); the workspace
- * is lg_edge_head_bwd_workspace_bytes.  ABI 19. */
+ * dpipe; reference detector.py:206-211 and the backward of its gather), fused into the
+ * backward kernel.  With a pipe schedule (sched: device copy of lg_pipe_schedule_build's
+ * buffer, sched_hdr: its first 16 words in HOST memory; ABI 22) the node sums are STREAMED:
+ * pipes are visited in the schedule's order, each tile's per-pipe rows stay in LDS and are
+ * added to the running sums of the nodes they touch (LDS slots for the nodes still open, the
+ * dh row at a node's last tile) — dpipe is neither written nor read.  The sums are those of
+ * lg_pipe_scatter_bwd over the schedule's incidence CSR (inc_rowptr / inc_item from the same
+ * build), bit for bit.  Without a schedule (NULL, NULL), or when the open sums do not fit in
+ * LDS, each workgroup owns whole windows and sums a window's node rows from its just-written
+ * dpipe rows (ABI 19; the CSR staged in LDS), or, when the CSR does not fit either, the two
+ * calls run.  dpipe: scratch [B][P][2][D] (untouched by the streamed path); dpool: NULL or
+ * [B][D] (lg_pool_head_bwd's dpooled, computed before this call); the workspace is
+ * lg_edge_head_bwd_workspace_bytes.  A schedule for another (P, N, D) is LG_EINVAL. */
 int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
                              const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
                              float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
-                             const int32_t* inc_item, const float* dpool, float* dh,
+                             const int32_t* inc_item, const int32_t* sched, const int32_t* sched_hdr,
+                             const float* dpool, float* dh,
                              int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                              int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream);
+
+/* Pipe schedule of the streamed EdgeHead backward (ABI 22), once per model; HOST memory in and
+ * out (upload sched to the device; keep its first 16 words on the host as sched_hdr).
+ *   ends : int64 [P][2];  D : 32 or 64 (the tile height 2048 / D);
+ *   sched : int32 [words] with words >= lg_pipe_schedule_words(P, N, D);
+ *   inc_rowptr [N+1], inc_item [2P]: the incidence CSR (as lg_incidence_build) with each node's
+ *     items in SCHEDULE order instead of ascending — pass it to lg_pipe_scatter_bwd /
+ *     lg_edge_head_bwd_scatter with this schedule, so every path sums in one order.
+ * Pipes are ordered by their endpoints' positions in lg_rcm_order of the pipe graph (the later
+ * one first, then the earlier, then the id); a node is "open" from its first tile to its last.
+ * Header words: version, P, N, D, TR, tiles, open slots, max events per tile, block words,
+ * nodes without pipes, the three section offsets, total words.  Deterministic.
+ * LG_EUNSUPPORTED when N >= 2^24. */
+#define LG_PIPE_SCHED_VERSION 1
+int64_t lg_pipe_schedule_words(int64_t P, int64_t N, int64_t D);
+int lg_pipe_schedule_build(const int64_t* ends, int64_t P, int64_t N, int64_t D, int32_t* sched, int64_t words,
+                           int32_t* inc_rowptr, int32_t* inc_item);
 
 /* K10 forward: per-window mean over the N node rows.
  * Replaces: global_mean_pool(x, batch) with batch = arange(B).repeat_interleave(N)

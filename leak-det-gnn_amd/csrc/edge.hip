@@ -28,6 +28,8 @@
 // dpipe is then summed per node over the incidence CSR by lg_pipe_scatter_bwd
 // (deterministic, no atomics).  Weight grads: per-workgroup slabs + fixed-order reduce.
 #include <algorithm>
+#include <tuple>
+#include <vector>
 #include "common.h"
 #include "reduce.h"
 #include "split_bf16.h"
@@ -59,7 +61,7 @@ struct EG {
     // forward workgroups resident per CU (VGPR-bound: 144 VGPRs of split W1 at D=64; the
     // bf16 tier keeps only the hi part, 48 VGPRs, and fits two)
     static constexpr int FWD_WG_PER_CU = 1, FWD_WG_PER_CU_BF = 2;
-    static constexpr int64_t FWD_LDS = int64_t{2} * 2 * 3 * FPL + 4 * (2 * 4 * TR + 2 * HID);  // images, partials, b1/W2
+    static constexpr int64_t FWD_LDS = int64_t{2} * 2 * 3 * FPL + 4 * (2 * 4 * TR + 2 * HID + 2 * TR);  // images, partials, b1/W2, row scales
     static constexpr int64_t BWD_LDS = int64_t{2} * (3 * FTPL + 3 * GPL) + 2 * TR * D + 16 * 64 * NRED;
 };
 static_assert(EG<64>::RBW == 2 && EG<32>::RBW == 2, "dfeat wave split");
@@ -110,9 +112,35 @@ __device__ __forceinline__ void st_split4(uint16_t* img, int pl, int off, const 
     *reinterpret_cast<lg_u32x2*>(img + 2 * pl + off) = c;
 }
 
-template <int D, bool BF>
+// 2-way fp16 split of 4 floats scaled by 2^e into 8-byte slots at img[off], img[pl + off]
+__device__ __forceinline__ void st_split2h(uint16_t* img, int pl, int off, const f32x4& x, float sc) {
+    uint32_t a0, a1, b0, b1;
+    split2_f16_pair(x[0] * sc, x[1] * sc, a0, a1);
+    split2_f16_pair(x[2] * sc, x[3] * sc, b0, b1);
+    *reinterpret_cast<lg_u32x2*>(img + off) = lg_u32x2{a0, b0};
+    *reinterpret_cast<lg_u32x2*>(img + pl + off) = lg_u32x2{a1, b1};
+}
+__device__ __forceinline__ f32x4 mfma_f16x2(const lg_f16x8 (&a)[2], const lg_f16x8 (&b)[2], f32x4 c) {
+    c = mfma_h(a[1], b[0], c);  // smallest terms first
+    c = mfma_h(a[0], b[1], c);
+    return mfma_h(a[0], b[0], c);
+}
+// max of a non-negative float's bits over the 16 lanes of a DPP row (row_ror within the row)
+__device__ __forceinline__ uint32_t lg_row16_max_bits(uint32_t m) {
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0xB1, 0xF, 0xF, false)));
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x4E, 0xF, 0xF, false)));
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x124, 0xF, 0xF, false)));
+    return max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x128, 0xF, 0xF, false)));
+}
+
+// F16 (fp32 tier, D = 64): the MLP's products on the 2-way fp16 split (split_bf16.h f16x2: 3 f16
+// MFMAs per product instead of 6 bf16 ones, dropped term <= 2^-22 of the product).  Scales
+// are uniform along K as the MFMA needs: W1 per wave (its own rows), the features per pipe
+// row (the B operand's columns; the row's 16 gather lanes take the max through DPP), so
+// hid = acc 2^-(sW + s_row) + b1 exactly unscaled.
+template <int D, bool BF, bool F16 = false>
 __global__ void __launch_bounds__(NT)
-__attribute__((amdgpu_waves_per_eu((BF ? EG<D>::FWD_WG_PER_CU_BF : EG<D>::FWD_WG_PER_CU) * 2, 4)))
+__attribute__((amdgpu_waves_per_eu((BF ? EG<D>::FWD_WG_PER_CU_BF : EG<D>::FWD_WG_PER_CU) * 2, F16 ? 2 : 4)))
 k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
            float* __restrict__ logit, int64_t ldo, float* __restrict__ hid_out, uint32_t sb, uint32_t sn,
@@ -135,17 +163,44 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     // from LDS feeds two MFMA chains) x row blocks [RBF rh, RBF rh + RBF)
     const int nh = w & 3, rh = w >> 2;
     // A operand: W1[n = 32 nh + 16 i + c][k = 32 ks + 8q + j], split once
+    static_assert(!F16 || (!BF && D == 64), "f16x2: fp32 tier, D = 64");
     lg_bf16x8 wa[2][G::KS][3];
+    lg_f16x8 wh[2][G::KS][F16 ? 2 : 1];
+    int sw = 0;  // F16: the wave's W1 scale exponent
+    if constexpr (F16) {
+        f32x4 wr[2][G::KS][2];
+        uint32_t m = 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-            const float* src = W1 + (32 * nh + 16 * i + c) * G::K3 + 32 * ks + 8 * q;
-            split3_x8(ld4(src), ld4(src + 4), wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
-        }
+            for (int ks = 0; ks < G::KS; ++ks) {
+                const float* src = W1 + (32 * nh + 16 * i + c) * G::K3 + 32 * ks + 8 * q;
+                wr[i][ks][0] = ld4(src);
+                wr[i][ks][1] = ld4(src + 4);
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) m = max(m, __float_as_uint(fabsf(wr[i][ks][h2][e])));
+            }
+        sw = lg_f16_scale_exp_c(lg_wave_max_bits(m));
+        const float sc = lg_pow2f(sw);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int ks = 0; ks < G::KS; ++ks) split2_f16_x8(wr[i][ks][0] * sc, wr[i][ks][1] * sc, wh[i][ks][0], wh[i][ks][1]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int ks = 0; ks < G::KS; ++ks) {
+                const float* src = W1 + (32 * nh + 16 * i + c) * G::K3 + 32 * ks + 8 * q;
+                split3_x8(ld4(src), ld4(src + 4), wa[i][ks][0], wa[i][ks][1], wa[i][ks][2]);
+            }
+    }
     // b1 / W2 of hidden units n = 32 nh + 16 i + 4q + reg (the accumulator rows) are re-read
     // from LDS per tile (VGPR budget)
     float* bw = reinterpret_cast<float*>(part + 2);  // [2][HID]: b1, W2
+    int* rsc = reinterpret_cast<int*>(bw + 2 * HID);  // F16: [2][TR] feature-row scale exponents
     if (threadIdx.x < HID) {
         bw[threadIdx.x] = b1[threadIdx.x];
         bw[HID + threadIdx.x] = W2[threadIdx.x];
@@ -162,8 +217,30 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     uint32_t nu, nv, nua, nva, nub = 0, nvb = 0;
     f32x4 pu0, pv0, pu1, pv1;
     auto rowof = [&](int64_t t) { return t * G::TR + arow; };
+    int srow = 0;  // F16: the row scale of the tile being staged (set by its first third)
     auto stage = [&](uint16_t* img, int part3, const f32x4& pu, const f32x4& pv) {  // a third of the slot
         if (lab & 4) return;
+        if constexpr (F16) {
+            if (part3 == 0) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    m = max(m, max(__float_as_uint(fabsf(pu[i])),
+                                   max(__float_as_uint(fabsf(pv[i])), __float_as_uint(fabsf(pu[i] - pv[i])))));
+                srow = lg_f16_scale_exp_c(lg_row16_max_bits(m));
+                if (af == 0) rsc[(img == fimg ? 0 : 1) * G::TR + arow] = srow;
+            }
+            const float sc = lg_pow2f(srow);
+            if (part3 == 0) st_split2h(img, G::FPL, arow * G::FSB + 4 * af, pu, sc);
+            if (part3 == 1) st_split2h(img, G::FPL, arow * G::FSB + D + 4 * af, pv, sc);
+            if (part3 == 2) {
+                f32x4 a;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = fabsf(pu[i] - pv[i]);
+                st_split2h(img, G::FPL, arow * G::FSB + 2 * D + 4 * af, a, sc);
+            }
+            return;
+        }
         if (part3 == 0) st_split4<BF>(img, G::FPL, arow * G::FSB + 4 * af, pu);
         if (part3 == 1) st_split4<BF>(img, G::FPL, arow * G::FSB + D + 4 * af, pv);
         if (part3 == 2) {
@@ -197,6 +274,10 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         f32x4 acc[RBF][2];
 #pragma unroll
         for (int rb = 0; rb < RBF; ++rb) {
+            if constexpr (F16) {  // bias after the unscale
+                acc[rb][0] = acc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                continue;
+            }
             acc[rb][0] = ld4(bw + 32 * nh + 4 * q);
             acc[rb][1] = ld4(bw + 32 * nh + 16 + 4 * q);
         }
@@ -205,13 +286,20 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 #pragma unroll
             for (int rb = 0; rb < RBF; ++rb) {
                 const uint16_t* src = cur + (16 * (RBF * rh + rb) + c) * G::FSB + 32 * ks + 8 * q;
-                const lg_bf16x8 bf[3] = {lds_frag_row(src), lds_frag_row(src + G::FPL), lds_frag_row(src + 2 * G::FPL)};
-                if (lab & 1) {
-                    acc[rb][0][0] += bf[0][0];
-                    continue;
+                if constexpr (F16) {
+                    const lg_f16x8 bh[2] = {__builtin_bit_cast(lg_f16x8, lds_frag_row(src)),
+                                            __builtin_bit_cast(lg_f16x8, lds_frag_row(src + G::FPL))};
+                    acc[rb][0] = mfma_f16x2(wh[0][ks], bh, acc[rb][0]);
+                    acc[rb][1] = mfma_f16x2(wh[1][ks], bh, acc[rb][1]);
+                } else {
+                    const lg_bf16x8 bf[3] = {lds_frag_row(src), lds_frag_row(src + G::FPL), lds_frag_row(src + 2 * G::FPL)};
+                    if (lab & 1) {
+                        acc[rb][0][0] += bf[0][0];
+                        continue;
+                    }
+                    acc[rb][0] = mfma_prec<BF>(wa[0][ks], bf, acc[rb][0]);
+                    acc[rb][1] = mfma_prec<BF>(wa[1][ks], bf, acc[rb][1]);
                 }
-                acc[rb][0] = mfma_prec<BF>(wa[0][ks], bf, acc[rb][0]);
-                acc[rb][1] = mfma_prec<BF>(wa[1][ks], bf, acc[rb][1]);
             }
             // the next tile's split, spread over the MFMA stream
             if (ks * 3 / G::KS != (ks + 1) * 3 / G::KS) stage(nxt, ks * 3 / G::KS, pu, pv);
@@ -224,6 +312,15 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         for (int rb = 0; rb < RBF; ++rb) {
             const int row = 16 * (RBF * rh + rb) + c;
             const int64_t r = row0 + row;
+            if constexpr (F16) {  // unscale (exact) and the bias in one rounding
+                const float us = lg_pow2f(-(sw + rsc[buf * G::TR + row]));
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const f32x4 bv = ld4(bw + 32 * nh + 16 * i + 4 * q);
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) acc[rb][i][reg] = fmaf(acc[rb][i][reg], us, bv[reg]);
+                }
+            }
             // row-stream dropout (oracle/dropout_ref.py edge_stream_mask): one stream per
             // (row, 4 nh + q), one xorshift step per pair of this lane's 8 units
             uint32_t st = dropout ? lg_row_stream_seed(key, static_cast<uint64_t>(r), 4 * nh + q) : 0u;
@@ -282,6 +379,12 @@ struct EdgeScatter {
     uint32_t N, P, B;
     int nm;   // dh node-major ([N][B][D]) or window-major
     int tpw;  // tiles per window
+    // STREAM (the pipe schedule of lg_pipe_schedule_build): pipe rows in schedule order, a
+    // block of scatter events per tile, the nodes without pipes
+    const int4* spipe;       // [P] {u, v, p, 0} in schedule order
+    const uint32_t* sblk;    // [tpw][bw] {count, 0, events [maxev][2], incidence bytes [2 TR]}
+    const int32_t* szero;    // [nzero]
+    int nzero, nslots, bw, maxev;
 };
 
 // dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
@@ -340,14 +443,59 @@ __device__ __forceinline__ void edge_scatter_window(const EdgeScatter& sc, const
     }
 }
 
+// STREAM: the node gradients summed tile by tile (lg_pipe_schedule_build).  Pipes are visited
+// in a bandwidth-reducing order, so a node's incidences fall in a few consecutive tiles; after
+// a tile's dfeat rows are in LDS (they never go to HBM), each node it touches adds them to its
+// running sum — a slot of LDS between its first and last tile, the HBM row at its last tile.
+// The running sum starts from dpool / N and adds the incidences in schedule order: the order
+// of the schedule's incidence CSR, so the sums are those of lg_pipe_scatter_bwd over it.
+// Event word 0: node | first << 24 | last << 25; word 1: slot | start << 16 | count << 24.
+template <int D>
+__device__ __forceinline__ void edge_stream_scatter(const EdgeScatter& sc, const uint32_t* eb, const float* dpl,
+                                                    float* lacc, const f32x4& g0, uint32_t win, int DPS) {
+    constexpr int LPR = D / 4, SLOTS = NT / LPR;
+    const int sr = threadIdx.x / LPR, sf = threadIdx.x % LPR;
+    const int ne = static_cast<int>(eb[0]);
+    const uint8_t* incl = reinterpret_cast<const uint8_t*>(eb + 2 + 2 * sc.maxev);
+    for (int e = sr; e < ne; e += SLOTS) {
+        const uint32_t w0 = eb[2 + 2 * e], w1 = eb[3 + 2 * e];
+        const uint32_t node = w0 & 0xFFFFFFu, slot = w1 & 0xFFFFu, st = (w1 >> 16) & 0xFFu, cnt = w1 >> 24;
+        f32x4 acc = (w0 >> 24) & 1u ? g0 : ld4(lacc + slot * D + 4 * sf);
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const uint32_t b = incl[st + i];  // 2 row + role
+            acc += ld4(dpl + (b >> 1) * DPS + (b & 1u) * D + 4 * sf);
+        }
+        if ((w0 >> 25) & 1u) {
+            const int64_t row = sc.nm ? static_cast<int64_t>(node) * sc.B + win : static_cast<int64_t>(win) * sc.N + node;
+            st4(sc.dh + row * D + 4 * sf, acc);
+        } else {
+            st4(lacc + slot * D + 4 * sf, acc);
+        }
+    }
+}
+// the window's nodes without pipes: dh = dpool / N
+template <int D>
+__device__ __forceinline__ void edge_stream_zero(const EdgeScatter& sc, const f32x4& g0, uint32_t win) {
+    constexpr int LPR = D / 4, SLOTS = NT / LPR;
+    const int sr = threadIdx.x / LPR, sf = threadIdx.x % LPR;
+    for (int i = sr; i < sc.nzero; i += SLOTS) {
+        const uint32_t node = static_cast<uint32_t>(sc.szero[i]);
+        const int64_t row = sc.nm ? static_cast<int64_t>(node) * sc.B + win : static_cast<int64_t>(win) * sc.N + node;
+        st4(sc.dh + row * D + 4 * sf, g0);
+    }
+}
+
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
-template <int D, bool BF, bool SCAT = false>
+// MODE 0: dpipe rows only; 1 (SCAT): + each window's node sums from its dpipe rows; 2
+// (STREAM): the node sums streamed per tile, no dpipe rows
+template <int D, bool BF, int MODE = 0>
 __global__ void __launch_bounds__(NT)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ W2, const float* __restrict__ hid, const float* __restrict__ dlogit, int64_t ldo,
            float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, uint32_t sb,
            uint32_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, float dscale, EdgeScatter sc) {
     using G = EG<D>;
+    constexpr bool SCAT = MODE == 1, STREAM = MODE == 2, WIN = MODE != 0;  // WIN: workgroups own windows
     constexpr int SL = HID * G::K3 + 2 * HID + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);     // [3][TR][FTB]  feat parts
@@ -389,24 +537,65 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     // (SCAT) tile k % tpw of window blockIdx.x + (k / tpw) gridDim.x; rows [rbase, rlim) count
     const int64_t gstep = gridDim.x;
     auto rbase = [&](int64_t k) -> int64_t {
-        if constexpr (SCAT) return (blockIdx.x + (k / sc.tpw) * gstep) * sc.P + (k % sc.tpw) * G::TR;
+        if constexpr (WIN) return (blockIdx.x + (k / sc.tpw) * gstep) * sc.P + (k % sc.tpw) * G::TR;
         return (blockIdx.x + k * gstep) * G::TR;
     };
     auto rlim = [&](int64_t k) -> int64_t {
-        if constexpr (SCAT) return std::min<int64_t>(BP, (blockIdx.x + (k / sc.tpw) * gstep + 1) * sc.P);
+        if constexpr (WIN) return std::min<int64_t>(BP, (blockIdx.x + (k / sc.tpw) * gstep + 1) * sc.P);
         return BP;
     };
-    const int64_t nk = SCAT ? (blockIdx.x < sc.B ? sc.tpw * ((sc.B - blockIdx.x + gstep - 1) / gstep) : 0)
+    const int64_t nk = WIN ? (blockIdx.x < sc.B ? sc.tpw * ((sc.B - blockIdx.x + gstep - 1) / gstep) : 0)
                             : (blockIdx.x < ntiles ? (ntiles - blockIdx.x + gstep - 1) / gstep : 0);
     uint32_t nu, nv;
     f32x4 pu, pv, hp[G::HPT];
     float dl[G::HPT];
-    auto load_hid = [&](int64_t rb) {  // raw (see load_ends); a row past the end is zeroed at use
+    // STREAM: rows are schedule slots; row off of tile k -> (window, slot), (0, 0) past the window
+    const uint32_t* spw = reinterpret_cast<const uint32_t*>(sc.spipe);
+    auto sslot = [&](int64_t k, int off, uint32_t& b, uint32_t& slot) {
+        const int64_t r = rbase(k) + off;
+        const bool ok = r < rlim(k);
+        b = ok ? static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep) : 0u;
+        slot = ok ? static_cast<uint32_t>(r - static_cast<int64_t>(b) * sc.P) : 0u;
+    };
+    uint32_t hpipe[G::HPT];  // STREAM: pipe ids of the hidden-slot rows, a tile ahead of their loads
+    auto load_ids = [&](int64_t k) {
+        if constexpr (STREAM) {
+            uint32_t b, slot;
+            sslot(k, arow, b, slot);
+            nu = spw[4 * slot];
+            nv = spw[4 * slot + 1];
+#pragma unroll
+            for (int i = 0; i < G::HPT; ++i) {
+                sslot(k, hrow + 16 * i, b, slot);
+                hpipe[i] = spw[4 * slot + 2];
+            }
+        } else {
+            load_ends(ends, rbase(k) + arow, BP, fdP, nu, nv);
+        }
+    };
+    auto load_feat = [&](int64_t k) {
+        if constexpr (STREAM) {
+            uint32_t b, slot;
+            sslot(k, arow, b, slot);
+            pu = ld4(h + ((b * sb + nu * sn) * D + 4 * af));
+            pv = ld4(h + ((b * sb + nv * sn) * D + 4 * af));
+        } else {
+            load_rows<D>(h, rbase(k) + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
+        }
+    };
+    auto load_hid = [&](int64_t k) {  // raw (see load_ends); a row past the end is zeroed at use
 #pragma unroll
         for (int i = 0; i < G::HPT; ++i) {
-            const uint32_t r = clamp_row(rb + hrow + 16 * i, BP);
-            hp[i] = ld4(hid + (r * HID + 4 * n4));
-            dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
+            if constexpr (STREAM) {
+                uint32_t b, slot;
+                sslot(k, hrow + 16 * i, b, slot);
+                hp[i] = ld4(hid + ((b * sc.P + hpipe[i]) * HID + 4 * n4));
+                dl[i] = dlogit[static_cast<int64_t>(b) * ldo + hpipe[i]];
+            } else {
+                const uint32_t r = clamp_row(rbase(k) + hrow + 16 * i, BP);
+                hp[i] = ld4(hid + (r * HID + 4 * n4));
+                dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
+            }
         }
     };
     // SCAT: the incidence CSR in LDS (after the kernel's images), staged before the first barrier
@@ -415,10 +604,47 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         for (uint32_t i = threadIdx.x; i <= sc.N; i += NT) icsr[i] = sc.inc_rowptr[i];
         for (uint32_t i = threadIdx.x; i < 2 * sc.P; i += NT) icsr[sc.N + 1 + i] = sc.inc_item[i];
     }
-    load_ends(ends, rbase(0) + arow, BP, fdP, nu, nv);
-    load_rows<D>(h, rbase(0) + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
-    load_hid(rbase(0));
-    load_ends(ends, rbase(1) + arow, BP, fdP, nu, nv);
+    // STREAM: after the images, the tile's dfeat rows [TR][DPS] (du | dv), the event blocks of
+    // two tiles, the open nodes' running sums [nslots][D]
+    constexpr int DPS = 2 * D + 4;  // row stride: the finishing waves' 16-row stores conflict-free
+    float* dpl = reinterpret_cast<float*>(smem + G::BWD_LDS);
+    uint32_t* evb = reinterpret_cast<uint32_t*>(dpl + G::TR * DPS);
+    float* lacc = reinterpret_cast<float*>(evb + 2 * sc.bw);
+    const int sf = threadIdx.x % (D / 4);
+    const float fN = static_cast<float>(sc.N);
+    const float* gsrc = sc.dpool ? sc.dpool : h;  // h: any readable row when there is no pool gradient
+    f32x4 graw = f32x4{0.f, 0.f, 0.f, 0.f};  // raw dpool row of the window of the tile scattered next
+    uint2 evn = uint2{0u, 0u};  // the next tile's event block, a uint2 per thread
+    auto load_evblock = [&](int64_t k) {
+        const int t = min(static_cast<int>(threadIdx.x), sc.bw / 2 - 1);
+        evn = reinterpret_cast<const uint2*>(sc.sblk + (k % sc.tpw) * sc.bw)[t];
+    };
+    auto store_evblock = [&](int64_t k) {
+        if (static_cast<int>(threadIdx.x) < sc.bw / 2) reinterpret_cast<uint2*>(evb + (k & 1) * sc.bw)[threadIdx.x] = evn;
+    };
+    auto scatter_tile = [&](int64_t kk) {
+        const uint32_t win = static_cast<uint32_t>(blockIdx.x + (kk / sc.tpw) * gstep);
+        f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (sc.dpool) {
+#pragma unroll
+            for (int c2 = 0; c2 < 4; ++c2) g0[c2] = graw[c2] / fN;
+        }
+        edge_stream_scatter<D>(sc, evb + (kk & 1) * sc.bw, dpl, lacc, g0, win, DPS);
+        if (sc.nzero > 0 && kk % sc.tpw == sc.tpw - 1) edge_stream_zero<D>(sc, g0, win);
+    };
+    auto load_graw = [&](int64_t k) {
+        const uint32_t win = static_cast<uint32_t>(min<int64_t>(blockIdx.x + (k / sc.tpw) * gstep, sc.B - 1));
+        graw = ld4(gsrc + (sc.dpool ? static_cast<int64_t>(win) * D : 0) + 4 * sf);
+    };
+    load_ids(0);
+    load_feat(0);
+    load_hid(0);
+    load_ids(1);
+    if constexpr (STREAM) {
+        load_evblock(0);
+        store_evblock(0);
+        load_graw(0);
+    }
     int buf = 0;
     for (int64_t k = 0; k < nk; ++k, buf ^= 1) {
         const int64_t row0 = rbase(k), rend = rlim(k);
@@ -451,9 +677,14 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
         }
         __syncthreads();
-        load_rows<D>(h, rbase(k + 1) + arow, BP, fdP, nu, nv, sb, sn, af, pu, pv);
-        load_hid(rbase(k + 1));
-        load_ends(ends, rbase(k + 2) + arow, BP, fdP, nu, nv);
+        load_feat(k + 1);
+        load_hid(k + 1);
+        load_ids(k + 2);
+        if constexpr (STREAM) {
+            load_evblock(k + 1);
+            if (k > 0) scatter_tile(k - 1);  // the previous tile's node sums
+            load_graw(k);                     // for this tile's, at the next one
+        }
 
         // dW1[n][k] += sum_rows g[row][n] feat[row][k]: n-tile w, every k-tile; the k (= row)
         // order inside a step is 4q + (j & 3) + 16 (j >> 2) in both operands
@@ -515,10 +746,11 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                     du[reg] = cu[reg] + sg * ca[reg];
                     dv[reg] = cv[reg] - sg * ca[reg];
                 }
-                float* o = dpipe + (static_cast<uint32_t>(r) * 2 * D + ku);
+                float* o = STREAM ? dpl + (row * DPS + ku) : dpipe + (static_cast<uint32_t>(r) * 2 * D + ku);
                 st4(o, du);
                 st4(o + D, dv);
             }
+            if constexpr (STREAM) store_evblock(k + 1);
         }
         if constexpr (SCAT) {
             if (k % sc.tpw == sc.tpw - 1 && k + 1 < nk) {  // a window's last tile (not the workgroup's last window)
@@ -578,9 +810,18 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                                                    static_cast<uint32_t>(blockIdx.x + ((nk - 1) / sc.tpw) * gstep));
         }
     }
+    if constexpr (STREAM) {
+        if (nk > 0) scatter_tile(nk - 1);  // the last tile's rows and events were stored before the barriers above
+    }
 }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// STREAM dynamic LDS: the images, the dfeat rows, two event blocks, the open nodes' sums
+int64_t edge_stream_lds(int64_t D, const EdgeScatter& sc) {
+    const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS, TR = 2048 / D;
+    return base + TR * (2 * D + 4) * 4 + 2 * int64_t{sc.bw} * 4 + int64_t{sc.nslots} * D * 4;
+}
 
 int64_t tile_rows(int64_t D) { return 2048 / D; }
 int bwd_grid(int64_t ntiles) { return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ntiles, lg_num_cus()))); }
@@ -622,16 +863,20 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 #else
     const int dropout_arg = dropout;
 #endif
-#define LG_EDGE_FWD(DD, BFB)                                                                                      \
+#define LG_EDGE_FWD(DD, BFB, F16B)                                                                                \
     do {                                                                                                          \
-        if (!allow_lds(k_edge_fwd<DD, BFB>, EG<DD>::FWD_LDS)) return LG_EHIP;                                     \
-        lg_launch(k_edge_fwd<DD, BFB>, grid, NT, EG<DD>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid, sb,   \
-                  sn, fdP, BP, ntiles, dropout_arg, dropout_p, scale, seed, salt);                                \
+        if (!allow_lds(k_edge_fwd<DD, BFB, F16B>, EG<DD>::FWD_LDS)) return LG_EHIP;                               \
+        lg_launch(k_edge_fwd<DD, BFB, F16B>, grid, NT, EG<DD>::FWD_LDS, s, ends, h, w1, b1, w2, b2, logits, ldo, hid,  \
+                  sb, sn, fdP, BP, ntiles, dropout_arg, dropout_p, scale, seed, salt);                            \
     } while (0)
+    // fp32 tier at D = 64: the f16x2 transform unless LG_F_BF16X3 asks for the 3-way bf16 split
+    const bool f16 = !bf && !(flags & LG_F_BF16X3);
     if (D == 64) {
-        if (bf) LG_EDGE_FWD(64, true); else LG_EDGE_FWD(64, false);
+        if (bf) LG_EDGE_FWD(64, true, false);
+        else if (f16) LG_EDGE_FWD(64, false, true);
+        else LG_EDGE_FWD(64, false, false);
     } else {
-        if (bf) LG_EDGE_FWD(32, true); else LG_EDGE_FWD(32, false);
+        if (bf) LG_EDGE_FWD(32, true, false); else LG_EDGE_FWD(32, false, false);
     }
 #undef LG_EDGE_FWD
     LG_RET_IF_LAUNCH_FAILED();
@@ -682,12 +927,18 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else {
         const bool bf = (flags & LG_F_BF16) != 0;
-        const int64_t lds = scat ? EG<64>::BWD_LDS * (D == 64) + EG<32>::BWD_LDS * (D == 32) + 4 * (N + 1 + 2 * P) : 0;
+        const bool stream = scat && scat->spipe;
+        const int64_t lds = stream ? edge_stream_lds(D, *scat)
+                          : scat ? EG<64>::BWD_LDS * (D == 64) + EG<32>::BWD_LDS * (D == 32) + 4 * (N + 1 + 2 * P) : 0;
 #define LG_EDGE_BWD(DD, BFB)                                                                                      \
     do {                                                                                                          \
-        if (scat) {                                                                                               \
-            if (!allow_lds(k_edge_bwd<DD, BFB, true>, lds)) return LG_EHIP;                                        \
-            lg_launch(k_edge_bwd<DD, BFB, true>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab, \
+        if (stream) {                                                                                             \
+            if (!allow_lds(k_edge_bwd<DD, BFB, 2>, lds)) return LG_EHIP;                                           \
+            lg_launch(k_edge_bwd<DD, BFB, 2>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab,    \
+                      dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                               \
+        } else if (scat) {                                                                                        \
+            if (!allow_lds(k_edge_bwd<DD, BFB, 1>, lds)) return LG_EHIP;                                           \
+            lg_launch(k_edge_bwd<DD, BFB, 1>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab,    \
                       dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                               \
         } else {                                                                                                  \
             if (!allow_lds(k_edge_bwd<DD, BFB>, EG<DD>::BWD_LDS)) return LG_EHIP;                                 \
@@ -721,13 +972,28 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
 extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
                                         const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
                                         float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
-                                        const int32_t* inc_item, const float* dpool, float* dh, int64_t B, int64_t N,
+                                        const int32_t* inc_item, const int32_t* sched, const int32_t* sched_hdr,
+                                        const float* dpool, float* dh, int64_t B, int64_t N,
                                         int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
                                         void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (!dh || !inc_rowptr || (P > 0 && !inc_item)) return LG_EINVAL;
+    if (!sched != !sched_hdr) return LG_EINVAL;
+    if (sched_hdr && (sched_hdr[0] != LG_PIPE_SCHED_VERSION || sched_hdr[1] != P || sched_hdr[2] != N || sched_hdr[3] != D))
+        return LG_EINVAL;  // a schedule built for another graph or width
     if (B == 0) return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D,
                                      hidden, flags, dropout_p, workspace, ws_bytes, stream, nullptr);
+    if (sched && P > 0 && B * N < kLgMaxRows) {
+        EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
+                       static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0, sched_hdr[5],
+                       reinterpret_cast<const int4*>(sched + sched_hdr[10]),
+                       reinterpret_cast<const uint32_t*>(sched + sched_hdr[11]), sched + sched_hdr[12],
+                       sched_hdr[9], sched_hdr[6], sched_hdr[8], sched_hdr[7]};
+        // STREAM when the open nodes' sums fit beside the images (L-TOWN-A at D = 64: 23 of them)
+        if (edge_stream_lds(D, sc) <= 160 * 1024)
+            return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
+                                 flags, dropout_p, workspace, ws_bytes, stream, &sc);
+    }
     const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS;
     if (P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
         // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
@@ -738,7 +1004,144 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
     }
     EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
                    static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0,
-                   static_cast<int>(cdiv(P, tile_rows(D)))};
+                   static_cast<int>(cdiv(P, tile_rows(D))), nullptr, nullptr, nullptr, 0, 0, 0, 0};
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
                          dropout_p, workspace, ws_bytes, stream, &sc);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Pipe schedule (host).  Pipes ordered by their endpoints' positions in the RCM order of the
+ * pipe graph (key: the later endpoint, then the earlier one, then the id), so each node's
+ * incidences fall in a few consecutive tiles; per tile, one event per node it touches.  Layout
+ * in int32 words: header [16] (the fields of sched_hdr), pipes [P][4] {u, v, p, 0}, tile blocks
+ * [tpw][bw] {event count, 0, events [maxev][2], incidence bytes [2 TR] (2 row + role, grouped
+ * by event, rows in order)}, nodes without pipes [nzero].
+ * -------------------------------------------------------------------------------------------*/
+extern "C" int64_t lg_pipe_schedule_words(int64_t P, int64_t N, int64_t D) {
+    if (P < 0 || N <= 0 || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
+    const int64_t TR = tile_rows(D), tpw = cdiv(P, TR);
+    return 16 + 4 * P + tpw * (2 + 4 * TR + TR / 2) + N;
+}
+
+extern "C" int lg_pipe_schedule_build(const int64_t* ends, int64_t P, int64_t N, int64_t D, int32_t* sched,
+                                      int64_t words, int32_t* inc_rowptr, int32_t* inc_item) {
+    if (P < 0 || N <= 0 || (P > 0 && !ends) || !sched || !inc_rowptr || (P > 0 && !inc_item)) return LG_EINVAL;
+    if (D != 32 && D != 64) return LG_EUNSUPPORTED;
+    if (N >= (int64_t{1} << 24) || P >= (int64_t{1} << 30)) return LG_EUNSUPPORTED;
+    for (int64_t i = 0; i < 2 * P; ++i)
+        if (ends[i] < 0 || ends[i] >= N) return LG_EINVAL;
+    const int64_t TR = tile_rows(D), tpw = cdiv(P, TR);
+    // node positions in the RCM order of the pipe graph
+    std::vector<int64_t> ei(2 * P);
+    for (int64_t p = 0; p < P; ++p) {
+        ei[p] = ends[2 * p];
+        ei[P + p] = ends[2 * p + 1];
+    }
+    std::vector<int32_t> order(N), pos(N);
+    if (P > 0) {
+        const int rc = lg_rcm_order(ei.data(), P, N, order.data());
+        if (rc != LG_OK) return rc;
+    }
+    for (int64_t i = 0; i < N; ++i) pos[order[i]] = static_cast<int32_t>(i);
+    std::vector<int32_t> perm(P);
+    for (int64_t p = 0; p < P; ++p) perm[p] = static_cast<int32_t>(p);
+    auto key = [&](int32_t p) {
+        const int32_t a = pos[ends[2 * p]], b = pos[ends[2 * p + 1]];
+        return std::make_tuple(std::max(a, b), std::min(a, b), p);
+    };
+    std::sort(perm.begin(), perm.end(), [&](int32_t x, int32_t y) { return key(x) < key(y); });
+    // the tile range of each node's incidences
+    std::vector<int64_t> first(N, -1), last(N, -1);
+    for (int64_t i = 0; i < P; ++i)
+        for (int role = 0; role < 2; ++role) {
+            const int64_t n = ends[2 * perm[i] + role], t = i / TR;
+            if (first[n] < 0) first[n] = t;
+            last[n] = t;
+        }
+    // events per tile: nodes in order of first touch, each with its incidences in row order
+    struct Ev { int32_t node, slot; int cnt; std::vector<uint8_t> inc; };
+    std::vector<std::vector<Ev>> tiles(tpw);
+    int64_t maxev = 0;
+    std::vector<int32_t> at(N, -1);  // event index of node n in the tile being built
+    for (int64_t t = 0; t < tpw; ++t) {
+        auto& ev = tiles[t];
+        const int64_t i1 = std::min(P, (t + 1) * TR);
+        for (int64_t i = t * TR; i < i1; ++i)
+            for (int role = 0; role < 2; ++role) {
+                const int32_t n = static_cast<int32_t>(ends[2 * perm[i] + role]);
+                if (at[n] < 0) {
+                    at[n] = static_cast<int32_t>(ev.size());
+                    ev.push_back(Ev{n, 0, 0, {}});
+                }
+                ev[at[n]].inc.push_back(static_cast<uint8_t>(2 * (i - t * TR) + role));
+            }
+        for (auto& e : ev) at[e.node] = -1;
+        maxev = std::max<int64_t>(maxev, static_cast<int64_t>(ev.size()));
+    }
+    // LDS slots of the nodes open across a tile boundary; a slot freed at tile t is reused from t + 1
+    std::vector<char> used;
+    std::vector<int32_t> slot_of(N, -1);
+    for (int64_t t = 0; t < tpw; ++t) {
+        std::vector<int32_t> freed;
+        for (auto& e : tiles[t]) {
+            const bool f = first[e.node] == t, l = last[e.node] == t;
+            if (f && !l) {
+                size_t sidx = 0;
+                while (sidx < used.size() && used[sidx]) ++sidx;
+                if (sidx == used.size()) used.push_back(0);
+                used[sidx] = 1;
+                slot_of[e.node] = static_cast<int32_t>(sidx);
+            }
+            e.slot = slot_of[e.node] < 0 ? 0 : slot_of[e.node];
+            if (!f && l) freed.push_back(slot_of[e.node]);
+        }
+        for (int32_t x : freed) used[x] = 0;
+    }
+    const int64_t nslots = static_cast<int64_t>(used.size());
+    if (nslots >= 65536) return LG_EUNSUPPORTED;
+    std::vector<int32_t> zero;
+    for (int64_t n = 0; n < N; ++n)
+        if (first[n] < 0) zero.push_back(static_cast<int32_t>(n));
+    const int64_t bw = 2 + 2 * maxev + TR / 2;
+    const int64_t off_pipes = 16, off_blocks = off_pipes + 4 * P, off_zero = off_blocks + tpw * bw;
+    const int64_t total = off_zero + static_cast<int64_t>(zero.size());
+    if (total > words) return LG_EINVAL;
+    std::fill(sched, sched + total, 0);
+    const int32_t hdr[16] = {LG_PIPE_SCHED_VERSION, static_cast<int32_t>(P), static_cast<int32_t>(N),
+                             static_cast<int32_t>(D), static_cast<int32_t>(TR), static_cast<int32_t>(tpw),
+                             static_cast<int32_t>(nslots), static_cast<int32_t>(maxev), static_cast<int32_t>(bw),
+                             static_cast<int32_t>(zero.size()), static_cast<int32_t>(off_pipes),
+                             static_cast<int32_t>(off_blocks), static_cast<int32_t>(off_zero),
+                             static_cast<int32_t>(total), 0, 0};
+    std::copy(hdr, hdr + 16, sched);
+    for (int64_t i = 0; i < P; ++i) {
+        sched[off_pipes + 4 * i] = static_cast<int32_t>(ends[2 * perm[i]]);
+        sched[off_pipes + 4 * i + 1] = static_cast<int32_t>(ends[2 * perm[i] + 1]);
+        sched[off_pipes + 4 * i + 2] = perm[i];
+    }
+    for (int64_t t = 0; t < tpw; ++t) {
+        int32_t* blk = sched + off_blocks + t * bw;
+        uint8_t* incl = reinterpret_cast<uint8_t*>(blk + 2 + 2 * maxev);
+        blk[0] = static_cast<int32_t>(tiles[t].size());
+        int st = 0;
+        for (size_t e = 0; e < tiles[t].size(); ++e) {
+            const Ev& v = tiles[t][e];
+            const uint32_t w0 = static_cast<uint32_t>(v.node) | (first[v.node] == t ? 1u << 24 : 0u) |
+                                (last[v.node] == t ? 1u << 25 : 0u);
+            const uint32_t w1 = static_cast<uint32_t>(v.slot) | (static_cast<uint32_t>(st) << 16) |
+                                (static_cast<uint32_t>(v.inc.size()) << 24);
+            blk[2 + 2 * e] = static_cast<int32_t>(w0);
+            blk[3 + 2 * e] = static_cast<int32_t>(w1);
+            for (uint8_t b : v.inc) incl[st++] = b;
+        }
+    }
+    std::copy(zero.begin(), zero.end(), sched + off_zero);
+    // the incidence CSR in schedule order (lg_pipe_scatter_bwd over it sums as the stream does)
+    std::fill(inc_rowptr, inc_rowptr + N + 1, 0);
+    for (int64_t i = 0; i < 2 * P; ++i) ++inc_rowptr[ends[i] + 1];
+    for (int64_t n = 0; n < N; ++n) inc_rowptr[n + 1] += inc_rowptr[n];
+    std::vector<int32_t> fill(inc_rowptr, inc_rowptr + N);
+    for (int64_t i = 0; i < P; ++i)
+        for (int role = 0; role < 2; ++role) inc_item[fill[ends[2 * perm[i] + role]]++] = 2 * perm[i] + role;
+    return LG_OK;
 }

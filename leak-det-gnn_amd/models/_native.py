@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 21  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 22  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02
@@ -87,7 +87,10 @@ SIGNATURES = {
                                 _u64, _u32, _p]),
     "lg_edge_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "lg_edge_head_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
-    "lg_edge_head_bwd_scatter": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
+    "lg_edge_head_bwd_scatter": (_i32, [_p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
+                                        _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
+    "lg_pipe_schedule_words": (_i64, [_i64, _i64, _i64]),
+    "lg_pipe_schedule_build": (_i32, [_p, _i64, _i64, _i64, _p, _i64, _p, _p]),
     "lg_mean_pool_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _p]),
     "lg_pool_head_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64,
                                 _u32, _p]),

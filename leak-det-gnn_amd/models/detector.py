@@ -207,8 +207,9 @@ class LeakDetector(nn.Module):
         keep = torch.is_grad_enabled() and (h_nodes.requires_grad or any(t.requires_grad for t in hw))
         seed = library.seed_tensor(residual.device) if (pe > 0.0 or pn > 0.0) else _NO_SEED
         # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-218)
+        sched, sched_hdr = inc.schedule(D)
         out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed,
-                                               bf16=self.mlp_dtype == "bf16")
+                                               sched, sched_hdr, bf16=self.mlp_dtype == "bf16")
         if self.capture is not None:
             if out_t[-1].numel() > 0:  # x_0 compressed: materialise it for the diagnostics
                 xs = [library.expand_x0(xs[0], out_t[-1], slot, bn, N, float(self.dropout.p) if drop else 0.0)] + xs[1:]

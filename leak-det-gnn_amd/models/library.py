@@ -23,6 +23,7 @@ draw fresh masks.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import threading
 
 from typing import List, Optional, Tuple
@@ -642,14 +643,16 @@ gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)
 @torch.library.custom_op(f"{NS}::detector_heads", mutates_args=(), device_types="cuda")
 def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw1: Tensor, nb1: Tensor, nw2: Tensor,
                    nb2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor, p_edge: float, p_noleak: float,
-                   node_major: bool, keep_hidden: bool, seed: Tensor, *,
-                   bf16: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+                   node_major: bool, keep_hidden: bool, seed: Tensor, sched: Optional[Tensor] = None,
+                   sched_hdr: Optional[List[int]] = None, *, bf16: bool = False) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """(logits (B, P+1), EdgeHead hidden, pooled, NoLeakHead hidden).  Columns [0, P) by
     lg_edge_head_fwd (endpoint gather -> MFMA MLP -> dot, the (B, P, 3D) features never
     stored), column P by lg_pool_head_fwd (mean pool + NoLeakHead): the torch.cat of
     detector.py:218 is never a separate copy.  keep_hidden: keep the EdgeHead hidden layer
     for a recompute-free backward (else it is empty).  bf16: the EdgeHead MLP as one bf16
-    MFMA product (LG_F_BF16, the configs[2] tier); the NoLeakHead stays fp32."""
+    MFMA product (LG_F_BF16, the configs[2] tier); the NoLeakHead stays fp32.  sched /
+    sched_hdr: the pipe schedule of inc_rowptr / inc_item (ops.Incidence.schedule(D)), for the
+    backward's streamed node sums; None / [] for the per-window scatter."""
     lib = load_library()
     h, w1, b1, w2, b2, nw1, nb1, nw2, nb2 = (_c(t) for t in (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2))
     _req(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2)
@@ -680,7 +683,7 @@ def detector_heads(h: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, nw
 
 @detector_heads.register_fake
 def _(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, keep_hidden,
-      seed, *, bf16=False):
+      seed, sched=None, sched_hdr=None, *, bf16=False):
     B = h.shape[1] if node_major else h.shape[0]
     D = h.shape[2]
     P = ends.shape[0]
@@ -691,7 +694,8 @@ def _(h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge,
 @torch.library.custom_op(f"{NS}::detector_heads_backward", mutates_args=(), device_types="cuda")
 def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, ehid: Tensor, pooled: Tensor,
                             hid: Tensor, nw1: Tensor, nw2: Tensor, ends: Tensor, inc_rowptr: Tensor, inc_item: Tensor,
-                            p_edge: float, p_noleak: float, node_major: bool, *, bf16: bool = False
+                            sched: Optional[Tensor], sched_hdr: List[int], p_edge: float, p_noleak: float,
+                            node_major: bool, *, bf16: bool = False
                             ) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
     """(dh, dW1, db1, dW2, db2, dnW1, dnb1, dnW2, dnb2): lg_pool_head_bwd -> dpooled and the
     NoLeakHead grads; lg_edge_head_bwd_scatter -> the per-pipe endpoint grads and, fused, their
@@ -718,14 +722,15 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     # one launch for the EdgeHead's and the NoLeakHead's weight-grad reductions; keep: the slabs
     # and every reduction target (alive until a deferred flush)
     with _reduce_batch(lib, st, keep=[ws, wsn, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2]):
-        _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N,
-                                 D, hidden, nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2, db2, ndw1,
-                                 ndb1, ndw2, ndb2, ws, wsn, st)
+        _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched,
+                                 sched_hdr, P, B, N, D, hidden, nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dh, dw1,
+                                 db1, dw2, db2, ndw1, ndb1, ndw2, ndb2, ws, wsn, st)
     return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 
-# True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter); False:
-# two launches (lg_edge_head_bwd + lg_pipe_scatter_bwd).  Same node gradient bit for bit.
+# True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter: streamed
+# per tile with a pipe schedule, else per window); False: two launches (lg_edge_head_bwd +
+# lg_pipe_scatter_bwd).  Same node gradient bit for bit (one incidence order for all).
 # Measured at B = 256: fused 152.6 us, step 0.659 ms (profiles/r03/r03al); two launches
 # 114.6 + 35.3 us, step 0.662 ms (r03am) -- equal within box-to-box noise.  With one window
 # per workgroup every workgroup reaches its scatter at the same time, after its MFMA work, so
@@ -733,9 +738,9 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
 _FUSED_SCATTER = True
 
 
-def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, P, B, N, D,
-                             hidden, nhidden, fe, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2,
-                             ndb2, ws, wsn, st):
+def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched,
+                             sched_hdr, P, B, N, D, hidden, nhidden, fe, fn, p_edge, p_noleak, dpipe, dh, dw1, db1, dw2,
+                             db2, ndw1, ndb1, ndw2, ndb2, ws, wsn, st):
     """NoLeakHead backward first (its dpooled feeds the node rows), then the EdgeHead backward
     with the incidence scatter fused in (lg_edge_head_bwd_scatter): dh complete."""
     dev = h.device
@@ -747,10 +752,12 @@ def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, en
     lay = fe & nat.LG_F_NODE_MAJOR
     if _FUSED_SCATTER:
         with _timed("edge_bwd", dev):
+            hdr = (ctypes.c_int32 * 16)(*sched_hdr) if (sched is not None and sched_hdr) else None
             check(lib.lg_edge_head_bwd_scatter(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1,
                                                ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2), ptr(db2), ptr(inc_rowptr),
-                                               ptr(inc_item), ptr(dpooled), ptr(dh), B, N, P, D, hidden, fe, p_edge,
-                                               ptr(ws), ws.numel(), st), "lg_edge_head_bwd_scatter")
+                                               ptr(inc_item), ptr(sched) if hdr else None, hdr, ptr(dpooled), ptr(dh),
+                                               B, N, P, D, hidden, fe, p_edge, ptr(ws), ws.numel(), st),
+                  "lg_edge_head_bwd_scatter")
         return
     with _timed("edge_bwd", dev):
         check(lib.lg_edge_head_bwd(ptr(ends), ptr(h), ptr(w1), ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe),
@@ -762,31 +769,34 @@ def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, en
 
 
 @detector_heads_backward.register_fake
-def _(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, *,
-      bf16=False):
+def _(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched, sched_hdr, p_edge, p_noleak,
+      node_major, *, bf16=False):
     H, NH = w1.shape[0], nw1.shape[0]
     return (torch.empty_like(h), torch.empty_like(w1), w1.new_empty(H), torch.empty_like(w2), w2.new_empty(1),
             torch.empty_like(nw1), nw1.new_empty(NH), torch.empty_like(nw2), nw2.new_empty(1))
 
 
 def _heads_setup(ctx, inputs, keyword_only_inputs, output):
-    (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, _, _) = inputs
+    (h, w1, b1, w2, b2, nw1, nb1, nw2, nb2, ends, inc_rowptr, inc_item, p_edge, p_noleak, node_major, _, _) = inputs[:17]
+    sched = inputs[17] if len(inputs) > 17 else None
+    sched_hdr = inputs[18] if len(inputs) > 18 else None
     bf16 = bool(keyword_only_inputs.get("bf16", False))
     _, ehid, pooled, hid = output
     ctx.mark_non_differentiable(ehid, pooled, hid)
     ctx.set_materialize_grads(False)  # else autograd zero-fills a (B*P, 128) gradient for ehid
-    ctx.cfg = (p_edge, p_noleak, node_major, bf16)
-    ctx.save_for_backward(h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item)
+    ctx.cfg = (p_edge, p_noleak, node_major, bf16, list(sched_hdr or []) if sched is not None else [])
+    ctx.nin = len(inputs)
+    ctx.save_for_backward(h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched)
 
 
 def _heads_bwd(ctx, dlogits, _dehid, _dpooled, _dhid):
     if dlogits is None:
-        return (None,) * 17
-    h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item = ctx.saved_tensors
-    p_edge, p_noleak, node_major, bf16 = ctx.cfg
+        return (None,) * ctx.nin
+    h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched = ctx.saved_tensors
+    p_edge, p_noleak, node_major, bf16, hdr = ctx.cfg
     g = torch.ops.leakgnn.detector_heads_backward(dlogits, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr,
-                                                  inc_item, p_edge, p_noleak, node_major, bf16=bf16)
-    return tuple(g) + (None,) * 8
+                                                  inc_item, sched, hdr, p_edge, p_noleak, node_major, bf16=bf16)
+    return tuple(g) + (None,) * (ctx.nin - 9)
 
 
 detector_heads.register_autograd(_heads_bwd, setup_context=_heads_setup)

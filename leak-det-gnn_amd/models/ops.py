@@ -247,10 +247,17 @@ class Incidence:
     num_pipes: int
     ends: torch.Tensor      # int64 (P, 2) device
     rowptr: torch.Tensor    # int32 (N+1,)
-    item: torch.Tensor      # int32 (2P,)
+    item: torch.Tensor      # int32 (2P,): ascending per node, or (schedule) in the pipe schedule's order
+    # D -> (device int32 schedule, its 16 header words): lg_pipe_schedule_build, the streamed
+    # node sums of the EdgeHead backward (ABI 22); empty when built without a schedule
+    sched: dict = None
 
     @staticmethod
-    def build(pipe_ends: torch.Tensor, num_nodes: int, device: torch.device) -> "Incidence":
+    def build(pipe_ends: torch.Tensor, num_nodes: int, device: torch.device, schedule: bool = True) -> "Incidence":
+        """schedule=True: the pipe schedules for D = 32 and 64 (host-built, uploaded) and the
+        incidence CSR in schedule order, from the same build, so every scatter path of the
+        EdgeHead backward sums each node's incidences in one order; False: lg_incidence_build
+        (items ascending, the reference order of index_add over item ids)."""
         lib = load_library()
         ends = pipe_ends.to(device=device, dtype=torch.long).contiguous()
         P, N = int(ends.size(0)), int(num_nodes)
@@ -259,12 +266,36 @@ class Incidence:
             if lo < 0 or hi >= N:
                 raise IndexError(f"pipe_ends values must lie in [0, {N}), got [{lo}, {hi}]")
         inc = Incidence(N, P, ends, torch.empty(N + 1, device=device, dtype=torch.int32),
-                        torch.empty(max(2 * P, 1), device=device, dtype=torch.int32))
+                        torch.empty(max(2 * P, 1), device=device, dtype=torch.int32), {})
+        if schedule and P > 0:
+            he = pipe_ends.detach().to("cpu", torch.long).contiguous()
+            rp = torch.empty(N + 1, dtype=torch.int32)
+            it = torch.empty(2 * P, dtype=torch.int32)
+            built = {}
+            for D in (32, 64):
+                words = int(lib.lg_pipe_schedule_words(P, N, D))
+                sc = torch.zeros(max(words, 16), dtype=torch.int32)
+                rc = lib.lg_pipe_schedule_build(he.data_ptr(), P, N, D, sc.data_ptr(), words, rp.data_ptr(), it.data_ptr())
+                if rc != 0:
+                    built = {}
+                    break
+                hdr = tuple(int(v) for v in sc[:16].tolist())
+                built[D] = (sc[:hdr[13]].to(device), hdr)
+            if built:
+                inc.rowptr.copy_(rp)
+                inc.item[:2 * P].copy_(it)
+                inc.sched = built
+                return inc
         ws = torch.empty(int(lib.lg_incidence_workspace_bytes(P, N)), device=device, dtype=torch.uint8)
         check(lib.lg_incidence_build(ptr(ends), P, N, ptr(inc.rowptr), ptr(inc.item), ptr(ws), ws.numel(), stream_of(ends)),
               "lg_incidence_build")
         inc._keepalive = ws
         return inc
+
+    def schedule(self, D: int):
+        """(device schedule or None, header words as a list) for the heads ops."""
+        t = (self.sched or {}).get(int(D))
+        return (t[0], list(t[1])) if t is not None else (None, [])
 
 
 def batchify_edge_index(edge_index_single: torch.Tensor, num_nodes: int, batch_size: int) -> torch.Tensor:

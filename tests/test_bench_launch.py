@@ -43,3 +43,20 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--dry-run"], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_short_kernel_name_and_small_kernel_entries():
+    """rocprofv3 kernel names -> the names the step accounting sums (bench.small_kernels_us),
+    including names whose argument list carries anonymous-namespace types."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    names = {"void (anonymous namespace)::k_slab_reduce<24>((anonymous namespace)::Segs)": "k_slab_reduce",
+             "void (anonymous namespace)::k_adam_update(float*, float const*, (anonymous namespace)::AdamArgs)":
+                 "k_adam_update",
+             "void (anonymous namespace)::k_gcn_fwd_pc<64, true, false>((anonymous namespace)::PcX0)": "k_gcn_fwd_pc",
+             "k_ce_fwd(float const*, long)": "k_ce_fwd"}
+    for full, short in names.items():
+        assert bench.short_kernel_name(full) == short
+    by = {"k_slab_reduce": 12.5, "k_adam_update": 3.0, "k_adam_norm": 1.0, "k_ce_fwd": 2.0, "k_ce_mean": 0.5}
+    got = bench.small_kernels_us({"by_name_us": by})
+    assert got["slab_reduce"] == 12.5 and got["adam"] == 4.0 and got["ce_fwd"] == 2.5 and got["seed"] == 0.0

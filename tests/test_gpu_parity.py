@@ -69,10 +69,16 @@ def test_graph_build_bit_exact_random(N, E, add_loops, normalize, improved):
 def test_incidence_and_batchify_bit_exact():
     from models.ops import Incidence, batchify_edge_index
     g = load("graph_ltown_a.npz")
-    inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV)
+    inc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV, schedule=False)
     rp, it = graph_ref.incidence_csr(g["pipe_ends"], 661)
     np.testing.assert_array_equal(inc.rowptr.cpu().numpy(), rp)
     np.testing.assert_array_equal(inc.item.cpu().numpy(), it)
+    # the schedule-ordered CSR (ABI 22): the same rows, each node's items reordered
+    sinc = Incidence.build(torch.from_numpy(g["pipe_ends"]), 661, DEV)
+    np.testing.assert_array_equal(sinc.rowptr.cpu().numpy(), rp)
+    sit = sinc.item.cpu().numpy()
+    for n in range(661):
+        assert sorted(sit[rp[n]:rp[n + 1]]) == list(it[rp[n]:rp[n + 1]])
     out = batchify_edge_index(torch.from_numpy(g["edge_index"]).to(DEV), 661, 3)
     np.testing.assert_array_equal(out.cpu().numpy(), g["batchified_b3"])
     from models.detector import _batchify_edge_index
@@ -512,6 +518,47 @@ def test_edge_head_eval_without_hidden():
     ps[1].requires_grad_(True)
     b = _heads(inc, 0.0, False, ps, keep=True)
     assert torch.equal(a, b.detach())
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_edge_fwd_f16x2_transform_accuracy(wide):
+    """The EdgeHead forward's default fp32-tier transform at D = 64 (2-way f16 split, W1 scaled
+    per wave, features per pipe row) and the 3-way bf16 split (LG_F_BF16X3) both within 1e-6
+    of each row's hidden-layer scale of the float64 product; `wide` spreads the node rows
+    over 2^-12 .. 2^12 so a per-row scale that failed to follow its row would show."""
+    from models import ops
+    nat = ops.nat
+    lib = ops.load_library()
+    g = load("graph_ltown_a.npz")
+    ends = torch.from_numpy(g["pipe_ends"]).long()
+    B, N, P, D = 37, 661, 764, 64
+    gen = torch.Generator().manual_seed(13 + wide)
+    h = torch.randn(B, N, D, generator=gen)
+    if wide:
+        h = h * torch.exp2(torch.randint(-12, 13, (B, N, 1), generator=gen).float())
+    W1 = torch.randn(128, 3 * D, generator=gen) / 8
+    b1 = torch.randn(128, generator=gen) / 4
+    W2 = torch.randn(128, generator=gen) / 8
+    b2 = torch.randn(1, generator=gen)
+    u, v = ends[:, 0], ends[:, 1]
+    hd = h.double()
+    feat = torch.cat([hd[:, u], hd[:, v], (hd[:, u] - hd[:, v]).abs()], -1).reshape(B * P, 3 * D)
+    pre = feat @ W1.double().t()
+    ref = torch.relu(pre + b1.double())
+    # per-row bound: the products' magnitude |feat| |W1| (the f16 split drops <= 2^-22 of it)
+    scale = (feat.abs() @ W1.double().abs().t()).amax(1, keepdim=True) + b1.double().abs().max()
+    hs, e = (t.to(DEV) for t in (h, ends))
+    for fl in (0, nat.LG_F_BF16X3):
+        logits = torch.empty(B, P, device=DEV)
+        hid = torch.full((B * P, 128), float("nan"), device=DEV)
+        ops.check(lib.lg_edge_head_fwd(ops.ptr(e), ops.ptr(hs), ops.ptr(W1.to(DEV)), ops.ptr(b1.to(DEV)),
+                                       ops.ptr(W2.to(DEV)), ops.ptr(b2.to(DEV)), ops.ptr(logits), P, ops.ptr(hid),
+                                       B, N, P, D, 128, fl, 0.0, 0, 0, ops.stream_of(hs)), "edge fwd")
+        torch.cuda.synchronize()
+        err = ((hid.cpu().double() - ref).abs() / scale).max().item()
+        assert err <= 1e-6, f"flags {fl:#x}: hidden layer err {err:.3e} of the row scale"
+        lr = (ref @ W2.double() + b2.double()).view(B, P)
+        assert_close(logits, lr, rtol=1e-5, what=f"logits flags {fl:#x}")
 
 
 def _heads_case(train, D, nm, B):

@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 21
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 22
     assert lib.lg_timing_arm(-1) == -1 and lib.lg_timing_disarm() == 0 and lib.lg_timing_elapsed(0, None) == -1
     assert lib.lg_nm_table_build(None, None, 661, None, None, None) == -1
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
@@ -162,7 +162,13 @@ def test_undersized_workspace_returns_einval():
     assert wse > 0
     eargs = (F, F, F, F, F, F, P, F, F, F, F, F)
     assert lib.lg_edge_head_bwd(*eargs, B, N, P, D, 128, 0, 0.0, F, wse - 1, None) == -1
-    assert lib.lg_edge_head_bwd_scatter(*eargs, F, F, None, F, B, N, P, D, 128, 0x20, 0.0, F, wse - 1, None) == -1
+    assert lib.lg_edge_head_bwd_scatter(*eargs, F, F, None, None, None, F, B, N, P, D, 128, 0x20, 0.0, F, wse - 1,
+                                        None) == -1
+    hdr = (ctypes.c_int32 * 16)(1, P, N, D)  # a schedule header (the streamed path checks the workspace too)
+    for D2 in (64, 32):
+        hdr[3] = D2
+        assert lib.lg_edge_head_bwd_scatter(*eargs, F, F, F, hdr, None, F, B, N, P, D2, 128, 0x20, 0.0, F,
+                                            lib.lg_edge_head_bwd_workspace_bytes(B, P, D2, 128) - 1, None) == -1
     wsp = lib.lg_pool_head_bwd_workspace_bytes(B, D, 128)
     assert lib.lg_pool_head_bwd(F, F, F, F, F, P + 1, P, F, F, F, F, F, B, D, 128, 0, 0.0, F, wsp - 1, None) == -1
     wsg = lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)
@@ -240,3 +246,111 @@ def test_gcn_conv_row_tiles_only_within_one_launch():
     assert library._use_rows(limit, 64)
     assert not library._use_rows(limit + 1, 64)
     assert not library._use_rows(100_000, 32)
+
+
+def _schedule(lib, ends, N, D):
+    P = ends.shape[0]
+    words = int(lib.lg_pipe_schedule_words(P, N, D))
+    sc = np.zeros(words, np.int32)
+    rp = np.zeros(N + 1, np.int32)
+    it = np.zeros(max(2 * P, 1), np.int32)
+    e = np.ascontiguousarray(ends, dtype=np.int64)
+    rc = lib.lg_pipe_schedule_build(e.ctypes.data, P, N, D, sc.ctypes.data, words, rp.ctypes.data, it.ctypes.data)
+    return rc, sc, rp, it
+
+
+def _stream_sums(sc, ends, g0, dp):
+    """The streamed EdgeHead scatter (edge.hip edge_stream_scatter) replayed on the host in
+    float32: events of a tile run in parallel, so they must touch distinct nodes and slots."""
+    ver, P, N, D, TR, tpw, nslots, maxev, bw, nzero, offp, offb, offz, total = (int(v) for v in sc[:14])
+    perm = sc[offp:offp + 4 * P].reshape(P, 4)[:, 2]
+    lacc = np.full((max(nslots, 1), dp.shape[-1]), np.nan, np.float32)
+    out = np.full((N, dp.shape[-1]), np.nan, np.float32)
+    seen = np.zeros(N, np.int64)
+    for t in range(tpw):
+        blk = sc[offb + t * bw: offb + (t + 1) * bw]
+        ne = int(blk[0])
+        ev = blk[2:2 + 2 * ne].reshape(ne, 2).view(np.uint32)
+        incl = blk[2 + 2 * maxev:].view(np.uint8)
+        nodes, slots = [], []
+        for w0, w1 in ev:
+            node, first, last = int(w0 & 0xFFFFFF), bool((w0 >> 24) & 1), bool((w0 >> 25) & 1)
+            slot, st, cnt = int(w1 & 0xFFFF), int((w1 >> 16) & 0xFF), int(w1 >> 24)
+            nodes.append(node)
+            if not (first and last):  # reads and/or writes its slot
+                slots.append(slot)
+            acc = g0.copy() if first else lacc[slot].copy()
+            assert not np.isnan(acc).any(), "an open node's running sum was read before it was written"
+            for i in range(cnt):
+                b = int(incl[st + i])
+                row = t * TR + (b >> 1)
+                assert row < P
+                acc = acc + dp[perm[row], b & 1]
+                seen[node] += 1
+            if last:
+                out[node] = acc
+            else:
+                lacc[slot] = acc
+        assert len(set(nodes)) == len(nodes), "a node with two events in one tile"
+        assert len(set(slots)) == len(slots), f"tile {t}: two events share an open-node slot"
+    for n in sc[offz:offz + nzero]:
+        out[n] = g0
+    return out, seen, perm
+
+
+@pytest.mark.parametrize("D", [64, 32])
+@pytest.mark.parametrize("graph", ["ltown", "odd"])
+def test_pipe_schedule_streams_the_csr_order_sums(D, graph):
+    """lg_pipe_schedule_build (ABI 22, host): the pipe order is a permutation, every incidence
+    is in exactly one event, the open-node slots never collide, and the streamed sums equal the
+    sums over its schedule-ordered incidence CSR (lg_pipe_scatter_bwd's order) bit for bit.
+    'odd': a hub of degree 40 (more incidences than a tile has rows), a self-loop pipe, nodes
+    without pipes."""
+    from models import _native
+    lib = _native.load_library()
+    if graph == "ltown":
+        ends, N = load("graph_ltown_a.npz")["pipe_ends"].astype(np.int64), 661
+    else:
+        rng = np.random.default_rng(3)
+        N = 60
+        ring = [(i, i + 1) for i in range(1, 44)]
+        hub = [(0, int(j)) for j in rng.permutation(np.arange(1, 45))[:40]]
+        ends = np.array(ring + hub + [(7, 7)], np.int64)
+    P = ends.shape[0]
+    rc, sc, rp, it = _schedule(lib, ends, N, D)
+    assert rc == 0
+    assert int(sc[0]) == 1 and tuple(int(v) for v in sc[1:4]) == (P, N, D) and int(sc[4]) == 2048 // D
+    rng = np.random.default_rng(D)
+    dp = (rng.standard_normal((P, 2, 4)) * np.exp2(rng.integers(-20, 20, (P, 2, 1)))).astype(np.float32)
+    g0 = rng.standard_normal(4).astype(np.float32)
+    out, seen, perm = _stream_sums(sc, ends, g0, dp)
+    assert sorted(perm.tolist()) == list(range(P))
+    np.testing.assert_array_equal(sc[16:16 + 4 * P].reshape(P, 4)[:, :2], ends[perm])
+    deg = np.bincount(ends.ravel(), minlength=N)
+    np.testing.assert_array_equal(seen, deg)
+    np.testing.assert_array_equal(rp, np.concatenate([[0], np.cumsum(deg)]))
+    spos = np.empty(P, np.int64)
+    spos[perm] = np.arange(P)
+    ref = np.empty((N, 4), np.float32)
+    for n in range(N):
+        items = it[rp[n]:rp[n + 1]]
+        keys = [(spos[i >> 1], i & 1) for i in items]
+        assert keys == sorted(keys), f"node {n}: CSR items not in schedule order"
+        acc = g0.copy()
+        for i in items:
+            acc = acc + dp[i >> 1, i & 1]
+        ref[n] = acc
+    assert out.tobytes() == ref.tobytes(), "streamed sums differ from the CSR-order sums"
+    if graph == "ltown":
+        assert int(sc[6]) <= 48, f"{int(sc[6])} open slots"  # RCM keeps L-TOWN-A's frontier small
+
+
+def test_pipe_schedule_rejects_bad_input():
+    from models import _native
+    lib = _native.load_library()
+    ends = np.array([[0, 1], [1, 5]], np.int64)
+    rc, *_ = _schedule(lib, ends, 3, 64)
+    assert rc == -1  # an endpoint id out of range
+    assert lib.lg_pipe_schedule_words(2, 3, 48) == -2
+    rc, sc, rp, it = _schedule(lib, np.zeros((0, 2), np.int64), 3, 64)
+    assert rc == 0 and int(sc[5]) == 0 and int(sc[9]) == 3  # no tiles; every node without pipes

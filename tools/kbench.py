@@ -4,6 +4,7 @@ HIP events on the launch stream.  Used for tuning and under rocprofv3 --pmc.
   python tools/kbench.py [--which gcn_fwd,gcn_bwd,spmm,edge_fwd,edge_bwd,gru_fwd,gru_bwd] [--B 256] [--iters 50]
 """
 import argparse
+import ctypes
 import json
 import sys
 from pathlib import Path
@@ -394,7 +395,8 @@ def main():
             t = timeit(f, args.iters)
             res["edge_fwd"] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
             labs = [(f"edge_fwd_eval_lab{v}", v << 28, None) for v in (int(x) for x in args.edgelab.split(",") if x)]
-            for name, fl, hp in [("edge_fwd_nohid", nat.LG_F_DROPOUT, None), ("edge_fwd_eval", 0, None)] + labs:
+            for name, fl, hp in [("edge_fwd_x3", nat.LG_F_DROPOUT | nat.LG_F_BF16X3, hid),
+                                 ("edge_fwd_nohid", nat.LG_F_DROPOUT, None), ("edge_fwd_eval", 0, None)] + labs:
                 g = lambda fl=fl, hp=hp: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2),
                                                                     ptr(b2), ptr(lo), P, hp, B, N, P, D, 128, fl, 0.1,
                                                                     5, 101, cs()), name)
@@ -412,6 +414,26 @@ def main():
                                                    nat.LG_F_DROPOUT, 0.1, ptr(ws), ws.numel(), cs()), "edge bwd")
             t = timeit(f, args.iters)
             res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
+            # with the node scatter fused, node-major h as in the step: per window (ABI 19) and
+            # streamed per tile through the pipe schedule (ABI 22)
+            xn = x.transpose(0, 1).contiguous()
+            dl1 = torch.randn(B, P + 1, device=dev)
+            dpool = torch.randn(B, D, device=dev)
+            dh = torch.empty_like(xn)
+            sched, hdr = inc.schedule(D)
+            hdr_c = (ctypes.c_int32 * 16)(*hdr)
+            for name, sp, hp in [("edge_bwd_scat", None, None), ("edge_bwd_stream", sched, hdr_c)]:
+                g = lambda sp=sp, hp=hp: check(lib.lg_edge_head_bwd_scatter(
+                    ptr(inc.ends), ptr(xn), ptr(W1), ptr(W2), ptr(hid), ptr(dl1), P + 1, ptr(dpipe), ptr(dW1), ptr(db1),
+                    ptr(dW2), ptr(db2), ptr(inc.rowptr), ptr(inc.item), ptr(sp) if sp is not None else None, hp,
+                    ptr(dpool), ptr(dh), B, N, P, D, 128, nat.LG_F_DROPOUT | nat.LG_F_NODE_MAJOR, 0.1, ptr(ws),
+                    ws.numel(), cs()), name)
+                t = timeit(g, args.iters)
+                res[name] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
+            g = lambda: check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe), ptr(dpool), ptr(dh),
+                                                      B, N, P, D, nat.LG_F_NODE_MAJOR, cs()), "pipe scatter")
+            t = timeit(g, args.iters)
+            res["pipe_scatter"] = {"us": t, "GBps": (B * P * 2 * D * 4 + B * N * D * 4) / t / 1e3}
     if "gru_fwd" in which or "gru_bwd" in which:
         S, L = 29, 36
         r = torch.randn(B, L, S, device=dev)

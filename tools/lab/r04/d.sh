@@ -7,6 +7,10 @@ OUT=gpurun_out/r04d; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_x0.py -x -q --timeout 120 --timeout-method thread -m gpu > $OUT/x0.log 2>&1 || { echo "x0 tests failed"; tail -40 $OUT/x0.log; exit 1; }
 tail -1 $OUT/x0.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -m gpu -k "edge or heads" > $OUT/edge.log 2>&1 || { echo "edge tests failed"; tail -40 $OUT/edge.log; exit 1; }
+tail -1 $OUT/edge.log
+timeout -k 10 300 python -u tools/kbench.py --which edge_fwd,edge_bwd --iters 50 > $OUT/kb_edge.txt 2>&1 || { tail -5 $OUT/kb_edge.txt; exit 1; }
+grep -v amdgpu.ids $OUT/kb_edge.txt
 timeout -k 10 300 python -u tools/kbench.py --which node_init,node_init_bits,gcn_fwd_x0,gcn_bwd_x0,gcn_fwd_nm_train,gcn_bwd_nm_l0s,copy --nmlab dflt,dflt+mask --iters 50 > $OUT/kb.txt 2>&1 || { tail -5 $OUT/kb.txt; exit 1; }
 grep -v amdgpu.ids $OUT/kb.txt
 LEAKGNN_LIB=leak-det-gnn_amd/lib/stamps/libleakgnn.so timeout -k 10 300 python -u tools/kbench.py --which none --nmlab dflt --stamps --iters 30 > $OUT/kb_stamps.txt 2>&1 || { tail -5 $OUT/kb_stamps.txt; exit 1; }
