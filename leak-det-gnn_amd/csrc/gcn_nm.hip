@@ -686,16 +686,19 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             for (int k = 0; k < G::K; ++k)
                 blk[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lk[k], base, 0));
         };
-        // slot k of a loaded neighbour block as values
+        // slot k of a loaded neighbour block as values.  X0: the sum of the row values (zeros for
+        // a non-sensor neighbour) and the mask-word values (zero bits for a sensor neighbour), one
+        // of them zero, so exact and branch-free (a branch on the neighbour kind here made the
+        // compiler read the rest-of-row mask words before their loads had landed: wrong bits for
+        // slots k >= 1 of degree-5 nodes, r04f)
         auto nbv = [&](int c, const f32x4 (&blk)[G::K], uint32_t bw, int k) -> f32x4 {
+            (void)c;
             if constexpr (X0) {
-                if (!(c & kLgSensorCol)) {
-                    const uint32_t w = bw >> (4 * k);
-                    f32x4 r;
+                const uint32_t w = bw >> (4 * k);
+                f32x4 r;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) r[i] = (w >> i) & 1u ? v0[i] : 0.f;
-                    return r;
-                }
+                for (int i = 0; i < 4; ++i) r[i] = blk[k][i] + ((w >> i) & 1u ? v0[i] : 0.f);
+                return r;
             }
             return blk[k];
         };
@@ -761,12 +764,10 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
                 for (int i = 0; i < NI; ++i) load_nb(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
 #pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    if (e0 + NPF + i < e1) {
-                        const float wa = __int_as_float(cur.p[NPF + i].y);
+                for (int i = 0; i < NI; ++i) {  // an absent entry: zero blocks at weight 0 (acc unchanged)
+                    const float wa = e0 + NPF + i < e1 ? __int_as_float(cur.p[NPF + i].y) : 0.f;
 #pragma unroll
-                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], vb[i], k));
-                    }
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], vb[i], k));
                 }
                 for (int e = e0 + kLgNmInline; e < e1; ++e) {
                     const int2 pa = pairs[e];

@@ -28,7 +28,6 @@ and replayed: one graph launch per step, the kernels back to back on the device.
 """
 from __future__ import annotations
 
-import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -62,16 +61,7 @@ class CapturedTrainStep:
         self.world = _world()
         self.slots = ops.SeedSlots(dev, seed_slots)
         self._one: Optional[torch.Tensor] = None
-
-        # every backward below reads its gradients only after backward() returns (set_to_none
-        # before each): its slab reductions run as ONE launch at the end of the pass
-        from . import library
-        defer0 = library.DEFER_REDUCE
-        library.DEFER_REDUCE = os.environ.get("LEAKGNN_DEFER_REDUCE", "0") == "1"
-        try:
-            self._build(model, warmup, preserve_state)
-        finally:
-            library.DEFER_REDUCE = defer0
+        self._build(model, warmup, preserve_state)
 
     def _build(self, model, warmup: int, preserve_state: bool) -> None:
         dev = self.label.device

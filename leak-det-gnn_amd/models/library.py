@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import threading
 
 from typing import List, Optional, Tuple
 
@@ -291,9 +290,7 @@ def gru_encoder_backward(dh: Tensor, residual: Tensor, tfeat: Optional[Tensor], 
     dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
     db_ih, db_hh = torch.empty(3 * H, device=dev), torch.empty(3 * H, device=dev)
     ws = torch.empty(int(lib.lg_gru_bwd_workspace_bytes(B, S, I, H)), device=dev, dtype=torch.uint8)
-    # keep: the slab and every reduction target (a target autograd drops must not be freed
-    # before a deferred flush writes it)
-    with _reduce_batch(lib, stream_of(residual), keep=[ws, dw_ih, dw_hh, db_ih, db_hh]), _timed("gru_bwd", dev):
+    with _reduce_batch(lib, stream_of(residual)), _timed("gru_bwd", dev):
         check(lib.lg_gru_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates), ptr(dh),
                              ptr(dx) if need_dx else None, ptr(dw_ih), ptr(dw_hh), ptr(db_ih), ptr(db_hh), B, L, S, I,
                              H, ptr(ws), ws.numel(), stream_of(residual)), "lg_gru_bwd")
@@ -338,51 +335,18 @@ gru_encoder.register_autograd(_gru_bwd, setup_context=_gru_setup)
 
 
 REDUCE_BATCH = True  # tests switch it off to compare with one reduction launch per op
-# DEFER_REDUCE (set by the training-step owners, models/graph_step.py): inside a backward pass
-# the backward ops' slab reductions are NOT flushed per op; the first op opens one batch for the
-# whole pass and an autograd final callback flushes it when the pass ends, so a detector
-# backward (heads, trunk, GRU) ends in ONE reduction launch instead of three.  Only for callers
-# that read the gradients after backward() returns and never accumulate into an existing .grad
-# during it (the reduced outputs are undefined until the flush).
-DEFER_REDUCE = False
-_pending = threading.local()
-
-
-def _flush_pending() -> None:
-    b = getattr(_pending, "batch", None)
-    _pending.batch = None
-    if b is not None:
-        check(b["lib"].lg_reduce_batch_flush(b["st"]), "lg_reduce_batch_flush (end of backward)")
-        b["keep"].clear()
 
 
 @contextlib.contextmanager
-def _reduce_batch(lib, st, keep=None):
+def _reduce_batch(lib, st):
     """All slab reductions of the enclosed backward launches as one launch at the end
     (lg_reduce_batch_begin / _flush, include/leakgnn.h).  The enclosed code keeps every
-    workspace it passes alive until the flush: the caller's locals, and under DEFER_REDUCE
-    the list `keep` (held by the pending batch until the end of the backward pass)."""
+    workspace it passes alive until the flush (the caller's locals).  A batch per backward pass
+    instead of per op was measured (+0.7 %) and dropped: autograd reads or copies an op's
+    gradients (AccumulateGrad into an existing .grad, a clone when another reference is held)
+    before an end-of-pass flush would have written them."""
     if not REDUCE_BATCH:
         yield
-        return
-    if DEFER_REDUCE:
-        b = getattr(_pending, "batch", None)
-        if b is None:
-            check(lib.lg_reduce_batch_begin(), "lg_reduce_batch_begin")
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
-            except RuntimeError:  # not inside a backward pass: flush at the end of this op
-                check(lib.lg_reduce_batch_flush(st), "lg_reduce_batch_flush")
-                check(lib.lg_reduce_batch_begin(), "lg_reduce_batch_begin")
-                try:
-                    yield
-                finally:
-                    check(lib.lg_reduce_batch_flush(st), "lg_reduce_batch_flush")
-                return
-            b = _pending.batch = {"lib": lib, "st": st, "keep": []}
-        yield
-        if keep is not None:
-            b["keep"].extend(keep)
         return
     check(lib.lg_reduce_batch_begin(), "lg_reduce_batch_begin")
     try:
@@ -531,13 +495,11 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: T
     dWs: List[Tensor] = [grad_out] * L
     dbs: List[Tensor] = [grad_out] * L
     dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
-    keep: List[Tensor] = []  # slabs and reduction targets, alive until a deferred flush
-    with _reduce_batch(lib, st, keep=keep):
+    with _reduce_batch(lib, st):
         dh_s, dWp, dbp = _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx,
                                                   nonsensor_idx, slot_live, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
                                                   node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st,
                                                   (x0bits, x0_bias, pos_slot_t) if x0bits is not None else None, p)
-        keep += wss + dWs + dbs + [dbias_ns, dWp, dbp]
     return dh_s, dWp, dbp, dWs, dbs
 
 
@@ -719,9 +681,8 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, hidden)), device=dev, dtype=torch.uint8)
     wsn = torch.empty(int(lib.lg_pool_head_bwd_workspace_bytes(B, D, nhidden)), device=dev, dtype=torch.uint8)
     dh = torch.empty_like(h)
-    # one launch for the EdgeHead's and the NoLeakHead's weight-grad reductions; keep: the slabs
-    # and every reduction target (alive until a deferred flush)
-    with _reduce_batch(lib, st, keep=[ws, wsn, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2]):
+    # one launch for the EdgeHead's and the NoLeakHead's weight-grad reductions
+    with _reduce_batch(lib, st):
         _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched,
                                  sched_hdr, P, B, N, D, hidden, nhidden, fe | lay, fn, p_edge, p_noleak, dpipe, dh, dw1,
                                  db1, dw2, db2, ndw1, ndb1, ndw2, ndb2, ws, wsn, st)

@@ -275,33 +275,6 @@ def test_reduce_batch_matches_per_op_reductions():
             assert torch.equal(g, ref), f"{n}: batched reduction differs"
 
 
-def test_deferred_reduce_batch_equals_per_pass_batches():
-    """DEFER_REDUCE (the captured training step's mode): every backward op's slab reductions
-    join ONE batch flushed by an autograd final callback at the end of the pass (one launch
-    for heads, trunk and GRU) — the same columns in the same order, so the gradients equal the
-    per-op batches bit for bit; the workspaces stay alive until the flush."""
-    from models.detector import LeakDetector
-    sensors, pipes = lta_ids()
-    torch.manual_seed(3)
-    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
-    r = torch.randn(64, 36, 29, device=DEV)
-    tf = torch.randn(64, 36, 9, device=DEV)
-    grads = []
-    for defer in (True, False):
-        library.DEFER_REDUCE = defer
-        try:
-            m.zero_grad(set_to_none=True)
-            torch.manual_seed(11)
-            m(r, tf).square().mean().backward()
-            assert getattr(library._pending, "batch", None) is None, "the end-of-backward flush did not run"
-            torch.cuda.synchronize()
-        finally:
-            library.DEFER_REDUCE = False
-        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
-    for n, g in grads[0].items():
-        assert torch.equal(g, grads[1][n]), f"{n}: deferred reduction differs"
-
-
 @pytest.mark.parametrize("B,npipes", [(3, None), (64, None), (300, None), (37, 6)])
 def test_fused_pipe_scatter_matches_two_launches(B, npipes):
     """lg_edge_head_bwd_scatter (the incidence scatter fused into the EdgeHead backward, one

@@ -547,13 +547,13 @@ def test_edge_fwd_f16x2_transform_accuracy(wide):
     ref = torch.relu(pre + b1.double())
     # per-row bound: the products' magnitude |feat| |W1| (the f16 split drops <= 2^-22 of it)
     scale = (feat.abs() @ W1.double().abs().t()).amax(1, keepdim=True) + b1.double().abs().max()
-    hs, e = (t.to(DEV) for t in (h, ends))
+    hs, e, w1d, b1d, w2d, b2d = (t.to(DEV) for t in (h, ends, W1, b1, W2, b2))  # alive across the launch
     for fl in (0, nat.LG_F_BF16X3):
         logits = torch.empty(B, P, device=DEV)
         hid = torch.full((B * P, 128), float("nan"), device=DEV)
-        ops.check(lib.lg_edge_head_fwd(ops.ptr(e), ops.ptr(hs), ops.ptr(W1.to(DEV)), ops.ptr(b1.to(DEV)),
-                                       ops.ptr(W2.to(DEV)), ops.ptr(b2.to(DEV)), ops.ptr(logits), P, ops.ptr(hid),
-                                       B, N, P, D, 128, fl, 0.0, 0, 0, ops.stream_of(hs)), "edge fwd")
+        ops.check(lib.lg_edge_head_fwd(ops.ptr(e), ops.ptr(hs), ops.ptr(w1d), ops.ptr(b1d), ops.ptr(w2d), ops.ptr(b2d),
+                                       ops.ptr(logits), P, ops.ptr(hid), B, N, P, D, 128, fl, 0.0, 0, 0,
+                                       ops.stream_of(hs)), "edge fwd")
         torch.cuda.synchronize()
         err = ((hid.cpu().double() - ref).abs() / scale).max().item()
         assert err <= 1e-6, f"flags {fl:#x}: hidden layer err {err:.3e} of the row scale"

@@ -398,7 +398,7 @@ def main():
             for name, fl, hp in [("edge_fwd_x3", nat.LG_F_DROPOUT | nat.LG_F_BF16X3, hid),
                                  ("edge_fwd_nohid", nat.LG_F_DROPOUT, None), ("edge_fwd_eval", 0, None)] + labs:
                 g = lambda fl=fl, hp=hp: check(lib.lg_edge_head_fwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(b1), ptr(W2),
-                                                                    ptr(b2), ptr(lo), P, hp, B, N, P, D, 128, fl, 0.1,
+                                                                    ptr(b2), ptr(lo), P, ptr(hp) if hp is not None else None, B, N, P, D, 128, fl, 0.1,
                                                                     5, 101, cs()), name)
                 t = timeit(g, args.iters)
                 res[name] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}

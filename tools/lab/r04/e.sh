@@ -13,5 +13,4 @@ timeout -k 10 300 python -u tools/kbench.py --which edge_fwd,edge_bwd,node_init,
 grep -v amdgpu.ids $OUT/kb.txt
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-c4 --no-c5 --no-pmc --no-tier-leg > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 python -c "import json,sys; d=json.load(open('$OUT/bench.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['kernels_us'], d.get('step_gap_us'))"
-LEAKGNN_DEFER_REDUCE=1 timeout -k 10 300 python -u -m pytest tests/test_graph_step.py tests/test_gpu_library.py -x -q $T -m gpu > $OUT/defer_tests.log 2>&1; echo "defer tests rc=$?"; tail -3 $OUT/defer_tests.log
 timeout -k 10 800 python -u -m pytest tests -x -q $T -m gpu > $OUT/tests.log 2>&1; echo "suite rc=$?"; tail -3 $OUT/tests.log
