@@ -63,10 +63,31 @@ struct EG {
     static constexpr int FWD_WG_PER_CU = 1, FWD_WG_PER_CU_BF = 2;
     static constexpr int64_t FWD_LDS = int64_t{2} * 2 * 3 * FPL + 4 * (2 * 4 * TR + 2 * HID + 2 * TR);  // images, partials, b1/W2, row scales
     static constexpr int64_t BWD_LDS = int64_t{2} * (3 * FTPL + 3 * GPL) + 2 * TR * D + 16 * 64 * NRED;
+    // F16 (the f16x2 transform): two image planes instead of three, then the per-row g scale
+    // exponents [2][TR] and the per-tile product scale exponents [2] (+ pad)
+    static constexpr int64_t BWD_LDS_F16 = int64_t{2} * (2 * FTPL + 2 * GPL) + 2 * TR * D + 16 * 64 * NRED + 4 * (2 * TR + 4);
+    static constexpr int64_t bwd_lds(bool f16) { return f16 ? BWD_LDS_F16 : BWD_LDS; }
 };
 static_assert(EG<64>::RBW == 2 && EG<32>::RBW == 2, "dfeat wave split");
 static_assert(EG<64>::NROLE == NW && EG<32>::NROLE == NW, "one dfeat output block per wave");
 static_assert(EG<64>::BWD_LDS <= 160 * 1024 && EG<32>::BWD_LDS <= 160 * 1024, "LDS budget");
+static_assert(EG<64>::BWD_LDS_F16 % 16 == 0 && EG<32>::BWD_LDS_F16 % 16 == 0, "16-byte aligned tail");
+
+// max of a non-negative float's bits over the lanes of one node row of the gather layout
+// (D / 4 lanes: 16 at D = 64, 8 at D = 32), broadcast to them
+template <int D>
+__device__ __forceinline__ uint32_t lg_rowgroup_max_bits(uint32_t m) {
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0xB1, 0xF, 0xF, false)));  // xor 1
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x4E, 0xF, 0xF, false)));  // xor 2
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x141, 0xF, 0xF, false)));  // half-row mirror
+    if constexpr (D == 64)
+        m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x140, 0xF, 0xF, false)));  // row mirror
+    return m;
+}
+__device__ __forceinline__ int lg_wave_min_i32(int v) {
+    for (int off = 1; off < 64; off <<= 1) v = min(v, __shfl_xor(v, off));
+    return v;
+}
 
 // row r = b*P + p of the (B, P) logit space -> element (b, p) of a buffer with row stride ldo
 __device__ __forceinline__ int64_t lg_row_index(int64_t r, const lg_fastdiv& fdP, int64_t ldo) {
@@ -385,6 +406,7 @@ struct EdgeScatter {
     const uint32_t* sblk;    // [tpw][bw] {count, 0, events [maxev][2], incidence bytes [2 TR]}
     const int32_t* szero;    // [nzero]
     int nzero, nslots, bw, maxev;
+    int lab;  // kernel-lab builds only (LG_KERNEL_LAB; results WRONG when set): 1 skip dW1 MFMA, 2 skip dfeat MFMA, 4 skip the streamed scatter
 };
 
 // dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
@@ -450,80 +472,139 @@ __device__ __forceinline__ void edge_scatter_window(const EdgeScatter& sc, const
 // The running sum starts from dpool / N and adds the incidences in schedule order: the order
 // of the schedule's incidence CSR, so the sums are those of lg_pipe_scatter_bwd over it.
 // Event word 0: node | first << 24 | last << 25; word 1: slot | start << 16 | count << 24.
+// An event per D / 8 lanes, 8 channels a lane (two float4, halves D / 2 apart): the 2 TR events
+// a tile can have (NT / (D / 8) = 2 TR slots) in ONE round.  g0l: the window's dpool / N row.
 template <int D>
 __device__ __forceinline__ void edge_stream_scatter(const EdgeScatter& sc, const uint32_t* eb, const float* dpl,
-                                                    float* lacc, const f32x4& g0, uint32_t win, int DPS) {
-    constexpr int LPR = D / 4, SLOTS = NT / LPR;
-    const int sr = threadIdx.x / LPR, sf = threadIdx.x % LPR;
+                                                    float* lacc, const float* g0l, uint32_t win, int DPS) {
+    constexpr int LPE = D / 8;
+    static_assert(NT / LPE == 2 * EG<D>::TR, "one round of events");
+    const int e = threadIdx.x / LPE, c0 = 4 * (threadIdx.x % LPE), c1 = c0 + D / 2;
     const int ne = static_cast<int>(eb[0]);
     const uint8_t* incl = reinterpret_cast<const uint8_t*>(eb + 2 + 2 * sc.maxev);
-    for (int e = sr; e < ne; e += SLOTS) {
+    if (e < ne) {
         const uint32_t w0 = eb[2 + 2 * e], w1 = eb[3 + 2 * e];
         const uint32_t node = w0 & 0xFFFFFFu, slot = w1 & 0xFFFFu, st = (w1 >> 16) & 0xFFu, cnt = w1 >> 24;
-        f32x4 acc = (w0 >> 24) & 1u ? g0 : ld4(lacc + slot * D + 4 * sf);
+        const float* src = (w0 >> 24) & 1u ? g0l : lacc + slot * D;
+        f32x4 a0 = ld4(src + c0), a1 = ld4(src + c1);
         for (uint32_t i = 0; i < cnt; ++i) {
             const uint32_t b = incl[st + i];  // 2 row + role
-            acc += ld4(dpl + (b >> 1) * DPS + (b & 1u) * D + 4 * sf);
+            const float* r = dpl + (b >> 1) * DPS + (b & 1u) * D;
+            a0 += ld4(r + c0);
+            a1 += ld4(r + c1);
         }
+        float* dst = lacc + slot * D;
         if ((w0 >> 25) & 1u) {
             const int64_t row = sc.nm ? static_cast<int64_t>(node) * sc.B + win : static_cast<int64_t>(win) * sc.N + node;
-            st4(sc.dh + row * D + 4 * sf, acc);
-        } else {
-            st4(lacc + slot * D + 4 * sf, acc);
+            dst = sc.dh + row * D;
         }
+        st4(dst + c0, a0);
+        st4(dst + c1, a1);
     }
 }
 // the window's nodes without pipes: dh = dpool / N
 template <int D>
-__device__ __forceinline__ void edge_stream_zero(const EdgeScatter& sc, const f32x4& g0, uint32_t win) {
-    constexpr int LPR = D / 4, SLOTS = NT / LPR;
-    const int sr = threadIdx.x / LPR, sf = threadIdx.x % LPR;
-    for (int i = sr; i < sc.nzero; i += SLOTS) {
+__device__ __forceinline__ void edge_stream_zero(const EdgeScatter& sc, const float* g0l, uint32_t win) {
+    constexpr int LPE = D / 8, SLOTS = NT / LPE;
+    const int e = threadIdx.x / LPE, c0 = 4 * (threadIdx.x % LPE), c1 = c0 + D / 2;
+    for (int i = e; i < sc.nzero; i += SLOTS) {
         const uint32_t node = static_cast<uint32_t>(sc.szero[i]);
         const int64_t row = sc.nm ? static_cast<int64_t>(node) * sc.B + win : static_cast<int64_t>(win) * sc.N + node;
-        st4(sc.dh + row * D + 4 * sf, g0);
+        st4(sc.dh + row * D + c0, ld4(g0l + c0));
+        st4(sc.dh + row * D + c1, ld4(g0l + c1));
     }
 }
 
 // slab per workgroup: [dW1 128*K3][db1 128][dW2 128][db2 1]
 // MODE 0: dpipe rows only; 1 (SCAT): + each window's node sums from its dpipe rows; 2
 // (STREAM): the node sums streamed per tile, no dpipe rows
-template <int D, bool BF, int MODE = 0>
+// F16 (the fp32 tier's default): both products on the 2-way f16 split (3 f16 MFMAs per product
+// instead of 6 bf16 ones) with power-of-two scales that keep the dfeat rows independent of
+// which rows share their tile (bit-identical results across MODEs):
+//   g rows scaled per ROW by 2^sg(row), from |dlogit(row)| max|W2| dscale (a bound on the row's
+//     |g|): dfeat^T = W1^T g^T contracts over hidden units, so a per-row (column) scale is
+//     allowed; W1^T scaled per wave by 2^sW; each wave unscales its partial by 2^-(sW + sg);
+//   dW1 = g^T feat contracts over rows: the feature rows are scaled by 2^(T - sg(row)), T per
+//     tile = min over its rows of sf(row) + sg(row) (sf from the row's max |feature|), so every
+//     row's products carry 2^T and the tile's dW1 block is added times 2^-T.  T is reduced
+//     (LDS atomic min) from the tile's loaded rows before the previous tile's second barrier.
+template <int D, bool BF, int MODE = 0, bool F16 = false>
 __global__ void __launch_bounds__(NT)
 k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const float* __restrict__ W1,
            const float* __restrict__ W2, const float* __restrict__ hid, const float* __restrict__ dlogit, int64_t ldo,
            float* __restrict__ dpipe, float* __restrict__ slab, double* __restrict__ db2slab, uint32_t sb,
            uint32_t sn, lg_fastdiv fdP, int64_t BP, int64_t ntiles, float dscale, EdgeScatter sc) {
     using G = EG<D>;
+    static_assert(!(F16 && BF), "one transform");
     constexpr bool SCAT = MODE == 1, STREAM = MODE == 2, WIN = MODE != 0;  // WIN: workgroups own windows
     constexpr int SL = HID * G::K3 + 2 * HID + 1;
+    constexpr int NPL = F16 ? 2 : 3;  // image planes
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);     // [3][TR][FTB]  feat parts
-    uint16_t* gimg = fimg + 3 * G::FTPL;                     // [3][TR][GSB]  g parts
-    int8_t* sgn = reinterpret_cast<int8_t*>(gimg + 3 * G::GPL);  // [2][TR][D]  sign(h_u - h_v), by tile parity
+    uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);     // [NPL][TR][FTB]  feat parts
+    uint16_t* gimg = fimg + NPL * G::FTPL;                   // [NPL][TR][GSB]  g parts
+    int8_t* sgn = reinterpret_cast<int8_t*>(gimg + NPL * G::GPL);  // [2][TR][D]  sign(h_u - h_v), by tile parity
     f32x4* red = reinterpret_cast<f32x4*>(sgn + 2 * G::TR * D);  // [2][NROLE][3][64] dfeat partials
+    int* rsg = reinterpret_cast<int*>(red + 2 * G::NROLE * 3 * 64);  // F16: [2][TR] row g scales, by tile parity
+    int* tmn = rsg + 2 * G::TR;                                       // F16: [2] tile product scales T
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
     const int tq = (lane >> 2) & 3, tp = lane & 3;  // transposed-read address slot of this lane
     // dfeat roles: features 16 kt + [0,16) of u, v, |u-v|, hidden half hh, row group rg
     const int kt = w % G::DT, hh = (w / G::DT) & 1, rg = w / (2 * G::DT);
     // A operand of dfeat^T = W1^T g^T: A[k = 16(kt + DT s3) + c][n = 64hh + 32ks + 8q + j] = W1[n][k]
     lg_bf16x8 wt[3][2][3];
+    lg_f16x8 wh[3][2][2];
+    int sW = 0;  // F16: this wave's W1^T scale exponent
+    {
+        f32x4 wx[3][2][2];
 #pragma unroll
-    for (int s3 = 0; s3 < 3; ++s3)
+        for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            f32x4 x0, x1;
-            const float* src = W1 + (64 * hh + 32 * ks + 8 * q) * G::K3 + 16 * (kt + G::DT * s3) + c;
+            for (int ks = 0; ks < 2; ++ks) {
+                const float* src = W1 + (64 * hh + 32 * ks + 8 * q) * G::K3 + 16 * (kt + G::DT * s3) + c;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                x0[j] = src[j * G::K3];
-                x1[j] = src[(j + 4) * G::K3];
+                for (int j = 0; j < 4; ++j) {
+                    wx[s3][ks][0][j] = src[j * G::K3];
+                    wx[s3][ks][1][j] = src[(j + 4) * G::K3];
+                }
             }
-            split3_x8(x0, x1, wt[s3][ks][0], wt[s3][ks][1], wt[s3][ks][2]);
+        if constexpr (F16) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) m = max(m, __float_as_uint(fabsf(wx[s3][ks][h2][j])));
+            sW = lg_f16_scale_exp_c(lg_wave_max_bits(m));
+            const float sc = lg_pow2f(sW);
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    split2_f16_x8(wx[s3][ks][0] * sc, wx[s3][ks][1] * sc, wh[s3][ks][0], wh[s3][ks][1]);
+        } else {
+#pragma unroll
+            for (int s3 = 0; s3 < 3; ++s3)
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks)
+                    split3_x8(wx[s3][ks][0], wx[s3][ks][1], wt[s3][ks][0], wt[s3][ks][1], wt[s3][ks][2]);
         }
+    }
     const int arow = threadIdx.x / G::F4, af = threadIdx.x % G::F4;  // feature gather slot
     const int n4 = threadIdx.x & 31, hrow = threadIdx.x >> 5;        // hidden slot: rows hrow + 16 i
     const f32x4 w2g = ld4(W2 + 4 * n4);
+    // F16: max |W2| (each wave's lanes 0-31 hold all of W2) times the dropout scale: the row
+    // g bound is |dlogit(row)| w2m
+    float w2m = 0.f;
+    if constexpr (F16) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m = max(m, __float_as_uint(fabsf(w2g[j])));
+        w2m = __uint_as_float(lg_wave_max_bits(m)) * dscale;
+    }
+    auto row_gscale = [&](float dlv) { return lg_f16_scale_exp_c(__float_as_uint(fabsf(dlv) * w2m)); };
     f32x4 dwa[G::KT];
 #pragma unroll
     for (int i = 0; i < G::KT; ++i) dwa[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -532,6 +613,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     // window sum to ~0 under the CE gradient): kept in fp64 end to end
     double db1a[4] = {0.0, 0.0, 0.0, 0.0};
     double db2 = 0.0;
+    int tcur = 0;  // F16: dwa is dW1 x 2^tcur
 
     // this workgroup's k-th tile: tile blockIdx.x + k gridDim.x of the (B, P) row space, or
     // (SCAT) tile k % tpw of window blockIdx.x + (k / tpw) gridDim.x; rows [rbase, rlim) count
@@ -558,12 +640,15 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         slot = ok ? static_cast<uint32_t>(r - static_cast<int64_t>(b) * sc.P) : 0u;
     };
     uint32_t hpipe[G::HPT];  // STREAM: pipe ids of the hidden-slot rows, a tile ahead of their loads
+    uint32_t apipe = 0;      // STREAM + F16: pipe id of the feature row
+    float dla = 0.f;         // F16: dlogit of the feature row (its g scale)
     auto load_ids = [&](int64_t k) {
         if constexpr (STREAM) {
             uint32_t b, slot;
             sslot(k, arow, b, slot);
             nu = spw[4 * slot];
             nv = spw[4 * slot + 1];
+            if constexpr (F16) apipe = spw[4 * slot + 2];
 #pragma unroll
             for (int i = 0; i < G::HPT; ++i) {
                 sslot(k, hrow + 16 * i, b, slot);
@@ -597,9 +682,34 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 dl[i] = dlogit[lg_row_index(r, fdP, ldo)];
             }
         }
+        if constexpr (F16) {
+            if constexpr (STREAM) {
+                uint32_t b, slot;
+                sslot(k, arow, b, slot);
+                dla = dlogit[static_cast<int64_t>(b) * ldo + apipe];
+            } else {
+                dla = dlogit[lg_row_index(clamp_row(rbase(k) + arow, BP), fdP, ldo)];
+            }
+        }
+    };
+    // F16: tile k's product scale candidate of this thread's feature row (pu, pv, dla hold
+    // tile k's row), min-reduced over the workgroup into tmn[k & 1]
+    auto post_tile_scale = [&](int64_t k) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            m = max(m, max(__float_as_uint(fabsf(pu[i])), max(__float_as_uint(fabsf(pv[i])),
+                                                              __float_as_uint(fabsf(pu[i] - pv[i])))));
+        // a row without gradient (past the end, or dlogit 0) contributes nothing to dW1 and must not
+        // lower T (its zero g leaves its features free: they are staged as zeros)
+        const float dlv = rbase(k) + arow < rlim(k) ? dla : 0.f;
+        const int sfe = lg_f16_scale_exp_c(lg_rowgroup_max_bits<D>(m));
+        const int cand = lg_wave_min_i32(dlv != 0.f ? sfe + row_gscale(dlv) : 0x7FFFFFFF);
+        if (lane == 0) __hip_atomic_fetch_min(&tmn[k & 1], cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     // SCAT: the incidence CSR in LDS (after the kernel's images), staged before the first barrier
-    int32_t* icsr = reinterpret_cast<int32_t*>(smem + G::BWD_LDS);
+    constexpr int64_t BASE = G::bwd_lds(F16);
+    int32_t* icsr = reinterpret_cast<int32_t*>(smem + BASE);
     if constexpr (SCAT) {
         for (uint32_t i = threadIdx.x; i <= sc.N; i += NT) icsr[i] = sc.inc_rowptr[i];
         for (uint32_t i = threadIdx.x; i < 2 * sc.P; i += NT) icsr[sc.N + 1 + i] = sc.inc_item[i];
@@ -607,9 +717,10 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     // STREAM: after the images, the tile's dfeat rows [TR][DPS] (du | dv), the event blocks of
     // two tiles, the open nodes' running sums [nslots][D]
     constexpr int DPS = 2 * D + 4;  // row stride: the finishing waves' 16-row stores conflict-free
-    float* dpl = reinterpret_cast<float*>(smem + G::BWD_LDS);
+    float* dpl = reinterpret_cast<float*>(smem + BASE);
     uint32_t* evb = reinterpret_cast<uint32_t*>(dpl + G::TR * DPS);
-    float* lacc = reinterpret_cast<float*>(evb + 2 * sc.bw);
+    float* g0l = reinterpret_cast<float*>(evb + 2 * sc.bw);  // [D] dpool / N of the window scattered next
+    float* lacc = g0l + D;
     const int sf = threadIdx.x % (D / 4);
     const float fN = static_cast<float>(sc.N);
     const float* gsrc = sc.dpool ? sc.dpool : h;  // h: any readable row when there is no pool gradient
@@ -624,13 +735,18 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     };
     auto scatter_tile = [&](int64_t kk) {
         const uint32_t win = static_cast<uint32_t>(blockIdx.x + (kk / sc.tpw) * gstep);
-        f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (sc.dpool) {
+        edge_stream_scatter<D>(sc, evb + (kk & 1) * sc.bw, dpl, lacc, g0l, win, DPS);
+        if (sc.nzero > 0 && kk % sc.tpw == sc.tpw - 1) edge_stream_zero<D>(sc, g0l, win);
+    };
+    auto post_g0 = [&]() {  // graw (this thread's 4 channels, threads < D / 4) -> g0l
+        if (threadIdx.x < D / 4) {
+            f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (sc.dpool) {
 #pragma unroll
-            for (int c2 = 0; c2 < 4; ++c2) g0[c2] = graw[c2] / fN;
+                for (int c2 = 0; c2 < 4; ++c2) g0[c2] = graw[c2] / fN;
+            }
+            st4(g0l + 4 * threadIdx.x, g0);
         }
-        edge_stream_scatter<D>(sc, evb + (kk & 1) * sc.bw, dpl, lacc, g0, win, DPS);
-        if (sc.nzero > 0 && kk % sc.tpw == sc.tpw - 1) edge_stream_zero<D>(sc, g0, win);
     };
     auto load_graw = [&](int64_t k) {
         const uint32_t win = static_cast<uint32_t>(min<int64_t>(blockIdx.x + (k / sc.tpw) * gstep, sc.B - 1));
@@ -645,10 +761,18 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         store_evblock(0);
         load_graw(0);
     }
+    if constexpr (F16) {  // tile 0's product scale (later tiles': posted during the tile before)
+        if (threadIdx.x == 0) tmn[0] = tmn[1] = 0x7FFFFFFF;
+        __syncthreads();
+        if (nk > 0) post_tile_scale(0);
+        __syncthreads();
+    }
     int buf = 0;
     for (int64_t k = 0; k < nk; ++k, buf ^= 1) {
         const int64_t row0 = rbase(k), rend = rlim(k);
         int8_t* sgnb = sgn + buf * G::TR * D;
+        int tT = 0;  // F16: the tile's product scale exponent T
+        if constexpr (STREAM) post_g0();  // the window of tile k - 1, scattered after the barrier
         {
             f32x4 a;
             uint32_t sw = 0;
@@ -658,9 +782,18 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 a[i] = fabsf(d);
                 sw |= static_cast<uint32_t>(static_cast<uint8_t>(d > 0.f ? 1 : (d < 0.f ? -1 : 0))) << (8 * i);
             }
-            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 4 * af, pu);
-            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv);
-            st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a);
+            if constexpr (F16) {
+                tT = tmn[buf];
+                const float dlv = row0 + arow < rend ? dla : 0.f;
+                const float fs = dlv != 0.f ? lg_pow2f(tT - row_gscale(dlv)) : 0.f;
+                st_split2h(fimg, G::FTPL, arow * G::FTB + 4 * af, pu, fs);
+                st_split2h(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv, fs);
+                st_split2h(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a, fs);
+            } else {
+                st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 4 * af, pu);
+                st_split4<BF>(fimg, G::FTPL, arow * G::FTB + D + 4 * af, pv);
+                st_split4<BF>(fimg, G::FTPL, arow * G::FTB + 2 * D + 4 * af, a);
+            }
             *reinterpret_cast<uint32_t*>(sgnb + arow * D + 4 * af) = sw;
         }
 #pragma unroll
@@ -674,39 +807,95 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                 db1a[j] += static_cast<double>(g[j]);
             }
             if (n4 == 0) db2 += static_cast<double>(dli);
-            st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
+            if constexpr (F16) {
+                const int sg = row_gscale(dli);
+                st_split2h(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g, lg_pow2f(sg));
+                if (n4 == 0) rsg[buf * G::TR + hrow + 16 * i] = sg;
+            } else {
+                st_split4<BF>(gimg, G::GPL, (hrow + 16 * i) * G::GSB + 4 * n4, g);
+            }
         }
         __syncthreads();
+        if constexpr (F16) {
+            if (threadIdx.x == 0) tmn[buf] = 0x7FFFFFFF;  // read above by every thread; tile k + 2's next
+        }
         load_feat(k + 1);
         load_hid(k + 1);
         load_ids(k + 2);
-        if constexpr (STREAM) {
-            load_evblock(k + 1);
-            if (k > 0) scatter_tile(k - 1);  // the previous tile's node sums
-            load_graw(k);                     // for this tile's, at the next one
-        }
+        if constexpr (STREAM) load_evblock(k + 1);
 
         // dW1[n][k] += sum_rows g[row][n] feat[row][k]: n-tile w, every k-tile; the k (= row)
         // order inside a step is 4q + (j & 3) + 16 (j >> 2) in both operands
+        if constexpr (F16) {  // dwa holds dW1 x 2^tcur: rescaled (exactly) when the tile's T differs
+            if (tT != tcur && tT != 0x7FFFFFFF) {  // 0x7FFFFFFF: no row of the tile has a gradient
+                const float rs = lg_pow2f(tT - tcur);
 #pragma unroll
-        for (int ks = 0; ks < G::TR / 32; ++ks) {
-            const int r0 = 32 * ks + 4 * q + tq;
-            lg_bf16x8 ga[3];
-#pragma unroll
-            for (int pp = 0; pp < 3; ++pp) {
-                const uint16_t* src = gimg + pp * G::GPL + r0 * G::GSB + 16 * w + 4 * tp;
-                ga[pp] = lds_frag_tr16(src, src + 16 * G::GSB);
+                for (int t = 0; t < G::KT; ++t) dwa[t] *= rs;
+                tcur = tT;
             }
 #pragma unroll
-            for (int t = 0; t < G::KT; ++t) {
-                lg_bf16x8 fb[3];
+            for (int ks = 0; ks < G::TR / 32; ++ks) {
+                const int r0 = 32 * ks + 4 * q + tq;
+                lg_f16x8 ga[2];
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) {
+                    const uint16_t* src = gimg + pp * G::GPL + r0 * G::GSB + 16 * w + 4 * tp;
+                    ga[pp] = __builtin_bit_cast(lg_f16x8, lds_frag_tr16(src, src + 16 * G::GSB));
+                }
+#pragma unroll
+                for (int t = 0; t < G::KT; ++t) {
+                    lg_f16x8 fb[2];
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp) {
+                        const uint16_t* src = fimg + pp * G::FTPL + r0 * G::FTB + 16 * t + 4 * tp;
+                        fb[pp] = __builtin_bit_cast(lg_f16x8, lds_frag_tr16(src, src + 16 * G::FTB));
+                    }
+#ifdef LG_KERNEL_LAB
+                    if (sc.lab & 1) {
+                        dwa[t][0] += static_cast<float>(fb[0][0]) + static_cast<float>(ga[0][0]);
+                        continue;
+                    }
+#endif
+                    dwa[t] = mfma_f16x2(ga, fb, dwa[t]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < G::TR / 32; ++ks) {
+                const int r0 = 32 * ks + 4 * q + tq;
+                lg_bf16x8 ga[3];
 #pragma unroll
                 for (int pp = 0; pp < 3; ++pp) {
-                    const uint16_t* src = fimg + pp * G::FTPL + r0 * G::FTB + 16 * t + 4 * tp;
-                    fb[pp] = lds_frag_tr16(src, src + 16 * G::FTB);
+                    const uint16_t* src = gimg + pp * G::GPL + r0 * G::GSB + 16 * w + 4 * tp;
+                    ga[pp] = lds_frag_tr16(src, src + 16 * G::GSB);
                 }
-                dwa[t] = mfma_prec<BF>(ga, fb, dwa[t]);
+#pragma unroll
+                for (int t = 0; t < G::KT; ++t) {
+                    lg_bf16x8 fb[3];
+#pragma unroll
+                    for (int pp = 0; pp < 3; ++pp) {
+                        const uint16_t* src = fimg + pp * G::FTPL + r0 * G::FTB + 16 * t + 4 * tp;
+                        fb[pp] = lds_frag_tr16(src, src + 16 * G::FTB);
+                    }
+#ifdef LG_KERNEL_LAB
+                    if (sc.lab & 1) {
+                        dwa[t][0] += static_cast<float>(fb[0][0]) + static_cast<float>(ga[0][0]);
+                        continue;
+                    }
+#endif
+                    dwa[t] = mfma_prec<BF>(ga, fb, dwa[t]);
+                }
             }
+        }
+        // STREAM: the previous tile's node sums (LDS reads and stores between the two MFMA
+        // blocks, overlapping the dW1 chains in flight)
+        if constexpr (STREAM) {
+#ifdef LG_KERNEL_LAB
+            if (k > 0 && !(sc.lab & 4)) scatter_tile(k - 1);
+#else
+            if (k > 0) scatter_tile(k - 1);
+#endif
+            load_graw(k);  // for this tile's, at the next one
         }
         // dfeat^T[k][row] = sum_n W1[n][k] g[row][n] over this wave's hidden half; partial
         // blocks role = (rg, kt, rbw) of both halves go to LDS
@@ -717,13 +906,40 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const uint16_t* src = gimg + (rowb + c) * G::GSB + 64 * hh + 32 * ks + 8 * q;
-                const lg_bf16x8 gb[3] = {lds_frag_row(src), lds_frag_row(src + G::GPL), lds_frag_row(src + 2 * G::GPL)};
+                if constexpr (F16) {
+                    const lg_f16x8 gb[2] = {__builtin_bit_cast(lg_f16x8, lds_frag_row(src)),
+                                            __builtin_bit_cast(lg_f16x8, lds_frag_row(src + G::GPL))};
+#ifdef LG_KERNEL_LAB
+                    if (sc.lab & 2) {
+                        cacc[0][0] += static_cast<float>(gb[0][0]);
+                        continue;
+                    }
+#endif
 #pragma unroll
-                for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_prec<BF>(wt[s3][ks], gb, cacc[s3]);
+                    for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_f16x2(wh[s3][ks], gb, cacc[s3]);
+                } else {
+                    const lg_bf16x8 gb[3] = {lds_frag_row(src), lds_frag_row(src + G::GPL), lds_frag_row(src + 2 * G::GPL)};
+#ifdef LG_KERNEL_LAB
+                    if (sc.lab & 2) {
+                        cacc[0][0] += static_cast<float>(gb[0][0]);
+                        continue;
+                    }
+#endif
+#pragma unroll
+                    for (int s3 = 0; s3 < 3; ++s3) cacc[s3] = mfma_prec<BF>(wt[s3][ks], gb, cacc[s3]);
+                }
+            }
+            if constexpr (F16) {  // this half's partial unscaled: 2^-(sW + sg(row)), row = column c
+                const float us = lg_pow2f(-(sW + rsg[buf * G::TR + rowb + c]));
+#pragma unroll
+                for (int s3 = 0; s3 < 3; ++s3) cacc[s3] *= us;
             }
             const int role = (rg * G::DT + kt) * G::RBW + rbw;
 #pragma unroll
             for (int s3 = 0; s3 < 3; ++s3) red[((hh * G::NROLE + role) * 3 + s3) * 64 + lane] = cacc[s3];
+        }
+        if constexpr (F16) {
+            if (k + 1 < nk) post_tile_scale(k + 1);  // pu, pv, dla hold tile k + 1's rows
         }
         __syncthreads();
         {
@@ -762,6 +978,11 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     }
 
     float* out = slab + static_cast<int64_t>(blockIdx.x) * SL;
+    if constexpr (F16) {
+        const float us = lg_pow2f(-tcur);
+#pragma unroll
+        for (int t = 0; t < G::KT; ++t) dwa[t] *= us;
+    }
 #pragma unroll
     for (int t = 0; t < G::KT; ++t)
 #pragma unroll
@@ -811,16 +1032,33 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         }
     }
     if constexpr (STREAM) {
-        if (nk > 0) scatter_tile(nk - 1);  // the last tile's rows and events were stored before the barriers above
+        if (nk > 0) {  // the last tile's rows and events were stored before the barriers above
+            post_g0();
+            __syncthreads();
+            scatter_tile(nk - 1);
+        }
     }
 }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+#ifdef LG_KERNEL_LAB
+inline int kEdgeLab(int flags) { return (flags >> 28) & 7; }
+#else
+inline int kEdgeLab(int) { return 0; }
+#endif
+
 // STREAM dynamic LDS: the images, the dfeat rows, two event blocks, the open nodes' sums
-int64_t edge_stream_lds(int64_t D, const EdgeScatter& sc) {
-    const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS, TR = 2048 / D;
-    return base + TR * (2 * D + 4) * 4 + 2 * int64_t{sc.bw} * 4 + int64_t{sc.nslots} * D * 4;
+// the backward's transform: the f16x2 split on the fp32 tier unless LG_F_BF16X3 asks for the
+// 3-way bf16 split; LG_F_BF16: one bf16 product
+bool edge_bwd_f16(int flags) { return !(flags & LG_F_BF16) && !(flags & LG_F_BF16X3); }
+int64_t edge_bwd_base_lds(int64_t D, int flags) {
+    const bool f16 = edge_bwd_f16(flags);
+    return D == 64 ? EG<64>::bwd_lds(f16) : EG<32>::bwd_lds(f16);
+}
+int64_t edge_stream_lds(int64_t D, int flags, const EdgeScatter& sc) {
+    const int64_t base = edge_bwd_base_lds(D, flags), TR = 2048 / D;
+    return base + TR * (2 * D + 4) * 4 + 2 * int64_t{sc.bw} * 4 + D * 4 + int64_t{sc.nslots} * D * 4;
 }
 
 int64_t tile_rows(int64_t D) { return 2048 / D; }
@@ -926,30 +1164,34 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
         if (hipMemsetAsync(slab, 0, SL * grid * sizeof(float), s) != hipSuccess) return LG_EHIP;
         if (hipMemsetAsync(dslab, 0, grid * sizeof(double), s) != hipSuccess) return LG_EHIP;
     } else {
-        const bool bf = (flags & LG_F_BF16) != 0;
+        const bool bf = (flags & LG_F_BF16) != 0, f16 = edge_bwd_f16(flags);
         const bool stream = scat && scat->spipe;
-        const int64_t lds = stream ? edge_stream_lds(D, *scat)
-                          : scat ? EG<64>::BWD_LDS * (D == 64) + EG<32>::BWD_LDS * (D == 32) + 4 * (N + 1 + 2 * P) : 0;
-#define LG_EDGE_BWD(DD, BFB)                                                                                      \
+        const int64_t base = edge_bwd_base_lds(D, flags);
+        const int64_t lds = stream ? edge_stream_lds(D, flags, *scat) : scat ? base + 4 * (N + 1 + 2 * P) : base;
+#define LG_EDGE_BWD(DD, BFB, F16B)                                                                                \
     do {                                                                                                          \
         if (stream) {                                                                                             \
-            if (!allow_lds(k_edge_bwd<DD, BFB, 2>, lds)) return LG_EHIP;                                           \
-            lg_launch(k_edge_bwd<DD, BFB, 2>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab,    \
-                      dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                               \
+            if (!allow_lds(k_edge_bwd<DD, BFB, 2, F16B>, lds)) return LG_EHIP;                                     \
+            lg_launch(k_edge_bwd<DD, BFB, 2, F16B>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe,    \
+                      slab, dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                         \
         } else if (scat) {                                                                                        \
-            if (!allow_lds(k_edge_bwd<DD, BFB, 1>, lds)) return LG_EHIP;                                           \
-            lg_launch(k_edge_bwd<DD, BFB, 1>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, slab,    \
-                      dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                               \
+            if (!allow_lds(k_edge_bwd<DD, BFB, 1, F16B>, lds)) return LG_EHIP;                                     \
+            lg_launch(k_edge_bwd<DD, BFB, 1, F16B>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe,    \
+                      slab, dslab, sb, sn, fdP, BP, ntiles, scale, *scat);                                         \
         } else {                                                                                                  \
-            if (!allow_lds(k_edge_bwd<DD, BFB>, EG<DD>::BWD_LDS)) return LG_EHIP;                                 \
-            lg_launch(k_edge_bwd<DD, BFB>, grid, NT, EG<DD>::BWD_LDS, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe, \
+            if (!allow_lds(k_edge_bwd<DD, BFB, 0, F16B>, lds)) return LG_EHIP;                                     \
+            lg_launch(k_edge_bwd<DD, BFB, 0, F16B>, grid, NT, lds, s, ends, h, w1, w2, hid, dlogits, ldo, dpipe,    \
                       slab, dslab, sb, sn, fdP, BP, ntiles, scale, none);                                          \
         }                                                                                                         \
     } while (0)
         if (D == 64) {
-            if (bf) LG_EDGE_BWD(64, true); else LG_EDGE_BWD(64, false);
+            if (bf) LG_EDGE_BWD(64, true, false);
+            else if (f16) LG_EDGE_BWD(64, false, true);
+            else LG_EDGE_BWD(64, false, false);
         } else {
-            if (bf) LG_EDGE_BWD(32, true); else LG_EDGE_BWD(32, false);
+            if (bf) LG_EDGE_BWD(32, true, false);
+            else if (f16) LG_EDGE_BWD(32, false, true);
+            else LG_EDGE_BWD(32, false, false);
         }
 #undef LG_EDGE_BWD
     }
@@ -988,13 +1230,13 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                        static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0, sched_hdr[5],
                        reinterpret_cast<const int4*>(sched + sched_hdr[10]),
                        reinterpret_cast<const uint32_t*>(sched + sched_hdr[11]), sched + sched_hdr[12],
-                       sched_hdr[9], sched_hdr[6], sched_hdr[8], sched_hdr[7]};
+                       sched_hdr[9], sched_hdr[6], sched_hdr[8], sched_hdr[7], kEdgeLab(flags)};
         // STREAM when the open nodes' sums fit beside the images (L-TOWN-A at D = 64: 23 of them)
-        if (edge_stream_lds(D, sc) <= 160 * 1024)
+        if (edge_stream_lds(D, flags, sc) <= 160 * 1024)
             return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
                                  flags, dropout_p, workspace, ws_bytes, stream, &sc);
     }
-    const int64_t base = D == 64 ? EG<64>::BWD_LDS : EG<32>::BWD_LDS;
+    const int64_t base = edge_bwd_base_lds(D, flags);
     if (P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
         // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
         const int rc = edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
@@ -1004,7 +1246,7 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
     }
     EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
                    static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0,
-                   static_cast<int>(cdiv(P, tile_rows(D))), nullptr, nullptr, nullptr, 0, 0, 0, 0};
+                   static_cast<int>(cdiv(P, tile_rows(D))), nullptr, nullptr, nullptr, 0, 0, 0, 0, kEdgeLab(flags)};
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
                          dropout_p, workspace, ws_bytes, stream, &sc);
 }

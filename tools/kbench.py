@@ -164,6 +164,8 @@ def main():
     ap.add_argument("--lab", default="", help="comma list of extra lg_gcn_fwd flag bits (kernel lab switches)")
     ap.add_argument("--edgelab", default="", help="comma list of lg_edge_head_fwd lab bits (1 nomfma, 2 noload, "
                                                    "4 nosplit; LEAKGNN_LIB=lib/lab build only)")
+    ap.add_argument("--edgebwdlab", default="", help="comma list of streamed EdgeHead backward lab bits (1 no dW1 "
+                                                      "MFMA, 2 no dfeat MFMA, 4 no scatter; LEAKGNN_LIB=lib/lab only)")
     ap.add_argument("--nmlab", default="", help="comma list of lg_gcn_fwd_nm schedules: v1 or bpc<n> (train mode)")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of a replayed HIP graph")
     ap.add_argument("--stamps", action="store_true", help="per-wave timeline of each --nmlab train launch "
@@ -422,11 +424,13 @@ def main():
             dh = torch.empty_like(xn)
             sched, hdr = inc.schedule(D)
             hdr_c = (ctypes.c_int32 * 16)(*hdr)
-            for name, sp, hp in [("edge_bwd_scat", None, None), ("edge_bwd_stream", sched, hdr_c)]:
-                g = lambda sp=sp, hp=hp: check(lib.lg_edge_head_bwd_scatter(
+            labs = [(f"edge_bwd_stream_lab{v}", sched, hdr_c, v << 28)
+                    for v in (int(x) for x in args.edgebwdlab.split(",") if x)]
+            for name, sp, hp, lb in [("edge_bwd_scat", None, None, 0), ("edge_bwd_stream", sched, hdr_c, 0)] + labs:
+                g = lambda sp=sp, hp=hp, lb=lb: check(lib.lg_edge_head_bwd_scatter(
                     ptr(inc.ends), ptr(xn), ptr(W1), ptr(W2), ptr(hid), ptr(dl1), P + 1, ptr(dpipe), ptr(dW1), ptr(db1),
                     ptr(dW2), ptr(db2), ptr(inc.rowptr), ptr(inc.item), ptr(sp) if sp is not None else None, hp,
-                    ptr(dpool), ptr(dh), B, N, P, D, 128, nat.LG_F_DROPOUT | nat.LG_F_NODE_MAJOR, 0.1, ptr(ws),
+                    ptr(dpool), ptr(dh), B, N, P, D, 128, nat.LG_F_DROPOUT | nat.LG_F_NODE_MAJOR | lb, 0.1, ptr(ws),
                     ws.numel(), cs()), name)
                 t = timeit(g, args.iters)
                 res[name] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
