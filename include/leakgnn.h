@@ -349,18 +349,16 @@ int lg_gcn_bwd_nm(const int32_t* nodetab_t, const int32_t* pairs_t, const float*
  * 4 (l % (D/4)) + i  ->  N * ceil(B/16) * 128 bytes (1/32 of y).  lg_gcn_bwd_nm_bits =
  * lg_gcn_bwd_nm that, under LG_F_MASK_IN with ymask non-NULL, reads the mask from those
  * bits instead of gathering y (y may then be NULL).  Same results as the y path. */
-/* ABI 17: the default fp32-tier transform of lg_gcn_fwd_nm[_bits] is the 2-way fp16 split
- * with power-of-two block scaling (LG_F_F16X2; |y - y_exact| ~ 4e-7 of max |y|, against
- * ~1e-8 for the 3-way bf16 split it replaces, which LG_F_NM3 keeps), run by the producer /
- * consumer pipeline (LG_F_PC). */
+/* The fp32-tier forward transform: see the LG_F_PC / LG_F_BF16X3 / LG_F_NM3 flags above. */
 int lg_gcn_fwd_nm_bits(const int32_t* nodetab, const int32_t* pairs, const float* x, const float* W,
                        const float* bias, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap,
                        int flags, float dropout_p, uint64_t seed, uint32_t salt, lg_stream_t stream,
                        uint16_t* ymask);
-/* lg_gcn_bwd_nm[_bits] lab variants (default: the 3-way bf16 split in the per-wave pipeline,
- * the fastest measured): LG_F_F16X2 the 2-way fp16 split (block-scaled, |err| ~3e-7 of
- * scale); LG_F_F16X2 | LG_F_PC at D = 64 the producer / consumer kernel.  Same results
- * within that tolerance. */
+/* lg_gcn_bwd_nm[_bits] transform (ABI 22): on the fp32 tier both GEMMs (dx^T = W^T t^T,
+ * dW = t^T x) run on the 2-way fp16 split with power-of-two scales — W^T per workgroup, each
+ * 16-row tile's t and x blocks per tile — (|err| ~1e-7 of scale); LG_F_BF16X3 restores the
+ * 3-way bf16 split (~1e-8).  Measured equal in time at B = 256 (the kernel is bound by its
+ * gathers, not the transform); LG_F_BF16: one bf16 product. */
 int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, const float* y,
                        const float* x, const float* W, float* dx_out, float* dW, float* db,
                        const int32_t* node_slot, float* dnode_bias, int64_t B, int64_t N, int64_t D,
@@ -480,7 +478,10 @@ int lg_edge_head_fwd(const int64_t* ends, const float* h, const float* w1, const
 /* Backward of lg_edge_head_fwd: hid (its hidden-layer output) and dlogits (row stride
  * ldo) -> dpipe fp32 [B][P][2][D] (grads w.r.t. h_u, h_v per pipe), dw1/db1/dw2/db2
  * (overwritten; deterministic fixed-order reduction of per-workgroup slabs).  flags and
- * dropout_p as in the forward (the keep mask is read back as [hid > 0]). */
+ * dropout_p as in the forward (the keep mask is read back as [hid > 0]).  Transform (ABI
+ * 22): on the fp32 tier the f16x2 split — g rows scaled per pipe row from |dlogit| (dpipe
+ * independent of which rows share a tile), W1^T per wave, dW1's products per tile (features
+ * scaled by 2^(T - sg(row))); LG_F_BF16X3: the 3-way bf16 split; LG_F_BF16: one product. */
 int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden);
 int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const float* w2,
                      const float* hid, const float* dlogits, int64_t ldo, float* dpipe,

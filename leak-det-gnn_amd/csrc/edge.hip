@@ -141,11 +141,6 @@ __device__ __forceinline__ void st_split2h(uint16_t* img, int pl, int off, const
     *reinterpret_cast<lg_u32x2*>(img + off) = lg_u32x2{a0, b0};
     *reinterpret_cast<lg_u32x2*>(img + pl + off) = lg_u32x2{a1, b1};
 }
-__device__ __forceinline__ f32x4 mfma_f16x2(const lg_f16x8 (&a)[2], const lg_f16x8 (&b)[2], f32x4 c) {
-    c = mfma_h(a[1], b[0], c);  // smallest terms first
-    c = mfma_h(a[0], b[1], c);
-    return mfma_h(a[0], b[0], c);
-}
 // max of a non-negative float's bits over the 16 lanes of a DPP row (row_ror within the row)
 __device__ __forceinline__ uint32_t lg_row16_max_bits(uint32_t m) {
     m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0xB1, 0xF, 0xF, false)));

@@ -1018,7 +1018,13 @@ struct NbX0 {
     uint32_t S;
     const int32_t* pos_slot;
 };
-template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false, bool X0 = false>
+// F16 (the fp32 tier's default, ABI 22): both GEMMs on the 2-way f16 split (split_bf16.h
+// f16x2: 3 f16 MFMAs per product instead of 6 bf16 ones, half the split VALU and W^T planes)
+// with power-of-two scales: W^T per workgroup (2^sW), a tile's t and x blocks per tile (the
+// wave's own tile: a wave max each, 2^st, 2^sx).  dx^T is unscaled by 2^-(sW + st); dW
+// accumulates in units of 2^T, T = st + sx of the latest tile, the accumulators rescaled
+// (exactly) when T changes and unscaled once at the end.
+template <int D, bool MASK_IN, bool NB, bool BF = false, bool MB = false, bool X0 = false, bool F16 = false>
 __global__ void __launch_bounds__(64 * kNmBwdWaves3, 2)
 k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, const float* __restrict__ dy,
               const float* __restrict__ yv, const float* __restrict__ x, const float* __restrict__ W,
@@ -1137,11 +1143,23 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         issue(nm_rec(tab, N + n0), n0, b00, nb00, pslot_of(n0));  // schedule section
     }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
+    static_assert(!(F16 && BF), "one transform");
+    int sW = 0;  // F16: W's scale exponent (every wave reads all of W for its max: no barrier)
+    if constexpr (F16) {
+        uint32_t m = 0;
+        for (int u = lane; u < D * D / 4; u += 64) {
+            const f32x4 v = ld4(W + 4 * u);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(v[c])));
+        }
+        sW = lg_f16_scale_exp_c(lg_wave_max_bits(m));
+    }
     {
         constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
         f32x4 wv[WPER];
 #pragma unroll
         for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
+        const float wsc = lg_pow2f(sW);
 #pragma unroll
         for (int u = 0; u < WPER; ++u) {
             const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
@@ -1151,6 +1169,13 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int c = 0; c < 4; ++c) {
                 const int e = (c4 + c) * SB + o;
                 const float w = wv[u][c];
+                if constexpr (F16) {
+                    const _Float16 h0 = static_cast<_Float16>(w * wsc);
+                    const _Float16 h1 = static_cast<_Float16>(w * wsc - static_cast<float>(h0));
+                    wsl[e] = __builtin_bit_cast(uint16_t, h0);
+                    wsl[D * SB + e] = __builtin_bit_cast(uint16_t, h1);
+                    continue;
+                }
                 const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
                 const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
                 const uint16_t h1 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r1));
@@ -1170,6 +1195,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
         for (int b = 0; b < G::CH; ++b) dw[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 dbacc = f32x4{0.f, 0.f, 0.f, 0.f};  // channels 4fg..4fg+3, summed over this lane's rows
+    int tc = 0;  // F16: dw holds dW x 2^tc
     f32x4 nbacc[NB ? G::CH : 1];              // NB: channels 16mt + 4q + reg over this lane's rows j
 #pragma unroll
     for (int mt = 0; mt < (NB ? G::CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1259,6 +1285,28 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         issue(nxt, nn, nb0, nnb, nslot);
         __builtin_amdgcn_sched_barrier(0);
 
+        int st = 0, sx = 0;  // F16: the tile's t and x scale exponents
+        if constexpr (F16) {
+            uint32_t mt4 = 0, mx4 = 0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    mt4 = max(mt4, __float_as_uint(fabsf(acc[k][c])));
+                    mx4 = max(mx4, __float_as_uint(fabsf(xv[k][c])));
+                }
+            st = lg_f16_scale_exp_c(lg_wave_max_bits(mt4));
+            sx = lg_f16_scale_exp_c(lg_wave_max_bits(mx4));
+            const int d = st + sx - tc;
+            if (d != 0) {  // two exact power-of-two factors (|d| <= 252)
+                const float r1 = lg_pow2f(d / 2), r2 = lg_pow2f(d - d / 2);
+#pragma unroll
+                for (int a = 0; a < G::CH; ++a)
+#pragma unroll
+                    for (int b = 0; b < G::CH; ++b) dw[a][b] = (dw[a][b] * r1) * r2;
+                tc = st + sx;
+            }
+        }
         wave_sync_nm();
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
@@ -1267,7 +1315,32 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         wave_sync_nm();
         // dW += t^T x over the tile's 16 rows: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
-        {
+        if constexpr (F16) {
+            const float tsc = lg_pow2f(st), xsc = lg_pow2f(sx);
+            lg_f16x4 xb[G::CH][2];
+#pragma unroll
+            for (int ni = 0; ni < G::CH; ++ni) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j] * xsc;
+                split2_f16_x4(v, xb[ni][0], xb[ni][1]);
+            }
+#pragma unroll
+            for (int mo = 0; mo < G::CH; ++mo) {
+                f32x4 v;
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j] * tsc;
+                lg_f16x4 a0, a1;
+                split2_f16_x4(v, a0, a1);
+#pragma unroll
+                for (int ni = 0; ni < G::CH; ++ni) {
+                    f32x4 c = dw[mo][ni];
+                    c = __builtin_amdgcn_mfma_f32_16x16x16f16(a1, xb[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][1], c, 0, 0, 0);
+                    dw[mo][ni] = __builtin_amdgcn_mfma_f32_16x16x16f16(a0, xb[ni][0], c, 0, 0, 0);
+                }
+            }
+        } else {
             lg_i16x4 xb[G::CH][3];
 #pragma unroll
             for (int ni = 0; ni < G::CH; ++ni) {
@@ -1310,6 +1383,26 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         f32x4 o[G::CH];
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (F16) {  // on the f16x2 split, unscaled by 2^-(sW + st)
+            const float tsc = lg_pow2f(st);
+#pragma unroll
+            for (int s2 = 0; s2 < D / 32; ++s2) {
+                lg_f16x8 bh[2];
+                split2_f16_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q) * tsc, ld4(tl + j * G::S + 32 * s2 + 8 * q + 4) * tsc,
+                              bh[0], bh[1]);
+#pragma unroll
+                for (int mt = 0; mt < G::CH; ++mt) {
+                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                    const lg_f16x8 ah[2] = {*reinterpret_cast<const lg_f16x8*>(wsl + ew),
+                                            *reinterpret_cast<const lg_f16x8*>(wsl + D * SB + ew)};
+                    o[mt] = mfma_f16x2(ah, bh, o[mt]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const float us = lg_pow2f(-(sW + st));
+#pragma unroll
+            for (int mt = 0; mt < G::CH; ++mt) o[mt] *= us;
+        } else {
 #pragma unroll
         for (int s2 = 0; s2 < D / 32; ++s2) {
             lg_bf16x8 b0f, b1f, b2f;
@@ -1332,6 +1425,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 o[mt] = mfma_bf(a0, b0f, o[mt]);
             }
             __builtin_amdgcn_sched_barrier(0);
+        }
         }
         if (mask_out & 1) {
 #pragma unroll
@@ -1362,6 +1456,13 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
                                                    dxs, tlo[k] + ob, 0, 0);
         lg_store_guard(vk);
+    }
+    if constexpr (F16) {  // dw back to units of 1 (two exact factors)
+        const float r1 = lg_pow2f(-(tc / 2)), r2 = lg_pow2f(-(tc - tc / 2));
+#pragma unroll
+        for (int a = 0; a < G::CH; ++a)
+#pragma unroll
+            for (int b = 0; b < G::CH; ++b) dw[a][b] = (dw[a][b] * r1) * r2;
     }
     if constexpr (NB) {  // fold the 16 row lanes j of each (q, reg)
 #pragma unroll
@@ -1967,6 +2068,8 @@ int nm_bwd(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, co
     float* slab = static_cast<float*>(workspace);
     hipStream_t s = lg_stream(stream);
     const bool bf = (flags & LG_F_BF16) != 0;
+    // fp32 tier: the f16x2 transform unless LG_F_BF16X3 asks for the 3-way bf16 split
+    const bool f16 = !bf && !(flags & LG_F_BF16X3);
     const NbX0 xz = x0 ? *x0 : NbX0{nullptr, nullptr, 1.f, 0u, nullptr};
     // k_gcn_bwd_nm3: the 3-way bf16 split (fp32 tier) or the single bf16 product (LG_F_BF16)
     int grid = 1;
@@ -1978,18 +2081,20 @@ int nm_bwd(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, co
                   static_cast<uint32_t>(N), static_cast<uint32_t>(B), static_cast<uint32_t>(ngroups), fd, mask_out,
                   scale_in, scale_out, ymask, xz);
     };
+#define LG_NM_BWD_P(DD, MI, NBB, MBB, X0B)                                                                        \
+    launch(bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MBB, X0B>                                                        \
+              : (f16 ? k_gcn_bwd_nm3<DD, MI, NBB, false, MBB, X0B, true> : k_gcn_bwd_nm3<DD, MI, NBB, false, MBB, X0B>), \
+           Nb3Lds<DD, MI>::BYTES)
 #define LG_NM_BWD(DD, MI, NBB)                                                                                     \
     do {                                                                                                           \
         if constexpr (!MI) {                                                                                       \
             if (x0) {                                                                                              \
-                launch(bf ? k_gcn_bwd_nm3<DD, false, NBB, true, false, true>                                       \
-                          : k_gcn_bwd_nm3<DD, false, NBB, false, false, true>, Nb3Lds<DD, false>::BYTES);          \
+                LG_NM_BWD_P(DD, false, NBB, false, true);                                                          \
                 break;                                                                                             \
             }                                                                                                      \
         }                                                                                                          \
-        launch((MI && mbits) ? (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true, MI> : k_gcn_bwd_nm3<DD, MI, NBB, false, MI>)  \
-                             : (bf ? k_gcn_bwd_nm3<DD, MI, NBB, true> : k_gcn_bwd_nm3<DD, MI, NBB, false>),         \
-               Nb3Lds<DD, MI>::BYTES);                                                                             \
+        if (MI && mbits) LG_NM_BWD_P(DD, MI, NBB, MI, false);                                                      \
+        else LG_NM_BWD_P(DD, MI, NBB, false, false);                                                               \
     } while (0)
 #define LG_NM_BWD_D(DD)                                  \
     do {                                                 \
@@ -2005,6 +2110,7 @@ int nm_bwd(const int32_t* nodetab_t, const int32_t* pairs_t, const float* dy, co
     else LG_NM_BWD_D(32);
 #undef LG_NM_BWD_D
 #undef LG_NM_BWD
+#undef LG_NM_BWD_P
     LG_RET_IF_LAUNCH_FAILED();
     const int64_t L = D * D + 2 * D;
     const LgSlabSeg segs[3] = {{0, D * D, dW}, {D * D, D, db}, {D * D + D, D, dnode_bias}};

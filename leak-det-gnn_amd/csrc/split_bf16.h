@@ -134,6 +134,12 @@ __device__ __forceinline__ void split2_f16_x8(const f32x4& u, const f32x4& v, lg
 __device__ __forceinline__ f32x4 mfma_h(const lg_f16x8& a, const lg_f16x8& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
+// a x b on the f16x2 split of both operands (hi, lo): the three products, smallest terms first
+__device__ __forceinline__ f32x4 mfma_f16x2(const lg_f16x8 (&a)[2], const lg_f16x8 (&b)[2], f32x4 c) {
+    c = mfma_h(a[1], b[0], c);
+    c = mfma_h(a[0], b[1], c);
+    return mfma_h(a[0], b[0], c);
+}
 // 2^e as a float for e in [-126, 127] (clamped)
 __device__ __forceinline__ float lg_pow2f(int e) {
     e = e < -126 ? -126 : (e > 127 ? 127 : e);
