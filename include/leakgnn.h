@@ -375,8 +375,9 @@ int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const f
  *            lg_gcn_fwd_nm_bits (ABI 15),
  * from which a non-sensor element is x0 = bit ? relu(bias) * scale : 0 exactly.
  * lg_gcn_fwd_nm_x0 is lg_gcn_fwd_nm_bits of layer 0 reading (xs0, x0bits, node_bias) through a
- * sensor-marked node table (lg_nm_table_sensor_mark): the same sums in the same order, so y is
- * bit-identical to the dense forward.  lg_gcn_bwd_nm_x0 is lg_gcn_bwd_nm_bits of layer 0 (no
+ * sensor-marked node table (lg_nm_table_sensor_mark): the gather waves read one 2-byte mask word
+ * per neighbour block and the transform waves add the sensor neighbours' xs0 rows (ABI 22), so
+ * y equals the dense forward up to that summation order (~1e-7 of scale).  lg_gcn_bwd_nm_x0 is lg_gcn_bwd_nm_bits of layer 0 (no
  * MASK_IN) with the tile's own x block from (xs0, x0bits); pos_slot_t = the transposed table's
  * schedule-section slots.  The node init and the layer share one Dropout (detector.py:190,
  * 201): flags' LG_F_DROPOUT and dropout_p describe both.  lg_node_init_expand materialises x0

@@ -497,6 +497,10 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #define LG_PC_NPF 3
 #endif
 constexpr int kPcRing = LG_PC_RING;
+// ring-slot metadata: n, b0, nb, X0's sensor entries (count, then up to kPcSens (slot, w) pairs)
+constexpr int kPcSens = 3;
+constexpr int kPcMeta = 16;
+static_assert(4 + 2 * kPcSens <= kPcMeta, "meta words");
 
 template <int D, int kPcProd, int NC>
 struct PcLds {  // floats
@@ -506,8 +510,8 @@ struct PcLds {  // floats
     static constexpr int WOFF = 0;                                  // W [out][in] * fold (fp32), bias * fold
     static constexpr int XOFF = D * WS + D;                         // per-wave max|W| bits (F16)
     static constexpr int FOFF = XOFF + 16;                          // ready[16], done[kPcProd * NC], fin[4], ctr
-    static constexpr int MOFF = FOFF + 16 + kPcProd * NC + 8;       // per (producer, slot): n, b0, nb, pad
-    static constexpr int ROFF = MOFF + 4 * kPcProd * kPcRing;       // the rings
+    static constexpr int MOFF = FOFF + 16 + kPcProd * NC + 8;       // per (producer, slot): kPcMeta words
+    static constexpr int ROFF = MOFF + kPcMeta * kPcProd * kPcRing;  // the rings
     static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
@@ -666,38 +670,36 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         uint32_t lo[2][G::K];
         NmRec rec[2];
         uint32_t tn[2], tb0[2], tnb[2];
-        // one neighbour's block: its rows into blk (under X0 a sensor row of xs0) and, X0, its mask
-        // word into bw.  Both loads are always issued, the one that does not apply (and both for
-        // an absent neighbour, have == false) out of range (zeros, no memory access): a load
-        // under a branch would make the compiler wait for it where the branch merges.
+        // one neighbour's block: its rows into blk or, X0, its mask word into bw (an absent
+        // neighbour, have == false, and X0's sensor neighbours read out of range: zero bits).
+        // X0's sensor rows are added by the consumer (ring-slot metadata), so the producer issues
+        // one 2-byte load per neighbour instead of the rows.
         auto load_nb = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K], uint32_t& bw) {
-            bool rows = have;
             if constexpr (X0) {
                 const bool sens = (c & kLgSensorCol) != 0;
                 bw = __builtin_amdgcn_raw_buffer_load_b16(
                     brs, have && !sens ? nm_mask_off(static_cast<uint32_t>(c), b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane,
                     0, 0);
-                rows = have && sens;
-                c &= ~kLgSensorCol;
+                return;
             }
+            const bool rows = have;
             const uint32_t base = rows ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
             const __amdgpu_buffer_rsrc_t rs = rows ? xrs : xrs0;
 #pragma unroll
             for (int k = 0; k < G::K; ++k)
                 blk[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lk[k], base, 0));
         };
-        // slot k of a loaded neighbour block as values.  X0: the sum of the row values (zeros for
-        // a non-sensor neighbour) and the mask-word values (zero bits for a sensor neighbour), one
-        // of them zero, so exact and branch-free (a branch on the neighbour kind here made the
-        // compiler read the rest-of-row mask words before their loads had landed: wrong bits for
-        // slots k >= 1 of degree-5 nodes, r04f)
+        // slot k of a loaded neighbour block as values.  X0: from the mask word (zero for a
+        // sensor neighbour), branch-free (a branch on the neighbour kind here made the compiler
+        // read the rest-of-row mask words before their loads had landed: wrong bits for slots
+        // k >= 1 of degree-5 nodes, r04f)
         auto nbv = [&](int c, const f32x4 (&blk)[G::K], uint32_t bw, int k) -> f32x4 {
             (void)c;
             if constexpr (X0) {
                 const uint32_t w = bw >> (4 * k);
                 f32x4 r;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) r[i] = blk[k][i] + ((w >> i) & 1u ? v0[i] : 0.f);
+                for (int i = 0; i < 4; ++i) r[i] = (w >> i) & 1u ? v0[i] : 0.f;
                 return r;
             }
             return blk[k];
@@ -779,6 +781,23 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vr, vw, k));
                 }
             }
+            // X0: the row's sensor entries (the consumer adds their rows): up to kPcSens in the
+            // slot metadata, more (a node with over kPcSens sensor neighbours) flagged for a scan
+            uint32_t nsx = 0, ss0 = 0, ss1 = 0, ss2 = 0, sw0 = 0, sw1 = 0, sw2 = 0;
+            if constexpr (X0) {
+                auto addsens = [&](int2 pe) {
+                    if (!(pe.x & kLgSensorCol)) return;
+                    const uint32_t sv = static_cast<uint32_t>(pe.x & ~kLgSensorCol), wv = static_cast<uint32_t>(pe.y);
+                    if (nsx == 0) { ss0 = sv; sw0 = wv; }
+                    if (nsx == 1) { ss1 = sv; sw1 = wv; }
+                    if (nsx == 2) { ss2 = sv; sw2 = wv; }
+                    ++nsx;
+                };
+#pragma unroll
+                for (int i = 0; i < kLgNmInline; ++i)
+                    if (e0 + i < e1) addsens(cur.p[i]);
+                for (int e = e0 + kLgNmInline; e < e1; ++e) addsens(pairs[e]);
+            }
             const int sl = static_cast<int>(t % R);
             const uint32_t mn = tn[b], mnb = tnb[b];
             // buffer b is free again: tile t + 2 goes in flight before the hand-off waits
@@ -789,10 +808,19 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
             for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
             if (lane == 0) {
-                uint32_t* m = meta + 4 * (prod * R + sl);
+                uint32_t* m = meta + kPcMeta * (prod * R + sl);
                 m[0] = mn;
                 m[1] = b0;
                 m[2] = mnb;
+                if constexpr (X0) {
+                    m[3] = nsx;
+                    m[4] = ss0;
+                    m[5] = sw0;
+                    m[6] = ss1;
+                    m[7] = sw1;
+                    m[8] = ss2;
+                    m[9] = sw2;
+                }
             }
             pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
 #ifdef LG_NM3_STAMPS
@@ -827,6 +855,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     // ---------------- consumer: transform + epilogue
     const __amdgpu_buffer_rsrc_t yrs = nm_rsrc(y, bytes);
+    const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : 0);  // X0: xs0
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];
 #pragma unroll
@@ -866,7 +895,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (!pc_wait_or_fin(&ready[prod], &fin[prod], static_cast<uint32_t>(t + 1))) break;
         const int sl = static_cast<int>(t % R);
         float* slot = ring + sl * LY::TILE;
-        const uint32_t* m = meta + 4 * (prod * R + sl);
+        const uint32_t* m = meta + kPcMeta * (prod * R + sl);
         const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
                        nb = __builtin_amdgcn_readfirstlane(m[2]);
         f32x4 bq[KS][2];
@@ -874,6 +903,34 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         for (int s2 = 0; s2 < KS; ++s2) {
             bq[s2][0] = ld4(slot + LY::tix(j, 8 * s2 + 2 * q));
             bq[s2][1] = ld4(slot + LY::tix(j, 8 * s2 + 2 * q + 1));
+        }
+        if constexpr (X0) {  // the tile's sensor neighbours: w x (their xs0 rows), in entry order
+            const uint32_t ns = __builtin_amdgcn_readfirstlane(m[3]);
+            auto addrow = [&](uint32_t sv, float wv) {
+#pragma unroll
+                for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t off = static_cast<uint32_t>(j) < nb
+                                                 ? ((sv * B + b0 + j) * D + 4 * (8 * s2 + 2 * q + h)) * 4u
+                                                 : kNm3RowOob;
+                        pk_fma4(bq[s2][h], wv,
+                                __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0)));
+                    }
+            };
+            if (ns > static_cast<uint32_t>(kPcSens)) {  // rare: scan the node's row (node-order section)
+                const NmRec r = nm_rec(tab, n);
+                for (int i = 0; i < kLgNmInline; ++i)
+                    if (r.e0 + i < r.e1 && (r.p[i].x & kLgSensorCol))
+                        addrow(static_cast<uint32_t>(r.p[i].x & ~kLgSensorCol), __int_as_float(r.p[i].y));
+                for (int e = r.e0 + kLgNmInline; e < r.e1; ++e) {
+                    const int2 pe = pairs[e];
+                    if (pe.x & kLgSensorCol) addrow(static_cast<uint32_t>(pe.x & ~kLgSensorCol), __int_as_float(pe.y));
+                }
+            } else {
+                for (uint32_t i = 0; i < ns; ++i)
+                    addrow(__builtin_amdgcn_readfirstlane(m[4 + 2 * i]), __uint_as_float(__builtin_amdgcn_readfirstlane(m[5 + 2 * i])));
+            }
         }
         uint32_t st = 0;
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);

@@ -280,18 +280,18 @@ k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
         }
         return;
     }
-    // non-sensor tiles: one lane of one tile per thread
+    // non-sensor tiles: one lane of one tile per thread.  The node's slot, the bias and (with a
+    // device seed) the dropout key are independent loads, all in flight before the first use.
     const uint32_t t = (blockIdx.x - static_cast<uint32_t>(GS)) * 4 + threadIdx.x / 64;
-    if (t >= N * ngroups) return;
-    const uint32_t n = lg_div(t, fdG), grp = t - n * ngroups;
-    if (slot[n] >= 0) return;
+    const bool tv = t < N * ngroups;
+    const uint32_t n = tv ? lg_div(t, fdG) : 0u, grp = t - n * ngroups;
     const int l = threadIdx.x % 64, rl = l / LPR, fg = l % LPR;
+    const int32_t sl = slot[n];
+    const f32x4 bv = ld4(bias + 4 * fg);
+    if (!tv || sl >= 0) return;
     uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
-    {
-        const f32x4 bv = ld4(bias + 4 * fg);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * (dropout ? scale : 1.0f) > 0.f) << i;
-    }
+    for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * (dropout ? scale : 1.0f) > 0.f) << i;
     uint32_t w = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {

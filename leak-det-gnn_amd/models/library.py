@@ -390,7 +390,7 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     nodetab_s, pairs_s, pos_slot_t (ops.SensorMarks; node-major, L >= 1): x_0 stays
     compressed (lg_node_init_bits_fwd): the returned x_0 is its sensor rows (S, B, D), x0bits
     [x_0 > 0] of every row (int16, ymask's layout), and layer 0 reads them through the marked
-    table (lg_gcn_fwd_nm_x0, bit-identical to the dense forward).  Otherwise x0bits is empty."""
+    table (lg_gcn_fwd_nm_x0: the dense forward up to the order of its sums).  Otherwise x0bits is empty."""
     lib = load_library()
     h_s, proj_weight, node_bias = _c(h_s), _c(proj_weight), _c(node_bias)
     weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]

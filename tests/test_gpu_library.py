@@ -311,3 +311,64 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
             assert_close(g, ref, rtol=1e-5, atol=1e-6 * ref.abs().max().item(), what=n)
         else:
             assert torch.equal(g, ref), f"{n}: fused scatter differs"
+
+
+@pytest.mark.parametrize("D", [64, 32])
+@pytest.mark.parametrize("B", [5, 40])
+def test_streamed_scatter_odd_graph(D, B):
+    """The streamed node scatter (ABI 22) on a graph built to hit its corner cases: a hub of
+    degree 40 (more incidences than a tile has rows, events with many incidences), a self-loop
+    pipe (both roles of one row on one node), nodes without pipes (dh = dpool / N only), windows
+    whose last tile is short.  dh must equal lg_edge_head_bwd + lg_pipe_scatter_bwd over the
+    schedule's incidence CSR bit for bit; the EdgeHead weight gradients within 1e-5."""
+    import ctypes
+    from models import _native as nat
+    from models import ops
+    lib = nat.load_library()
+    rng = np.random.default_rng(D + B)
+    N = 60
+    ring = [(i, i + 1) for i in range(1, 44)]
+    hub = [(0, int(j)) for j in rng.permutation(np.arange(1, 45))[:40]]
+    ends_np = np.array(ring + hub + [(7, 7)], np.int64)  # nodes 45..59: no pipes
+    P = ends_np.shape[0]
+    inc = ops.Incidence.build(torch.from_numpy(ends_np), N, DEV)
+    sched, hdr = inc.schedule(D)
+    assert sched is not None and hdr[9] == N - 45  # the nodes without pipes
+    gen = torch.Generator().manual_seed(D * 100 + B)
+    h = torch.randn(N, B, D, generator=gen).to(DEV)  # node-major
+    W1 = (torch.randn(128, 3 * D, generator=gen) / 8).to(DEV)
+    b1 = (torch.randn(128, generator=gen) / 4).to(DEV)
+    W2 = (torch.randn(1, 128, generator=gen) / 8).to(DEV)
+    b2 = torch.randn(1, generator=gen).to(DEV)
+    st = ops.stream_of(h)
+    logits = torch.empty(B, P + 1, device=DEV)
+    hid = torch.empty(B * P, 128, device=DEV)
+    fl = nat.LG_F_NODE_MAJOR | nat.LG_F_DROPOUT
+    ops.check(lib.lg_edge_head_fwd(ops.ptr(inc.ends), ops.ptr(h), ops.ptr(W1), ops.ptr(b1), ops.ptr(W2), ops.ptr(b2),
+                                   ops.ptr(logits), P + 1, ops.ptr(hid), B, N, P, D, 128, fl, 0.1, 77, 5, st), "fwd")
+    dl = torch.randn(B, P + 1, generator=gen).to(DEV)
+    dpool = torch.randn(B, D, generator=gen).to(DEV)
+    ws = torch.empty(int(lib.lg_edge_head_bwd_workspace_bytes(B, P, D, 128)), device=DEV, dtype=torch.uint8)
+    hdr_c = (ctypes.c_int32 * 16)(*hdr)
+    outs = []
+    for streamed in (True, False):
+        dh = torch.full((N, B, D), float("nan"), device=DEV)
+        dpipe = torch.empty(B, P, 2, D, device=DEV)
+        g = [torch.empty_like(W1), torch.empty_like(b1), torch.empty_like(W2), torch.empty(1, device=DEV)]
+        if streamed:
+            ops.check(lib.lg_edge_head_bwd_scatter(
+                ops.ptr(inc.ends), ops.ptr(h), ops.ptr(W1), ops.ptr(W2), ops.ptr(hid), ops.ptr(dl), P + 1, ops.ptr(dpipe),
+                *(ops.ptr(t) for t in g), ops.ptr(inc.rowptr), ops.ptr(inc.item), ops.ptr(sched), hdr_c, ops.ptr(dpool),
+                ops.ptr(dh), B, N, P, D, 128, fl, 0.1, ops.ptr(ws), ws.numel(), st), "streamed")
+        else:
+            ops.check(lib.lg_edge_head_bwd(ops.ptr(inc.ends), ops.ptr(h), ops.ptr(W1), ops.ptr(W2), ops.ptr(hid),
+                                           ops.ptr(dl), P + 1, ops.ptr(dpipe), *(ops.ptr(t) for t in g), B, N, P, D,
+                                           128, fl, 0.1, ops.ptr(ws), ws.numel(), st), "bwd")
+            ops.check(lib.lg_pipe_scatter_bwd(ops.ptr(inc.rowptr), ops.ptr(inc.item), ops.ptr(dpipe), ops.ptr(dpool),
+                                              ops.ptr(dh), B, N, P, D, nat.LG_F_NODE_MAJOR, st), "scatter")
+        torch.cuda.synchronize()
+        outs.append((dh, g))
+    assert not torch.isnan(outs[0][0]).any(), "a node row the streamed scatter never wrote"
+    assert torch.equal(outs[0][0], outs[1][0]), "streamed dh differs from the two launches"
+    for a, c, name in zip(outs[0][1], outs[1][1], ("dW1", "db1", "dW2", "db2")):
+        assert_close(a, c, rtol=1e-5, atol=1e-6 * c.abs().max().item(), what=name)

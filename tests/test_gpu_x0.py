@@ -1,9 +1,11 @@
 """The compressed node init (ABI 21) on MI355X: x_0 kept as its sensor rows plus [x_0 > 0]
 bits (lg_node_init_bits_fwd) and read by layer 0 through the sensor-marked node table
 (lg_gcn_fwd_nm_x0, lg_gcn_bwd_nm_x0).  The reference materialises x_0 = dropout(relu(
-sensor_to_node([h0, mask]))) (detector.py:179-190); every result here must be BIT-identical to
-the dense path (lg_node_init_proj_fwd + lg_gcn_fwd_nm_bits / lg_gcn_bwd_nm_bits), which the
-oracle tests pin to the reference."""
+sensor_to_node([h0, mask]))) (detector.py:179-190).  Checked against the dense path
+(lg_node_init_proj_fwd + lg_gcn_fwd_nm_bits / lg_gcn_bwd_nm_bits), which the oracle tests pin
+to the reference: the node init and the layer-0 backward bit for bit; the layer-0 forward
+within 1e-6 of its output scale (ABI 22: the sensor neighbours' terms are added after the
+others, by the consumer waves) with the same ReLU/dropout pattern wherever |y| clears that."""
 from __future__ import annotations
 
 import pytest
@@ -106,7 +108,15 @@ def test_layer0_x0_forward_and_backward_equal_dense(state, B, D, extra):
     ops.check(lib.lg_gcn_fwd_nm_x0(ops.ptr(mk.nodetab_s), ops.ptr(mk.pairs_s), ops.ptr(xs0), ops.ptr(bits),
                                    ops.ptr(nbias), ops.ptr(W), ops.ptr(b), ops.ptr(y_x), B, N, S, D, flags, p, 7, 1, st),
               "fwd x0")
-    assert torch.equal(y_x, y_d), "layer-0 forward on the compressed x0 differs from the dense forward"
+    # the sums' order differs (sensor terms last): fp32 tier within 1e-6 of scale; the bf16
+    # tier rounds z to bf16 before its single product, so one bf16 ulp (2^-8) of z can differ
+    tol = 1e-3 if extra == "bf16" else 1e-6
+    scale = y_d.abs().max().item()
+    err = (y_x - y_d).abs().max().item()
+    assert err <= tol * scale, f"layer-0 forward on the compressed x0: err {err:.3e} of scale {scale:.3e}"
+    # same relu / dropout decisions except where the pre-activation is within rounding of 0
+    flip = (y_x > 0) != (y_d > 0)
+    assert (torch.maximum(y_x.abs(), y_d.abs())[flip] <= tol * scale).all()
 
     dy = torch.randn(N, B, D, generator=gen).to(DEV)
     scale = 1.0 / (1.0 - p)
@@ -135,8 +145,8 @@ def test_layer0_x0_forward_and_backward_equal_dense(state, B, D, extra):
 @pytest.mark.parametrize("train", [False, True])
 def test_detector_compressed_x0_equals_dense(train):
     """The whole detector step with the node init compressed (the default) equals the dense node
-    init bit for bit: logits, loss and every parameter gradient (train mode: the same dropout
-    draws from the same seed)."""
+    init: logits and every parameter gradient within 1e-5 of their scale (train mode: the same
+    dropout draws from the same seed; the layer-0 forward sums its sensor terms last)."""
     from models.detector import LeakDetector
     sensors, pipes = lta_ids()
     torch.manual_seed(0)
@@ -155,6 +165,7 @@ def test_detector_compressed_x0_equals_dense(train):
         loss = torch.nn.functional.cross_entropy(logits, lab)
         loss.backward()
         res.append((logits.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
-    assert torch.equal(res[0][0], res[1][0]), "logits differ"
+    from helpers import assert_close
+    assert_close(res[1][0], res[0][0], rtol=1e-5, what="logits")
     for k in res[0][1]:
-        assert torch.equal(res[0][1][k], res[1][1][k]), f"grad {k} differs"
+        assert_close(res[1][1][k], res[0][1][k], rtol=1e-5, atol=0.0, what=f"grad {k}")

@@ -384,7 +384,7 @@ def main():
                                          nat.LG_F_MASK_IN | nat.LG_F_MASK_OUT, 1.0, 1.0, ptr(ws), ws.numel(), cs()), "bwd")
         t = timeit(f, args.iters)
         res["gcn_bwd"] = {"us": t, "GBps": (16 * B * N * D) / t / 1e3}
-    if "edge_fwd" in which or "edge_bwd" in which:
+    if "edge_fwd" in which or "edge_bwd" in which or "edge_bwd_stream" in which:
         W1 = torch.randn(128, 3 * D, device=dev) / 16
         b1 = torch.randn(128, device=dev)
         W2 = torch.randn(1, 128, device=dev) / 8
@@ -406,7 +406,8 @@ def main():
                 res[name] = {"us": t, "TFLOPs": 2 * B * P * 3 * D * 128 / t / 1e6}
         else:
             f()
-        if "edge_bwd" in which:
+        if "edge_bwd" in which or "edge_bwd_stream" in which:  # edge_bwd_stream alone: only the streamed launch
+            only_stream = "edge_bwd" not in which
             dl = torch.randn(B, P, device=dev)
             dpipe = torch.empty(B, P, 2, D, device=dev)
             dW1, db1, dW2, db2 = (torch.empty_like(t) for t in (W1, b1, W2, b2))
@@ -414,8 +415,9 @@ def main():
             f = lambda: check(lib.lg_edge_head_bwd(ptr(inc.ends), ptr(x), ptr(W1), ptr(W2), ptr(hid), ptr(dl), P,
                                                    ptr(dpipe), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), B, N, P, D, 128,
                                                    nat.LG_F_DROPOUT, 0.1, ptr(ws), ws.numel(), cs()), "edge bwd")
-            t = timeit(f, args.iters)
-            res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
+            if not only_stream:
+                t = timeit(f, args.iters)
+                res["edge_bwd"] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
             # with the node scatter fused, node-major h as in the step: per window (ABI 19) and
             # streamed per tile through the pipe schedule (ABI 22)
             xn = x.transpose(0, 1).contiguous()
@@ -426,7 +428,8 @@ def main():
             hdr_c = (ctypes.c_int32 * 16)(*hdr)
             labs = [(f"edge_bwd_stream_lab{v}", sched, hdr_c, v << 28)
                     for v in (int(x) for x in args.edgebwdlab.split(",") if x)]
-            for name, sp, hp, lb in [("edge_bwd_scat", None, None, 0), ("edge_bwd_stream", sched, hdr_c, 0)] + labs:
+            runs = [("edge_bwd_scat", None, None, 0), ("edge_bwd_stream", sched, hdr_c, 0)] + labs
+            for name, sp, hp, lb in (runs[1:2] if only_stream else runs):
                 g = lambda sp=sp, hp=hp, lb=lb: check(lib.lg_edge_head_bwd_scatter(
                     ptr(inc.ends), ptr(xn), ptr(W1), ptr(W2), ptr(hid), ptr(dl1), P + 1, ptr(dpipe), ptr(dW1), ptr(db1),
                     ptr(dW2), ptr(db2), ptr(inc.rowptr), ptr(inc.item), ptr(sp) if sp is not None else None, hp,
@@ -434,10 +437,11 @@ def main():
                     ws.numel(), cs()), name)
                 t = timeit(g, args.iters)
                 res[name] = {"us": t, "TFLOPs": 2 * 2 * B * P * 3 * D * 128 / t / 1e6}
-            g = lambda: check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe), ptr(dpool), ptr(dh),
-                                                      B, N, P, D, nat.LG_F_NODE_MAJOR, cs()), "pipe scatter")
-            t = timeit(g, args.iters)
-            res["pipe_scatter"] = {"us": t, "GBps": (B * P * 2 * D * 4 + B * N * D * 4) / t / 1e3}
+            if not only_stream:
+                g = lambda: check(lib.lg_pipe_scatter_bwd(ptr(inc.rowptr), ptr(inc.item), ptr(dpipe), ptr(dpool),
+                                                          ptr(dh), B, N, P, D, nat.LG_F_NODE_MAJOR, cs()), "pipe scatter")
+                t = timeit(g, args.iters)
+                res["pipe_scatter"] = {"us": t, "GBps": (B * P * 2 * D * 4 + B * N * D * 4) / t / 1e3}
     if "gru_fwd" in which or "gru_bwd" in which:
         S, L = 29, 36
         r = torch.randn(B, L, S, device=dev)
