@@ -500,7 +500,8 @@ int lg_edge_head_bwd(const int64_t* ends, const float* h, const float* w1, const
  * build), bit for bit.  Without a schedule (NULL, NULL), or when the open sums do not fit in
  * LDS, each workgroup owns whole windows and sums a window's node rows from its just-written
  * dpipe rows (ABI 19; the CSR staged in LDS), or, when the CSR does not fit either, the two
- * calls run.  dpipe: scratch [B][P][2][D] (untouched by the streamed path); dpool: NULL or
+ * calls run.  Both fused forms run one workgroup per window, so with fewer windows (B) than
+ * CUs the two calls run instead.  dpipe: scratch [B][P][2][D] (untouched by the streamed path); dpool: NULL or
  * [B][D] (lg_pool_head_bwd's dpooled, computed before this call); the workspace is
  * lg_edge_head_bwd_workspace_bytes.  A schedule for another (P, N, D) is LG_EINVAL. */
 int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,

@@ -1220,7 +1220,11 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
         return LG_EINVAL;  // a schedule built for another graph or width
     if (B == 0) return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D,
                                      hidden, flags, dropout_p, workspace, ws_bytes, stream, nullptr);
-    if (sched && P > 0 && B * N < kLgMaxRows) {
+    // the fused forms run one workgroup per window: with fewer windows than CUs most of the
+    // GPU would idle through the windows' tiles (C4: 64 windows of 235 tiles, 2.0 vs 1.1 ms per
+    // step), so the two launches take over there
+    const bool per_window = B >= lg_num_cus();
+    if (per_window && sched && P > 0 && B * N < kLgMaxRows) {
         EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
                        static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0, sched_hdr[5],
                        reinterpret_cast<const int4*>(sched + sched_hdr[10]),
@@ -1232,7 +1236,7 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                                  flags, dropout_p, workspace, ws_bytes, stream, &sc);
     }
     const int64_t base = edge_bwd_base_lds(D, flags);
-    if (P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
+    if (!per_window || P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
         // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
         const int rc = edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
                                      flags, dropout_p, workspace, ws_bytes, stream, nullptr);

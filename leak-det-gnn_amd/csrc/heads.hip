@@ -179,6 +179,8 @@ k_node_init_proj(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
 // each: the same per-row arithmetic as k_node_init_proj, so the rows are bit-identical),
 // posting each row's nibbles to LDS and storing the tile's mask words; the workgroups after
 // them write the non-sensor tiles' mask words, one lane of one tile per thread.
+// non-sensor tiles per thread of k_node_init_bits: 1 (r04m: 4 measured 14.1 us against 11.7)
+constexpr int kNibTiles = 1;
 template <int D, int DS>
 __global__ void __launch_bounds__(256)
 k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ sidx, const float* __restrict__ hs,
@@ -280,28 +282,40 @@ k_node_init_bits(const int32_t* __restrict__ slot, const int64_t* __restrict__ s
         }
         return;
     }
-    // non-sensor tiles: one lane of one tile per thread.  The node's slot, the bias and (with a
-    // device seed) the dropout key are independent loads, all in flight before the first use.
-    const uint32_t t = (blockIdx.x - static_cast<uint32_t>(GS)) * 4 + threadIdx.x / 64;
-    const bool tv = t < N * ngroups;
-    const uint32_t n = tv ? lg_div(t, fdG) : 0u, grp = t - n * ngroups;
+    // non-sensor tiles: one lane of kNibTiles tiles per thread (the workgroup's 4 x kNibTiles
+    // tiles, strided by 4): the tiles' slots, the bias and (with a device seed) the dropout key
+    // are independent loads, all in flight before the first use.
+    const uint32_t t0 = (blockIdx.x - static_cast<uint32_t>(GS)) * 4 * kNibTiles + threadIdx.x / 64;
     const int l = threadIdx.x % 64, rl = l / LPR, fg = l % LPR;
-    const int32_t sl = slot[n];
+    uint32_t tn[kNibTiles], tg[kNibTiles];
+    int32_t tsl[kNibTiles];
+#pragma unroll
+    for (int u = 0; u < kNibTiles; ++u) {
+        const uint32_t t = t0 + 4 * u;
+        const bool tv = t < N * ngroups;
+        tn[u] = tv ? lg_div(t, fdG) : 0u;
+        tg[u] = t - tn[u] * ngroups;
+        tsl[u] = tv ? slot[tn[u]] : 0;
+    }
     const f32x4 bv = ld4(bias + 4 * fg);
-    if (!tv || sl >= 0) return;
     uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
 #pragma unroll
     for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * (dropout ? scale : 1.0f) > 0.f) << i;
-    uint32_t w = 0;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const uint32_t b = 16 * grp + RPI * k + rl;
-        if (b < B) {
-            const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * N + n, 4 * fg, thr) : 0xFu;
-            w |= (kb & pos) << (4 * k);
+    for (int u = 0; u < kNibTiles; ++u) {
+        const uint32_t t = t0 + 4 * u;
+        if (t >= N * ngroups || tsl[u] >= 0) continue;  // past the end, or a sensor node's tile
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint32_t b = 16 * tg[u] + RPI * k + rl;
+            if (b < B) {
+                const uint32_t kb = dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * N + tn[u], 4 * fg, thr) : 0xFu;
+                w |= (kb & pos) << (4 * k);
+            }
         }
+        bits[static_cast<size_t>(t) * 64 + l] = static_cast<uint16_t>(w);
     }
-    bits[static_cast<size_t>(t) * 64 + l] = static_cast<uint16_t>(w);
 }
 
 // x0 materialised from its compressed form (lg_node_init_expand; diagnostics and tests):
@@ -660,7 +674,7 @@ extern "C" int lg_node_init_bits_fwd(const int32_t* sensor_slot, const int64_t* 
     hipStream_t s = lg_stream(stream);
     const int64_t tpi = 256 / (16 * (D / 4));
     const int GS = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(S * ngroups, tpi), 2 * lg_num_cus())));
-    const unsigned grid = static_cast<unsigned>(GS + ceil_div(N * ngroups, 4));
+    const unsigned grid = static_cast<unsigned>(GS + ceil_div(N * ngroups, 4 * kNibTiles));
     const lg_fastdiv fdG = lg_make_fastdiv(static_cast<uint32_t>(ngroups));
     const uint32_t B32 = static_cast<uint32_t>(B), N32 = static_cast<uint32_t>(N), S32 = static_cast<uint32_t>(S),
                    G32 = static_cast<uint32_t>(ngroups);

@@ -275,15 +275,17 @@ def test_reduce_batch_matches_per_op_reductions():
             assert torch.equal(g, ref), f"{n}: batched reduction differs"
 
 
-@pytest.mark.parametrize("B,npipes", [(3, None), (64, None), (300, None), (37, 6)])
+@pytest.mark.parametrize("B,npipes", [(3, None), (64, None), (256, None), (300, None), (37, 6), (256, 6)])
 def test_fused_pipe_scatter_matches_two_launches(B, npipes):
     """lg_edge_head_bwd_scatter (the incidence scatter fused into the EdgeHead backward, one
     workgroup per window) against lg_edge_head_bwd + lg_pipe_scatter_bwd: the node gradient
     is the same sums in the same order, so every gradient upstream of it (trunk, GRU, sensor
     projection, NoLeakHead) is bitwise equal; the EdgeHead's weight gradients change only by
-    the slab grouping of the fixed-order reduction (window-owned tiles).  B = 3: window-major
-    trunk; 64: node-major; 300: more windows than CUs (several windows per workgroup); 6 pipes
-    (the synthetic training sets): fewer pipe rows than a tile, so the per-window grid is larger
+    the slab grouping of the fixed-order reduction (window-owned tiles).  The fused forms run
+    a workgroup per window, so only from B = CUs (256 on MI355X) on; below it the call is the
+    two launches itself (B = 3: window-major trunk; 64: node-major).  256: the streamed scatter
+    (pipe schedule); 300: more windows than CUs (several windows per workgroup); 6 pipes (the
+    synthetic training sets): fewer pipe rows than a tile, so the per-window grid is larger
     than the tile grid the workspace used to be sized for."""
     from models.detector import LeakDetector
     sensors, pipes = lta_ids()
@@ -314,7 +316,7 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
 
 
 @pytest.mark.parametrize("D", [64, 32])
-@pytest.mark.parametrize("B", [5, 40])
+@pytest.mark.parametrize("B", [256, 300])  # the fused forms need a window per CU (B >= CUs)
 def test_streamed_scatter_odd_graph(D, B):
     """The streamed node scatter (ABI 22) on a graph built to hit its corner cases: a hub of
     degree 40 (more incidences than a tile has rows, events with many incidences), a self-loop
