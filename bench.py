@@ -196,7 +196,9 @@ def small_kernels_us(breakdown: dict | None) -> dict:
 def step_breakdown(batch: int, ms_per_step: float, steps: int = 20) -> dict | None:
     """Every kernel of one replay of the captured step (tools/step_trace.py under a child
     `rocprofv3 --kernel-trace`): per-kernel device time, their sum, the replay's span, and
-    `step_gap_us` = ms_per_step (the bench's own, unprofiled clock) minus the sum.  The
+    `step_gap_us` = the replay's span minus the sum (the time between kernels), beside
+    `step_minus_kernels_us` = ms_per_step (the bench's own, unprofiled clock) minus the sum
+    (negative when the profiler's per-dispatch cost inflates the kernels more).  The
     replays between two k_gru_fwd launches are one step each; the median replay is reported."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
@@ -233,7 +235,8 @@ def step_breakdown(batch: int, ms_per_step: float, steps: int = 20) -> dict | No
     return {"source": "rocprofv3 --kernel-trace over tools/step_trace.py (the same captured step), median replay",
             "kernels": [[n, round(t, 2)] for n, t in ks], "by_name_us": agg, "launches": len(ks),
             "sum_us": round(tot, 1), "replay_span_us": round(span, 1), "step_us": round(ms_per_step * 1e3, 1),
-            "step_gap_us": round(ms_per_step * 1e3 - tot, 1),
+            "step_gap_us": round(span - tot, 1),
+            "step_minus_kernels_us": round(ms_per_step * 1e3 - tot, 1),
             "accounted_frac": round(tot / (ms_per_step * 1e3), 4)}
 
 
