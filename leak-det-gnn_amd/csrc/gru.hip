@@ -25,6 +25,8 @@
 // workgroup writes its partial sums once to a slab reduced in fixed order
 // (deterministic).
 #include <algorithm>
+#include <cstdlib>
+#include <type_traits>
 #include "common.h"
 #include "reduce.h"
 #include "split_bf16.h"
@@ -414,36 +416,58 @@ k_gru_bwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     }
 }
 
-// ------------------------------------------------------------------ backward, split-bf16
+// ------------------------------------------------------------------ backward, split MFMA
 // The training step's backward (no dx: the residual is data).  One workgroup = 32
 // sequences x 2 H/16 waves: wave (w, s) owns hidden units [16w, 16w+16) of sequences
 // [16s, 16s+16).  Per step t (descending), one barrier:
 //   1. elementwise gate backward for the lane's 4 units (gates, h_{t-1} and x_t prefetched
 //      two steps ahead from global); dG = (dG_r, dG_z, dG_hn, dG_in), h_{t-1} and x_t are
-//      split into three bf16 parts (split_bf16.h) and posted row-major [seq][column] to a
-//      double-buffered LDS image
-//   2. dh_{t-1} = d z + W_hh^T dG_h on v_mfma_f32_16x16x32_bf16 (K = the 3H gate rows read
-//      straight from the [seq][rho] rows: one b128 per chunk and part), W_hh^T split once into
+//      split (below) and posted row-major [seq][column] to a double-buffered LDS image
+//   2. dh_{t-1} = d z + W_hh^T dG_h on 16x16x32 MFMAs (K = the 3H gate rows read straight
+//      from the [seq][rho] rows: one b128 per chunk and part), W_hh^T split once into
 //      registers
 //   3. dW_hh += dG_h^T h_{t-1} and dW_ih += dG_i^T x_t over the 32 sequences (K = 32: one
 //      16x16x32 per tile and product); both operands come from the row-major images through
 //      ds_read_b64_tr_b16 (transposing 4 x 16 blocks), wave (w, s) owning the dW_hh column
 //      tiles of its half
-// Six products per MFMA operand pair keep fp32-level accuracy.  MFMA cycles per wave and step:
-// 36 x 16 (dh) + 36-48 x 16 (dW) against 108 x 32 for the fp32 v_mfma_f32_16x16x4_f32 kernel
-// above, which stays for the dx variant.
+//
+// Two splits of the fp32 operands, both at fp32-level accuracy:
+//  - F16 (default): the f16x2 transform (split_bf16.h: 2 parts, 3 products per operand pair),
+//    with power-of-two scales that are uniform along every MFMA's K: W_hh^T per wave (the
+//    wave's unit rows), h_{t-1} fixed at 2^14 (|h| <= 1), x_t and dG_t one scale per step for
+//    the whole workgroup.  A workgroup-wide scale needs a bound on the step's largest |dG|
+//    before any wave has computed it, and a second barrier per step would cost what the
+//    halved MFMAs save; the bound comes from the previous step instead.  With d = dh_t,
+//      |dG_in|, |dG_hn| <= |d|,  |dG_z| <= |d| / 2,  |dG_r| <= |d| |W_hn h + b_hn| / 4
+//    (r, z, n, h in [0, 1] / [-1, 1]), and dh_t = z dh_{t+1} + W_hh^T dG_h,t+1, so
+//      max |dG_t| <= (max |dh_{t+1}| + |W_hh^T|_inf max |dG_h,t+1|) max(1, max |hn_t| / 4)
+//    and, as hn = W_hn h + b_hn with |h| <= 1, max |hn_t| <= max |hn_{L-1}| + 2 H max |W_hn|
+//    for every t (one factor per launch).  Each step posts max |dh| and max |dG_h| into a
+//    3-slot LDS ring (ds_max over the four row leaders of each wave); the following step reads
+//    them after the barrier.  x is data: its scale is the workgroup's max |x| over all steps,
+//    scanned once before the loop.  The
+//    bound only ever overshoots, which f16x2 tolerates (block max placed at [2^14, 2^15):
+//    values down to 2^-17 of it keep both parts normal).  A scale is kept while the bound
+//    stays within 2^6 of it, so the dW accumulators (in units of the product scale) are
+//    rescaled only when it moves; they are unscaled once at the end.
+//  - 3-way bf16 (LG_KERNEL_LAB builds, LG_LAB_GRU_BF16X3=1, for A/B runs): six products
+//    per operand pair, no scales.
+// MFMA cycles per wave and step: 18 x 16 (dh) + 18-24 x 16 (dW) on the f16x2 split against
+// 36 x 16 + 36-48 x 16 on the 3-way bf16 split and 108 x 32 for the fp32
+// v_mfma_f32_16x16x4_f32 kernel above, which stays for the dx variant.
 constexpr int TS2 = 32;  // sequences per workgroup
 template <int H>
 struct GB2 {
     static constexpr int NW = H / 16;         // unit groups
     static constexpr int NWAVE = 2 * NW;      // x 2 sequence halves
     static constexpr int NTH = 64 * NWAVE;
-    static constexpr int DGS = 4 * H + 16;    // dG row (bf16): [r | z | hn | in], 8 dwords mod 64: conflict-free
-    static constexpr int HLS = H + 16;        // h row (bf16)
-    static constexpr int XLS = 16;            // x row (bf16): 16 columns (I <= 10, col 10 = 1)
+    static constexpr int DGS = 4 * H + 16;    // dG row (16-bit): [r | z | hn | in], 8 dwords mod 64: conflict-free
+    static constexpr int HLS = H + 16;        // h row (16-bit)
+    static constexpr int XLS = 16;            // x row (16-bit): 16 columns (I <= 10, col 10 = 1)
     static constexpr int NCH = 3 * H / 32;    // dh contraction chunks
     static constexpr int NTS = NW / 2;        // dW_hh column tiles per wave
 };
+constexpr int kGruKeep = 6;  // f16x2: a step scale is kept while the new bound is within 2^6 of it
 
 __device__ __forceinline__ void split3_1(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
     const uint32_t a = pk_bf16(x, 0.f);
@@ -454,72 +478,207 @@ __device__ __forceinline__ void split3_1(float x, uint16_t& p0, uint16_t& p1, ui
     p1 = static_cast<uint16_t>(b);
     p2 = static_cast<uint16_t>(c);
 }
+// two floats (already scaled) -> the packed hi and lo f16 parts of the f16x2 split:
+// hi = v_cvt_pk_f16_f32, each lo = f16(x - hi) one v_fma_mix{lo,hi}_f16 reading hi's half
+// (3 instructions a pair; the compiler's form converts hi back and subtracts: 5-7)
+__device__ __forceinline__ void split2_pair_mix(float a, float b, uint32_t& p0, uint32_t& p1) {
+    const lg_f32x2 v = {a, b};
+    p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_f16x2));
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(a), "v"(p0));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(p0));
+    p1 = lo;
+}
+// one float -> the two f16 parts of the f16x2 split (already scaled)
+__device__ __forceinline__ void split2_1(float x, uint16_t& p0, uint16_t& p1) {
+    const _Float16 h = static_cast<_Float16>(x);
+    p0 = __builtin_bit_cast(uint16_t, h);
+    p1 = __builtin_bit_cast(uint16_t, static_cast<_Float16>(x - static_cast<float>(h)));
+}
+// max of a non-negative float's bits over each row of 16 lanes (every lane of the row; every
+// source lane of these patterns exists, so bound_ctrl only lets the move fold into the max)
+__device__ __forceinline__ uint32_t gru_row_max_bits(uint32_t m) {
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0xB1, 0xF, 0xF, true)));  // xor 1
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x4E, 0xF, 0xF, true)));  // xor 2
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x124, 0xF, 0xF, true)));  // row_ror 4
+    m = max(m, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(m), 0x128, 0xF, 0xF, true)));  // row_ror 8
+    return m;
+}
+// ds_max_u32 on an LDS word from the lanes that call it.  The offset is hidden from the
+// compiler so that its atomic optimizer does not wrap a (provably) uniform address in a
+// readlane loop over the active lanes (~30 instructions per atomic).
+__device__ __forceinline__ void lds_max_u32(uint32_t* p, uint32_t v) {
+    int off = 0;
+    asm volatile("" : "+v"(off));
+    atomicMax(p + off, v);
+}
+__device__ __forceinline__ float absmax4(const f32x4& v) {
+    return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
 
-template <int H, bool UT>
+template <int H, bool UT, bool F16>
 __global__ void __launch_bounds__(GB2<H>::NTH)
 k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Whh,
            const float* __restrict__ hs, const float* __restrict__ gates, const float* __restrict__ dhL,
            float* __restrict__ slab, uint32_t Nseq, int L, int S, lg_fastdiv fdS) {
     using G = GB2<H>;
+    using AF = std::conditional_t<F16, lg_f16x8, lg_bf16x8>;
+    constexpr int NP = F16 ? 2 : 3;  // split parts
     constexpr int I = UT ? 10 : 1, G3 = 3 * H;
     constexpr int SLAB = G3 * H + G3 * I + 2 * G3;
     constexpr int XPT = TS2 * 16 / G::NTH;  // x values staged per thread and step
-    __shared__ __attribute__((aligned(16))) uint16_t dgs[2][3][TS2][G::DGS];
-    __shared__ __attribute__((aligned(16))) uint16_t hls[2][3][TS2][G::HLS];
-    __shared__ __attribute__((aligned(16))) uint16_t xls[2][3][TS2][G::XLS];
+    __shared__ __attribute__((aligned(16))) uint16_t dgs[2][NP][TS2][G::DGS];
+    __shared__ __attribute__((aligned(16))) uint16_t hls[2][NP][TS2][G::HLS];
+    __shared__ __attribute__((aligned(16))) uint16_t xls[2][NP][TS2][G::XLS];
     __shared__ __attribute__((aligned(16))) float dbh[H];
+    // F16: per-step maxima (float bits) {max |dh|, max |dG_h|}, ring of 3 (written at step t,
+    // read at t-1, cleared at t-2); |W_hh^T|_inf, max |W_hn|, max |hn_{L-1}|, max |x|
+    __shared__ __attribute__((aligned(8))) uint32_t gmx[3][2];
+    __shared__ uint32_t wnm[4];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int w = wid % G::NW, sh = wid / G::NW;
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
     const int sl = 16 * sh + j;  // local sequence of this lane (elementwise, dh)
     const uint32_t seq0 = blockIdx.x * TS2, seq = seq0 + sl;
     const bool valid = seq < Nseq;
-    const uint32_t seqc = valid ? seq : 0u;
     const int u0 = 16 * w + 4 * q;  // this lane's 4 units
 
-    // W_hh^T A fragments: row = unit 16w + j, k = gate row 32c + 8q + p
-    lg_bf16x8 adh[G::NCH][3];
-#pragma unroll
-    for (int c = 0; c < G::NCH; ++c) {
-        f32x4 v0, v1;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            v0[p] = Whh[(32 * c + 8 * q + p) * H + 16 * w + j];
-            v1[p] = Whh[(32 * c + 8 * q + 4 + p) * H + 16 * w + j];
+    auto frag_row = [](const uint16_t* p) { return __builtin_bit_cast(AF, lds_frag_row(p)); };
+    auto frag_tr = [](const uint16_t* r0, const uint16_t* r1) {
+        return __builtin_bit_cast(AF, lds_frag_tr16(r0, r1));
+    };
+    auto mm = [](const AF (&a)[NP], const AF (&b)[NP], f32x4 c) {
+        if constexpr (F16) return mfma_f16x2(a, b, c);
+        else return mfma_split(a, b, c);
+    };
+    // value -> its NP 16-bit parts (F16: already scaled)
+    auto split_x4 = [](const f32x4& v, lg_u32x2 (&f)[NP]) {
+        if constexpr (F16) {
+            uint32_t a0, a1, b0, b1;
+            split2_pair_mix(v[0], v[1], a0, a1);
+            split2_pair_mix(v[2], v[3], b0, b1);
+            f[0] = lg_u32x2{a0, b0};
+            f[1] = lg_u32x2{a1, b1};
+        } else {
+            split3_x4(v, f[0], f[1], f[2]);
         }
-        split3_x8(v0, v1, adh[c][0], adh[c][1], adh[c][2]);
+    };
+
+    // W_hh^T A fragments: row = unit 16w + j, k = gate row 32c + 8q + p
+    AF adh[G::NCH][NP];
+    float sWinv = 1.f;  // F16: 2^-sW, the wave's W_hh^T scale
+    {
+        f32x4 wv[G::NCH][2];
+#pragma unroll
+        for (int c = 0; c < G::NCH; ++c)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                wv[c][0][p] = Whh[(32 * c + 8 * q + p) * H + 16 * w + j];
+                wv[c][1][p] = Whh[(32 * c + 8 * q + 4 + p) * H + 16 * w + j];
+            }
+        if constexpr (F16) {
+            // max |W| of the wave, of its W_hn rows, |W| sum of column 16w + j (this lane's rows)
+            float m = 0.f, mn = 0.f, cs = 0.f;
+#pragma unroll
+            for (int c = 0; c < G::NCH; ++c) {
+                m = fmaxf(m, fmaxf(absmax4(wv[c][0]), absmax4(wv[c][1])));
+                if (32 * c >= 2 * H) mn = fmaxf(mn, fmaxf(absmax4(wv[c][0]), absmax4(wv[c][1])));
+#pragma unroll
+                for (int p = 0; p < 4; ++p) cs += fabsf(wv[c][0][p]) + fabsf(wv[c][1][p]);
+            }
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            const int sW = lg_f16_scale_exp_c(lg_wave_max_bits(__float_as_uint(m)));
+            const float sc = lg_pow2f(sW);
+            sWinv = lg_pow2f(-sW);
+#pragma unroll
+            for (int c = 0; c < G::NCH; ++c) split2_f16_x8(wv[c][0] * sc, wv[c][1] * sc, adh[c][0], adh[c][1]);
+            if (threadIdx.x < 6) (&gmx[0][0])[threadIdx.x] = 0u;
+            if (threadIdx.x < 4) wnm[threadIdx.x] = 0u;
+            __syncthreads();
+            const uint32_t cm = gru_row_max_bits(__float_as_uint(cs)), nm = gru_row_max_bits(__float_as_uint(mn));
+            if (j == 0) {
+                lds_max_u32(&wnm[0], cm);
+                lds_max_u32(&wnm[1], nm);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < G::NCH; ++c) split3_x8(wv[c][0], wv[c][1], adh[c][0], adh[c][1], adh[c][2]);
+        }
     }
 
     // Prefetch loads are unconditional and raw: addresses clamped in range (a padded
-    // sequence reads sequence 0, t < 0 reads step 0) and nothing selected on the loaded
+    // sequence's x is the last sequence's, its gates and h read 0, t < 0 reads step 0) and nothing selected on the loaded
     // value until it is consumed — a load under a divergent branch, or a select on its
     // result, makes the compiler wait for it (vmcnt) in the iteration that issued it, which
     // serialises the two-step prefetch.  A padded sequence needs no masking: its dh is zero,
-    // every dG term is proportional to dh, and its h / x rows only ever multiply its own dG.
+    // every dG term is proportional to dh, and its h / x rows only ever multiply its own dG
+    // (its gates read as 0 leave the F16 bounds alone; its x lies in the scanned windows, so it
+    // cannot overflow the x scale and make 0 x inf).
+    // gates / h through buffer loads: the base (step t, the workgroup's first sequence) is
+    // scalar, the lane's offset fixed, and a padded sequence's rows lie past the resource's
+    // end (read as 0)
+    const int nsq = static_cast<int>(min(Nseq - seq0, static_cast<uint32_t>(TS2)));
     auto load_g = [&](int t, f32x4 (&g)[4]) {
-        const float* p = gates + (static_cast<int64_t>(max(t, 0)) * Nseq + seqc) * 4 * H + u0;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(gates + (static_cast<int64_t>(max(t, 0)) * Nseq + seq0) * 4 * H), static_cast<short>(0),
+            nsq * 4 * H * 4, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g[k] = ld4(p + k * H);
+        for (int k = 0; k < 4; ++k)
+            g[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * 4 * H + u0 + k * H) * 4, 0, 0));
     };
     auto load_h = [&](int t) -> f32x4 {  // h_t of this lane's units (h_0 for t < 0: masked at use)
-        return ld4(hs + (static_cast<int64_t>(max(t, 0)) * Nseq + seqc) * H + u0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(hs + (static_cast<int64_t>(max(t, 0)) * Nseq + seq0) * H), static_cast<short>(0),
+            nsq * H * 4, 0x00020000);
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * H + u0) * 4, 0, 0));
     };
+    // x value i of this thread: step 0's element and the per-step stride (hoisted out of the loop)
+    const float* xp0[XPT];
+    int xst[XPT];
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+        const int e = threadIdx.x + i * G::NTH, xs = e >> 4, k = e & 15;
+        const uint32_t sg = seq0 + xs;
+        const uint32_t sgc = sg < Nseq ? sg : Nseq - 1;  // the last sequence's x: inside the F16 x scan
+        const uint32_t b = lg_div(sgc, fdS), s = sgc - b * fdS.d;
+        const int64_t row0 = static_cast<int64_t>(b) * L;
+        const bool from_t = UT && k >= 1 && k <= 9;
+        xp0[i] = from_t ? tfeat + row0 * 9 + (k - 1) : resid + row0 * S + s;
+        xst[i] = from_t ? 9 : S;
+    }
     auto load_x = [&](int t, float (&x)[XPT]) {  // raw residual / tfeat value (see x_val)
 #pragma unroll
-        for (int i = 0; i < XPT; ++i) {
-            const int e = threadIdx.x + i * G::NTH, xs = e >> 4, k = e & 15;
-            const uint32_t sg = seq0 + xs;
-            const uint32_t sgc = sg < Nseq ? sg : 0u;
-            const uint32_t b = lg_div(sgc, fdS), s = sgc - b * fdS.d;
-            const int64_t row = static_cast<int64_t>(b) * L + max(t, 0);
-            const bool from_t = UT && k >= 1 && k <= 9;
-            x[i] = *(from_t ? tfeat + row * 9 + (k - 1) : resid + row * S + s);
-        }
+        for (int i = 0; i < XPT; ++i) x[i] = xp0[i][static_cast<int64_t>(max(t, 0)) * xst[i]];
     };
     auto x_val = [&](int i, float raw) {  // x row column k: residual, tfeat, the constant 1, 0
         const int k = (threadIdx.x + i * G::NTH) & 15;
         return (k == 0 || (UT && k >= 1 && k <= 9)) ? raw : (k == 10 ? 1.f : 0.f);
     };
+    // F16: post this wave's maxima into ring slot `slot` (the four row leaders, ds_max)
+    auto post = [&](int slot, float md, float mg) {
+        const uint32_t a = gru_row_max_bits(__float_as_uint(md)), b = gru_row_max_bits(__float_as_uint(mg));
+        if (j == 0) {
+            lds_max_u32(&gmx[slot][0], a);
+            lds_max_u32(&gmx[slot][1], b);
+        }
+    };
+    if constexpr (F16) {
+        // the x scale: max |x| over every step of the workgroup's windows (a superset of its
+        // sequences' values, contiguous in memory: coalesced, all loads of a round in flight)
+        const uint32_t b0 = lg_div(seq0, fdS), b1 = lg_div(min(seq0 + TS2, Nseq) - 1, fdS);
+        float m = 1.f;  // the constant-1 column
+        auto scan = [&](const float* base, int64_t n) {
+            for (int64_t i0 = threadIdx.x; i0 < n; i0 += 8 * G::NTH)
+#pragma unroll
+                for (int u = 0; u < 8; ++u) m = fmaxf(m, fabsf(base[min(i0 + u * G::NTH, n - 1)]));
+        };
+        const int64_t nb = static_cast<int64_t>(b1 - b0 + 1) * L;
+        scan(resid + static_cast<int64_t>(b0) * L * S, nb * S);
+        if (UT) scan(tfeat + static_cast<int64_t>(b0) * L * 9, nb * 9);
+        const uint32_t xm = gru_row_max_bits(__float_as_uint(m));
+        if (j == 0) lds_max_u32(&wnm[3], xm);
+    }
 
     f32x4 dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + u0) : zero4();
     f32x4 dwh[3][G::NTS], dwx[2], dbhn = zero4();
@@ -532,64 +691,117 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
     // Two prefetch slots (steps of one parity each), each consumed and refilled with the
     // step two earlier by the same unrolled copy of the step: no register rotation, whose
     // moves would wait for the loads just issued.
+    // Issued slot by slot in the refill's order (x, gates, h): the loop's first step then
+    // waits for slot A and slot B's x only, as every later step does.
     f32x4 gA[4], gB[4], hA, hB;
     float xA[XPT], xB[XPT];
-    load_g(L - 1, gA);
-    load_g(L - 2, gB);
-    hA = load_h(L - 2);
-    hB = load_h(L - 3);
     load_x(L - 1, xA);
+    load_g(L - 1, gA);
+    hA = load_h(L - 2);
     load_x(L - 2, xB);
+    load_g(L - 2, gB);
+    hB = load_h(L - 3);
+
+    float Wn = 0.f, Cg = 1.f;  // F16: |W_hh^T|_inf, max(1, max |hn| / 4) of the workgroup
+    float xsc = 1.f;           // F16: the x scale 2^sx
+    int sg_cur = 0, sx = 0;    // F16: current dG scale exponent (uniform), the x scale exponent
+    if constexpr (F16) {
+        // the bound for step L-1: max |dh_L|, no dG; max |hn_{L-1}|
+        post(L % 3, absmax4(dh), 0.f);
+        const uint32_t hm = gru_row_max_bits(__float_as_uint(absmax4(gA[3])));
+        if (j == 0) lds_max_u32(&wnm[2], hm);
+        __syncthreads();
+        Wn = __uint_as_float(__builtin_amdgcn_readfirstlane(wnm[0]));
+        const float mhn = __uint_as_float(__builtin_amdgcn_readfirstlane(wnm[2]));
+        Cg = fmaxf(1.f, 0.25f * fmaf(static_cast<float>(2 * H), __uint_as_float(__builtin_amdgcn_readfirstlane(wnm[1])), mhn));
+        sx = lg_f16_scale_exp_c(__builtin_amdgcn_readfirstlane(wnm[3]));
+        xsc = lg_pow2f(sx);
+    }
 
     auto step = [&](const int t, f32x4 (&g_cur)[4], f32x4& h_cur, float (&x_cur)[XPT]) {
         const int bf = t & 1;
+        float gsc = 1.f, gin_ = 1.f;  // F16: this step's dG scale and its inverse
+        if constexpr (F16) {
+            // this step's scales from the bound posted by step t+1 (or the prologue)
+            const lg_u32x2 m = *reinterpret_cast<const lg_u32x2*>(&gmx[(t + 1) % 3][0]);
+            const float md = __uint_as_float(__builtin_amdgcn_readfirstlane(m[0]));
+            const float mg = __uint_as_float(__builtin_amdgcn_readfirstlane(m[1]));
+            const uint32_t bound = __builtin_amdgcn_readfirstlane(__float_as_uint(fmaf(Wn, mg, md) * Cg));
+            int sg = lg_f16_scale_exp_c(bound);
+            sg = (sg < sg_cur || sg > sg_cur + kGruKeep) ? sg : sg_cur;
+            if (sg != sg_cur) {  // dW_hh in units of 2^(sg + 14)
+                const float f = lg_pow2f(sg - sg_cur);
+#pragma unroll
+                for (int gi = 0; gi < 3; ++gi)
+#pragma unroll
+                    for (int n = 0; n < G::NTS; ++n) dwh[gi][n] *= f;
+            }
+            if (sg != sg_cur) {  // dW_ih in units of 2^(sg + sx)
+                const float f = lg_pow2f(sg - sg_cur);
+                dwx[0] *= f;
+                dwx[1] *= f;
+            }
+            sg_cur = sg;
+            gsc = lg_pow2f(sg);
+            gin_ = lg_pow2f(-sg);
+            if (threadIdx.x < 2) gmx[(t + 2) % 3][threadIdx.x] = 0u;  // read by step t+1, written next by t-1
+        }
         // (1) elementwise gate backward (h_cur = h_{t-1})
         {
             const f32x4 r = g_cur[0], z = g_cur[1], n = g_cur[2], hnp = g_cur[3];
             const f32x4 hp = t >= 1 ? h_cur : zero4();  // h_{-1} = 0
             f32x4 gr, gz, ghn, gin, dhp;
+            // dG is linear in dh: F16 forms it at the step's scale straight away
+            const f32x4 ds = F16 ? dh * gsc : dh;
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                const float d = dh[reg];
+                const float d = ds[reg];
                 const float dn = d * (1.f - z[reg]);
                 const float dzv = d * (hp[reg] - n[reg]);
-                dhp[reg] = d * z[reg];
+                dhp[reg] = dh[reg] * z[reg];
                 const float dnp = dn * (1.f - n[reg] * n[reg]);
                 gin[reg] = dnp;
                 ghn[reg] = dnp * r[reg];
                 gr[reg] = dnp * hnp[reg] * r[reg] * (1.f - r[reg]);
                 gz[reg] = dzv * z[reg] * (1.f - z[reg]);
             }
-            dbhn += ghn;
+            if constexpr (F16) {
+                post(t % 3, absmax4(dh), fmaxf(absmax4(gr), fmaxf(absmax4(gz), absmax4(ghn))) * gin_);
+                dbhn += ghn * gin_;
+            } else {
+                dbhn += ghn;
+            }
+            // d z materialised here: left to the compiler it is formed in (2), which keeps z live
+            // across the slot's refill and costs a register move at the loop's back edge that
+            // waits for the loads just issued
+            asm volatile("" : "+v"(dhp[0]), "+v"(dhp[1]), "+v"(dhp[2]), "+v"(dhp[3]));
             dh = dhp;
             const f32x4 blk[4] = {gr, gz, ghn, gin};
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                lg_u32x2 f0, f1, f2;
-                split3_x4(blk[b], f0, f1, f2);
-                *reinterpret_cast<lg_u32x2*>(&dgs[bf][0][sl][b * H + u0]) = f0;
-                *reinterpret_cast<lg_u32x2*>(&dgs[bf][1][sl][b * H + u0]) = f1;
-                *reinterpret_cast<lg_u32x2*>(&dgs[bf][2][sl][b * H + u0]) = f2;
+                lg_u32x2 f[NP];
+                split_x4(blk[b], f);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) *reinterpret_cast<lg_u32x2*>(&dgs[bf][p][sl][b * H + u0]) = f[p];
             }
-            lg_u32x2 f0, f1, f2;
-            split3_x4(hp, f0, f1, f2);
-            *reinterpret_cast<lg_u32x2*>(&hls[bf][0][sl][u0]) = f0;
-            *reinterpret_cast<lg_u32x2*>(&hls[bf][1][sl][u0]) = f1;
-            *reinterpret_cast<lg_u32x2*>(&hls[bf][2][sl][u0]) = f2;
+            lg_u32x2 f[NP];
+            split_x4(F16 ? hp * 16384.f : hp, f);  // F16: |h| <= 1 at the fixed scale 2^14
+#pragma unroll
+            for (int p = 0; p < NP; ++p) *reinterpret_cast<lg_u32x2*>(&hls[bf][p][sl][u0]) = f[p];
 #pragma unroll
             for (int i = 0; i < XPT; ++i) {
                 const int e = threadIdx.x + i * G::NTH;
-                uint16_t p0, p1, p2;
-                split3_1(x_val(i, x_cur[i]), p0, p1, p2);
-                xls[bf][0][e >> 4][e & 15] = p0;
-                xls[bf][1][e >> 4][e & 15] = p1;
-                xls[bf][2][e >> 4][e & 15] = p2;
+                uint16_t pp[3];
+                if constexpr (F16) split2_1(x_val(i, x_cur[i]) * xsc, pp[0], pp[1]);
+                else split3_1(x_val(i, x_cur[i]), pp[0], pp[1], pp[2]);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) xls[bf][p][e >> 4][e & 15] = pp[p];
             }
         }
-        // refill this slot: step t-2's gates / x and h_{t-3}
+        // refill this slot: step t-2's x / gates and h_{t-3}
+        load_x(t - 2, x_cur);
         load_g(t - 2, g_cur);
         h_cur = load_h(t - 3);
-        load_x(t - 2, x_cur);
         // dgs/hls/xls[bf] complete.  Buffer bf was last read at step t+2, which every wave
         // finished before arriving at step t+1's barrier: one barrier per step suffices.
         __syncthreads();
@@ -599,12 +811,13 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
             for (int c = 0; c < G::NCH; ++c) {
-                lg_bf16x8 b[3];
+                AF b[NP];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) b[p] = lds_frag_row(&dgs[bf][p][sl][32 * c + 8 * q]);
-                acc[c & 1] = mfma_split(adh[c], b, acc[c & 1]);
+                for (int p = 0; p < NP; ++p) b[p] = frag_row(&dgs[bf][p][sl][32 * c + 8 * q]);
+                acc[c & 1] = mm(adh[c], b, acc[c & 1]);
             }
-            dh += acc[0] + acc[1];
+            if constexpr (F16) dh += (acc[0] + acc[1]) * (sWinv * lg_pow2f(-sg_cur));
+            else dh += acc[0] + acc[1];
         }
         // (3) dW over the 32 sequences: A = dG^T tiles (rows = gate rows 16w.., K = seq),
         // B = h_{t-1} / x_t (K = seq, columns = units / x columns)
@@ -615,40 +828,49 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             // distinct banks at these row strides (rows 8q.. and 8q+4.. did 2-way:
             // MI355X_MICROARCH.md §LDS, 54 % of LDS-active cycles were conflicts)
             const int tr = 4 * q + (j >> 2), tc = 4 * (j & 3);
-            lg_bf16x8 bh[G::NTS][3], bx[3];
+            AF bh[G::NTS][NP], bx[NP];
 #pragma unroll
             for (int n = 0; n < G::NTS; ++n)
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    bh[n][p] = lds_frag_tr16(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
-                                             &hls[bf][p][tr + 16][16 * (sh * G::NTS + n) + tc]);
+                for (int p = 0; p < NP; ++p)
+                    bh[n][p] = frag_tr(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
+                                       &hls[bf][p][tr + 16][16 * (sh * G::NTS + n) + tc]);
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bx[p] = lds_frag_tr16(&xls[bf][p][tr][tc], &xls[bf][p][tr + 16][tc]);
+            for (int p = 0; p < NP; ++p) bx[p] = frag_tr(&xls[bf][p][tr][tc], &xls[bf][p][tr + 16][tc]);
 #pragma unroll
             for (int gi = 0; gi < 3; ++gi) {
-                lg_bf16x8 a[3];
+                AF a[NP];
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 16][gi * H + 16 * w + tc]);
+                for (int p = 0; p < NP; ++p)
+                    a[p] = frag_tr(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 16][gi * H + 16 * w + tc]);
 #pragma unroll
-                for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mfma_split(a, bh[n], dwh[gi][n]);
-                if (sh == 0 && gi < 2) dwx[gi] = mfma_split(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
+                for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mm(a, bh[n], dwh[gi][n]);
+                if (sh == 0 && gi < 2) dwx[gi] = mm(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
             }
             if (sh == 1) {  // n gate's input side: dG_in
-                lg_bf16x8 a[3];
+                AF a[NP];
 #pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    a[p] = lds_frag_tr16(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 16][3 * H + 16 * w + tc]);
-                dwx[0] = mfma_split(a, bx, dwx[0]);
+                for (int p = 0; p < NP; ++p)
+                    a[p] = frag_tr(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 16][3 * H + 16 * w + tc]);
+                dwx[0] = mm(a, bx, dwx[0]);
             }
         }
     };
     int t = L - 1;
-    for (; t >= 1; t -= 2) {  // unconditional pairs: a conditional second half would merge
-        step(t, gA, hA, xA);  // the slot registers in a phi, i.e. moves that wait for loads
+    for (; t >= 1; t -= 2) {     // unconditional pairs: a conditional second half would merge
+        step(t, gA, hA, xA);      // the slot registers in a phi, i.e. moves that wait for loads
         step(t - 1, gB, hB, xB);
     }
     if (t == 0) step(0, gA, hA, xA);
+    if constexpr (F16) {  // back to plain units
+        const float fh = lg_pow2f(-(sg_cur + 14)), fx = lg_pow2f(-(sg_cur + sx));
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi)
+#pragma unroll
+            for (int n = 0; n < G::NTS; ++n) dwh[gi][n] *= fh;
+        dwx[0] *= fx;
+        dwx[1] *= fx;
+    }
 
     // per-workgroup slab (the layout of k_gru_bwd): C rows = gate rows 16w + 4q + reg, columns j
     float* out = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
@@ -716,13 +938,20 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
 #define LG_GRU_BWD(UT, DX)                                                                                       \
     lg_launch(k_gru_bwd<H, UT, DX>, grid, 4 * H, 0, s, residual, tfeat, w_ih, w_hh, h_seq, gates, dh_last, dx, slab,   \
                                                  Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
-#define LG_GRU_BWD2(UT)                                                                                          \
-    lg_launch(k_gru_bwd2<H, UT>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual, tfeat,  \
+#define LG_GRU_BWD2(UT, F)                                                                                       \
+    lg_launch(k_gru_bwd2<H, UT, F>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual, tfeat, \
               w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
-    if (ut) {
-        if (need_dx) LG_GRU_BWD(true, true); else LG_GRU_BWD2(true);
+#ifdef LG_KERNEL_LAB
+    const bool f16 = !getenv("LG_LAB_GRU_BF16X3");  // lab A/B: the 3-way bf16 split
+#else
+    constexpr bool f16 = true;
+#endif
+    if (need_dx) {
+        if (ut) LG_GRU_BWD(true, true); else LG_GRU_BWD(false, true);
+    } else if (ut) {
+        if (f16) LG_GRU_BWD2(true, true); else LG_GRU_BWD2(true, false);
     } else {
-        if (need_dx) LG_GRU_BWD(false, true); else LG_GRU_BWD2(false);
+        if (f16) LG_GRU_BWD2(false, true); else LG_GRU_BWD2(false, false);
     }
 #undef LG_GRU_BWD
 #undef LG_GRU_BWD2

@@ -687,6 +687,34 @@ def test_gru_encoder_vs_torch_cpu(use_time, dx, H, B):
                        {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
 
 
+@pytest.mark.parametrize("gscale,wmax,H", [(1e-9, 0.3, 64), (1e6, 0.3, 64), (1.0, 0.5, 64), (3e-5, 1.0, 32)])
+def test_gru_bwd_f16x2_scales(gscale, wmax, H):
+    """The training backward (k_gru_bwd2 on the f16x2 split) keeps fp32-level accuracy when the
+    incoming gradient is tiny or huge (the per-step dG scale follows it: bound from the previous
+    step's maxima) and with larger weights, whose dh grows or shrinks fast over the 36 steps.
+    (At +-1 and H = 64 the recurrence is chaotic: the fp32 CPU reference and the GPU forward
+    part by 1.5e-3 of the gradient whichever split the backward uses, r04n2.)"""
+    from models.detector import SharedSensorGRUEncoder
+    from oracle.detector_ref import _GRUEncoder
+    torch.manual_seed(7)
+    ref = _GRUEncoder(H, use_time=True)
+    with torch.no_grad():
+        for p in ref.parameters():
+            p.uniform_(-wmax, wmax)
+    enc = SharedSensorGRUEncoder(hidden_size=H, use_time=True)
+    enc.gru.load_state_dict(ref.gru.state_dict())
+    enc = enc.to(DEV)
+    gen = torch.Generator().manual_seed(11)
+    B = 40
+    r = torch.randn(B, 36, 29, generator=gen) * 3.0
+    tf = torch.randn(B, 36, 9, generator=gen)
+    gy = torch.randn(B, 29, H, generator=gen) * gscale
+    (ref(r, tf) * gy).sum().backward()
+    (enc(r.to(DEV), tf.to(DEV)) * gy.to(DEV)).sum().backward()
+    assert_grads_close([(n, p.grad) for n, p in enc.gru.named_parameters()],
+                       {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
+
+
 @pytest.mark.parametrize("K,M,N", [(7424, 64, 64), (1857, 32, 32), (3, 64, 32), (250, 32, 64)])
 def test_linear_dw_vs_fp64(K, M, N):
     """lg_linear_dw (node-init Linear weight grad on [x, 1] rows) vs float64 torch, ragged K."""
