@@ -469,7 +469,7 @@ struct GB2 {
 };
 constexpr int kGruKeep = 6;  // f16x2: a step scale is kept while the new bound is within 2^6 of it
 
-__device__ __forceinline__ void split3_1(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
+[[maybe_unused]] __device__ __forceinline__ void split3_1(float x, uint16_t& p0, uint16_t& p1, uint16_t& p2) {
     const uint32_t a = pk_bf16(x, 0.f);
     const float r = x - bf_lo(a);
     const uint32_t b = pk_bf16(r, 0.f);
@@ -516,7 +516,7 @@ __device__ __forceinline__ float absmax4(const f32x4& v) {
     return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
 
-template <int H, bool UT, bool F16>
+template <int H, bool UT, bool F16, bool DEFER>
 __global__ void __launch_bounds__(GB2<H>::NTH)
 k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Whh,
            const float* __restrict__ hs, const float* __restrict__ gates, const float* __restrict__ dhL,
@@ -702,6 +702,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
     load_g(L - 2, gB);
     hB = load_h(L - 3);
 
+    lg_u32x2 mcur = {0u, 0u};  // F16: the maxima the next step's bound is built from (read early)
     float Wn = 0.f, Cg = 1.f;  // F16: |W_hh^T|_inf, max(1, max |hn| / 4) of the workgroup
     float xsc = 1.f;           // F16: the x scale 2^sx
     int sg_cur = 0, sx = 0;    // F16: current dG scale exponent (uniform), the x scale exponent
@@ -716,32 +717,57 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         Cg = fmaxf(1.f, 0.25f * fmaf(static_cast<float>(2 * H), __uint_as_float(__builtin_amdgcn_readfirstlane(wnm[1])), mhn));
         sx = lg_f16_scale_exp_c(__builtin_amdgcn_readfirstlane(wnm[3]));
         xsc = lg_pow2f(sx);
+        mcur = *reinterpret_cast<const lg_u32x2*>(&gmx[L % 3][0]);
     }
 
+    // (3) dW over the 32 sequences of LDS image bf: A = dG^T tiles (rows = gate rows 16w..,
+    // K = seq), B = h_{t-1} / x_t (K = seq, columns = units / x columns)
+    auto dw_products = [&](const int bf) {
+        // tr16 addressing of this lane.  K = the 32 sequences, lane group q taking rows
+        // 4q..4q+3 (elements 0-3) and 16+4q..16+4q+3 (elements 4-7), the same in both
+        // operands: a 32-lane half then reads 8 consecutive rows, whose 8-dword windows meet
+        // distinct banks at these row strides (rows 8q.. and 8q+4.. did 2-way:
+        // MI355X_MICROARCH.md §LDS, 54 % of LDS-active cycles were conflicts)
+        const int tr = 4 * q + (j >> 2), tc = 4 * (j & 3);
+        AF bh[G::NTS][NP], bx[NP];
+#pragma unroll
+        for (int n = 0; n < G::NTS; ++n)
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                bh[n][p] = frag_tr(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
+                                   &hls[bf][p][tr + 16][16 * (sh * G::NTS + n) + tc]);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) bx[p] = frag_tr(&xls[bf][p][tr][tc], &xls[bf][p][tr + 16][tc]);
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            AF a[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                a[p] = frag_tr(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 16][gi * H + 16 * w + tc]);
+#pragma unroll
+            for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mm(a, bh[n], dwh[gi][n]);
+            if (sh == 0 && gi < 2) dwx[gi] = mm(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
+        }
+        if (sh == 1) {  // n gate's input side: dG_in
+            AF a[NP];
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                a[p] = frag_tr(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 16][3 * H + 16 * w + tc]);
+            dwx[0] = mm(a, bx, dwx[0]);
+        }
+    };
     auto step = [&](const int t, f32x4 (&g_cur)[4], f32x4& h_cur, float (&x_cur)[XPT]) {
         const int bf = t & 1;
         float gsc = 1.f, gin_ = 1.f;  // F16: this step's dG scale and its inverse
+        int sg = 0;                   // F16: its exponent
         if constexpr (F16) {
-            // this step's scales from the bound posted by step t+1 (or the prologue)
-            const lg_u32x2 m = *reinterpret_cast<const lg_u32x2*>(&gmx[(t + 1) % 3][0]);
-            const float md = __uint_as_float(__builtin_amdgcn_readfirstlane(m[0]));
-            const float mg = __uint_as_float(__builtin_amdgcn_readfirstlane(m[1]));
+            // this step's scales from the bound posted by step t+1 (or the prologue), read right
+            // after that step's barrier
+            const float md = __uint_as_float(__builtin_amdgcn_readfirstlane(mcur[0]));
+            const float mg = __uint_as_float(__builtin_amdgcn_readfirstlane(mcur[1]));
             const uint32_t bound = __builtin_amdgcn_readfirstlane(__float_as_uint(fmaf(Wn, mg, md) * Cg));
-            int sg = lg_f16_scale_exp_c(bound);
-            sg = (sg < sg_cur || sg > sg_cur + kGruKeep) ? sg : sg_cur;
-            if (sg != sg_cur) {  // dW_hh in units of 2^(sg + 14)
-                const float f = lg_pow2f(sg - sg_cur);
-#pragma unroll
-                for (int gi = 0; gi < 3; ++gi)
-#pragma unroll
-                    for (int n = 0; n < G::NTS; ++n) dwh[gi][n] *= f;
-            }
-            if (sg != sg_cur) {  // dW_ih in units of 2^(sg + sx)
-                const float f = lg_pow2f(sg - sg_cur);
-                dwx[0] *= f;
-                dwx[1] *= f;
-            }
-            sg_cur = sg;
+            int s = lg_f16_scale_exp_c(bound);
+            sg = (s < sg_cur || s > sg_cur + kGruKeep) ? s : sg_cur;
             gsc = lg_pow2f(sg);
             gin_ = lg_pow2f(-sg);
             if (threadIdx.x < 2) gmx[(t + 2) % 3][threadIdx.x] = 0u;  // read by step t+1, written next by t-1
@@ -802,9 +828,26 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         load_x(t - 2, x_cur);
         load_g(t - 2, g_cur);
         h_cur = load_h(t - 3);
+        // DEFER: step t+1's dW (image bf ^ 1, rewritten only after this step's barrier) in the
+        // MFMA pipe while this step's LDS writes land and the workgroup gathers at the barrier
+        if constexpr (DEFER)
+            if (t < L - 1) dw_products(bf ^ 1);
+        if constexpr (F16) {
+            if (sg != sg_cur) {  // dW in units of 2^(sg + 14) / 2^(sg + sx) from here on
+                const float f = lg_pow2f(sg - sg_cur);
+#pragma unroll
+                for (int gi = 0; gi < 3; ++gi)
+#pragma unroll
+                    for (int n = 0; n < G::NTS; ++n) dwh[gi][n] *= f;
+                dwx[0] *= f;
+                dwx[1] *= f;
+            }
+            sg_cur = sg;
+        }
         // dgs/hls/xls[bf] complete.  Buffer bf was last read at step t+2, which every wave
         // finished before arriving at step t+1's barrier: one barrier per step suffices.
         __syncthreads();
+        if constexpr (F16) mcur = *reinterpret_cast<const lg_u32x2*>(&gmx[t % 3][0]);  // cleared at t-2
 
         // (2) dh_{t-1} = d z + W_hh^T dG_h: two accumulator chains
         {
@@ -819,42 +862,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             if constexpr (F16) dh += (acc[0] + acc[1]) * (sWinv * lg_pow2f(-sg_cur));
             else dh += acc[0] + acc[1];
         }
-        // (3) dW over the 32 sequences: A = dG^T tiles (rows = gate rows 16w.., K = seq),
-        // B = h_{t-1} / x_t (K = seq, columns = units / x columns)
-        {
-            // tr16 addressing of this lane.  K = the 32 sequences, lane group q taking rows
-            // 4q..4q+3 (elements 0-3) and 16+4q..16+4q+3 (elements 4-7), the same in both
-            // operands: a 32-lane half then reads 8 consecutive rows, whose 8-dword windows meet
-            // distinct banks at these row strides (rows 8q.. and 8q+4.. did 2-way:
-            // MI355X_MICROARCH.md §LDS, 54 % of LDS-active cycles were conflicts)
-            const int tr = 4 * q + (j >> 2), tc = 4 * (j & 3);
-            AF bh[G::NTS][NP], bx[NP];
-#pragma unroll
-            for (int n = 0; n < G::NTS; ++n)
-#pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    bh[n][p] = frag_tr(&hls[bf][p][tr][16 * (sh * G::NTS + n) + tc],
-                                       &hls[bf][p][tr + 16][16 * (sh * G::NTS + n) + tc]);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) bx[p] = frag_tr(&xls[bf][p][tr][tc], &xls[bf][p][tr + 16][tc]);
-#pragma unroll
-            for (int gi = 0; gi < 3; ++gi) {
-                AF a[NP];
-#pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    a[p] = frag_tr(&dgs[bf][p][tr][gi * H + 16 * w + tc], &dgs[bf][p][tr + 16][gi * H + 16 * w + tc]);
-#pragma unroll
-                for (int n = 0; n < G::NTS; ++n) dwh[gi][n] = mm(a, bh[n], dwh[gi][n]);
-                if (sh == 0 && gi < 2) dwx[gi] = mm(a, bx, dwx[gi]);  // r, z: dG_i == dG_h
-            }
-            if (sh == 1) {  // n gate's input side: dG_in
-                AF a[NP];
-#pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    a[p] = frag_tr(&dgs[bf][p][tr][3 * H + 16 * w + tc], &dgs[bf][p][tr + 16][3 * H + 16 * w + tc]);
-                dwx[0] = mm(a, bx, dwx[0]);
-            }
-        }
+        if constexpr (!DEFER) dw_products(bf);
     };
     int t = L - 1;
     for (; t >= 1; t -= 2) {     // unconditional pairs: a conditional second half would merge
@@ -862,6 +870,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         step(t - 1, gB, hB, xB);
     }
     if (t == 0) step(0, gA, hA, xA);
+    if constexpr (DEFER) dw_products(0);  // step 0's dW
     if constexpr (F16) {  // back to plain units
         const float fh = lg_pow2f(-(sg_cur + 14)), fx = lg_pow2f(-(sg_cur + sx));
 #pragma unroll
@@ -938,20 +947,30 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
 #define LG_GRU_BWD(UT, DX)                                                                                       \
     lg_launch(k_gru_bwd<H, UT, DX>, grid, 4 * H, 0, s, residual, tfeat, w_ih, w_hh, h_seq, gates, dh_last, dx, slab,   \
                                                  Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
-#define LG_GRU_BWD2(UT, F)                                                                                       \
-    lg_launch(k_gru_bwd2<H, UT, F>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual, tfeat, \
-              w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+#define LG_GRU_BWD2(UT, F, DF)                                                                                   \
+    lg_launch(k_gru_bwd2<H, UT, F, DF>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual,    \
+              tfeat, w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
 #ifdef LG_KERNEL_LAB
-    const bool f16 = !getenv("LG_LAB_GRU_BF16X3");  // lab A/B: the 3-way bf16 split
-#else
-    constexpr bool f16 = true;
+    // lab A/B: LG_LAB_GRU_BF16X3 the 3-way bf16 split, LG_LAB_GRU_NODEFER each step's dW after its dh
+    if (!need_dx && (getenv("LG_LAB_GRU_BF16X3") || getenv("LG_LAB_GRU_NODEFER"))) {
+        const bool x3 = getenv("LG_LAB_GRU_BF16X3") != nullptr, nd = getenv("LG_LAB_GRU_NODEFER") != nullptr;
+        if (ut) {
+            if (x3) { if (nd) LG_GRU_BWD2(true, false, false); else LG_GRU_BWD2(true, false, true); }
+            else LG_GRU_BWD2(true, true, false);
+        } else {
+            if (x3) { if (nd) LG_GRU_BWD2(false, false, false); else LG_GRU_BWD2(false, false, true); }
+            else LG_GRU_BWD2(false, true, false);
+        }
+        LG_RET_IF_LAUNCH_FAILED();
+        return LG_OK;
+    }
 #endif
     if (need_dx) {
         if (ut) LG_GRU_BWD(true, true); else LG_GRU_BWD(false, true);
     } else if (ut) {
-        if (f16) LG_GRU_BWD2(true, true); else LG_GRU_BWD2(true, false);
+        LG_GRU_BWD2(true, true, true);
     } else {
-        if (f16) LG_GRU_BWD2(false, true); else LG_GRU_BWD2(false, false);
+        LG_GRU_BWD2(false, true, true);
     }
 #undef LG_GRU_BWD
 #undef LG_GRU_BWD2
