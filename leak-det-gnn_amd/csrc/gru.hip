@@ -95,17 +95,30 @@ __device__ __forceinline__ void stage_x(float* __restrict__ xs, const float* __r
     }
 }
 
+// two floats (already scaled) -> the packed hi and lo f16 parts of the f16x2 split:
+// hi = v_cvt_pk_f16_f32, each lo = f16(x - hi) one v_fma_mix{lo,hi}_f16 reading hi's half
+// (3 instructions a pair; the compiler's form converts hi back and subtracts: 5-7)
+__device__ __forceinline__ void split2_pair_mix(float a, float b, uint32_t& p0, uint32_t& p1) {
+    const lg_f32x2 v = {a, b};
+    p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_f16x2));
+    uint32_t lo;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(a), "v"(p0));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(p0));
+    p1 = lo;
+}
+
 // ------------------------------------------------------------------ forward
 // One wave per 16-row gate tile: 3 * H/16 waves per 16 sequences (12 at H = 64).  Wave
 // (g, u), g in {r, z, n}, u = unit group: the r and z waves post sigma(.) tiles to LDS; the
 // n wave u keeps W_in x + b_in and W_hn h + b_hn, forms n = tanh(.), h' = (1-z) n + z h for
 // units [16u, 16u+16) (h of its own units stays in registers, fp32) and posts h' to LDS,
 // from where every wave reads the next step's B operand.  Two barriers per step.
-// The recurrent product W_hh h runs on v_mfma_f32_16x16x32_bf16 with 3-way split operands
-// (split_bf16.h: six products, fp32-level accuracy): 12 MFMAs of 16 cycles per wave and
-// step instead of 16 v_mfma_f32_16x16x4_f32 of 32.  W_hh is split once into registers; h'
-// is split ONCE, by the n wave that produces it (4 values per lane), and posted as bf16
-// parts.  The K order of chunk c is permuted, k = 8q + p <-> unit 16(2c + p/4) + 4q + p%4,
+// The recurrent product W_hh h runs on v_mfma_f32_16x16x32_f16 with f16x2 split operands
+// (split_bf16.h: two parts, three products, fp32-level accuracy): 6 MFMAs of 16 cycles per
+// wave and step (12 on round 3's 3-way bf16 split, 16 v_mfma_f32_16x16x4_f32 of 32 before).
+// The scales need no bookkeeping: W_hh's per wave (its 16 rows, all of K), h' at the fixed
+// 2^14 (|h| <= 1).  W_hh is split once into registers; h' is split ONCE, by the n wave that
+// produces it (4 values per lane), and posted as f16 parts.  The K order of chunk c is permuted, k = 8q + p <-> unit 16(2c + p/4) + 4q + p%4,
 // so a lane's B fragment is exactly the lane's own outputs of n waves 2c and 2c+1: the
 // exchange is lane-major (reader lane == writer lane), one b128 read per chunk and part.
 // The x part (K = I <= 12) stays on v_mfma_f32_16x16x4_f32 (exact, off the critical path).
@@ -123,7 +136,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     constexpr int LC = H == 64 ? kLC : 30;  // H = 32: four workgroups per CU fit in LDS
     __shared__ __attribute__((aligned(16))) float xs[LC * TS * XR];
     __shared__ __attribute__((aligned(16))) f32x4 grz[2][NU][64];   // [r|z][unit group][lane]: sigma tiles
-    __shared__ __attribute__((aligned(16))) lg_u32x4 hbs[3][NC][64];  // h_t split parts: [part][chunk][lane]
+    __shared__ __attribute__((aligned(16))) lg_u32x4 hbs[2][NC][64];  // h_t split parts: [part][chunk][lane]
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = w / NU, u = w % NU;  // gate (0 r, 1 z, 2 n), unit group
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
@@ -131,16 +144,25 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     const bool valid = seq < Nseq;
 
     const int row = g * H + 16 * u + j;  // A-operand row of this lane
-    lg_bf16x8 ah[NC][3];
+    lg_f16x8 ah[NC][2];
+    float hunsc;  // 2^-(sW + 14): the h product's unscale
+    {
+        f32x4 v[NC][2];
+        float m = 0.f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        f32x4 v0, v1;
+        for (int c = 0; c < NC; ++c) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            v0[p] = Whh[row * H + 32 * c + 4 * q + p];
-            v1[p] = Whh[row * H + 32 * c + 16 + 4 * q + p];
+            for (int p = 0; p < 4; ++p) {
+                v[c][0][p] = Whh[row * H + 32 * c + 4 * q + p];
+                v[c][1][p] = Whh[row * H + 32 * c + 16 + 4 * q + p];
+                m = fmaxf(m, fmaxf(fabsf(v[c][0][p]), fabsf(v[c][1][p])));
+            }
         }
-        split3_x8(v0, v1, ah[c][0], ah[c][1], ah[c][2]);
+        const int sW = lg_f16_scale_exp_c(lg_wave_max_bits(__float_as_uint(m)));
+        const float sc = lg_pow2f(sW);
+        hunsc = lg_pow2f(-(sW + 14));
+#pragma unroll
+        for (int c = 0; c < NC; ++c) split2_f16_x8(v[c][0] * sc, v[c][1] * sc, ah[c][0], ah[c][1]);
     }
     // x-side A operand; column 10 meets x's constant-1 column: the x-side bias (r, z: both
     // biases) rides in the x product, exactly (x = 1)
@@ -156,7 +178,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     if (g == 2) {  // h_{-1} = 0 (published by the first staging barrier)
         lg_u32x2* dst = reinterpret_cast<lg_u32x2*>(&hbs[0][u >> 1][lane]) + (u & 1);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) dst[2 * NC * 64 * p] = lg_u32x2{0u, 0u};
+        for (int p = 0; p < 2; ++p) dst[2 * NC * 64 * p] = lg_u32x2{0u, 0u};
     }
 
     for (int t0 = 0; t0 < L; t0 += LC) {
@@ -174,11 +196,12 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
             f32x4 hp = zero4();
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
-                lg_bf16x8 hf[3];
+                lg_f16x8 hf[2];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) hf[p] = __builtin_bit_cast(lg_bf16x8, hbs[p][c][lane]);
-                hp = mfma_split(ah[c], hf, hp);
+                for (int p = 0; p < 2; ++p) hf[p] = __builtin_bit_cast(lg_f16x8, hbs[p][c][lane]);
+                hp = mfma_f16x2(ah[c], hf, hp);
             }
+            hp *= hunsc;
             if (g < 2) {
                 f32x4 sg;
 #pragma unroll
@@ -206,12 +229,13 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                         st4(gp + 3 * H, hp);
                     }
                 }
-                lg_u32x2 f0, f1, f2;
-                split3_x4(hcur, f0, f1, f2);
+                const f32x4 hsc = hcur * 16384.f;  // |h| <= 1 at the fixed scale 2^14
+                uint32_t a0, a1, b0, b1;
+                split2_pair_mix(hsc[0], hsc[1], a0, a1);
+                split2_pair_mix(hsc[2], hsc[3], b0, b1);
                 lg_u32x2* dst = reinterpret_cast<lg_u32x2*>(&hbs[0][u >> 1][lane]) + (u & 1);
-                dst[0] = f0;
-                dst[2 * NC * 64] = f1;
-                dst[4 * NC * 64] = f2;
+                dst[0] = lg_u32x2{a0, b0};
+                dst[2 * NC * 64] = lg_u32x2{a1, b1};
             }
             __syncthreads();  // (B) h_t posted; sigma slots free again
         }
@@ -477,17 +501,6 @@ constexpr int kGruKeep = 6;  // f16x2: a step scale is kept while the new bound 
     p0 = static_cast<uint16_t>(a);
     p1 = static_cast<uint16_t>(b);
     p2 = static_cast<uint16_t>(c);
-}
-// two floats (already scaled) -> the packed hi and lo f16 parts of the f16x2 split:
-// hi = v_cvt_pk_f16_f32, each lo = f16(x - hi) one v_fma_mix{lo,hi}_f16 reading hi's half
-// (3 instructions a pair; the compiler's form converts hi back and subtracts: 5-7)
-__device__ __forceinline__ void split2_pair_mix(float a, float b, uint32_t& p0, uint32_t& p1) {
-    const lg_f32x2 v = {a, b};
-    p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, lg_f16x2));
-    uint32_t lo;
-    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=&v"(lo) : "v"(a), "v"(p0));
-    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lo) : "v"(b), "v"(p0));
-    p1 = lo;
 }
 // one float -> the two f16 parts of the f16x2 split (already scaled)
 __device__ __forceinline__ void split2_1(float x, uint16_t& p0, uint16_t& p1) {
