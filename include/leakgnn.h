@@ -570,7 +570,12 @@ int lg_pool_head_bwd(const float* pooled, const float* hid, const float* w1, con
  * H in {32, 64}, I in {1, 10} (use_time False/True), one layer.
  * Backward (BPTT from the saved gates, no recompute): dh_last -> dx (fp32
  * [B*S][L][I], may be NULL), dW_ih, dW_hh, db_ih, db_hh (overwritten,
- * deterministic). */
+ * deterministic).
+ * Precision (round 4): the recurrent products of the forward and of the dx == NULL backward
+ * run on the f16x2 split (two f16 parts, power-of-two scales, fp32 accumulate: |error| <=
+ * 2^-22 of each product); the backward's dG scale follows a bound on the previous step's
+ * maxima, so gradients of any magnitude keep that accuracy (tests/test_gpu_parity.py
+ * test_gru_bwd_f16x2_scales).  The dx != NULL backward stays on fp32 MFMA. */
 int lg_gru_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
                const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last,
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H, lg_stream_t stream);

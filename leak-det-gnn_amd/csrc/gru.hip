@@ -529,6 +529,24 @@ __device__ __forceinline__ float absmax4(const f32x4& v) {
     return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
 
+#ifdef LG_NM3_STAMPS
+// kernel-lab timeline (stamps builds only): per wave, for steps t = kGruStampT0 .. +7, clock at
+// the step's start, before its barrier, after it, and once dh is formed; slot 32 the hw id
+constexpr int kGruStampT0 = 20, kGruStamps = 33;
+__device__ uint64_t g_gru_stamps[256 * 8 * kGruStamps];
+#define LG_GRU_STAMP(t, k)                                                                                 \
+    do {                                                                                                   \
+        const int st_ = kGruStampT0 + 7 - (t);                                                             \
+        if (lane == 0 && st_ >= 0 && st_ < 8 && blockIdx.x < 256)                                          \
+            g_gru_stamps[(static_cast<size_t>(blockIdx.x) * 8 + wid) * kGruStamps + 4 * st_ + (k)] =       \
+                __builtin_amdgcn_s_memtime();                                                              \
+    } while (0)
+#else
+#define LG_GRU_STAMP(t, k) \
+    do {                   \
+    } while (0)
+#endif
+
 template <int H, bool UT, bool F16, bool DEFER>
 __global__ void __launch_bounds__(GB2<H>::NTH)
 k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Whh,
@@ -771,6 +789,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
     };
     auto step = [&](const int t, f32x4 (&g_cur)[4], f32x4& h_cur, float (&x_cur)[XPT]) {
         const int bf = t & 1;
+        LG_GRU_STAMP(t, 0);
         float gsc = 1.f, gin_ = 1.f;  // F16: this step's dG scale and its inverse
         int sg = 0;                   // F16: its exponent
         if constexpr (F16) {
@@ -859,7 +878,9 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         }
         // dgs/hls/xls[bf] complete.  Buffer bf was last read at step t+2, which every wave
         // finished before arriving at step t+1's barrier: one barrier per step suffices.
+        LG_GRU_STAMP(t, 1);
         __syncthreads();
+        LG_GRU_STAMP(t, 2);
         if constexpr (F16) mcur = *reinterpret_cast<const lg_u32x2*>(&gmx[t % 3][0]);  // cleared at t-2
 
         // (2) dh_{t-1} = d z + W_hh^T dG_h: two accumulator chains
@@ -874,7 +895,11 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             }
             if constexpr (F16) dh += (acc[0] + acc[1]) * (sWinv * lg_pow2f(-sg_cur));
             else dh += acc[0] + acc[1];
+#ifdef LG_NM3_STAMPS
+            asm volatile("" ::"v"(dh[0]));  // the stamp after dh exists
+#endif
         }
+        LG_GRU_STAMP(t, 3);
         if constexpr (!DEFER) dw_products(bf);
     };
     int t = L - 1;
@@ -996,6 +1021,19 @@ bool dims_ok(int64_t B, int64_t L, int64_t S) {
 }
 
 }  // namespace
+
+#ifdef LG_NM3_STAMPS
+extern "C" int lg_lab_gru_stamps(uint64_t* host, int64_t n) {
+    if (n > static_cast<int64_t>(256) * 8 * kGruStamps) return LG_EINVAL;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gru_stamps), static_cast<size_t>(n) * 8) == hipSuccess ? LG_OK
+                                                                                                         : LG_EHIP;
+}
+extern "C" int lg_lab_gru_stamps_clear(void) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_gru_stamps)) != hipSuccess) return LG_EHIP;
+    return hipMemset(p, 0, sizeof(uint64_t) * 256 * 8 * kGruStamps) == hipSuccess ? LG_OK : LG_EHIP;
+}
+#endif
 
 extern "C" int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H) {
     if (B < 0 || S < 0 || (I != 1 && I != 10) || (H != 32 && H != 64)) return LG_EINVAL;

@@ -101,6 +101,36 @@ def stamps_summary(lib, launch):
             "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
 
 
+def gru_stamps_summary(lib, launch, nst=33, steps=8):
+    """k_gru_bwd2 per-step timeline (stamps build): for 8 mid-kernel steps of every wave, the
+    clocks at the step's start (a), before its barrier (b), after it (c) and once dh is formed
+    (d).  Medians over waves and steps, in clock cycles: a->b (elementwise part, refill, the
+    deferred dW, rescale), b->c (barrier wait), c->d (dh product), d->next a, the step period."""
+    lib.lg_lab_gru_stamps_clear.restype = ctypes.c_int
+    lib.lg_lab_gru_stamps.restype = ctypes.c_int
+    lib.lg_lab_gru_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    check(lib.lg_lab_gru_stamps_clear(), "gru stamps clear")
+    launch()
+    torch.cuda.synchronize()
+    n = 256 * 8 * nst
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib.lg_lab_gru_stamps(buf.ctypes.data, n), "gru stamps read")
+    a = buf.reshape(256 * 8, nst)[:, :4 * steps].reshape(-1, steps, 4).astype(np.float64)
+    a = a[(a > 0).all(axis=(1, 2))]  # waves that stamped every step (slot order: t descending)
+    if not len(a):
+        return {"waves": 0}
+    d = {"waves": int(len(a)),
+         "elementwise_dw_to_barrier": np.diff(a[:, :, 0:2], axis=2)[..., 0],
+         "barrier_wait": np.diff(a[:, :, 1:3], axis=2)[..., 0],
+         "dh_product": np.diff(a[:, :, 2:4], axis=2)[..., 0],
+         "dh_to_next_step": a[:, 1:, 0] - a[:, :-1, 3],
+         "step_period": a[:, 1:, 0] - a[:, :-1, 0]}
+    out = {"waves": d.pop("waves")}
+    for k, v in d.items():
+        out[k + "_cyc_p10_50_90"] = [round(float(np.percentile(v, p)), 1) for p in (10, 50, 90)]
+    return out
+
+
 def pc_stamps_summary(lib, launch, waves_per_wg=12, prod=4):
     """Per-wave timeline of one eager k_gcn_fwd_pc launch (LG_NM3_STAMPS build): producers and
     consumers separately — start / end, tiles handed over / stored, the per-tile interval, and
@@ -472,6 +502,8 @@ def main():
                                              ptr(ws), ws.numel(), cs()), "gru bwd")
             t = timeit(f, args.iters)
             res["gru_bwd"] = {"us": t, "TFLOPs": 2 * flops / t / 1e6}
+            if args.stamps and hasattr(lib, "lg_lab_gru_stamps"):
+                res["stamps_gru_bwd"] = gru_stamps_summary(lib, f)
     if "tcn" in which:
         # frozen-predictor residual builder, B segments of l_pred + l_det = 72 steps
         from models import tcn_plan
