@@ -531,14 +531,15 @@ __device__ __forceinline__ float absmax4(const f32x4& v) {
 
 #ifdef LG_NM3_STAMPS
 // kernel-lab timeline (stamps builds only): per wave, for steps t = kGruStampT0 .. +7, clock at
-// the step's start, before its barrier, after it, and once dh is formed; slot 32 the hw id
-constexpr int kGruStampT0 = 20, kGruStamps = 33;
+// the step's start, before its barrier, after it, once dh is formed, once the gate backward is
+// done (its loads waited for), after the LDS image and the refill are issued
+constexpr int kGruStampT0 = 20, kGruStamps = 48;
 __device__ uint64_t g_gru_stamps[256 * 8 * kGruStamps];
 #define LG_GRU_STAMP(t, k)                                                                                 \
     do {                                                                                                   \
         const int st_ = kGruStampT0 + 7 - (t);                                                             \
         if (lane == 0 && st_ >= 0 && st_ < 8 && blockIdx.x < 256)                                          \
-            g_gru_stamps[(static_cast<size_t>(blockIdx.x) * 8 + wid) * kGruStamps + 4 * st_ + (k)] =       \
+            g_gru_stamps[(static_cast<size_t>(blockIdx.x) * 8 + wid) * kGruStamps + 6 * st_ + (k)] =       \
                 __builtin_amdgcn_s_memtime();                                                              \
     } while (0)
 #else
@@ -823,6 +824,10 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
                 gr[reg] = dnp * hnp[reg] * r[reg] * (1.f - r[reg]);
                 gz[reg] = dzv * z[reg] * (1.f - z[reg]);
             }
+#ifdef LG_NM3_STAMPS
+            asm volatile("" ::"v"(gr[0]), "v"(gz[3]), "v"(ghn[1]), "v"(gin[2]));
+#endif
+            LG_GRU_STAMP(t, 4);
             if constexpr (F16) {
                 post(t % 3, absmax4(dh), fmaxf(absmax4(gr), fmaxf(absmax4(gz), absmax4(ghn))) * gin_);
                 dbhn += ghn * gin_;
@@ -860,6 +865,7 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         load_x(t - 2, x_cur);
         load_g(t - 2, g_cur);
         h_cur = load_h(t - 3);
+        LG_GRU_STAMP(t, 5);
         // DEFER: step t+1's dW (image bf ^ 1, rewritten only after this step's barrier) in the
         // MFMA pipe while this step's LDS writes land and the workgroup gathers at the barrier
         if constexpr (DEFER)

@@ -101,7 +101,7 @@ def stamps_summary(lib, launch):
             "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
 
 
-def gru_stamps_summary(lib, launch, nst=33, steps=8):
+def gru_stamps_summary(lib, launch, nst=48, steps=8):
     """k_gru_bwd2 per-step timeline (stamps build): for 8 mid-kernel steps of every wave, the
     clocks at the step's start (a), before its barrier (b), after it (c) and once dh is formed
     (d).  Medians over waves and steps, in clock cycles: a->b (elementwise part, refill, the
@@ -115,11 +115,14 @@ def gru_stamps_summary(lib, launch, nst=33, steps=8):
     n = 256 * 8 * nst
     buf = np.zeros(n, dtype=np.uint64)
     check(lib.lg_lab_gru_stamps(buf.ctypes.data, n), "gru stamps read")
-    a = buf.reshape(256 * 8, nst)[:, :4 * steps].reshape(-1, steps, 4).astype(np.float64)
+    a = buf.reshape(256 * 8, nst)[:, :6 * steps].reshape(-1, steps, 6).astype(np.float64)
     a = a[(a > 0).all(axis=(1, 2))]  # waves that stamped every step (slot order: t descending)
     if not len(a):
         return {"waves": 0}
     d = {"waves": int(len(a)),
+         "start_to_gates_done": a[:, :, 4] - a[:, :, 0],
+         "gates_done_to_refill_issued": a[:, :, 5] - a[:, :, 4],
+         "refill_to_barrier": a[:, :, 1] - a[:, :, 5],
          "elementwise_dw_to_barrier": np.diff(a[:, :, 0:2], axis=2)[..., 0],
          "barrier_wait": np.diff(a[:, :, 1:3], axis=2)[..., 0],
          "dh_product": np.diff(a[:, :, 2:4], axis=2)[..., 0],
