@@ -55,6 +55,14 @@ def all_pipe_ids(inp: Path):
     return sorted({ln.split()[0] for ln in sec["PIPES"]})  # dataset order: sorted pipe ids (datasets.py:353)
 
 
+def sampled_pipe_ids(ratio: float, seed: int = 198):
+    """The reference example's leak-set pipes (cmd.sh:10: --pipe_sample_ratio 0.5 --seed 198):
+    leak_generation.py:90-99's pick over the .inp's pipe order, sorted (models/synth.pick_pipes)."""
+    from models.synth import pick_pipes
+    from models.utils import parse_epanet_inp
+    return pick_pipes([ln.split()[0] for ln in parse_epanet_inp(LTA_INP)["PIPES"]], ratio, seed)
+
+
 def time_features(B: int, L: int, gen: torch.Generator) -> torch.Tensor:
     """(B, L, 9): hour sin/cos + day-of-week one-hot at 5-min steps (datasets.py:49-59)."""
     start = torch.randint(0, 7 * 288, (B, 1), generator=gen)
@@ -194,12 +202,20 @@ def small_kernels_us(breakdown: dict | None) -> dict:
 
 
 def step_breakdown(batch: int, ms_per_step: float, steps: int = 20) -> dict | None:
-    """Every kernel of one replay of the captured step (tools/step_trace.py under a child
-    `rocprofv3 --kernel-trace`): per-kernel device time, their sum, the replay's span, and
-    `step_gap_us` = the replay's span minus the sum (the time between kernels), beside
-    `step_minus_kernels_us` = ms_per_step (the bench's own, unprofiled clock) minus the sum
-    (negative when the profiler's per-dispatch cost inflates the kernels more).  The
-    replays between two k_gru_fwd launches are one step each; the median replay is reported."""
+    """Every kernel of the captured step as it runs in the graph replays (tools/step_trace.py
+    under a child `rocprofv3 --kernel-trace`).  The replays between two k_gru_fwd launches are
+    one step each; the later half (steady state) is used:
+      kernels          the median replay's kernels in launch order, with their durations;
+      kernels_mean_us  per launch position (name#occurrence: k_gcn_fwd_pc#1 is the second
+                       k_gcn_fwd_pc of the step, layer 1) the mean duration over the replays;
+      sum_us / replay_span_us / step_gap_us
+                       the median replay's kernel sum, its span (first kernel start to the next
+                       replay's first kernel start) and span minus sum (the gaps between kernels,
+                       including the one between replays);
+      replay_gap_us    median over replays of the next replay's first kernel start minus this
+                       replay's last kernel end: the device idles there while the host submits
+                       the next graph launch;
+      step_minus_kernels_us  ms_per_step (the bench's own, unprofiled clock) minus the sum."""
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None
@@ -221,23 +237,51 @@ def step_breakdown(batch: int, ms_per_step: float, steps: int = 20) -> dict | No
     marks = [i for i, r in enumerate(rows) if "k_gru_fwd" in r["Kernel_Name"]]
     if len(marks) < 4:
         return None
-    reps = []
+    reps, gaps = [], []
     for a, b in zip(marks[len(marks) // 2:-1], marks[len(marks) // 2 + 1:]):  # the later half: steady state
         ks = [(short_kernel_name(r["Kernel_Name"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
               for r in rows[a:b]]
         span = (int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+        gaps.append((int(rows[b]["Start_Timestamp"]) - int(rows[b - 1]["End_Timestamp"])) / 1e3)
         reps.append((sum(t for _, t in ks), span, ks))
+    n0 = len(reps[0][2])
+    same = [r for r in reps if len(r[2]) == n0]
+    pos = []
+    seen: dict = {}
+    for n, _ in reps[0][2]:
+        pos.append(f"{n}#{seen.get(n, 0)}")
+        seen[n] = seen.get(n, 0) + 1
+    mean_pos = {p: round(float(np.mean([r[2][i][1] for r in same])), 2) for i, p in enumerate(pos)}
     reps.sort(key=lambda x: x[0])
     tot, span, ks = reps[len(reps) // 2]
     agg: dict = {}
     for n, t in ks:
         agg[n] = round(agg.get(n, 0.0) + t, 2)
     return {"source": "rocprofv3 --kernel-trace over tools/step_trace.py (the same captured step), median replay",
-            "kernels": [[n, round(t, 2)] for n, t in ks], "by_name_us": agg, "launches": len(ks),
+            "kernels": [[n, round(t, 2)] for n, t in ks], "kernels_mean_us": mean_pos, "replays": len(same),
+            "by_name_us": agg, "launches": len(ks),
             "sum_us": round(tot, 1), "replay_span_us": round(span, 1), "step_us": round(ms_per_step * 1e3, 1),
-            "step_gap_us": round(span - tot, 1),
+            "step_gap_us": round(span - tot, 1), "replay_gap_us": round(float(np.median(gaps)), 2),
             "step_minus_kernels_us": round(ms_per_step * 1e3 - tot, 1),
             "accounted_frac": round(tot / (ms_per_step * 1e3), 4)}
+
+
+# kernels_us names -> launch position in the captured step (step_breakdown kernels_mean_us)
+STEP_POSITIONS = {"gru_fwd": "k_gru_fwd#0", "node_init": "k_node_init_bits#0", "gcn_fwd_l0": "k_gcn_fwd_pc#0",
+                  "gcn_fwd": "k_gcn_fwd_pc#1", "edge_fwd": "k_edge_fwd#0", "pool_head": "k_pool_head_fwd#0",
+                  "pool_head_bwd": "k_pool_head_bwd#0", "edge_bwd": "k_edge_bwd#0", "gcn_bwd": "k_gcn_bwd_nm3#0",
+                  "gcn_bwd_l0": "k_gcn_bwd_nm3#1", "linear_dw": "k_sensor_proj_bwd#0", "gru_bwd": "k_gru_bwd2#0"}
+
+
+def in_step_kernels_us(breakdown: dict | None) -> dict:
+    """kernels_us from the captured step's trace: each named kernel's mean in-graph duration
+    (us) at its launch position, plus the small launches' per-step sums."""
+    if not breakdown:
+        return {}
+    mp = breakdown["kernels_mean_us"]
+    out = {k: mp[v] for k, v in STEP_POSITIONS.items() if v in mp}
+    out.update(small_kernels_us(breakdown))
+    return out
 
 
 def stream_copy_peak(dev, nbytes: int = 2 << 30, iters: int = 10) -> dict:
@@ -505,15 +549,18 @@ def CrossEntropyLoss():
     return _CE()
 
 
-def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str, batch: int) -> dict:
+def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str, batch: int,
+             pipe_ratio: float = 1.0) -> dict:
     """BASELINE configs[2] as written — "bf16 node-MLP on MFMA" (SURVEY §8 d C3: bf16 for the
     K5 GCN transforms and the K9 EdgeHead MLP, fp32 accumulate): the same L-TOWN-A training
     step with LeakDetector(mlp_dtype=...), captured, timed like the main line; plus the
-    in-step durations of the kernels whose products change."""
+    in-step durations of the kernels whose products change.  pipe_ratio 0.5: the same step
+    with the reference example's leak set (cmd.sh:10 --pipe_sample_ratio 0.5: P = 382 of the
+    764 pipes, models/synth.pick_pipes), SURVEY §8(d) C3's "also report P=382"."""
     from models import ops
     from models.detector import LeakDetector
     from models.graph_step import CapturedTrainStep
-    pipes = all_pipe_ids(LTA_INP)
+    pipes = all_pipe_ids(LTA_INP) if pipe_ratio >= 1.0 else sampled_pipe_ids(pipe_ratio)
     P, B = len(pipes), batch
     torch.manual_seed(0)
     m = LeakDetector(LTA_INP, SENSORS, pipes, sensor_hidden=64, node_hidden=64, gnn_layers=2, dropout=0.1,
@@ -551,13 +598,13 @@ def tier_leg(dev, steps: int, warmup: int, rank: int, world: int, mlp_dtype: str
     timer.enabled = False
     ops.set_kernel_timer(None)
     kms = {k: timer.mean_ms(k) for k in names}
-    return {"metric": "windowed graphs/sec fwd+bwd on L-TOWN-A (BASELINE configs[2]: bf16 node-MLP on MFMA)"
-            if mlp_dtype == "bf16" else "windowed graphs/sec fwd+bwd on L-TOWN-A (fp32 node-MLP)",
+    what = ("bf16 node-MLP on MFMA" if mlp_dtype == "bf16" else "fp32 node-MLP") + (f", P = {P}" if pipe_ratio < 1 else "")
+    return {"metric": f"windowed graphs/sec fwd+bwd on L-TOWN-A (BASELINE configs[2]: {what})",
             "value": round(B * world * steps / el, 2), "unit": "windows/s", "ms_per_step": round(el * 1e3 / steps, 4),
-            "mlp_dtype": mlp_dtype, "windows_per_rank": B, "scaling": "weak",
+            "mlp_dtype": mlp_dtype, "windows_per_rank": B, "scaling": "weak", "pipes": P,
             "parity": "logits within 2e-2 of the fp32 oracle (tests/test_gpu_configs.py::test_bf16_tier_b256)"
             if mlp_dtype == "bf16" else "fp32 bars",
-            "kernels_us": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()}}
+            "kernels_us_eager": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()}}
 
 
 def _event_ms(fn, iters: int) -> float:
@@ -700,6 +747,7 @@ def main() -> None:
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="node-MLP tier of the main line: fp32 (split-bf16 MFMA, fp32 parity) or bf16 (configs[2])")
     ap.add_argument("--no-tier-leg", action="store_true", help="skip the leg of the other node-MLP tier")
+    ap.add_argument("--no-p382", action="store_true", help="skip the P = 382 leg (cmd.sh:10's pipe_sample_ratio 0.5)")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
 
@@ -825,18 +873,27 @@ def main() -> None:
     fwd_bytes = 8 * B * N * D + csr_bytes           # read x once, write y once
     # layer-L-1 backward: read dy, x and the forward's [y > 0] bits (B*N*D/8 bytes); write dx
     bwd_bytes = 12 * B * N * D + N * ((B + 15) // 16) * 128 + csr_bytes
-    fwd_ms, bwd_ms = kms["gcn_fwd"], kms["gcn_bwd"]
+    pmc = world == 1 and not args.no_pmc
+    # the kernels as they run in the timed (captured) step: rocprofv3 kernel trace of the same
+    # step graph's replays; the eager pass-2 event timings are reported beside as *_eager
+    breakdown = step_breakdown(B, elapsed * 1e3 / args.steps) if (pmc and not args.eager) else None
+    kin = in_step_kernels_us(breakdown)
+    timing = "in-graph (captured step replays, rocprofv3 kernel trace: step_kernels)" if kin else \
+        "eager launches, HIP event pairs (pass 2)"
+    fwd_ms = kin["gcn_fwd"] * 1e-3 if "gcn_fwd" in kin else kms["gcn_fwd"]
+    bwd_ms = kin["gcn_bwd"] * 1e-3 if "gcn_bwd" in kin else kms["gcn_bwd"]
     achieved = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     graph = model._device_state(dev)[0]
     prop_ms = time_propagate(graph, B, N, D, dev)
     prop_gbs = fwd_bytes / (prop_ms * 1e-3) / 1e9
     copy = stream_copy_peak(dev)
-    pmc = world == 1 and not args.no_pmc
     traffic = pmc_traffic("gcn_fwd_nm_train", "k_gcn_fwd_pc", B) if pmc else None
     traffic_bwd = pmc_traffic("gcn_bwd_nm", "k_gcn_bwd_nm", B) if pmc else None
-    gru_rep = gru_mfma_report(kms, B, len(SENSORS))
-    breakdown = step_breakdown(B, elapsed * 1e3 / args.steps) if (pmc and not args.eager) else None
+    gru_rep = gru_mfma_report({k: (kin[k] * 1e-3 if k in kin else kms.get(k)) for k in ("gru_fwd", "gru_bwd")},
+                              B, len(SENSORS))
+    p382 = None if (args.no_p382 or args.batch != 256) else tier_leg(dev, args.steps, 3, rank, world, args.dtype, B,
+                                                                     pipe_ratio=0.5)
     src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the same launch, 2*FETCH+WRITE (gfx950)"
     out = {
         "metric": "windowed graphs/sec fwd+bwd on L-TOWN-A", "value": round(value, 2), "unit": "windows/s",
@@ -857,7 +914,8 @@ def main() -> None:
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": round(traffic["bytes"]) if traffic else None,
                      "traffic_source": src if traffic else None,
-                     "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2),
+                     "bytes_per_launch": fwd_bytes, "avg_launch_us": round(fwd_ms * 1e3, 2), "timing": timing,
+                     "avg_launch_us_eager": round(kms["gcn_fwd"] * 1e3, 2),
                      "frac_of_measured_copy": round(achieved / copy["GBps"], 4)},
         "roofline_bwd": {"kernel": "lg_gcn_bwd_nm_bits (layer 2: gather of dy * [y > 0] over the transposed CSR, "
                                    "[y > 0] from the forward's mask bits; dx = t W, dW, db, masked by [x > 0])",
@@ -866,16 +924,18 @@ def main() -> None:
                          "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
                          "traffic": round(traffic_bwd["bytes"]) if traffic_bwd else None,
                          "traffic_source": src if traffic_bwd else None,
-                         "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2)},
+                         "bytes_per_launch": bwd_bytes, "avg_launch_us": round(bwd_ms * 1e3, 2), "timing": timing,
+                         "avg_launch_us_eager": round(kms["gcn_bwd"] * 1e3, 2)},
         "roofline_propagate": {"kernel": "lg_spmm (K6 alone, same graph and shape)", "bound": "hbm",
                                "achieved": round(prop_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(prop_gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(prop_ms * 1e3, 2)},
         "stream_copy": copy,
         **xchg,
         "gru_mfma": gru_rep,
-        "kernels_us": {**{k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
-                       **small_kernels_us(breakdown)},
+        "kernels_us": kin or None,
+        "kernels_us_eager": {k: (round(v * 1e3, 2) if v is not None else None) for k, v in kms.items()},
         "step_gap_us": breakdown["step_gap_us"] if breakdown else None,
+        "replay_gap_us": breakdown["replay_gap_us"] if breakdown else None,
         "step_kernels": breakdown,
         "final_loss": round(final_loss, 4),
     }
@@ -890,6 +950,8 @@ def main() -> None:
         out["c5"] = c5
     if tier is not None:
         out["mlp_tier"] = tier
+    if p382 is not None:
+        out["p382"] = p382
     if world == 1:
         out["e2e_training"] = e2e_training(model, opt, label, B, max(5, args.steps // 2), dev)
     if world == 1 and not args.no_cpu_baseline:

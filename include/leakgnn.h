@@ -129,6 +129,11 @@ int lg_stream_copy(const void* src, void* dst, int64_t bytes, lg_stream_t stream
  * streams at every replay without the host.  No reference counterpart (the reference's
  * nn.Dropout draws from torch's generator). */
 int lg_seed_slots_advance(uint64_t* slots, int64_t n, uint64_t* state, lg_stream_t stream);
+
+/* Replay of a captured step: hipGraphLaunch(graph_exec, stream), n times in a row (graph_exec:
+ * an instantiated hipGraphExec_t, e.g. torch.cuda.CUDAGraph.raw_cuda_graph_exec()).  Replaces
+ * nothing in the reference (its training step is eager, train_detector.py:296-317). */
+int lg_graph_replay(void* graph_exec, int64_t n, lg_stream_t stream);
 const char* lg_strerror(int code);
 
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;

@@ -130,12 +130,18 @@ struct Nm3Lds {  // dynamic LDS layout (floats)
     static __device__ __forceinline__ int tix(int r, int c) { return r * NmGeo<D>::S + 4 * c; }
 };
 
-#ifdef LG_NM3_STAMPS
+#if defined(LG_NM3_STAMPS) || defined(LG_PC_PROBE)
 // kernel-lab timeline (LG_NM3_STAMPS builds only): per wave, slot 0 realtime at start, 1 clock
 // at start, 2 after the W staging barrier, 3 + 3 t .. 5 + 3 t for tile t < 6 (rows
 // accumulated, transform done, stores issued), 21 clock at end, 22 realtime at end, 23 hw id.
+// LG_PC_PROBE builds (k_gcn_fwd_pc only): the same slots 0, 1, 2, 21, 22, 23 and the wave's
+// tile count in slot 3, all held in registers and stored once at the wave's end, so the
+// kernel runs at product speed (the per-tile stamps' s_memtime waits on lgkmcnt, which also
+// drains the record prefetch and the LDS traffic: that build runs 2.9x slow).
 constexpr int kNm3Stamps = 24;
 __device__ uint64_t g_nm3_stamps[8192 * kNm3Stamps];
+#endif
+#ifdef LG_NM3_STAMPS
 #define LG_NM3_STAMP(slot, v)                                                                      \
     do {                                                                                           \
         if (lane == 0) g_nm3_stamps[(static_cast<size_t>(blockIdx.x) * WAVES + wave) * kNm3Stamps + (slot)] = (v); \
@@ -585,6 +591,23 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
     }
 #endif
+#ifdef LG_PC_PROBE
+    const uint64_t probe_rt0 = __builtin_amdgcn_s_memrealtime(), probe_c0 = __builtin_amdgcn_s_memtime();
+    auto probe_end = [&](uint64_t c1, uint64_t tiles) {
+        const uint64_t c2 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            uint64_t* o = g_nm3_stamps + (static_cast<size_t>(blockIdx.x) * (kPcProd * (1 + NC)) + wave) * kNm3Stamps;
+            o[0] = probe_rt0;
+            o[1] = probe_c0;
+            o[2] = c1;
+            o[3] = tiles;
+            o[21] = c2;
+            o[22] = rt1;
+            o[23] = (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                    static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
+        }
+    };
+#endif
     const int prod = producer ? wave : (wave - kPcProd) % kPcProd;  // the producer this wave is or serves
     const int cons = producer ? 0 : (wave - kPcProd) / kPcProd;     // consumer index 0 .. NC-1
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
@@ -638,6 +661,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (threadIdx.x == 0) *ctr = 0u;
     }
     __syncthreads();
+#ifdef LG_PC_PROBE
+    const uint64_t probe_c1 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef LG_NM3_STAMPS
     LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
     auto pc_stamp_end = [&]() {
@@ -850,6 +876,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #ifdef LG_NM3_STAMPS
         pc_stamp_end();
 #endif
+#ifdef LG_PC_PROBE
+        probe_end(probe_c1, static_cast<uint64_t>(t));
+#endif
         return;
     }
 
@@ -889,7 +918,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     }
     const uint32_t key = lg_dropout_key_dev(seed, salt);
     const uint32_t thr = lg_keep_threshold16(p_drop);
-    for (int64_t u = 0;; ++u) {
+    int64_t u = 0;
+    for (;; ++u) {
         const int64_t t = u * NC + cons;  // this consumer's u-th tile of its producer
         // wait for tile t, or for the producer's end (it handed over fin[prod] tiles in all)
         if (!pc_wait_or_fin(&ready[prod], &fin[prod], static_cast<uint32_t>(t + 1))) break;
@@ -1036,6 +1066,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     }
 #ifdef LG_NM3_STAMPS
     pc_stamp_end();
+#endif
+#ifdef LG_PC_PROBE
+    probe_end(probe_c1, static_cast<uint64_t>(u));
 #endif
 }
 
@@ -2075,8 +2108,8 @@ extern "C" int lg_gcn_fwd_nm_x0(const int32_t* nodetab_s, const int32_t* pairs_s
     return nm_fwd(nodetab_s, pairs_s, xs0, W, bias, y, B, N, D, flags, dropout_p, seed, salt, stream, nullptr, &x0);
 }
 
-#ifdef LG_NM3_STAMPS
-// kernel-lab timeline readout (LG_NM3_STAMPS builds only; see g_nm3_stamps)
+#if defined(LG_NM3_STAMPS) || defined(LG_PC_PROBE)
+// kernel-lab timeline readout (LG_NM3_STAMPS / LG_PC_PROBE builds only; see g_nm3_stamps)
 extern "C" int lg_lab_nm3_stamps(uint64_t* host, int64_t n) {
     if (n > static_cast<int64_t>(8192) * kNm3Stamps) return LG_EINVAL;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_nm3_stamps), static_cast<size_t>(n) * 8) == hipSuccess ? LG_OK

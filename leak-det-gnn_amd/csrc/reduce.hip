@@ -262,3 +262,14 @@ extern "C" int lg_seed_slots_advance(uint64_t* slots, int64_t n, uint64_t* state
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
+
+// ---------------------------------------------------------------- graph replay
+// A captured training step (models/graph_step.py) replayed by hipGraphLaunch of its
+// instantiated executable: torch's CUDAGraph.replay() adds its own per-replay host work
+// (generator-state prologue) in front of the same launch.
+extern "C" int lg_graph_replay(void* graph_exec, int64_t n, lg_stream_t stream) {
+    if (!graph_exec || n < 0) return LG_EINVAL;
+    for (int64_t i = 0; i < n; ++i)
+        if (hipGraphLaunch(static_cast<hipGraphExec_t>(graph_exec), lg_stream(stream)) != hipSuccess) return LG_EHIP;
+    return LG_OK;
+}

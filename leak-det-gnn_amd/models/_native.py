@@ -42,6 +42,7 @@ SIGNATURES = {
     "lg_reduce_batch_flush": (_i32, [_p]),
     "lg_stream_copy": (_i32, [_p, _p, _i64, _p]),
     "lg_seed_slots_advance": (_i32, [_p, _i64, _p, _p]),
+    "lg_graph_replay": (_i32, [_p, _i64, _p]),
     "lg_cross_entropy_fwd": (_i32, [_p, _p, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p]),
     "lg_cross_entropy_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_clip_adamw_workspace_bytes": (_i64, [_p, _i32]),

@@ -141,6 +141,11 @@ class LeakDetector(nn.Module):
         # node-major trunk: keep the node init compressed (sensor rows + [x0 > 0] bits,
         # lg_node_init_bits_fwd) instead of materialising x_0 (43 MB at B = 256)
         self.compress_x0 = True
+        # EdgeHead backward node sums: True = streamed per tile through the pipe schedule (each
+        # node's incidences summed in schedule order); False = the reference's order (items
+        # ascending, as index_add over pipe ids), per-window scatter.  Read when the device
+        # state is first built.
+        self.incidence_schedule = True
         self.boundary: Optional[torch.Tensor] = None
 
     def overlap_split(self):
@@ -154,18 +159,28 @@ class LeakDetector(nn.Module):
         if st is None:
             N = len(self.node_names)
             graph = ops.GCNGraph.build(self.edge_index_single, N, device, add_self_loops=True, normalize=True)
-            inc = ops.Incidence.build(self.pipe_ends, N, device)
+            inc = ops.Incidence.build(self.pipe_ends, N, device, schedule=self.incidence_schedule)
             slot = torch.full((N,), -1, dtype=torch.int32)
             for s, n in enumerate(self.sensor_node_idx.tolist()):
                 slot[n] = s  # duplicate sensor ids: last write wins, as h0[:, idx] = h_s does
             live = torch.tensor([float(slot[n] == s) for s, n in enumerate(self.sensor_node_idx.tolist())])
             nonsensor = torch.nonzero(slot < 0).flatten()
-            # the compressed layer-0 input's sensor-marked node tables (lg_nm_table_sensor_mark)
-            graph.x0marks = ops.SensorMarks.build(graph, slot.to(device))
+            graph.x0marks = None  # built on the first node-major forward that compresses x_0 (_x0marks)
             st = (graph, inc, slot.to(device), self.sensor_node_idx.to(device),
                   None if bool(live.all()) else live.to(device), nonsensor.to(device))
             self._dev_state[device] = st
         return st
+
+    def _x0marks(self, graph, slot: torch.Tensor):
+        """The compressed layer-0 input's sensor-marked node tables (lg_nm_table_sensor_mark),
+        built once per device on the first forward that uses them (window-major batches never
+        do).  Its launches must run eagerly, not be recorded into a graph being captured."""
+        if graph.x0marks is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("LeakDetector: run one eager node-major forward before capturing a graph "
+                                   "(the compressed node init's tables are built on first use)")
+            graph.x0marks = ops.SensorMarks.build(graph, slot)
+        return graph.x0marks
 
     def forward(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
         if not residual.is_cuda:
@@ -185,7 +200,7 @@ class LeakDetector(nn.Module):
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
         # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init
-        mk = g.x0marks if (nm and self.compress_x0) else None
+        mk = self._x0marks(g, slot) if (nm and self.compress_x0 and len(self.convs) > 1) else None
         out = torch.ops.leakgnn.gnn_trunk(
             h_s, Wn, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
             nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,

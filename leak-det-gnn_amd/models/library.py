@@ -367,6 +367,17 @@ def expand_x0(xs0: Tensor, x0bits: Tensor, sensor_slot: Tensor, node_bias: Tenso
 
 
 # ============================================================================ gnn_trunk
+def _compress_x0(nodetab_s: Optional[Tensor], node_major: bool, L: int) -> bool:
+    """Whether gnn_trunk keeps x_0 compressed (sensor rows + [x_0 > 0] bits).  Needs a layer
+    after layer 0 (L >= 2): the last layer's backward reads its input mask through
+    LG_F_MASK_IN, which the x0 backward has no form of (lg_gcn_bwd_nm_x0 returns
+    LG_EUNSUPPORTED), so at L == 1 the dense node init runs.  A trunk-forward flag that selects
+    another forward kernel (LG_F_NM3, LG_F_F32_MFMA: the A/B and exact-fp32 modes) has no x0
+    variant either; it also gets the dense node init, so the flag applies to every layer."""
+    other = GCN_FWD_NM_EXTRA_FLAGS & (nat.LG_F_NM3 | nat.LG_F_F32_MFMA)
+    return nodetab_s is not None and node_major and L > 1 and not other
+
+
 @torch.library.custom_op(f"{NS}::gnn_trunk", mutates_args=(), device_types="cuda")
 def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor],
               sensor_slot: Tensor, sensor_idx: Tensor, nonsensor_idx: Tensor, slot_live: Optional[Tensor],
@@ -409,7 +420,7 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
     st = stream_of(h_s)
     L = len(weights)
     nmask = N * ((B + 15) // 16) * 64
-    x0c = nodetab_s is not None and node_major and L > 0
+    x0c = _compress_x0(nodetab_s, node_major, L)
     if x0c:
         x0 = torch.empty((S, B, D), device=h_s.device, dtype=torch.float32)
         x0bits = torch.empty(nmask, device=h_s.device, dtype=torch.int16)
@@ -457,7 +468,7 @@ def _(h_s, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx, non
     shape = (N, B, D) if node_major else (B, N, D)
     L = len(weights)
     nmask = N * ((B + 15) // 16) * 64 if (node_major and L > 0) else 0
-    x0c = nodetab_s is not None and node_major and L > 0
+    x0c = _compress_x0(nodetab_s, node_major, L)
     x0 = h_s.new_empty((S, B, D)) if x0c else h_s.new_empty(shape)
     return ([x0] + [h_s.new_empty(shape) for _ in range(L)] + [h_s.new_empty((nmask,), dtype=torch.int16)]
             + [h_s.new_empty((nmask if x0c else 0,), dtype=torch.int16)])

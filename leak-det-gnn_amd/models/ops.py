@@ -228,8 +228,9 @@ class SensorMarks:
                                           ptr(pairs_s), ptr(pos), st), "lg_nm_table_sensor_mark")
         check(lib.lg_nm_table_sensor_mark(ptr(g.nodetab_t), ptr(g.pairs_t), N, g.pairs_t.shape[0], ptr(slot),
                                           ptr(scratch_t), ptr(scratch_p), ptr(pos_t), st), "lg_nm_table_sensor_mark")
-        torch.cuda.current_stream(slot.device).synchronize()  # the scratch copies go out of scope here
-        return SensorMarks(tab_s, pairs_s, pos_t)
+        marks = SensorMarks(tab_s, pairs_s, pos_t)
+        marks._keepalive = (slot, pos, scratch_t, scratch_p)  # live until the stream has consumed them
+        return marks
 
 
 def schedule_order(edge_index: torch.Tensor, num_nodes: int) -> torch.Tensor:

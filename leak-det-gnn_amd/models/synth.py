@@ -102,6 +102,19 @@ def pick_sensors(node_ids: Sequence[str], count: int = 29, seed: int = 0) -> lis
     return [node_ids[i] for i in sorted(rng.choice(len(node_ids) - 1, size=count, replace=False))]
 
 
+def pick_pipes(pipe_ids: Sequence[str], ratio: float, seed: int = 198) -> list:
+    """The leak set's pipe list for `--pipe_sample_ratio ratio` (reference
+    data_gen/leak_generation.py:90-99 with default_rng(seed), seed 198 as in cmd.sh:10),
+    sorted as the datasets order them (datasets.py:353): the detector's pipe_ids_in_order.
+    ratio 0.5 on L-TOWN-A's 764 pipes gives P = 382."""
+    ratio = min(max(float(ratio), 0.0), 1.0)
+    if ratio <= 0 or not pipe_ids:
+        return []
+    n = max(1, int(round(len(pipe_ids) * ratio)))
+    idx = np.random.default_rng(int(seed)).choice(len(pipe_ids), size=n, replace=False)
+    return sorted(pipe_ids[i] for i in idx)
+
+
 # ------------------------------------------------------------------ sensor data sets
 def _sensor_frame(sensor_ids: Sequence[str], T: int, rng: np.random.Generator, start: str,
                   drop: Optional[np.ndarray] = None):

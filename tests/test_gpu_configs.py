@@ -243,9 +243,21 @@ def test_c5_detector_vs_oracle(tmp_path):
 
 
 # ----------------------------------------------------------------------------- configs[2] at B = 256
-def _random_ref(seed: int):
+def lta_pipes_p382(pipes):
+    """configs[2] with the reference example's `--pipe_sample_ratio 0.5` (cmd.sh:10): 382 of the
+    764 pipes, picked as leak_generation.py:90-99 does (models/synth.pick_pipes)."""
+    from models.synth import pick_pipes
+    from models.utils import parse_epanet_inp
+    inp_order = [ln.split()[0] for ln in parse_epanet_inp(LTA_INP)["PIPES"]]
+    sub = pick_pipes(inp_order, 0.5, seed=198)
+    assert len(sub) == 382 and set(sub) <= set(pipes)
+    return sub
+
+
+def _random_ref(seed: int, pipes=None):
     from oracle.detector_ref import LeakDetectorRef
-    sensors, pipes = lta_ids()
+    sensors, all_pipes = lta_ids()
+    pipes = all_pipes if pipes is None else pipes
     torch.manual_seed(seed)
     ref = LeakDetectorRef(LTA_INP, sensors, pipes).eval()
     with torch.no_grad():
@@ -254,8 +266,10 @@ def _random_ref(seed: int):
     return {k: v.clone() for k, v in ref.state_dict().items()}
 
 
-def test_detector_b256_eval_vs_oracle():
-    """L-TOWN-A at the bench batch (B = 256, node-major trunk), eval mode, random weights:
+@pytest.mark.parametrize("P", [764, 382])
+def test_detector_b256_eval_vs_oracle(P):
+    """P = 764 (every pipe) and P = 382 (cmd.sh:10's --pipe_sample_ratio 0.5: a different pipe
+    schedule, 12 pipe tiles per window instead of 24).  L-TOWN-A at the bench batch (B = 256, node-major trunk), eval mode, random weights:
     logits within 1e-5 of the oracle; grads for the oracle's fp64 CE gradient vs fp64 truth
     on the same side of every kink.  A ReLU pre-activation within fp32 rounding of 0, or an
     h_u - h_v of two nodes with (near-)identical features behind |h_u - h_v|, may fall
@@ -265,13 +279,16 @@ def test_detector_b256_eval_vs_oracle():
     fp64 truth and the fp32 yardsticks are all evaluated on the HIP path's side."""
     from models.detector import LeakDetector
     sensors, pipes = lta_ids()
-    sd = _random_ref(41)
+    if P == 382:
+        pipes = lta_pipes_p382(pipes)
+    net = (LTA_INP, sensors, pipes, {})
+    sd = _random_ref(41, pipes)
     B = 256
     gen = torch.Generator().manual_seed(42)
     r = torch.randn(B, 36, 29, generator=gen)
     tf = torch.randn(B, 36, 9, generator=gen)
     lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen)
-    _, _, pre64, up = oracle_run(sd, r, tf, torch.float64, "cpu", lab=lab)
+    _, _, pre64, up = oracle_run(sd, r, tf, torch.float64, "cpu", lab=lab, net=net)
     m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
     m.load_state_dict(sd)
     m.capture = {}
@@ -280,9 +297,9 @@ def test_detector_b256_eval_vs_oracle():
     masks = hip_relu_masks(m.capture, B, len(m.node_names), len(pipes), m.pipe_ends)
     check_relu_ties(pre64, masks)
     # truth and fp32 yardsticks all on the HIP path's side of every kink
-    _, g64, _, _ = oracle_run(sd, r, tf, torch.float64, "cpu", up=up, masks=masks)
-    o32, g32, _, _ = oracle_run(sd, r, tf, torch.float32, "cpu", up=up, masks=masks)
-    _, g32d, _, _ = oracle_run(sd, r, tf, torch.float32, DEV, up=up, masks=masks)
+    _, g64, _, _ = oracle_run(sd, r, tf, torch.float64, "cpu", up=up, masks=masks, net=net)
+    o32, g32, _, _ = oracle_run(sd, r, tf, torch.float32, "cpu", up=up, masks=masks, net=net)
+    _, g32d, _, _ = oracle_run(sd, r, tf, torch.float32, DEV, up=up, masks=masks, net=net)
     assert_close(lg, o32, what="B=256 logits")
     # The CE gradient makes dW1 of the EdgeHead and the conv bias grads the difference of two
     # sums over ~2e5 rows that nearly cancel (the label rows against all the others): per

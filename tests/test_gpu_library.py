@@ -114,7 +114,7 @@ def test_opcheck_trunk_and_heads(B, p):
     bs = [c.bias.detach().clone().normal_(0, 0.1).requires_grad_(True) for c in m.convs]
     nb = torch.randn(64, device=DEV, requires_grad=True)
     g = graph
-    mk = g.x0marks  # node-major: the compressed node init (lg_node_init_bits_fwd, lg_gcn_*_nm_x0)
+    mk = m._x0marks(g, slot)  # node-major: the compressed node init (lg_node_init_bits_fwd, lg_gcn_*_nm_x0)
     marks = (mk.nodetab_s, mk.pairs_s, mk.pos_slot_t) if nm else (None, None, None)
     _check(torch.ops.leakgnn.gnn_trunk.default,
            (h_s, Wn, nb, wts, bs, slot, sidx, nons, live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t,

@@ -162,7 +162,14 @@ def test_detector_vs_reference_fixture(fixture):
     assert_grads_match_truth({n: p.grad for n, p in m.named_parameters()}, g32, g64)
 
 
-def test_detector_vs_oracle_b64_random_weights():
+@pytest.mark.parametrize("schedule", [True, False])
+def test_detector_vs_oracle_b64_random_weights(schedule):
+    """B=64, random weights (schedule: the pipe-schedule order of the EdgeHead backward's node
+    sums, the default; False: the reference's ascending incidence order, per-window scatter)."""
+    _b64_vs_oracle(schedule)
+
+
+def _b64_vs_oracle(schedule: bool):
     """B=64, random weights.  Forward within 1e-5 of the oracle; backward driven by ONE
     fixed upstream gradient dL/dlogits (the fp64 cross-entropy gradient of the oracle's
     logits) fed to both paths, so the comparison covers the detector and not torch's
@@ -179,7 +186,9 @@ def test_detector_vs_oracle_b64_random_weights():
             c.bias.normal_(0, 0.1)
     sd = {k: v.clone() for k, v in ref.state_dict().items()}
     from models.detector import LeakDetector
-    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
+    m = LeakDetector(LTA_INP, sensors, pipes)
+    m.incidence_schedule = schedule
+    m = m.to(DEV).eval()
     m.load_state_dict(sd)
     B = 64
     gen = torch.Generator().manual_seed(12)
@@ -687,15 +696,19 @@ def test_gru_encoder_vs_torch_cpu(use_time, dx, H, B):
                        {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
 
 
-@pytest.mark.parametrize("gscale,wmax,H", [(1e-9, 0.3, 64), (1e6, 0.3, 64), (1.0, 0.5, 64), (3e-5, 1.0, 32)])
+@pytest.mark.parametrize("gscale,wmax,H", [(1e-9, 0.3, 64), (1e6, 0.3, 64), (1.0, 0.5, 64), (1.0, 1.0, 64),
+                                            (3e-5, 1.0, 32)])
 def test_gru_bwd_f16x2_scales(gscale, wmax, H):
     """The training backward (k_gru_bwd2 on the f16x2 split) keeps fp32-level accuracy when the
     incoming gradient is tiny or huge (the per-step dG scale follows it: bound from the previous
     step's maxima) and with larger weights, whose dh grows or shrinks fast over the 36 steps.
-    (At +-1 and H = 64 the recurrence is chaotic: the fp32 CPU reference and the GPU forward
-    part by 1.5e-3 of the gradient whichever split the backward uses, r04n2.)"""
+    Judged against the fp64 truth (nn.GRU in float64 on the CPU): every gradient within 4x the
+    fp32 CPU reference's own error or 1e-5 of its scale.  At +-1 and H = 64 the recurrence
+    amplifies rounding (any fp32 evaluation is ~1e-3 of the gradient off fp64, r04n2), so a
+    direct GPU-vs-fp32-CPU comparison measures the CPU's error as much as the kernel's."""
     from models.detector import SharedSensorGRUEncoder
     from oracle.detector_ref import _GRUEncoder
+    from helpers import assert_grads_match_truth
     torch.manual_seed(7)
     ref = _GRUEncoder(H, use_time=True)
     with torch.no_grad():
@@ -709,10 +722,16 @@ def test_gru_bwd_f16x2_scales(gscale, wmax, H):
     r = torch.randn(B, 36, 29, generator=gen) * 3.0
     tf = torch.randn(B, 36, 9, generator=gen)
     gy = torch.randn(B, 29, H, generator=gen) * gscale
-    (ref(r, tf) * gy).sum().backward()
+    grads = {}
+    for dt in (torch.float32, torch.float64):
+        m = _GRUEncoder(H, use_time=True)
+        m.load_state_dict(ref.state_dict())
+        m = m.to(dt)
+        (m(r.to(dt), tf.to(dt)) * gy.to(dt)).sum().backward()
+        grads[dt] = {n: p.grad.detach() for n, p in m.gru.named_parameters()}
     (enc(r.to(DEV), tf.to(DEV)) * gy.to(DEV)).sum().backward()
-    assert_grads_close([(n, p.grad) for n, p in enc.gru.named_parameters()],
-                       {n: p.grad for n, p in ref.gru.named_parameters()}, prefix="GRU grad ")
+    assert_grads_match_truth({n: p.grad for n, p in enc.gru.named_parameters()}, grads[torch.float32],
+                             grads[torch.float64])
 
 
 @pytest.mark.parametrize("K,M,N", [(7424, 64, 64), (1857, 32, 32), (3, 64, 32), (250, 32, 64)])

@@ -97,10 +97,7 @@ def test_layer0_x0_forward_and_backward_equal_dense(state, B, D, extra):
     xf = {0: 0, "x3": nat.LG_F_BF16X3, "bf16": nat.LG_F_BF16 | nat.LG_F_PC}[extra]
     flags = nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT | xf
     st = ops.stream_of(x0)
-    if D == 64:
-        mk = g.x0marks
-    else:  # the marks are graph-level: the same tables at any D
-        mk = g.x0marks
+    mk = m._x0marks(g, slot)  # graph-level: the same tables at any D
     y_d = torch.empty(N, B, D, device=DEV)
     y_x = torch.empty(N, B, D, device=DEV)
     ops.check(lib.lg_gcn_fwd_nm_bits(ops.ptr(g.nodetab), ops.ptr(g.pairs), ops.ptr(x0), ops.ptr(W), ops.ptr(b),
@@ -166,6 +163,36 @@ def test_detector_compressed_x0_equals_dense(train):
         loss.backward()
         res.append((logits.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     from helpers import assert_close
+    assert_close(res[1][0], res[0][0], rtol=1e-5, what="logits")
+    for k in res[0][1]:
+        assert_close(res[1][1][k], res[0][1][k], rtol=1e-5, atol=0.0, what=f"grad {k}")
+
+
+@pytest.mark.parametrize("layers", [1, 3])
+def test_detector_gnn_layers_train_step(layers):
+    """gnn_layers is a public constructor argument (reference detector.py:128,162-164).  At 1
+    layer, layer 0 is also the last: its backward needs the input mask (LG_F_MASK_IN), which
+    only the dense node init provides, so x_0 is not compressed there.  A train-mode step at
+    B = 32 (node-major) must run and equal the dense node init's step at any depth."""
+    from models.detector import LeakDetector
+    from helpers import assert_close
+    sensors, pipes = lta_ids()
+    torch.manual_seed(0)
+    m = LeakDetector(LTA_INP, sensors, pipes, gnn_layers=layers).to(DEV).train()
+    gen = torch.Generator().manual_seed(6)
+    B = 32
+    r = torch.randn(B, 36, 29, generator=gen).to(DEV)
+    tf = torch.randn(B, 36, 9, generator=gen).to(DEV)
+    lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen).to(DEV)
+    res = []
+    for comp in (False, True):
+        m.compress_x0 = comp
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(12)
+        logits = m(r, tf)
+        torch.nn.functional.cross_entropy(logits, lab).backward()
+        assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in m.parameters())
+        res.append((logits.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
     assert_close(res[1][0], res[0][0], rtol=1e-5, what="logits")
     for k in res[0][1]:
         assert_close(res[1][1][k], res[0][1][k], rtol=1e-5, atol=0.0, what=f"grad {k}")

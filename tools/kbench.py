@@ -185,6 +185,52 @@ def pc_stamps_summary(lib, launch, waves_per_wg=12, prod=4):
     return out
 
 
+def pc_probe_summary(lib, launch, waves_per_wg=12, prod=4, reps=5):
+    """Product-speed timeline of k_gcn_fwd_pc (LG_PC_PROBE build: per wave only start, after-W-
+    staging and end clocks plus its tile count, stored once at the wave's end).  The launch is
+    run `reps` times back to back (the last one is read), so it starts the way it does in a
+    step: behind another kernel.  Per role: start / staging-done / end (us from the first wave's
+    start), the tail (last end minus median end), the end by tile count and by XCC."""
+    lib.lg_lab_nm3_stamps_clear.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    torch.cuda.synchronize()
+    for _ in range(reps):
+        launch()
+    torch.cuda.synchronize()
+    check(lib.lg_lab_nm3_stamps_clear(), "stamps clear")
+    torch.cuda.synchronize()
+    launch()
+    torch.cuda.synchronize()
+    n = 8192 * 24
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib.lg_lab_nm3_stamps(buf.ctypes.data, n), "stamps read")
+    st = buf.reshape(8192, 24).astype(np.int64)
+    rows = np.nonzero(st[:, 0] != 0)[0]
+    st = st[rows]
+    role = np.where((rows % waves_per_wg) < prod, "prod", "cons")
+    rt0, rt1, c0, c1, c2 = st[:, 0], st[:, 22], st[:, 1], st[:, 2], st[:, 21]
+    ghz = float(np.median((c2 - c0) / np.maximum(rt1 - rt0, 1))) * 0.1
+    t0 = rt0.min()
+    start = (rt0 - t0) / 100.0
+    end = (rt1 - t0) / 100.0
+    staged = start + (c1 - c0) / (ghz * 1e3)
+    q = lambda a: [round(float(np.percentile(a, p)), 3) for p in (0, 10, 50, 90, 99, 100)] if len(a) else []
+    xcc = (st[:, 23] >> 32) & 0xF
+    out = {"waves": int(len(st)), "clock_GHz": round(ghz, 3), "span_us": round(float(end.max()), 3),
+           "percentiles": [0, 10, 50, 90, 99, 100]}
+    for r in ("prod", "cons"):
+        m = role == r
+        e, tiles = end[m], st[m, 3]
+        out[r] = {"start_us": q(start[m]), "staged_us": q(staged[m]), "end_us": q(e),
+                  "tail_us": round(float(e.max() - np.median(e)), 3),
+                  "tiles_hist": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
+                  "end_by_tiles_p50": {int(k): round(float(np.median(e[tiles == k])), 3) for k in np.unique(tiles)},
+                  "end_by_xcc_max": [round(float(e[xcc[m] == i].max()), 3) if (xcc[m] == i).any() else None
+                                     for i in range(8)]}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="gcn_fwd,gcn_fwd_train,gcn_bwd,gcn_fwd_nm,gcn_fwd_nm_train,gcn_bwd_nm,spmm,"
@@ -203,6 +249,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of a replayed HIP graph")
     ap.add_argument("--stamps", action="store_true", help="per-wave timeline of each --nmlab train launch "
                                                            "(LEAKGNN_LIB=lib/lab_stamps build only)")
+    ap.add_argument("--probe", action="store_true", help="product-speed start/end timeline of each --nmlab train "
+                                                          "launch of k_gcn_fwd_pc (LEAKGNN_LIB=lib/probe build only)")
     args = ap.parse_args()
     global GRAPH
     GRAPH = not args.eager
@@ -266,6 +314,8 @@ def main():
                 nat.LG_F_BIAS | nat.LG_F_RELU | fl | bits, 0.1, 123, 1, cs(), ptr(ymask) if wm else None), "nmlab")
             t = timeit(f, args.iters)
             res[f"gcn_fwd_nm_{lab}_{mode}"] = {"us": t, "GBps": fwd_bytes / t / 1e3}
+            if args.probe and mode == "train" and hasattr(lib, "lg_lab_nm3_stamps"):
+                res[f"probe_{lab}"] = pc_probe_summary(lib, f)
             if args.stamps and mode == "train" and hasattr(lib, "lg_lab_nm3_stamps"):
                 pcs = not (bits & (nat.LG_F_NM3 | nat.LG_F_F32_MFMA)) and not (bits & nat.LG_F_BF16 and not bits & nat.LG_F_PC)
                 res[f"stamps_{lab}"] = pc_stamps_summary(lib, f) if pcs else stamps_summary(lib, f)

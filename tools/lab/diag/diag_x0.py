@@ -34,7 +34,7 @@ for B in (256, 37):
     W = (torch.randn(D, D, generator=gen) / 8).to(DEV)
     b = (torch.randn(D, generator=gen) / 4).to(DEV)
     base = nat.LG_F_BIAS | nat.LG_F_RELU | nat.LG_F_DROPOUT
-    mk = g.x0marks
+    mk = m._x0marks(g, slot)
     outs = {}
     for name, xf in [("dflt", 0), ("x3", nat.LG_F_BF16X3), ("f32", nat.LG_F_F32_MFMA)]:
         for rep in range(2):

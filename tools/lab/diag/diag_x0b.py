@@ -33,7 +33,7 @@ ops.check(lib.lg_node_init_bits_fwd(ops.ptr(slot), ops.ptr(sidx), ops.ptr(h_s), 
 W = torch.eye(D, device=DEV)
 b = torch.zeros(D, device=DEV)
 fl = nat.LG_F_BF16X3 | nat.LG_F_DROPOUT  # layer-0 dropout: the same mask in both; x0's scale needs p
-mk = g.x0marks
+mk = m._x0marks(g, slot)
 yd = torch.full((N, B, D), float("nan"), device=DEV)
 yx = torch.full((N, B, D), float("nan"), device=DEV)
 ops.check(lib.lg_gcn_fwd_nm_bits(ops.ptr(g.nodetab), ops.ptr(g.pairs), ops.ptr(x0), ops.ptr(W), ops.ptr(b),
