@@ -139,9 +139,9 @@ const char* lg_strerror(int code);
 /* Training loss: nn.CrossEntropyLoss() (mean over rows whose target != ignore_index;
  * reference train_detector.py:235, 311) over logits [B][C] (row stride ldx).
  *   fwd: loss (device fp32 scalar), lse [B] (saved for the backward), rowloss [B] scratch;
- *        two launches: the rows, then one wave forms the mean over rows in row order.
- *        counter: kept for ABI stability (must be non-NULL; unused since ABI 19 — the
- *        last-workgroup mean behind it needed a device-scope fence, an L2 writeback on gfx950).
+ *        ONE launch (ABI 23): the rows, and the workgroup that finishes last forms the mean
+ *        over rows in row order.  counter: a device uint32, 0 between launches (the launch
+ *        resets it); one per stream that may run this concurrently.
  *   bwd: dlogits[b][c] = grad_loss[0] / n * (exp(x - lse[b]) - [c == target[b]]), 0 for
  *        ignored rows (row stride ldd).  Three launches for what torch runs as six. */
 int lg_cross_entropy_fwd(const float* logits, const int64_t* target, int64_t B, int64_t C, int64_t ldx,
@@ -152,13 +152,17 @@ int lg_cross_entropy_bwd(const float* logits, const int64_t* target, const float
                          lg_stream_t stream);
 
 /* Training-step tail: torch.nn.utils.clip_grad_norm_(params, max_norm) then
- * torch.optim.AdamW.step() (reference train_detector.py:313-317), two launches.
+ * torch.optim.AdamW.step() (reference train_detector.py:313-317), ONE launch (ABI 23; two
+ * before).
  *   table : int64 [T][4] (HOST array) device addresses of (param, grad, exp_avg, exp_avg_sq), fp32
  *   sizes : int64 [T] (HOST array) element counts, T <= 48 (passed by value to the launches, so
  *           captured launches need no host copy)
- *   step  : device fp32 [2]: step[0] the AdamW step counter (incremented), step[1] scratch
+ *   step  : device fp32 [2]: step[0] the AdamW step counter (incremented); step[1] the launch's
+ *           workgroup ticket counter, read as uint32, which must be 0 between launches (zeros
+ *           at creation; it is reset by the launch itself)
  *   max_norm <= 0: no clipping.  norm_out (device fp32, may be NULL): the pre-clip total norm.
- *   workspace: lg_clip_adamw_workspace_bytes(sizes, T) bytes (per-slice fp64 partial norms).
+ *   workspace: lg_clip_adamw_workspace_bytes(sizes, T) bytes (unused since ABI 23; still checked
+ *           non-NULL).
  * The norm is summed in fp64 in a fixed order (deterministic). */
 int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T);
 int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,

@@ -4,11 +4,17 @@
 // backward); here:
 //   forward : one wave per row: lse = max + log(sum exp(x - max)) (fp32, fixed lane order
 //             then a fixed shuffle tree), row loss = lse - x[target] -> lse[b], rowloss[b];
-//             then one single-wave launch sums the counted rows in row order (deterministic).
-//             (The mean used to be taken by the last workgroup behind a device-scope counter:
-//             on gfx950 that release / acquire is an L2 writeback + invalidate in every
+//             the workgroup that finishes last sums the counted rows in row order
+//             (deterministic), in the same launch.  The hand-off is fence-free
+//             (MI355X_MICROARCH.md, the sc1 hand-off table's first row): the row losses are
+//             stored sc1 (agent-scope relaxed atomic stores, 4 B), every wave waits for its
+//             stores (vmcnt 0), then behind a workgroup barrier one lane adds to the counter
+//             (agent scope); the workgroup whose add returns gridDim - 1 reads the row losses
+//             with sc1 loads and resets the counter.  (Round 3 took the mean behind a release /
+//             acquire fence pair: on gfx950 that is an L2 writeback + invalidate in every
 //             workgroup — buffer_wbl2 / buffer_inv — which, right after the EdgeHead forward's
-//             100 MB of stores, made the launch 12 us for 0.8 MB of logits.)
+//             100 MB of stores, made the launch 12 us for 0.8 MB of logits; round 4 ran the
+//             mean as a second, single-wave launch, ~5 us in the step.)
 //   backward: dx[b][c] = g / n * (exp(x - lse[b]) - [c == target[b]])   (0 for ignored rows)
 #include <algorithm>
 #include "common.h"
@@ -30,9 +36,29 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// the mean over the counted rows, in row order (one wave; sc1 loads: the rows were stored sc1
+// by other workgroups of the same launch)
+__device__ __forceinline__ void ce_mean_wave(float* rowloss, const int64_t* __restrict__ target, int64_t B,
+                                             int64_t ignore, float* __restrict__ loss) {
+    const int lane = threadIdx.x & 63;
+    float acc = 0.f, cnt = 0.f;
+    for (int64_t b0 = 0; b0 < B; b0 += 64) {
+        const int64_t b = b0 + lane;
+        float v = 0.f, c = 0.f;
+        if (b < B) {
+            v = __hip_atomic_load(rowloss + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c = target[b] == ignore ? 0.f : 1.f;
+        }
+        acc += wave_sum(v);
+        cnt += wave_sum(c);
+    }
+    if (lane == 0) loss[0] = acc / cnt;  // NaN when every row is ignored, as torch
+}
+
 __global__ void __launch_bounds__(kCeThreads)
 k_ce_fwd(const float* __restrict__ x, const int64_t* __restrict__ target, int64_t B, int64_t C, int64_t ldx,
-         int64_t ignore, float* __restrict__ lse, float* __restrict__ rowloss) {
+         int64_t ignore, float* __restrict__ lse, float* rowloss, unsigned* counter, float* __restrict__ loss) {
+    __shared__ unsigned is_last;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int64_t b = static_cast<int64_t>(blockIdx.x) * kCeWaves + w; b < B; b += static_cast<int64_t>(gridDim.x) * kCeWaves) {
         const float* row = x + b * ldx;
@@ -60,28 +86,20 @@ k_ce_fwd(const float* __restrict__ x, const int64_t* __restrict__ target, int64_
             const int64_t t = target[b];
             lse[b] = l;
             // a target outside [0, C) (torch raises) poisons the loss with NaN, never reads out of bounds
-            rowloss[b] = t == ignore ? 0.f : (t >= 0 && t < C ? l - row[t] : __builtin_nanf(""));
+            const float rl = t == ignore ? 0.f : (t >= 0 && t < C ? l - row[t] : __builtin_nanf(""));
+            __hip_atomic_store(rowloss + b, rl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-}
-
-// the mean over the counted rows, in row order (one wave)
-__global__ void __launch_bounds__(64)
-k_ce_mean(const float* __restrict__ rowloss, const int64_t* __restrict__ target, int64_t B, int64_t ignore,
-          float* __restrict__ loss) {
-    const int lane = threadIdx.x & 63;
-    float acc = 0.f, cnt = 0.f;
-    for (int64_t b0 = 0; b0 < B; b0 += 64) {
-        const int64_t b = b0 + lane;
-        float v = 0.f, c = 0.f;
-        if (b < B) {
-            v = rowloss[b];
-            c = target[b] == ignore ? 0.f : 1.f;
-        }
-        acc += wave_sum(v);
-        cnt += wave_sum(c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row losses have left
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = old + 1 == gridDim.x ? 1u : 0u;
     }
-    if (lane == 0) loss[0] = acc / cnt;  // NaN when every row is ignored, as torch
+    __syncthreads();
+    if (!is_last) return;
+    if (w == 0) ce_mean_wave(rowloss, target, B, ignore, loss);
+    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(kCeThreads)
@@ -132,9 +150,9 @@ extern "C" int lg_cross_entropy_fwd(const float* logits, const int64_t* target, 
                                                                                                           : LG_EHIP;
     }
     if (!logits || !target || !lse || !rowloss) return LG_EINVAL;
-    const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, 4 * lg_num_cus()));
-    lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss);
-    lg_launch(k_ce_mean, 1, 64, 0, s, rowloss, target, B, ignore_index, loss);
+    // at most one workgroup per CU: the sc1 hand-off above was measured in that configuration
+    const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, lg_num_cus()));
+    lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss, counter, loss);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }

@@ -1,24 +1,30 @@
 // The training step's tail (reference train_detector.py:313-317): clip_grad_norm_(max_norm)
-// then AdamW.step(), as TWO launches.  The detector has ~60k parameters in ~20 tensors; torch
+// then AdamW.step(), as ONE launch.  The detector has ~60k parameters in ~20 tensors; torch
 // runs the pair as ~11 launches (foreach norms, norm of norms, clamp, foreach mul, the fused
 // AdamW), each a few microseconds of dispatch for almost no work.  Here the parameters are
-// one flattened index space cut into kOptChunk-element slices, one workgroup each:
-//   launch 1: per-slice sums of squared gradients (fp64, fixed order) -> partial[G]
-//   launch 2: every workgroup sums partial[0..G) in the same fixed order, forms
+// one flattened index space cut into kOptChunk-element slices, one 1024-thread workgroup each.
+// Every workgroup first forms the WHOLE norm itself (thread i sums the squares of elements
+// i, i + 1024, ... in fp64, then a fixed LDS tree: the same order in every workgroup, so
+// every workgroup clips with the same bits; 242 KB of L2-resident gradients per workgroup),
+// then updates its slice:
 //     g     = grad * min(1, max_norm / (||grad||_2 + 1e-6))     (written back, as torch does)
 //     p    *= 1 - lr * weight_decay                              (decoupled decay)
 //     m     = beta1 m + (1 - beta1) g,   v = beta2 v + (1 - beta2) g^2
 //     p    -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps)
-//   for its slice.  t lives on the device (step[0]; launch 1 stages t + 1 in step[1], launch 2
-//   reads it and commits it), so the step can live in a captured HIP graph.
+// The step counter t lives on the device (step[0]), so the step can live in a captured HIP
+// graph.  Every workgroup reads step[0] BEFORE it takes a ticket (an agent-scope atomic on
+// step[1], used as a uint32 counter); the workgroup that draws the launch's last ticket has
+// therefore seen every other workgroup's read done, commits step[0] = t and resets the
+// counter.  (Round 4 ran the norm as its own launch of per-slice partials: 6.7 + 9.8 us in the
+// step for the pair.)
 #include <algorithm>
 #include "common.h"
 
 namespace {
 
-constexpr int kOptThreads = 256;
-constexpr int kOptChunk = 512;       // elements per workgroup (two per thread: one round trip)
-constexpr int kOptMaxTensors = 48;   // by-value kernel argument: a captured launch needs no host copy
+constexpr int kOptThreads = 1024;
+constexpr int kOptChunk = kOptThreads;  // elements per workgroup (one per thread)
+constexpr int kOptMaxTensors = 48;      // by-value kernel argument: a captured launch needs no host copy
 
 struct AdamTensors {
     int64_t ptr[kOptMaxTensors][4];  // param, grad, exp_avg, exp_avg_sq
@@ -26,76 +32,70 @@ struct AdamTensors {
     int T;
 };
 
-// visit f(tensor, index) for the flattened indices [lo, hi) of this workgroup, thread-strided
-template <typename F>
-__device__ __forceinline__ void for_slice(const AdamTensors& a, int64_t lo, int64_t hi, F&& f) {
-    for (int t = 0; t < a.T; ++t) {
-        const int64_t b0 = max(lo, a.off[t]), b1 = min(hi, a.off[t + 1]);
-        for (int64_t i = b0 + threadIdx.x; i < b1; i += kOptThreads) f(t, i - a.off[t]);
-    }
-}
-
-__device__ __forceinline__ double block_sum(double x) {
+__global__ void __launch_bounds__(kOptThreads)
+k_adam(AdamTensors a, float* __restrict__ step, float lr, float beta1, float beta2, float eps, float wd,
+       float max_norm, float* __restrict__ norm_out) {
     __shared__ double red[kOptThreads];
-    red[threadIdx.x] = x;
+    __shared__ float tsh;
+    const int tid = threadIdx.x;
+    // the committed step count, read before this workgroup's ticket (below)
+    if (tid == 0) tsh = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1.0f;
+    // the whole norm: element i of the flattened space by thread i % kOptThreads, fixed order
+    double ss = 0.0;
+    if (max_norm > 0.f || norm_out) {
+        for (int t = 0; t < a.T; ++t) {
+            const float* g = reinterpret_cast<const float*>(a.ptr[t][1]);
+            const int64_t o = a.off[t], n = a.off[t + 1] - o;
+            // first element of tensor t owned by this thread: (o + j) % kOptThreads == tid
+            for (int64_t j = (tid - o % kOptThreads + kOptThreads) % kOptThreads; j < n; j += kOptThreads) {
+                const double x = g[j];
+                ss += x * x;
+            }
+        }
+    }
+    red[tid] = ss;
     __syncthreads();
     for (int h = kOptThreads / 2; h > 0; h >>= 1) {
-        if (static_cast<int>(threadIdx.x) < h) red[threadIdx.x] += red[threadIdx.x + h];
+        if (tid < h) red[tid] += red[tid + h];
         __syncthreads();
     }
-    const double r = red[0];
-    __syncthreads();
-    return r;
-}
-
-__global__ void __launch_bounds__(kOptThreads) k_adam_norm(AdamTensors a, double* __restrict__ partial,
-                                                           float* __restrict__ step) {
-    const int64_t lo = static_cast<int64_t>(blockIdx.x) * kOptChunk, hi = lo + kOptChunk;
-    double ss = 0.0;
-    for_slice(a, lo, hi, [&](int t, int64_t i) {
-        const double x = reinterpret_cast<const float*>(a.ptr[t][1])[i];
-        ss += x * x;
-    });
-    ss = block_sum(ss);
-    if (threadIdx.x == 0) {
-        partial[blockIdx.x] = ss;
-        if (blockIdx.x == 0) step[1] = step[0] + 1.0f;
+    const double norm = sqrt(red[0]);
+    const float t1 = tsh;
+    if (tid == 0) {
+        // tsh was read above; the ticket is taken only after that read has returned
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(step + 1);
+        const uint32_t tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tk + 1 == gridDim.x) {  // every other workgroup has read step[0]: commit t
+            __hip_atomic_store(step, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (blockIdx.x == 0 && norm_out) norm_out[0] = static_cast<float>(norm);
     }
-}
-
-__global__ void __launch_bounds__(kOptThreads)
-k_adam_update(AdamTensors a, const double* __restrict__ partial, int G, float* __restrict__ step, float lr,
-              float beta1, float beta2, float eps, float wd, float max_norm, float* __restrict__ norm_out) {
-    double ss = 0.0;
-    for (int g = threadIdx.x; g < G; g += kOptThreads) ss += partial[g];
-    const double norm = sqrt(block_sum(ss));
     const float coef = max_norm > 0.f ? static_cast<float>(fmin(1.0, static_cast<double>(max_norm) / (norm + 1e-6)))
                                       : 1.0f;
-    const float t1 = step[1];
     const float bc1 = 1.0f - powf(beta1, t1), bc2 = 1.0f - powf(beta2, t1);
     const float step_size = lr / bc1, bc2s = sqrtf(bc2), decay = 1.0f - lr * wd;
-    const int64_t lo = static_cast<int64_t>(blockIdx.x) * kOptChunk, hi = lo + kOptChunk;
-    for_slice(a, lo, hi, [&](int t, int64_t i) {
-        float* p = reinterpret_cast<float*>(a.ptr[t][0]);
-        float* g = reinterpret_cast<float*>(a.ptr[t][1]);
-        float* m = reinterpret_cast<float*>(a.ptr[t][2]);
-        float* v = reinterpret_cast<float*>(a.ptr[t][3]);
-        float gi = g[i];
-        if (max_norm > 0.f) {
-            gi *= coef;
-            g[i] = gi;
-        }
-        const float pi = p[i] * decay;
-        const float mi = beta1 * m[i] + (1.0f - beta1) * gi;
-        const float vi = beta2 * v[i] + (1.0f - beta2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
-        p[i] = pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
-    });
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        step[0] = t1;  // step[1] stays t1: no workgroup of this launch writes what another reads
-        if (norm_out) norm_out[0] = static_cast<float>(norm);
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * kOptChunk + tid;
+    int t = 0;
+    while (t < a.T && a.off[t + 1] <= e) ++t;
+    if (t >= a.T) return;
+    const int64_t i = e - a.off[t];
+    float* p = reinterpret_cast<float*>(a.ptr[t][0]);
+    float* g = reinterpret_cast<float*>(a.ptr[t][1]);
+    float* m = reinterpret_cast<float*>(a.ptr[t][2]);
+    float* v = reinterpret_cast<float*>(a.ptr[t][3]);
+    float gi = g[i];
+    if (max_norm > 0.f) {
+        gi *= coef;
+        g[i] = gi;
     }
+    const float pi = p[i] * decay;
+    const float mi = beta1 * m[i] + (1.0f - beta1) * gi;
+    const float vi = beta2 * v[i] + (1.0f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi - step_size * mi / (sqrtf(vi) / bc2s + eps);
 }
 
 }  // namespace
@@ -104,7 +104,8 @@ extern "C" int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T) {
     if (T < 0 || T > kOptMaxTensors || (T > 0 && !sizes)) return LG_EUNSUPPORTED;
     int64_t n = 0;
     for (int t = 0; t < T; ++t) n += std::max<int64_t>(sizes[t], 0);
-    return std::max<int64_t>(1, (n + kOptChunk - 1) / kOptChunk) * static_cast<int64_t>(sizeof(double));
+    (void)n;
+    return 8;  // unused since the single-launch form (kept: callers size and pass it)
 }
 
 extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
@@ -125,12 +126,9 @@ extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, 
     }
     a.T = T;
     const int G = static_cast<int>(std::max<int64_t>(1, (a.off[T] + kOptChunk - 1) / kOptChunk));
-    if (ws_bytes < G * static_cast<int64_t>(sizeof(double))) return LG_EINVAL;  // one fp64 partial per slice
-    double* partial = static_cast<double*>(workspace);
-    hipStream_t s = lg_stream(stream);
-    lg_launch(k_adam_norm, G, kOptThreads, 0, s, a, partial, step);
-    LG_RET_IF_LAUNCH_FAILED();
-    lg_launch(k_adam_update, G, kOptThreads, 0, s, a, partial, G, step, lr, beta1, beta2, eps, weight_decay, max_norm,
+    (void)workspace;
+    (void)ws_bytes;
+    lg_launch(k_adam, G, kOptThreads, 0, lg_stream(stream), a, step, lr, beta1, beta2, eps, weight_decay, max_norm,
               norm_out);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;

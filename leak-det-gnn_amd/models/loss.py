@@ -1,5 +1,5 @@
 """The training loss, nn.CrossEntropyLoss() (reference train_detector.py:235, 311), as a
-registered op on two HIP launches (csrc/loss.hip: lg_cross_entropy_fwd / _bwd).
+registered op on one HIP launch each way (csrc/loss.hip: lg_cross_entropy_fwd / _bwd).
 
 torch's cross_entropy is six launches per step here (log_softmax, nll forward, two fills,
 nll backward, log_softmax backward).  `CrossEntropyLoss` is a drop-in for the reference's

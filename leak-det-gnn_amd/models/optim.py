@@ -6,8 +6,9 @@ The reference ends every step with
     opt.step()                      # torch.optim.AdamW(lr, weight_decay)
 
 which torch runs as ~11 launches for the detector's ~60k parameters (foreach norms, the
-norm of norms, clamp, foreach mul, the fused AdamW).  ClipAdamW does both in TWO HIP
-launches (lg_clip_adamw, csrc/optim.hip: per-slice fp64 norm partials, then the update): the same AdamW arithmetic (decoupled weight
+norm of norms, clamp, foreach mul, the fused AdamW).  ClipAdamW does both in ONE HIP
+launch (lg_clip_adamw, csrc/optim.hip: every workgroup forms the whole fp64 norm in a fixed
+order, then updates its slice): the same AdamW arithmetic (decoupled weight
 decay, bias corrections, amsgrad=False) on gradients scaled by
 min(1, max_norm / (||g||_2 + 1e-6)), written back to .grad as clip_grad_norm_ does.  The
 step counter is device-resident, so the step can be captured in a HIP graph
@@ -40,6 +41,12 @@ class ClipAdamW(torch.optim.Optimizer):
         self.last_grad_norm: Optional[torch.Tensor] = None
         self._ws: dict = {}  # group index -> per-slice partial-norm workspace
 
+    def load_state_dict(self, state_dict) -> None:
+        super().load_state_dict(state_dict)
+        for group in self.param_groups:  # word 1 is the launch's ticket counter: 0 between launches
+            if torch.is_tensor(group.get("step_t")):
+                group["step_t"][1:].zero_()
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -65,7 +72,7 @@ class ClipAdamW(torch.optim.Optimizer):
                 if not st:
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
-            if "step_t" not in group:  # [step, scratch]
+            if "step_t" not in group:  # [step, the launch's workgroup ticket counter (uint32 bits, 0 between launches)]
                 group["step_t"] = torch.zeros(2, dtype=torch.float32, device=params[0].device)
             if self.last_grad_norm is None:
                 self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=params[0].device)

@@ -216,10 +216,14 @@ def test_clip_adamw_matches_torch():
         for (n, pa), pb in zip(ma.named_parameters(), mb.parameters()):
             assert_close(pb.grad, pa.grad, rtol=1e-6, what=f"clipped grad {n}")
             assert_close(pb, pa, rtol=1e-6, what=f"param {n} after step {it}")
+        # the device step counter is committed by the launch's last workgroup, whose ticket
+        # counter (word 1, uint32) is back at 0 between launches
+        st = ob.param_groups[0]["step_t"]
+        assert st[0].item() == it + 1 and st[1:].view(torch.int32).item() == 0
 
 
 def test_cross_entropy_matches_torch():
-    """models/loss.py CrossEntropyLoss (two HIP launches) == torch's nn.CrossEntropyLoss:
+    """models/loss.py CrossEntropyLoss (one HIP launch each way) == torch's nn.CrossEntropyLoss:
     loss and dlogits at the detector's shape, with ignored rows, and the all-ignored NaN;
     a non-default configuration falls through to torch."""
     from models.loss import CrossEntropyLoss
