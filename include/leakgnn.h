@@ -595,6 +595,33 @@ int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, con
                int64_t B, int64_t L, int64_t S, int64_t I, int64_t H,
                void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
+/* The GRU encoder and the node init in one launch each way (ABI 23; the node-major trunk's
+ * compressed node init, lg_node_init_bits_fwd, with the sensor projection's backward,
+ * lg_sensor_proj_bwd).  Replaces detector.py:60-73 (the shared GRU) followed by :179-190 (h0,
+ * the mask column, sensor_to_node, ReLU, dropout) when node_hidden == sensor_hidden == H.
+ *   fwd: lg_gru_fwd's outputs, plus xs0 [S][B][H] and x0bits exactly as lg_node_init_bits_fwd
+ *        writes them from h_last (W = proj_w [H][H + 1], bias = node_bias, dropout stream =
+ *        (seed, salt)), except that the sensor nodes' words of x0bits are left unwritten (no
+ *        reader: lg_gcn_fwd_nm_x0 / lg_gcn_bwd_nm_x0 take those rows from xs0).  One launch.
+ *   bwd: lg_gru_bwd without dx, its dh_last formed in the launch from the node init's
+ *        pre-activation gradient, as lg_sensor_proj_bwd does: dx0 is node-major [N][B][H] (the
+ *        sensor nodes' rows: lg_gcn_bwd_nm_x0 with LG_F_DX_SENSOR_ROWS), live [S] (may be NULL);
+ *        also dproj_w [H][H + 1] and dproj_b [H] (+ dbias_in, the non-sensor rows' sum, which
+ *        may be a pending output of an open reduce batch).  One launch + one slab reduction of
+ *        all six gradients.  Workspace: lg_gru_node_init_bwd_workspace_bytes. */
+int lg_gru_node_init_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+                         const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last,
+                         const int32_t* sensor_slot, const int64_t* sensor_idx, const float* proj_w,
+                         const float* node_bias, float* xs0, uint16_t* x0bits, int64_t B, int64_t L, int64_t S,
+                         int64_t I, int64_t H, int64_t N, int flags, float dropout_p, uint64_t seed, uint32_t salt,
+                         lg_stream_t stream);
+int64_t lg_gru_node_init_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H);
+int lg_gru_node_init_bwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+                         const float* h_seq, const float* gates, const float* dx0, const int64_t* sensor_idx,
+                         const float* live, const float* proj_w, const float* dbias_in, float* dw_ih, float* dw_hh,
+                         float* db_ih, float* db_hh, float* dproj_w, float* dproj_b, int64_t B, int64_t L, int64_t S,
+                         int64_t I, int64_t H, int64_t N, void* workspace, int64_t ws_bytes, lg_stream_t stream);
+
 /* ---- Frozen-predictor residual builder (SURVEY 8 f rank 1) ----------------------
  * Replaces the per-window NormalPredictorTCN passes of
  * build_residual_sequence_from_segment (reference models/utils.py:169-216, TCN

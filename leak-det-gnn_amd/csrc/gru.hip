@@ -125,13 +125,37 @@ __device__ __forceinline__ void split2_pair_mix(float a, float b, uint32_t& p0, 
 // Measured and dropped (MI355X, B = 256): one wave per unit group owning all three gates
 // (one barrier per step, no sigma exchange) — 114 vs 116 us with fp32 MFMA; PMC
 // (profiles/pmc/r02m_pmc_summary.txt): 51% of its wave time in dependency stalls.
+// The node init fused into the training forward's epilogue (lg_gru_node_init_fwd, NI): the
+// GRU's h_L of the block's 16 sequences (window b, sensor slot s) are the sensor rows of the
+// node init (detector.py:181-190), so the block forms them right there:
+//   xs0[s][b] = dropout(relu([h_L, 1] W^T + b))     for the slot's node if s is its live slot
+// with the arithmetic of k_node_init_bits (heads.hip: W^T staged in LDS, the ascending-k fmaf
+// chain, the same row-stream dropout), so xs0 is bit-identical to lg_node_init_bits_fwd's; and
+// every block writes a grid-strided share of the NON-sensor tiles' [x0 > 0] words (the bias
+// sign and the dropout stream alone; the sensor tiles' words are never read: layer 0 takes
+// those nodes' rows from xs0).  Node init and its launch leave the step.
+struct GruNi {
+    const int32_t* slot;  // [N] node -> its live sensor slot, or -1
+    const int64_t* sidx;  // [S] slot -> node
+    const float* W;       // [D][H + 1] sensor_to_node.weight (D = H)
+    const float* bias;    // [D]
+    float* xs0;           // [S][B][D]
+    uint16_t* bits;       // [N][ngroups][64]
+    uint32_t B, N, ngroups;
+    lg_fastdiv fdG;       // division by ngroups
+    int dropout;
+    float p, scale;
+    uint64_t seed;
+    uint32_t salt;
+};
+
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
-template <int H, bool UT, bool SAVE>
+template <int H, bool UT, bool SAVE, bool NI = false>
 __global__ void __launch_bounds__(12 * H) __attribute__((amdgpu_waves_per_eu(6, 8)))  // 2 workgroups / CU
 k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Wih,
           const float* __restrict__ Whh, const float* __restrict__ bih, const float* __restrict__ bhh,
           float* __restrict__ hs, float* __restrict__ gates, float* __restrict__ hout, uint32_t Nseq, int L, int S,
-          lg_fastdiv fdS) {
+          lg_fastdiv fdS, GruNi ni) {
     constexpr int NU = H / 16, NC = H / 32, I = UT ? 10 : 1;
     constexpr int LC = H == 64 ? kLC : 30;  // H = 32: four workgroups per CU fit in LDS
     __shared__ __attribute__((aligned(16))) float xs[LC * TS * XR];
@@ -241,6 +265,72 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
         }
     }
     if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hcur);
+    if constexpr (NI) {
+        constexpr int D = H, LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI, HS = H + 4;
+        static_assert(TS * HS + H * D + D <= LC * TS * XR, "node-init staging fits the x buffer");
+        float* hl = xs;             // [TS][HS] h_L of the block's sequences (fp32)
+        float* wt = xs + TS * HS;   // W^T [H][D]
+        float* bfv = wt + H * D;    // [D] W[o][H] + bias[o]
+        __syncthreads();            // the last step's reads of xs are done
+        for (int i = threadIdx.x; i < D * (H + 1); i += blockDim.x) {
+            const int o = i / (H + 1), k = i - o * (H + 1);
+            const float v = ni.W[i];
+            if (k < H) wt[k * D + o] = v;
+            else bfv[o] = v + ni.bias[o];  // the constant-1 column's weight + the bias
+        }
+        if (g == 2) st4(hl + j * HS + 16 * u + 4 * q, hcur);
+        __syncthreads();
+        const uint32_t key = ni.dropout ? lg_dropout_key_dev(ni.seed, ni.salt) : 0u;
+        const uint32_t thr = lg_keep_threshold16(ni.p);
+        const float vs = ni.dropout ? ni.scale : 1.0f;
+        if (static_cast<int>(threadIdx.x) < TS * LPR) {
+            const int r = threadIdx.x / LPR, fg = threadIdx.x % LPR;
+            const uint32_t sq = seq0 + r;
+            if (sq < Nseq) {
+                const uint32_t b = lg_div(sq, fdS), sl = sq - b * fdS.d;
+                const uint32_t n = static_cast<uint32_t>(ni.sidx[sl]);
+                if (ni.slot[n] == static_cast<int32_t>(sl)) {
+                    f32x4 acc = zero4();
+#pragma unroll 8
+                    for (int k = 0; k < H; ++k) {
+                        const float hk = hl[r * HS + k];
+                        const f32x4 w = ld4(wt + k * D + 4 * fg);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[i] = fmaf(hk, w[i], acc[i]);
+                    }
+                    f32x4 v = acc + ld4(bfv + 4 * fg);
+                    const uint32_t kb =
+                        ni.dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * ni.N + n, 4 * fg, thr) : 0xFu;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[i] = ((kb >> i) & 1u) ? fmaxf(v[i], 0.f) * vs : 0.0f;
+                    st4(ni.xs0 + (static_cast<size_t>(sl) * ni.B + b) * D + 4 * fg, v);
+                }
+            }
+        }
+        // the non-sensor tiles' [x0 > 0] words, one lane word per thread (blockDim.x is a multiple
+        // of 64, so a thread keeps its lane and its four channels over the stride)
+        const uint32_t l = threadIdx.x & 63, rl = l / LPR, fg = l % LPR;
+        const f32x4 bv = ld4(ni.bias + 4 * fg);
+        uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * vs > 0.f) << i;
+        const uint32_t words = ni.N * ni.ngroups * 64u, stride = gridDim.x * blockDim.x;
+        for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
+            const uint32_t t = e >> 6, n = lg_div(t, ni.fdG), gg = t - n * ni.ngroups;
+            if (ni.slot[n] >= 0) continue;  // a sensor node's tile: never read
+            uint32_t wd = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t b = 16 * gg + RPI * k + rl;
+                if (b < ni.B) {
+                    const uint32_t kb =
+                        ni.dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * ni.N + n, 4 * fg, thr) : 0xFu;
+                    wd |= (kb & pos) << (4 * k);
+                }
+            }
+            ni.bits[e] = static_cast<uint16_t>(wd);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ backward
@@ -548,11 +638,28 @@ __device__ uint64_t g_gru_stamps[256 * 8 * kGruStamps];
     } while (0)
 #endif
 
-template <int H, bool UT, bool F16, bool DEFER>
+// The sensor projection's backward fused into the training backward (lg_gru_node_init_bwd, NI;
+// the arithmetic of k_sensor_proj_bwd, heads.hip, with the same 32-row groups, so every value
+// is bit-identical to lg_sensor_proj_bwd's):
+//   prologue: dh_L of the lane's sequence (window b, slot s) = dproj W[:, :H], dproj = the
+//             layer-0 backward's dx at node sidx[s], row b (already masked by the node init's
+//             ReLU / dropout), times live[s]; W staged in the dG image before its first use;
+//   epilogue: the workgroup's slab row of dW (D x (H + 1): [h_L, 1] columns) and db, after the
+//             GRU's own slab row.
+struct GruNiB {
+    const float* dx0;     // node-major [N][B][D] (the sensor nodes' rows)
+    const int64_t* sidx;  // [S] slot -> node
+    const float* live;    // [S] 1 / 0, or null (every slot live)
+    const float* W;       // [D][H + 1]
+    const float* dbias_in;  // [D] added to db by workgroup 0 (the non-sensor rows' sum), or null
+    uint32_t B;
+};
+
+template <int H, bool UT, bool F16, bool DEFER, bool NI = false>
 __global__ void __launch_bounds__(GB2<H>::NTH)
 k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, const float* __restrict__ Whh,
            const float* __restrict__ hs, const float* __restrict__ gates, const float* __restrict__ dhL,
-           float* __restrict__ slab, uint32_t Nseq, int L, int S, lg_fastdiv fdS) {
+           float* __restrict__ slab, uint32_t Nseq, int L, int S, lg_fastdiv fdS, GruNiB ni) {
     using G = GB2<H>;
     using AF = std::conditional_t<F16, lg_f16x8, lg_bf16x8>;
     constexpr int NP = F16 ? 2 : 3;  // split parts
@@ -712,7 +819,45 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         if (j == 0) lds_max_u32(&wnm[3], xm);
     }
 
-    f32x4 dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + u0) : zero4();
+    f32x4 dh = zero4();
+    if constexpr (NI) {
+        // W[:, :H] as [D][H] and the block's 32 dproj rows (times live) in the dG image, which is
+        // unused until step L-1; every load of both in flight at once (coalesced)
+        constexpr int D = H, DP = D + 4;
+        float* wl = reinterpret_cast<float*>(&dgs[0][0][0][0]);
+        float* dpl = wl + D * H;  // [TS2][DP]
+        static_assert(sizeof(dgs) >= sizeof(float) * (D * H + TS2 * DP), "staging fits the dG image");
+        for (int i = threadIdx.x; i < D * H; i += G::NTH) {
+            const int o = i / H, k = i - o * H;
+            wl[i] = ni.W[o * (H + 1) + k];
+        }
+        for (int i = threadIdx.x; i < TS2 * (D / 4); i += G::NTH) {
+            const int rr = i / (D / 4), c4 = 4 * (i % (D / 4));
+            const uint32_t sq = seq0 + rr;
+            f32x4 v = zero4();
+            if (sq < Nseq) {
+                const uint32_t b = lg_div(sq, fdS), sl2 = sq - b * fdS.d;
+                v = ld4(ni.dx0 + (static_cast<int64_t>(ni.sidx[sl2]) * ni.B + b) * D + c4);
+                if (ni.live) v = v * ni.live[sl2];
+            }
+            st4(dpl + rr * DP + c4, v);
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int o4 = 0; o4 < D / 4; ++o4) {
+            const f32x4 gz = ld4(dpl + sl * DP + 4 * o4);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const f32x4 wv = ld4(wl + (4 * o4 + jj) * H + u0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dh[i] = fmaf(gz[jj], wv[i], dh[i]);
+            }
+        }
+        if (!valid) dh = zero4();
+        __syncthreads();  // the staging area is the dG image of step L-1
+    } else {
+        dh = valid ? ld4(dhL + static_cast<int64_t>(seq) * H + u0) : zero4();
+    }
     f32x4 dwh[3][G::NTS], dwx[2], dbhn = zero4();
 #pragma unroll
     for (int gi = 0; gi < 3; ++gi)
@@ -956,6 +1101,54 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
     if (sh == 1 && j == 0) st4(&dbh[u0], dbhn);
     __syncthreads();
     if (sh == 0 && j == 0) st4(obhh + 2 * H + u0, dbhn + ld4(&dbh[u0]));
+    if constexpr (NI) {
+        // the projection's slab row: dW[o][k] = sum over the block's 32 rows of dproj[o] [h_L, 1][k]
+        // (rows in order, one fmaf chain per output), db[o] = the same sum of dproj[o]
+        constexpr int D = H, DP = D + 4, HP = H + 4;
+        float* dpl = reinterpret_cast<float*>(&dgs[0][0][0][0]);  // [TS2][DP] dproj rows
+        float* hx = dpl + TS2 * DP;                               // [TS2][HP] [h_L, 1]
+        static_assert(sizeof(dgs) >= sizeof(float) * TS2 * (DP + HP), "projection staging fits the dG image");
+        // (every read of the images ended before the db_hh barrier above)
+        for (int i = threadIdx.x; i < TS2 * (D / 4); i += G::NTH) {
+            const int rr = i / (D / 4), c4 = 4 * (i % (D / 4));
+            const uint32_t sq = seq0 + rr;
+            f32x4 v = zero4(), hv = zero4();
+            if (sq < Nseq) {
+                const uint32_t b = lg_div(sq, fdS), sl2 = sq - b * fdS.d;
+                v = ld4(ni.dx0 + (static_cast<int64_t>(ni.sidx[sl2]) * ni.B + b) * D + c4);
+                if (ni.live) v = v * ni.live[sl2];
+                hv = ld4(hs + (static_cast<int64_t>(L - 1) * Nseq + sq) * H + c4);
+            }
+            st4(dpl + rr * DP + c4, v);
+            st4(hx + rr * HP + c4, hv);
+            if (c4 == 0) hx[rr * HP + H] = 1.f;
+        }
+        __syncthreads();
+        float* outp = out + SLAB;  // [D][H + 1] dW, then [D] db
+        constexpr int KQ = G::NTH / D, KW = H / KQ;
+        static_assert(KW % 4 == 0, "float4 columns");
+        const int o = threadIdx.x / KQ, kb = (threadIdx.x % KQ) * KW;
+        float acc[KW];
+#pragma unroll
+        for (int jj = 0; jj < KW; ++jj) acc[jj] = 0.f;
+        float a1 = 0.f;
+        for (int rr = 0; rr < TS2; ++rr) {
+            const float gz = dpl[rr * DP + o];
+#pragma unroll
+            for (int jj = 0; jj < KW; jj += 4) {
+                const f32x4 hv = ld4(hx + rr * HP + kb + jj);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[jj + i] = fmaf(gz, hv[i], acc[jj + i]);
+            }
+            a1 += gz;
+        }
+#pragma unroll
+        for (int jj = 0; jj < KW; ++jj) outp[o * (H + 1) + kb + jj] = acc[jj];
+        if (kb == 0) {
+            outp[o * (H + 1) + H] = a1;
+            outp[D * (H + 1) + o] = a1 + ((blockIdx.x == 0 && ni.dbias_in) ? ni.dbias_in[o] : 0.f);
+        }
+    }
 }
 
 inline int64_t nblocks_seq(int64_t nseq) { return (nseq + TS - 1) / TS; }
@@ -970,7 +1163,7 @@ int launch_fwd(bool ut, bool save, const float* residual, const float* tfeat, co
     const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
 #define LG_GRU_FWD(UT, SV)                                                                                        \
     lg_launch(k_gru_fwd<H, UT, SV>, grid, 12 * H, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, h_last, \
-              Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+              Nseq, static_cast<int>(L), static_cast<int>(S), fdS, GruNi{})
     if (ut) {
         if (save) LG_GRU_FWD(true, true); else LG_GRU_FWD(true, false);
     } else {
@@ -993,7 +1186,7 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
                                                  Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
 #define LG_GRU_BWD2(UT, F, DF)                                                                                   \
     lg_launch(k_gru_bwd2<H, UT, F, DF>, static_cast<unsigned>(nblocks_seq2(B * S)), GB2<H>::NTH, 0, s, residual,    \
-              tfeat, w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS)
+              tfeat, w_hh, h_seq, gates, dh_last, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS, GruNiB{})
 #ifdef LG_KERNEL_LAB
     // lab A/B: LG_LAB_GRU_BF16X3 the 3-way bf16 split, LG_LAB_GRU_NODEFER each step's dW after its dh
     if (!need_dx && (getenv("LG_LAB_GRU_BF16X3") || getenv("LG_LAB_GRU_NODEFER"))) {
@@ -1090,4 +1283,96 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
     const LgSlabSeg segs[4] = {{0, nWhh, dw_hh}, {nWhh, nWih, dw_ih}, {nWhh + nWih, G3, db_ih},
                                {nWhh + nWih + G3, G3, db_hh}};
     return lg_launch_slab_reduce_multi(slab, nb, len, segs, 4, nullptr, nullptr, s);
+}
+
+// ------------------------------------------------------------------ GRU + node init, fused
+extern "C" int lg_gru_node_init_fwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+                                    const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last,
+                                    const int32_t* sensor_slot, const int64_t* sensor_idx, const float* proj_w,
+                                    const float* node_bias, float* xs0, uint16_t* x0bits, int64_t B, int64_t L,
+                                    int64_t S, int64_t I, int64_t H, int64_t N, int flags, float dropout_p,
+                                    uint64_t seed, uint32_t salt, lg_stream_t stream) {
+    if (!dims_ok(B, L, S) || N <= 0 || N >= (int64_t{1} << 24)) return LG_EINVAL;
+    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
+    if (!sensor_slot || !sensor_idx || !proj_w || !node_bias || !xs0 || !x0bits) return LG_EINVAL;
+    if (gates && !h_seq) return LG_EINVAL;
+    const bool drop = (flags & LG_F_DROPOUT) != 0;
+    if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
+    if (B == 0) return LG_OK;
+    const int64_t ngroups = (B + 15) / 16;
+    if (N * ngroups * 64 >= (int64_t{1} << 32) || B * N >= kLgMaxRows) return LG_EUNSUPPORTED;
+    hipStream_t s = lg_stream(stream);
+    const uint32_t Nseq = static_cast<uint32_t>(B * S);
+    const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
+    const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
+    const GruNi ni{sensor_slot, sensor_idx, proj_w, node_bias, xs0, x0bits, static_cast<uint32_t>(B),
+                   static_cast<uint32_t>(N), static_cast<uint32_t>(ngroups),
+                   lg_make_fastdiv(static_cast<uint32_t>(ngroups)), drop ? 1 : 0, dropout_p,
+                   drop ? 1.0f / (1.0f - dropout_p) : 1.0f, seed, salt};
+#define LG_GRU_NI(HH, UT, SV)                                                                                     \
+    lg_launch(k_gru_fwd<HH, UT, SV, true>, grid, 12 * HH, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, \
+              h_last, Nseq, static_cast<int>(L), static_cast<int>(S), fdS, ni)
+    const bool ut = I == 10, save = gates != nullptr;
+    if (H == 64) {
+        if (ut) { if (save) LG_GRU_NI(64, true, true); else LG_GRU_NI(64, true, false); }
+        else { if (save) LG_GRU_NI(64, false, true); else LG_GRU_NI(64, false, false); }
+    } else {
+        if (ut) { if (save) LG_GRU_NI(32, true, true); else LG_GRU_NI(32, true, false); }
+        else { if (save) LG_GRU_NI(32, false, true); else LG_GRU_NI(32, false, false); }
+    }
+#undef LG_GRU_NI
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
+extern "C" int64_t lg_gru_node_init_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H) {
+    if (B < 0 || S < 0 || (I != 1 && I != 10) || (H != 32 && H != 64)) return LG_EINVAL;
+    const int64_t slab = 3 * H * H + 3 * H * I + 6 * H + H * (H + 1) + H;
+    return std::max<int64_t>(1, nblocks_seq2(B * S)) * slab * static_cast<int64_t>(sizeof(float));
+}
+
+extern "C" int lg_gru_node_init_bwd(const float* residual, const float* tfeat, const float* w_ih, const float* w_hh,
+                                    const float* h_seq, const float* gates, const float* dx0,
+                                    const int64_t* sensor_idx, const float* live, const float* proj_w,
+                                    const float* dbias_in, float* dw_ih, float* dw_hh, float* db_ih, float* db_hh,
+                                    float* dproj_w, float* dproj_b, int64_t B, int64_t L, int64_t S, int64_t I,
+                                    int64_t H, int64_t N, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
+    if (!dims_ok(B, L, S) || N <= 0) return LG_EINVAL;
+    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (!residual || !w_ih || !w_hh || !h_seq || !gates || !dx0 || !sensor_idx || !proj_w || !dw_ih || !dw_hh ||
+        !db_ih || !db_hh || !dproj_w || !dproj_b || !workspace || (I == 10 && !tfeat))
+        return LG_EINVAL;
+    if (B * N >= kLgMaxRows) return LG_EUNSUPPORTED;
+    hipStream_t s = lg_stream(stream);
+    const int nb = static_cast<int>(std::max<int64_t>(1, nblocks_seq2(B * S)));
+    const int64_t G3 = 3 * H, gl = G3 * H + G3 * I + 2 * G3, len = gl + H * (H + 1) + H;
+    if (ws_bytes < nb * len * static_cast<int64_t>(sizeof(float))) return LG_EINVAL;
+    float* slab = static_cast<float*>(workspace);
+    // inside a reduce batch dbias_in may still be pending (the layer-0 backward's reduction not
+    // yet launched): its partials are then summed into db by the batch instead (as
+    // lg_sensor_proj_bwd does)
+    LgSlabSeg dbseg{gl + H * (H + 1), H, dproj_b};
+    if (lg_reduce_batch_pending(dbias_in, &dbseg.slab2, &dbseg.G2, &dbseg.stride2, &dbseg.off2)) dbias_in = nullptr;
+    if (B == 0) {
+        if (hipMemsetAsync(slab, 0, sizeof(float) * len, s) != hipSuccess) return LG_EHIP;
+    } else {
+        const uint32_t Nseq = static_cast<uint32_t>(B * S);
+        const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
+        const GruNiB ni{dx0, sensor_idx, live, proj_w, dbias_in, static_cast<uint32_t>(B)};
+#define LG_GRU_NIB(HH, UT)                                                                                        \
+    lg_launch(k_gru_bwd2<HH, UT, true, true, true>, static_cast<unsigned>(nb), GB2<HH>::NTH, 0, s, residual, tfeat,   \
+              w_hh, h_seq, gates, nullptr, slab, Nseq, static_cast<int>(L), static_cast<int>(S), fdS, ni)
+        if (H == 64) {
+            if (I == 10) LG_GRU_NIB(64, true); else LG_GRU_NIB(64, false);
+        } else {
+            if (I == 10) LG_GRU_NIB(32, true); else LG_GRU_NIB(32, false);
+        }
+#undef LG_GRU_NIB
+        LG_RET_IF_LAUNCH_FAILED();
+    }
+    const int64_t nWhh = G3 * H, nWih = G3 * I;
+    const LgSlabSeg segs[6] = {{0, nWhh, dw_hh}, {nWhh, nWih, dw_ih}, {nWhh + nWih, G3, db_ih},
+                               {nWhh + nWih + G3, G3, db_hh}, {gl, H * (H + 1), dproj_w}, dbseg};
+    return lg_launch_slab_reduce_multi(slab, nb, len, segs, 6, nullptr, nullptr, s);
 }

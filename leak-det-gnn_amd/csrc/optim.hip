@@ -126,8 +126,7 @@ extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, 
     }
     a.T = T;
     const int G = static_cast<int>(std::max<int64_t>(1, (a.off[T] + kOptChunk - 1) / kOptChunk));
-    (void)workspace;
-    (void)ws_bytes;
+    if (ws_bytes < 8) return LG_EINVAL;  // the (unused) workspace keeps the sized-workspace contract
     lg_launch(k_adam, G, kOptThreads, 0, lg_stream(stream), a, step, lr, beta1, beta2, eps, weight_decay, max_norm,
               norm_out);
     LG_RET_IF_LAUNCH_FAILED();

@@ -100,6 +100,11 @@ SIGNATURES = {
     "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
+    "lg_gru_node_init_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                    _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _u64, _u32, _p]),
+    "lg_gru_node_init_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "lg_gru_node_init_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                    _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_tcn_packed_weight_floats": (_i64, [_i64]),
     "lg_tcn_pack_weight": (_i32, [_p, _p, _i64, _p]),
     "lg_tcn_conv_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _f32, _p, _i64, _i64, _i64, _i64, _i64, _p]),

@@ -146,6 +146,10 @@ class LeakDetector(nn.Module):
         # ascending, as index_add over pipe ids), per-window scatter.  Read when the device
         # state is first built.
         self.incidence_schedule = True
+        # node-major training: the GRU encoder, node init and GCN layers as one op
+        # (library.encoder_trunk: the node init formed in the GRU's epilogue, the projection's
+        # backward in the GRU backward's); False: the encoder module, then library.gnn_trunk
+        self.fuse_encoder = True
         self.boundary: Optional[torch.Tensor] = None
 
     def overlap_split(self):
@@ -182,34 +186,65 @@ class LeakDetector(nn.Module):
             graph.x0marks = ops.SensorMarks.build(graph, slot)
         return graph.x0marks
 
+    def _fused_encoder(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor], B: int, N: int, D: int,
+                       nm: bool) -> bool:
+        """Whether this forward runs the encoder, node init and layers as ONE op
+        (library.encoder_trunk): the node-major trunk with the compressed node init, the
+        reference encoder (1 layer, bias) with node_hidden == sensor_hidden, and residual /
+        tfeat as data (no gradient wanted for them: the fused backward forms no dx)."""
+        g = self.sensor_encoder.gru
+        if not (self.fuse_encoder and g.num_layers == 1 and g.bias and not g.bidirectional):
+            return False
+        if residual.requires_grad or (tfeat is not None and self.sensor_encoder.use_time and tfeat.requires_grad):
+            return False
+        return library.encoder_trunk_supported(B, N, g.hidden_size, D, len(self.convs), nm, self.compress_x0)
+
     def forward(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
         if not residual.is_cuda:
             raise RuntimeError("LeakDetector runs on a ROCm GPU only (libleakgnn has no CPU path)")
         B, L, S = residual.shape
         graph, inc, slot, sensor_idx, slot_live, nonsensor = self._device_state(residual.device)
-
-        h_s = self.sensor_encoder(residual, tfeat)                        # (B, S, Ds)
         f = ops._f32
         Wn, bn = f(self.sensor_to_node.weight), f(self.sensor_to_node.bias)  # (D, Ds+1), (D,)
         N, D = len(self.node_names), Wn.shape[0]
-        if self.capture is not None and torch.is_grad_enabled():
-            if h_s.requires_grad:
-                h_s.retain_grad()
-            self.capture["h_s"] = h_s
         nm = ops.use_node_major(B, N, D, bf16=self.mlp_dtype == "bf16")
         drop = self.training and float(self.dropout.p) > 0.0
         g = graph
-        # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init
-        mk = self._x0marks(g, slot) if (nm and self.compress_x0 and len(self.convs) > 1) else None
-        out = torch.ops.leakgnn.gnn_trunk(
-            h_s, Wn, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
-            nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
-            g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
-            library.seed_tensor(residual.device) if drop else _NO_SEED,
-            mk.nodetab_s if mk is not None else None, mk.pairs_s if mk is not None else None,
-            mk.pos_slot_t if mk is not None else None, bf16=self.mlp_dtype == "bf16")
-        out_t = out
-        xs = out[:-2]                       # [x_0 .. x_L] (then x_L's mask bits and x_0's, when compressed)
+        bf16 = self.mlp_dtype == "bf16"
+        enc = self.sensor_encoder
+        if enc.use_time and tfeat is None:
+            raise ValueError("tfeat required when use_time=True")
+        if self._fused_encoder(residual, tfeat, B, N, D, nm):
+            # encoder + node init + layers as one op (library.encoder_trunk)
+            mk = self._x0marks(g, slot)
+            gw = [f(t) for t in (enc.gru.weight_ih_l0, enc.gru.weight_hh_l0, enc.gru.bias_ih_l0, enc.gru.bias_hh_l0)]
+            cw, cb = [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs]
+            save = torch.is_grad_enabled() and any(t.requires_grad for t in gw + [Wn, bn] + cw + cb)
+            tf = f(tfeat).contiguous() if enc.use_time else None
+            out_t = torch.ops.leakgnn.encoder_trunk(
+                f(residual), tf, *gw, Wn, bn, cw, cb, slot, sensor_idx, slot_live, g.nodetab, g.pairs, g.nodetab_t,
+                g.pairs_t, mk.nodetab_s, mk.pairs_s, mk.pos_slot_t, float(self.dropout.p) if drop else 0.0,
+                library.seed_tensor(residual.device) if drop else _NO_SEED, save, bf16=bf16)
+            nl = len(self.convs)
+            xs = [out_t[nl + 1]] + list(out_t[:nl])  # [x_0 (its sensor rows), x_1 .. x_L]
+            x0bits = out_t[nl + 2]
+        else:
+            h_s = self.sensor_encoder(residual, tfeat)                        # (B, S, Ds)
+            if self.capture is not None and torch.is_grad_enabled():
+                if h_s.requires_grad:
+                    h_s.retain_grad()
+                self.capture["h_s"] = h_s
+            # sensor_to_node (rows with a sensor: [h_s, 1] W^T + b; without: b) folded into node init
+            mk = self._x0marks(g, slot) if (nm and self.compress_x0 and len(self.convs) > 1) else None
+            out_t = torch.ops.leakgnn.gnn_trunk(
+                h_s, Wn, bn, [f(c.lin.weight) for c in self.convs], [f(c.bias) for c in self.convs], slot, sensor_idx,
+                nonsensor, slot_live, g.nodetab, g.pairs, g.rowptr, g.col, g.w, g.nodetab_t, g.pairs_t, g.rowptr_t,
+                g.col_t, g.w_t, float(self.dropout.p) if drop else 0.0, nm,
+                library.seed_tensor(residual.device) if drop else _NO_SEED,
+                mk.nodetab_s if mk is not None else None, mk.pairs_s if mk is not None else None,
+                mk.pos_slot_t if mk is not None else None, bf16=bf16)
+            xs = out_t[:-2]                     # [x_0 .. x_L] (then x_L's mask bits and x_0's, when compressed)
+            x0bits = out_t[-1]
         h_nodes = xs[-1]                                                   # (N, B, D) node-major, else (B, N, D)
         if self.keep_boundary:
             self.boundary = h_nodes
@@ -224,10 +259,10 @@ class LeakDetector(nn.Module):
         # (B, P+1): pipe logits, then the no-leak logit of the mean-pooled window (:206-218)
         sched, sched_hdr = inc.schedule(D)
         out = torch.ops.leakgnn.detector_heads(h_nodes, *hw, inc.ends, inc.rowptr, inc.item, pe, pn, nm, keep, seed,
-                                               sched, sched_hdr, bf16=self.mlp_dtype == "bf16")
+                                               sched, sched_hdr, bf16=bf16)
         if self.capture is not None:
-            if out_t[-1].numel() > 0:  # x_0 compressed: materialise it for the diagnostics
-                xs = [library.expand_x0(xs[0], out_t[-1], slot, bn, N, float(self.dropout.p) if drop else 0.0)] + xs[1:]
+            if x0bits.numel() > 0:  # x_0 compressed: materialise it for the diagnostics
+                xs = [library.expand_x0(xs[0], x0bits, slot, bn, N, float(self.dropout.p) if drop else 0.0)] + xs[1:]
             self.capture.update(xs=xs, node_major=nm, edge_hidden=out[1], noleak_hidden=out[3])
         return out[0]
 

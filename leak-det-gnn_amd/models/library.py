@@ -517,6 +517,8 @@ def gnn_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, h_s: T
 def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sensor_slot, sensor_idx, nonsensor_idx, slot_live,
                              nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_major, bf16, scale, wss, dWs, dbs, dbias_ns,
                              st, x0c=None, p=0.0):
+    dy = _trunk_layer_launches(lib, dy, xs, ymask, weights, sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t,
+                               node_major, bf16, scale, wss, dWs, dbs, dbias_ns, st, x0c, p)
     L = len(weights)
     dev = dy.device
     if node_major:
@@ -524,6 +526,33 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
     else:
         B, N, D = xs[0].shape
     S, Ds = h_s.shape[1], h_s.shape[2]
+    if L == 0:  # no layer-0 launch applied the node init's relu/dropout mask
+        dy = dy * (xs[0] > 0) * scale
+        dbias_ns = dy.index_select(0 if node_major else 1, nonsensor_idx).sum(dim=(0, 1))
+    dh_s = torch.empty(B, S, Ds, device=dev, dtype=torch.float32)
+    dWp = torch.empty(D, Ds + 1, device=dev, dtype=torch.float32)
+    dbp = torch.empty(D, device=dev, dtype=torch.float32)
+    wsp = torch.empty(int(lib.lg_sensor_proj_bwd_workspace_bytes(B, S, Ds, D)), device=dev, dtype=torch.uint8)
+    wss.append(wsp)  # held by the caller until the reduce batch is flushed
+    with _timed("linear_dw", dev):
+        check(lib.lg_sensor_proj_bwd(ptr(dy), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
+                                     ptr(h_s), ptr(proj_weight), ptr(dbias_ns), ptr(dh_s), ptr(dWp), ptr(dbp), B, N,
+                                     S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), wsp.numel(), st),
+              "lg_sensor_proj_bwd")
+    return dh_s, dWp, dbp
+
+
+def _trunk_layer_launches(lib, dy, xs, ymask, weights, sensor_slot, nodetab_t, pairs_t, rowptr_t, col_t, w_t, node_major,
+                          bf16, scale, wss, dWs, dbs, dbias_ns, st, x0c=None, p=0.0) -> Tensor:
+    """The GCN layers' backward, last first; returns the node init's pre-activation gradient
+    (layer 0's dx: masked by the node init's ReLU / dropout; node-major with the compressed
+    node init: the sensor nodes' rows only) and leaves the non-sensor rows' sum in dbias_ns."""
+    L = len(weights)
+    dev = dy.device
+    if node_major:
+        N, B, D = xs[-1].shape
+    else:
+        B, N, D = xs[0].shape
     for l in range(L - 1, -1, -1):
         ws = wss[l]
         flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
@@ -551,20 +580,7 @@ def _trunk_backward_launches(lib, dy, xs, ymask, h_s, proj_weight, weights, sens
                                      col_t.numel(), flags, scale, scale, ptr(ws), ws.numel(), st), "lg_gcn_bwd")
         dWs[l], dbs[l] = dW, db
         dy = dx  # already masked by the previous op's relu/dropout
-    if L == 0:  # no layer-0 launch applied the node init's relu/dropout mask
-        dy = dy * (xs[0] > 0) * scale
-        dbias_ns = dy.index_select(0 if node_major else 1, nonsensor_idx).sum(dim=(0, 1))
-    dh_s = torch.empty(B, S, Ds, device=dev, dtype=torch.float32)
-    dWp = torch.empty(D, Ds + 1, device=dev, dtype=torch.float32)
-    dbp = torch.empty(D, device=dev, dtype=torch.float32)
-    wsp = torch.empty(int(lib.lg_sensor_proj_bwd_workspace_bytes(B, S, Ds, D)), device=dev, dtype=torch.uint8)
-    wss.append(wsp)  # held by the caller until the reduce batch is flushed
-    with _timed("linear_dw", dev):
-        check(lib.lg_sensor_proj_bwd(ptr(dy), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
-                                     ptr(h_s), ptr(proj_weight), ptr(dbias_ns), ptr(dh_s), ptr(dWp), ptr(dbp), B, N,
-                                     S, Ds, D, nat.LG_F_NODE_MAJOR if node_major else 0, ptr(wsp), wsp.numel(), st),
-              "lg_sensor_proj_bwd")
-    return dh_s, dWp, dbp
+    return dy
 
 
 @gnn_trunk_backward.register_fake
@@ -610,6 +626,188 @@ def _trunk_bwd(ctx, grads):
 
 
 gnn_trunk.register_autograd(_trunk_bwd, setup_context=_trunk_setup)
+
+
+# ============================================================================ encoder_trunk
+# The sensor encoder, the node init and the GCN layers as ONE registered op (the node-major
+# trunk with the compressed node init): the GRU's training forward forms the node init's
+# sensor rows and [x0 > 0] words in its epilogue (lg_gru_node_init_fwd), and the backward runs
+# the layers, then the GRU with the sensor projection's backward in its prologue / epilogue
+# (lg_gru_node_init_bwd), all weight-gradient reductions in one launch.  Against gru_encoder +
+# gnn_trunk: the node-init launch and the projection-backward launch leave the step, and the
+# trunk's and the GRU's reductions share one launch.  Same arithmetic, bit for bit
+# (tests/test_gpu_x0.py::test_encoder_trunk_equals_separate_ops).
+def encoder_trunk_supported(B: int, N: int, H: int, D: int, L: int, node_major: bool, compress: bool) -> bool:
+    """The fused op's case: node-major layout, the compressed node init (L >= 2, no alternate
+    forward-kernel flag), node_hidden == sensor_hidden in {32, 64}."""
+    return (node_major and compress and H == D and D in (32, 64)
+            and _compress_x0(torch.empty(0), node_major, L))
+
+
+@torch.library.custom_op(f"{NS}::encoder_trunk", mutates_args=(), device_types="cuda")
+def encoder_trunk(residual: Tensor, tfeat: Optional[Tensor], w_ih: Tensor, w_hh: Tensor, b_ih: Tensor, b_hh: Tensor,
+                  proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], biases: List[Tensor],
+                  sensor_slot: Tensor, sensor_idx: Tensor, slot_live: Optional[Tensor], nodetab: Tensor, pairs: Tensor,
+                  nodetab_t: Tensor, pairs_t: Tensor, nodetab_s: Tensor, pairs_s: Tensor, pos_slot_t: Tensor, p: float,
+                  seed: Tensor, save: bool, *, bf16: bool = False) -> List[Tensor]:
+    """[x_1, ..., x_L, ymask, xs0, x0bits, h_seq, gates]: SharedSensorGRUEncoder (detector.py:60-73),
+    the node init (:179-190: h0, the mask column, sensor_to_node, ReLU, dropout) and L x
+    dropout(relu(GCNConv)) (:198-201) on the node-major layout [N][B][D].  x_0 stays
+    compressed: xs0 (S, B, D) its sensor rows, x0bits [x_0 > 0] of the other rows.  ymask: x_L's
+    [x > 0] bits.  h_seq / gates: the GRU's saved steps (empty unless save).  residual and tfeat
+    are data (no gradient)."""
+    lib = load_library()
+    residual, tfeat = _c(residual), _c(tfeat)
+    w_ih, w_hh, b_ih, b_hh, proj_weight, node_bias = (_c(t) for t in (w_ih, w_hh, b_ih, b_hh, proj_weight, node_bias))
+    weights, biases = [_c(t) for t in weights], [_c(t) for t in biases]
+    _req(residual, tfeat, w_ih, w_hh, b_ih, b_hh, proj_weight, node_bias, *weights, *biases)
+    B, Lw, S = residual.shape
+    G, I = w_ih.shape
+    H = w_hh.shape[1]
+    D = proj_weight.shape[0]
+    N = sensor_slot.shape[0]
+    L = len(weights)
+    if not encoder_trunk_supported(B, N, H, D, L, True, True):
+        raise NotImplementedError("encoder_trunk: node-major trunk with the compressed node init, "
+                                  "node_hidden == sensor_hidden in {32, 64}, at least two layers")
+    if tuple(proj_weight.shape) != (D, H + 1):
+        raise ValueError(f"proj_weight must be ({D}, {H + 1}), got {tuple(proj_weight.shape)}")
+    dev = residual.device
+    st = stream_of(residual)
+    drop = p > 0.0
+    seed_v, sbit = _seed_args(seed) if drop else (0, 0)
+    dflag = nat.LG_F_DROPOUT if drop else 0
+    nmask = N * ((B + 15) // 16) * 64
+    h_seq = torch.empty(Lw, B * S, H, device=dev) if save else torch.empty(0, device=dev)
+    gates = torch.empty(Lw, B * S, 4, H, device=dev) if save else torch.empty(0, device=dev)
+    h_last = torch.empty(B, S, H, device=dev)
+    xs0 = torch.empty((S, B, D), device=dev, dtype=torch.float32)
+    x0bits = torch.empty(nmask, device=dev, dtype=torch.int16)
+    with _timed("gru_fwd", dev):
+        check(lib.lg_gru_node_init_fwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(b_ih), ptr(b_hh),
+                                       ptr(h_seq) if save else None, ptr(gates) if save else None, ptr(h_last),
+                                       ptr(sensor_slot), ptr(sensor_idx), ptr(proj_weight), ptr(node_bias), ptr(xs0),
+                                       ptr(x0bits), B, Lw, S, I, H, N, dflag, p, seed_v, 0 | sbit, st),
+              "lg_gru_node_init_fwd")
+    ymask = torch.empty(nmask, device=dev, dtype=torch.int16)
+    xs = [xs0]
+    for l, (W, b) in enumerate(zip(weights, biases)):
+        y = torch.empty((N, B, D), device=dev, dtype=torch.float32)
+        flags = nat.LG_F_BIAS | nat.LG_F_RELU | dflag | (nat.LG_F_BF16 if bf16 else 0)
+        with _timed("gcn_fwd" if l > 0 else "gcn_fwd_l0", dev):
+            if l == 0:
+                check(lib.lg_gcn_fwd_nm_x0(ptr(nodetab_s), ptr(pairs_s), ptr(xs0), ptr(x0bits), ptr(node_bias), ptr(W),
+                                           ptr(b), ptr(y), B, N, S, D, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v,
+                                           (l + 1) | sbit, st), "lg_gcn_fwd_nm_x0")
+            else:
+                check(lib.lg_gcn_fwd_nm_bits(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
+                                             pairs.shape[0], flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v, (l + 1) | sbit,
+                                             st, ptr(ymask) if l == L - 1 else None), "lg_gcn_fwd_nm_bits")
+        xs.append(y)
+    return xs[1:] + [ymask, xs0, x0bits, h_seq, gates]
+
+
+@encoder_trunk.register_fake
+def _(residual, tfeat, w_ih, w_hh, b_ih, b_hh, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx,
+      slot_live, nodetab, pairs, nodetab_t, pairs_t, nodetab_s, pairs_s, pos_slot_t, p, seed, save, *, bf16=False):
+    B, Lw, S = residual.shape
+    H = w_hh.shape[1]
+    D = proj_weight.shape[0]
+    N = sensor_slot.shape[0]
+    nmask = N * ((B + 15) // 16) * 64
+    h_seq = residual.new_empty(Lw, B * S, H) if save else residual.new_empty(0)
+    gates = residual.new_empty(Lw, B * S, 4, H) if save else residual.new_empty(0)
+    return ([residual.new_empty(N, B, D) for _ in weights] + [residual.new_empty((nmask,), dtype=torch.int16),
+            residual.new_empty(S, B, D), residual.new_empty((nmask,), dtype=torch.int16), h_seq, gates])
+
+
+@torch.library.custom_op(f"{NS}::encoder_trunk_backward", mutates_args=(), device_types="cuda")
+def encoder_trunk_backward(grad_out: Tensor, xs: List[Tensor], ymask: Tensor, x0bits: Tensor, residual: Tensor,
+                           tfeat: Optional[Tensor], w_ih: Tensor, w_hh: Tensor, h_seq: Tensor, gates: Tensor,
+                           proj_weight: Tensor, node_bias: Tensor, weights: List[Tensor], sensor_slot: Tensor,
+                           sensor_idx: Tensor, slot_live: Optional[Tensor], nodetab_t: Tensor, pairs_t: Tensor,
+                           pos_slot_t: Tensor, p: float, *, bf16: bool = False) -> List[Tensor]:
+    """[dw_ih, dw_hh, db_ih, db_hh, dproj_weight, dnode_bias, dW_0 .. dW_{L-1}, db_0 .. db_{L-1}]: the
+    layers' backward (last first; layer 0 on the compressed x_0, its dx for the sensor rows
+    only), then lg_gru_node_init_bwd; one reduce batch for all of them."""
+    lib = load_library()
+    if h_seq.numel() == 0 or gates.numel() == 0:
+        raise RuntimeError("encoder_trunk was run with save=False; no backward")
+    L = len(weights)
+    dev = grad_out.device
+    st = stream_of(grad_out)
+    N, B, D = xs[-1].shape
+    S, Lw = residual.shape[2], residual.shape[1]
+    I, H = w_ih.shape[1], w_hh.shape[1]
+    scale = 1.0 / (1.0 - p) if p > 0.0 else 1.0
+    wsb = lib.lg_gcn_bwd_nm_workspace_bytes(D)
+    wss = [torch.empty(int(wsb), device=dev, dtype=torch.uint8) for _ in range(L)]
+    dWs: List[Tensor] = [grad_out] * L
+    dbs: List[Tensor] = [grad_out] * L
+    dbias_ns = torch.empty(D, device=dev, dtype=torch.float32)
+    dw_ih, dw_hh = torch.empty_like(w_ih), torch.empty_like(w_hh)
+    db_ih, db_hh = torch.empty(3 * H, device=dev), torch.empty(3 * H, device=dev)
+    dWp, dbp = torch.empty_like(proj_weight), torch.empty(D, device=dev)
+    wsg = torch.empty(int(lib.lg_gru_node_init_bwd_workspace_bytes(B, S, I, H)), device=dev, dtype=torch.uint8)
+    with _reduce_batch(lib, st):
+        dx0 = _trunk_layer_launches(lib, grad_out.contiguous(), xs, ymask, weights, sensor_slot, nodetab_t, pairs_t,
+                                    None, None, None, True, bf16, scale, wss, dWs, dbs, dbias_ns, st,
+                                    (x0bits, node_bias, pos_slot_t), p)
+        with _timed("gru_bwd", dev):
+            check(lib.lg_gru_node_init_bwd(ptr(residual), ptr(tfeat), ptr(w_ih), ptr(w_hh), ptr(h_seq), ptr(gates),
+                                           ptr(dx0), ptr(sensor_idx), ptr(slot_live) if slot_live is not None else None,
+                                           ptr(proj_weight), ptr(dbias_ns), ptr(dw_ih), ptr(dw_hh), ptr(db_ih),
+                                           ptr(db_hh), ptr(dWp), ptr(dbp), B, Lw, S, I, H, N, ptr(wsg), wsg.numel(),
+                                           st), "lg_gru_node_init_bwd")
+    return [dw_ih, dw_hh, db_ih, db_hh, dWp, dbp] + dWs + dbs
+
+
+@encoder_trunk_backward.register_fake
+def _(grad_out, xs, ymask, x0bits, residual, tfeat, w_ih, w_hh, h_seq, gates, proj_weight, node_bias, weights,
+      sensor_slot, sensor_idx, slot_live, nodetab_t, pairs_t, pos_slot_t, p, *, bf16=False):
+    H = w_hh.shape[1]
+    D = proj_weight.shape[0]
+    return ([torch.empty_like(w_ih), torch.empty_like(w_hh), w_ih.new_empty(3 * H), w_ih.new_empty(3 * H),
+             torch.empty_like(proj_weight), proj_weight.new_empty(D)] + [torch.empty_like(t) for t in weights]
+            + [proj_weight.new_empty(D) for _ in weights])
+
+
+def _et_setup(ctx, inputs, keyword_only_inputs, output):
+    (residual, tfeat, w_ih, w_hh, b_ih, b_hh, proj_weight, node_bias, weights, biases, sensor_slot, sensor_idx,
+     slot_live, nodetab, pairs, nodetab_t, pairs_t, nodetab_s, pairs_s, pos_slot_t, p, seed, save) = inputs
+    L = len(weights)
+    ctx.L, ctx.p, ctx.bf16 = L, p, bool(keyword_only_inputs.get("bf16", False))
+    ctx.has_tfeat, ctx.has_live = tfeat is not None, slot_live is not None
+    # x_1 .. x_{L-1}, ymask, xs0, x0bits, h_seq, gates: saved, never differentiated
+    ctx.mark_non_differentiable(*output[:L - 1], *output[L:])
+    ctx.set_materialize_grads(False)
+    ctx.save_for_backward(*output[:L], output[L], output[L + 1], output[L + 2], output[L + 3], output[L + 4],
+                          residual, tfeat if tfeat is not None else residual, w_ih, w_hh, proj_weight, node_bias,
+                          *weights, sensor_slot, sensor_idx, slot_live if slot_live is not None else sensor_slot,
+                          nodetab_t, pairs_t, pos_slot_t)
+
+
+def _et_bwd(ctx, grads):
+    L = ctx.L
+    g = grads[L - 1]
+    if g is None:
+        return (None,) * 23
+    sv = ctx.saved_tensors
+    xl = list(sv[:L])
+    ymask, xs0, x0bits, h_seq, gates = sv[L:L + 5]
+    residual, tfeat, w_ih, w_hh, proj_weight, node_bias = sv[L + 5:L + 11]
+    weights = list(sv[L + 11:2 * L + 11])
+    sensor_slot, sensor_idx, live, nodetab_t, pairs_t, pos_slot_t = sv[2 * L + 11:]
+    out = torch.ops.leakgnn.encoder_trunk_backward(
+        g, [xs0] + xl, ymask, x0bits, residual, tfeat if ctx.has_tfeat else None, w_ih, w_hh, h_seq, gates,
+        proj_weight, node_bias, weights, sensor_slot, sensor_idx, live if ctx.has_live else None, nodetab_t, pairs_t,
+        pos_slot_t, ctx.p, bf16=ctx.bf16)
+    dw_ih, dw_hh, db_ih, db_hh, dWp, dbp = out[:6]
+    dWs, dbs = list(out[6:6 + L]), list(out[6 + L:])
+    return (None, None, dw_ih, dw_hh, db_ih, db_hh, dWp, dbp, dWs, dbs) + (None,) * 13
+
+
+encoder_trunk.register_autograd(_et_bwd, setup_context=_et_setup)
 
 
 # ============================================================================ detector_heads

@@ -128,6 +128,32 @@ def test_opcheck_trunk_and_heads(B, p):
            {"bf16": B == 16})
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_opcheck_encoder_trunk(p):
+    """leakgnn::encoder_trunk (the GRU, node init and layers as one op) at B = 16, node-major,
+    with the detector's own graph state and marks."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV)
+    graph, inc, slot, sidx, live, nons = m._device_state(DEV)
+    mk = m._x0marks(graph, slot)
+    B = 16
+    seed = torch.tensor([4242], dtype=torch.long)
+    r, tf = torch.randn(B, 36, 29, device=DEV), torch.randn(B, 36, 9, device=DEV)
+    gw = [t.detach().clone().requires_grad_(True) for t in (m.sensor_encoder.gru.weight_ih_l0,
+                                                              m.sensor_encoder.gru.weight_hh_l0,
+                                                              m.sensor_encoder.gru.bias_ih_l0,
+                                                              m.sensor_encoder.gru.bias_hh_l0)]
+    Wn = torch.randn(64, 65, device=DEV).div_(8).requires_grad_(True)
+    nb = torch.randn(64, device=DEV, requires_grad=True)
+    wts = [c.lin.weight.detach().clone().requires_grad_(True) for c in m.convs]
+    bs = [c.bias.detach().clone().normal_(0, 0.1).requires_grad_(True) for c in m.convs]
+    g = graph
+    _check(torch.ops.leakgnn.encoder_trunk.default,
+           (r, tf, *gw, Wn, nb, wts, bs, slot, sidx, live, g.nodetab, g.pairs, g.nodetab_t, g.pairs_t, mk.nodetab_s,
+            mk.pairs_s, mk.pos_slot_t, p, seed, True), {"bf16": False})
+
+
 @pytest.mark.parametrize("fullgraph", [False, True])
 def test_torch_compile_aot_eager_matches_eager(fullgraph):
     """The detector forward + backward traced by torch.compile (aot_eager: every

@@ -196,3 +196,57 @@ def test_detector_gnn_layers_train_step(layers):
     assert_close(res[1][0], res[0][0], rtol=1e-5, what="logits")
     for k in res[0][1]:
         assert_close(res[1][1][k], res[0][1][k], rtol=1e-5, atol=0.0, what=f"grad {k}")
+
+
+@pytest.mark.parametrize("train,B", [(True, 48), (False, 48), (True, 256), (True, 37)])
+def test_encoder_trunk_equals_separate_ops(train, B):
+    """library.encoder_trunk (the GRU, node init and layers as one op: the node init in the GRU
+    forward's epilogue, the projection's backward in the GRU backward's prologue / epilogue)
+    equals gru_encoder + gnn_trunk bit for bit: logits and every parameter gradient (same
+    arithmetic, same dropout draws, the reductions over the same partials in the same order)."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    torch.manual_seed(0)
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train(train)
+    with torch.no_grad():
+        for c in m.convs:
+            c.bias.normal_(0, 0.1)
+    gen = torch.Generator().manual_seed(7)
+    r = torch.randn(B, 36, 29, generator=gen).to(DEV)
+    tf = torch.randn(B, 36, 9, generator=gen).to(DEV)
+    lab = torch.randint(0, len(pipes) + 1, (B,), generator=gen).to(DEV)
+    res = []
+    for fused in (False, True):
+        m.fuse_encoder = fused
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(13)
+        logits = m(r, tf)
+        torch.nn.functional.cross_entropy(logits, lab).backward()
+        res.append((logits.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    assert torch.equal(res[1][0], res[0][0]), "logits differ"
+    for k in res[0][1]:
+        assert torch.equal(res[1][1][k], res[0][1][k]), f"grad {k} differs: {(res[1][1][k] - res[0][1][k]).abs().max():.3e}"
+
+
+def test_encoder_trunk_eval_no_grad_and_fallbacks():
+    """Eval under no_grad takes the fused op without saving the GRU steps; a residual that wants
+    a gradient, or the window-major layout (B < 16), takes the separate ops."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    torch.manual_seed(0)
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).eval()
+    gen = torch.Generator().manual_seed(8)
+    r = torch.randn(32, 36, 29, generator=gen).to(DEV)
+    tf = torch.randn(32, 36, 9, generator=gen).to(DEV)
+    with torch.no_grad():
+        m.fuse_encoder = True
+        a = m(r, tf)
+        m.fuse_encoder = False
+        b = m(r, tf)
+    assert torch.equal(a, b)
+    m.fuse_encoder = True
+    rg = r.clone().requires_grad_(True)
+    assert not m._fused_encoder(rg, tf, 32, 661, 64, True)
+    m(rg, tf).sum().backward()
+    assert rg.grad is not None and torch.isfinite(rg.grad).all()
+    assert not m._fused_encoder(r[:8], tf[:8], 8, 661, 64, False)

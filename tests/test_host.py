@@ -183,9 +183,13 @@ def test_undersized_workspace_returns_einval():
     sizes = (ctypes.c_int64 * 1)(1000)
     table = (ctypes.c_int64 * 4)(F, F, F, F)
     wsa = lib.lg_clip_adamw_workspace_bytes(ctypes.addressof(sizes), 1)
-    assert wsa == 16  # two 512-element slices, one fp64 partial each
+    assert wsa == 8  # one launch since ABI 23: no partials (the workspace stays a sized argument)
     assert lib.lg_clip_adamw(ctypes.addressof(table), ctypes.addressof(sizes), 1, F, 1e-3, 0.9, 0.999, 1e-8, 0.0,
                              1.0, None, F, wsa - 1, None) == -1
+    wsn = lib.lg_gru_node_init_bwd_workspace_bytes(B, S, 10, 64)
+    assert wsn > 0
+    assert lib.lg_gru_node_init_bwd(F, F, F, F, F, F, F, F, None, F, None, F, F, F, F, F, F, B, 36, S, 10, 64, N, F,
+                                    wsn - 1, None) == -1
 
 
 def test_library_built_for_gfx950_only():
