@@ -196,7 +196,7 @@ def small_kernels_us(breakdown: dict | None) -> dict:
     if not breakdown:
         return {}
     by = breakdown["by_name_us"]
-    pick = {"ce_fwd": ["k_ce_fwd", "k_ce_mean"], "ce_bwd": ["k_ce_bwd"], "adam": ["k_adam_norm", "k_adam_update"],
+    pick = {"ce_fwd": ["k_ce_fwd", "k_ce_mean"], "ce_bwd": ["k_ce_bwd"], "adam": ["k_adam", "k_adam_norm", "k_adam_update"],
             "seed": ["k_seed_advance"], "slab_reduce": ["k_slab_reduce"], "sensor_proj_bwd": ["k_sensor_proj_bwd"]}
     return {k: round(sum(by.get(n, 0.0) for n in v), 2) for k, v in pick.items()}
 

@@ -168,6 +168,13 @@ int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T);
 int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
                   float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace, int64_t ws_bytes,
                   lg_stream_t stream);
+/* lg_clip_adamw, then (ABI 23) the draw of lg_seed_slots_advance(seed_slots, n_slots, seed_state)
+ * in the same launch, by its last workgroup: a captured training step ends by drawing the NEXT
+ * replay's dropout seeds, one launch fewer per step. */
+int lg_clip_adamw_seeds(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
+                        float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace,
+                        int64_t ws_bytes, uint64_t* seed_slots, int64_t n_slots, uint64_t* seed_state,
+                        lg_stream_t stream);
 
 /* Kernel timing (bench.py; no reference counterpart — the reference has no kernels).
  * lg_timing_arm(slot): the NEXT library kernel launch on this host thread that is the main

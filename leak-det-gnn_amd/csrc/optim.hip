@@ -32,9 +32,24 @@ struct AdamTensors {
     int T;
 };
 
+// the next step's dropout seed slots (lg_clip_adamw_seeds): lg_seed_slots_advance's draw, by
+// the launch's last workgroup
+__device__ __forceinline__ uint64_t opt_splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+struct AdamSeeds {
+    uint64_t* slots;
+    uint64_t* state;
+    int n;
+};
+
 __global__ void __launch_bounds__(kOptThreads)
 k_adam(AdamTensors a, float* __restrict__ step, float lr, float beta1, float beta2, float eps, float wd,
-       float max_norm, float* __restrict__ norm_out) {
+       float max_norm, float* __restrict__ norm_out, AdamSeeds seeds) {
+    __shared__ uint32_t last;
     __shared__ double red[kOptThreads];
     __shared__ float tsh;
     const int tid = threadIdx.x;
@@ -66,11 +81,22 @@ k_adam(AdamTensors a, float* __restrict__ step, float lr, float beta1, float bet
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         uint32_t* ctr = reinterpret_cast<uint32_t*>(step + 1);
         const uint32_t tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tk + 1 == gridDim.x) {  // every other workgroup has read step[0]: commit t
+        last = tk + 1 == gridDim.x ? 1u : 0u;
+        if (last) {  // every other workgroup has read step[0]: commit t
             __hip_atomic_store(step, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (blockIdx.x == 0 && norm_out) norm_out[0] = static_cast<float>(norm);
+    }
+    if (seeds.slots) {  // the next step's dropout seeds: nothing in this launch reads them
+        __syncthreads();
+        if (last && tid < 64) {
+            const uint64_t c = seeds.state[0] + 1;  // every lane reads before lane 0 writes (one wave)
+            for (int i = tid; i < seeds.n; i += 64)
+                seeds.slots[i] = opt_splitmix64(c * static_cast<uint64_t>(seeds.n) + static_cast<uint64_t>(i) + 1) &
+                                 ((1ull << 62) - 1);
+            if (tid == 0) seeds.state[0] = c;
+        }
     }
     const float coef = max_norm > 0.f ? static_cast<float>(fmin(1.0, static_cast<double>(max_norm) / (norm + 1e-6)))
                                       : 1.0f;
@@ -108,9 +134,10 @@ extern "C" int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T) {
     return 8;  // unused since the single-launch form (kept: callers size and pass it)
 }
 
-extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
-                             float beta2, float eps, float weight_decay, float max_norm, float* norm_out,
-                             void* workspace, int64_t ws_bytes, lg_stream_t stream) {
+namespace {
+int clip_adamw_impl(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1, float beta2,
+                    float eps, float weight_decay, float max_norm, float* norm_out, void* workspace, int64_t ws_bytes,
+                    const AdamSeeds& seeds, lg_stream_t stream) {
     if (T > kOptMaxTensors) return LG_EUNSUPPORTED;
     if (T < 0 || (T > 0 && (!table || !sizes)) || !step || !workspace) return LG_EINVAL;
     if (!(beta1 >= 0.f && beta1 < 1.f) || !(beta2 >= 0.f && beta2 < 1.f) || !(eps >= 0.f)) return LG_EINVAL;
@@ -128,7 +155,25 @@ extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, 
     const int G = static_cast<int>(std::max<int64_t>(1, (a.off[T] + kOptChunk - 1) / kOptChunk));
     if (ws_bytes < 8) return LG_EINVAL;  // the (unused) workspace keeps the sized-workspace contract
     lg_launch(k_adam, G, kOptThreads, 0, lg_stream(stream), a, step, lr, beta1, beta2, eps, weight_decay, max_norm,
-              norm_out);
+              norm_out, seeds);
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
+}
+}  // namespace
+
+extern "C" int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, float max_norm, float* norm_out,
+                             void* workspace, int64_t ws_bytes, lg_stream_t stream) {
+    return clip_adamw_impl(table, sizes, T, step, lr, beta1, beta2, eps, weight_decay, max_norm, norm_out, workspace,
+                           ws_bytes, AdamSeeds{nullptr, nullptr, 0}, stream);
+}
+
+extern "C" int lg_clip_adamw_seeds(const int64_t* table, const int64_t* sizes, int T, float* step, float lr,
+                                   float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                                   float* norm_out, void* workspace, int64_t ws_bytes, uint64_t* seed_slots,
+                                   int64_t n_slots, uint64_t* seed_state, lg_stream_t stream) {
+    if (n_slots < 0 || n_slots > 4096 || (n_slots > 0 && (!seed_slots || !seed_state))) return LG_EINVAL;
+    return clip_adamw_impl(table, sizes, T, step, lr, beta1, beta2, eps, weight_decay, max_norm, norm_out, workspace,
+                           ws_bytes, AdamSeeds{n_slots > 0 ? seed_slots : nullptr, seed_state, static_cast<int>(n_slots)},
+                           stream);
 }

@@ -47,6 +47,8 @@ SIGNATURES = {
     "lg_cross_entropy_bwd": (_i32, [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _p, _i64, _p]),
     "lg_clip_adamw_workspace_bytes": (_i64, [_p, _i32]),
     "lg_clip_adamw": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _i64, _p]),
+    "lg_clip_adamw_seeds": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _i64, _p, _i64, _p,
+                                   _p]),
     "lg_timing_arm": (_i32, [_i32]),
     "lg_timing_disarm": (_i32, []),
     "lg_timing_elapsed": (_i32, [_i32, _p]),

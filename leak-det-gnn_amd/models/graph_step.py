@@ -12,7 +12,10 @@ and replayed: one graph launch per step, the kernels back to back on the device.
     as the reference's `.to(device)` is, train_detector.py:297-299).
   * Dropout stays random per replay: while capturing, the library's dropout call sites
     read their seeds from device slots (ops.SeedSlots, include/leakgnn.h
-    LG_SALT_SEED_PTR) that a captured torch RNG op re-draws at the head of every replay.
+    LG_SALT_SEED_PTR) that are re-drawn on the device for every replay: by the optimizer's
+    own launch at the END of the previous replay when the optimizer can (ClipAdamW:
+    lg_clip_adamw_seeds; one eager draw before the first replay), else by a launch at the
+    head of the step (lg_seed_slots_advance).
   * The optimizer must be built with capturable=True (device-side step counters).
   * world > 1: no collective is ever captured.  A model that names a gradient split
     (`overlap_split()` -> the parameters whose gradients are final at a boundary tensor
@@ -85,20 +88,25 @@ class CapturedTrainStep:
         hid = {id(p) for p in self.heads}
         self.trunk = [p for p in self.params if id(p) not in hid]
         ops.use_device_seeds(self.slots)
+        # the optimizer draws the next replay's seeds in its own launch (ClipAdamW)
+        self.fold_seeds = hasattr(self.opt, "seed_slots")
+        head_refresh = not self.fold_seeds
         try:
             if self.world == 1:
                 with torch.cuda.graph(self.graph_a):
-                    self.slots.refresh()
+                    if head_refresh:
+                        self.slots.refresh()
                     # detached: the static loss must not keep the capture-time autograd graph
                     # (and its AccumulateGrad nodes, bound to the capture stream) alive, or a
                     # later eager backward on another stream would sync on them
                     self.loss = self._forward_backward().detach()
-                    self._update()
+                    self._update(fold=self.fold_seeds)
             elif self.heads:
                 model.keep_boundary = True
                 try:
                     with torch.cuda.graph(self.graph_a):
-                        self.slots.refresh()
+                        if head_refresh:
+                            self.slots.refresh()
                         loss = self.loss_fn(self.model(*self.inputs), self.label)
                         bnd = model.boundary
                         self._one = torch.ones_like(loss)
@@ -117,7 +125,8 @@ class CapturedTrainStep:
                 self.buckets = [(self.flat_h, self.heads), (self.flat_t, self.trunk)]
             else:
                 with torch.cuda.graph(self.graph_a):
-                    self.slots.refresh()
+                    if head_refresh:
+                        self.slots.refresh()
                     self.loss = self._forward_backward().detach()
                     self.flat = torch.cat([p.grad.reshape(-1) for p in self.params])
                 self.buckets = [(self.flat, self.params)]
@@ -125,6 +134,9 @@ class CapturedTrainStep:
             ops.use_device_seeds(None)
         if snap is not None:
             self._restore(snap)
+        if self.fold_seeds and self.world == 1:
+            self.slots.refresh()  # the first replay's seeds (each replay then draws the next one's)
+            torch.cuda.synchronize(dev)
         if self.world > 1:
             grads, views = [], []
             for flat, ps in self.buckets:
@@ -136,7 +148,10 @@ class CapturedTrainStep:
             self.graph_b = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph_b):
                 torch._foreach_copy_(grads, views)
-                self._update()
+                self._update(fold=self.fold_seeds)
+            if self.fold_seeds:
+                self.slots.refresh()
+                torch.cuda.synchronize(dev)
 
     def _opt_tensors(self) -> list:
         out = []
@@ -174,10 +189,16 @@ class CapturedTrainStep:
         loss.backward(self._one)
         return loss
 
-    def _update(self) -> None:
+    def _update(self, fold: bool = False) -> None:
         if self.clip is not None:
             torch.nn.utils.clip_grad_norm_(self.params, self.clip)
-        self.opt.step()
+        if fold:  # the optimizer's launch also draws the next replay's dropout seeds
+            self.opt.seed_slots = self.slots
+        try:
+            self.opt.step()
+        finally:
+            if fold:
+                self.opt.seed_slots = None
 
     def _eager_step(self) -> None:
         self.opt.zero_grad(set_to_none=True)

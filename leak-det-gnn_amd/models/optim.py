@@ -40,6 +40,10 @@ class ClipAdamW(torch.optim.Optimizer):
                                       max_norm=max_norm, capturable=True))
         self.last_grad_norm: Optional[torch.Tensor] = None
         self._ws: dict = {}  # group index -> per-slice partial-norm workspace
+        # ops.SeedSlots whose next draw step() makes in its own launch (lg_clip_adamw_seeds):
+        # set by graph_step.CapturedTrainStep while it captures the step, so the step ends by
+        # drawing the next replay's dropout seeds instead of starting with a launch of its own
+        self.seed_slots = None
 
     def load_state_dict(self, state_dict) -> None:
         super().load_state_dict(state_dict)
@@ -89,10 +93,13 @@ class ClipAdamW(torch.optim.Optimizer):
                 ws = self._ws[gi] = torch.empty(nws, dtype=torch.uint8, device=params[0].device)
             b1, b2 = group["betas"]
             mn = group["max_norm"]
-            check(lib.lg_clip_adamw(ctypes.addressof(table), ctypes.addressof(sizes), len(params),
-                                    group["step_t"].data_ptr(),
-                                    float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                    float(group["weight_decay"]), float(mn) if mn is not None else 0.0,
-                                    self.last_grad_norm.data_ptr(), ws.data_ptr(), ws.numel(), stream_of(params[0])),
-                  "lg_clip_adamw")
+            args = (ctypes.addressof(table), ctypes.addressof(sizes), len(params), group["step_t"].data_ptr(),
+                    float(group["lr"]), float(b1), float(b2), float(group["eps"]), float(group["weight_decay"]),
+                    float(mn) if mn is not None else 0.0, self.last_grad_norm.data_ptr(), ws.data_ptr(), ws.numel())
+            sl = self.seed_slots if gi == len(self.param_groups) - 1 else None  # the last group's launch draws them
+            if sl is not None:
+                check(lib.lg_clip_adamw_seeds(*args, sl.buf.data_ptr(), sl.n, sl.state.data_ptr(), stream_of(params[0])),
+                      "lg_clip_adamw_seeds")
+            else:
+                check(lib.lg_clip_adamw(*args, stream_of(params[0])), "lg_clip_adamw")
         return loss
