@@ -528,6 +528,23 @@ int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w
                              int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden,
                              int flags, float dropout_p, void* workspace, int64_t ws_bytes, lg_stream_t stream);
 
+/* Both heads' backward (ABI 23): lg_pool_head_bwd (the NoLeakHead, first argument block) then
+ * lg_edge_head_bwd_scatter, as ONE launch when the streamed form applies (a pipe schedule, a
+ * window per workgroup): the NoLeakHead backward of each workgroup's windows runs in its
+ * prologue (the same sums in the same order as k_pool_head_bwd), dpool [B][D] becomes a scratch
+ * the launch writes and reads back.  Otherwise the two calls, in that order (dpool their
+ * hand-off).  nworkspace: lg_pool_head_bwd_workspace_bytes; workspace:
+ * lg_edge_head_bwd_workspace_bytes.  Replaces detector.py:214-216's and :206-211's autograd
+ * (global_mean_pool + NoLeakHead, pipe gather + EdgeHead). */
+int lg_heads_bwd_scatter(const float* pooled, const float* nhid, const float* nw1, const float* nw2, float* ndw1,
+                         float* ndb1, float* ndw2, float* ndb2, int nflags, float n_dropout_p, void* nworkspace,
+                         int64_t nws_bytes, const int64_t* ends, const float* h, const float* w1, const float* w2,
+                         const float* hid, const float* dlogits, int64_t ldo, float* dpipe, float* dw1, float* db1,
+                         float* dw2, float* db2, const int32_t* inc_rowptr, const int32_t* inc_item,
+                         const int32_t* sched, const int32_t* sched_hdr, float* dpool, float* dh, int64_t B, int64_t N,
+                         int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p, void* workspace,
+                         int64_t ws_bytes, lg_stream_t stream);
+
 /* Pipe schedule of the streamed EdgeHead backward (ABI 22), once per model; HOST memory in and
  * out (upload sched to the device; keep its first 16 words on the host as sched_hdr).
  *   ends : int64 [P][2];  D : 32 or 64 (the tile height 2048 / D);

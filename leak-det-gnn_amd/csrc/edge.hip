@@ -402,6 +402,15 @@ struct EdgeScatter {
     const int32_t* szero;    // [nzero]
     int nzero, nslots, bw, maxev;
     int lab;  // kernel-lab builds only (LG_KERNEL_LAB; results WRONG when set): 1 skip dW1 MFMA, 2 skip dfeat MFMA, 4 skip the streamed scatter
+    // POOL (lg_heads_bwd_scatter, STREAM only): the NoLeakHead backward of the workgroup's windows
+    // in its prologue (k_pool_head_bwd's arithmetic), dpool written to the `dpool` scratch above
+    const float* pooled = nullptr;  // [B][D]
+    const float* nhid = nullptr;    // [B][HID] the NoLeakHead's saved hidden layer
+    const float* nW1 = nullptr;     // [HID][D]
+    const float* nw2 = nullptr;     // [HID]
+    float nscale = 1.f;             // its dropout scale
+    float* nslab = nullptr;         // per workgroup: [dW1 HID * D][db1 HID][dw2 HID]
+    double* ndslab = nullptr;       // per workgroup: db2
 };
 
 // dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
@@ -535,6 +544,58 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     constexpr int SL = HID * G::K3 + 2 * HID + 1;
     constexpr int NPL = F16 ? 2 : 3;  // image planes
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if constexpr (STREAM) {
+        if (sc.nslab) {
+            // NoLeakHead backward (k_pool_head_bwd, pool.hip: the same sums in the same order) for
+            // the windows this workgroup owns, before the images take the LDS:
+            //   dhid = dlogit[b][P] * w2 * scale * [hid > 0],  dpool[b] = dhid W1 (fixed kk order),
+            //   the slab row: dW1 += dhid pooled[b]^T, db1 += dhid, dw2 += dlogit[b][P] hid, db2 (fp64)
+            constexpr int WS = D + 1, DQ = D / 4;
+            static_assert(NT == 4 * HID, "four column quarters per hidden unit");
+            float* w1l = reinterpret_cast<float*>(smem);  // [HID][WS]
+            float* dhl = w1l + HID * WS;                   // [HID]
+            float* pl = dhl + HID;                         // [D]
+            for (int i = threadIdx.x; i < HID * D; i += NT) w1l[(i / D) * WS + (i % D)] = sc.nW1[i];
+            const int k = threadIdx.x % HID, dq = threadIdx.x / HID;
+            const float w2k = sc.nw2[k];
+            float dw1n[DQ];
+#pragma unroll
+            for (int d = 0; d < DQ; ++d) dw1n[d] = 0.f;
+            float db1n = 0.f, dw2n = 0.f;
+            double db2n = 0.0;
+            for (int64_t b = blockIdx.x; b < sc.B; b += gridDim.x) {
+                const float dout = dlogit[b * ldo + sc.P];
+                const float hk = sc.nhid[b * HID + k];
+                if (threadIdx.x < D) pl[threadIdx.x] = sc.pooled[b * D + threadIdx.x];
+                const float dhk = hk > 0.f ? dout * w2k * sc.nscale : 0.f;
+                if (dq == 0) {
+                    dhl[k] = dhk;
+                    db1n += dhk;
+                    dw2n = fmaf(dout, hk, dw2n);
+                    if (k == 0) db2n += static_cast<double>(dout);
+                }
+                __syncthreads();  // pl, dhl (and on the first pass w1l) visible
+#pragma unroll
+                for (int d = 0; d < DQ; ++d) dw1n[d] = fmaf(dhk, pl[dq * DQ + d], dw1n[d]);
+                if (threadIdx.x < D) {
+                    float sdp = 0.f;
+#pragma unroll 16
+                    for (int kk = 0; kk < HID; ++kk) sdp = fmaf(dhl[kk], w1l[kk * WS + threadIdx.x], sdp);
+                    const_cast<float*>(sc.dpool)[b * D + threadIdx.x] = sdp;  // read back by this workgroup's tiles
+                }
+                __syncthreads();
+            }
+            float* out = sc.nslab + static_cast<int64_t>(blockIdx.x) * (HID * D + 2 * HID);
+#pragma unroll
+            for (int d = 0; d < DQ; ++d) out[k * D + dq * DQ + d] = dw1n[d];
+            if (dq == 0) {
+                out[HID * D + k] = db1n;
+                out[HID * D + HID + k] = dw2n;
+            }
+            if (threadIdx.x == 0) sc.ndslab[blockIdx.x] = db2n;
+            __syncthreads();  // the LDS goes to the images
+        }
+    }
     uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);     // [NPL][TR][FTB]  feat parts
     uint16_t* gimg = fimg + NPL * G::FTPL;                   // [NPL][TR][GSB]  g parts
     int8_t* sgn = reinterpret_cast<int8_t*>(gimg + NPL * G::GPL);  // [2][TR][D]  sign(h_u - h_v), by tile parity
@@ -1128,10 +1189,15 @@ extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_
 
 namespace {
 
+struct PoolGrads {  // lg_heads_bwd_scatter: the NoLeakHead's weight gradients
+    float *dw1, *db1, *dw2, *db2;
+};
+
 int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const float* w2, const float* hid,
                   const float* dlogits, int64_t ldo, float* dpipe, float* dw1, float* db1, float* dw2, float* db2,
                   int64_t B, int64_t N, int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
-                  void* workspace, int64_t ws_bytes, lg_stream_t stream, const EdgeScatter* scat) {
+                  void* workspace, int64_t ws_bytes, lg_stream_t stream, const EdgeScatter* scat,
+                  const PoolGrads* pool = nullptr) {
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
     const int dropout = (flags & LG_F_DROPOUT) ? 1 : 0;
@@ -1193,7 +1259,11 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
     LG_RET_IF_LAUNCH_FAILED();
     const int64_t K3 = 3 * D;
     const LgSlabSeg segs[3] = {{0, HID * K3, dw1}, {HID * K3, HID, db1}, {HID * K3 + HID, HID, dw2}};
-    return lg_launch_slab_reduce_multi(slab, grid, SL, segs, 3, dslab, db2, s);
+    const int rc = lg_launch_slab_reduce_multi(slab, grid, SL, segs, 3, dslab, db2, s);
+    if (rc != LG_OK || !pool) return rc;
+    // the NoLeakHead's slab rows (lg_heads_bwd_scatter: written by the same grid's prologue)
+    const LgSlabSeg psegs[3] = {{0, HID * D, pool->dw1}, {HID * D, HID, pool->db1}, {HID * D + HID, HID, pool->dw2}};
+    return lg_launch_slab_reduce_multi(scat->nslab, grid, HID * D + 2 * HID, psegs, 3, scat->ndslab, pool->db2, s);
 }
 
 }  // namespace
@@ -1206,13 +1276,17 @@ extern "C" int lg_edge_head_bwd(const int64_t* ends, const float* h, const float
                          dropout_p, workspace, ws_bytes, stream, nullptr);
 }
 
-extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
-                                        const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
-                                        float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
-                                        const int32_t* inc_item, const int32_t* sched, const int32_t* sched_hdr,
-                                        const float* dpool, float* dh, int64_t B, int64_t N,
-                                        int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
-                                        void* workspace, int64_t ws_bytes, lg_stream_t stream) {
+namespace {
+// lg_edge_head_bwd_scatter; with `pool` (lg_heads_bwd_scatter) the STREAM form runs the
+// NoLeakHead backward in its prologue (its slab in pool_ws) and returns 1 when it did, 0 when
+// it took another form (the caller then runs lg_pool_head_bwd first: dpool is an input there)
+int edge_bwd_scatter_impl(const int64_t* ends, const float* h, const float* w1, const float* w2, const float* hid,
+                          const float* dlogits, int64_t ldo, float* dpipe, float* dw1, float* db1, float* dw2,
+                          float* db2, const int32_t* inc_rowptr, const int32_t* inc_item, const int32_t* sched,
+                          const int32_t* sched_hdr, const float* dpool, float* dh, int64_t B, int64_t N, int64_t P,
+                          int64_t D, int64_t hidden, int flags, float dropout_p, void* workspace, int64_t ws_bytes,
+                          lg_stream_t stream, const EdgeScatter* pool_sc, const PoolGrads* pool, bool* fused) {
+    if (fused) *fused = false;
     if (B < 0 || N <= 0 || P < 0) return LG_EINVAL;
     if (!dh || !inc_rowptr || (P > 0 && !inc_item)) return LG_EINVAL;
     if (!sched != !sched_hdr) return LG_EINVAL;
@@ -1231,10 +1305,22 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                        reinterpret_cast<const uint32_t*>(sched + sched_hdr[11]), sched + sched_hdr[12],
                        sched_hdr[9], sched_hdr[6], sched_hdr[8], sched_hdr[7], kEdgeLab(flags)};
         // STREAM when the open nodes' sums fit beside the images (L-TOWN-A at D = 64: 23 of them)
-        if (edge_stream_lds(D, flags, sc) <= 160 * 1024)
+        if (edge_stream_lds(D, flags, sc) <= 160 * 1024) {
+            if (pool_sc) {
+                sc.pooled = pool_sc->pooled;
+                sc.nhid = pool_sc->nhid;
+                sc.nW1 = pool_sc->nW1;
+                sc.nw2 = pool_sc->nw2;
+                sc.nscale = pool_sc->nscale;
+                sc.nslab = pool_sc->nslab;
+                sc.ndslab = pool_sc->ndslab;
+                if (fused) *fused = true;
+            }
             return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden,
-                                 flags, dropout_p, workspace, ws_bytes, stream, &sc);
+                                 flags, dropout_p, workspace, ws_bytes, stream, &sc, pool_sc ? pool : nullptr);
+        }
     }
+    if (pool_sc) return LG_OK;  // the caller runs the two-step form
     const int64_t base = edge_bwd_base_lds(D, flags);
     if (!per_window || P == 0 || base + 4 * (N + 1 + 2 * P) > 160 * 1024 || B * N >= kLgMaxRows) {
         // the incidence CSR does not fit beside the kernel's images: the separate scatter launch
@@ -1248,6 +1334,65 @@ extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, con
                    static_cast<int>(cdiv(P, tile_rows(D))), nullptr, nullptr, nullptr, 0, 0, 0, 0, kEdgeLab(flags)};
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
                          dropout_p, workspace, ws_bytes, stream, &sc);
+}
+}  // namespace
+
+extern "C" int lg_edge_head_bwd_scatter(const int64_t* ends, const float* h, const float* w1, const float* w2,
+                                        const float* hid, const float* dlogits, int64_t ldo, float* dpipe,
+                                        float* dw1, float* db1, float* dw2, float* db2, const int32_t* inc_rowptr,
+                                        const int32_t* inc_item, const int32_t* sched, const int32_t* sched_hdr,
+                                        const float* dpool, float* dh, int64_t B, int64_t N,
+                                        int64_t P, int64_t D, int64_t hidden, int flags, float dropout_p,
+                                        void* workspace, int64_t ws_bytes, lg_stream_t stream) {
+    return edge_bwd_scatter_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, inc_rowptr, inc_item,
+                                 sched, sched_hdr, dpool, dh, B, N, P, D, hidden, flags, dropout_p, workspace, ws_bytes,
+                                 stream, nullptr, nullptr, nullptr);
+}
+
+extern "C" int lg_heads_bwd_scatter(const float* pooled, const float* nhid, const float* nw1, const float* nw2,
+                                    float* ndw1, float* ndb1, float* ndw2, float* ndb2, int nflags, float n_dropout_p,
+                                    void* nworkspace, int64_t nws_bytes, const int64_t* ends, const float* h,
+                                    const float* w1, const float* w2, const float* hid, const float* dlogits,
+                                    int64_t ldo, float* dpipe, float* dw1, float* db1, float* dw2, float* db2,
+                                    const int32_t* inc_rowptr, const int32_t* inc_item, const int32_t* sched,
+                                    const int32_t* sched_hdr, float* dpool, float* dh, int64_t B, int64_t N, int64_t P,
+                                    int64_t D, int64_t hidden, int flags, float dropout_p, void* workspace,
+                                    int64_t ws_bytes, lg_stream_t stream) {
+    if (B < 0 || N <= 0 || P < 0 || ldo <= P) return LG_EINVAL;
+    if (hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
+    const bool ndrop = (nflags & LG_F_DROPOUT) != 0;
+    if (ndrop && !(n_dropout_p >= 0.f && n_dropout_p < 1.f)) return LG_EINVAL;
+    if (!nw1 || !nw2 || !ndw1 || !ndb1 || !ndw2 || !ndb2 || !nworkspace || !dpool) return LG_EINVAL;
+    if (B > 0 && (!pooled || !nhid)) return LG_EINVAL;
+    // the fused form writes one NoLeakHead slab row per workgroup of the edge grid (<= B, <= CUs),
+    // which lg_pool_head_bwd_workspace_bytes covers
+    const int64_t nwsb = lg_pool_head_bwd_workspace_bytes(B, D, hidden);
+    if (nwsb < 0) return static_cast<int>(nwsb);
+    if (nws_bytes < nwsb) return LG_EINVAL;
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(B, 2LL * lg_num_cus()));  // lg_pool_head_bwd's grid
+    EdgeScatter psc{};
+    psc.pooled = pooled;
+    psc.nhid = nhid;
+    psc.nW1 = nw1;
+    psc.nw2 = nw2;
+    psc.nscale = ndrop ? 1.0f / (1.0f - n_dropout_p) : 1.0f;
+    psc.nslab = static_cast<float*>(nworkspace);
+    psc.ndslab = reinterpret_cast<double*>(static_cast<char*>(nworkspace) + ((G * (HID * D + 2 * HID) * 4 + 255) & ~int64_t(255)));
+    const PoolGrads pg{ndw1, ndb1, ndw2, ndb2};
+    if (B > 0) {
+        bool fused = false;
+        const int rc = edge_bwd_scatter_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, inc_rowptr,
+                                             inc_item, sched, sched_hdr, dpool, dh, B, N, P, D, hidden, flags,
+                                             dropout_p, workspace, ws_bytes, stream, &psc, &pg, &fused);
+        if (rc != LG_OK || fused) return rc;
+    }
+    // another form: the NoLeakHead backward first (its dpool is the scatter's input)
+    const int rc = lg_pool_head_bwd(pooled, nhid, nw1, nw2, dlogits, ldo, P, dpool, ndw1, ndb1, ndw2, ndb2, B, D, hidden,
+                                    nflags, n_dropout_p, nworkspace, nws_bytes, stream);
+    if (rc != LG_OK) return rc;
+    return lg_edge_head_bwd_scatter(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, inc_rowptr, inc_item,
+                                    sched, sched_hdr, dpool, dh, B, N, P, D, hidden, flags, dropout_p, workspace,
+                                    ws_bytes, stream);
 }
 
 /* ---------------------------------------------------------------------------------------------

@@ -99,6 +99,9 @@ SIGNATURES = {
                                 _u32, _p]),
     "lg_pool_head_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64]),
     "lg_pool_head_bwd": (_i32, [_p, _p, _p, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
+    "lg_heads_bwd_scatter": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _i32, _f32, _p, _i64,
+                                    _p, _p, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                    _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p, _i64, _p]),
     "lg_gru_fwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p]),
     "lg_gru_bwd_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "lg_gru_bwd": (_i32, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _p]),

@@ -898,14 +898,18 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
     return dh, dw1, db1, dw2, db2, ndw1, ndb1, ndw2, ndb2
 
 
-# True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter: streamed
-# per tile with a pipe schedule, else per window); False: two launches (lg_edge_head_bwd +
-# lg_pipe_scatter_bwd).  Same node gradient bit for bit (one incidence order for all).
-# Measured at B = 256: fused 152.6 us, step 0.659 ms (profiles/r03/r03al); two launches
-# 114.6 + 35.3 us, step 0.662 ms (r03am) -- equal within box-to-box noise.  With one window
-# per workgroup every workgroup reaches its scatter at the same time, after its MFMA work, so
-# the scatter's traffic overlaps nothing; the fused form saves the launch.
+# True: the pipe scatter fused into the EdgeHead backward (lg_edge_head_bwd_scatter): with the
+# pipe schedule (ABI 22, the default at B >= the CU count) the node sums are STREAMED tile by
+# tile from the dfeat rows in LDS, so no per-pipe row reaches HBM; without one, per window
+# after its last tile (ABI 19).  False: two launches (lg_edge_head_bwd + lg_pipe_scatter_bwd).
+# Same node gradient bit for bit (one incidence order for all;
+# tests/test_gpu_library.py::test_fused_pipe_scatter_matches_two_launches).  Measured at
+# B = 256 (DESIGN §3 "Round 4"): streamed 125-132 us in the step (profiles/r04/r04z3), against
+# 152.6 us for the per-window form and 114.6 + 35.3 us for the two launches (round 3).
 _FUSED_SCATTER = True
+# True: with the streamed scatter, the NoLeakHead backward runs in the EdgeHead backward's
+# prologue (lg_heads_bwd_scatter: one launch for both heads); False: lg_pool_head_bwd first
+_FUSED_HEADS = True
 
 
 def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, ends, inc_rowptr, inc_item, sched,
@@ -915,11 +919,22 @@ def _heads_backward_launches(lib, dl, h, w1, w2, ehid, pooled, hid, nw1, nw2, en
     with the incidence scatter fused in (lg_edge_head_bwd_scatter): dh complete."""
     dev = h.device
     dpooled = torch.empty(B, D, device=dev)
+    lay = fe & nat.LG_F_NODE_MAJOR
+    if _FUSED_SCATTER and _FUSED_HEADS:
+        # both heads in one launch where the streamed form applies (else the two calls inside)
+        with _timed("edge_bwd", dev):
+            hdr = (ctypes.c_int32 * 16)(*sched_hdr) if (sched is not None and sched_hdr) else None
+            check(lib.lg_heads_bwd_scatter(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(ndw1), ptr(ndb1), ptr(ndw2),
+                                           ptr(ndb2), fn, p_noleak, ptr(wsn), wsn.numel(), ptr(ends), ptr(h), ptr(w1),
+                                           ptr(w2), ptr(ehid), ptr(dl), P + 1, ptr(dpipe), ptr(dw1), ptr(db1), ptr(dw2),
+                                           ptr(db2), ptr(inc_rowptr), ptr(inc_item), ptr(sched) if hdr else None, hdr,
+                                           ptr(dpooled), ptr(dh), B, N, P, D, hidden, fe, p_edge, ptr(ws), ws.numel(),
+                                           st), "lg_heads_bwd_scatter")
+        return
     with _timed("pool_head_bwd", dev):
         check(lib.lg_pool_head_bwd(ptr(pooled), ptr(hid), ptr(nw1), ptr(nw2), ptr(dl), P + 1, P, ptr(dpooled),
                                    ptr(ndw1), ptr(ndb1), ptr(ndw2), ptr(ndb2), B, D, nhidden, fn, p_noleak, ptr(wsn), wsn.numel(),
                                    st), "lg_pool_head_bwd")
-    lay = fe & nat.LG_F_NODE_MAJOR
     if _FUSED_SCATTER:
         with _timed("edge_bwd", dev):
             hdr = (ctypes.c_int32 * 16)(*sched_hdr) if (sched is not None and sched_hdr) else None

@@ -310,8 +310,10 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
     """lg_edge_head_bwd_scatter (the incidence scatter fused into the EdgeHead backward, one
     workgroup per window) against lg_edge_head_bwd + lg_pipe_scatter_bwd: the node gradient
     is the same sums in the same order, so every gradient upstream of it (trunk, GRU, sensor
-    projection, NoLeakHead) is bitwise equal; the EdgeHead's weight gradients change only by
-    the slab grouping of the fixed-order reduction (window-owned tiles).  The fused forms run
+    projection) is bitwise equal; the EdgeHead's weight gradients change only by the slab
+    grouping of the fixed-order reduction (window-owned tiles), and so do the NoLeakHead's when
+    its backward runs in the streamed launch's prologue (lg_heads_bwd_scatter: windows grouped
+    by the edge grid, one per CU, instead of lg_pool_head_bwd's two per CU).  The fused forms run
     a workgroup per window, so only from B = CUs (256 on MI355X) on; below it the call is the
     two launches itself (B = 3: window-major trunk; 64: node-major).  256: the streamed scatter
     (pipe schedule); 300: more windows than CUs (several windows per workgroup); 6 pipes (the
@@ -339,10 +341,43 @@ def test_fused_pipe_scatter_matches_two_launches(B, npipes):
         grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
     for n, g in grads[0].items():
         ref = grads[1][n]
-        if n.startswith("edge_head."):
+        if n.startswith("edge_head.") or n.startswith("noleak_head."):
             assert_close(g, ref, rtol=1e-5, atol=1e-6 * ref.abs().max().item(), what=n)
         else:
             assert torch.equal(g, ref), f"{n}: fused scatter differs"
+
+
+@pytest.mark.parametrize("B", [256, 300])
+def test_fused_heads_backward_matches_separate(B):
+    """lg_heads_bwd_scatter (the NoLeakHead backward in the streamed EdgeHead backward's
+    prologue) against lg_pool_head_bwd + lg_edge_head_bwd_scatter: dpool per window is the same
+    sum in the same order, so every gradient but the NoLeakHead's weights is bitwise equal; those
+    are bitwise equal at B = 256 (a window per workgroup in both grids) and within rounding at
+    B = 300 (windows grouped differently into slab rows)."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    torch.manual_seed(6)
+    m = LeakDetector(LTA_INP, sensors, pipes).to(DEV).train()
+    r = torch.randn(B, 36, 29, device=DEV)
+    tf = torch.randn(B, 36, 9, device=DEV)
+    grads = []
+    saved = library._FUSED_HEADS
+    for fused in (True, False):
+        library._FUSED_HEADS = fused
+        try:
+            m.zero_grad(set_to_none=True)
+            torch.manual_seed(18)
+            m(r, tf).square().mean().backward()
+            torch.cuda.synchronize()
+        finally:
+            library._FUSED_HEADS = saved
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    for n, g in grads[0].items():
+        ref = grads[1][n]
+        if n.startswith("noleak_head.") and B != 256:
+            assert_close(g, ref, rtol=1e-5, atol=1e-6 * ref.abs().max().item(), what=n)
+        else:
+            assert torch.equal(g, ref), f"{n}: fused heads backward differs"
 
 
 @pytest.mark.parametrize("D", [64, 32])

@@ -171,6 +171,8 @@ def test_undersized_workspace_returns_einval():
                                             lib.lg_edge_head_bwd_workspace_bytes(B, P, D2, 128) - 1, None) == -1
     wsp = lib.lg_pool_head_bwd_workspace_bytes(B, D, 128)
     assert lib.lg_pool_head_bwd(F, F, F, F, F, P + 1, P, F, F, F, F, F, B, D, 128, 0, 0.0, F, wsp - 1, None) == -1
+    hargs = (F, F, F, F, F, F, P + 1, F, F, F, F, F, F, F, None, None, F, F, B, N, P, D, 128, 0x20, 0.0, F, wse, None)
+    assert lib.lg_heads_bwd_scatter(F, F, F, F, F, F, F, F, 0, 0.0, F, wsp - 1, *hargs) == -1
     wsg = lib.lg_gru_bwd_workspace_bytes(B, S, 10, 64)
     assert lib.lg_gru_bwd(F, F, F, F, F, F, F, None, F, F, F, F, B, 36, S, 10, 64, F, wsg // 2 - 1, None) == -1
     wss = lib.lg_sensor_proj_bwd_workspace_bytes(B, S, D, D)
