@@ -625,8 +625,8 @@ int lg_gru_bwd(const float* residual, const float* tfeat, const float* w_ih, con
  * the mask column, sensor_to_node, ReLU, dropout) when node_hidden == sensor_hidden == H.
  *   fwd: lg_gru_fwd's outputs, plus xs0 [S][B][H] and x0bits exactly as lg_node_init_bits_fwd
  *        writes them from h_last (W = proj_w [H][H + 1], bias = node_bias, dropout stream =
- *        (seed, salt)), except that the sensor nodes' words of x0bits are left unwritten (no
- *        reader: lg_gcn_fwd_nm_x0 / lg_gcn_bwd_nm_x0 take those rows from xs0).  One launch.
+ *        (seed, salt)), except that the sensor nodes' words of x0bits are 0 (no reader:
+ *        lg_gcn_fwd_nm_x0 / lg_gcn_bwd_nm_x0 take those rows from xs0).  One launch.
  *   bwd: lg_gru_bwd without dx, its dh_last formed in the launch from the node init's
  *        pre-activation gradient, as lg_sensor_proj_bwd does: dx0 is node-major [N][B][H] (the
  *        sensor nodes' rows: lg_gcn_bwd_nm_x0 with LG_F_DX_SENSOR_ROWS), live [S] (may be NULL);

@@ -317,12 +317,11 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
         const uint32_t words = ni.N * ni.ngroups * 64u, stride = gridDim.x * blockDim.x;
         for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
             const uint32_t t = e >> 6, n = lg_div(t, ni.fdG), gg = t - n * ni.ngroups;
-            if (ni.slot[n] >= 0) continue;  // a sensor node's tile: never read
-            uint32_t wd = 0;
+            uint32_t wd = 0;  // a sensor node's tile: never read, written 0 (a deterministic output)
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint32_t b = 16 * gg + RPI * k + rl;
-                if (b < ni.B) {
+                if (b < ni.B && ni.slot[n] < 0) {
                     const uint32_t kb =
                         ni.dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * ni.N + n, 4 * fg, thr) : 0xFu;
                     wd |= (kb & pos) << (4 * k);
@@ -1070,8 +1069,10 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         dwx[1] *= fx;
     }
 
-    // per-workgroup slab (the layout of k_gru_bwd): C rows = gate rows 16w + 4q + reg, columns j
-    float* out = slab + static_cast<int64_t>(blockIdx.x) * SLAB;
+    // per-workgroup slab (the layout of k_gru_bwd): C rows = gate rows 16w + 4q + reg, columns j;
+    // NI: each row then carries the projection's dW and db (lg_gru_node_init_bwd_workspace_bytes)
+    constexpr int SLROW = SLAB + (NI ? H * (H + 1) + H : 0);
+    float* out = slab + static_cast<int64_t>(blockIdx.x) * SLROW;
     float* oWhh = out;
     float* oWih = out + G3 * H;
     float* obih = oWih + G3 * I;

@@ -563,8 +563,9 @@ def _trunk_layer_launches(lib, dy, xs, ymask, weights, sensor_slot, nodetab_t, p
         db = torch.empty(D, device=dev, dtype=torch.float32)
         slot_p, dbias_p = (ptr(sensor_slot), ptr(dbias_ns)) if l == 0 else (None, None)
         with _timed("gcn_bwd" if l == L - 1 else f"gcn_bwd_l{l}", dev):
-            if x0c is not None and l == 0:  # the compressed node init (xs[0]: its sensor rows)
+            if x0c is not None and l == 0:  # the compressed node init (xs[0]: its sensor rows, (S, B, D))
                 x0bits, node_bias, pos_slot_t = x0c
+                S = xs[0].shape[0]
                 check(lib.lg_gcn_bwd_nm_x0(ptr(nodetab_t), ptr(pairs_t), ptr(pos_slot_t), ptr(dy), ptr(xs[0]),
                                            ptr(x0bits), ptr(node_bias), ptr(weights[0]), ptr(dx), ptr(dW), ptr(db),
                                            slot_p, dbias_p, B, N, S, D, flags | (nat.LG_F_DROPOUT if p > 0.0 else 0),
