@@ -785,7 +785,26 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, nbv(cur.p[i].x, pf[b][i], pb[b][X0 ? i : 0], k));
                 }
             }
-            if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
+            // the rest of the row (degree > NPF).  Dense input with at most kLgNmInline entries: its
+            // blocks are added by the CONSUMER (entries listed in the ring slot's metadata), so the
+            // producer's round does not wait a memory round trip for them (32 % of L-TOWN-A's nodes);
+            // the sums run in the same order, so y is bit-identical
+            uint32_t nrest = 0;
+            if constexpr (!X0) {
+                if (e0 + NPF < e1 && e1 - e0 <= kLgNmInline) nrest = static_cast<uint32_t>(e1 - e0 - NPF);
+            }
+            if (e0 + NPF < e1 && nrest == 0 && !X0) {  // over kLgNmInline entries: here, one block at a time
+                for (int e = e0 + NPF; e < e1; ++e) {
+                    const int2 pa = pairs[e];
+                    f32x4 vr[G::K];
+                    uint32_t vw;
+                    load_nb(pa.x, true, b0, lo[b], vr, vw);
+                    const float wa = __int_as_float(pa.y);
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vr, vw, k));
+                }
+            }
+            if (X0 && e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
                 constexpr int NI = kLgNmInline - NPF;
                 f32x4 va[NI][G::K];
                 uint32_t vb[NI];
@@ -846,6 +865,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     m[7] = sw1;
                     m[8] = ss2;
                     m[9] = sw2;
+                } else {  // the entries the consumer adds (kLgNmInline - NPF at most)
+                    static_assert(4 + 2 * (kLgNmInline - NPF) <= kPcMeta, "rest entries fit the metadata");
+                    m[3] = nrest;
+#pragma unroll
+                    for (int i = 0; i < kLgNmInline - NPF; ++i) {
+                        m[4 + 2 * i] = static_cast<uint32_t>(cur.p[NPF + i].x);
+                        m[5 + 2 * i] = static_cast<uint32_t>(cur.p[NPF + i].y);
+                    }
                 }
             }
             pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
@@ -884,7 +911,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     // ---------------- consumer: transform + epilogue
     const __amdgpu_buffer_rsrc_t yrs = nm_rsrc(y, bytes);
-    const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : 0);  // X0: xs0
+    // X0: xs0 (the sensor rows); else x (the rest-of-row blocks)
+    const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : bytes);
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];
 #pragma unroll
@@ -960,6 +988,27 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             } else {
                 for (uint32_t i = 0; i < ns; ++i)
                     addrow(__builtin_amdgcn_readfirstlane(m[4 + 2 * i]), __uint_as_float(__builtin_amdgcn_readfirstlane(m[5 + 2 * i])));
+            }
+        }
+        if constexpr (!X0) {  // the row's entries past NPF, in entry order (the producer's own sum order)
+            const uint32_t nr = __builtin_amdgcn_readfirstlane(m[3]);
+            for (uint32_t i = 0; i < nr; ++i) {
+                const uint32_t c = __builtin_amdgcn_readfirstlane(m[4 + 2 * i]);
+                const float wv = __uint_as_float(__builtin_amdgcn_readfirstlane(m[5 + 2 * i]));
+                f32x4 v[KS][2];
+#pragma unroll
+                for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t off = static_cast<uint32_t>(j) < nb
+                                                 ? ((c * B + b0 + j) * D + 4 * (8 * s2 + 2 * q + h)) * 4u
+                                                 : kNm3RowOob;
+                        v[s2][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0));
+                    }
+#pragma unroll
+                for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) pk_fma4(bq[s2][h], wv, v[s2][h]);
             }
         }
         uint32_t st = 0;

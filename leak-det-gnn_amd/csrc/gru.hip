@@ -198,6 +198,33 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     }
     __shared__ __attribute__((aligned(16))) float bhn[H];  // b_hn (n waves add it to W_hn h)
     for (int i = threadIdx.x; i < H; i += blockDim.x) bhn[i] = bhh[2 * H + i];
+    // NI: W^T [H][D] and W[o][H] + bias[o], staged now (their loads overlap the first x chunk's),
+    // read by the epilogue
+    __shared__ __attribute__((aligned(16))) float niw[NI ? H * H + H : 1];
+    if constexpr (NI) {
+        constexpr int D = H, NW1 = D * (H + 1), NTT = 12 * H, PER = (NW1 + NTT - 1) / NTT;
+        float v[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = u * NTT + static_cast<int>(threadIdx.x);
+            v[u] = i < NW1 ? ni.W[i] : 0.f;
+        }
+        float bo[PER];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = u * NTT + static_cast<int>(threadIdx.x);
+            bo[u] = (i < NW1 && i % (H + 1) == H) ? ni.bias[i / (H + 1)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = u * NTT + static_cast<int>(threadIdx.x);
+            if (i < NW1) {
+                const int o = i / (H + 1), k = i - o * (H + 1);
+                if (k < H) niw[k * D + o] = v[u];
+                else niw[H * D + o] = v[u] + bo[u];  // the constant-1 column's weight + the bias
+            }
+        }
+    }
     f32x4 hcur = zero4();  // n waves: h of units 16u + 4q + reg, fp32
     if (g == 2) {  // h_{-1} = 0 (published by the first staging barrier)
         lg_u32x2* dst = reinterpret_cast<lg_u32x2*>(&hbs[0][u >> 1][lane]) + (u & 1);
@@ -267,17 +294,11 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hcur);
     if constexpr (NI) {
         constexpr int D = H, LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI, HS = H + 4;
-        static_assert(TS * HS + H * D + D <= LC * TS * XR, "node-init staging fits the x buffer");
+        static_assert(TS * HS <= LC * TS * XR, "node-init staging fits the x buffer");
         float* hl = xs;             // [TS][HS] h_L of the block's sequences (fp32)
-        float* wt = xs + TS * HS;   // W^T [H][D]
-        float* bfv = wt + H * D;    // [D] W[o][H] + bias[o]
+        const float* wt = niw;      // W^T [H][D] (staged at the start)
+        const float* bfv = niw + H * D;  // [D] W[o][H] + bias[o]
         __syncthreads();            // the last step's reads of xs are done
-        for (int i = threadIdx.x; i < D * (H + 1); i += blockDim.x) {
-            const int o = i / (H + 1), k = i - o * (H + 1);
-            const float v = ni.W[i];
-            if (k < H) wt[k * D + o] = v;
-            else bfv[o] = v + ni.bias[o];  // the constant-1 column's weight + the bias
-        }
         if (g == 2) st4(hl + j * HS + 16 * u + 4 * q, hcur);
         __syncthreads();
         const uint32_t key = ni.dropout ? lg_dropout_key_dev(ni.seed, ni.salt) : 0u;
@@ -826,9 +847,17 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
         float* wl = reinterpret_cast<float*>(&dgs[0][0][0][0]);
         float* dpl = wl + D * H;  // [TS2][DP]
         static_assert(sizeof(dgs) >= sizeof(float) * (D * H + TS2 * DP), "staging fits the dG image");
-        for (int i = threadIdx.x; i < D * H; i += G::NTH) {
-            const int o = i / H, k = i - o * H;
-            wl[i] = ni.W[o * (H + 1) + k];
+        static_assert((D * H) % G::NTH == 0, "W staging: whole rounds");
+        {
+            constexpr int PER = D * H / G::NTH;
+            float v[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {  // every load in flight before the first store
+                const int i = u * G::NTH + static_cast<int>(threadIdx.x), o = i / H, k = i - o * H;
+                v[u] = ni.W[o * (H + 1) + k];
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u) wl[u * G::NTH + threadIdx.x] = v[u];
         }
         for (int i = threadIdx.x; i < TS2 * (D / 4); i += G::NTH) {
             const int rr = i / (D / 4), c4 = 4 * (i % (D / 4));
