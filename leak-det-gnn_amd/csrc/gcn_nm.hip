@@ -503,6 +503,14 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #define LG_PC_NPF 3
 #endif
 constexpr int kPcRing = LG_PC_RING;
+// 1: the consumer waves load W's fragments straight from global memory (L2-resident) and the
+// producers start gathering at once; 0 (lab A/B): the round-3 prologue, W staged in LDS by the
+// whole workgroup behind a barrier every wave waits at (probe, r05a: ~1.3 us before the first
+// producer load)
+#ifndef LG_PC_WREG
+#define LG_PC_WREG 1
+#endif
+constexpr bool kPcWreg = LG_PC_WREG != 0;
 // ring-slot metadata: n, b0, nb, X0's sensor entries (count, then up to kPcSens (slot, w) pairs)
 constexpr int kPcSens = 3;
 constexpr int kPcMeta = 16;
@@ -632,8 +640,13 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         nb = valid ? min(16u, B - b0) : 0u;
     };
 
-    // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|)
-    {
+    // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|); with
+    // kPcWreg only the hand-off counters are set here (the consumers load W themselves)
+    if constexpr (kPcWreg) {
+        if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
+        if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
+        if (threadIdx.x == 0) *ctr = 0u;
+    } else {
         constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT;
         f32x4 wv[WPER];
 #pragma unroll
@@ -785,26 +798,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], w, nbv(cur.p[i].x, pf[b][i], pb[b][X0 ? i : 0], k));
                 }
             }
-            // the rest of the row (degree > NPF).  Dense input with at most kLgNmInline entries: its
-            // blocks are added by the CONSUMER (entries listed in the ring slot's metadata), so the
-            // producer's round does not wait a memory round trip for them (32 % of L-TOWN-A's nodes);
-            // the sums run in the same order, so y is bit-identical
-            uint32_t nrest = 0;
-            if constexpr (!X0) {
-                if (e0 + NPF < e1 && e1 - e0 <= kLgNmInline) nrest = static_cast<uint32_t>(e1 - e0 - NPF);
-            }
-            if (e0 + NPF < e1 && nrest == 0 && !X0) {  // over kLgNmInline entries: here, one block at a time
-                for (int e = e0 + NPF; e < e1; ++e) {
-                    const int2 pa = pairs[e];
-                    f32x4 vr[G::K];
-                    uint32_t vw;
-                    load_nb(pa.x, true, b0, lo[b], vr, vw);
-                    const float wa = __int_as_float(pa.y);
-#pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vr, vw, k));
-                }
-            }
-            if (X0 && e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
+            if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
                 constexpr int NI = kLgNmInline - NPF;
                 f32x4 va[NI][G::K];
                 uint32_t vb[NI];
@@ -865,14 +859,6 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     m[7] = sw1;
                     m[8] = ss2;
                     m[9] = sw2;
-                } else {  // the entries the consumer adds (kLgNmInline - NPF at most)
-                    static_assert(4 + 2 * (kLgNmInline - NPF) <= kPcMeta, "rest entries fit the metadata");
-                    m[3] = nrest;
-#pragma unroll
-                    for (int i = 0; i < kLgNmInline - NPF; ++i) {
-                        m[4 + 2 * i] = static_cast<uint32_t>(cur.p[NPF + i].x);
-                        m[5 + 2 * i] = static_cast<uint32_t>(cur.p[NPF + i].y);
-                    }
                 }
             }
             pc_store_rel(&ready[prod], static_cast<uint32_t>(t + 1));
@@ -911,14 +897,45 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     // ---------------- consumer: transform + epilogue
     const __amdgpu_buffer_rsrc_t yrs = nm_rsrc(y, bytes);
-    // X0: xs0 (the sensor rows); else x (the rest-of-row blocks)
-    const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : bytes);
+    const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : 0);  // X0: xs0
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
     uint32_t loff[G::K];
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
     int sw = 0;  // F16: W's scale exponent
-    if constexpr (F16) {
+    // kPcWreg: this wave's W fragments (all of W: rows 16 mt + j, columns 32 s2 + 8 q .. + 7) from
+    // global memory, times fold, rounded before any split; every consumer wave holds the whole
+    // matrix, so its own max |W| is the workgroup's.  The bias * fold row goes to LDS (each wave
+    // writes the same values; a lane reads back what a lane of its own wave wrote)
+    f32x4 wgl[G::CH][KS][2];
+    if constexpr (kPcWreg) {
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                const float* wp = W + (16 * mt + j) * D + 32 * s2 + 8 * q;
+                wgl[mt][s2][0] = ld4(wp);
+                wgl[mt][s2][1] = ld4(wp + 4);
+            }
+        if (lane < D / 4) {
+            f32x4 bb = bias ? ld4(bias + 4 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
+            st4(wst + D * LY::WS + 4 * lane, bb * fold);
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt)
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    f32x4 w = wgl[mt][s2][h] * fold;
+                    asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
+                    wgl[mt][s2][h] = w;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(w[c])));
+                }
+        if constexpr (F16) sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(lg_wave_max_bits(m)));
+    } else if constexpr (F16) {
         uint32_t m = 0;
         for (int w = 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
         sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
@@ -930,13 +947,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
             const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
+            const f32x4 wa = kPcWreg ? wgl[mt][s2][0] : ld4(wp), wb = kPcWreg ? wgl[mt][s2][1] : ld4(wp + 4);
             if constexpr (F16) {
                 const float sc2 = lg_pow2f(sw);
-                split2_f16_x8(ld4(wp) * sc2, ld4(wp + 4) * sc2, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
+                split2_f16_x8(wa * sc2, wb * sc2, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
                 continue;
             }
             lg_bf16x8 f0, f1, f2;
-            split3_x8(ld4(wp), ld4(wp + 4), f0, f1, f2);
+            split3_x8(wa, wb, f0, f1, f2);
             wf[0][mt][s2] = f0;
             if constexpr (!BF) {
                 wf[NP > 1 ? 1 : 0][mt][s2] = f1;
@@ -988,27 +1006,6 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             } else {
                 for (uint32_t i = 0; i < ns; ++i)
                     addrow(__builtin_amdgcn_readfirstlane(m[4 + 2 * i]), __uint_as_float(__builtin_amdgcn_readfirstlane(m[5 + 2 * i])));
-            }
-        }
-        if constexpr (!X0) {  // the row's entries past NPF, in entry order (the producer's own sum order)
-            const uint32_t nr = __builtin_amdgcn_readfirstlane(m[3]);
-            for (uint32_t i = 0; i < nr; ++i) {
-                const uint32_t c = __builtin_amdgcn_readfirstlane(m[4 + 2 * i]);
-                const float wv = __uint_as_float(__builtin_amdgcn_readfirstlane(m[5 + 2 * i]));
-                f32x4 v[KS][2];
-#pragma unroll
-                for (int s2 = 0; s2 < KS; ++s2)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t off = static_cast<uint32_t>(j) < nb
-                                                 ? ((c * B + b0 + j) * D + 4 * (8 * s2 + 2 * q + h)) * 4u
-                                                 : kNm3RowOob;
-                        v[s2][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 0));
-                    }
-#pragma unroll
-                for (int s2 = 0; s2 < KS; ++s2)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) pk_fma4(bq[s2][h], wv, v[s2][h]);
             }
         }
         uint32_t st = 0;
