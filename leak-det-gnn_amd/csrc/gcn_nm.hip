@@ -503,12 +503,21 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #define LG_PC_NPF 3
 #endif
 constexpr int kPcRing = LG_PC_RING;
-// 1: the consumer waves load W's fragments straight from global memory (L2-resident) and the
-// producers start gathering at once; 0 (lab A/B): the round-3 prologue, W staged in LDS by the
-// whole workgroup behind a barrier every wave waits at (probe, r05a: ~1.3 us before the first
-// producer load)
+// 1 (lab A/B): the consumer waves load W's fragments straight from global memory (L2-resident)
+// and the producers start gathering without the W staging barrier.  Measured and dropped
+// (r05f, B = 256 train mode, isolated): 21.96 us against 19.73 for the staged prologue (0, the
+// default) — the per-wave W loads (16 KB per consumer wave) delay every consumer's first tile,
+// and the producers' start is set by the workgroups' dispatch spread (~1.4 us), not the barrier
 #ifndef LG_PC_WREG
-#define LG_PC_WREG 1
+#define LG_PC_WREG 0
+#endif
+// 1 (lab A/B): a producer draws tile t + 3 and requests its node-table record while it
+// accumulates tile t (the record of tile t + 2, drawn one step earlier, has landed by the time
+// t + 2's loads are issued); 0 (default): tile t + 2 drawn and its record requested in step t.
+// Measured and dropped (r05g, isolated train mode): 22.5-22.8 us against 20.3-21.4 — the
+// held record costs 16 SGPRs and the kernel spills 31 of them (10 without)
+#ifndef LG_PC_RECAHEAD
+#define LG_PC_RECAHEAD 0
 #endif
 constexpr bool kPcWreg = LG_PC_WREG != 0;
 // ring-slot metadata: n, b0, nb, X0's sensor entries (count, then up to kPcSens (slot, w) pairs)
@@ -751,6 +760,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             return sc.first + static_cast<int64_t>(i) * sc.stride;
         };
         int64_t tl[2];  // the tile whose blocks are in flight in buffer b
+        int64_t ptile = 0;  // LG_PC_RECAHEAD: the next tile drawn, its record requested
+        NmRec prec{};
         // r: the tile's node-table record (schedule section: slot -> record with its node id),
         // requested by the caller a phase earlier
         auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
@@ -774,11 +785,23 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             const int64_t tile = tl[b];
             if (tile >= tend) return false;
             // the producer's tile t + 2 is drawn, and its record goes in flight while this tile is
-            // accumulated
+            // accumulated (LG_PC_RECAHEAD: tile t + 2 and its record came from step t - 1; tile
+            // t + 3 is drawn now)
+#if LG_PC_RECAHEAD
+            const int64_t tnext = ptile;
+            const NmRec nxt = prec;
+            {
+                ptile = grab();
+                uint32_t pn, pb0, pnb;
+                tile_coords(ptile, pn, pb0, pnb);
+                prec = nm_rec(tab, N + pn);
+            }
+#else
             const int64_t tnext = grab();
             uint32_t nn, nb0, nnb;
             tile_coords(tnext, nn, nb0, nnb);
             const NmRec nxt = nm_rec(tab, N + nn);
+#endif
             asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
             const NmRec& cur = rec[b];
             const int e0 = cur.e0, e1 = cur.e1;
@@ -875,6 +898,12 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
             issue(std::integral_constant<int, 0>{}, r0, f0);
             issue(std::integral_constant<int, 1>{}, r1, f1);
+#if LG_PC_RECAHEAD
+            ptile = grab();
+            uint32_t pn, pb0, pnb;
+            tile_coords(ptile, pn, pb0, pnb);
+            prec = nm_rec(tab, N + pn);
+#endif
         }
         int64_t t = 0;
         for (;; t += 2) {

@@ -131,9 +131,12 @@ __device__ __forceinline__ void split2_pair_mix(float a, float b, uint32_t& p0, 
 //   xs0[s][b] = dropout(relu([h_L, 1] W^T + b))     for the slot's node if s is its live slot
 // with the arithmetic of k_node_init_bits (heads.hip: W^T staged in LDS, the ascending-k fmaf
 // chain, the same row-stream dropout), so xs0 is bit-identical to lg_node_init_bits_fwd's; and
-// every block writes a grid-strided share of the NON-sensor tiles' [x0 > 0] words (the bias
-// sign and the dropout stream alone; the sensor tiles' words are never read: layer 0 takes
-// those nodes' rows from xs0).  Node init and its launch leave the step.
+// the NON-sensor tiles' [x0 > 0] words (the bias sign and the dropout stream alone; the sensor
+// tiles' words are never read: layer 0 takes those nodes' rows from xs0) are written by extra
+// workgroups past the sequence blocks (GruNi::nseqblk), which need nothing from the recurrence:
+// they fill the CU slots the sequence blocks leave free (48 of 512 at B = 256) and run beside
+// the serial loop instead of after it (r05d: every block's grid-strided share in the epilogue,
+// the fused forward 92.8 us in the step).  Node init and its launch leave the step.
 struct GruNi {
     const int32_t* slot;  // [N] node -> its live sensor slot, or -1
     const int64_t* sidx;  // [S] slot -> node
@@ -147,7 +150,41 @@ struct GruNi {
     float p, scale;
     uint64_t seed;
     uint32_t salt;
+    uint32_t nseqblk;     // blocks [0, nseqblk) run the GRU, the rest write the bits words
 };
+
+// [x0 > 0] words of the non-sensor tiles, block `blk` of `nblk` (D = H)
+template <int H>
+__device__ __forceinline__ void gru_ni_bits(const GruNi& ni, uint32_t blk, uint32_t nblk) {
+    constexpr int D = H, LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI;
+    const uint32_t key = ni.dropout ? lg_dropout_key_dev(ni.seed, ni.salt) : 0u;
+    const uint32_t thr = lg_keep_threshold16(ni.p);
+    const float vs = ni.dropout ? ni.scale : 1.0f;
+    // one lane word per thread (blockDim.x is a multiple of 64, so a thread keeps its lane and
+    // its four channels over the stride)
+    const uint32_t l = threadIdx.x & 63, rl = l / LPR, fg = l % LPR;
+    const f32x4 bv = ld4(ni.bias + 4 * fg);
+    uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * vs > 0.f) << i;
+    const uint32_t words = ni.N * ni.ngroups * 64u, stride = nblk * blockDim.x;
+    for (uint32_t e = blk * blockDim.x + threadIdx.x; e < words; e += stride) {
+        const uint32_t t = e >> 6, n = lg_div(t, ni.fdG), gg = t - n * ni.ngroups;
+        uint32_t wd = 0;  // a sensor node's tile: never read, written 0 (a deterministic output)
+        if (ni.slot[n] < 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t b = 16 * gg + RPI * k + rl;
+                if (b < ni.B) {
+                    const uint32_t kb =
+                        ni.dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * ni.N + n, 4 * fg, thr) : 0xFu;
+                    wd |= (kb & pos) << (4 * k);
+                }
+            }
+        }
+        ni.bits[e] = static_cast<uint16_t>(wd);
+    }
+}
 
 // gates (optional) [L][Nseq][4][H]: r, z, n, W_hn h_{t-1} + b_hn
 template <int H, bool UT, bool SAVE, bool NI = false>
@@ -158,6 +195,12 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
           lg_fastdiv fdS, GruNi ni) {
     constexpr int NU = H / 16, NC = H / 32, I = UT ? 10 : 1;
     constexpr int LC = H == 64 ? kLC : 30;  // H = 32: four workgroups per CU fit in LDS
+    if constexpr (NI) {
+        if (blockIdx.x >= ni.nseqblk) {  // a bits block (uniform: before any barrier)
+            gru_ni_bits<H>(ni, blockIdx.x - ni.nseqblk, gridDim.x - ni.nseqblk);
+            return;
+        }
+    }
     __shared__ __attribute__((aligned(16))) float xs[LC * TS * XR];
     __shared__ __attribute__((aligned(16))) f32x4 grz[2][NU][64];   // [r|z][unit group][lane]: sigma tiles
     __shared__ __attribute__((aligned(16))) lg_u32x4 hbs[2][NC][64];  // h_t split parts: [part][chunk][lane]
@@ -293,7 +336,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     }
     if (g == 2 && valid) st4(hout + static_cast<int64_t>(seq) * H + 16 * u + 4 * q, hcur);
     if constexpr (NI) {
-        constexpr int D = H, LPR = D / 4, RPI = 64 / LPR, K = 16 / RPI, HS = H + 4;
+        constexpr int D = H, LPR = D / 4, HS = H + 4;
         static_assert(TS * HS <= LC * TS * XR, "node-init staging fits the x buffer");
         float* hl = xs;             // [TS][HS] h_L of the block's sequences (fp32)
         const float* wt = niw;      // W^T [H][D] (staged at the start)
@@ -327,28 +370,6 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                     st4(ni.xs0 + (static_cast<size_t>(sl) * ni.B + b) * D + 4 * fg, v);
                 }
             }
-        }
-        // the non-sensor tiles' [x0 > 0] words, one lane word per thread (blockDim.x is a multiple
-        // of 64, so a thread keeps its lane and its four channels over the stride)
-        const uint32_t l = threadIdx.x & 63, rl = l / LPR, fg = l % LPR;
-        const f32x4 bv = ld4(ni.bias + 4 * fg);
-        uint32_t pos = 0;  // [relu(b) * scale > 0] of the lane's four channels
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pos |= static_cast<uint32_t>(fmaxf(bv[i], 0.f) * vs > 0.f) << i;
-        const uint32_t words = ni.N * ni.ngroups * 64u, stride = gridDim.x * blockDim.x;
-        for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += stride) {
-            const uint32_t t = e >> 6, n = lg_div(t, ni.fdG), gg = t - n * ni.ngroups;
-            uint32_t wd = 0;  // a sensor node's tile: never read, written 0 (a deterministic output)
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const uint32_t b = 16 * gg + RPI * k + rl;
-                if (b < ni.B && ni.slot[n] < 0) {
-                    const uint32_t kb =
-                        ni.dropout ? lg_row_stream_keep4(key, static_cast<uint64_t>(b) * ni.N + n, 4 * fg, thr) : 0xFu;
-                    wd |= (kb & pos) << (4 * k);
-                }
-            }
-            ni.bits[e] = static_cast<uint16_t>(wd);
         }
     }
 }
@@ -1334,12 +1355,16 @@ extern "C" int lg_gru_node_init_fwd(const float* residual, const float* tfeat, c
     if (N * ngroups * 64 >= (int64_t{1} << 32) || B * N >= kLgMaxRows) return LG_EUNSUPPORTED;
     hipStream_t s = lg_stream(stream);
     const uint32_t Nseq = static_cast<uint32_t>(B * S);
-    const unsigned grid = static_cast<unsigned>(nblocks_seq(B * S));
+    // the sequence blocks, then the bits blocks: the CU slots the sequence blocks leave free (two
+    // workgroups per CU at H = 64, four at H = 32), at least 16
+    const int64_t nseqblk = nblocks_seq(B * S), slots = (H == 64 ? 2 : 4) * static_cast<int64_t>(lg_num_cus());
+    const int64_t nbits = std::max<int64_t>(16, nseqblk < slots ? slots - nseqblk : 0);
+    const unsigned grid = static_cast<unsigned>(nseqblk + nbits);
     const lg_fastdiv fdS = lg_make_fastdiv(static_cast<uint32_t>(S));
     const GruNi ni{sensor_slot, sensor_idx, proj_w, node_bias, xs0, x0bits, static_cast<uint32_t>(B),
                    static_cast<uint32_t>(N), static_cast<uint32_t>(ngroups),
                    lg_make_fastdiv(static_cast<uint32_t>(ngroups)), drop ? 1 : 0, dropout_p,
-                   drop ? 1.0f / (1.0f - dropout_p) : 1.0f, seed, salt};
+                   drop ? 1.0f / (1.0f - dropout_p) : 1.0f, seed, salt, static_cast<uint32_t>(nseqblk)};
 #define LG_GRU_NI(HH, UT, SV)                                                                                     \
     lg_launch(k_gru_fwd<HH, UT, SV, true>, grid, 12 * HH, 0, s, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates, \
               h_last, Nseq, static_cast<int>(L), static_cast<int>(S), fdS, ni)
