@@ -503,23 +503,57 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #define LG_PC_NPF 3
 #endif
 constexpr int kPcRing = LG_PC_RING;
-// 1 (lab A/B): the consumer waves load W's fragments straight from global memory (L2-resident)
-// and the producers start gathering without the W staging barrier.  Measured and dropped
-// (r05f, B = 256 train mode, isolated): 21.96 us against 19.73 for the staged prologue (0, the
-// default) — the per-wave W loads (16 KB per consumer wave) delay every consumer's first tile,
-// and the producers' start is set by the workgroups' dispatch spread (~1.4 us), not the barrier
-#ifndef LG_PC_WREG
-#define LG_PC_WREG 0
+// The node-table records of a workgroup's first kPcRecs tiles are staged in LDS with W, so a
+// producer's record is an LDS read after its tile draw instead of a scalar load from L2 (whose
+// latency sat between drawing tile t + 2 and issuing its loads, every tile); later tiles (large
+// graphs) read theirs with nm_rec.
+#ifndef LG_PC_RECS
+#define LG_PC_RECS 256
 #endif
-// 1 (lab A/B): a producer draws tile t + 3 and requests its node-table record while it
-// accumulates tile t (the record of tile t + 2, drawn one step earlier, has landed by the time
-// t + 2's loads are issued); 0 (default): tile t + 2 drawn and its record requested in step t.
-// Measured and dropped (r05g, isolated train mode): 22.5-22.8 us against 20.3-21.4 — the
-// held record costs 16 SGPRs and the kernel spills 31 of them (10 without)
-#ifndef LG_PC_RECAHEAD
-#define LG_PC_RECAHEAD 0
+constexpr int kPcRecs = LG_PC_RECS;
+// 1: the producers' prefetch loads are issued through inline asm and waited for with explicit
+// vmcnt counts (the other buffer's loads stay in flight).  The compiler's own wait insertion
+// lost track of the unrolled pair's two buffers (the loop it builds is irreducible) and waited
+// for every load in flight at each tile's accumulate — one tile of prefetch instead of two
+// (r05j: 10.7 us for the launch with neither loads nor consumer work, 15.1 with the loads).
+// Its waits for loads it does see stay correct: the asm loads are older, and vmcnt counts in
+// order.  0: the builtin loads (A/B).
+#ifndef LG_PC_ASMLOAD
+#define LG_PC_ASMLOAD 1
 #endif
-constexpr bool kPcWreg = LG_PC_WREG != 0;
+__device__ __forceinline__ f32x4 pc_load_b128(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+#if LG_PC_ASMLOAD
+    f32x4 v;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rs), "s"(soff));
+    return v;
+#else
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+#endif
+}
+__device__ __forceinline__ uint32_t pc_load_u16(__amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+#if LG_PC_ASMLOAD
+    uint32_t v;
+    asm volatile("buffer_load_ushort %0, %1, %2, 0 offen" : "=v"(v) : "v"(voff), "s"(rs));
+    return v;
+#else
+    return __builtin_amdgcn_raw_buffer_load_b16(rs, voff, 0, 0);
+#endif
+}
+// wait until at most N of this wave's vector memory loads are in flight (asm loads only)
+template <int N>
+__device__ __forceinline__ void pc_vm_wait() {
+#if LG_PC_ASMLOAD
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N));
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void pc_pin(T& v) {  // v is read only after the waits above it
+#if LG_PC_ASMLOAD
+    asm volatile("" : "+v"(v));
+#else
+    (void)v;
+#endif
+}
 // ring-slot metadata: n, b0, nb, X0's sensor entries (count, then up to kPcSens (slot, w) pairs)
 constexpr int kPcSens = 3;
 constexpr int kPcMeta = 16;
@@ -534,7 +568,8 @@ struct PcLds {  // floats
     static constexpr int XOFF = D * WS + D;                         // per-wave max|W| bits (F16)
     static constexpr int FOFF = XOFF + 16;                          // ready[16], done[kPcProd * NC], fin[4], ctr
     static constexpr int MOFF = FOFF + 16 + kPcProd * NC + 8;       // per (producer, slot): kPcMeta words
-    static constexpr int ROFF = MOFF + kPcMeta * kPcProd * kPcRing;  // the rings
+    static constexpr int COFF = MOFF + kPcMeta * kPcProd * kPcRing;  // kPcRecs node-table records (16 words)
+    static constexpr int ROFF = COFF + 16 * kPcRecs;                  // the rings
     static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
@@ -637,10 +672,14 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // workgroup's tiles finish together (with 4 producers per workgroup the static per-producer
     // split left 1/3 of them a whole tile behind the rest: 10 vs 11 tiles at B = 256).
     const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, 0, 1);
-    const int64_t tend = sc.end;
+    // tile indices as 32-bit scalars (ntiles < 2^26, lg_gcn_fwd_nm): a 64-bit compare needs a VGPR
+    // pair, which the compiler took from a prefetch buffer's registers — and then drained every load
+    // in flight at each step's issue (s_waitcnt vmcnt(0)) before it could reuse them
+    const int32_t tend = static_cast<int32_t>(sc.end), tfirst = static_cast<int32_t>(sc.first),
+                  tstride = static_cast<int32_t>(sc.stride);
     const float fold = DROP ? dscale : 1.0f;  // relu(s z) = s relu(z), s > 0
 
-    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+    auto tile_coords = [&](int32_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
         const bool valid = tile < tend;
         const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
         const uint32_t grp = lg_div(t32, fdN);
@@ -649,17 +688,23 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         nb = valid ? min(16u, B - b0) : 0u;
     };
 
-    // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|); with
-    // kPcWreg only the hand-off counters are set here (the consumers load W themselves)
-    if constexpr (kPcWreg) {
-        if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
-        if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
-        if (threadIdx.x == 0) *ctr = 0u;
-    } else {
-        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT;
+    // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|), and the
+    // records of the workgroup's first kPcRecs tiles (every load in flight before the first store)
+    int32_t* recs = reinterpret_cast<int32_t*>(lds + LY::COFF);
+    const int nrec = min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    {
+        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT, RPER = kPcRecs ? (4 * kPcRecs + NT - 1) / NT : 1;
         f32x4 wv[WPER];
 #pragma unroll
         for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * NT + threadIdx.x, W4 - 1));
+        lg_u32x4 rv[RPER];
+#pragma unroll
+        for (int u = 0; u < RPER; ++u) {  // quarter (i & 3) of record i >> 2
+            const int i = u * NT + threadIdx.x;
+            uint32_t n, b0, nb;
+            tile_coords(i < 4 * nrec ? tfirst + (i >> 2) * tstride : tend, n, b0, nb);
+            rv[u] = reinterpret_cast<const lg_u32x4*>(tab)[4 * (static_cast<size_t>(N) + n) + (i & 3)];
+        }
         const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
         uint32_t wm = 0;
 #pragma unroll
@@ -672,6 +717,11 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
                 for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
             }
+        }
+#pragma unroll
+        for (int u = 0; u < RPER; ++u) {
+            const int i = u * NT + threadIdx.x;
+            if (i < 4 * nrec) reinterpret_cast<lg_u32x4*>(recs)[i] = rv[u];
         }
         if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
         if constexpr (F16) {
@@ -723,6 +773,26 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         // X0's sensor rows are added by the consumer (ring-slot metadata), so the producer issues
         // one 2-byte load per neighbour instead of the rows.
         auto load_nb = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K], uint32_t& bw) {
+#ifdef LG_PC_LAB_NOLOAD  // lab: no gather loads (the neighbour blocks read as lane-dependent constants)
+            bw = lane;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) blk[k] = f32x4{1.f * k, 1.f * lane, 0.5f, 0.25f};
+            return;
+#endif
+            if constexpr (X0) {
+                const bool sens = (c & kLgSensorCol) != 0;
+                bw = pc_load_u16(brs, have && !sens ? nm_mask_off(static_cast<uint32_t>(c), b0 >> 4, ngroups, lane)
+                                                    : kNm3BlkOob + 2u * lane);
+                return;
+            }
+            const bool rows = have;
+            const uint32_t base = rows ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
+            const __amdgpu_buffer_rsrc_t rs = rows ? xrs : xrs0;
+#pragma unroll
+            for (int k = 0; k < G::K; ++k) blk[k] = pc_load_b128(rs, lk[k], base);
+        };
+        // the rest-of-row blocks (loaded and consumed within one tile): the compiler's loads
+        auto load_rest = [&](int c, bool have, uint32_t b0, const uint32_t (&lk)[G::K], f32x4 (&blk)[G::K], uint32_t& bw) {
             if constexpr (X0) {
                 const bool sens = (c & kLgSensorCol) != 0;
                 bw = __builtin_amdgcn_raw_buffer_load_b16(
@@ -730,13 +800,13 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     0, 0);
                 return;
             }
-            const bool rows = have;
-            const uint32_t base = rows ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
-            const __amdgpu_buffer_rsrc_t rs = rows ? xrs : xrs0;
+            const uint32_t base = have ? (static_cast<uint32_t>(c) * B + b0) * (4u * D) : 0u;
+            const __amdgpu_buffer_rsrc_t rs = have ? xrs : xrs0;
 #pragma unroll
             for (int k = 0; k < G::K; ++k)
                 blk[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lk[k], base, 0));
         };
+        constexpr int LPT = X0 ? NPF : NPF * G::K;  // prefetch loads per tile
         // slot k of a loaded neighbour block as values.  X0: from the mask word (zero for a
         // sensor neighbour), branch-free (a branch on the neighbour kind here made the compiler
         // read the rest-of-row mask words before their loads had landed: wrong bits for slots
@@ -752,19 +822,38 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             }
             return blk[k];
         };
-        // the workgroup's next tile (an LDS atomic; past tend once its tiles are all dealt)
-        auto grab = [&]() -> int64_t {
+        // the workgroup's next tile (an LDS atomic; past tend once its tiles are all dealt) and
+        // its record (staged in LDS for the first kPcRecs draws)
+        auto grab = [&](NmRec& r) -> int32_t {
             uint32_t i = 0;
             if (lane == 0) i = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             i = __builtin_amdgcn_readfirstlane(i);
-            return sc.first + static_cast<int64_t>(i) * sc.stride;
+            const int32_t tile = tfirst + static_cast<int32_t>(i) * tstride;
+            if (static_cast<int>(i) < nrec) {
+                const int4* rp = reinterpret_cast<const int4*>(recs) + 4 * i;
+                const int4 a = rp[0], b = rp[1], c = rp[2], d = rp[3];
+                auto u = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+                r.e0 = u(a.x);
+                r.e1 = u(a.y);
+                r.p[0] = int2{u(a.z), u(a.w)};
+                r.p[1] = int2{u(b.x), u(b.y)};
+                r.p[2] = int2{u(b.z), u(b.w)};
+                r.p[3] = int2{u(c.x), u(c.y)};
+                r.p[4] = int2{u(c.z), u(c.w)};
+                r.p[5] = int2{u(d.x), u(d.y)};
+                r.self = u(d.z);
+                r.node = u(d.w);
+            } else {
+                uint32_t n, b0, nb;
+                tile_coords(tile, n, b0, nb);
+                r = nm_rec(tab, N + n);
+            }
+            return tile;
         };
-        int64_t tl[2];  // the tile whose blocks are in flight in buffer b
-        int64_t ptile = 0;  // LG_PC_RECAHEAD: the next tile drawn, its record requested
-        NmRec prec{};
+        int32_t tl[2];  // the tile whose blocks are in flight in buffer b
         // r: the tile's node-table record (schedule section: slot -> record with its node id),
         // requested by the caller a phase earlier
-        auto issue = [&](auto bc, const NmRec& r, int64_t tile) {
+        auto issue = [&](auto bc, const NmRec& r, int32_t tile) {
             constexpr int b = decltype(bc)::value;
             uint32_t n, b0, nb;
             tile_coords(tile, n, b0, nb);
@@ -782,30 +871,26 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         // tile t of this producer from buffer b: accumulate, hand over, refill b with tile t + 2
         auto step = [&](auto bc, int64_t t) -> bool {
             constexpr int b = decltype(bc)::value;
-            const int64_t tile = tl[b];
+            const int32_t tile = tl[b];
             if (tile >= tend) return false;
-            // the producer's tile t + 2 is drawn, and its record goes in flight while this tile is
-            // accumulated (LG_PC_RECAHEAD: tile t + 2 and its record came from step t - 1; tile
-            // t + 3 is drawn now)
-#if LG_PC_RECAHEAD
-            const int64_t tnext = ptile;
-            const NmRec nxt = prec;
-            {
-                ptile = grab();
-                uint32_t pn, pb0, pnb;
-                tile_coords(ptile, pn, pb0, pnb);
-                prec = nm_rec(tab, N + pn);
-            }
-#else
-            const int64_t tnext = grab();
-            uint32_t nn, nb0, nnb;
-            tile_coords(tnext, nn, nb0, nnb);
-            const NmRec nxt = nm_rec(tab, N + nn);
-#endif
+            // the producer's tile t + 2 is drawn (its record from LDS, or in flight while this tile
+            // is accumulated)
+            NmRec nxt;
+            const int32_t tnext = grab(nxt);
             asm volatile("" ::: "memory");  // keep the request here (the compiler sinks it to its use)
             const NmRec& cur = rec[b];
             const int e0 = cur.e0, e1 = cur.e1;
             const uint32_t b0 = tb0[b];
+            // this buffer's loads are the older half of those in flight (the other buffer's tile
+            // was issued after them)
+            pc_vm_wait<LPT>();
+#pragma unroll
+            for (int i = 0; i < NPF; ++i) {
+                if constexpr (X0) pc_pin(pb[b][i]);
+                else
+#pragma unroll
+                    for (int k = 0; k < G::K; ++k) pc_pin(pf[b][i][k]);
+            }
             f32x4 acc[G::K];
             {
                 const float w = e0 < e1 ? __int_as_float(cur.p[0].y) : 0.f;
@@ -826,7 +911,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 f32x4 va[NI][G::K];
                 uint32_t vb[NI];
 #pragma unroll
-                for (int i = 0; i < NI; ++i) load_nb(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
+                for (int i = 0; i < NI; ++i) load_rest(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
 #pragma unroll
                 for (int i = 0; i < NI; ++i) {  // an absent entry: zero blocks at weight 0 (acc unchanged)
                     const float wa = e0 + NPF + i < e1 ? __int_as_float(cur.p[NPF + i].y) : 0.f;
@@ -837,7 +922,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     const int2 pa = pairs[e];
                     f32x4 vr[G::K];
                     uint32_t vw;
-                    load_nb(pa.x, true, b0, lo[b], vr, vw);
+                    load_rest(pa.x, true, b0, lo[b], vr, vw);
                     const float wa = __int_as_float(pa.y);
 #pragma unroll
                     for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(pa.x, vr, vw, k));
@@ -891,19 +976,10 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             return true;
         };
         {
-            const int64_t f0 = grab(), f1 = grab();
-            uint32_t n0, b00, nb00, n1, b01, nb01;
-            tile_coords(f0, n0, b00, nb00);
-            tile_coords(f1, n1, b01, nb01);
-            const NmRec r0 = nm_rec(tab, N + n0), r1 = nm_rec(tab, N + n1);
+            NmRec r0, r1;
+            const int32_t f0 = grab(r0), f1 = grab(r1);
             issue(std::integral_constant<int, 0>{}, r0, f0);
             issue(std::integral_constant<int, 1>{}, r1, f1);
-#if LG_PC_RECAHEAD
-            ptile = grab();
-            uint32_t pn, pb0, pnb;
-            tile_coords(ptile, pn, pb0, pnb);
-            prec = nm_rec(tab, N + pn);
-#endif
         }
         int64_t t = 0;
         for (;; t += 2) {
@@ -914,6 +990,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             }
         }
         // tiles are drawn in increasing order, so the first one past tend ends the producer
+        pc_vm_wait<0>();  // the last (empty) prefetches
         if (lane == 0) pc_store_rel(&fin[prod], static_cast<uint32_t>(t));
 #ifdef LG_NM3_STAMPS
         pc_stamp_end();
@@ -932,39 +1009,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
     int sw = 0;  // F16: W's scale exponent
-    // kPcWreg: this wave's W fragments (all of W: rows 16 mt + j, columns 32 s2 + 8 q .. + 7) from
-    // global memory, times fold, rounded before any split; every consumer wave holds the whole
-    // matrix, so its own max |W| is the workgroup's.  The bias * fold row goes to LDS (each wave
-    // writes the same values; a lane reads back what a lane of its own wave wrote)
-    f32x4 wgl[G::CH][KS][2];
-    if constexpr (kPcWreg) {
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt)
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2) {
-                const float* wp = W + (16 * mt + j) * D + 32 * s2 + 8 * q;
-                wgl[mt][s2][0] = ld4(wp);
-                wgl[mt][s2][1] = ld4(wp + 4);
-            }
-        if (lane < D / 4) {
-            f32x4 bb = bias ? ld4(bias + 4 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
-            st4(wst + D * LY::WS + 4 * lane, bb * fold);
-        }
-        uint32_t m = 0;
-#pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt)
-#pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    f32x4 w = wgl[mt][s2][h] * fold;
-                    asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
-                    wgl[mt][s2][h] = w;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) m = max(m, __float_as_uint(fabsf(w[c])));
-                }
-        if constexpr (F16) sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(lg_wave_max_bits(m)));
-    } else if constexpr (F16) {
+    if constexpr (F16) {
         uint32_t m = 0;
         for (int w = 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
         sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
@@ -976,7 +1021,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
             const float* wp = wst + (16 * mt + j) * LY::WS + 32 * s2 + 8 * q;
-            const f32x4 wa = kPcWreg ? wgl[mt][s2][0] : ld4(wp), wb = kPcWreg ? wgl[mt][s2][1] : ld4(wp + 4);
+            const f32x4 wa = ld4(wp), wb = ld4(wp + 4);
             if constexpr (F16) {
                 const float sc2 = lg_pow2f(sw);
                 split2_f16_x8(wa * sc2, wb * sc2, wh[0][mt][s2], wh[F16 ? 1 : 0][mt][s2]);
@@ -1003,6 +1048,10 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         const uint32_t* m = meta + kPcMeta * (prod * R + sl);
         const uint32_t n = __builtin_amdgcn_readfirstlane(m[0]), b0 = __builtin_amdgcn_readfirstlane(m[1]),
                        nb = __builtin_amdgcn_readfirstlane(m[2]);
+#ifdef LG_PC_LAB_NOCONS  // lab: consumers hand the slot straight back
+        pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));
+        continue;
+#endif
         f32x4 bq[KS][2];
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
@@ -1041,15 +1090,16 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
         f32x4 o[G::CH];
         if constexpr (F16) {
-            // the tile's scale from its largest |value| (the B-operand values are the whole tile)
-            uint32_t mx = 0;
+            // the tile's scale from its largest |value| (the B-operand values are the whole tile;
+            // fmaxf on |.| source modifiers: three values an instruction)
+            float mxf = 0.f;
 #pragma unroll
             for (int s2 = 0; s2 < KS; ++s2)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) mx = max(mx, __float_as_uint(fabsf(bq[s2][h][c])));
-            const int sa = lg_f16_scale_exp(lg_wave_max_bits(mx));
+                    for (int c = 0; c < 4; ++c) mxf = fmaxf(mxf, fabsf(bq[s2][h][c]));
+            const int sa = lg_f16_scale_exp(lg_wave_max_bits(__float_as_uint(mxf)));
             const float sc2 = lg_pow2f(sa);
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -390,6 +390,8 @@ def main():
                                                 nat.LG_F_DROPOUT, 0.1, 123, 1, cs()), "fwd x0")
         t = timeit(fx, args.iters)
         res["gcn_fwd_x0"] = {"us": t, "GBps": (4 * B * N * D + nbits * 2 + 4 * S5 * B * D) / t / 1e3}
+        if args.probe and hasattr(lib, "lg_lab_nm3_stamps"):
+            res["probe_x0"] = pc_probe_summary(lib, fx)
         dy = torch.randn_like(x)
         dx = torch.empty_like(x)
         dW, db, dnb = torch.empty(D, D, device=dev), torch.empty(D, device=dev), torch.empty(D, device=dev)
