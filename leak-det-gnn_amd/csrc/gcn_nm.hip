@@ -511,6 +511,11 @@ constexpr int kPcRing = LG_PC_RING;
 #define LG_PC_RECS 256
 #endif
 constexpr int kPcRecs = LG_PC_RECS;
+// producer wave priority (s_setprio; 0: the default, equal to the consumers').  Measured (r05m,
+// isolated train mode, two rounds): 2 and 3 within the box's noise of 0 (20.5-21.3 us each)
+#ifndef LG_PC_PRIO
+#define LG_PC_PRIO 0
+#endif
 // 1: the producers' prefetch loads are issued through inline asm and waited for with explicit
 // vmcnt counts (the other buffer's loads stay in flight).  The compiler's own wait insertion
 // lost track of the unrolled pair's two buffers (the loop it builds is irreducible) and waited
@@ -748,6 +753,11 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     if (producer) {
         // ---------------- producer: gather + accumulate, two tiles in flight
+#if LG_PC_PRIO
+        // the producer's instruction stream is the pipeline's critical path; its two consumers on
+        // the same SIMD have ring slack, so the producer goes first when both are ready to issue
+        __builtin_amdgcn_s_setprio(LG_PC_PRIO);
+#endif
         // X0 (layer 0 on the compressed node init): a neighbour whose record col carries
         // kLgSensorCol is a sensor row of x (= xs0 [S][B][D]) at its slot; any other
         // neighbour's block is its [x0 > 0] mask word (one uint16 per lane), x0 = bit ? v0 : 0
