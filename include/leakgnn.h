@@ -434,6 +434,17 @@ int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t, const floa
 int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w,
             const float* x, float* y, int64_t B, int64_t N, int64_t D, int64_t nnz_cap, lg_stream_t stream);
 
+/* Propagate of any width: y[n][c] = sum over row n of the CSR (entry order) of
+ * w[e] x[col[e]][c], plus bias[c] when bias is non-null, for n < N, c < C (row strides ldx,
+ * ldy >= C, in floats; x and y must not alias).  The general path of GCNConv (in_channels !=
+ * out_channels or widths other than 32 / 64: reference detector.py:198-199 builds
+ * GCNConv(hidden, hidden), PyG's GCNConv takes any pair): y = Ahat (x W^T) + b with the
+ * transform on a library GEMM, or (x's width < the output's) (Ahat x) W^T + b; the backward is
+ * the same call over the transposed CSR (lg_graph_build's rowptr_t / col_t / w_t).  No
+ * capacity limits beyond N * C < 2^62.  (ABI 24) */
+int lg_spmm_cols(const int32_t* rowptr, const int32_t* col, const float* w, const float* x, int64_t ldx,
+                 const float* bias, float* y, int64_t ldy, int64_t N, int64_t C, lg_stream_t stream);
+
 /* Fused GCN layer backward (one main launch + one deterministic slab reduction).
  * Given dy = dL/dy of this layer's output:
  *   dz     = LG_F_MASK_IN ? dy * scale_in * [y > 0] : dy

@@ -755,6 +755,57 @@ extern "C" int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w
     return LG_OK;
 }
 
+// ------------------------------------------------------------------ propagate, any width
+// y[n][c] = sum over row n's CSR entries (entry order) of w[e] x[col[e]][c] (+ bias[c]) for any
+// column count C: GCNConv's general path (in_channels != out_channels, or widths other than the
+// fused kernels' 32 / 64; models/gcn.py).  A thread owns four consecutive columns of one row
+// (VEC, when C and both row strides are multiples of 4 and the bases 16-byte aligned) or one
+// column; consecutive threads take consecutive columns, so a row's reads and writes coalesce.
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_spmm_cols(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                   const float* __restrict__ w, const float* __restrict__ x,
+                                                   int64_t ldx, const float* __restrict__ bias, float* __restrict__ y,
+                                                   int64_t ldy, int64_t N, int64_t C) {
+    constexpr int V = VEC ? 4 : 1;
+    const int64_t CV = C / V, total = N * CV;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t n = i / CV, c = (i - n * CV) * V;
+        const int e0 = rowptr[n], e1 = rowptr[n + 1];
+        if constexpr (VEC) {
+            f32x4 acc = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int e = e0; e < e1; ++e) {
+                const f32x4 v = ld4(x + static_cast<int64_t>(col[e]) * ldx + c);
+                const float we = w[e];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) s[k] = fmaf(we, v[k], s[k]);
+            }
+            st4(y + n * ldy + c, s + acc);
+        } else {
+            float s = 0.f;
+            for (int e = e0; e < e1; ++e) s = fmaf(w[e], x[static_cast<int64_t>(col[e]) * ldx + c], s);
+            y[n * ldy + c] = s + (bias ? bias[c] : 0.f);
+        }
+    }
+}
+
+extern "C" int lg_spmm_cols(const int32_t* rowptr, const int32_t* col, const float* w, const float* x, int64_t ldx,
+                            const float* bias, float* y, int64_t ldy, int64_t N, int64_t C, lg_stream_t stream) {
+    if (N < 0 || C < 0 || ldx < C || ldy < C) return LG_EINVAL;
+    if (N == 0 || C == 0) return LG_OK;
+    if (!rowptr || !col || !w || !x || !y || x == y) return LG_EINVAL;
+    hipStream_t s = lg_stream(stream);
+    const bool vec = C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(y) % 16 == 0 && (!bias || reinterpret_cast<uintptr_t>(bias) % 16 == 0);
+    const int64_t items = N * (vec ? C / 4 : C);
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 64LL * lg_num_cus())));
+    if (vec) lg_launch(k_spmm_cols<true>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+    else lg_launch(k_spmm_cols<false>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+    LG_RET_IF_LAUNCH_FAILED();
+    return LG_OK;
+}
+
 extern "C" int64_t lg_gcn_bwd_workspace_bytes(int64_t D) {
     if (D != 32 && D != 64) return LG_EUNSUPPORTED;
     return static_cast<int64_t>(bwd_grid_max()) * (D * D + 2 * D) * static_cast<int64_t>(sizeof(float));

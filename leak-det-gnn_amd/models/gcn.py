@@ -14,7 +14,9 @@ reference; the semantics restated here are PyG 2.x's published ones:
 Here forward runs the registered op leakgnn::gcn_conv (models/library.py: one fused HIP
 launch of (Ahat x) W^T + b — lg_gcn_fwd_rows, 16-node tiles off the node table, at D = 64;
 lg_gcn_fwd at D = 32) and its autograd formula leakgnn::gcn_conv_backward
-(lg_gcn_bwd_rows / lg_gcn_bwd).  The gcn_norm'ed CSR is built on the device
+(lg_gcn_bwd_rows / lg_gcn_bwd).  Other widths (in != out, or not 32 / 64) take the general
+path: leakgnn::spmm_cols (lg_spmm_cols, any column count, bias fused) for the propagate and a
+library GEMM for the transform, on the narrower side.  The gcn_norm'ed CSR is built on the device
 (lg_graph_build) and, unlike PyG with cached=False, re-used while an edge_index
 with the SAME CONTENT is passed again — the graph is a pure function of edge_index,
 so results are unchanged.  The same tensor object at the same version counter is a
@@ -33,7 +35,7 @@ import torch
 import torch.nn as nn
 
 from . import library  # noqa: F401  (registers the leakgnn:: ops)
-from .ops import GCNGraph, _f32
+from .ops import SUPPORTED_D, GCNGraph, _f32
 
 
 def _glorot_(t: torch.Tensor) -> None:
@@ -101,8 +103,17 @@ class GCNConv(nn.Module):
         if edge_weight is not None:
             raise NotImplementedError("edge_weight is not used on the Leak-det-gnn path")
         g = self.graph_for(edge_index, x.size(0), x.device)
-        return torch.ops.leakgnn.gcn_conv(_f32(x), _f32(self.lin.weight), _f32(self.bias), g.rowptr, g.col, g.w,
-                                          g.rowptr_t, g.col_t, g.w_t, g.nodetab, g.pairs, g.nodetab_t, g.pairs_t)
+        if self.in_channels == self.out_channels and self.in_channels in SUPPORTED_D:
+            return torch.ops.leakgnn.gcn_conv(_f32(x), _f32(self.lin.weight), _f32(self.bias), g.rowptr, g.col, g.w,
+                                              g.rowptr_t, g.col_t, g.w_t, g.nodetab, g.pairs, g.nodetab_t, g.pairs_t)
+        # general widths: propagate on lg_spmm_cols, transform on a library GEMM, on the narrower
+        # side (PyG's order, lin then propagate, when the output is not wider than the input)
+        x, W, b = _f32(x), _f32(self.lin.weight), _f32(self.bias)
+        csr = (g.rowptr, g.col, g.w, g.rowptr_t, g.col_t, g.w_t)
+        if self.out_channels <= self.in_channels:
+            return torch.ops.leakgnn.spmm_cols(x @ W.t(), b, *csr)
+        p = torch.ops.leakgnn.spmm_cols(x, None, *csr)
+        return torch.addmm(b, p, W.t()) if b is not None else p @ W.t()
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"

@@ -148,6 +148,46 @@ def _gcn_conv_bwd(ctx, dy):
 gcn_conv.register_autograd(_gcn_conv_bwd, setup_context=_gcn_conv_setup)
 
 
+# ============================================================================ spmm_cols
+# GCNConv's general path (models/gcn.py): widths other than the fused kernels' 32 / 64, or
+# in_channels != out_channels.  The propagate runs on lg_spmm_cols (any column count, bias
+# fused), the transform on a library GEMM.
+@torch.library.custom_op(f"{NS}::spmm_cols", mutates_args=(), device_types="cuda")
+def spmm_cols(x: Tensor, bias: Optional[Tensor], rowptr: Tensor, col: Tensor, w: Tensor, rowptr_t: Tensor,
+              col_t: Tensor, w_t: Tensor) -> Tensor:
+    """y = Ahat x (+ bias) for x [N][C], any C (lg_spmm_cols over the gcn_norm'ed CSR)."""
+    lib = load_library()
+    x, bias = _c(x), _c(bias)
+    _req(x, bias)
+    N, C = x.shape
+    y = torch.empty_like(x)
+    with _timed("spmm_cols", x.device):
+        check(lib.lg_spmm_cols(ptr(rowptr), ptr(col), ptr(w), ptr(x), C, ptr(bias), ptr(y), C, N, C, stream_of(x)),
+              "lg_spmm_cols")
+    return y
+
+
+@spmm_cols.register_fake
+def _(x, bias, rowptr, col, w, rowptr_t, col_t, w_t):
+    return torch.empty_like(x)
+
+
+def _spmm_cols_setup(ctx, inputs, output):
+    _, bias, _, _, _, rowptr_t, col_t, w_t = inputs
+    ctx.has_bias = bias is not None
+    ctx.save_for_backward(rowptr_t, col_t, w_t)
+
+
+def _spmm_cols_bwd(ctx, dy):
+    rowptr_t, col_t, w_t = ctx.saved_tensors
+    # dx = Ahat^T dy: the same propagate over the transposed CSR (its rows are the columns of Ahat)
+    dx = torch.ops.leakgnn.spmm_cols(dy, None, rowptr_t, col_t, w_t, rowptr_t, col_t, w_t)
+    return dx, (dy.sum(0) if ctx.has_bias else None), None, None, None, None, None, None
+
+
+spmm_cols.register_autograd(_spmm_cols_bwd, setup_context=_spmm_cols_setup)
+
+
 # ============================================================================ mean_pool
 @torch.library.custom_op(f"{NS}::mean_pool", mutates_args=(), device_types="cuda")
 def mean_pool(x: Tensor, B: int, N: int) -> Tensor:

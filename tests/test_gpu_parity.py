@@ -117,6 +117,66 @@ def test_gcnconv_fwd_bwd_vs_oracle(D, graph):
     assert_close(conv.bias.grad, bc.grad, what="GCNConv db")
 
 
+@pytest.mark.parametrize("din,dout", [(48, 80), (64, 16), (32, 64), (96, 96), (7, 5), (64, 128)])
+@pytest.mark.parametrize("graph", ["ltown_a_b4", "random"])
+def test_gcnconv_general_widths_vs_oracle(din, dout, graph):
+    """GCNConv(in, out) at widths the fused kernels do not take (in != out, or not 32 / 64):
+    lg_spmm_cols for the propagate (any column count; the bias fused; scalar columns at odd
+    widths) and a library GEMM for the transform, against the PyG-semantics oracle, forward and
+    all three gradients (1e-5 of each tensor's scale)."""
+    from models.gcn import GCNConv
+    if graph == "random":
+        N = 3001
+        ei = _rand_graph(N, 12000, seed=7)
+    else:
+        g = load("graph_ltown_a.npz")
+        ei = torch.from_numpy(graph_ref.batchify(g["edge_index"], 661, 4))
+        N = 4 * 661
+    torch.manual_seed(din * 1000 + dout)
+    conv = GCNConv(din, dout).to(DEV)
+    with torch.no_grad():
+        conv.bias.normal_()
+    x = torch.randn(N, din)
+    xg = x.to(DEV).requires_grad_(True)
+    y = conv(xg, ei.to(DEV))
+    assert y.shape == (N, dout)
+    gy = torch.randn(N, dout)
+    y.backward(gy.to(DEV))
+    xc = x.clone().requires_grad_(True)
+    Wc = conv.lin.weight.detach().cpu().clone().requires_grad_(True)
+    bc = conv.bias.detach().cpu().clone().requires_grad_(True)
+    yc = gcn_ref.gcn_conv(xc, ei, Wc, bc)
+    yc.backward(gy)
+    assert_close(y, yc, what=f"GCNConv({din},{dout}) fwd")
+    assert_close(xg.grad, xc.grad, what=f"GCNConv({din},{dout}) dx")
+    assert_close(conv.lin.weight.grad, Wc.grad, what=f"GCNConv({din},{dout}) dW")
+    assert_close(conv.bias.grad, bc.grad, what=f"GCNConv({din},{dout}) db")
+
+
+def test_spmm_cols_strided_and_empty_rows():
+    """lg_spmm_cols through the C ABI: row strides wider than C, no bias, a graph whose last rows
+    have only their self loop, and C = 0 / N = 0 (no launch); against the oracle's propagate."""
+    from models import ops
+    from models.ops import GCNGraph
+    lib = ops.load_library()
+    N = 500
+    ei = _rand_graph(N - 50, 2000, seed=3)  # nodes 450..499: self loops only
+    graph = GCNGraph.build(ei, N, DEV)
+    for C, ld in ((40, 44), (13, 13), (64, 72)):
+        x = torch.randn(N, ld)
+        xd = x.to(DEV)
+        y = torch.full((N, ld + 4), 7.0, device=DEV)
+        ops.check(lib.lg_spmm_cols(ops.ptr(graph.rowptr), ops.ptr(graph.col), ops.ptr(graph.w), ops.ptr(xd), ld, None,
+                                   ops.ptr(y), ld + 4, N, C, ops.stream_of(xd)), "spmm_cols")
+        torch.cuda.synchronize()
+        yc = gcn_ref.gcn_conv(x[:, :C].contiguous(), ei, torch.eye(C), None)
+        assert_close(y[:, :C], yc, what=f"spmm_cols C={C} ld={ld}")
+        assert torch.all(y[:, C:] == 7.0), "columns past C untouched"
+    for n_, c_ in ((0, 8), (N, 0)):
+        assert lib.lg_spmm_cols(ops.ptr(graph.rowptr), ops.ptr(graph.col), ops.ptr(graph.w), ops.ptr(xd), 64, None,
+                                ops.ptr(y), 64, n_, c_, ops.stream_of(xd)) == 0
+
+
 def test_spmm_vs_oracle_and_linearity():
     from models.ops import GCNGraph, spmm
     g = load("graph_ltown_a.npz")
