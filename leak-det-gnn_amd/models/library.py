@@ -946,7 +946,9 @@ def detector_heads_backward(dlogits: Tensor, h: Tensor, w1: Tensor, w2: Tensor, 
 # Same node gradient bit for bit (one incidence order for all;
 # tests/test_gpu_library.py::test_fused_pipe_scatter_matches_two_launches).  Measured at
 # B = 256 (DESIGN §3 "Round 4"): streamed 125-132 us in the step (profiles/r04/r04z3), against
-# 152.6 us for the per-window form and 114.6 + 35.3 us for the two launches (round 3).
+# 152.6 us for the per-window form and 114.6 + 35.3 us for the two launches (round 3); since
+# round 5 the streamed launch also runs the NoLeakHead backward (_FUSED_HEADS below):
+# 135-139 us in the step for both heads (profiles/r05/r05p), against 125-132 + 10-11 us.
 _FUSED_SCATTER = True
 # True: with the streamed scatter, the NoLeakHead backward runs in the EdgeHead backward's
 # prologue (lg_heads_bwd_scatter: one launch for both heads); False: lg_pool_head_bwd first
