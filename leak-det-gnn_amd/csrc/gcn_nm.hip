@@ -511,6 +511,15 @@ constexpr int kPcRing = LG_PC_RING;
 #define LG_PC_RECS 256
 #endif
 constexpr int kPcRecs = LG_PC_RECS;
+// 1: the workgroup-wide barrier at the start only covers the hand-off counters; the CONSUMER
+// waves stage W (and the bias, the max |W|) among themselves behind an LDS counter, so the
+// producers start gathering at once instead of waiting ~1.3 us for W's loads (probe, r05h/i).
+// The node-table records then come from scalar loads (nothing else to stage).  0: one barrier
+// after W and the records are staged by the whole workgroup.
+#ifndef LG_PC_WSPLIT
+#define LG_PC_WSPLIT 1
+#endif
+constexpr bool kPcWsplit = LG_PC_WSPLIT != 0;
 // producer wave priority (s_setprio; 0: the default, equal to the consumers').  Measured (r05m,
 // isolated train mode, two rounds): 2 and 3 within the box's noise of 0 (20.5-21.3 us each)
 #ifndef LG_PC_PRIO
@@ -696,8 +705,16 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|), and the
     // records of the workgroup's first kPcRecs tiles (every load in flight before the first store)
     int32_t* recs = reinterpret_cast<int32_t*>(lds + LY::COFF);
-    const int nrec = min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
-    {
+    const int nrec = kPcWsplit ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    uint32_t* wrdy = ctr + 1;  // kPcWsplit: consumer waves done staging W
+    if constexpr (kPcWsplit) {
+        if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
+        if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
+        if (threadIdx.x == 0) {
+            *ctr = 0u;
+            *wrdy = 0u;
+        }
+    } else {
         constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT, RPER = kPcRecs ? (4 * kPcRecs + NT - 1) / NT : 1;
         f32x4 wv[WPER];
 #pragma unroll
@@ -738,6 +755,33 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (threadIdx.x == 0) *ctr = 0u;
     }
     __syncthreads();
+    if (kPcWsplit && !producer) {  // the consumers' W staging (all loads in flight before the first store)
+        constexpr int CT = 64 * kPcProd * NC, W4 = D * D / 4, WPER = (W4 + CT - 1) / CT;
+        const int ct = static_cast<int>(threadIdx.x) - 64 * kPcProd;
+        f32x4 wv[WPER];
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * CT + ct, W4 - 1));
+        const float bb = (bias && ct < D) ? bias[ct] : 0.f;
+        uint32_t wm = 0;
+#pragma unroll
+        for (int u = 0; u < WPER; ++u) {
+            const int i = u * CT + ct;
+            f32x4 w = wv[u] * fold;
+            asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
+            if (i < W4) {
+                st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
+            }
+        }
+        if (ct < D) wst[D * LY::WS + ct] = bb * fold;
+        if constexpr (F16) {
+            wm = lg_wave_max_bits(wm);
+            if (lane == 0) wmx[wave] = wm;
+        }
+        if (lane == 0) __hip_atomic_fetch_add(wrdy, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pc_wait(wrdy, static_cast<uint32_t>(kPcProd * NC));
+    }
 #ifdef LG_PC_PROBE
     const uint64_t probe_c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1021,7 +1065,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     int sw = 0;  // F16: W's scale exponent
     if constexpr (F16) {
         uint32_t m = 0;
-        for (int w = 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
+        for (int w = kPcWsplit ? kPcProd : 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
         sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
     }
     lg_bf16x8 wf[NP][G::CH][KS];
