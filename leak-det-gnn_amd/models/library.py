@@ -32,7 +32,8 @@ from torch import Tensor
 
 from . import _native as nat
 from ._native import check, load_library, ptr, stream_of
-from .ops import EDGE_HEAD_SALT, GCN_FWD_NM_EXTRA_FLAGS, NM_MAX_BYTES, NOLEAK_HEAD_SALT, _check_d, _timed
+from .ops import (EDGE_HEAD_SALT, GCN_BWD_NM_EXTRA_FLAGS, GCN_FWD_DENSE_EXTRA_FLAGS, GCN_FWD_NM_EXTRA_FLAGS,
+                  NM_MAX_BYTES, NOLEAK_HEAD_SALT, _check_d, _timed)
 
 NS = "leakgnn"
 
@@ -487,8 +488,9 @@ def gnn_trunk(h_s: Tensor, proj_weight: Tensor, node_bias: Tensor, weights: List
                                            ptr(W), ptr(b), ptr(y), B, N, S, D, flags | GCN_FWD_NM_EXTRA_FLAGS, p,
                                            seed_v, (l + 1) | sbit, st), "lg_gcn_fwd_nm_x0")
             elif node_major:
+                fx = GCN_FWD_DENSE_EXTRA_FLAGS if not bf16 else 0
                 check(lib.lg_gcn_fwd_nm_bits(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N,
-                                             D, col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v,
+                                             D, col.numel(), flags | GCN_FWD_NM_EXTRA_FLAGS | fx, p, seed_v,
                                              (l + 1) | sbit, st, ptr(ymask) if l == L - 1 else None),
                       "lg_gcn_fwd_nm_bits")
             else:
@@ -596,6 +598,8 @@ def _trunk_layer_launches(lib, dy, xs, ymask, weights, sensor_slot, nodetab_t, p
     for l in range(L - 1, -1, -1):
         ws = wss[l]
         flags = nat.LG_F_MASK_OUT | (nat.LG_F_MASK_IN if l == L - 1 else 0) | (nat.LG_F_BF16 if bf16 else 0)
+        if node_major and not bf16:
+            flags |= GCN_BWD_NM_EXTRA_FLAGS
         if l == 0:  # lg_sensor_proj_bwd reads only the sensor rows of layer 0's dx
             flags |= nat.LG_F_DX_SENSOR_ROWS
         dx = torch.empty_like(dy)
@@ -741,8 +745,9 @@ def encoder_trunk(residual: Tensor, tfeat: Optional[Tensor], w_ih: Tensor, w_hh:
                                            ptr(b), ptr(y), B, N, S, D, flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v,
                                            (l + 1) | sbit, st), "lg_gcn_fwd_nm_x0")
             else:
+                fx = GCN_FWD_DENSE_EXTRA_FLAGS if not bf16 else 0
                 check(lib.lg_gcn_fwd_nm_bits(ptr(nodetab), ptr(pairs), ptr(xs[-1]), ptr(W), ptr(b), ptr(y), B, N, D,
-                                             pairs.shape[0], flags | GCN_FWD_NM_EXTRA_FLAGS, p, seed_v, (l + 1) | sbit,
+                                             pairs.shape[0], flags | GCN_FWD_NM_EXTRA_FLAGS | fx, p, seed_v, (l + 1) | sbit,
                                              st, ptr(ymask) if l == L - 1 else None), "lg_gcn_fwd_nm_bits")
         xs.append(y)
     return xs[1:] + [ymask, xs0, x0bits, h_seq, gates]

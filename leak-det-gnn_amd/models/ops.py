@@ -58,6 +58,15 @@ def use_node_major(B: int, N: int, D: int, bf16: bool = False) -> bool:
 # lg_gcn_fwd_nm kernel / transform bits (LG_F_NM3, LG_F_BF16X3, LG_F_F32_MFMA; include/leakgnn.h) for
 # A/B timing of the trunk forward inside the training step (bench.py --trunk-fwd-flags).
 GCN_FWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_NM_FLAGS", "0"), 0)
+# the dense (non-x0) trunk layers' forward only (layer 0 keeps its x0 kernel): the same-box in-step A/B
+# of the forward pipelines (LG_F_NM3 = 0x20000: nm3, one wave per tile, 3-way bf16 split)
+GCN_FWD_DENSE_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_FWD_DENSE_FLAGS", "0"), 0)
+# lg_gcn_bwd_nm* transform bits on the fp32 tier.  Default LG_F_BF16X3 (0x8000): the 3-way bf16
+# split, measured faster in the step than the kernel's f16x2 default on the same box (r05r:
+# 48.2 / 37.2 against 50.2 / 38.1 us for layers 2 / 1, step 0.5848 against 0.5882 ms; VERDICT
+# r04 item 4's "restore bf16x3 unless f16x2 is >= 3 % faster").  LEAKGNN_GCN_BWD_NM_FLAGS=0
+# selects the f16x2 split.
+GCN_BWD_NM_EXTRA_FLAGS = int(os.environ.get("LEAKGNN_GCN_BWD_NM_FLAGS", "0x8000"), 0)
 
 
 # ----------------------------------------------------------------------------- timing hook
