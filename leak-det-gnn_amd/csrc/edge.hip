@@ -411,6 +411,7 @@ struct EdgeScatter {
     float nscale = 1.f;             // its dropout scale
     float* nslab = nullptr;         // per workgroup: [dW1 HID * D][db1 HID][dw2 HID]
     double* ndslab = nullptr;       // per workgroup: db2
+    lg_fastdiv fdT{};               // division by tpw (SCAT / STREAM tile -> window, slot)
 };
 
 // dh rows of window `win` (SCAT): node n = a slot of 16 (D = 64) lanes, kScatNodes nodes per lane
@@ -674,12 +675,18 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     // this workgroup's k-th tile: tile blockIdx.x + k gridDim.x of the (B, P) row space, or
     // (SCAT) tile k % tpw of window blockIdx.x + (k / tpw) gridDim.x; rows [rbase, rlim) count
     const int64_t gstep = gridDim.x;
+    // WIN: tile k -> (its window's rank kq(k) among this workgroup's windows, its tile kr(k) within
+    // the window), on 32-bit fastdiv (a 64-bit division by the runtime tpw was ~60 scalar
+    // instructions, evaluated several times per tile: 6,565 SALU per wave, PMC r04 / r05)
+    auto kq = [&](int64_t k) -> uint32_t { return lg_div(static_cast<uint32_t>(k), sc.fdT); };
+    auto kr = [&](int64_t k) -> uint32_t { return static_cast<uint32_t>(k) - kq(k) * static_cast<uint32_t>(sc.tpw); };
+    auto kwin = [&](int64_t k) -> uint32_t { return blockIdx.x + kq(k) * static_cast<uint32_t>(gstep); };
     auto rbase = [&](int64_t k) -> int64_t {
-        if constexpr (WIN) return (blockIdx.x + (k / sc.tpw) * gstep) * sc.P + (k % sc.tpw) * G::TR;
+        if constexpr (WIN) return static_cast<int64_t>(kwin(k)) * sc.P + kr(k) * G::TR;
         return (blockIdx.x + k * gstep) * G::TR;
     };
     auto rlim = [&](int64_t k) -> int64_t {
-        if constexpr (WIN) return std::min<int64_t>(BP, (blockIdx.x + (k / sc.tpw) * gstep + 1) * sc.P);
+        if constexpr (WIN) return std::min<int64_t>(BP, (static_cast<int64_t>(kwin(k)) + 1) * sc.P);
         return BP;
     };
     const int64_t nk = WIN ? (blockIdx.x < sc.B ? sc.tpw * ((sc.B - blockIdx.x + gstep - 1) / gstep) : 0)
@@ -692,7 +699,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     auto sslot = [&](int64_t k, int off, uint32_t& b, uint32_t& slot) {
         const int64_t r = rbase(k) + off;
         const bool ok = r < rlim(k);
-        b = ok ? static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep) : 0u;
+        b = ok ? kwin(k) : 0u;
         slot = ok ? static_cast<uint32_t>(r - static_cast<int64_t>(b) * sc.P) : 0u;
     };
     uint32_t hpipe[G::HPT];  // STREAM: pipe ids of the hidden-slot rows, a tile ahead of their loads
@@ -784,15 +791,15 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     uint2 evn = uint2{0u, 0u};  // the next tile's event block, a uint2 per thread
     auto load_evblock = [&](int64_t k) {
         const int t = min(static_cast<int>(threadIdx.x), sc.bw / 2 - 1);
-        evn = reinterpret_cast<const uint2*>(sc.sblk + (k % sc.tpw) * sc.bw)[t];
+        evn = reinterpret_cast<const uint2*>(sc.sblk + kr(k) * sc.bw)[t];
     };
     auto store_evblock = [&](int64_t k) {
         if (static_cast<int>(threadIdx.x) < sc.bw / 2) reinterpret_cast<uint2*>(evb + (k & 1) * sc.bw)[threadIdx.x] = evn;
     };
     auto scatter_tile = [&](int64_t kk) {
-        const uint32_t win = static_cast<uint32_t>(blockIdx.x + (kk / sc.tpw) * gstep);
+        const uint32_t win = kwin(kk);
         edge_stream_scatter<D>(sc, evb + (kk & 1) * sc.bw, dpl, lacc, g0l, win, DPS);
-        if (sc.nzero > 0 && kk % sc.tpw == sc.tpw - 1) edge_stream_zero<D>(sc, g0l, win);
+        if (sc.nzero > 0 && kr(kk) == static_cast<uint32_t>(sc.tpw - 1)) edge_stream_zero<D>(sc, g0l, win);
     };
     auto post_g0 = [&]() {  // graw (this thread's 4 channels, threads < D / 4) -> g0l
         if (threadIdx.x < D / 4) {
@@ -805,7 +812,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         }
     };
     auto load_graw = [&](int64_t k) {
-        const uint32_t win = static_cast<uint32_t>(min<int64_t>(blockIdx.x + (k / sc.tpw) * gstep, sc.B - 1));
+        const uint32_t win = min(kwin(k), sc.B - 1);
         graw = ld4(gsrc + (sc.dpool ? static_cast<int64_t>(win) * D : 0) + 4 * sf);
     };
     load_ids(0);
@@ -1025,10 +1032,10 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
             if constexpr (STREAM) store_evblock(k + 1);
         }
         if constexpr (SCAT) {
-            if (k % sc.tpw == sc.tpw - 1 && k + 1 < nk) {  // a window's last tile (not the workgroup's last window)
+            if (kr(k) == static_cast<uint32_t>(sc.tpw - 1) && k + 1 < nk) {  // a window's last tile (not the workgroup's last window)
                 __syncthreads();                            // every wave's dpipe rows of the window are stored
                 edge_scatter_window<D, kScatNodesLoop>(sc, icsr, dpipe,
-                                                       static_cast<uint32_t>(blockIdx.x + (k / sc.tpw) * gstep));
+                                                       kwin(k));
             }
         }
     }
@@ -1084,7 +1091,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
         if (nk > 0) {  // the last window's node gradients (its dpipe rows were stored before the barriers above)
             __syncthreads();
             edge_scatter_window<D, kScatNodesTail>(sc, icsr, dpipe,
-                                                   static_cast<uint32_t>(blockIdx.x + ((nk - 1) / sc.tpw) * gstep));
+                                                   kwin(nk - 1));
         }
     }
     if constexpr (STREAM) {
@@ -1304,6 +1311,7 @@ int edge_bwd_scatter_impl(const int64_t* ends, const float* h, const float* w1, 
                        reinterpret_cast<const int4*>(sched + sched_hdr[10]),
                        reinterpret_cast<const uint32_t*>(sched + sched_hdr[11]), sched + sched_hdr[12],
                        sched_hdr[9], sched_hdr[6], sched_hdr[8], sched_hdr[7], kEdgeLab(flags)};
+        sc.fdT = lg_make_fastdiv(static_cast<uint32_t>(std::max(1, sc.tpw)));
         // STREAM when the open nodes' sums fit beside the images (L-TOWN-A at D = 64: 23 of them)
         if (edge_stream_lds(D, flags, sc) <= 160 * 1024) {
             if (pool_sc) {
@@ -1332,6 +1340,7 @@ int edge_bwd_scatter_impl(const int64_t* ends, const float* h, const float* w1, 
     EdgeScatter sc{inc_rowptr, inc_item, dpool, dh, static_cast<uint32_t>(N), static_cast<uint32_t>(P),
                    static_cast<uint32_t>(B), (flags & LG_F_NODE_MAJOR) ? 1 : 0,
                    static_cast<int>(cdiv(P, tile_rows(D))), nullptr, nullptr, nullptr, 0, 0, 0, 0, kEdgeLab(flags)};
+    sc.fdT = lg_make_fastdiv(static_cast<uint32_t>(std::max(1, sc.tpw)));
     return edge_bwd_impl(ends, h, w1, w2, hid, dlogits, ldo, dpipe, dw1, db1, dw2, db2, B, N, P, D, hidden, flags,
                          dropout_p, workspace, ws_bytes, stream, &sc);
 }
