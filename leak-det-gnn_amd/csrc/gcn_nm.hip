@@ -1332,9 +1332,11 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
     const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmBwdWaves3);
-    const int64_t tend = sc.end;
+    // 32-bit scalar tile indices (ntiles < 2^26; see k_gcn_fwd_pc): no 64-bit compares in VGPR pairs
+    const int32_t tend = static_cast<int32_t>(sc.end), tfirst = static_cast<int32_t>(sc.first),
+                  tstride = static_cast<int32_t>(sc.stride);
 
-    auto tile_coords = [&](int64_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
+    auto tile_coords = [&](int32_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
         const bool valid = tile < tend;
         const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
         const uint32_t grp = lg_div(t32, fdN);
@@ -1408,7 +1410,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     auto pslot_of = [&](uint32_t i) -> int { return X0 ? __builtin_amdgcn_readfirstlane(x0.pos_slot[i]) : -1; };
     {
         uint32_t n0, b00, nb00;
-        tile_coords(sc.first, n0, b00, nb00);
+        tile_coords(tfirst, n0, b00, nb00);
         issue(nm_rec(tab, N + n0), n0, b00, nb00, pslot_of(n0));  // schedule section
     }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
@@ -1469,14 +1471,14 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
     for (int mt = 0; mt < (NB ? G::CH : 1); ++mt) nbacc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int64_t tile = sc.first; tile < tend; tile += sc.stride) {
+    for (int32_t tile = tfirst; tile < tend; tile += tstride) {
         const uint32_t n = cn, b0 = cb0;
         const int e0 = cur.e0, e1 = cur.e1, self = cur.self;
         uint32_t tlo[G::K];
 #pragma unroll
         for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
         uint32_t nn, nb0, nnb;
-        tile_coords(tile + sc.stride, nn, nb0, nnb);
+        tile_coords(tile + tstride, nn, nb0, nnb);
         const NmRec nxt = nm_rec(tab, N + nn);
         const int nslot = pslot_of(nn);
         asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
