@@ -705,9 +705,12 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // W (fp32, x fold) and bias to LDS by the whole workgroup (F16: and the max |W|), and the
     // records of the workgroup's first kPcRecs tiles (every load in flight before the first store)
     int32_t* recs = reinterpret_cast<int32_t*>(lds + LY::COFF);
-    const int nrec = kPcWsplit ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
-    uint32_t* wrdy = ctr + 1;  // kPcWsplit: consumer waves done staging W
-    if constexpr (kPcWsplit) {
+    // the split W staging pays on layer 0 (X0: -1 us in the step) and costs the dense layers ~1 us
+    // (r05w, same box, in-graph: 22.1-22.5 against 21.0-21.1 us), so only X0 takes it
+    constexpr bool kWs = kPcWsplit && X0;
+    const int nrec = kWs ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    uint32_t* wrdy = ctr + 1;  // kWs: consumer waves done staging W
+    if constexpr (kWs) {
         if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
         if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
         if (threadIdx.x == 0) {
@@ -755,7 +758,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (threadIdx.x == 0) *ctr = 0u;
     }
     __syncthreads();
-    if (kPcWsplit && !producer) {  // the consumers' W staging (all loads in flight before the first store)
+    if (kWs && !producer) {  // the consumers' W staging (all loads in flight before the first store)
         constexpr int CT = 64 * kPcProd * NC, W4 = D * D / 4, WPER = (W4 + CT - 1) / CT;
         const int ct = static_cast<int>(threadIdx.x) - 64 * kPcProd;
         f32x4 wv[WPER];
@@ -1065,7 +1068,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     int sw = 0;  // F16: W's scale exponent
     if constexpr (F16) {
         uint32_t m = 0;
-        for (int w = kPcWsplit ? kPcProd : 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
+        for (int w = kWs ? kPcProd : 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
         sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
     }
     lg_bf16x8 wf[NP][G::CH][KS];
