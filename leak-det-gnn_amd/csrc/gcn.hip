@@ -761,16 +761,16 @@ extern "C" int lg_spmm(const int32_t* rowptr, const int32_t* col, const float* w
 // fused kernels' 32 / 64; models/gcn.py).  A thread owns four consecutive columns of one row
 // (VEC, when C and both row strides are multiples of 4 and the bases 16-byte aligned) or one
 // column; consecutive threads take consecutive columns, so a row's reads and writes coalesce.
-template <bool VEC>
+template <bool VEC, typename IX>  // IX: uint32_t when N * C < 2^32 (no 64-bit division per item)
 __global__ void __launch_bounds__(256) k_spmm_cols(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                    const float* __restrict__ w, const float* __restrict__ x,
                                                    int64_t ldx, const float* __restrict__ bias, float* __restrict__ y,
                                                    int64_t ldy, int64_t N, int64_t C) {
     constexpr int V = VEC ? 4 : 1;
-    const int64_t CV = C / V, total = N * CV;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t n = i / CV, c = (i - n * CV) * V;
+    const IX CV = static_cast<IX>(C / V), total = static_cast<IX>(N) * CV;
+    for (IX i = static_cast<IX>(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += static_cast<IX>(gridDim.x) * blockDim.x) {
+        const IX nq = i / CV;
+        const int64_t n = nq, c = static_cast<int64_t>(i - nq * CV) * V;
         const int e0 = rowptr[n], e1 = rowptr[n + 1];
         if constexpr (VEC) {
             f32x4 acc = bias ? ld4(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -800,8 +800,14 @@ extern "C" int lg_spmm_cols(const int32_t* rowptr, const int32_t* col, const flo
                      reinterpret_cast<uintptr_t>(y) % 16 == 0 && (!bias || reinterpret_cast<uintptr_t>(bias) % 16 == 0);
     const int64_t items = N * (vec ? C / 4 : C);
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((items + 255) / 256, 64LL * lg_num_cus())));
-    if (vec) lg_launch(k_spmm_cols<true>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
-    else lg_launch(k_spmm_cols<false>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+    const bool i32 = items + 256LL * grid < (int64_t{1} << 32);
+    if (vec) {
+        if (i32) lg_launch(k_spmm_cols<true, uint32_t>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+        else lg_launch(k_spmm_cols<true, int64_t>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+    } else {
+        if (i32) lg_launch(k_spmm_cols<false, uint32_t>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+        else lg_launch(k_spmm_cols<false, int64_t>, grid, 256, 0, s, rowptr, col, w, x, ldx, bias, y, ldy, N, C);
+    }
     LG_RET_IF_LAUNCH_FAILED();
     return LG_OK;
 }
