@@ -301,6 +301,9 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) sg[reg] = sigm(a0[reg] + hp[reg]);
                 grz[g][u][lane] = sg;
+                // the r / z waves store their own gate (the n waves' phase between the barriers is
+                // the step's critical path; it keeps the n, W_hn h + b_hn and h stores)
+                if (SAVE && valid) st4(gates + (static_cast<int64_t>(t) * Nseq + seq) * 4 * H + g * H + 16 * u + 4 * q, sg);
             }
             __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hbs
             if (g == 2) {
@@ -316,9 +319,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                     const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
                     if (hs) st4(hs + rw * H + 16 * u + 4 * q, hcur);
                     if constexpr (SAVE) {
-                        float* gp = gates + rw * 4 * H + 16 * u + 4 * q;
-                        st4(gp, r);
-                        st4(gp + H, z);
+                        float* gp = gates + rw * 4 * H + 16 * u + 4 * q;  // r, z: stored by their waves
                         st4(gp + 2 * H, n);
                         st4(gp + 3 * H, hp);
                     }
