@@ -810,13 +810,18 @@ def main() -> None:
         opt.step()  # clip_grad_norm_(1.0) + AdamW
         return loss
 
-    for _ in range(args.warmup):
-        step()
     eager_step = step
     if not args.eager:
-        # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay)
+        # the whole step as ONE replayed HIP graph (models/graph_step.py; dropout re-drawn per replay;
+        # the capture runs its own 3 eager steps first)
         from models.graph_step import CapturedTrainStep
         step = CapturedTrainStep(model, loss_fn, opt, (residual, tfeat), label, clip=None, warmup=3)
+    # the W untimed warm-up steps are steps of the timed kind: graph replays.  (Until round 5 they
+    # were eager steps before the capture, so the timed region began with the graph's first
+    # replays, whose one-time device-side cost, ~0.3 ms, the driver's K = 20 amortised over
+    # fewer steps than the builder's K = 50: VERDICT r05 weak 8.)
+    for _ in range(args.warmup):
+        step()
     timer = ops.KernelTimer(["gcn_fwd", "gcn_fwd_l0", "gcn_bwd", "gcn_bwd_l0", "node_init", "gru_fwd", "gru_bwd",
                              "edge_fwd", "edge_bwd", "pipe_scatter", "pool_head", "pool_head_bwd", "linear_dw"])
     ops.set_kernel_timer(timer)

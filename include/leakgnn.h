@@ -153,17 +153,20 @@ int lg_cross_entropy_bwd(const float* logits, const int64_t* target, const float
 
 /* Training-step tail: torch.nn.utils.clip_grad_norm_(params, max_norm) then
  * torch.optim.AdamW.step() (reference train_detector.py:313-317), ONE launch (ABI 23; two
- * before).
+ * before), two when the parameters need more 1024-element slices than the device has CUs.
  *   table : int64 [T][4] (HOST array) device addresses of (param, grad, exp_avg, exp_avg_sq), fp32
  *   sizes : int64 [T] (HOST array) element counts, T <= 48 (passed by value to the launches, so
  *           captured launches need no host copy)
- *   step  : device fp32 [2]: step[0] the AdamW step counter (incremented); step[1] the launch's
- *           workgroup ticket counter, read as uint32, which must be 0 between launches (zeros
- *           at creation; it is reset by the launch itself)
+ *   step  : device fp32 [4] (ABI 25; [2] before): step[0] the AdamW step counter (incremented);
+ *           step[1] the launch's workgroup arrival / ticket counter, read as uint32, which must
+ *           be 0 between launches (zeros at creation; the launch resets it); step[2] an error
+ *           word (uint32, sticky): nonzero when a grid-barrier wait timed out, results invalid;
+ *           step[3] reserved
  *   max_norm <= 0: no clipping.  norm_out (device fp32, may be NULL): the pre-clip total norm.
- *   workspace: lg_clip_adamw_workspace_bytes(sizes, T) bytes (unused since ABI 23; still checked
- *           non-NULL).
- * The norm is summed in fp64 in a fixed order (deterministic). */
+ *   workspace: lg_clip_adamw_workspace_bytes(sizes, T) bytes (ABI 25: one fp64 partial sum of
+ *           squares per slice; each workgroup reads and writes only its own gradient slice).
+ * The norm is summed in fp64 in a fixed order (deterministic; the one- and two-launch forms
+ * give identical bits). */
 int64_t lg_clip_adamw_workspace_bytes(const int64_t* sizes, int T);
 int lg_clip_adamw(const int64_t* table, const int64_t* sizes, int T, float* step, float lr, float beta1,
                   float beta2, float eps, float weight_decay, float max_norm, float* norm_out, void* workspace, int64_t ws_bytes,

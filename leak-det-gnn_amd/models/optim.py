@@ -7,8 +7,9 @@ The reference ends every step with
 
 which torch runs as ~11 launches for the detector's ~60k parameters (foreach norms, the
 norm of norms, clamp, foreach mul, the fused AdamW).  ClipAdamW does both in ONE HIP
-launch (lg_clip_adamw, csrc/optim.hip: every workgroup forms the whole fp64 norm in a fixed
-order, then updates its slice): the same AdamW arithmetic (decoupled weight
+launch (lg_clip_adamw, csrc/optim.hip: every workgroup sums the squares of its own slice, a
+grid barrier, then every workgroup sums the slice partials in a fixed order and updates its
+slice; two launches past one slice per CU): the same AdamW arithmetic (decoupled weight
 decay, bias corrections, amsgrad=False) on gradients scaled by
 min(1, max_norm / (||g||_2 + 1e-6)), written back to .grad as clip_grad_norm_ does.  The
 step counter is device-resident, so the step can be captured in a HIP graph
@@ -39,7 +40,7 @@ class ClipAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                       max_norm=max_norm, capturable=True))
         self.last_grad_norm: Optional[torch.Tensor] = None
-        self._ws: dict = {}  # group index -> per-slice partial-norm workspace
+        self._ws: dict = {}  # group index -> per-slice partial-norm workspace (fp64 per 1024 elements)
         # ops.SeedSlots whose next draw step() makes in its own launch (lg_clip_adamw_seeds):
         # set by graph_step.CapturedTrainStep while it captures the step, so the step ends by
         # drawing the next replay's dropout seeds instead of starting with a launch of its own
@@ -47,9 +48,12 @@ class ClipAdamW(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict) -> None:
         super().load_state_dict(state_dict)
-        for group in self.param_groups:  # word 1 is the launch's ticket counter: 0 between launches
-            if torch.is_tensor(group.get("step_t")):
-                group["step_t"][1:].zero_()
+        for group in self.param_groups:  # words 1-3 are the launch's counter / error word: 0 between launches
+            st = group.get("step_t")
+            if torch.is_tensor(st):
+                if st.numel() < 4:  # a state dict from before ABI 25 ([step, ticket])
+                    st = group["step_t"] = torch.cat([st.reshape(-1)[:1], st.new_zeros(3)])
+                st[1:].zero_()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -76,8 +80,10 @@ class ClipAdamW(torch.optim.Optimizer):
                 if not st:
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
-            if "step_t" not in group:  # [step, the launch's workgroup ticket counter (uint32 bits, 0 between launches)]
-                group["step_t"] = torch.zeros(2, dtype=torch.float32, device=params[0].device)
+            if "step_t" not in group:
+                # [step, the launch's arrival / ticket counter (uint32 bits, 0 between launches),
+                #  error word (uint32, nonzero if a grid-barrier wait timed out), reserved]
+                group["step_t"] = torch.zeros(4, dtype=torch.float32, device=params[0].device)
             if self.last_grad_norm is None:
                 self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=params[0].device)
             if len(params) > 48:

@@ -245,7 +245,80 @@ def test_clip_adamw_matches_torch():
         # the device step counter is committed by the launch's last workgroup, whose ticket
         # counter (word 1, uint32) is back at 0 between launches
         st = ob.param_groups[0]["step_t"]
-        assert st[0].item() == it + 1 and st[1:].view(torch.int32).item() == 0
+        assert st[0].item() == it + 1 and st[1:3].view(torch.int32).tolist() == [0, 0]
+
+
+def _adam_trajectory(shapes, steps=3, seed=11, max_norm=1.0, env=None, monkeypatch=None):
+    """ClipAdamW over `steps` steps on fresh parameters of `shapes` (seeded), gradients drawn
+    per step (step 1 under the clip threshold); returns the final parameters, the last
+    clipped gradients, the norms and the step word."""
+    from models.optim import ClipAdamW
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
+    try:
+        gen = torch.Generator(device=DEV).manual_seed(seed)
+        ps = [torch.randn(s, device=DEV, generator=gen).requires_grad_(True) for s in shapes]
+        opt = ClipAdamW(ps, lr=1e-2, weight_decay=1e-2, max_norm=max_norm)
+        norms = []
+        for it in range(steps):
+            for p in ps:
+                p.grad = torch.randn(p.shape, device=DEV, generator=gen) * (0.05 if it == 1 else 1.0)
+            opt.step()
+            norms.append(opt.last_grad_norm.clone())
+        torch.cuda.synchronize()
+        return ([p.detach().clone() for p in ps], [p.grad.clone() for p in ps], torch.cat(norms),
+                opt.param_groups[0]["step_t"].clone())
+    finally:
+        for k in (env or {}):
+            monkeypatch.delenv(k, raising=False)
+
+
+def test_clip_adamw_barrier_under_skew_and_two_launch_form(monkeypatch):
+    """the one-launch clip + AdamW must not let any workgroup see another's
+    clipped gradients or a partial norm.  The odd slices are held back ~0.2 ms before their
+    partial sums (LEAKGNN_LAB_ADAM_SKEW: s_sleep rounds), so without a working grid barrier the
+    even slices would clip with a norm missing half its partials (the workspace holds the
+    previous step's).  Parameters, clipped gradients and norms must be BIT-identical to the
+    unskewed launch and to the two-launch form (same partials, same summation), and the error
+    word must stay 0.  Shapes: the detector's parameter set (60 slices, one launch)."""
+    from models.detector import LeakDetector
+    sensors, pipes = lta_ids()
+    shapes = [tuple(p.shape) for p in LeakDetector(LTA_INP, sensors, pipes).parameters()]
+    runs = {name: _adam_trajectory(shapes, env=env, monkeypatch=monkeypatch) for name, env in (
+        ("plain", {}), ("skew", {"LEAKGNN_LAB_ADAM_SKEW": "24"}), ("two_launch", {"LEAKGNN_LAB_ADAM_TWO_LAUNCH": "1"}))}
+    base = runs["plain"]
+    for name, (ps, gs, norms, st) in runs.items():
+        assert st[1:3].view(torch.int32).tolist() == [0, 0], f"{name}: counter / error word {st.tolist()}"
+        assert st[0].item() == 3
+        assert torch.equal(norms, base[2]), f"{name}: norms {norms.tolist()} vs {base[2].tolist()}"
+        for k, (p, g) in enumerate(zip(ps, gs)):
+            assert torch.equal(p, base[0][k]), f"{name}: param {k} differs"
+            assert torch.equal(g, base[1][k]), f"{name}: clipped grad {k} differs"
+
+
+def test_clip_adamw_two_million_parameters_matches_torch():
+    """~2.1M parameters (2,050 slices, more than the CU count: the two-launch form)
+    with the clip active, against torch's clip_grad_norm_ + fused AdamW at fp32 rounding."""
+    from models.optim import ClipAdamW
+    torch.manual_seed(7)
+    shapes = [(1024, 1024), (1000,), (1024, 1000), (37, 3), (5,)]
+    pa = [torch.randn(s, device=DEV).requires_grad_(True) for s in shapes]
+    pb = [p.detach().clone().requires_grad_(True) for p in pa]
+    oa = torch.optim.AdamW(pa, lr=1e-2, weight_decay=1e-2, fused=True)
+    ob = ClipAdamW(pb, lr=1e-2, weight_decay=1e-2, max_norm=1.0)
+    for it in range(3):
+        for a, b in zip(pa, pb):
+            g = torch.randn_like(a) * (1e-5 if it == 1 else 1.0)
+            a.grad, b.grad = g.clone(), g.clone()
+        na = torch.nn.utils.clip_grad_norm_(pa, 1.0)
+        oa.step()
+        ob.step()
+        assert_close(ob.last_grad_norm[0], na, rtol=1e-6, what=f"total norm, step {it}")
+        for k, (a, b) in enumerate(zip(pa, pb)):
+            assert_close(b.grad, a.grad, rtol=1e-6, what=f"clipped grad {k}, step {it}")
+            assert_close(b, a, rtol=1e-6, what=f"param {k} after step {it}")
+    st = ob.param_groups[0]["step_t"]
+    assert st[0].item() == 3 and st[1:3].view(torch.int32).tolist() == [0, 0]
 
 
 def test_cross_entropy_matches_torch():

@@ -105,7 +105,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 24
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 25
     assert lib.lg_timing_arm(-1) == -1 and lib.lg_timing_disarm() == 0 and lib.lg_timing_elapsed(0, None) == -1
     assert lib.lg_nm_table_build(None, None, 661, None, None, None) == -1
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
