@@ -179,6 +179,12 @@ int lg_clip_adamw_seeds(const int64_t* table, const int64_t* sizes, int T, float
                         int64_t ws_bytes, uint64_t* seed_slots, int64_t n_slots, uint64_t* seed_state,
                         lg_stream_t stream);
 
+/* Hand-off error word (ABI 25; no reference counterpart).  The producer / consumer trunk
+ * forward (k_gcn_fwd_pc) bounds every LDS hand-off poll; a poll that runs out sets a bit of a
+ * device word (1: producer / W staging, 2: consumer), and that launch's results are invalid.
+ * lg_spin_errors copies the word to *out (synchronous, device-wide) and zeroes it if reset. */
+int lg_spin_errors(uint32_t* out, int reset);
+
 /* Kernel timing (bench.py; no reference counterpart — the reference has no kernels).
  * lg_timing_arm(slot): the NEXT library kernel launch on this host thread that is the main
  * kernel of an entry point (lg_gcn_fwd[_nm], lg_gcn_bwd[_nm], lg_edge_head_fwd/bwd,
@@ -400,7 +406,8 @@ int lg_gcn_bwd_nm_bits(const int32_t* nodetab_t, const int32_t* pairs_t, const f
  * MASK_IN) with the tile's own x block from (xs0, x0bits); pos_slot_t = the transposed table's
  * schedule-section slots.  The node init and the layer share one Dropout (detector.py:190,
  * 201): flags' LG_F_DROPOUT and dropout_p describe both.  lg_node_init_expand materialises x0
- * (diagnostics, tests). */
+ * (diagnostics, tests).  lg_gcn_fwd_nm_x0 runs on the producer / consumer kernel only: LG_F_NM3
+ * and LG_F_F32_MFMA return LG_EUNSUPPORTED (ABI 25; ignored before). */
 int lg_node_init_bits_fwd(const int32_t* sensor_slot, const int64_t* sensor_idx, const float* h_s, const float* W,
                           const float* bias, float* xs0, uint16_t* x0bits, int64_t B, int64_t N, int64_t S,
                           int64_t Ds, int64_t D, int flags, float dropout_p, uint64_t seed, uint32_t salt,

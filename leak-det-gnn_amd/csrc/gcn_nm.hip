@@ -499,10 +499,22 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #ifndef LG_PC_RING
 #define LG_PC_RING 4
 #endif
+// Neighbour blocks per tile in the producers' two-tile prefetch.  A tile with more neighbours
+// issues the rest when it is accumulated, and waiting for those youngest loads waits for the
+// other buffer's tile too (vmcnt counts in order): at 3, the 32 % of L-TOWN-A's tiles with a
+// fourth neighbour (degree 4 with the self loop) exposed a full memory round trip each.  4
+// (168 VGPRs, 3 waves per SIMD) leaves that to the 3.5 % of degree 5-6 (r06c, isolated, same
+// box: layer 1 21.5-22.8 -> 20.2-21.0 us).  The X0 layer loads one 2-byte mask word per
+// neighbour, so it prefetches all kLgNmInline.
 #ifndef LG_PC_NPF
-#define LG_PC_NPF 3
+#define LG_PC_NPF 4
 #endif
 constexpr int kPcRing = LG_PC_RING;
+// consumer waves per producer wave (4 producers per workgroup)
+#ifndef LG_PC_NC
+#define LG_PC_NC 2
+#endif
+constexpr int kPcNC = LG_PC_NC;
 // The node-table records of a workgroup's first kPcRecs tiles are staged in LDS with W, so a
 // producer's record is an LDS read after its tile draw instead of a scalar load from L2 (whose
 // latency sat between drawing tile t + 2 and issuing its loads, every tile); later tiles (large
@@ -587,7 +599,7 @@ struct PcLds {  // floats
     static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
-static_assert(kPcRing % 2 == 0, "ring slots alternate between consumers");
+static_assert(kPcRing >= kPcNC, "a ring slot per consumer at least");
 
 __device__ __forceinline__ uint32_t pc_load_acq(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -595,12 +607,19 @@ __device__ __forceinline__ uint32_t pc_load_acq(const uint32_t* p) {
 __device__ __forceinline__ void pc_store_rel(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// The hand-off polls are bounded (a broken protocol ends the launch instead of hanging the
+// GPU); a poll that runs out sets a bit of g_pc_spin_err (1: a producer's or a W-staging wait,
+// 2: a consumer's wait for its tile), which lg_spin_errors reads back -- the launch's results
+// are then invalid.  The tests assert it stays 0 (tests/conftest.py, after every GPU module).
+__device__ uint32_t g_pc_spin_err;
 // wait until *p >= v (bounded: ~2^20 polls)
 __device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
     for (int it = 0; it < (1 << 20); ++it) {
         if (pc_load_acq(p) >= v) return;
         __builtin_amdgcn_s_sleep(1);
     }
+    __hip_atomic_fetch_or(&g_pc_spin_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the atomic must not shift the producers' vmcnt counts
 }
 // wait until *p >= v (true) or the producer has finished with *fin < v tiles (false); bounded
 __device__ __forceinline__ bool pc_wait_or_fin(const uint32_t* p, const uint32_t* fin, uint32_t v) {
@@ -609,6 +628,8 @@ __device__ __forceinline__ bool pc_wait_or_fin(const uint32_t* p, const uint32_t
         if (pc_load_acq(fin) < v) return false;
         __builtin_amdgcn_s_sleep(1);
     }
+    __hip_atomic_fetch_or(&g_pc_spin_err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return false;
 }
 
@@ -629,7 +650,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
              uint32_t salt, uint16_t* __restrict__ ymask, PcX0 x0) {
     using G = NmGeo<D>;
     using LY = PcLds<D, kPcProd, NC>;
-    constexpr int NPF = LG_PC_NPF;
+    constexpr int NPF = X0 ? kLgNmInline : LG_PC_NPF;
     constexpr int KS = D / 32;
     constexpr int NP = BF ? 1 : 3;
     constexpr int R = kPcRing;
@@ -964,16 +985,18 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 }
             }
             if (e0 + NPF < e1) {  // the rest of the row (degree > NPF): all inline blocks in flight at once
-                constexpr int NI = kLgNmInline - NPF;
-                f32x4 va[NI][G::K];
-                uint32_t vb[NI];
+                if constexpr (NPF < kLgNmInline) {
+                    constexpr int NI = kLgNmInline - NPF;
+                    f32x4 va[NI][G::K];
+                    uint32_t vb[NI];
 #pragma unroll
-                for (int i = 0; i < NI; ++i) load_rest(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
+                    for (int i = 0; i < NI; ++i) load_rest(cur.p[NPF + i].x, e0 + NPF + i < e1, b0, lo[b], va[i], vb[i]);
 #pragma unroll
-                for (int i = 0; i < NI; ++i) {  // an absent entry: zero blocks at weight 0 (acc unchanged)
-                    const float wa = e0 + NPF + i < e1 ? __int_as_float(cur.p[NPF + i].y) : 0.f;
+                    for (int i = 0; i < NI; ++i) {  // an absent entry: zero blocks at weight 0 (acc unchanged)
+                        const float wa = e0 + NPF + i < e1 ? __int_as_float(cur.p[NPF + i].y) : 0.f;
 #pragma unroll
-                    for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], vb[i], k));
+                        for (int k = 0; k < G::K; ++k) pk_fma4(acc[k], wa, nbv(cur.p[NPF + i].x, va[i], vb[i], k));
+                    }
                 }
                 for (int e = e0 + kLgNmInline; e < e1; ++e) {
                     const int2 pa = pairs[e];
@@ -2203,8 +2226,9 @@ auto nm3_kernel(int flags) {
 }
 template <int D, bool DR, bool RL, bool X0>
 auto pc_kernel(bool bf16, bool f16) {
-    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, 2, X0>
-                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, 2, X0> : k_gcn_fwd_pc<D, DR, RL, false, false, 4, 2, X0>);
+    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, kPcNC, X0>
+                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, kPcNC, X0>
+                       : k_gcn_fwd_pc<D, DR, RL, false, false, 4, kPcNC, X0>);
 }
 
 // lg_gcn_fwd_nm_bits (x0 == NULL) and lg_gcn_fwd_nm_x0 (x the sensor rows, *x0 the rest)
@@ -2249,8 +2273,8 @@ int nm_fwd(const int32_t* nodetab, const int32_t* pairs, const float* x, const f
         } else {
             auto kern = x0 ? (relu ? pc_kernel<DD, DR, true, true>(bf16, f16) : pc_kernel<DD, DR, false, true>(bf16, f16))
                            : (relu ? pc_kernel<DD, DR, true, false>(bf16, f16) : pc_kernel<DD, DR, false, false>(bf16, f16));
-            const size_t dyn = PcLds<DD, 4, 2>::BYTES;
-            const int thr = 64 * 4 * 3;
+            const size_t dyn = PcLds<DD, 4, kPcNC>::BYTES;
+            const int thr = 64 * 4 * (1 + kPcNC);
             const int grid = nm_grid(kern, thr, dyn, ntiles, 4, 1);
             lg_launch(kern, grid, thr, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
                       salt, ymask, xz);
@@ -2286,6 +2310,9 @@ extern "C" int lg_gcn_fwd_nm_x0(const int32_t* nodetab_s, const int32_t* pairs_s
                                 uint64_t seed, uint32_t salt, lg_stream_t stream) {
     if (S < 0 || S > 0xFFFF || !x0bits || !node_bias || !xs0) return LG_EINVAL;
     if (S * B * D * 4 > static_cast<int64_t>(kNm3MaxBytes)) return LG_EUNSUPPORTED;
+    // the compressed layer-0 input runs on the producer / consumer kernel only: the nm3 and exact
+    // fp32 forms are refused rather than silently replaced
+    if (flags & (LG_F_NM3 | LG_F_F32_MFMA)) return LG_EUNSUPPORTED;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
     const float scale = drop && dropout_p >= 0.f && dropout_p < 1.f ? 1.0f / (1.0f - dropout_p) : 1.0f;
     const PcX0 x0{x0bits, node_bias, scale, static_cast<uint32_t>(S)};
@@ -2466,4 +2493,14 @@ extern "C" int lg_gcn_bwd_rows(const int32_t* nodetab_t, const int32_t* pairs_t,
     const int64_t L = D * D + 2 * D;
     const LgSlabSeg segs[2] = {{0, D * D, dW}, {D * D, D, db}};
     return lg_launch_slab_reduce_multi(slab, grid, L, segs, 2, nullptr, nullptr, s);
+}
+
+extern "C" int lg_spin_errors(uint32_t* out, int reset) {
+    if (!out) return LG_EINVAL;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pc_spin_err), sizeof(uint32_t)) != hipSuccess) return LG_EHIP;
+    if (reset) {
+        const uint32_t z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pc_spin_err), &z, sizeof(uint32_t)) != hipSuccess) return LG_EHIP;
+    }
+    return LG_OK;
 }

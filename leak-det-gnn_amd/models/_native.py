@@ -49,6 +49,7 @@ SIGNATURES = {
     "lg_clip_adamw": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _i64, _p]),
     "lg_clip_adamw_seeds": (_i32, [_p, _p, _i32, _p, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p, _i64, _p, _i64, _p,
                                    _p]),
+    "lg_spin_errors": (_i32, [_p, _i32]),
     "lg_timing_arm": (_i32, [_i32]),
     "lg_timing_disarm": (_i32, []),
     "lg_timing_elapsed": (_i32, [_i32, _p]),

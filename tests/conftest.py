@@ -33,3 +33,20 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _pc_spin_error_word(request):
+    """After every GPU test module: the trunk forward's bounded hand-off polls never ran out
+    (lg_spin_errors, include/leakgnn.h; a poll that runs out would leave that launch's results
+    invalid without failing a parity check on a lucky schedule)."""
+    yield
+    if not any(m.name == "gpu" for m in request.node.iter_markers()) or not gpu_available():
+        return
+    import ctypes
+    from models import _native
+    if _native._lib is None:
+        return
+    word = ctypes.c_uint32(0)
+    assert _native._lib.lg_spin_errors(ctypes.byref(word), 1) == 0
+    assert word.value == 0, f"k_gcn_fwd_pc hand-off poll ran out (error word {word.value:#x})"

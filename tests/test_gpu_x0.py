@@ -105,6 +105,12 @@ def test_layer0_x0_forward_and_backward_equal_dense(state, B, D, extra):
     ops.check(lib.lg_gcn_fwd_nm_x0(ops.ptr(mk.nodetab_s), ops.ptr(mk.pairs_s), ops.ptr(xs0), ops.ptr(bits),
                                    ops.ptr(nbias), ops.ptr(W), ops.ptr(b), ops.ptr(y_x), B, N, S, D, flags, p, 7, 1, st),
               "fwd x0")
+    # the nm3 / exact-fp32 forms have no compressed-input variant: refused, not silently replaced
+    for bad in (nat.LG_F_NM3, nat.LG_F_F32_MFMA):
+        rc = lib.lg_gcn_fwd_nm_x0(ops.ptr(mk.nodetab_s), ops.ptr(mk.pairs_s), ops.ptr(xs0), ops.ptr(bits),
+                                  ops.ptr(nbias), ops.ptr(W), ops.ptr(b), ops.ptr(y_x), B, N, S, D, flags | bad, p, 7, 1,
+                                  st)
+        assert rc == -2, f"flag {bad:#x} on the x0 layer: rc {rc} (LG_EUNSUPPORTED expected)"
     # the sums' order differs (sensor terms last): fp32 tier within 1e-6 of scale; the bf16
     # tier rounds z to bf16 before its single product, so one bf16 ulp (2^-8) of z can differ
     tol = 1e-3 if extra == "bf16" else 1e-6

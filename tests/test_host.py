@@ -5,6 +5,8 @@ from __future__ import annotations
 
 import ctypes
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -360,3 +362,44 @@ def test_pipe_schedule_rejects_bad_input():
     assert lib.lg_pipe_schedule_words(2, 3, 48) == -2
     rc, sc, rp, it = _schedule(lib, np.zeros((0, 2), np.int64), 3, 64)
     assert rc == 0 and int(sc[5]) == 0 and int(sc[9]) == 3  # no tiles; every node without pipes
+
+
+def _vm_ins(lines):
+    """(addr, mnemonic, operands, target) tuples for tools/check_vmcnt.check_kernel."""
+    out = []
+    for i, ln in enumerate(lines):
+        mn, _, ops = ln.partition(" ")
+        out.append((4 * i, mn, ops, None))
+    return out
+
+
+def test_vmcnt_checker_catches_an_early_copy():
+    """tools/check_vmcnt.py: a copy of a register whose load is in flight is
+    reported, in both modes; after the covering s_waitcnt it is not; vmcnt counts stores too."""
+    sys.path.insert(0, str(REPO / "tools"))
+    import check_vmcnt as cv
+    early = _vm_ins(["buffer_load_dwordx4 v[0:3], v8, s[0:3], 0 offen", "v_mov_b32_e32 v5, v1",
+                     "s_waitcnt vmcnt(0)", "v_add_f32_e32 v6, v0, v1", "s_endpgm"])
+    for copies_only in (False, True):
+        v = cv.check_kernel(early, copies_only=copies_only)
+        assert [a for a, _, _ in v] == [4], v
+    late = _vm_ins(["buffer_load_dwordx4 v[0:3], v8, s[0:3], 0 offen", "buffer_store_dword v9, v8, s[0:3], 0 offen",
+                    "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v5, v1", "s_endpgm"])
+    assert cv.check_kernel(late) == []
+    short = _vm_ins(["buffer_load_dwordx4 v[0:3], v8, s[0:3], 0 offen", "buffer_store_dword v9, v8, s[0:3], 0 offen",
+                     "s_waitcnt vmcnt(2)", "v_mov_b32_e32 v5, v1", "s_endpgm"])
+    assert [a for a, _, _ in cv.check_kernel(short)] == [12]
+
+
+def test_every_kernel_waits_for_its_loads():
+    """Every gfx950 kernel of the library passes tools/check_vmcnt.py: no instruction touches a
+    VGPR whose vector-memory load is still in flight (k_gcn_fwd_pc, whose producers issue their
+    prefetch through inline asm with hand-written vmcnt waits: no copy, select or spill of such
+    a register before its wait)."""
+    objs = sorted((PKG / "build").glob("*.o"))
+    if not objs:
+        pytest.skip("no build/*.o (run make)")
+    r = subprocess.run([sys.executable, str(REPO / "tools" / "check_vmcnt.py")] + [str(o) for o in objs],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "k_gcn_fwd_pc" in (REPO / "tools" / "check_vmcnt.py").read_text()
