@@ -504,10 +504,15 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 // other buffer's tile too (vmcnt counts in order): at 3, the 32 % of L-TOWN-A's tiles with a
 // fourth neighbour (degree 4 with the self loop) exposed a full memory round trip each.  4
 // (168 VGPRs, 3 waves per SIMD) leaves that to the 3.5 % of degree 5-6 (r06c, isolated, same
-// box: layer 1 21.5-22.8 -> 20.2-21.0 us).  The X0 layer loads one 2-byte mask word per
-// neighbour, so it prefetches all kLgNmInline.
+// box: layer 1 21.5-22.8 -> 20.2-21.0 us; in the step 21.1-21.2 -> 20.7-21.0, r06e).  The X0
+// layer (2-byte mask words per neighbour) measured best at 4 too: 6 (no rest-of-row path at all)
+// took 25.5 us in the step against 24.4-24.8 (r06e), its wider issue costing more than the 3.5 %
+// of degree-5/6 tiles' round trip.
 #ifndef LG_PC_NPF
 #define LG_PC_NPF 4
+#endif
+#ifndef LG_PC_NPF_X0
+#define LG_PC_NPF_X0 4
 #endif
 constexpr int kPcRing = LG_PC_RING;
 // consumer waves per producer wave (4 producers per workgroup)
@@ -532,6 +537,14 @@ constexpr int kPcRecs = LG_PC_RECS;
 #define LG_PC_WSPLIT 1
 #endif
 constexpr bool kPcWsplit = LG_PC_WSPLIT != 0;
+// lab: the split W staging on the dense layers too (LG_PC_WS_DENSE), and with it the node-table
+// records staged by the producer waves instead of read from L2 per tile (LG_PC_PREC)
+#ifndef LG_PC_WS_DENSE
+#define LG_PC_WS_DENSE 0
+#endif
+#ifndef LG_PC_PREC
+#define LG_PC_PREC 0
+#endif
 // producer wave priority (s_setprio; 0: the default, equal to the consumers').  Measured (r05m,
 // isolated train mode, two rounds): 2 and 3 within the box's noise of 0 (20.5-21.3 us each)
 #ifndef LG_PC_PRIO
@@ -650,7 +663,8 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
              uint32_t salt, uint16_t* __restrict__ ymask, PcX0 x0) {
     using G = NmGeo<D>;
     using LY = PcLds<D, kPcProd, NC>;
-    constexpr int NPF = X0 ? kLgNmInline : LG_PC_NPF;
+    constexpr int NPF = X0 ? LG_PC_NPF_X0 : LG_PC_NPF;
+    static_assert(NPF >= 1 && NPF <= kLgNmInline, "prefetch depth");
     constexpr int KS = D / 32;
     constexpr int NP = BF ? 1 : 3;
     constexpr int R = kPcRing;
@@ -727,16 +741,21 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // records of the workgroup's first kPcRecs tiles (every load in flight before the first store)
     int32_t* recs = reinterpret_cast<int32_t*>(lds + LY::COFF);
     // the split W staging pays on layer 0 (X0: -1 us in the step) and costs the dense layers ~1 us
-    // (r05w, same box, in-graph: 22.1-22.5 against 21.0-21.1 us), so only X0 takes it
-    constexpr bool kWs = kPcWsplit && X0;
-    const int nrec = kWs ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    // (r05w, same box, in-graph: 22.1-22.5 against 21.0-21.1 us: their producers then read every
+    // record from L2), so only X0 takes it -- unless the producers stage the records themselves
+    // (kPrecs: after the counter barrier, synchronised among the producer waves alone)
+    constexpr bool kWs = kPcWsplit && (X0 || LG_PC_WS_DENSE);
+    constexpr bool kPrecs = kWs && LG_PC_PREC && kPcRecs > 0;
+    const int nrec = (kWs && !kPrecs) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
     uint32_t* wrdy = ctr + 1;  // kWs: consumer waves done staging W
+    uint32_t* prdy = ctr + 2;  // kPrecs: producer waves done staging the records
     if constexpr (kWs) {
         if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
         if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
         if (threadIdx.x == 0) {
             *ctr = 0u;
             *wrdy = 0u;
+            *prdy = 0u;
         }
     } else {
         constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT, RPER = kPcRecs ? (4 * kPcRecs + NT - 1) / NT : 1;
@@ -779,6 +798,26 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         if (threadIdx.x == 0) *ctr = 0u;
     }
     __syncthreads();
+    if (kPrecs && producer) {  // the producers' record staging (the workgroup's first nrec tiles)
+        constexpr int PT = 64 * kPcProd, RP = (4 * kPcRecs + PT - 1) / PT;
+        lg_u32x4 rv[RP];
+#pragma unroll
+        for (int u = 0; u < RP; ++u) {  // quarter (i & 3) of record i >> 2
+            const int i = u * PT + static_cast<int>(threadIdx.x);
+            if (i < 4 * nrec) {
+                uint32_t n, b0, nb;
+                tile_coords(tfirst + (i >> 2) * tstride, n, b0, nb);
+                rv[u] = reinterpret_cast<const lg_u32x4*>(tab)[4 * (static_cast<size_t>(N) + n) + (i & 3)];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < RP; ++u) {
+            const int i = u * PT + static_cast<int>(threadIdx.x);
+            if (i < 4 * nrec) reinterpret_cast<lg_u32x4*>(recs)[i] = rv[u];
+        }
+        if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(prdy, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pc_wait(prdy, static_cast<uint32_t>(kPcProd));
+    }
     if (kWs && !producer) {  // the consumers' W staging (all loads in flight before the first store)
         constexpr int CT = 64 * kPcProd * NC, W4 = D * D / 4, WPER = (W4 + CT - 1) / CT;
         const int ct = static_cast<int>(threadIdx.x) - 64 * kPcProd;
@@ -1288,9 +1327,18 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 //   dW  += t^T x     (16x16x16, K = the tile's 16 rows; t and x columns split per tile)
 // The round-1 kernel (k_gcn_bwd_nm) walked rowptr -> pair -> block as dependent round trips
 // and ran dW and dx on f32 MFMA (4096 cycles per tile against 1536 here).
+#ifndef LG_NB3_SBPAD
+#define LG_NB3_SBPAD 16  // lab: 8 = the round-5 W^T plane stride at D = 64
+#endif
 template <int D, bool MASK_IN>
 struct Nb3Lds {
-    static constexpr int SB = D + 8;
+    // W^T plane row stride (halves).  The dx product reads a plane with ds_read_b128, lane (j, q)
+    // at row 16 mt + j, halves 32 s2 + 8 q; the lane groups {0-3, 12-15, 20-27}, ... then hit
+    // each bank once at 80 halves (40 dwords), twice at D + 8 = 72 (the round-5 layout, 2-way on
+    // all 24 plane reads of a tile; modelled with the guide's LDS banking, tools/lab/lds_banks.py).
+    // An XOR-swizzled tile and plane layout, conflict-free for every access, measured 48.8 ->
+    // 71 us (r06e: per-lane addresses pushed the kernel past 256 VGPRs into scratch).
+    static constexpr int SB = D == 64 ? D + LG_NB3_SBPAD : D + 8;
     static constexpr int WF = (3 * D * SB) / 2;          // W^T split parts (bf16), in floats
     static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
     static constexpr int L = D * D + 2 * D;               // slab row: dW, db, d(node bias)
@@ -1342,6 +1390,12 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     const int rl = lane / G::LPR, fg = lane % G::LPR;
     float* tl = tiles + wave * LY::TL;  // t tile [row][feature], later dx
     float* xl = tl + G::TILE;           // x tile [row][feature]
+    // LDS addresses: tile row r, 16-byte chunk c4 (rows padded to G::S floats); W^T plane element
+    // (row i, column o) at i * SB + o halves
+    auto tix = [&](int r, int c4) { return r * G::S + 4 * c4; };
+    auto tel = [&](int r, int c) { return r * G::S + c; };
+    auto wix = [&](int i, int o) { return i * SB + o; };
+    constexpr int WP = D * SB;  // halves per W^T plane
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MY ? yv : dy, bytes),
                                  xs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : bytes),
@@ -1464,13 +1518,13 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             const int o = i4 / (D / 4), c4 = 4 * (i4 % (D / 4));
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const int e = (c4 + c) * SB + o;
+                const int e = wix(c4 + c, o);
                 const float w = wv[u][c];
                 if constexpr (F16) {
                     const _Float16 h0 = static_cast<_Float16>(w * wsc);
                     const _Float16 h1 = static_cast<_Float16>(w * wsc - static_cast<float>(h0));
                     wsl[e] = __builtin_bit_cast(uint16_t, h0);
-                    wsl[D * SB + e] = __builtin_bit_cast(uint16_t, h1);
+                    wsl[WP + e] = __builtin_bit_cast(uint16_t, h1);
                     continue;
                 }
                 const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
@@ -1479,8 +1533,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                 const float r2 = r1 - __uint_as_float(static_cast<uint32_t>(h1) << 16);
                 const uint16_t h2 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r2));
                 wsl[e] = h0;
-                wsl[D * SB + e] = h1;
-                wsl[2 * D * SB + e] = h2;
+                wsl[WP + e] = h1;
+                wsl[2 * WP + e] = h2;
             }
         }
     }
@@ -1607,8 +1661,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         wave_sync_nm();
 #pragma unroll
         for (int k = 0; k < G::K; ++k) {
-            st4(tl + (G::RPI * k + rl) * G::S + 4 * fg, acc[k]);
-            st4(xl + (G::RPI * k + rl) * G::S + 4 * fg, xv[k]);
+            st4(tl + tix(G::RPI * k + rl, fg), acc[k]);
+            st4(xl + tix(G::RPI * k + rl, fg), xv[k]);
         }
         wave_sync_nm();
         // dW += t^T x over the tile's 16 rows: A[o][r] = t[r][o], B[r][i] = x[r][i], K = rows 4q..4q+3
@@ -1619,14 +1673,14 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int ni = 0; ni < G::CH; ++ni) {
                 f32x4 v;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j] * xsc;
+                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[tel(4 * q + kk, 16 * ni + j)] * xsc;
                 split2_f16_x4(v, xb[ni][0], xb[ni][1]);
             }
 #pragma unroll
             for (int mo = 0; mo < G::CH; ++mo) {
                 f32x4 v;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j] * tsc;
+                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[tel(4 * q + kk, 16 * mo + j)] * tsc;
                 lg_f16x4 a0, a1;
                 split2_f16_x4(v, a0, a1);
 #pragma unroll
@@ -1643,7 +1697,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int ni = 0; ni < G::CH; ++ni) {
                 f32x4 v;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[(4 * q + kk) * G::S + 16 * ni + j];
+                for (int kk = 0; kk < 4; ++kk) v[kk] = xl[tel(4 * q + kk, 16 * ni + j)];
                 lg_u32x2 f0, f1, f2;
                 split3_x4(v, f0, f1, f2);
                 xb[ni][0] = __builtin_bit_cast(lg_i16x4, f0);
@@ -1654,7 +1708,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int mo = 0; mo < G::CH; ++mo) {
                 f32x4 v;
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[(4 * q + kk) * G::S + 16 * mo + j];
+                for (int kk = 0; kk < 4; ++kk) v[kk] = tl[tel(4 * q + kk, 16 * mo + j)];
                 lg_u32x2 f0, f1, f2;
                 split3_x4(v, f0, f1, f2);
                 const lg_i16x4 a0 = __builtin_bit_cast(lg_i16x4, f0), a1 = __builtin_bit_cast(lg_i16x4, f1),
@@ -1685,13 +1739,13 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
             for (int s2 = 0; s2 < D / 32; ++s2) {
                 lg_f16x8 bh[2];
-                split2_f16_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q) * tsc, ld4(tl + j * G::S + 32 * s2 + 8 * q + 4) * tsc,
+                split2_f16_x8(ld4(tl + tix(j, 8 * s2 + 2 * q)) * tsc, ld4(tl + tix(j, 8 * s2 + 2 * q + 1)) * tsc,
                               bh[0], bh[1]);
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) {
-                    const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                    const int ew = wix(16 * mt + j, 32 * s2 + 8 * q);
                     const lg_f16x8 ah[2] = {*reinterpret_cast<const lg_f16x8*>(wsl + ew),
-                                            *reinterpret_cast<const lg_f16x8*>(wsl + D * SB + ew)};
+                                            *reinterpret_cast<const lg_f16x8*>(wsl + WP + ew)};
                     o[mt] = mfma_f16x2(ah, bh, o[mt]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -1703,17 +1757,17 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
         for (int s2 = 0; s2 < D / 32; ++s2) {
             lg_bf16x8 b0f, b1f, b2f;
-            split3_x8(ld4(tl + j * G::S + 32 * s2 + 8 * q), ld4(tl + j * G::S + 32 * s2 + 8 * q + 4), b0f, b1f, b2f);
+            split3_x8(ld4(tl + tix(j, 8 * s2 + 2 * q)), ld4(tl + tix(j, 8 * s2 + 2 * q + 1)), b0f, b1f, b2f);
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
-                const int ew = (16 * mt + j) * SB + 32 * s2 + 8 * q;
+                const int ew = wix(16 * mt + j, 32 * s2 + 8 * q);
                 const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
                 if constexpr (BF) {
                     o[mt] = mfma_bf(a0, b0f, o[mt]);
                     continue;
                 }
-                const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + D * SB + ew);
-                const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * D * SB + ew);
+                const lg_bf16x8 a1 = *reinterpret_cast<const lg_bf16x8*>(wsl + WP + ew);
+                const lg_bf16x8 a2 = *reinterpret_cast<const lg_bf16x8*>(wsl + 2 * WP + ew);
                 o[mt] = mfma_bf(a2, b0f, o[mt]);
                 o[mt] = mfma_bf(a1, b1f, o[mt]);
                 o[mt] = mfma_bf(a0, b2f, o[mt]);
@@ -1727,7 +1781,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         if (mask_out & 1) {
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
-                const f32x4 xm = ld4(xl + j * G::S + 16 * mt + 4 * q);
+                const f32x4 xm = ld4(xl + tix(j, 4 * mt + q));
 #pragma unroll
                 for (int reg = 0; reg < 4; ++reg) o[mt][reg] = xm[reg] > 0.f ? o[mt][reg] * scale_out : 0.f;
             }
@@ -1742,12 +1796,12 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         wave_sync_nm();
 #pragma unroll
-        for (int mt = 0; mt < G::CH; ++mt) st4(tl + j * G::S + 16 * mt + 4 * q, o[mt]);
+        for (int mt = 0; mt < G::CH; ++mt) st4(tl + tix(j, 4 * mt + q), o[mt]);
         wave_sync_nm();
         const uint32_t ob = (n * B + b0) * (4u * D);
         f32x4 vk[G::K];
 #pragma unroll
-        for (int k = 0; k < G::K; ++k) vk[k] = ld4(tl + (G::RPI * k + rl) * G::S + 4 * fg);
+        for (int k = 0; k < G::K; ++k) vk[k] = ld4(tl + tix(G::RPI * k + rl, fg));
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),

@@ -17,15 +17,32 @@ from torch import Tensor
 from ._native import check, load_library, ptr, stream_of
 
 NS = "leakgnn"
-_COUNTERS: dict = {}
+_POOL_SLOTS = 256
+_POOLS: dict = {}   # device -> int32 [_POOL_SLOTS] of completion counters, zeros at rest
+_SLOTS: dict = {}   # (device, stream handle) -> index into the device's pool
 
 
-def _counter(dev: torch.device) -> Tensor:
-    """The per-device completion counter of lg_cross_entropy_fwd (0 at rest)."""
-    c = _COUNTERS.get(dev)
-    if c is None:
-        c = _COUNTERS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
-    return c
+def _counter(dev: torch.device, stream: int) -> Tensor:
+    """lg_cross_entropy_fwd's completion counter for launches on `stream` (include/leakgnn.h:
+    one per stream that may run the loss concurrently; the launch leaves it at 0).  Counters are
+    slots of one per-device pool allocated (zeroed) on the first call, so a stream first seen
+    while a HIP graph is being captured takes a slot without a captured fill; the graph keeps
+    that slot's address for every replay (a shared per-device counter let an eager
+    loss on one stream and a replayed step on another interleave their tickets)."""
+    key = (dev, stream)
+    i = _SLOTS.get(key)
+    pool = _POOLS.get(dev)
+    if pool is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("leakgnn cross_entropy: run the loss once eagerly before capturing it "
+                               "(its counter pool is allocated on the first call)")
+        pool = _POOLS[dev] = torch.zeros(_POOL_SLOTS, dtype=torch.int32, device=dev)
+    if i is None:
+        i = len([k for k in _SLOTS if k[0] == dev])
+        if i >= _POOL_SLOTS:
+            raise RuntimeError(f"leakgnn cross_entropy: more than {_POOL_SLOTS} streams on {dev}")
+        _SLOTS[key] = i
+    return pool[i:i + 1]
 
 
 @torch.library.custom_op(f"{NS}::cross_entropy", mutates_args=(), device_types="cuda")
@@ -38,8 +55,9 @@ def cross_entropy(logits: Tensor, target: Tensor, ignore_index: int) -> Tuple[Te
     loss = torch.empty((), device=x.device, dtype=torch.float32)
     lse = torch.empty(B, device=x.device, dtype=torch.float32)
     rowloss = torch.empty(B, device=x.device, dtype=torch.float32)
+    st = stream_of(x)
     check(lib.lg_cross_entropy_fwd(ptr(x), ptr(t), B, C, C, ignore_index, ptr(loss), ptr(lse), ptr(rowloss),
-                                   ptr(_counter(x.device)), stream_of(x)), "lg_cross_entropy_fwd")
+                                   ptr(_counter(x.device, st)), st), "lg_cross_entropy_fwd")
     return loss, lse
 
 

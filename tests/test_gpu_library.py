@@ -347,6 +347,32 @@ def test_cross_entropy_matches_torch():
                  rtol=1e-6, what="fallback")
 
 
+def test_cross_entropy_counter_per_stream():
+    """the fused loss forward's completion counter is per (device, stream), so loss
+    launches running concurrently on two streams never share tickets: every mean is right and
+    both counters are back at 0."""
+    from models.loss import CrossEntropyLoss, _counter
+    torch.manual_seed(4)
+    x = torch.randn(256, 765, device=DEV) * 3
+    t = torch.randint(0, 765, (256,), device=DEV)
+    ref = torch.nn.functional.cross_entropy(x, t)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for s in (s1, s2):
+        s.wait_stream(torch.cuda.current_stream())
+    outs = []
+    with torch.no_grad():
+        for _ in range(25):
+            for s in (s1, s2):
+                with torch.cuda.stream(s):
+                    outs.append(CrossEntropyLoss()(x, t))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert_close(o, ref, rtol=1e-6, what="loss on a concurrent stream")
+    c1, c2 = _counter(DEV, s1.cuda_stream), _counter(DEV, s2.cuda_stream)
+    assert c1.data_ptr() != c2.data_ptr()
+    assert int(c1.item()) == 0 and int(c2.item()) == 0
+
+
 def test_reduce_batch_matches_per_op_reductions():
     """The backward ops' slab reductions merged into one launch per op group
     (lg_reduce_batch_begin / _flush; the trunk's layer-0 node-bias partials folded into the
