@@ -144,3 +144,31 @@ constexpr int64_t kLgMaxRows = int64_t{1} << 31;  // row-index space of the fast
 
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+
+// Cache policy (the raw buffer stores' aux operand) of the activation stores: the large
+// per-launch outputs that later kernels read (trunk y and its mask words, dx, the EdgeHead
+// hidden layer, the GRU's h and gates).  16 = sc1: agent-scope stores, written through the
+// XCD's L2 while the kernel runs.  With the default write-back policy the last few MiB of
+// each XCD's L2 were still dirty when the kernel ended and were written back then, after
+// its work (r06h-j, same box: the trunk forward without its y stores ran 16-17 us against
+// 21; sc1 on them, in the step, layer 1 21.1 -> 19.8-20.0 us and layer 0 24.9 -> 23.0, with
+// the kernels that read y unchanged; nt (2) instead sent y past the Infinity Cache and the
+// next layer's gather took 26.6 us).  0 restores write-back (lab A/B).  Stores that write
+// partial cache lines per instruction keep write-back: the GRU forward's h / gate stores
+// (64 B of a row per lane group) took 88-91 us under sc1 against 82-83 (r06k).
+#ifndef LG_ACT_AUX
+#define LG_ACT_AUX 16
+#endif
+constexpr int kLgActAux = LG_ACT_AUX;
+// A buffer descriptor over n floats at p for activation stores (n * 4 < 2^31; callers with a
+// larger buffer use st4), and one 16-byte store at float offset e with the activation policy.
+// The data registers stay unwritten for a few wait states after the store (lg_store_guard:
+// the compiler was seen reusing them at once, gcn_nm.hip).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lg_act_rsrc(float* p, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(p, static_cast<short>(0), static_cast<int>(n * 4), 0x00020000);
+}
+template <int AUX = kLgActAux>
+__device__ __forceinline__ void st4_act(__amdgpu_buffer_rsrc_t rs, uint32_t e, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v), rs,
+                                           4u * e, 0, AUX);
+}

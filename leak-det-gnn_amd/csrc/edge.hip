@@ -172,6 +172,8 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     constexpr int lab = 0;
 #endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const bool hbuf = BP * HID * 4 < 0x7FFFFFFF;  // the hidden layer's stores (common.h lg_act_rsrc)
+    const __amdgpu_buffer_rsrc_t hrs = lg_act_rsrc(hid_out, hid_out && hbuf ? BP * HID : 0);
     uint16_t* fimg = reinterpret_cast<uint16_t*>(smem);                                  // [2][3][TR][FSB]
     float(*part)[4][G::TR] = reinterpret_cast<float(*)[4][G::TR]>(fimg + 2 * 3 * G::FPL);  // [2][4][TR]
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
@@ -356,8 +358,11 @@ k_edge_fwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
                     hv[reg] = v;
                     s = fmaf(v, w2v[reg], s);
                 }
-                if (hid_out && r < BP)
-                    st4(hid_out + (static_cast<uint32_t>(r) * HID + 32 * nh + 16 * i + 4 * q), hv);
+                if (hid_out && r < BP) {  // the activation cache policy when 32-bit offsets reach
+                    const uint32_t e = static_cast<uint32_t>(r) * HID + 32 * nh + 16 * i + 4 * q;
+                    if (hbuf) st4_act(hrs, e, hv);
+                    else st4(hid_out + e, hv);
+                }
             }
             s += __shfl_xor(s, 16);
             s += __shfl_xor(s, 32);

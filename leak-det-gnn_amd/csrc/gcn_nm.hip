@@ -457,13 +457,13 @@ k_gcn_fwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         for (int k = 0; k < G::K; ++k) {
             const f32x4 v = ld4(tl + LY::tix(G::RPI * k + rl, fg));
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                                   yrs, tlo[k] + ob, 0, 0);
+                                                   yrs, tlo[k] + ob, 0, kLgActAux);
 #pragma unroll
             for (int i = 0; i < 4; ++i) bits |= (v[i] > 0.f ? 1u : 0u) << (4 * k + i);
         }
         if (ymask)
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
-                                                  0, 0);
+                                                  0, kLgActAux);
 #ifdef LG_NM3_STAMPS
         if (tcount < 6) LG_NM3_STAMP(5 + 3 * tcount, __builtin_amdgcn_s_memtime());
         ++tcount;
@@ -544,6 +544,11 @@ constexpr bool kPcWsplit = LG_PC_WSPLIT != 0;
 #endif
 #ifndef LG_PC_PREC
 #define LG_PC_PREC 0
+#endif
+// lab: tiles dealt to a workgroup's producers statically (p, p + 4, ...) with their records
+// by scalar loads a step ahead, instead of an LDS counter and LDS-staged records
+#ifndef LG_PC_STATIC
+#define LG_PC_STATIC 0
 #endif
 // producer wave priority (s_setprio; 0: the default, equal to the consumers').  Measured (r05m,
 // isolated train mode, two rounds): 2 and 3 within the box's noise of 0 (20.5-21.3 us each)
@@ -746,7 +751,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // (kPrecs: after the counter barrier, synchronised among the producer waves alone)
     constexpr bool kWs = kPcWsplit && (X0 || LG_PC_WS_DENSE);
     constexpr bool kPrecs = kWs && LG_PC_PREC && kPcRecs > 0;
-    const int nrec = (kWs && !kPrecs) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    const int nrec = ((kWs && !kPrecs) || LG_PC_STATIC) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
     uint32_t* wrdy = ctr + 1;  // kWs: consumer waves done staging W
     uint32_t* prdy = ctr + 2;  // kPrecs: producer waves done staging the records
     if constexpr (kWs) {
@@ -941,7 +946,20 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         };
         // the workgroup's next tile (an LDS atomic; past tend once its tiles are all dealt) and
         // its record (staged in LDS for the first kPcRecs draws)
+        uint32_t gcount = 0;  // LG_PC_STATIC: this producer's draws so far
         auto grab = [&](NmRec& r) -> int32_t {
+#if LG_PC_STATIC
+            // static dealing: draw i of producer p is the workgroup's tile p + 4 i; its record by
+            // scalar loads, requested a whole step before the tile's loads issue
+            const int32_t tile = tfirst + static_cast<int32_t>(gcount * kPcProd + prod) * tstride;
+            ++gcount;
+            {
+                uint32_t n, b0, nb;
+                tile_coords(tile, n, b0, nb);
+                r = nm_rec(tab, N + n);
+            }
+            return tile;
+#else
             uint32_t i = 0;
             if (lane == 0) i = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             i = __builtin_amdgcn_readfirstlane(i);
@@ -966,6 +984,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 r = nm_rec(tab, N + n);
             }
             return tile;
+#endif
         };
         int32_t tl[2];  // the tile whose blocks are in flight in buffer b
         // r: the tile's node-table record (schedule section: slot -> record with its node id),
@@ -1208,7 +1227,13 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         uint32_t st = 0;
         if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
         f32x4 o[G::CH];
+#ifdef LG_PC_LAB_NOMFMA  // lab: no transform (the tile's values stand in for the product)
+#pragma unroll
+        for (int mt = 0; mt < G::CH; ++mt) o[mt] = bq[mt % KS][mt / KS % 2];
+        if constexpr (false) {
+#else
         if constexpr (F16) {
+#endif
             // the tile's scale from its largest |value| (the B-operand values are the whole tile;
             // fmaxf on |.| source modifiers: three values an instruction)
             float mxf = 0.f;
@@ -1262,6 +1287,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 }
             }
         }
+#ifndef LG_PC_LAB_NOEPI  // lab: no ReLU / dropout
 #pragma unroll
         for (int mt = 0; mt < G::CH; ++mt) {
 #pragma unroll
@@ -1276,6 +1302,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                 o[mt][reg] = v;
             }
         }
+#endif
         // y back through the slot (the B-operand reads above are older LDS operations of
         // this wave, so they complete first)
 #pragma unroll
@@ -1286,10 +1313,16 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         for (int k = 0; k < G::K; ++k) {
             const uint32_t lk = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
             vk[k] = ld4(slot + LY::tix(G::RPI * k + rl, fg));
+#if !defined(LG_PC_LAB_NOSTORE) && !defined(LG_PC_LAB_NOYSTORE)  // lab: no y stores (NOSTORE: nor mask words)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                   yrs, lk, ob, 0);
+                                                   yrs, lk, ob, kLgActAux);
+#endif
         }
+#if defined(LG_PC_LAB_NOSTORE) || defined(LG_PC_LAB_NOMASK)
+        if (false) {
+#else
         if (ymask) {
+#endif
             uint32_t bits = 0;
 #pragma unroll
             for (int k = G::K - 1; k >= 0; --k)
@@ -1300,7 +1333,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
                     bits = __builtin_amdgcn_alignbit(bits, uu + 0x7FFFFFFFu, 31);
                 }
             __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(bits), mrs, nm_mask_off(n, b0 >> 4, ngroups, lane),
-                                                  0, 0);
+                                                  0, kLgActAux);
         }
         lg_store_guard(vk);
         pc_store_rel(&done[prod * NC + cons], static_cast<uint32_t>(u + 1));  // the slot's reads are done (release)
@@ -1328,16 +1361,18 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 // The round-1 kernel (k_gcn_bwd_nm) walked rowptr -> pair -> block as dependent round trips
 // and ran dW and dx on f32 MFMA (4096 cycles per tile against 1536 here).
 #ifndef LG_NB3_SBPAD
-#define LG_NB3_SBPAD 16  // lab: 8 = the round-5 W^T plane stride at D = 64
+#define LG_NB3_SBPAD 8  // lab: 16 = conflict-free dx-product W^T reads (measured slower, r06f)
 #endif
 template <int D, bool MASK_IN>
 struct Nb3Lds {
     // W^T plane row stride (halves).  The dx product reads a plane with ds_read_b128, lane (j, q)
-    // at row 16 mt + j, halves 32 s2 + 8 q; the lane groups {0-3, 12-15, 20-27}, ... then hit
-    // each bank once at 80 halves (40 dwords), twice at D + 8 = 72 (the round-5 layout, 2-way on
-    // all 24 plane reads of a tile; modelled with the guide's LDS banking, tools/lab/lds_banks.py).
-    // An XOR-swizzled tile and plane layout, conflict-free for every access, measured 48.8 ->
-    // 71 us (r06e: per-lane addresses pushed the kernel past 256 VGPRs into scratch).
+    // at row 16 mt + j, halves 32 s2 + 8 q; by the guide's LDS banking (tools/lab/lds_banks.py)
+    // the lane groups {0-3, 12-15, 20-27}, ... hit each bank once at 80 halves and twice at
+    // D + 8 = 72, on all 24 plane reads of a tile.  Measured (r06f, in the step, same box): 80
+    // took 51.0 / 43.6 us for layers 2 / 1 against 48.8 / 41.9 at 72 (the kernel's allocation
+    // went 241 -> 255 VGPRs); an XOR-swizzled tile and plane layout, conflict-free for every
+    // access, 71 us (r06e: per-lane addresses, 19 VGPRs spilled).  The conflicts are not what
+    // bounds this kernel; 72 stays.
     static constexpr int SB = D == 64 ? D + LG_NB3_SBPAD : D + 8;
     static constexpr int WF = (3 * D * SB) / 2;          // W^T split parts (bf16), in floats
     static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
@@ -1805,7 +1840,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 #pragma unroll
         for (int k = 0; k < G::K; ++k)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                   dxs, tlo[k] + ob, 0, 0);
+                                                   dxs, tlo[k] + ob, 0, kLgActAux);
         lg_store_guard(vk);
     }
     if constexpr (F16) {  // dw back to units of 1 (two exact factors)
@@ -2101,7 +2136,7 @@ k_gcn_fwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
             const bool valid = 16 * tile + 4 * k + rl < N;
             const uint32_t off = valid ? static_cast<uint32_t>(r.node[k]) * (4u * D) + 16u * fg : kNm3RowOob;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                   ys, off, 0, 0);
+                                                   ys, off, 0, kLgActAux);
         }
         lg_store_guard(vk);
 #ifdef LG_NM3_STAMPS
@@ -2227,7 +2262,7 @@ k_gcn_bwd_rows(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, 
             const bool valid = 16 * tile + 4 * k + rl < N;
             const uint32_t off = valid ? static_cast<uint32_t>(r.node[k]) * (4u * D) + 16u * fg : kNm3RowOob;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
-                                                   dxs, off, 0, 0);
+                                                   dxs, off, 0, kLgActAux);
         }
         lg_store_guard(vk);
     }

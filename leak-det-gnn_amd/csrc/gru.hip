@@ -210,6 +210,10 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
     const uint32_t seq0 = blockIdx.x * TS, seq = seq0 + j;
     const bool valid = seq < Nseq;
 
+    // the h / gate stores go through buffer descriptors over one step's rows (base advanced per
+    // step in SGPRs, 32-bit offsets within the step: Nseq * 4H * 4 bytes < 2^31, checked on the
+    // host): 10 fewer VGPRs than 64-bit addresses.  Write-back policy (common.h kLgActAux: these
+    // stores write 64-byte pieces of rows)
     const int row = g * H + 16 * u + j;  // A-operand row of this lane
     lg_f16x8 ah[NC][2];
     float hunsc;  // 2^-(sW + 14): the h product's unscale
@@ -303,7 +307,9 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                 grz[g][u][lane] = sg;
                 // the r / z waves store their own gate (the n waves' phase between the barriers is
                 // the step's critical path; it keeps the n, W_hn h + b_hn and h stores)
-                if (SAVE && valid) st4(gates + (static_cast<int64_t>(t) * Nseq + seq) * 4 * H + g * H + 16 * u + 4 * q, sg);
+                if (SAVE && valid)
+                    st4_act<0>(lg_act_rsrc(gates + static_cast<int64_t>(t) * Nseq * 4 * H, static_cast<int64_t>(Nseq) * 4 * H),
+                            seq * 4 * H + g * H + 16 * u + 4 * q, sg);
             }
             __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hbs
             if (g == 2) {
@@ -317,11 +323,15 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                 }
                 if (valid) {
                     const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
-                    if (hs) st4(hs + rw * H + 16 * u + 4 * q, hcur);
-                    if constexpr (SAVE) {
-                        float* gp = gates + rw * 4 * H + 16 * u + 4 * q;  // r, z: stored by their waves
-                        st4(gp + 2 * H, n);
-                        st4(gp + 3 * H, hp);
+                    (void)rw;
+                    if (hs)
+                        st4_act<0>(lg_act_rsrc(hs + static_cast<int64_t>(t) * Nseq * H, static_cast<int64_t>(Nseq) * H),
+                                seq * H + 16 * u + 4 * q, hcur);
+                    if constexpr (SAVE) {  // r, z: stored by their waves
+                        const __amdgpu_buffer_rsrc_t gr =
+                            lg_act_rsrc(gates + static_cast<int64_t>(t) * Nseq * 4 * H, static_cast<int64_t>(Nseq) * 4 * H);
+                        st4_act<0>(gr, seq * 4 * H + 2 * H + 16 * u + 4 * q, n);
+                        st4_act<0>(gr, seq * 4 * H + 3 * H + 16 * u + 4 * q, hp);
                     }
                 }
                 const f32x4 hsc = hcur * 16384.f;  // |h| <= 1 at the fixed scale 2^14
@@ -1270,6 +1280,8 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
 bool dims_ok(int64_t B, int64_t L, int64_t S) {
     return B >= 0 && L > 0 && S > 0 && L <= INT32_MAX && S <= INT32_MAX && B * S < (int64_t{1} << 31);
 }
+// the forward's h / gate stores address one step's rows of gates by 32-bit byte offsets
+bool fwd_rows_ok(int64_t B, int64_t S, int64_t H) { return B * S * 4 * H * 4 < (int64_t{1} << 31); }
 
 }  // namespace
 
@@ -1299,6 +1311,7 @@ extern "C" int lg_gru_fwd(const float* residual, const float* tfeat, const float
     if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
     if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
     if (gates && !h_seq) return LG_EINVAL;  // the backward needs both
+    if (!fwd_rows_ok(B, S, H)) return LG_EUNSUPPORTED;
     if (B == 0) return LG_OK;
     hipStream_t s = lg_stream(stream);
     return H == 64 ? launch_fwd<64>(I == 10, gates != nullptr, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates,
@@ -1349,6 +1362,7 @@ extern "C" int lg_gru_node_init_fwd(const float* residual, const float* tfeat, c
     if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
     if (!sensor_slot || !sensor_idx || !proj_w || !node_bias || !xs0 || !x0bits) return LG_EINVAL;
     if (gates && !h_seq) return LG_EINVAL;
+    if (!fwd_rows_ok(B, S, H)) return LG_EUNSUPPORTED;
     const bool drop = (flags & LG_F_DROPOUT) != 0;
     if (drop && !(dropout_p >= 0.f && dropout_p < 1.f)) return LG_EINVAL;
     if (B == 0) return LG_OK;
