@@ -34,6 +34,10 @@
 #include "reduce.h"
 #include "split_bf16.h"
 
+#ifndef LG_EDGE_DH_AUX
+#define LG_EDGE_DH_AUX LG_ACT_AUX  // lab A/B of the streamed scatter's dh stores
+#endif
+
 namespace {
 
 constexpr int HID = 128;
@@ -503,13 +507,21 @@ __device__ __forceinline__ void edge_stream_scatter(const EdgeScatter& sc, const
             a0 += ld4(r + c0);
             a1 += ld4(r + c1);
         }
-        float* dst = lacc + slot * D;
-        if ((w0 >> 25) & 1u) {
+        if ((w0 >> 25) & 1u) {  // the node's last tile: its dh row (activation cache policy, common.h)
             const int64_t row = sc.nm ? static_cast<int64_t>(node) * sc.B + win : static_cast<int64_t>(win) * sc.N + node;
-            dst = sc.dh + row * D;
+            if (static_cast<int64_t>(sc.B) * sc.N * D < (int64_t{1} << 29)) {
+                const __amdgpu_buffer_rsrc_t dhr = lg_act_rsrc(sc.dh, static_cast<int64_t>(sc.B) * sc.N * D);
+                st4_act<LG_EDGE_DH_AUX>(dhr, static_cast<uint32_t>(row * D) + c0, a0);
+                st4_act<LG_EDGE_DH_AUX>(dhr, static_cast<uint32_t>(row * D) + c1, a1);
+            } else {
+                st4(sc.dh + row * D + c0, a0);
+                st4(sc.dh + row * D + c1, a1);
+            }
+        } else {
+            float* dst = lacc + slot * D;
+            st4(dst + c0, a0);
+            st4(dst + c1, a1);
         }
-        st4(dst + c0, a0);
-        st4(dst + c1, a1);
     }
 }
 // the window's nodes without pipes: dh = dpool / N
