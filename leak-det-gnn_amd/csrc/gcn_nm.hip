@@ -520,6 +520,12 @@ constexpr int kPcRing = LG_PC_RING;
 #define LG_PC_NC 2
 #endif
 constexpr int kPcNC = LG_PC_NC;
+// producer waves per workgroup
+#ifndef LG_PC_PROD
+#define LG_PC_PROD 4
+#endif
+constexpr int kPcProdN = LG_PC_PROD;
+static_assert(kPcProdN <= 16 && kPcProdN * (1 + LG_PC_NC) <= 16, "ready[16]; at most 16 waves");
 // The node-table records of a workgroup's first kPcRecs tiles are staged in LDS with W, so a
 // producer's record is an LDS read after its tile draw instead of a scalar load from L2 (whose
 // latency sat between drawing tile t + 2 and issuing its loads, every tile); later tiles (large
@@ -598,6 +604,19 @@ __device__ __forceinline__ void pc_pin(T& v) {  // v is read only after the wait
     (void)v;
 #endif
 }
+// lab: work moved from the consumer waves (the pipeline's bound) to the producers: the tile's
+// largest |value| for the f16 scale (LG_PC_PMAX, dense layers; word 10 of the slot metadata) and
+// the dropout row-stream seeds (LG_PC_PSEED, one per consumer lane, in LDS beside the slot);
+// LG_PC_CPRIO: consumer wave priority (s_setprio)
+#ifndef LG_PC_PMAX
+#define LG_PC_PMAX 0
+#endif
+#ifndef LG_PC_PSEED
+#define LG_PC_PSEED 0
+#endif
+#ifndef LG_PC_CPRIO
+#define LG_PC_CPRIO 0
+#endif
 // ring-slot metadata: n, b0, nb, X0's sensor entries (count, then up to kPcSens (slot, w) pairs)
 constexpr int kPcSens = 3;
 constexpr int kPcMeta = 16;
@@ -611,9 +630,10 @@ struct PcLds {  // floats
     static constexpr int WOFF = 0;                                  // W [out][in] * fold (fp32), bias * fold
     static constexpr int XOFF = D * WS + D;                         // per-wave max|W| bits (F16)
     static constexpr int FOFF = XOFF + 16;                          // ready[16], done[kPcProd * NC], fin[4], ctr
-    static constexpr int MOFF = FOFF + 16 + kPcProd * NC + 8;       // per (producer, slot): kPcMeta words
+    static constexpr int MOFF = FOFF + 16 + kPcProd * NC + kPcProd + 4;  // per (producer, slot): kPcMeta words
     static constexpr int COFF = MOFF + kPcMeta * kPcProd * kPcRing;  // kPcRecs node-table records (16 words)
-    static constexpr int ROFF = COFF + 16 * kPcRecs;                  // the rings
+    static constexpr int SOFF = COFF + 16 * kPcRecs;                  // LG_PC_PSEED: per (producer, slot) 64 row-stream seeds
+    static constexpr int ROFF = SOFF + (LG_PC_PSEED ? 64 * kPcProd * kPcRing : 0);  // the rings
     static constexpr size_t BYTES = 4 * static_cast<size_t>(ROFF + kPcProd * kPcRing * TILE);
     static __device__ __forceinline__ int tix(int r, int c) { return SWZ ? r * D + 4 * (c ^ r) : r * NmGeo<D>::S + 4 * c; }
 };
@@ -865,6 +885,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 
     if (producer) {
         // ---------------- producer: gather + accumulate, two tiles in flight
+        const uint32_t pkey = LG_PC_PSEED && DROP ? lg_dropout_key_dev(seed, salt) : 0u;
 #if LG_PC_PRIO
         // the producer's instruction stream is the pipeline's critical path; its two consumers on
         // the same SIMD have ring slack, so the producer goes first when both are ready to issue
@@ -1092,11 +1113,25 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             float* slot = ring + sl * LY::TILE;
 #pragma unroll
             for (int k = 0; k < G::K; ++k) st4(slot + LY::tix(G::RPI * k + rl, fg), acc[k]);
+            uint32_t pmx = 0;
+            if constexpr (LG_PC_PMAX && F16 && !X0) {  // the tile's largest |value| (the consumer's f16 scale)
+                float mf = 0.f;
+#pragma unroll
+                for (int k = 0; k < G::K; ++k)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) mf = fmaxf(mf, fabsf(acc[k][c]));
+                pmx = lg_wave_max_bits(__float_as_uint(mf));
+            }
+            if constexpr (LG_PC_PSEED && DROP) {  // the consumer lane (j, q)'s row-stream seed
+                uint32_t* sd = reinterpret_cast<uint32_t*>(lds + LY::SOFF) + 64 * (prod * R + sl);
+                sd[lane] = lg_row_stream_seed(pkey, static_cast<uint64_t>(b0 + j) * N + mn, static_cast<uint32_t>(q));
+            }
             if (lane == 0) {
                 uint32_t* m = meta + kPcMeta * (prod * R + sl);
                 m[0] = mn;
                 m[1] = b0;
                 m[2] = mnb;
+                if constexpr (LG_PC_PMAX && F16 && !X0) m[10] = pmx;
                 if constexpr (X0) {
                     m[3] = nsx;
                     m[4] = ss0;
@@ -1140,6 +1175,9 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     }
 
     // ---------------- consumer: transform + epilogue
+#if LG_PC_CPRIO
+    __builtin_amdgcn_s_setprio(LG_PC_CPRIO);
+#endif
     const __amdgpu_buffer_rsrc_t yrs = nm_rsrc(y, bytes);
     const __amdgpu_buffer_rsrc_t srs = nm_rsrc(x, X0 ? static_cast<uint64_t>(x0.S) * B * (4u * D) : 0);  // X0: xs0
     const __amdgpu_buffer_rsrc_t mrs = nm_mask_rsrc(ymask, N, ngroups);
@@ -1225,7 +1263,10 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             }
         }
         uint32_t st = 0;
-        if constexpr (DROP) st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+        if constexpr (DROP) {
+            if constexpr (LG_PC_PSEED) st = reinterpret_cast<const uint32_t*>(lds + LY::SOFF)[64 * (prod * R + sl) + lane];
+            else st = lg_row_stream_seed(key, static_cast<uint64_t>(b0 + j) * N + n, q);
+        }
         f32x4 o[G::CH];
 #ifdef LG_PC_LAB_NOMFMA  // lab: no transform (the tile's values stand in for the product)
 #pragma unroll
@@ -1236,14 +1277,19 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 #endif
             // the tile's scale from its largest |value| (the B-operand values are the whole tile;
             // fmaxf on |.| source modifiers: three values an instruction)
-            float mxf = 0.f;
+            int sa;
+            if constexpr (LG_PC_PMAX && !X0) {
+                sa = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m[10]));
+            } else {
+                float mxf = 0.f;
 #pragma unroll
-            for (int s2 = 0; s2 < KS; ++s2)
+                for (int s2 = 0; s2 < KS; ++s2)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
+                    for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int c = 0; c < 4; ++c) mxf = fmaxf(mxf, fabsf(bq[s2][h][c]));
-            const int sa = lg_f16_scale_exp(lg_wave_max_bits(__float_as_uint(mxf)));
+                        for (int c = 0; c < 4; ++c) mxf = fmaxf(mxf, fabsf(bq[s2][h][c]));
+                sa = lg_f16_scale_exp(lg_wave_max_bits(__float_as_uint(mxf)));
+            }
             const float sc2 = lg_pow2f(sa);
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) o[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2315,9 +2361,9 @@ auto nm3_kernel(int flags) {
 }
 template <int D, bool DR, bool RL, bool X0>
 auto pc_kernel(bool bf16, bool f16) {
-    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, 4, kPcNC, X0>
-                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, 4, kPcNC, X0>
-                       : k_gcn_fwd_pc<D, DR, RL, false, false, 4, kPcNC, X0>);
+    return bf16 ? k_gcn_fwd_pc<D, DR, RL, true, false, kPcProdN, kPcNC, X0>
+                : (f16 ? k_gcn_fwd_pc<D, DR, RL, false, true, kPcProdN, kPcNC, X0>
+                       : k_gcn_fwd_pc<D, DR, RL, false, false, kPcProdN, kPcNC, X0>);
 }
 
 // lg_gcn_fwd_nm_bits (x0 == NULL) and lg_gcn_fwd_nm_x0 (x the sensor rows, *x0 the rest)
@@ -2362,8 +2408,8 @@ int nm_fwd(const int32_t* nodetab, const int32_t* pairs, const float* x, const f
         } else {
             auto kern = x0 ? (relu ? pc_kernel<DD, DR, true, true>(bf16, f16) : pc_kernel<DD, DR, false, true>(bf16, f16))
                            : (relu ? pc_kernel<DD, DR, true, false>(bf16, f16) : pc_kernel<DD, DR, false, false>(bf16, f16));
-            const size_t dyn = PcLds<DD, 4, kPcNC>::BYTES;
-            const int thr = 64 * 4 * (1 + kPcNC);
+            const size_t dyn = PcLds<DD, kPcProdN, kPcNC>::BYTES;
+            const int thr = 64 * kPcProdN * (1 + kPcNC);
             const int grid = nm_grid(kern, thr, dyn, ntiles, 4, 1);
             lg_launch(kern, grid, thr, dyn, s, nodetab, pr, x, W, bp, y, N32, B32, G32, fd, dropout_p, scale, seed,
                       salt, ymask, xz);
