@@ -650,6 +650,13 @@ __device__ __forceinline__ void pc_store_rel(uint32_t* p, uint32_t v) {
 // 2: a consumer's wait for its tile), which lg_spin_errors reads back -- the launch's results
 // are then invalid.  The tests assert it stays 0 (tests/conftest.py, after every GPU module).
 __device__ uint32_t g_pc_spin_err;
+// lab (LG_PC_DYN): per-XCD tile counters (one 256-byte line each) and the producers' finish
+// counter; zero between launches (the launch's last producer resets them)
+#ifndef LG_PC_DYN
+#define LG_PC_DYN 0
+#endif
+__device__ uint32_t g_pc_dyn[8 * 64];
+__device__ uint32_t g_pc_dyn_fin;
 // wait until *p >= v (bounded: ~2^20 polls)
 __device__ __forceinline__ void pc_wait(const uint32_t* p, uint32_t v) {
     for (int it = 0; it < (1 << 20); ++it) {
@@ -771,7 +778,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // (kPrecs: after the counter barrier, synchronised among the producer waves alone)
     constexpr bool kWs = kPcWsplit && (X0 || LG_PC_WS_DENSE);
     constexpr bool kPrecs = kWs && LG_PC_PREC && kPcRecs > 0;
-    const int nrec = ((kWs && !kPrecs) || LG_PC_STATIC) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
+    const int nrec = ((kWs && !kPrecs) || LG_PC_STATIC || LG_PC_DYN) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
     uint32_t* wrdy = ctr + 1;  // kWs: consumer waves done staging W
     uint32_t* prdy = ctr + 2;  // kPrecs: producer waves done staging the records
     if constexpr (kWs) {
@@ -969,7 +976,24 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         // its record (staged in LDS for the first kPcRecs draws)
         uint32_t gcount = 0;  // LG_PC_STATIC: this producer's draws so far
         auto grab = [&](NmRec& r) -> int32_t {
-#if LG_PC_STATIC
+#if LG_PC_DYN
+            // dynamic dealing over the XCD's tile range: a global counter per XCD, one atomic per
+            // draw, requested a whole step before the tile's loads issue
+            uint32_t di = 0;
+            if (lane == 0)
+                di = __hip_atomic_fetch_add(&g_pc_dyn[64 * (blockIdx.x % 8)], 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+            di = __builtin_amdgcn_readfirstlane(di);
+            const int32_t dchunk = static_cast<int32_t>((static_cast<int64_t>(ngroups) * N + 7) / 8);
+            const int32_t tile = gridDim.x >= 8 ? static_cast<int32_t>(blockIdx.x % 8) * dchunk + static_cast<int32_t>(di)
+                                                : tend;
+            {
+                uint32_t n, b0, nb;
+                tile_coords(tile, n, b0, nb);
+                r = nm_rec(tab, N + n);
+            }
+            return tile;
+#elif LG_PC_STATIC
             // static dealing: draw i of producer p is the workgroup's tile p + 4 i; its record by
             // scalar loads, requested a whole step before the tile's loads issue
             const int32_t tile = tfirst + static_cast<int32_t>(gcount * kPcProd + prod) * tstride;
@@ -1165,6 +1189,15 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         // tiles are drawn in increasing order, so the first one past tend ends the producer
         pc_vm_wait<0>();  // the last (empty) prefetches
         if (lane == 0) pc_store_rel(&fin[prod], static_cast<uint32_t>(t));
+#if LG_PC_DYN
+        if (lane == 0) {  // the launch's last producer: the counters back to 0 for the next launch
+            const uint32_t f = __hip_atomic_fetch_add(&g_pc_dyn_fin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f + 1 == gridDim.x * kPcProd) {
+                for (int x = 0; x < 8; ++x) __hip_atomic_store(&g_pc_dyn[64 * x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&g_pc_dyn_fin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+#endif
 #ifdef LG_NM3_STAMPS
         pc_stamp_end();
 #endif

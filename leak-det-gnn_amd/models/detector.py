@@ -10,15 +10,19 @@ and models/window_evaluator.py use it unchanged:
   edge_head.mlp.{0,3}.*             EdgeHead                  (detector.py:76-88)
   noleak_head.mlp.{0,3}.*           NoLeakHead                (detector.py:91-102)
 
-What runs where (forward + backward):
-  * The 29-row sensor projection (one small GEMM), the NoLeakHead MLP on the
-    (B, 64) pooled vector and the loss: stock PyTorch-ROCm.
-  * The GRU sensor encoder, node init, every GCNConv + ReLU + dropout, the fused
-    EdgeHead (endpoint gather -> MLP -> logit, never materialising the (B,P,3D)
-    features) and the per-window mean pool: libleakgnn HIP kernels behind the
-    registered ops leakgnn::gru_encoder / sensor_proj / gnn_trunk / detector_heads
-    (models/library.py) over ONE device-resident single-graph CSR; the (2, B*E)
-    batchified edge_index of the reference (detector.py:195-196) is never built.
+What runs where (forward + backward): everything on libleakgnn HIP kernels behind the
+registered ops of models/library.py (leakgnn::encoder_trunk / gru_encoder / sensor_proj /
+gnn_trunk / detector_heads) and models/loss.py (leakgnn::cross_entropy):
+  * the GRU sensor encoder with the node init (sensor projection, mask column, ReLU,
+    dropout) fused into its epilogue, and the projection's backward into the GRU backward;
+  * every GCNConv + ReLU + dropout on the node-major trunk kernels over ONE device-resident
+    single-graph CSR (the (2, B*E) batchified edge_index of the reference,
+    detector.py:195-196, is never built);
+  * the fused EdgeHead (endpoint gather -> MLP -> logit, the (B, P, 3D) features never
+    materialised), the per-window mean pool with the NoLeakHead MLP, and their backward
+    with the node scatter streamed per tile;
+  * the loss (CrossEntropyLoss) and, in the training scripts, clip_grad_norm_ + AdamW
+    (models/optim.py).
 There is no CPU path: forward raises on CPU tensors.
 """
 from __future__ import annotations
@@ -194,6 +198,8 @@ class LeakDetector(nn.Module):
         tfeat as data (no gradient wanted for them: the fused backward forms no dx)."""
         g = self.sensor_encoder.gru
         if not (self.fuse_encoder and g.num_layers == 1 and g.bias and not g.bidirectional):
+            return False
+        if self.capture is not None:  # the capture reads h_s, which the fused op never forms (ADVICE r05)
             return False
         if residual.requires_grad or (tfeat is not None and self.sensor_encoder.use_time and tfeat.requires_grad):
             return False
