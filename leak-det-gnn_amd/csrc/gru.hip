@@ -28,6 +28,19 @@
 #include <cstdlib>
 #include <type_traits>
 #include "common.h"
+
+#ifndef LG_GRU_AUX
+// Cache policy of the forward's h / gate stores (342 MB at B = 256, read by the backward ~0.3 ms
+// and ~400 MB of other traffic later): 18 = sc1 | nt, past the Infinity Cache.  Write-back let them
+// evict the trunk's and the heads' working sets from the 256 MB Infinity Cache: under sc1 | nt
+// every later kernel of the step ran faster (trunk backward 48.2 -> 45.5 us, GRU backward 101.5
+// -> 96.7, EdgeHead 56.1 / 130.0 -> 53.2 / 127.2) for 5 us more in this kernel; step sum 561 ->
+// 552 us (r06t, same box).  nt alone took this kernel to 124 us (64-byte row pieces per store).
+#define LG_GRU_AUX 18
+#endif
+#ifndef LG_GRU_LAUX
+#define LG_GRU_LAUX 0  // cache policy of the backward's h / gate loads (lab: 2 = nt)
+#endif
 #include "reduce.h"
 #include "split_bf16.h"
 
@@ -308,7 +321,7 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                 // the r / z waves store their own gate (the n waves' phase between the barriers is
                 // the step's critical path; it keeps the n, W_hn h + b_hn and h stores)
                 if (SAVE && valid)
-                    st4_act<0>(lg_act_rsrc(gates + static_cast<int64_t>(t) * Nseq * 4 * H, static_cast<int64_t>(Nseq) * 4 * H),
+                    st4_act<LG_GRU_AUX>(lg_act_rsrc(gates + static_cast<int64_t>(t) * Nseq * 4 * H, static_cast<int64_t>(Nseq) * 4 * H),
                             seq * 4 * H + g * H + 16 * u + 4 * q, sg);
             }
             __syncthreads();  // (A) sigma(r), sigma(z) posted; every wave is done reading hbs
@@ -325,13 +338,13 @@ k_gru_fwd(const float* __restrict__ resid, const float* __restrict__ tfeat, cons
                     const int64_t rw = static_cast<int64_t>(t) * Nseq + seq;
                     (void)rw;
                     if (hs)
-                        st4_act<0>(lg_act_rsrc(hs + static_cast<int64_t>(t) * Nseq * H, static_cast<int64_t>(Nseq) * H),
+                        st4_act<LG_GRU_AUX>(lg_act_rsrc(hs + static_cast<int64_t>(t) * Nseq * H, static_cast<int64_t>(Nseq) * H),
                                 seq * H + 16 * u + 4 * q, hcur);
                     if constexpr (SAVE) {  // r, z: stored by their waves
                         const __amdgpu_buffer_rsrc_t gr =
                             lg_act_rsrc(gates + static_cast<int64_t>(t) * Nseq * 4 * H, static_cast<int64_t>(Nseq) * 4 * H);
-                        st4_act<0>(gr, seq * 4 * H + 2 * H + 16 * u + 4 * q, n);
-                        st4_act<0>(gr, seq * 4 * H + 3 * H + 16 * u + 4 * q, hp);
+                        st4_act<LG_GRU_AUX>(gr, seq * 4 * H + 2 * H + 16 * u + 4 * q, n);
+                        st4_act<LG_GRU_AUX>(gr, seq * 4 * H + 3 * H + 16 * u + 4 * q, hp);
                     }
                 }
                 const f32x4 hsc = hcur * 16384.f;  // |h| <= 1 at the fixed scale 2^14
@@ -816,13 +829,13 @@ k_gru_bwd2(const float* __restrict__ resid, const float* __restrict__ tfeat, con
             nsq * 4 * H * 4, 0x00020000);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            g[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * 4 * H + u0 + k * H) * 4, 0, 0));
+            g[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * 4 * H + u0 + k * H) * 4, 0, LG_GRU_LAUX));
     };
     auto load_h = [&](int t) -> f32x4 {  // h_t of this lane's units (h_0 for t < 0: masked at use)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(hs + (static_cast<int64_t>(max(t, 0)) * Nseq + seq0) * H), static_cast<short>(0),
             nsq * H * 4, 0x00020000);
-        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * H + u0) * 4, 0, 0));
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (sl * H + u0) * 4, 0, LG_GRU_LAUX));
     };
     // x value i of this thread: step 0's element and the per-step stride (hoisted out of the loop)
     const float* xp0[XPT];
