@@ -621,7 +621,10 @@ int lg_pool_head_bwd(const float* pooled, const float* hid, const float* w1, con
  *   gates    : fp32 [L][B*S][4][H] per step (r, z, n, W_hn h + b_hn) for the
  *              backward, or NULL (inference); non-NULL requires h_seq
  *   h_last   : fp32 [B*S][H]  (= h_s of detector.py:176 as [B][S][H])
- * H in {32, 64}, I in {1, 10} (use_time False/True), one layer.
+ * H in {32, 64} on the tiled kernels below; any other H in 1..1024 (ABI 26; LG_EUNSUPPORTED
+ * before) on a generic kernel (one hidden unit per thread, fp32 FMAs, same saved layouts: a
+ * generality path for LeakDetector(sensor_hidden=...), not the bench's).  I in {1, 10}
+ * (use_time False/True), one layer.
  * Backward (BPTT from the saved gates, no recompute): dh_last -> dx (fp32
  * [B*S][L][I], may be NULL), dW_ih, dW_hh, db_ih, db_hh (overwritten,
  * deterministic).

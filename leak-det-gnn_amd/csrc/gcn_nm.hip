@@ -1439,20 +1439,23 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
 //   dW  += t^T x     (16x16x16, K = the tile's 16 rows; t and x columns split per tile)
 // The round-1 kernel (k_gcn_bwd_nm) walked rowptr -> pair -> block as dependent round trips
 // and ran dW and dx on f32 MFMA (4096 cycles per tile against 1536 here).
+#ifndef LG_NB3_WFRAG
+#define LG_NB3_WFRAG 1  // lab: 0 = the round-5 row-major W^T planes (stride LG_NB3_SBPAD + D halves)
+#endif
 #ifndef LG_NB3_SBPAD
-#define LG_NB3_SBPAD 8  // lab: 16 = conflict-free dx-product W^T reads (measured slower, r06f)
+#define LG_NB3_SBPAD 8
 #endif
 template <int D, bool MASK_IN>
 struct Nb3Lds {
-    // W^T plane row stride (halves).  The dx product reads a plane with ds_read_b128, lane (j, q)
-    // at row 16 mt + j, halves 32 s2 + 8 q; by the guide's LDS banking (tools/lab/lds_banks.py)
-    // the lane groups {0-3, 12-15, 20-27}, ... hit each bank once at 80 halves and twice at
-    // D + 8 = 72, on all 24 plane reads of a tile.  Measured (r06f, in the step, same box): 80
-    // took 51.0 / 43.6 us for layers 2 / 1 against 48.8 / 41.9 at 72 (the kernel's allocation
-    // went 241 -> 255 VGPRs); an XOR-swizzled tile and plane layout, conflict-free for every
-    // access, 71 us (r06e: per-lane addresses, 19 VGPRs spilled).  The conflicts are not what
-    // bounds this kernel; 72 stays.
-    static constexpr int SB = D == 64 ? D + LG_NB3_SBPAD : D + 8;
+    // W^T planes.  The dx product reads a plane as MFMA A fragments, ds_read_b128, lane (j, q)
+    // at row 16 mt + j, halves 32 s2 + 8 q.  Row-major with a padded row stride, the guide's LDS
+    // banking (tools/lab/lds_banks.py: lane groups {0-3, 12-15, 20-27}, ...) hits banks twice at
+    // D + 8 = 72 halves on all 24 plane reads of a tile, and a conflict-free stride (80) cost
+    // VGPRs (r06f).  LG_NB3_WFRAG: the planes are stored in fragment order instead, fragment
+    // (mt, s2) a 1 KB block with lane l's 16 bytes at 16 l: every read is 64 consecutive 16-byte
+    // pieces (conflict-free), addressed by one per-lane base plus immediates, and a plane is
+    // D x D halves (no padding).  The prologue's element writes scatter (once per workgroup).
+    static constexpr int SB = LG_NB3_WFRAG ? D : (D == 64 ? D + LG_NB3_SBPAD : D + 8);
     static constexpr int WF = (3 * D * SB) / 2;          // W^T split parts (bf16), in floats
     static constexpr int TL = 2 * NmGeo<D>::TILE;         // per wave: t tile + x tile
     static constexpr int L = D * D + 2 * D;               // slab row: dW, db, d(node bias)
@@ -1505,10 +1508,22 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     float* tl = tiles + wave * LY::TL;  // t tile [row][feature], later dx
     float* xl = tl + G::TILE;           // x tile [row][feature]
     // LDS addresses: tile row r, 16-byte chunk c4 (rows padded to G::S floats); W^T plane element
-    // (row i, column o) at i * SB + o halves
+    // (row i, column o) at wix(i, o) halves
     auto tix = [&](int r, int c4) { return r * G::S + 4 * c4; };
     auto tel = [&](int r, int c) { return r * G::S + c; };
-    auto wix = [&](int i, int o) { return i * SB + o; };
+    auto wix = [&](int i, int o) {
+        if constexpr (LG_NB3_WFRAG)  // fragment (i / 16, o / 32), lane (i % 16) + 16 ((o % 32) / 8), half o % 8
+            return (((i >> 4) * (D / 32) + (o >> 5)) * 64 + (i & 15) + 16 * ((o & 31) >> 3)) * 8 + (o & 7);
+        else
+            return i * SB + o;
+    };
+    // the A fragment (mt, s2) of lane (j, q): W^T rows 16 mt + j, columns 32 s2 + 8 q .. + 7
+    auto wrd = [&](int mt, int s2) {
+        if constexpr (LG_NB3_WFRAG)
+            return (mt * (D / 32) + s2) * 512 + 8 * lane;
+        else
+            return wix(16 * mt + j, 32 * s2 + 8 * q);
+    };
     constexpr int WP = D * SB;  // halves per W^T plane
     const uint64_t bytes = static_cast<uint64_t>(N) * B * (4u * D);
     const __amdgpu_buffer_rsrc_t dys = nm_rsrc(dy, bytes), ms = nm_rsrc(MY ? yv : dy, bytes),
@@ -1857,7 +1872,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
                               bh[0], bh[1]);
 #pragma unroll
                 for (int mt = 0; mt < G::CH; ++mt) {
-                    const int ew = wix(16 * mt + j, 32 * s2 + 8 * q);
+                    const int ew = wrd(mt, s2);
                     const lg_f16x8 ah[2] = {*reinterpret_cast<const lg_f16x8*>(wsl + ew),
                                             *reinterpret_cast<const lg_f16x8*>(wsl + WP + ew)};
                     o[mt] = mfma_f16x2(ah, bh, o[mt]);
@@ -1874,7 +1889,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             split3_x8(ld4(tl + tix(j, 8 * s2 + 2 * q)), ld4(tl + tix(j, 8 * s2 + 2 * q + 1)), b0f, b1f, b2f);
 #pragma unroll
             for (int mt = 0; mt < G::CH; ++mt) {
-                const int ew = wix(16 * mt + j, 32 * s2 + 8 * q);
+                const int ew = wrd(mt, s2);
                 const lg_bf16x8 a0 = *reinterpret_cast<const lg_bf16x8*>(wsl + ew);
                 if constexpr (BF) {
                     o[mt] = mfma_bf(a0, b0f, o[mt]);

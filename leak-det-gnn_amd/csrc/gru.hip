@@ -1290,6 +1290,150 @@ int launch_bwd(bool ut, bool need_dx, const float* residual, const float* tfeat,
     return LG_OK;
 }
 
+// ------------------------------------------------------------------ any hidden width
+// The encoder at a hidden width the tiled kernels above do not cover (H not 32 / 64; ABI 26):
+// the same recurrence (detector.py:60-73 through nn.GRU) with one hidden unit per thread and a
+// workgroup per sequence (grid-stride over the B*S sequences), h_{t-1} and x_t in LDS, W read
+// through the caches.  Same saved layouts as the tiled kernels: h_seq [t][seq][H] = h_t and
+// gates [t][seq][4][H] = sigma(r), sigma(z), n, W_hn h_{t-1} + b_hn.  A generality path (the
+// reference's widths run the tiled kernels), sized for correctness at any H <= 1024.
+constexpr int kGenMaxH = 1024;
+constexpr int kGenBwdBlocks = 512;  // slab rows of the generic backward
+
+inline int gen_threads(int64_t H) { return static_cast<int>((H + 63) / 64 * 64); }
+
+__global__ void __launch_bounds__(kGenMaxH) k_gru_gen_fwd(const float* __restrict__ residual,
+                                                          const float* __restrict__ tfeat, const float* __restrict__ w_ih,
+                                                          const float* __restrict__ w_hh, const float* __restrict__ b_ih,
+                                                          const float* __restrict__ b_hh, float* __restrict__ h_seq,
+                                                          float* __restrict__ gates, float* __restrict__ h_last, int B,
+                                                          int L, int S, int I, int H) {
+    extern __shared__ float gsm[];
+    float* hs = gsm;      // h_{t-1} [H]
+    float* xs = gsm + H;  // x_t [I]
+    const int u = threadIdx.x;
+    const int64_t nseq = static_cast<int64_t>(B) * S;
+    for (int64_t seq = blockIdx.x; seq < nseq; seq += gridDim.x) {
+        const int64_t b = seq / S, sn = seq % S;
+        if (u < H) hs[u] = 0.f;
+        for (int t = 0; t < L; ++t) {
+            if (u < I) xs[u] = u == 0 ? residual[(b * L + t) * S + sn] : tfeat[(b * L + t) * (I - 1) + u - 1];
+            __syncthreads();
+            float hn = 0.f, g[4] = {0.f, 0.f, 0.f, 0.f};
+            if (u < H) {
+                float a[3], c[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int row = k * H + u;
+                    a[k] = b_ih[row];
+                    for (int i = 0; i < I; ++i) a[k] = fmaf(w_ih[static_cast<int64_t>(row) * I + i], xs[i], a[k]);
+                    c[k] = b_hh[row];
+                    const float* wr = w_hh + static_cast<int64_t>(row) * H;
+                    for (int i = 0; i < H; ++i) c[k] = fmaf(wr[i], hs[i], c[k]);
+                }
+                g[0] = sigm(a[0] + c[0]);
+                g[1] = sigm(a[1] + c[1]);
+                g[2] = gru_tanh(a[2] + g[0] * c[2]);
+                g[3] = c[2];
+                hn = (1.f - g[1]) * g[2] + g[1] * hs[u];
+            }
+            __syncthreads();
+            if (u < H) {
+                hs[u] = hn;
+                const int64_t r = static_cast<int64_t>(t) * nseq + seq;
+                if (h_seq) h_seq[r * H + u] = hn;
+                if (gates) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) gates[(r * 4 + k) * H + u] = g[k];
+                }
+            }
+        }
+        if (u < H) h_last[seq * H + u] = hs[u];
+        __syncthreads();
+    }
+}
+
+// BPTT per sequence; the weight gradients accumulate into the workgroup's own slab row
+// [dW_hh 3H x H | dW_ih 3H x I | db_ih 3H | db_hh 3H] (every element read-modified-written by
+// one fixed thread: no races, no atomics), reduced over the rows in row order afterwards.
+__global__ void __launch_bounds__(kGenMaxH) k_gru_gen_bwd(const float* __restrict__ residual,
+                                                          const float* __restrict__ tfeat, const float* __restrict__ w_ih,
+                                                          const float* __restrict__ w_hh, const float* __restrict__ h_seq,
+                                                          const float* __restrict__ gates,
+                                                          const float* __restrict__ dh_last, float* __restrict__ dx,
+                                                          float* __restrict__ slab, int B, int L, int S, int I, int H) {
+    extern __shared__ float gsm[];
+    float* dh = gsm;            // dL/dh_t [H]
+    float* hp = dh + H;         // h_{t-1} [H]
+    float* dgh = hp + H;        // d(W_h. h + b_h.) [3H]
+    float* dgn = dgh + 3 * H;   // d(W_in x + b_in) [H] (the r and z parts equal dgh's)
+    float* xs = dgn + H;        // x_t [I]
+    const int u = threadIdx.x, nt = blockDim.x;
+    const int G3 = 3 * H;
+    const int64_t nseq = static_cast<int64_t>(B) * S, len = static_cast<int64_t>(G3) * (H + I) + 2 * G3;
+    float* row = slab + blockIdx.x * len;
+    float* dwhh = row;
+    float* dwih = row + static_cast<int64_t>(G3) * H;
+    float* dbih = dwih + static_cast<int64_t>(G3) * I;
+    float* dbhh = dbih + G3;
+    // each element is zeroed by the thread that accumulates it
+    if (u < H)
+        for (int j = 0; j < G3; ++j) dwhh[static_cast<int64_t>(j) * H + u] = 0.f;
+    if (u < I)
+        for (int j = 0; j < G3; ++j) dwih[static_cast<int64_t>(j) * I + u] = 0.f;
+    for (int j = u; j < G3; j += nt) dbih[j] = dbhh[j] = 0.f;
+    auto dgi = [&](int j) { return j < 2 * H ? dgh[j] : dgn[j - 2 * H]; };
+    for (int64_t seq = blockIdx.x; seq < nseq; seq += gridDim.x) {
+        const int64_t b = seq / S, sn = seq % S;
+        if (u < H) dh[u] = dh_last[seq * H + u];
+        for (int t = L - 1; t >= 0; --t) {
+            const int64_t r = static_cast<int64_t>(t) * nseq + seq;
+            if (u < I) xs[u] = u == 0 ? residual[(b * L + t) * S + sn] : tfeat[(b * L + t) * (I - 1) + u - 1];
+            float dz_keep = 0.f;
+            if (u < H) {
+                const float h0 = t > 0 ? h_seq[(r - nseq) * H + u] : 0.f;
+                hp[u] = h0;
+                const float rg = gates[(r * 4 + 0) * H + u], zg = gates[(r * 4 + 1) * H + u];
+                const float ng = gates[(r * 4 + 2) * H + u], ghn = gates[(r * 4 + 3) * H + u];
+                const float d = dh[u];
+                const float dnp = d * (1.f - zg) * (1.f - ng * ng);
+                const float dzp = d * (h0 - ng) * zg * (1.f - zg);
+                const float drp = dnp * ghn * rg * (1.f - rg);
+                dgh[u] = drp;
+                dgh[H + u] = dzp;
+                dgh[2 * H + u] = dnp * rg;
+                dgn[u] = dnp;
+                dz_keep = d * zg;
+            }
+            __syncthreads();
+            float acc = dz_keep;
+            if (u < H) {
+                for (int j = 0; j < G3; ++j) {
+                    const float gj = dgh[j];
+                    acc = fmaf(w_hh[static_cast<int64_t>(j) * H + u], gj, acc);
+                    dwhh[static_cast<int64_t>(j) * H + u] += gj * hp[u];
+                }
+            }
+            if (u < I) {
+                float dxi = 0.f;
+                for (int j = 0; j < G3; ++j) {
+                    const float gj = dgi(j);
+                    dxi = fmaf(w_ih[static_cast<int64_t>(j) * I + u], gj, dxi);
+                    dwih[static_cast<int64_t>(j) * I + u] += gj * xs[u];
+                }
+                if (dx) dx[(seq * L + t) * I + u] = dxi;
+            }
+            for (int j = u; j < G3; j += nt) {
+                dbih[j] += dgi(j);
+                dbhh[j] += dgh[j];
+            }
+            __syncthreads();
+            if (u < H) dh[u] = acc;
+        }
+        __syncthreads();
+    }
+}
+
 bool dims_ok(int64_t B, int64_t L, int64_t S) {
     return B >= 0 && L > 0 && S > 0 && L <= INT32_MAX && S <= INT32_MAX && B * S < (int64_t{1} << 31);
 }
@@ -1312,8 +1456,10 @@ extern "C" int lg_lab_gru_stamps_clear(void) {
 #endif
 
 extern "C" int64_t lg_gru_bwd_workspace_bytes(int64_t B, int64_t S, int64_t I, int64_t H) {
-    if (B < 0 || S < 0 || (I != 1 && I != 10) || (H != 32 && H != 64)) return LG_EINVAL;
+    if (B < 0 || S < 0 || (I != 1 && I != 10) || H < 1 || H > kGenMaxH) return LG_EINVAL;
     const int64_t slab = 3 * H * H + 3 * H * I + 6 * H;
+    if (H != 32 && H != 64)
+        return std::max<int64_t>(1, std::min<int64_t>(B * S, kGenBwdBlocks)) * slab * static_cast<int64_t>(sizeof(float));
     return std::max<int64_t>(1, nblocks_seq(B * S)) * slab * static_cast<int64_t>(sizeof(float));
 }
 
@@ -1321,12 +1467,20 @@ extern "C" int lg_gru_fwd(const float* residual, const float* tfeat, const float
                           const float* b_ih, const float* b_hh, float* h_seq, float* gates, float* h_last, int64_t B,
                           int64_t L, int64_t S, int64_t I, int64_t H, lg_stream_t stream) {
     if (!dims_ok(B, L, S)) return LG_EINVAL;
-    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (H < 1 || H > kGenMaxH || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
     if (!residual || !w_ih || !w_hh || !b_ih || !b_hh || !h_last || (I == 10 && !tfeat)) return LG_EINVAL;
     if (gates && !h_seq) return LG_EINVAL;  // the backward needs both
-    if (!fwd_rows_ok(B, S, H)) return LG_EUNSUPPORTED;
     if (B == 0) return LG_OK;
     hipStream_t s = lg_stream(stream);
+    if (H != 32 && H != 64) {  // any other width: the generic kernel
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(B * S, 4096));
+        lg_launch(k_gru_gen_fwd, grid, gen_threads(H), sizeof(float) * (H + I), s, residual, tfeat, w_ih, w_hh, b_ih,
+                  b_hh, h_seq, gates, h_last, static_cast<int>(B), static_cast<int>(L), static_cast<int>(S),
+                  static_cast<int>(I), static_cast<int>(H));
+        LG_RET_IF_LAUNCH_FAILED();
+        return LG_OK;
+    }
+    if (!fwd_rows_ok(B, S, H)) return LG_EUNSUPPORTED;
     return H == 64 ? launch_fwd<64>(I == 10, gates != nullptr, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates,
                                     h_last, B, L, S, s)
                    : launch_fwd<32>(I == 10, gates != nullptr, residual, tfeat, w_ih, w_hh, b_ih, b_hh, h_seq, gates,
@@ -1338,18 +1492,26 @@ extern "C" int lg_gru_bwd(const float* residual, const float* tfeat, const float
                           float* dw_hh, float* db_ih, float* db_hh, int64_t B, int64_t L, int64_t S, int64_t I,
                           int64_t H, void* workspace, int64_t ws_bytes, lg_stream_t stream) {
     if (!dims_ok(B, L, S)) return LG_EINVAL;
-    if ((H != 32 && H != 64) || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
+    if (H < 1 || H > kGenMaxH || (I != 1 && I != 10)) return LG_EUNSUPPORTED;
     if (!residual || !w_ih || !w_hh || !h_seq || !gates || !dh_last || !dw_ih || !dw_hh || !db_ih || !db_hh ||
         !workspace || (I == 10 && !tfeat))
         return LG_EINVAL;
     hipStream_t s = lg_stream(stream);
-    // slabs written: one per workgroup (16 sequences with dx, 32 without)
-    const int nb = static_cast<int>(std::max<int64_t>(1, dx ? nblocks_seq(B * S) : nblocks_seq2(B * S)));
+    const bool gen = H != 32 && H != 64;
+    // slabs written: one per workgroup (16 sequences with dx, 32 without; the generic kernel:
+    // one per workgroup of its grid-stride)
+    const int nb = static_cast<int>(std::max<int64_t>(
+        1, gen ? std::min<int64_t>(B * S, kGenBwdBlocks) : (dx ? nblocks_seq(B * S) : nblocks_seq2(B * S))));
     float* slab = static_cast<float*>(workspace);
     const int64_t G3 = 3 * H, len = G3 * H + G3 * I + 2 * G3;
     if (ws_bytes < nb * len * static_cast<int64_t>(sizeof(float))) return LG_EINVAL;
     if (B == 0) {
         if (hipMemsetAsync(slab, 0, sizeof(float) * len, s) != hipSuccess) return LG_EHIP;
+    } else if (gen) {
+        lg_launch(k_gru_gen_bwd, static_cast<unsigned>(nb), gen_threads(H), sizeof(float) * (6 * H + I), s, residual,
+                  tfeat, w_ih, w_hh, h_seq, gates, dh_last, dx, slab, static_cast<int>(B), static_cast<int>(L),
+                  static_cast<int>(S), static_cast<int>(I), static_cast<int>(H));
+        LG_RET_IF_LAUNCH_FAILED();
     } else {
         const int rc = H == 64 ? launch_bwd<64>(I == 10, dx != nullptr, residual, tfeat, w_ih, w_hh, h_seq, gates,
                                                 dh_last, dx, slab, B, L, S, s)

@@ -773,7 +773,7 @@ extern "C" int lg_linear_dw(const float* dy, const float* x, int64_t K, int64_t 
     return lg_launch_slab_reduce_multi(slab, G, SL, segs, 2, nullptr, nullptr, s);
 }
 
-extern "C" int lg_abi_version(void) { return 25; }
+extern "C" int lg_abi_version(void) { return 26; }
 
 // ------------------------------------------------------------------ kernel timing
 // The event pairs are process-wide (a backward op runs on autograd's worker thread, the

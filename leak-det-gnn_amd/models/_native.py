@@ -15,7 +15,7 @@ import torch
 _PKG_ROOT = Path(__file__).resolve().parent.parent
 LIB_PATH = Path(os.environ.get("LEAKGNN_LIB", _PKG_ROOT / "lib" / "libleakgnn.so"))
 
-ABI_VERSION = 25  # lg_abi_version() of the libleakgnn.so these signatures describe
+ABI_VERSION = 26  # lg_abi_version() of the libleakgnn.so these signatures describe
 
 LG_F_BIAS = 0x01
 LG_F_RELU = 0x02

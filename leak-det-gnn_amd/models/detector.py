@@ -32,6 +32,7 @@ from typing import Dict, Optional, Sequence
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import library, ops
 from .gcn import GCNConv, global_mean_pool  # noqa: F401  (re-exported PyG-compatible API)
@@ -57,8 +58,9 @@ class SharedSensorGRUEncoder(nn.Module):
         if not r.is_cuda:
             raise RuntimeError("SharedSensorGRUEncoder runs on a ROCm GPU only (libleakgnn has no CPU path)")
         g = self.gru
-        if g.num_layers != 1 or g.hidden_size not in (32, 64) or g.bidirectional or not g.bias:
-            raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 32/64, bias")
+        if g.num_layers != 1 or not 1 <= g.hidden_size <= 1024 or g.bidirectional or not g.bias:
+            raise NotImplementedError("the HIP GRU kernels cover the reference encoder: 1 layer, hidden 1..1024 "
+                                      "(32 / 64 tiled, others generic), bias")
         f = ops._f32
         ws = [f(t) for t in (g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)]
         # contiguous once here: a strided tfeat (a slice of a longer segment) would otherwise be
@@ -155,6 +157,7 @@ class LeakDetector(nn.Module):
         # backward in the GRU backward's); False: the encoder module, then library.gnn_trunk
         self.fuse_encoder = True
         self.boundary: Optional[torch.Tensor] = None
+        self._batched_edges: Dict[tuple, torch.Tensor] = {}  # (B, device) -> (2, B*E): the general path's edge_index
 
     def overlap_split(self):
         """Parameters whose gradients are final once the backward reaches `boundary` (the
@@ -205,9 +208,47 @@ class LeakDetector(nn.Module):
             return False
         return library.encoder_trunk_supported(B, N, g.hidden_size, D, len(self.convs), nm, self.compress_x0)
 
+    def _widths_tiled(self) -> bool:
+        """Whether the trunk and heads run the tiled kernels: sensor_hidden == node_hidden in
+        {32, 64} (the reference's callers use 64 and 64, train_detector.py:250-254)."""
+        return (self.sensor_encoder.hidden_size in ops.SUPPORTED_D
+                and self.sensor_to_node.out_features == self.sensor_encoder.hidden_size)
+
+    def _forward_general(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor]) -> torch.Tensor:
+        """Any sensor_hidden / node_hidden (detector.py:128-129): the reference's forward
+        (:170-218) composed from the width-general pieces — the GRU encoder (lg_gru_fwd's generic
+        kernel off 32 / 64), GCNConv's general path (lg_spmm_cols propagate, library GEMM
+        transform) over the batchified edge_index, and library GEMMs / device indexing for the
+        node init and the heads; dropout from torch's generator (the tiled path's counter RNG
+        is a kernel feature).  A generality path: the bench's widths never take it."""
+        B, L, S = residual.shape
+        dev = residual.device
+        graph, inc, slot, sensor_idx, slot_live, nonsensor = self._device_state(dev)
+        N = len(self.node_names)
+        h_s = self.sensor_encoder(residual, tfeat)                           # (B, S, Ds)
+        # h0 rows: [h_s of the node's sensor, 1] for sensor nodes (last duplicate wins, as
+        # h0[:, idx] = h_s), zeros for the rest (:178-187)
+        has = (slot >= 0).to(h_s.dtype).view(1, N, 1)
+        h0 = torch.cat([h_s.index_select(1, slot.clamp(min=0).long()) * has, has.expand(B, N, 1)], dim=-1)
+        p = float(self.dropout.p)
+        x = F.dropout(F.relu(self.sensor_to_node(h0)), p, self.training).reshape(B * N, -1)
+        ei = self._batched_edges.get((B, dev))
+        if ei is None:
+            ei = _batchify_edge_index(self.edge_index_single.to(dev), N, B)
+            self._batched_edges[(B, dev)] = ei
+        for conv in self.convs:
+            x = F.dropout(F.relu(conv(x, ei)), p, self.training)
+        h_nodes = x.view(B, N, -1)
+        ends = inc.ends.long()
+        pipe_logits = self.edge_head(h_nodes[:, ends[:, 0]], h_nodes[:, ends[:, 1]])     # (B, P)
+        pooled = global_mean_pool(x, torch.arange(B, device=dev).repeat_interleave(N), size=B)
+        return torch.cat([pipe_logits, self.noleak_head(pooled).unsqueeze(-1)], dim=-1)
+
     def forward(self, residual: torch.Tensor, tfeat: Optional[torch.Tensor] = None) -> torch.Tensor:
         if not residual.is_cuda:
             raise RuntimeError("LeakDetector runs on a ROCm GPU only (libleakgnn has no CPU path)")
+        if not self._widths_tiled():
+            return self._forward_general(residual, tfeat)
         B, L, S = residual.shape
         graph, inc, slot, sensor_idx, slot_live, nonsensor = self._device_state(residual.device)
         f = ops._f32

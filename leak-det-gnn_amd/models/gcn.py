@@ -9,7 +9,7 @@ reference; the semantics restated here are PyG 2.x's published ones:
      lin = Linear(in, out, bias=False, glorot init)  -> state key ``lin.weight`` [out, in]
      bias = zeros(out)                                -> state key ``bias``
      forward(x, edge_index) = propagate(gcn_norm(edge_index), lin(x)) + bias
-  global_mean_pool(x, batch, size=None) = scatter(x, batch, reduce='mean')
+  global_mean_pool(x, batch, size=None) = scatter(x, batch, reduce='mean', dim_size=size)
 
 Here forward runs the registered op leakgnn::gcn_conv (models/library.py: one fused HIP
 launch of (Ahat x) W^T + b — lg_gcn_fwd_rows, 16-node tiles off the node table, at D = 64;
@@ -119,16 +119,43 @@ class GCNConv(nn.Module):
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"
 
 
+_WINDOW_BATCH: dict = {}  # id(batch) -> (weakref, version, B, N or None): its layout, checked once
+
+
+def _window_layout(batch: torch.Tensor, B: int, rows: int) -> Optional[int]:
+    """N when batch == arange(B).repeat_interleave(N) (equal windows, the detector's layout),
+    else None.  Decided once per batch tensor (object and version counter, as GCNConv's CSR
+    cache): later calls with the same tensor need no device sync."""
+    ent = _WINDOW_BATCH.get(id(batch))
+    if ent is not None and ent[0]() is batch and ent[1] == batch._version and ent[2] == B:
+        return ent[3]
+    N = None
+    if rows % B == 0 and batch.numel() == rows:
+        n = rows // B
+        if torch.equal(batch, torch.arange(B, device=batch.device).repeat_interleave(n)):
+            N = n
+    if len(_WINDOW_BATCH) > 64:
+        _WINDOW_BATCH.clear()
+    _WINDOW_BATCH[id(batch)] = (weakref.ref(batch), batch._version, B, N)
+    return N
+
+
 def global_mean_pool(x: torch.Tensor, batch: Optional[torch.Tensor], size: Optional[int] = None) -> torch.Tensor:
-    """PyG global_mean_pool.  Windows of equal size N (the detector's batch vector,
-    detector.py:214) run the HIP kernel; pass ``size`` to avoid a device sync."""
+    """PyG global_mean_pool(x, batch, size): per-graph mean of the rows of x, graph ids in
+    `batch` (any order, any sizes; a graph with no rows pools to 0, as PyG's scatter mean).
+    Equal windows in order (the detector's batch vector, detector.py:214) at D = 32 / 64 run
+    the HIP kernel (lg_mean_pool_fwd); other batches a device scatter-sum and count.  Pass
+    ``size`` to skip the max() sync; the layout check syncs once per batch tensor."""
+    if not x.is_cuda:
+        raise RuntimeError("global_mean_pool runs on a ROCm GPU only (libleakgnn has no CPU path)")
     if batch is None:
         return x.mean(dim=0, keepdim=True)
     B = int(size) if size is not None else int(batch.max().item()) + 1
-    if x.size(0) % B == 0:
-        N = x.size(0) // B
-        expected = torch.arange(B, device=batch.device).repeat_interleave(N)
-        if not torch.equal(batch, expected):
-            raise NotImplementedError("global_mean_pool kernels need batch = arange(B).repeat_interleave(N)")
-        return torch.ops.leakgnn.mean_pool(_f32(x), B, N)
-    raise NotImplementedError("global_mean_pool kernels need equal-size windows")
+    if x.size(-1) in SUPPORTED_D and x.dim() == 2:
+        N = _window_layout(batch, B, x.size(0))
+        if N is not None:
+            return torch.ops.leakgnn.mean_pool(_f32(x), B, N)
+    idx = batch.to(device=x.device, dtype=torch.long)
+    sums = x.new_zeros((B,) + tuple(x.shape[1:])).index_add(0, idx, x)
+    cnt = torch.bincount(idx, minlength=B).clamp(min=1).to(x.dtype)
+    return sums / cnt.view((B,) + (1,) * (x.dim() - 1))

@@ -107,7 +107,7 @@ def test_c_abi_host_only_calls():
     sizes and argument validation (returns LG_EINVAL before any HIP call)."""
     from models import _native
     lib = _native.load_library()
-    assert lib.lg_abi_version() == _native.ABI_VERSION == 25
+    assert lib.lg_abi_version() == _native.ABI_VERSION == 26
     assert lib.lg_timing_arm(-1) == -1 and lib.lg_timing_disarm() == 0 and lib.lg_timing_elapsed(0, None) == -1
     assert lib.lg_nm_table_build(None, None, 661, None, None, None) == -1
     assert lib.lg_strerror(0) == b"ok" and lib.lg_strerror(-1) == b"invalid argument"
@@ -135,10 +135,13 @@ def test_c_abi_host_only_calls():
                                 101, None) == -1
     assert lib.lg_edge_head_bwd(None, None, None, None, None, None, 764, None, None, None, None, None, 2, 661, 764, 64,
                                 128, 0, 0.0, None, 0, None) == -1
-    # GRU: H in {32, 64}; the backward needs the saved gates; gates need h_seq
-    assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 48) == -1
+    # GRU: H in {32, 64} tiled, other H in 1..1024 generic (ABI 26: 512 slab rows at most);
+    # the backward needs the saved gates; gates need h_seq
+    assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 48) == 512 * (3 * 48 * (48 + 10) + 6 * 48) * 4
+    assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 1025) == -1
     assert lib.lg_gru_bwd_workspace_bytes(256, 29, 10, 32) > 0
-    assert lib.lg_gru_fwd(None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 48, None) == -2
+    assert lib.lg_gru_fwd(None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 48, None) == -1
+    assert lib.lg_gru_fwd(None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 1025, None) == -2
     assert lib.lg_gru_bwd(None, None, None, None, None, None, None, None, None, None, None, None, 2, 36, 29, 10, 64,
                           None, 0, None) == -1
 
