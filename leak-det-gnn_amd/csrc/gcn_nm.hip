@@ -1463,6 +1463,9 @@ struct Nb3Lds {
     static constexpr size_t BYTES = 4 * static_cast<size_t>(MX);
 };
 
+#ifndef LG_NB3_SPLIT
+#define LG_NB3_SPLIT 0  // lab: 1 = the tail round of k_gcn_bwd_nm3 in pieces (r06x: 50.3 vs 48.0 us, slower)
+#endif
 #ifndef LG_NB3_NPF
 #define LG_NB3_NPF 4  // neighbour blocks in flight in the backward (lab builds override)
 #endif
@@ -1504,6 +1507,12 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+#ifdef LG_NM3_STAMPS
+    constexpr int WAVES = kNmBwdWaves3;
+    LG_NM3_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(1, __builtin_amdgcn_s_memtime());
+    int tcount = 0;
+#endif
     const int rl = lane / G::LPR, fg = lane % G::LPR;
     float* tl = tiles + wave * LY::TL;  // t tile [row][feature], later dx
     float* xl = tl + G::TILE;           // x tile [row][feature]
@@ -1542,16 +1551,53 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     for (int k = 0; k < G::K; ++k) loff[k] = (G::RPI * k + rl) * (4u * D) + 16u * fg;
     const NmSched sc = nm_sched(static_cast<int64_t>(ngroups) * N, wave, kNmBwdWaves3);
     // 32-bit scalar tile indices (ntiles < 2^26; see k_gcn_fwd_pc): no 64-bit compares in VGPR pairs
-    const int32_t tend = static_cast<int32_t>(sc.end), tfirst = static_cast<int32_t>(sc.first),
-                  tstride = static_cast<int32_t>(sc.stride);
+    const int32_t tfirst = static_cast<int32_t>(sc.first), tstride = static_cast<int32_t>(sc.stride);
+    // LG_NB3_SPLIT: the tail round in pieces.  The waves of an XCD's chunk (nm_sched) walk
+    // F = C / stride full rounds of its C tiles; the R = C - F stride tiles left would run as a
+    // last round on R of the stride waves (L-TOWN-A, B = 256: 1,322 tiles over 256 waves, a 6th
+    // round for 42 of them).  Those R tiles are cut into q pieces of 16 / q rows each (q the
+    // largest power of two <= K with q R <= stride), so the last round is q R shorter tiles on
+    // as many waves.  A piece is the tile with the other rows' loads out of range (their t, x and
+    // dx rows are zeros, their stores dropped): the same record, mask words and arithmetic.
+    // Virtual index v: [cs, cs + F stride) full tiles, then q R pieces.
+    int32_t vcs = 0, vfull = 0, vend = static_cast<int32_t>(sc.end);
+    int qsh = 0;
+    {
+        const int64_t G = gridDim.x;
+        const int64_t ntiles = static_cast<int64_t>(ngroups) * N;
+        int64_t c0 = 0, c1 = ntiles;
+        if (G >= 8) {
+            const int64_t chunk = (ntiles + 7) / 8, x = blockIdx.x % 8;
+            c0 = std::min<int64_t>(ntiles, x * chunk);
+            c1 = std::min<int64_t>(ntiles, c0 + chunk);
+        }
+        const int64_t C = c1 - c0, W = sc.stride, F = C / W, R = C - F * W;
+        vcs = static_cast<int32_t>(c0);
+        vfull = static_cast<int32_t>(c0 + F * W);
+        if (LG_NB3_SPLIT && R > 0)
+            while (qsh < 2 && (int64_t{2} << qsh) <= G::K && (R << (qsh + 1)) <= W) ++qsh;
+        vend = static_cast<int32_t>(c0 + F * W + (R << qsh));
+    }
+    const int32_t tend = vend;
 
-    auto tile_coords = [&](int32_t tile, uint32_t& n, uint32_t& b0, uint32_t& nb) {
-        const bool valid = tile < tend;
-        const uint32_t t32 = static_cast<uint32_t>(valid ? tile : 0);
+    // virtual index -> (node, window base b0, rows [rlo, nb) of the 16-row block)
+    auto tile_coords = [&](int32_t v, uint32_t& n, uint32_t& b0, uint32_t& nb, uint32_t& rlo) {
+        const bool valid = v < vend;
+        int32_t tile = valid ? v : vcs;
+        rlo = 0;
+        uint32_t rhi = 16;
+        if (qsh && tile >= vfull) {
+            const int32_t h = tile - vfull;
+            tile = vfull + (h >> qsh);
+            const uint32_t rows = 16u >> qsh;
+            rlo = static_cast<uint32_t>(h & ((1 << qsh) - 1)) * rows;
+            rhi = rlo + rows;
+        }
+        const uint32_t t32 = static_cast<uint32_t>(tile);
         const uint32_t grp = lg_div(t32, fdN);
         n = t32 - grp * N;
         b0 = grp * 16;
-        nb = valid ? min(16u, B - b0) : 0u;
+        nb = valid ? min(rhi, B - b0) : 0u;
     };
     auto ld = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off) {
         return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -1585,20 +1631,23 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     NmRec cur;
     uint32_t cn, cb0;
     int cslot = -1;  // X0: the tile's sensor slot (-1: its x block is a mask word in px[0][0])
-    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb, int pslot) {
+    auto issue = [&](const NmRec& r, uint32_t n, uint32_t b0, uint32_t nb, uint32_t rlo, int pslot) {
         n = static_cast<uint32_t>(r.node);  // tiles run in the table's schedule order (slot -> node)
         cur = r;
         cn = n;
         cb0 = b0;
         cslot = pslot;
 #pragma unroll
-        for (int k = 0; k < G::K; ++k) lo[k] = (G::RPI * k + rl) < static_cast<int>(nb) ? loff[k] : kNm3RowOob;
+        for (int k = 0; k < G::K; ++k) {
+            const int row = G::RPI * k + rl;
+            lo[k] = row < static_cast<int>(nb) && row >= static_cast<int>(rlo) ? loff[k] : kNm3RowOob;
+        }
         // X0: both the sensor-row and the mask-word loads are always issued, the one that does
         // not apply out of range (a load under a branch is waited for where the branch merges)
         if constexpr (X0)
             pxb = __builtin_amdgcn_raw_buffer_load_b16(
                 x0bs, nb && pslot < 0 ? nm_mask_off(n, b0 >> 4, ngroups, lane) : kNm3BlkOob + 2u * lane, 0, 0);
-        const bool rows = nb && (!X0 || pslot >= 0);
+        const bool rows = nb > rlo && (!X0 || pslot >= 0);
         const uint32_t ob = rows ? ((X0 ? static_cast<uint32_t>(pslot) : n) * B + b0) * (4u * D) : kNm3BlkOob;
 #pragma unroll
         for (int k = 0; k < G::K; ++k) px[k] = ld(xs, lo[k] + ob);
@@ -1617,11 +1666,6 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
     // X0: the sensor slot of schedule position i (wave-uniform scalar load, no dependence on
     // the record)
     auto pslot_of = [&](uint32_t i) -> int { return X0 ? __builtin_amdgcn_readfirstlane(x0.pos_slot[i]) : -1; };
-    {
-        uint32_t n0, b00, nb00;
-        tile_coords(tfirst, n0, b00, nb00);
-        issue(nm_rec(tab, N + n0), n0, b00, nb00, pslot_of(n0));  // schedule section
-    }
     // W^T split to LDS: element (o, i) of W lands at row i, column o of each part
     static_assert(!(F16 && BF), "one transform");
     int sW = 0;  // F16: W's scale exponent (every wave reads all of W for its max: no barrier)
@@ -1634,40 +1678,95 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         }
         sW = lg_f16_scale_exp_c(lg_wave_max_bits(m));
     }
-    {
-        constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
-        f32x4 wv[WPER];
+    if constexpr (LG_NB3_WFRAG) {
+        // fragment (mt, s2), lane l: W^T rows 16 mt + (l & 15), columns 32 s2 + 8 (l >> 4) .. + 7,
+        // i.e. W[o][i] for 8 consecutive o: column reads of W (16 lanes = 64 contiguous bytes) and
+        // one 16-byte LDS store per plane (64 consecutive pieces).  The per-element form (4 float4
+        // reads, 48 2-byte LDS stores a thread) left the waves 9.3 us from start to this barrier (r06y).
+        constexpr int CH = D / 16, KS = D / 32, NF = CH * KS * 64, NT3 = 64 * kNmBwdWaves3;
+        constexpr int IT = (NF + NT3 - 1) / NT3;
+        f32x4 wu[IT], wv[IT];
 #pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
+        for (int it = 0; it < IT; ++it) {
+            const int f = min(it * NT3 + static_cast<int>(threadIdx.x), NF - 1), l = f & 63, ms = f >> 6;
+            const int i = 16 * (ms / KS) + (l & 15), k0 = 32 * (ms % KS) + 8 * (l >> 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                wu[it][e] = W[(k0 + e) * D + i];
+                wv[it][e] = W[(k0 + 4 + e) * D + i];
+            }
+        }
+        {  // the first tile's loads after W's (vmcnt counts in order: the stores below wait for W alone)
+            uint32_t n0, b00, nb00, rl00;
+            tile_coords(tfirst, n0, b00, nb00, rl00);
+            issue(nm_rec(tab, N + n0), n0, b00, nb00, rl00, pslot_of(n0));  // schedule section
+        }
         const float wsc = lg_pow2f(sW);
 #pragma unroll
-        for (int u = 0; u < WPER; ++u) {
-            const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
-            if (i4 >= W4) continue;
-            const int o = i4 / (D / 4), c4 = 4 * (i4 % (D / 4));
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int e = wix(c4 + c, o);
-                const float w = wv[u][c];
-                if constexpr (F16) {
-                    const _Float16 h0 = static_cast<_Float16>(w * wsc);
-                    const _Float16 h1 = static_cast<_Float16>(w * wsc - static_cast<float>(h0));
-                    wsl[e] = __builtin_bit_cast(uint16_t, h0);
-                    wsl[WP + e] = __builtin_bit_cast(uint16_t, h1);
-                    continue;
+        for (int it = 0; it < IT; ++it) {
+            const int f = it * NT3 + static_cast<int>(threadIdx.x);
+            if (f >= NF) continue;
+            uint16_t* dst = wsl + 8 * f;
+            if constexpr (F16) {
+                lg_f16x8 h0, h1;
+                split2_f16_x8(wu[it] * wsc, wv[it] * wsc, h0, h1);
+                *reinterpret_cast<lg_f16x8*>(dst) = h0;
+                *reinterpret_cast<lg_f16x8*>(dst + WP) = h1;
+            } else {
+                lg_bf16x8 h0, h1, h2;
+                split3_x8(wu[it], wv[it], h0, h1, h2);
+                *reinterpret_cast<lg_bf16x8*>(dst) = h0;
+                if constexpr (!BF) {
+                    *reinterpret_cast<lg_bf16x8*>(dst + WP) = h1;
+                    *reinterpret_cast<lg_bf16x8*>(dst + 2 * WP) = h2;
                 }
-                const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
-                const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
-                const uint16_t h1 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r1));
-                const float r2 = r1 - __uint_as_float(static_cast<uint32_t>(h1) << 16);
-                const uint16_t h2 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r2));
-                wsl[e] = h0;
-                wsl[WP + e] = h1;
-                wsl[2 * WP + e] = h2;
+            }
+        }
+    } else {
+    {
+            constexpr int W4 = D * D / 4, WPER = (W4 + 64 * kNmBwdWaves3 - 1) / (64 * kNmBwdWaves3);
+            f32x4 wv[WPER];
+    #pragma unroll
+            for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * 64 * kNmBwdWaves3 + threadIdx.x, W4 - 1));
+            // the first tile's loads AFTER W's: vmcnt counts in order, so the staging below waits for
+            // W alone (issued first, the staging waited for the tile's 20 gathered blocks as well:
+            // 9.3 us from start to the barrier, r06y)
+            {
+                uint32_t n0, b00, nb00, rl00;
+                tile_coords(tfirst, n0, b00, nb00, rl00);
+                issue(nm_rec(tab, N + n0), n0, b00, nb00, rl00, pslot_of(n0));  // schedule section
+            }
+            const float wsc = lg_pow2f(sW);
+    #pragma unroll
+            for (int u = 0; u < WPER; ++u) {
+                const int i4 = u * 64 * kNmBwdWaves3 + threadIdx.x;
+                if (i4 >= W4) continue;
+                const int o = i4 / (D / 4), c4 = 4 * (i4 % (D / 4));
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int e = wix(c4 + c, o);
+                    const float w = wv[u][c];
+                    if constexpr (F16) {
+                        const _Float16 h0 = static_cast<_Float16>(w * wsc);
+                        const _Float16 h1 = static_cast<_Float16>(w * wsc - static_cast<float>(h0));
+                        wsl[e] = __builtin_bit_cast(uint16_t, h0);
+                        wsl[WP + e] = __builtin_bit_cast(uint16_t, h1);
+                        continue;
+                    }
+                    const uint16_t h0 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(w));
+                    const float r1 = w - __uint_as_float(static_cast<uint32_t>(h0) << 16);
+                    const uint16_t h1 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r1));
+                    const float r2 = r1 - __uint_as_float(static_cast<uint32_t>(h1) << 16);
+                    const uint16_t h2 = __builtin_bit_cast(uint16_t, static_cast<__bf16>(r2));
+                    wsl[e] = h0;
+                    wsl[WP + e] = h1;
+                    wsl[2 * WP + e] = h2;
+                }
             }
         }
     }
     __syncthreads();
+    LG_NM3_STAMP(2, __builtin_amdgcn_s_memtime());
 
     f32x4 dw[G::CH][G::CH];  // dW tile (mo, ni): rows o = 16mo + 4q + reg, cols i = 16ni + j
 #pragma unroll
@@ -1686,8 +1785,8 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
         uint32_t tlo[G::K];
 #pragma unroll
         for (int k = 0; k < G::K; ++k) tlo[k] = lo[k];
-        uint32_t nn, nb0, nnb;
-        tile_coords(tile + tstride, nn, nb0, nnb);
+        uint32_t nn, nb0, nnb, nrlo;
+        tile_coords(tile + tstride, nn, nb0, nnb, nrlo);
         const NmRec nxt = nm_rec(tab, N + nn);
         const int nslot = pslot_of(nn);
         asm volatile("" ::: "memory");  // keep the record request here (the compiler sinks it otherwise)
@@ -1762,7 +1861,7 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             for (int k = 0; k < G::K; ++k)
                 dbacc += MB ? dzb(ld(dys, tlo[k] + ob), bo, k) : dzf(ld(dys, tlo[k] + ob), MY ? ld(ms, tlo[k] + ob) : f32x4{});
         }
-        issue(nxt, nn, nb0, nnb, nslot);
+        issue(nxt, nn, nb0, nnb, nrlo, nslot);
         __builtin_amdgcn_sched_barrier(0);
 
         int st = 0, sx = 0;  // F16: the tile's t and x scale exponents
@@ -1936,7 +2035,17 @@ k_gcn_bwd_nm3(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, c
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vk[k]),
                                                    dxs, tlo[k] + ob, 0, kLgActAux);
         lg_store_guard(vk);
+#ifdef LG_NM3_STAMPS
+        if (tcount < 16) LG_NM3_STAMP(3 + tcount, __builtin_amdgcn_s_memtime());
+        ++tcount;
+#endif
     }
+#ifdef LG_NM3_STAMPS
+    LG_NM3_STAMP(21, __builtin_amdgcn_s_memtime());
+    LG_NM3_STAMP(22, __builtin_amdgcn_s_memrealtime());
+    LG_NM3_STAMP(23, (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11))) << 32) |
+                         static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11))));
+#endif
     if constexpr (F16) {  // dw back to units of 1 (two exact factors)
         const float r1 = lg_pow2f(-(tc / 2)), r2 = lg_pow2f(-(tc - tc / 2));
 #pragma unroll

@@ -101,6 +101,55 @@ def stamps_summary(lib, launch):
             "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
 
 
+def bwd_stamps_summary(lib, launch):
+    """k_gcn_bwd_nm3 per-wave timeline (LG_NM3_STAMPS build): W staging, each tile's duration
+    (end stamp to end stamp; the first from the staging barrier), tiles per wave, the wave ends
+    and the latest end per XCD, in microseconds."""
+    import ctypes
+    lib.lg_lab_nm3_stamps_clear.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.restype = ctypes.c_int
+    lib.lg_lab_nm3_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    torch.cuda.synchronize()
+    check(lib.lg_lab_nm3_stamps_clear(), "stamps clear")
+    torch.cuda.synchronize()
+    launch()
+    torch.cuda.synchronize()
+    n = 8192 * 24
+    buf = np.zeros(n, dtype=np.uint64)
+    check(lib.lg_lab_nm3_stamps(buf.ctypes.data, n), "stamps read")
+    st = buf.reshape(8192, 24).astype(np.int64)
+    st = st[st[:, 0] != 0]
+    rt0, rt1, c0, c1 = st[:, 0], st[:, 22], st[:, 1], st[:, 21]
+    ghz = float(np.median((c1 - c0) / np.maximum(rt1 - rt0, 1))) * 0.1
+    us = lambda cyc: cyc / (ghz * 1e3)
+    t0 = rt0.min()
+    start, end = (rt0 - t0) / 100.0, (rt1 - t0) / 100.0
+    tiles = np.array([int((r[3:19] != 0).sum()) for r in st])
+    dur, first, last = [], [], []
+    for r in st:
+        prev = r[2]
+        for t in range(16):
+            if r[3 + t] == 0:
+                break
+            d = us(r[3 + t] - prev)
+            dur.append(d)
+            if t == 0:
+                first.append(d)
+            prev = r[3 + t]
+        if r[3] != 0:
+            last.append(us(r[21] - prev))
+    q = lambda a: [round(float(np.percentile(a, p)), 3) for p in (10, 50, 90, 99)]
+    xcc = (st[:, 23] >> 32) & 0xF
+    return {"waves": int(len(st)), "clock_GHz": round(ghz, 3), "span_us": round(float(end.max()), 3),
+            "start_us_p10_50_90_99": q(start), "end_us_p10_50_90_99": q(end),
+            "staging_us_p10_50_90_99": q(us(st[:, 2] - st[:, 1])),
+            "tile_us_p10_50_90_99": q(dur), "first_tile_us_p10_50_90_99": q(first) if first else None,
+            "epilogue_us_p10_50_90_99": q(last) if last else None,
+            "tiles_hist": {int(k): int(v) for k, v in zip(*np.unique(tiles, return_counts=True))},
+            "end_by_tiles_p50": {int(k): round(float(np.median(end[tiles == k])), 3) for k in np.unique(tiles)},
+            "end_by_xcc_us": [round(float(end[xcc == i].max()), 3) if (xcc == i).any() else None for i in range(8)]}
+
+
 def gru_stamps_summary(lib, launch, nst=48, steps=8):
     """k_gru_bwd2 per-step timeline (stamps build): for 8 mid-kernel steps of every wave, the
     clocks at the step's start (a), before its barrier (b), after it (c) and once dh is formed
@@ -354,6 +403,8 @@ def main():
         else:
             byts = (16 if fl & nat.LG_F_MASK_IN else 12) * B * N * D
         res[name] = {"us": t, "GBps": byts / t / 1e3}
+        if args.stamps and hasattr(lib, "lg_lab_nm3_stamps"):
+            res[name]["stamps"] = bwd_stamps_summary(lib, f)
     if "node_init" in which:  # sensor projection + node init (x0 = B*N*D fp32 written, node-major)
         S5 = 29
         slot = torch.full((N,), -1, dtype=torch.int32, device=dev)
