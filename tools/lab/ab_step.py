@@ -3,7 +3,8 @@
 and per launch position the mean in-graph duration (bench.step_breakdown's kernels_mean_us).
 
   python tools/lab/ab_step.py --reps 2 base wsd prec      (base = the product library;
-                                                           <name> = leak-det-gnn_amd/lib/<name>/)
+                                                           <name> = leak-det-gnn_amd/lib/<name>/;
+                                                           <name>:K=V,.. also sets environment)
 """
 import argparse
 import json
@@ -26,11 +27,20 @@ def main():
     res = {v: [] for v in args.variants}
     for r in range(args.reps):
         for v in args.variants:
-            if v == "base":
+            lib, _, envs = v.partition(":")  # <lib>[:K=V,K=V]: environment for the traced step too
+            if lib == "base":
                 os.environ.pop("LEAKGNN_LIB", None)
             else:
-                os.environ["LEAKGNN_LIB"] = str(REPO / "leak-det-gnn_amd" / "lib" / v / "libleakgnn.so")
+                os.environ["LEAKGNN_LIB"] = str(REPO / "leak-det-gnn_amd" / "lib" / lib / "libleakgnn.so")
+            kv = dict(e.split("=", 1) for e in envs.split(",") if e)
+            old = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
             bd = bench.step_breakdown(args.B, 1.0)
+            for k, o in old.items():
+                if o is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = o
             if bd is None:
                 print(f"{v} round {r}: no trace", flush=True)
                 continue
