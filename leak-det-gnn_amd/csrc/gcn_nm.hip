@@ -568,6 +568,9 @@ constexpr bool kPcWsplit = LG_PC_WSPLIT != 0;
 // (r05j: 10.7 us for the launch with neither loads nor consumer work, 15.1 with the loads).
 // Its waits for loads it does see stay correct: the asm loads are older, and vmcnt counts in
 // order.  0: the builtin loads (A/B).
+#ifndef LG_PC_EARLY
+#define LG_PC_EARLY 1
+#endif
 #ifndef LG_PC_ASMLOAD
 #define LG_PC_ASMLOAD 1
 #endif
@@ -778,6 +781,11 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     // (kPrecs: after the counter barrier, synchronised among the producer waves alone)
     constexpr bool kWs = kPcWsplit && (X0 || LG_PC_WS_DENSE);
     constexpr bool kPrecs = kWs && LG_PC_PREC && kPcRecs > 0;
+    // LG_PC_EARLY (dense layers): the producers' first two tiles (draws p and kPcProd + p, the
+    // counter starting past them) are issued before the prologue barrier, from records read
+    // through the scalar cache, while the consumer waves alone stage W, the bias and the records:
+    // the kernel's first gathers overlap the W staging instead of following it
+    constexpr bool kEarly = LG_PC_EARLY && !kWs && !LG_PC_STATIC && !LG_PC_DYN;
     const int nrec = ((kWs && !kPrecs) || LG_PC_STATIC || LG_PC_DYN) ? 0 : min(kPcRecs, tend > tfirst ? (tend - tfirst + tstride - 1) / tstride : 0);
     uint32_t* wrdy = ctr + 1;  // kWs: consumer waves done staging W
     uint32_t* prdy = ctr + 2;  // kPrecs: producer waves done staging the records
@@ -790,46 +798,51 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
             *prdy = 0u;
         }
     } else {
-        constexpr int W4 = D * D / 4, WPER = (W4 + NT - 1) / NT, RPER = kPcRecs ? (4 * kPcRecs + NT - 1) / NT : 1;
-        f32x4 wv[WPER];
+        // the staging threads: all of the workgroup, or (kEarly) its consumer waves
+        constexpr int SNT = kEarly ? NT - 64 * kPcProd : NT;
+        const int st = static_cast<int>(threadIdx.x) - (kEarly ? 64 * kPcProd : 0);
+        if (!kEarly || !producer) {
+            constexpr int W4 = D * D / 4, WPER = (W4 + SNT - 1) / SNT, RPER = kPcRecs ? (4 * kPcRecs + SNT - 1) / SNT : 1;
+            f32x4 wv[WPER];
 #pragma unroll
-        for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * NT + threadIdx.x, W4 - 1));
-        lg_u32x4 rv[RPER];
+            for (int u = 0; u < WPER; ++u) wv[u] = ld4(W + 4 * min<int>(u * SNT + st, W4 - 1));
+            lg_u32x4 rv[RPER];
 #pragma unroll
-        for (int u = 0; u < RPER; ++u) {  // quarter (i & 3) of record i >> 2
-            const int i = u * NT + threadIdx.x;
-            uint32_t n, b0, nb;
-            tile_coords(i < 4 * nrec ? tfirst + (i >> 2) * tstride : tend, n, b0, nb);
-            rv[u] = reinterpret_cast<const lg_u32x4*>(tab)[4 * (static_cast<size_t>(N) + n) + (i & 3)];
-        }
-        const float bb = (bias && threadIdx.x < D) ? bias[threadIdx.x] : 0.f;
-        uint32_t wm = 0;
-#pragma unroll
-        for (int u = 0; u < WPER; ++u) {
-            const int i = u * NT + threadIdx.x;
-            f32x4 w = wv[u] * fold;
-            asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
-            if (i < W4) {
-                st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
+            for (int u = 0; u < RPER; ++u) {  // quarter (i & 3) of record i >> 2
+                const int i = u * SNT + st;
+                uint32_t n, b0, nb;
+                tile_coords(i < 4 * nrec ? tfirst + (i >> 2) * tstride : tend, n, b0, nb);
+                rv[u] = reinterpret_cast<const lg_u32x4*>(tab)[4 * (static_cast<size_t>(N) + n) + (i & 3)];
             }
-        }
+            const float bb = (bias && st < D) ? bias[st] : 0.f;
+            uint32_t wm = 0;
 #pragma unroll
-        for (int u = 0; u < RPER; ++u) {
-            const int i = u * NT + threadIdx.x;
-            if (i < 4 * nrec) reinterpret_cast<lg_u32x4*>(recs)[i] = rv[u];
-        }
-        if (threadIdx.x < D) wst[D * LY::WS + threadIdx.x] = bb * fold;
-        if constexpr (F16) {
-            wm = lg_wave_max_bits(wm);
-            if (lane == 0) wmx[wave] = wm;
+            for (int u = 0; u < WPER; ++u) {
+                const int i = u * SNT + st;
+                f32x4 w = wv[u] * fold;
+                asm volatile("" : "+v"(w));  // rounded before any split (no contraction)
+                if (i < W4) {
+                    st4(wst + (i / (D / 4)) * LY::WS + 4 * (i % (D / 4)), w);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) wm = max(wm, __float_as_uint(fabsf(w[c])));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RPER; ++u) {
+                const int i = u * SNT + st;
+                if (i < 4 * nrec) reinterpret_cast<lg_u32x4*>(recs)[i] = rv[u];
+            }
+            if (st < D) wst[D * LY::WS + st] = bb * fold;
+            if constexpr (F16) {
+                wm = lg_wave_max_bits(wm);
+                if (lane == 0) wmx[wave] = wm;
+            }
         }
         if (threadIdx.x < 16 + kPcProd * NC) ready[threadIdx.x] = 0u;  // ready[] and done[]
         if (threadIdx.x < kPcProd) fin[threadIdx.x] = ~0u;
-        if (threadIdx.x == 0) *ctr = 0u;
+        if (threadIdx.x == 0) *ctr = kEarly ? 2u * kPcProd : 0u;
     }
-    __syncthreads();
+    if (!kEarly || !producer) __syncthreads();  // kEarly: the producers arrive after their first issues
     if (kPrecs && producer) {  // the producers' record staging (the workgroup's first nrec tiles)
         constexpr int PT = 64 * kPcProd, RP = (4 * kPcRecs + PT - 1) / PT;
         lg_u32x4 rv[RP];
@@ -1174,10 +1187,25 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
         };
         {
             NmRec r0, r1;
-            const int32_t f0 = grab(r0), f1 = grab(r1);
+            int32_t f0, f1;
+            if constexpr (kEarly) {  // draws prod and kPcProd + prod, records through the scalar cache
+                auto early = [&](int i, NmRec& r) {
+                    const int32_t tile = tfirst + i * tstride;
+                    uint32_t n, b0, nb;
+                    tile_coords(tile, n, b0, nb);
+                    r = nm_rec(tab, N + n);
+                    return tile;
+                };
+                f0 = early(prod, r0);
+                f1 = early(kPcProd + prod, r1);
+            } else {
+                f0 = grab(r0);
+                f1 = grab(r1);
+            }
             issue(std::integral_constant<int, 0>{}, r0, f0);
             issue(std::integral_constant<int, 1>{}, r1, f1);
         }
+        if constexpr (kEarly) __syncthreads();  // the prologue barrier (W, bias, records, counter)
         int64_t t = 0;
         for (;; t += 2) {
             if (!step(std::integral_constant<int, 0>{}, t)) break;
@@ -1220,7 +1248,7 @@ k_gcn_fwd_pc(const int32_t* __restrict__ tab, const int2* __restrict__ pairs, co
     int sw = 0;  // F16: W's scale exponent
     if constexpr (F16) {
         uint32_t m = 0;
-        for (int w = kWs ? kPcProd : 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
+        for (int w = (kWs || kEarly) ? kPcProd : 0; w < kPcProd * (1 + NC); ++w) m = max(m, wmx[w]);
         sw = lg_f16_scale_exp(__builtin_amdgcn_readfirstlane(m));
     }
     lg_bf16x8 wf[NP][G::CH][KS];
