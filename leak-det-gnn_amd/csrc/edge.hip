@@ -559,7 +559,7 @@ k_edge_bwd(const int64_t* __restrict__ ends, const float* __restrict__ h, const 
     using G = EG<D>;
     static_assert(!(F16 && BF), "one transform");
     constexpr bool SCAT = MODE == 1, STREAM = MODE == 2, WIN = MODE != 0;  // WIN: workgroups own windows
-    constexpr int SL = HID * G::K3 + 2 * HID + 1;
+    constexpr int SL = (HID * G::K3 + 2 * HID + 1 + 3) & ~3;  // rows padded to 16 bytes (the reduce's vector loads)
     constexpr int NPL = F16 ? 2 : 3;  // image planes
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if constexpr (STREAM) {
@@ -1203,7 +1203,7 @@ extern "C" int lg_edge_head_fwd(const int64_t* ends, const float* h, const float
 
 extern "C" int64_t lg_edge_head_bwd_workspace_bytes(int64_t B, int64_t P, int64_t D, int64_t hidden) {
     if (B < 0 || P < 0 || hidden != HID || (D != 32 && D != 64)) return LG_EUNSUPPORTED;
-    const int64_t SL = HID * 3 * D + 2 * HID + 1;
+    const int64_t SL = (HID * 3 * D + 2 * HID + 1 + 3) & ~int64_t(3);  // = k_edge_bwd's padded slab row
     // rows for the larger of the two grids: tile-strided (lg_edge_head_bwd) and one workgroup per
     // window (lg_edge_head_bwd_scatter), which is the larger when P < 2048 / D pipes
     const int64_t G = std::max<int64_t>(bwd_grid(cdiv(std::max<int64_t>(B * P, 1), tile_rows(D))),
@@ -1238,7 +1238,7 @@ int edge_bwd_impl(const int64_t* ends, const float* h, const float* w1, const fl
     // of lg_edge_head_bwd_workspace_bytes has a row for every one of them
     const int grid = scat ? static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(B, lg_num_cus()))) : bwd_grid(ntiles);
     const float scale = dropout ? 1.0f / (1.0f - dropout_p) : 1.0f;
-    const int64_t SL = HID * 3 * D + 2 * HID + 1;
+    const int64_t SL = (HID * 3 * D + 2 * HID + 1 + 3) & ~int64_t(3);  // = k_edge_bwd's padded slab row
     // the slab the launch grid writes: a row per workgroup + one fp64 per workgroup
     if (ws_bytes < ((grid * SL * 4 + 255) & ~int64_t(255)) + grid * 8) return LG_EINVAL;
     float* slab = static_cast<float*>(workspace);

@@ -151,6 +151,10 @@ extern "C" int lg_cross_entropy_fwd(const float* logits, const int64_t* target, 
     }
     if (!logits || !target || !lse || !rowloss) return LG_EINVAL;
     // at most one workgroup per CU: the sc1 hand-off above was measured in that configuration
+    // at most one workgroup per CU: every workgroup of the launch is co-resident, so the last
+    // ticket is taken only after every workgroup's row losses have left (the fence-free
+    // hand-off above was validated at this grid; larger B loops inside the workgroups,
+    // tests/test_gpu_library.py::test_cross_entropy_matches_torch at B = 65,536)
     const int grid = static_cast<int>(std::min<int64_t>((B + kCeWaves - 1) / kCeWaves, lg_num_cus()));
     lg_launch(k_ce_fwd, grid, kCeThreads, 0, s, logits, target, B, C, ldx, ignore_index, lse, rowloss, counter, loss);
     LG_RET_IF_LAUNCH_FAILED();

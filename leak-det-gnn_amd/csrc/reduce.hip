@@ -21,6 +21,9 @@ namespace {
 
 constexpr int kJobSegs = 24;  // segments per launch (a whole detector backward: trunk 8, heads 6, GRU 4)
 constexpr int kJobD = 4;      // fp64 columns per launch
+#ifndef LG_SLAB_VEC
+#define LG_SLAB_VEC 1  // 16-byte column loads for aligned segments (lab: 0 = one column per lane)
+#endif
 
 struct Segs {
     const float* slab[kJobSegs];
@@ -28,6 +31,7 @@ struct Segs {
     int64_t stride[kJobSegs], off[kJobSegs], stride2[kJobSegs], off2[kJobSegs], len[kJobSegs];
     float* out[kJobSegs];
     int G[kJobSegs], G2[kJobSegs];
+    int vec[kJobSegs];        // 1: 16-byte aligned rows (stride, off, len multiples of 4): a lane sums 4 columns
     int first[kJobSegs + 1];  // first block of each segment; first[n] = total column blocks
     int n;
     const double* dslab[kJobD];
@@ -52,6 +56,29 @@ __device__ __forceinline__ void slab_col_sum(const float* __restrict__ src, int 
     for (; g < G; g += 16) acc += src[static_cast<int64_t>(g) * stride + col];
 }
 
+// the same as slab_col_sum for 4 adjacent columns (one 16-byte load per slab row): each column
+// keeps slab_col_sum's order, so the sums are bit-identical to the scalar form
+__device__ __forceinline__ void slab_col_sum4(const float* __restrict__ src, int G, int64_t stride, int64_t col, int w,
+                                              double (&acc)[4]) {
+    constexpr int kRedInflight = 16;
+    int g = w;
+    for (; g + 16 * (kRedInflight - 1) < G; g += 16 * kRedInflight) {
+        f32x4 v[kRedInflight];
+#pragma unroll
+        for (int u = 0; u < kRedInflight; ++u)
+            v[u] = *reinterpret_cast<const f32x4*>(src + static_cast<int64_t>(g + 16 * u) * stride + col);
+#pragma unroll
+        for (int u = 0; u < kRedInflight; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] += v[u][c];
+    }
+    for (; g < G; g += 16) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(src + static_cast<int64_t>(g) * stride + col);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] += v[c];
+    }
+}
+
 __global__ void __launch_bounds__(1024) k_slab_reduce(Segs sg) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.x;
@@ -71,6 +98,27 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(Segs sg) {
     }
     int k = 0;
     while (k + 1 < sg.n && b >= sg.first[k + 1]) ++k;
+    if (sg.vec[k]) {  // 256 columns per block, 4 per lane
+        __shared__ double part4[16][256];
+        const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 256 + 4 * lane;
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        if (col < sg.len[k]) {
+            slab_col_sum4(sg.slab[k] + sg.off[k], sg.G[k], sg.stride[k], col, w, acc);
+            if (sg.slab2[k]) slab_col_sum4(sg.slab2[k] + sg.off2[k], sg.G2[k], sg.stride2[k], col, w, acc);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) part4[w][4 * lane + c] = acc[c];
+        __syncthreads();
+        if (threadIdx.x < 256) {
+            const int64_t cc = static_cast<int64_t>(b - sg.first[k]) * 256 + threadIdx.x;
+            if (cc < sg.len[k]) {
+                double t = part4[0][threadIdx.x];
+                for (int i = 1; i < 16; ++i) t += part4[i][threadIdx.x];
+                sg.out[k][cc] = static_cast<float>(t);
+            }
+        }
+        return;
+    }
     const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 64 + lane;
     __shared__ double part[16][64];
     double acc = 0.0;
@@ -122,8 +170,16 @@ int launch_jobs(const SegJob* segs, int nseg, const DJob* dj, int nd, hipStream_
         sg.G2[i] = j.seg.G2;
         sg.stride2[i] = j.seg.stride2;
         sg.off2[i] = j.seg.off2;
+        auto al4 = [](uint64_t v) { return (v & 3u) == 0; };
+        // 4 columns a lane cut the blocks 4x: only where each wave's rows fit one round of loads
+        // (G <= 256: the heads' and the GRU's slabs; the trunk's 512 rows measured slower, r06zd)
+        const bool vec = LG_SLAB_VEC && j.G <= 256 && (!j.seg.slab2 || j.seg.G2 <= 256) && al4(reinterpret_cast<uintptr_t>(j.slab) / 4) && al4(j.stride) &&
+                         al4(j.seg.off) && al4(j.seg.len) &&
+                         (!j.seg.slab2 || (al4(reinterpret_cast<uintptr_t>(j.seg.slab2) / 4) && al4(j.seg.stride2) &&
+                                           al4(j.seg.off2)));
+        sg.vec[i] = vec ? 1 : 0;
         sg.first[i] = blocks;
-        blocks += static_cast<int>((j.seg.len + 63) / 64);
+        blocks += static_cast<int>(vec ? (j.seg.len + 255) / 256 : (j.seg.len + 63) / 64);
     }
     sg.first[nseg] = blocks;
     sg.n = nseg;

@@ -324,10 +324,12 @@ def test_clip_adamw_two_million_parameters_matches_torch():
 def test_cross_entropy_matches_torch():
     """models/loss.py CrossEntropyLoss (one HIP launch each way) == torch's nn.CrossEntropyLoss:
     loss and dlogits at the detector's shape, with ignored rows, and the all-ignored NaN;
-    a non-default configuration falls through to torch."""
+    a non-default configuration falls through to torch.  B = 65,536: 64x
+    more rows than the capped grid's waves, so every workgroup loops over many rows before the
+    fence-free last-workgroup hand-off (loss.hip header)."""
     from models.loss import CrossEntropyLoss
     torch.manual_seed(3)
-    for B, C, n_ign in ((256, 765, 0), (37, 100, 5), (4, 3, 4)):
+    for B, C, n_ign in ((256, 765, 0), (37, 100, 5), (4, 3, 4), (65536, 765, 100)):
         x = torch.randn(B, C, device=DEV) * 3
         t = torch.randint(0, C, (B,), device=DEV)
         t[:n_ign] = -100
