@@ -21,6 +21,9 @@ namespace {
 
 constexpr int kJobSegs = 24;  // segments per launch (a whole detector backward: trunk 8, heads 6, GRU 4)
 constexpr int kJobD = 4;      // fp64 columns per launch
+#ifndef LG_SLAB_VEC_G
+#define LG_SLAB_VEC_G 256  // most slab rows a vector segment takes (lab: 512, 32 rows in flight: 11.2 -> 14.7 us, r06zh)
+#endif
 #ifndef LG_SLAB_VEC
 #define LG_SLAB_VEC 1  // 16-byte column loads for aligned segments (lab: 0 = one column per lane)
 #endif
@@ -58,9 +61,9 @@ __device__ __forceinline__ void slab_col_sum(const float* __restrict__ src, int 
 
 // the same as slab_col_sum for 4 adjacent columns (one 16-byte load per slab row): each column
 // keeps slab_col_sum's order, so the sums are bit-identical to the scalar form
+template <int kRedInflight>
 __device__ __forceinline__ void slab_col_sum4(const float* __restrict__ src, int G, int64_t stride, int64_t col, int w,
                                               double (&acc)[4]) {
-    constexpr int kRedInflight = 16;
     int g = w;
     for (; g + 16 * (kRedInflight - 1) < G; g += 16 * kRedInflight) {
         f32x4 v[kRedInflight];
@@ -102,9 +105,17 @@ __global__ void __launch_bounds__(1024) k_slab_reduce(Segs sg) {
         __shared__ double part4[16][256];
         const int64_t col = static_cast<int64_t>(b - sg.first[k]) * 256 + 4 * lane;
         double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        if (col < sg.len[k]) {
-            slab_col_sum4(sg.slab[k] + sg.off[k], sg.G[k], sg.stride[k], col, w, acc);
-            if (sg.slab2[k]) slab_col_sum4(sg.slab2[k] + sg.off2[k], sg.G2[k], sg.stride2[k], col, w, acc);
+        if (col < sg.len[k]) {  // one round of loads per wave: 16 rows (G <= 256) or 32 (G <= 512)
+            if (sg.G[k] > 256)
+                slab_col_sum4<32>(sg.slab[k] + sg.off[k], sg.G[k], sg.stride[k], col, w, acc);
+            else
+                slab_col_sum4<16>(sg.slab[k] + sg.off[k], sg.G[k], sg.stride[k], col, w, acc);
+            if (sg.slab2[k]) {
+                if (sg.G2[k] > 256)
+                    slab_col_sum4<32>(sg.slab2[k] + sg.off2[k], sg.G2[k], sg.stride2[k], col, w, acc);
+                else
+                    slab_col_sum4<16>(sg.slab2[k] + sg.off2[k], sg.G2[k], sg.stride2[k], col, w, acc);
+            }
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) part4[w][4 * lane + c] = acc[c];
@@ -173,7 +184,7 @@ int launch_jobs(const SegJob* segs, int nseg, const DJob* dj, int nd, hipStream_
         auto al4 = [](uint64_t v) { return (v & 3u) == 0; };
         // 4 columns a lane cut the blocks 4x: only where each wave's rows fit one round of loads
         // (G <= 256: the heads' and the GRU's slabs; the trunk's 512 rows measured slower, r06zd)
-        const bool vec = LG_SLAB_VEC && j.G <= 256 && (!j.seg.slab2 || j.seg.G2 <= 256) && al4(reinterpret_cast<uintptr_t>(j.slab) / 4) && al4(j.stride) &&
+        const bool vec = LG_SLAB_VEC && j.G <= LG_SLAB_VEC_G && (!j.seg.slab2 || j.seg.G2 <= LG_SLAB_VEC_G) && al4(reinterpret_cast<uintptr_t>(j.slab) / 4) && al4(j.stride) &&
                          al4(j.seg.off) && al4(j.seg.len) &&
                          (!j.seg.slab2 || (al4(reinterpret_cast<uintptr_t>(j.seg.slab2) / 4) && al4(j.seg.stride2) &&
                                            al4(j.seg.off2)));
