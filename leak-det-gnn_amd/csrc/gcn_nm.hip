@@ -1495,7 +1495,7 @@ struct Nb3Lds {
 #define LG_NB3_SPLIT 0  // lab: 1 = the tail round of k_gcn_bwd_nm3 in pieces (r06x: 50.3 vs 48.0 us, slower)
 #endif
 #ifndef LG_NB3_NPF
-#define LG_NB3_NPF 4  // neighbour blocks in flight in the backward (lab builds override)
+#define LG_NB3_NPF 3  // neighbour blocks in flight in the backward (4: 44.6 / 40.2 against 43.2 / 38.7 us, r06zl)
 #endif
 // MB (with MASK_IN): the layer's output mask comes as the forward's ymask bits instead of a
 // gather of y, so the prefetch keeps the unmasked depth.
